@@ -1,0 +1,186 @@
+#!/usr/bin/env python3
+"""SqueezeNet-1.0 fp32 images/s on MI355X (BASELINE.json metric), one process per GPU.
+
+A step = one pass of the whole 66-node graph over one batch of 256 synthetic 3x224x224 images
+already resident in HBM (per GPU: weak scaling), plus, for N > 1, the RCCL all-gather of the
+[256, 1000] softmax rows (the only collective, BASELINE.json north_star).  Prints one JSON line
+on rank 0 with the roofline of the dominant kernel (the MFMA implicit-GEMM conv) and the CPU
+baseline (the C restatement of the reference's algorithm, timed on this host's cores).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "onnx-rusty-inference-engine_amd"))
+sys.path.insert(0, REPO)
+
+METRIC = "SqueezeNet-1.0 fp32 images/s at batch 256, 1/2/4/8 MI355X; max-abs diff vs CPU"
+PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
+    ap.add_argument("--hw", type=int, default=224)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--no-step-timing", action="store_true", help="no per-kernel HIP events in the timed loop")
+    return ap.parse_args()
+
+
+def cpu_baseline(model_bytes, hw, threads):
+    """The oracle in the reference's cost structure (per-dot heap buffer, im2col, weights decoded
+    per op call), one independent batch-1 image per thread — timed on this host."""
+    import numpy as np
+    import oracle
+    from ore import squeezenet
+    x = squeezenet.synthetic_input(threads, hw, seed=77)
+    models = [oracle.Model(model_bytes) for _ in range(threads)]
+    done = [0.0] * threads
+
+    def work(i):
+        t0 = time.perf_counter()
+        models[i].run(x[i:i + 1], 1000, faithful=True)
+        done[i] = time.perf_counter() - t0
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    wall = time.perf_counter() - t0
+    for m in models:
+        m.close()
+    return {"value": threads / wall, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} SqueezeNet-1.0 224x224 images, one batch-1 inference() per thread, "
+                      f"reference cost structure (oracle faithful mode); single-image latency "
+                      f"{float(np.median(done)):.2f} s"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import ore
+    from ore import squeezenet
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    B = args.batch
+    model_bytes = squeezenet.build(args.hw)
+    ctx = ore.Context(local)
+    model = ore.Model(ctx, model_bytes, max_batch=B)
+    g = torch.Generator(device=f"cuda:{local}")
+    g.manual_seed(1000 + rank)
+    x = (torch.rand((B, 3, args.hw, args.hw), generator=g, device=f"cuda:{local}") * 100.0 - 50.0).contiguous()
+    out = torch.empty((B, model.output_elems), dtype=torch.float32, device=f"cuda:{local}")
+    gathered = torch.empty((world * B, model.output_elems), dtype=torch.float32, device=f"cuda:{local}") \
+        if world > 1 else out
+
+    def step():
+        model.run_into(x, out)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    timing = not args.no_step_timing
+    model.enable_timing(timing)
+    infos = model.steps() if timing else []
+    per_step_ms = np.zeros(len(infos)) if timing else None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        if timing:
+            per_step_ms += np.asarray(model.step_times_ms())  # waits on the step's last event only
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    model.enable_timing(False)
+
+    if rank == 0:
+        value = world * B * args.steps / elapsed
+        result = {
+            "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded U(-50,50) 3x224x224 images; seeded He-normal SqueezeNet-1.0 weights)",
+            "config": {"workload": f"SqueezeNet-1.0 (66 nodes, 818.9 MMAC/img) fp32 inference, batch {B} per GPU, "
+                                   f"3x{args.hw}x{args.hw}",
+                       "model": "squeezenet1.0-8 topology, synthetic weights", "global_batch": world * B,
+                       "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}",
+                       "collective": "RCCL all_gather of [256,1000] logits per step" if world > 1 else None},
+        }
+        if timing:
+            per_step_ms /= args.steps
+            classes = {}
+            for info, ms in zip(infos, per_step_ms):
+                c = classes.setdefault(info["op"], {"ms": 0.0, "flops": 0.0, "bytes": 0.0, "launches": 0})
+                c["ms"] += float(ms)
+                c["flops"] += info["flops"]
+                c["bytes"] += info["bytes"]
+                c["launches"] += 1
+            conv = classes.get("Conv", {"ms": 1e-9, "flops": 0.0, "launches": 1})
+            achieved = conv["flops"] / (conv["ms"] * 1e-3) / 1e12
+            result["roofline"] = {
+                "bound": "mfma", "kernel": "conv_gemm_kernel (implicit-GEMM MFMA 32x32x2 f32, 26 launches/step)",
+                "achieved": round(achieved, 2), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4), "traffic": None,
+                "per_launch_avg_us": round(1000.0 * conv["ms"] / conv["launches"], 2),
+                "algorithmic": "2*Cout*Ho*Wo*Cin*kh*kw per image (1.638 GFLOP/img)"}
+            result["breakdown_ms_per_step"] = {
+                k: {"ms": round(v["ms"], 4), "launches": v["launches"],
+                    "TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["flops"] else None,
+                    "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1)} for k, v in classes.items()}
+        if world == 1:
+            # max-abs vs the CPU restatement on a bounded sample (2 images of this batch)
+            import oracle
+            torch.cuda.synchronize()
+            xs = x[:2].cpu().numpy()
+            ref = oracle.Model(model_bytes).run(xs, 1000)
+            result["max_abs_diff_vs_cpu"] = float(np.abs(out[:2].cpu().numpy() - ref).max())
+            result["max_abs_sample"] = "2 images of the timed batch vs oracle (C restatement of the reference)"
+            if not args.no_cpu_baseline:
+                threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+                result["cpu_baseline"] = cpu_baseline(model_bytes, args.hw, threads)
+        print(json.dumps(result), flush=True)
+
+    model.close()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,177 @@
+/*
+ * ore.h — C ABI of the MI355X-native (gfx950) fp32 ONNX op executor.
+ *
+ * Drop-in boundary for the fp32 op path of jackperlo/onnx-rusty-inference-engine.  The
+ * reference dispatches every node through `node_inference`
+ * (src/inference_engine/model_inference.rs:128-162, match at :137-161) into one Rust function
+ * per op in src/inference_fp32_ops/.  Each entry point below replaces one of those functions
+ * (cited on the declaration), operating on device tensors that stay resident in HBM.  The
+ * graph-level entry points (ore_model_*) replace `inference()` (model_inference.rs:29-120)
+ * together with the tensor plumbing of src/inference_engine/utils.rs.
+ *
+ * Conventions
+ *  - Every function returns an ore_status (0 = ORE_OK).  Nothing throws or aborts across the
+ *    ABI; the message of the last failure on a context is ore_last_error(ctx) (or
+ *    ore_last_error(NULL) for failures before a context exists).  The reference panics in the
+ *    same situations (unknown op / attribute / auto_pad string, missing input, shape mismatch).
+ *  - Tensors are fp32, NCHW row-major, device memory.  `nstride` is the element distance
+ *    between consecutive images (0 = contiguous); it lets an op write a channel slice of a
+ *    wider tensor (Concat in place).
+ *  - Launches are asynchronous on the context's HIP stream; ore_sync() joins.  A context is
+ *    bound to one device and is not thread-safe (one per host thread / device).
+ *  - Padding is resolved exactly as the reference does (including its SAME split with the
+ *    larger half at the top/left, convolution_op.rs:519-557) before any kernel is launched.
+ */
+#ifndef ORE_H
+#define ORE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORE_ABI_VERSION 1
+
+typedef enum ore_status {
+  ORE_OK = 0,
+  ORE_ERR_INVALID = 1,     /* bad argument / shape mismatch (reference: assert / unwrap panic) */
+  ORE_ERR_UNSUPPORTED = 2, /* op, attribute or mode the reference does not implement (panic!) */
+  ORE_ERR_HIP = 3,         /* HIP runtime failure */
+  ORE_ERR_OOM = 4,         /* device allocation failed */
+  ORE_ERR_PARSE = 5        /* malformed ONNX protobuf */
+} ore_status;
+
+typedef enum ore_auto_pad {
+  ORE_PAD_NOTSET = 0,     /* explicit `pads` */
+  ORE_PAD_SAME_UPPER = 1,
+  ORE_PAD_SAME_LOWER = 2,
+  ORE_PAD_VALID = 3
+} ore_auto_pad;
+
+typedef struct ore_ctx ore_ctx;
+typedef struct ore_model ore_model;
+
+typedef struct ore_tensor {
+  float* data;      /* device pointer to element [0,0,0,0] */
+  int32_t ndim;     /* 1..4 */
+  int64_t dims[4];
+  int64_t nstride;  /* elements between images (dims[0] steps); 0 = contiguous */
+} ore_tensor;
+
+/* Conv attributes (convolution_op.rs:132-173).  pads use ONNX order
+ * [h_begin, w_begin, h_end, w_end]; n_pads = 0 when the attribute is absent.  As in the
+ * reference, any positive pad forces NOTSET (:169-173) and kernel_shape is ignored (:151). */
+typedef struct ore_conv_attrs {
+  int32_t auto_pad;      /* ore_auto_pad; reference default VALID (:134) */
+  int32_t n_pads;
+  int64_t pads[4];
+  int64_t strides[2];    /* required (the reference unwraps them, :285-290) */
+  int64_t dilations[2];  /* must be 1 (dilation > 1 is not a working path in the reference) */
+  int64_t group;         /* must be 1 (asserted, :252) */
+  int32_t fuse_relu;     /* extension: apply Relu in the epilogue (a following Relu node) */
+} ore_conv_attrs;
+
+/* MaxPool attributes (max_pool_op.rs:85-114).  Unlike Conv, pads do NOT force NOTSET: with
+ * the default auto_pad (VALID) the pads are ignored, as in the reference. */
+typedef struct ore_pool_attrs {
+  int32_t auto_pad;
+  int32_t n_pads;
+  int64_t pads[4];
+  int64_t kernel[2];
+  int64_t strides[2];
+} ore_pool_attrs;
+
+/* ------------------------------------------------------------------ context & memory */
+int32_t ore_abi_version(void);
+ore_status ore_ctx_create(int32_t device, ore_ctx** out);
+ore_status ore_ctx_destroy(ore_ctx* ctx);
+/* Launch on an external HIP stream (e.g. the caller's framework stream).  NULL selects the
+ * legacy default (null) stream; the context starts on a stream of its own. */
+ore_status ore_ctx_set_stream(ore_ctx* ctx, void* hip_stream);
+void* ore_ctx_get_stream(ore_ctx* ctx);
+ore_status ore_sync(ore_ctx* ctx);
+const char* ore_last_error(ore_ctx* ctx);
+
+ore_status ore_malloc(ore_ctx* ctx, size_t bytes, void** dptr);
+ore_status ore_free(ore_ctx* ctx, void* dptr);
+ore_status ore_upload(ore_ctx* ctx, void* dst, const void* src, size_t bytes);
+ore_status ore_download(ore_ctx* ctx, void* dst, const void* src, size_t bytes);
+
+/* ------------------------------------------------------------------ shape inference
+ * Output geometry exactly as the reference computes it (convolution_op.rs:292-324,
+ * max_pool_op.rs:214-246); pads_tlbr receives the resolved [top, left, bottom, right]. */
+ore_status ore_conv_out_shape(const int64_t x_dims[4], const int64_t w_dims[4], const ore_conv_attrs* a,
+                              int64_t y_dims[4], int64_t pads_tlbr[4]);
+ore_status ore_pool_out_shape(const int64_t x_dims[4], const ore_pool_attrs* a, int64_t y_dims[4],
+                              int64_t pads_tlbr[4]);
+
+/* ------------------------------------------------------------------ ops (node_inference arms) */
+/* "Conv"     convolution()  convolution_op.rs:94-193 (conv2d :224-517).  x [N,C,H,W],
+ *            w [M,C,kh,kw] (ONNX layout), bias [M] or NULL, y [N,M,Ho,Wo] (may be a slice). */
+ore_status ore_conv2d_f32(ore_ctx* ctx, const ore_tensor* x, const ore_tensor* w, const ore_tensor* bias,
+                          const ore_conv_attrs* a, ore_tensor* y);
+/* "MaxPool"  max_pool()  max_pool_op.rs:65-129 (max_pool2d :157-360). */
+ore_status ore_maxpool2d_f32(ore_ctx* ctx, const ore_tensor* x, const ore_pool_attrs* a, ore_tensor* y);
+/* "Relu"     relu()  relu_op.rs:11-29 (relu_wrapper :31-33).  y may alias x. */
+ore_status ore_relu_f32(ore_ctx* ctx, const ore_tensor* x, ore_tensor* y);
+/* "Add"      add()  add_op.rs:16-107: a + b with b broadcast right-aligned onto a
+ *            ([N,C,H,W] + [C,1,1], or [N,K] + [1,K]). */
+ore_status ore_add_f32(ore_ctx* ctx, const ore_tensor* a, const ore_tensor* b, ore_tensor* y);
+/* "Softmax"  softmax()  softmax_op.rs:13-42 (softmax_wrapper :45-57): rows = dims[0],
+ *            row length = product of the remaining dims; y is [rows, D]. */
+ore_status ore_softmax_f32(ore_ctx* ctx, const ore_tensor* x, ore_tensor* y);
+/* "MatMul"   mul()  mul_op.rs:11-32: y[M,N] = a[M,K] . b[K,N] (MFMA). */
+ore_status ore_matmul_f32(ore_ctx* ctx, const ore_tensor* a, const ore_tensor* b, ore_tensor* y);
+/* "GlobalAveragePool"  global_average_pool()  global_average_pool_op.rs:11-51: y [N,C,1,1]. */
+ore_status ore_gap_f32(ore_ctx* ctx, const ore_tensor* x, ore_tensor* y);
+/* "Concat"   concatenation()  concatenate_op.rs:11-41: exactly two inputs on `axis`. */
+ore_status ore_concat_f32(ore_ctx* ctx, const ore_tensor* a, const ore_tensor* b, int64_t axis, ore_tensor* y);
+/* "Dropout"  drop_out()  dropout_op.rs:12-89: inference identity (training_mode = false).
+ *            Copies when y != x, no-op when they alias. */
+ore_status ore_dropout_f32(ore_ctx* ctx, const ore_tensor* x, ore_tensor* y);
+/* "Reshape"  reshape()  reshape_op.rs:16-92: metadata only (row-major reinterpretation to
+ *            2-D; a 0 in `shape` copies the input dim).  Writes the resulting view to y. */
+ore_status ore_reshape(const ore_tensor* x, const int64_t* shape, int32_t n_shape, ore_tensor* y);
+
+/* ------------------------------------------------------------------ graph walker (inference()) */
+/* Parse an ONNX ModelProto (bytes), upload every initializer to HBM once, plan the value
+ * buffers for up to max_batch images, and prepare the node list in file order.
+ * Unsupported ops/attributes fail here (the reference panics when it reaches them). */
+ore_status ore_model_load(ore_ctx* ctx, const void* onnx_bytes, size_t len, int64_t max_batch,
+                          ore_model** out);
+ore_status ore_model_destroy(ore_model* m);
+/* flags: bit 0 = fuse Conv->Relu, bit 1 = Concat in place, bit 2 = alias Dropout/Reshape.
+ * ORE_FUSE_ALL is the default; 0 runs every node as its own kernel (op-by-op parity). */
+#define ORE_FUSE_CONV_RELU 1
+#define ORE_FUSE_CONCAT 2
+#define ORE_FUSE_ALIAS 4
+#define ORE_FUSE_ALL 7
+/* debug: give every value its own storage (no liveness reuse) so any value can be read back */
+#define ORE_KEEP_VALUES 8
+ore_status ore_model_set_fusion(ore_model* m, int32_t flags);
+/* The seeded model input (graph.input entries that are not initializers, utils.rs:29-45):
+ * per-image dims; dims[0] is the batch. */
+ore_status ore_model_input_dims(ore_model* m, int64_t dims[4]);
+/* Elements per image of graph.output[0] (the reference only prints it; we keep it). */
+ore_status ore_model_output_elems(ore_model* m, int64_t* elems);
+/* Run all nodes on n <= max_batch images.  d_input/d_output are device pointers
+ * (n * input elems / n * output elems).  Asynchronous on the context stream. */
+ore_status ore_model_run(ore_model* m, const float* d_input, int64_t n, float* d_output);
+/* Copy a named value of the last run to host memory (for node-level parity checks; values
+ * elided by fusion are unavailable -> ORE_ERR_INVALID).  Synchronises. */
+ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst, size_t cap_elems,
+                                int64_t dims[4], int32_t* ndim);
+/* Per-node timing with HIP events on the context stream (enable, run, then query).
+ * ore_model_node_count/ore_model_node_info describe the executed kernel steps. */
+ore_status ore_model_enable_timing(ore_model* m, int32_t on);
+int32_t ore_model_step_count(ore_model* m);
+ore_status ore_model_step_info(ore_model* m, int32_t i, const char** op, const char** name, double* flops,
+                               double* bytes);
+ore_status ore_model_step_times(ore_model* m, float* ms, int32_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORE_H */

@@ -1,0 +1,89 @@
+// Host-side internals shared by the C ABI implementation files.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/ore.h"
+#include "ore_kernels.h"
+
+struct ore_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+};
+
+namespace ore {
+
+// ---------------------------------------------------------------- errors
+ore_status set_error(ore_ctx* ctx, ore_status st, const char* fmt, ...);
+#define ORE_HIP_CHECK(ctx, expr)                                                          \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return ::ore::set_error((ctx), ORE_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+// ---------------------------------------------------------------- ONNX subset (onnx.proto)
+struct Attr {
+  std::string name;
+  int type = 0;
+  float f = 0.f;
+  int64_t i = 0;
+  std::string s;
+  std::vector<int64_t> ints;
+  std::vector<float> floats;
+  bool has_i = false, has_f = false, has_s = false;
+};
+
+struct Node {
+  std::string op_type, name;
+  std::vector<std::string> inputs, outputs;
+  std::vector<Attr> attrs;
+};
+
+struct Initializer {
+  std::string name;
+  std::vector<int64_t> dims;
+  int dtype = 0;
+  std::vector<float> f32;
+  std::vector<int64_t> i64;
+};
+
+struct ValueInfo {
+  std::string name;
+  std::vector<int64_t> shape;
+};
+
+struct Graph {
+  std::vector<Node> nodes;
+  std::vector<Initializer> inits;
+  std::vector<ValueInfo> inputs, outputs;
+};
+
+// Parses a ModelProto; returns false with a message on malformed input.
+bool parse_model(const uint8_t* data, size_t len, Graph* g, std::string* err);
+
+// ---------------------------------------------------------------- reference geometry
+// Resolved window geometry (convolution_op.rs:266-350, max_pool_op.rs:188-264).
+struct Window {
+  int64_t pt = 0, pl = 0, pb = 0, pr = 0;
+  int64_t Ho = 0, Wo = 0;
+};
+// auto_pad as ore_auto_pad; pads in ONNX order.  Returns ORE_OK or an error status.
+ore_status resolve_window(ore_ctx* ctx, int auto_pad, const int64_t* pads, int n_pads, int64_t H, int64_t W,
+                          int64_t kh, int64_t kw, int64_t sh, int64_t sw, Window* out);
+
+// ---------------------------------------------------------------- launches over resolved geometry
+ore_status run_conv(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
+                    const float* w, int64_t M, int64_t kh, int64_t kw, bool w_kmajor, const float* bias,
+                    const Window& win, int64_t sh, int64_t sw, bool relu, float* y, int64_t y_nstride);
+ore_status run_maxpool(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
+                       int64_t x_nstride, int64_t kh, int64_t kw, const Window& win, int64_t sh, int64_t sw,
+                       float* y, int64_t y_nstride);
+
+}  // namespace ore

@@ -1,0 +1,804 @@
+// Graph walker: the device-resident replacement of `inference()` / `node_inference()`
+// (model_inference.rs:29-162) and of the value map they share
+// (`Arc<Mutex<HashMap<String, (Option<Array2>, Option<Array4>)>>>`, :30-32).
+//
+//  * Load: parse the ModelProto, upload every f32 initializer to HBM once (the reference
+//    re-decodes them on every op call, utils.rs:113-185), run the reference's per-op shape and
+//    attribute rules over the nodes in file order (the order the reference executes them in,
+//    :84-115; its branch threads only reorder independent siblings), and turn each node into
+//    a kernel step.  Anything the reference would panic on is reported here.
+//  * Fuse (ORE_FUSE_*): Conv -> Relu into the conv epilogue; Concat(axis 1) of two
+//    conv/pool outputs by writing both producers into channel slices of the concat buffer;
+//    Dropout and activation Reshape as aliases.
+//  * Plan: every materialised activation gets a slot in one device arena sized for max_batch,
+//    slots reused by liveness (first-fit over [first write, last read] intervals).
+//  * Run: launch the steps in order on the context stream; the model input and output are the
+//    caller's device buffers.
+//
+// Batch: every activation carries a leading batch dim n (the reference is batch-1: it writes
+// only image 0, e.g. convolution_op.rs:480).  Constants (initializers, Reshape of an
+// initializer) carry none.
+#include <algorithm>
+#include <cstring>
+
+#include "ore_internal.h"
+
+using namespace ore;
+
+namespace {
+
+enum StepKind { S_CONV, S_MAXPOOL, S_RELU, S_ADD, S_SOFTMAX, S_MATMUL, S_GAP, S_CONCAT, S_COPY, S_NOP };
+
+struct Value {
+  std::string name;
+  bool is_const = false;
+  bool is_input = false;
+  bool is_output = false;
+  int ndim = 0;
+  int64_t dims[4] = {0, 0, 0, 0};  // activations: dims[0] = 1 (per image)
+  float* cptr = nullptr;           // const f32 device data
+  std::vector<int64_t> i64;        // const int64 host data
+  bool has_i64 = false;
+  int alias_of = -1;               // view into another value's storage
+  int64_t alias_off = 0;           // per-image element offset inside the base
+  int64_t nstride = 0;             // per-image stride of the storage (0 = own size)
+  bool elided = false;             // produced and consumed inside one fused kernel
+  int64_t arena_off = -1;          // byte offset in the arena (root values)
+  int first = -1, last = -1;       // live interval in step indices
+  int uses = 0;                    // consumer count (node inputs)
+
+  int64_t per_image() const {
+    int64_t s = 1;
+    for (int i = 1; i < ndim; ++i) s *= dims[i];
+    return s;
+  }
+  int64_t numel_const() const {
+    int64_t s = 1;
+    for (int i = 0; i < ndim; ++i) s *= dims[i];
+    return s;
+  }
+};
+
+struct Step {
+  StepKind kind = S_NOP;
+  std::string op, name;
+  int in0 = -1, in1 = -1, in2 = -1, out = -1;
+  // conv / pool geometry (per image)
+  int64_t C = 0, H = 0, W = 0, M = 0, kh = 0, kw = 0, sh = 1, sw = 1;
+  Window win;
+  bool relu = false;
+  bool w_kmajor = false;
+  int64_t axis = 1;
+  double flops_per_img = 0, bytes_per_img = 0, bytes_fixed = 0;
+};
+
+}  // namespace
+
+struct ore_model {
+  ore_ctx* ctx = nullptr;
+  int64_t max_batch = 0;
+  int32_t fusion = ORE_FUSE_ALL;
+  std::vector<Value> values;
+  std::map<std::string, int> by_name;
+  std::vector<Step> base_steps;  // unfused, one per node
+  std::vector<Step> steps;       // after fusion
+  int input_value = -1;
+  int output_value = -1;
+  float* consts = nullptr;       // one device allocation for all f32 initializers
+  char* arena = nullptr;
+  size_t arena_bytes = 0;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> events;
+  std::vector<int> exec_steps;   // indices into steps of launched (non-NOP) steps
+  // run-time binding
+  const float* cur_in = nullptr;
+  float* cur_out = nullptr;
+  bool out_bound = false;
+  int64_t last_n = 0;
+};
+
+namespace {
+
+ore_status err(ore_model* m, ore_status st, const std::string& msg) {
+  return set_error(m->ctx, st, "%s", msg.c_str());
+}
+
+int value_id(ore_model* m, const std::string& name) {
+  auto it = m->by_name.find(name);
+  return it == m->by_name.end() ? -1 : it->second;
+}
+
+int new_value(ore_model* m, const std::string& name) {
+  Value v;
+  v.name = name;
+  m->values.push_back(v);
+  int id = int(m->values.size()) - 1;
+  m->by_name[name] = id;  // re-definition shadows, as HashMap::insert does
+  return id;
+}
+
+bool is_act(const Value& v, int rank) { return !v.is_const && v.ndim == rank; }
+
+// ------------------------------------------------------------------ per-node shape/attr rules
+ore_status build_conv(ore_model* m, const Node& n, Step* s) {
+  if (n.inputs.size() < 2) return err(m, ORE_ERR_INVALID, "Conv '" + n.name + "' needs 2 inputs");
+  int x = value_id(m, n.inputs[0]), w = value_id(m, n.inputs[1]);
+  if (x < 0 || w < 0) return err(m, ORE_ERR_INVALID, "Conv '" + n.name + "': input not available");
+  const Value &X = m->values[x], &Wt = m->values[w];
+  if (!is_act(X, 4)) return err(m, ORE_ERR_UNSUPPORTED, "Conv '" + n.name + "': input must be a 4-D activation");
+  if (!Wt.is_const || Wt.ndim != 4 || !Wt.cptr)
+    return err(m, ORE_ERR_UNSUPPORTED, "Conv '" + n.name + "': weights must be a 4-D f32 initializer");
+  int b = -1;
+  if (n.inputs.size() > 2) {  // get_stored_tensor(2) (:124-130)
+    b = value_id(m, n.inputs[2]);
+    if (b < 0 || !m->values[b].is_const || m->values[b].ndim != 1 || !m->values[b].cptr)
+      return err(m, ORE_ERR_UNSUPPORTED, "Conv '" + n.name + "': bias must be a 1-D f32 initializer");
+    if (m->values[b].dims[0] != Wt.dims[0]) return err(m, ORE_ERR_INVALID, "Bias array has the wrong shape");
+  }
+  ore_conv_attrs a{};
+  a.auto_pad = ORE_PAD_VALID;  // default (:134)
+  a.group = 1;
+  a.dilations[0] = a.dilations[1] = 1;
+  bool have_strides = false;
+  for (auto& at : n.attrs) {  // :137-163
+    if (at.name == "auto_pad") {
+      if (at.s == "SAME_UPPER") a.auto_pad = ORE_PAD_SAME_UPPER;
+      else if (at.s == "SAME_LOWER") a.auto_pad = ORE_PAD_SAME_LOWER;
+      else if (at.s == "VALID") a.auto_pad = ORE_PAD_VALID;
+      else if (at.s == "NOT_SET") a.auto_pad = ORE_PAD_NOTSET;
+      else return err(m, ORE_ERR_UNSUPPORTED, "Convolution Auto Pad specified not found: " + at.s);
+    } else if (at.name == "dilations") {
+      if (at.ints.size() < 2) return err(m, ORE_ERR_INVALID, "Conv dilations need 2 values");
+      a.dilations[0] = at.ints[0]; a.dilations[1] = at.ints[1];
+    } else if (at.name == "group") {
+      a.group = at.i;
+    } else if (at.name == "kernel_shape") {
+    } else if (at.name == "pads") {
+      a.n_pads = int32_t(std::min<size_t>(at.ints.size(), 4));
+      for (int i = 0; i < a.n_pads; ++i) a.pads[i] = at.ints[i];
+    } else if (at.name == "strides") {
+      if (at.ints.size() < 2) return err(m, ORE_ERR_INVALID, "Conv strides need 2 values");
+      a.strides[0] = at.ints[0]; a.strides[1] = at.ints[1];
+      have_strides = true;
+    } else {
+      return err(m, ORE_ERR_UNSUPPORTED, "ATTRIBUTE NAME FOR CONVOLUTION NOT FOUND, " + at.name);
+    }
+  }
+  if (!have_strides) return err(m, ORE_ERR_UNSUPPORTED, "Conv '" + n.name + "': strides attribute required");
+  int64_t yd[4], p[4];
+  if (ore_status st = ore_conv_out_shape(X.dims, Wt.dims, &a, yd, p)) {
+    return err(m, st, "Conv '" + n.name + "': " + ore_last_error(nullptr));
+  }
+  s->kind = S_CONV;
+  s->in0 = x; s->in1 = w; s->in2 = b;
+  s->C = X.dims[1]; s->H = X.dims[2]; s->W = X.dims[3];
+  s->M = Wt.dims[0]; s->kh = Wt.dims[2]; s->kw = Wt.dims[3];
+  s->sh = a.strides[0]; s->sw = a.strides[1];
+  s->win.pt = p[0]; s->win.pl = p[1]; s->win.pb = p[2]; s->win.pr = p[3];
+  s->win.Ho = yd[2]; s->win.Wo = yd[3];
+  const double P = double(yd[2] * yd[3]);
+  s->flops_per_img = 2.0 * double(s->M) * P * double(s->C * s->kh * s->kw);
+  s->bytes_per_img = 4.0 * (double(s->C * s->H * s->W) + double(s->M) * P);
+  s->bytes_fixed = 4.0 * double(Wt.numel_const() + (b >= 0 ? s->M : 0));
+  int y = new_value(m, n.outputs[0]);
+  Value& Y = m->values[y];
+  Y.ndim = 4; Y.dims[0] = 1; Y.dims[1] = yd[1]; Y.dims[2] = yd[2]; Y.dims[3] = yd[3];
+  s->out = y;
+  return ORE_OK;
+}
+
+ore_status build_maxpool(ore_model* m, const Node& n, Step* s) {
+  int x = value_id(m, n.inputs.empty() ? "" : n.inputs[0]);
+  if (x < 0) return err(m, ORE_ERR_INVALID, "MaxPool '" + n.name + "': input not available");
+  const Value& X = m->values[x];
+  if (!is_act(X, 4)) return err(m, ORE_ERR_UNSUPPORTED, "MaxPool '" + n.name + "': input must be a 4-D activation");
+  ore_pool_attrs a{};
+  a.auto_pad = ORE_PAD_VALID;  // default (max_pool_op.rs:88); pads do NOT force NOTSET here
+  bool have_k = false, have_s = false;
+  for (auto& at : n.attrs) {  // :90-114
+    if (at.name == "auto_pad") {
+      if (at.s == "SAME_UPPER") a.auto_pad = ORE_PAD_SAME_UPPER;
+      else if (at.s == "SAME_LOWER") a.auto_pad = ORE_PAD_SAME_LOWER;
+      else if (at.s == "VALID") a.auto_pad = ORE_PAD_VALID;
+      else if (at.s == "NOTSET") a.auto_pad = ORE_PAD_NOTSET;
+      else return err(m, ORE_ERR_UNSUPPORTED, "MaxPool Auto Pad specified not found: " + at.s);
+    } else if (at.name == "kernel_shape") {
+      if (at.ints.size() < 2) return err(m, ORE_ERR_INVALID, "MaxPool kernel_shape needs 2 values");
+      a.kernel[0] = at.ints[0]; a.kernel[1] = at.ints[1]; have_k = true;
+    } else if (at.name == "pads") {
+      a.n_pads = int32_t(std::min<size_t>(at.ints.size(), 4));
+      for (int i = 0; i < a.n_pads; ++i) a.pads[i] = at.ints[i];
+    } else if (at.name == "storage_order") {
+    } else if (at.name == "strides") {
+      if (at.ints.size() < 2) return err(m, ORE_ERR_INVALID, "MaxPool strides need 2 values");
+      a.strides[0] = at.ints[0]; a.strides[1] = at.ints[1]; have_s = true;
+    } else {
+      return err(m, ORE_ERR_UNSUPPORTED, "ATTRIBUTE NAME FOR MAX POOL NOT FOUND, " + at.name);
+    }
+  }
+  if (!have_k || !have_s) return err(m, ORE_ERR_UNSUPPORTED, "MaxPool '" + n.name + "': kernel_shape and strides required");
+  int64_t yd[4], p[4];
+  if (ore_status st = ore_pool_out_shape(X.dims, &a, yd, p))
+    return err(m, st, "MaxPool '" + n.name + "': " + ore_last_error(nullptr));
+  s->kind = S_MAXPOOL;
+  s->in0 = x;
+  s->C = X.dims[1]; s->H = X.dims[2]; s->W = X.dims[3];
+  s->kh = a.kernel[0]; s->kw = a.kernel[1]; s->sh = a.strides[0]; s->sw = a.strides[1];
+  s->win.pt = p[0]; s->win.pl = p[1]; s->win.pb = p[2]; s->win.pr = p[3];
+  s->win.Ho = yd[2]; s->win.Wo = yd[3];
+  s->bytes_per_img = 4.0 * double(X.per_image() + s->C * yd[2] * yd[3]);
+  int y = new_value(m, n.outputs[0]);
+  Value& Y = m->values[y];
+  Y.ndim = 4; Y.dims[0] = 1; Y.dims[1] = yd[1]; Y.dims[2] = yd[2]; Y.dims[3] = yd[3];
+  s->out = y;
+  return ORE_OK;
+}
+
+ore_status build_unary4(ore_model* m, const Node& n, Step* s, StepKind kind) {
+  int x = value_id(m, n.inputs.empty() ? "" : n.inputs[0]);
+  if (x < 0 || !is_act(m->values[x], 4))  // `.1.clone().unwrap()` on a map entry
+    return err(m, ORE_ERR_UNSUPPORTED, n.op_type + " '" + n.name + "': input must be a 4-D activation");
+  s->kind = kind;
+  s->in0 = x;
+  const Value X = m->values[x];
+  int y = new_value(m, n.outputs[0]);
+  Value& Y = m->values[y];
+  Y.ndim = X.ndim;
+  for (int i = 0; i < 4; ++i) Y.dims[i] = X.dims[i];
+  s->out = y;
+  s->bytes_per_img = 8.0 * double(X.per_image());
+  return ORE_OK;
+}
+
+ore_status build_node(ore_model* m, const Node& n, Step* s) {
+  s->op = n.op_type;
+  s->name = n.name.empty() ? (n.outputs.empty() ? n.op_type : n.outputs[0]) : n.name;
+  if (n.outputs.empty()) return err(m, ORE_ERR_INVALID, "node '" + n.name + "' has no outputs");
+  const std::string& op = n.op_type;
+  if (op == "Conv") return build_conv(m, n, s);
+  if (op == "MaxPool") return build_maxpool(m, n, s);
+  if (op == "Relu") return build_unary4(m, n, s, S_RELU);
+  if (op == "Dropout") {  // dropout_op.rs:22-28: only `ratio`
+    for (auto& at : n.attrs)
+      if (at.name != "ratio") return err(m, ORE_ERR_UNSUPPORTED, "ATTRIBUTE NAME FOR DROP OUT NOT FOUND, " + at.name);
+    return build_unary4(m, n, s, S_COPY);
+  }
+  if (op == "GlobalAveragePool") {
+    ore_status st = build_unary4(m, n, s, S_GAP);
+    if (st) return st;
+    Value& Y = m->values[s->out];
+    const Value& X = m->values[s->in0];
+    Y.dims[2] = 1; Y.dims[3] = 1;
+    s->bytes_per_img = 4.0 * double(X.per_image() + X.dims[1]);
+    return ORE_OK;
+  }
+  if (op == "Softmax") {  // softmax_wrapper flattens to (N, C*H*W), axis 1 (:46-51)
+    ore_status st = build_unary4(m, n, s, S_SOFTMAX);
+    if (st) return st;
+    Value& Y = m->values[s->out];
+    const Value& X = m->values[s->in0];
+    Y.ndim = 2; Y.dims[0] = 1; Y.dims[1] = X.per_image(); Y.dims[2] = Y.dims[3] = 0;
+    return ORE_OK;
+  }
+  if (op == "Concat") {  // concatenate_op.rs:22-32
+    int64_t axis = 1;
+    for (auto& at : n.attrs) {
+      if (at.name != "axis") return err(m, ORE_ERR_UNSUPPORTED, "ATTRIBUTE NAME FOR CONCATENATE NOT FOUND, " + at.name);
+      axis = at.i;
+    }
+    if (n.inputs.size() != 2) return err(m, ORE_ERR_UNSUPPORTED, "Concat '" + n.name + "': exactly 2 inputs supported");
+    int a = value_id(m, n.inputs[0]), b = value_id(m, n.inputs[1]);
+    if (a < 0 || b < 0 || !is_act(m->values[a], 4) || !is_act(m->values[b], 4))
+      return err(m, ORE_ERR_UNSUPPORTED, "Concat '" + n.name + "': inputs must be 4-D activations");
+    if (axis < 1 || axis > 3)
+      return err(m, ORE_ERR_UNSUPPORTED, "Concat '" + n.name + "': axis must be 1..3 (axis 0 is the batch)");
+    const Value A = m->values[a], B = m->values[b];
+    for (int i = 1; i < 4; ++i)
+      if (i != axis && A.dims[i] != B.dims[i]) return err(m, ORE_ERR_INVALID, "Concat '" + n.name + "': shape mismatch");
+    s->kind = S_CONCAT; s->in0 = a; s->in1 = b; s->axis = axis;
+    int y = new_value(m, n.outputs[0]);
+    Value& Y = m->values[y];
+    Y.ndim = 4;
+    for (int i = 0; i < 4; ++i) Y.dims[i] = A.dims[i];
+    Y.dims[axis] = A.dims[axis] + B.dims[axis];
+    s->out = y;
+    s->bytes_per_img = 8.0 * double(Y.per_image());
+    return ORE_OK;
+  }
+  if (op == "Add") {  // add_op.rs:16-107
+    if (n.inputs.size() < 2) return err(m, ORE_ERR_INVALID, "Add '" + n.name + "' needs 2 inputs");
+    int a = value_id(m, n.inputs[0]), b = value_id(m, n.inputs[1]);
+    if (a < 0) return err(m, ORE_ERR_INVALID, "Cannot retrieve input 1 for Add operation from hashmap input/output");
+    if (b < 0 || !m->values[b].is_const || !m->values[b].cptr)
+      return err(m, ORE_ERR_UNSUPPORTED, "Cannot retrieve input 2 for Add operation");
+    const Value A = m->values[a], B = m->values[b];
+    if (A.is_const) return err(m, ORE_ERR_UNSUPPORTED, "Add '" + n.name + "': constant first input not supported");
+    if (!((A.ndim == 4 && B.ndim == 3) || (A.ndim == 2 && B.ndim == 2)))
+      return err(m, ORE_ERR_UNSUPPORTED, "Add '" + n.name + "': supports 4-D + 3-D or 2-D + 2-D");
+    for (int i = 0; i < B.ndim; ++i) {  // right-aligned broadcast; the batch axis of A is 1 here
+      const int ai = A.ndim - B.ndim + i;
+      const int64_t ad = A.dims[ai];
+      if (B.dims[i] != 1 && B.dims[i] != ad && !(ai == 0 && B.dims[i] == 1))
+        return err(m, ORE_ERR_INVALID, "Add '" + n.name + "': shapes not broadcastable");
+      if (ai == 0 && B.dims[i] != 1)
+        return err(m, ORE_ERR_UNSUPPORTED, "Add '" + n.name + "': constant may not span the batch axis");
+    }
+    s->kind = S_ADD; s->in0 = a; s->in1 = b;
+    int y = new_value(m, n.outputs[0]);
+    Value& Y = m->values[y];
+    Y.ndim = A.ndim;
+    for (int i = 0; i < 4; ++i) Y.dims[i] = A.dims[i];
+    s->out = y;
+    s->bytes_per_img = 8.0 * double(A.per_image());
+    return ORE_OK;
+  }
+  if (op == "Reshape") {  // reshape_op.rs:16-92
+    if (n.inputs.size() < 2) return err(m, ORE_ERR_INVALID, "Reshape '" + n.name + "' needs 2 inputs");
+    int x = value_id(m, n.inputs[0]), sh = value_id(m, n.inputs[1]);
+    if (x < 0) return err(m, ORE_ERR_INVALID, "Reshape '" + n.name + "': input not available");
+    if (sh < 0 || !m->values[sh].is_const || !m->values[sh].has_i64)
+      return err(m, ORE_ERR_UNSUPPORTED, "Unable to retrieve Shape for Reshape operation");
+    const Value X = m->values[x];
+    const std::vector<int64_t> shape = m->values[sh].i64;
+    if (X.ndim != 4) return err(m, ORE_ERR_UNSUPPORTED, "Reshape '" + n.name + "': data must be 4-D");
+    if (shape.size() < 2) return err(m, ORE_ERR_UNSUPPORTED, "Reshape '" + n.name + "': shape must have 2 values");
+    int64_t ns[2] = {shape[0], shape[1]};
+    for (int i = 0; i < 2; ++i)
+      if (ns[i] == 0) ns[i] = X.dims[i];
+    if (ns[0] < 0 || ns[1] < 0) return err(m, ORE_ERR_UNSUPPORTED, "Reshape '" + n.name + "': negative dims");
+    if (X.is_const) {  // fold: a reinterpretation of the uploaded initializer
+      if (ns[0] * ns[1] != X.numel_const()) return err(m, ORE_ERR_INVALID, "Reshape: element count mismatch");
+      int y = new_value(m, n.outputs[0]);
+      Value& Y = m->values[y];
+      Y.is_const = true; Y.ndim = 2; Y.dims[0] = ns[0]; Y.dims[1] = ns[1]; Y.cptr = m->values[x].cptr;
+      s->kind = S_NOP;
+      s->out = y;
+      return ORE_OK;
+    }
+    if (ns[0] != 1 || ns[1] != X.per_image())
+      return err(m, ORE_ERR_UNSUPPORTED, "Reshape '" + n.name + "': activation reshape must be [1 or 0, C*H*W] per image");
+    s->kind = S_COPY; s->in0 = x;
+    int y = new_value(m, n.outputs[0]);
+    Value& Y = m->values[y];
+    Y.ndim = 2; Y.dims[0] = 1; Y.dims[1] = ns[1];
+    s->out = y;
+    s->bytes_per_img = 8.0 * double(X.per_image());
+    return ORE_OK;
+  }
+  if (op == "MatMul") {  // mul_op.rs:11-32: both operands Array2 from the map
+    if (n.inputs.size() < 2) return err(m, ORE_ERR_INVALID, "MatMul '" + n.name + "' needs 2 inputs");
+    int a = value_id(m, n.inputs[0]), b = value_id(m, n.inputs[1]);
+    if (a < 0 || b < 0) return err(m, ORE_ERR_INVALID, "MatMul '" + n.name + "': input not available");
+    const Value A = m->values[a], B = m->values[b];
+    if (A.ndim != 2 || B.ndim != 2) return err(m, ORE_ERR_UNSUPPORTED, "MatMul '" + n.name + "': operands must be 2-D");
+    if (A.is_const || !B.is_const || !B.cptr)
+      return err(m, ORE_ERR_UNSUPPORTED, "MatMul '" + n.name + "': expects activation . constant");
+    if (A.dims[1] != B.dims[0]) return err(m, ORE_ERR_INVALID, "MatMul '" + n.name + "': inner dims differ");
+    s->kind = S_MATMUL; s->in0 = a; s->in1 = b;
+    s->C = A.dims[1]; s->M = B.dims[1]; s->w_kmajor = true;
+    s->win.Ho = 1; s->win.Wo = 1; s->H = 1; s->W = 1; s->kh = 1; s->kw = 1;
+    s->flops_per_img = 2.0 * double(A.dims[1] * B.dims[1]);
+    s->bytes_per_img = 4.0 * double(A.dims[1] + B.dims[1]);
+    s->bytes_fixed = 4.0 * double(B.numel_const());
+    int y = new_value(m, n.outputs[0]);
+    Value& Y = m->values[y];
+    Y.ndim = 2; Y.dims[0] = 1; Y.dims[1] = B.dims[1];
+    s->out = y;
+    return ORE_OK;
+  }
+  return err(m, ORE_ERR_UNSUPPORTED, "INFERENCE OPERATION '" + op + "' NOT FOUND FOR NODE " + n.name);
+}
+
+// ------------------------------------------------------------------ fusion + planning
+void count_uses(ore_model* m, const std::vector<Step>& steps) {
+  for (auto& v : m->values) v.uses = 0;
+  for (auto& s : steps)
+    for (int id : {s.in0, s.in1, s.in2})
+      if (id >= 0) m->values[id].uses++;
+}
+
+bool strided_writer(const Step& s) { return s.kind == S_CONV || s.kind == S_MAXPOOL; }
+
+ore_status plan(ore_model* m) {
+  m->steps = m->base_steps;
+  for (auto& v : m->values) {
+    v.alias_of = -1; v.alias_off = 0; v.nstride = 0; v.elided = false; v.arena_off = -1; v.first = v.last = -1;
+  }
+  count_uses(m, m->steps);
+  std::vector<int> producer(m->values.size(), -1);
+  for (size_t i = 0; i < m->steps.size(); ++i)
+    if (m->steps[i].out >= 0 && m->steps[i].kind != S_NOP) producer[m->steps[i].out] = int(i);
+
+  // (1) Conv -> Relu
+  if (m->fusion & ORE_FUSE_CONV_RELU) {
+    for (size_t i = 0; i < m->steps.size(); ++i) {
+      Step& r = m->steps[i];
+      if (r.kind != S_RELU) continue;
+      int v = r.in0;
+      int p = producer[v];
+      if (p < 0 || m->steps[p].kind != S_CONV || m->steps[p].relu) continue;
+      if (m->values[v].uses != 1 || m->values[v].is_output) continue;
+      m->steps[p].out = r.out;
+      m->steps[p].relu = true;
+      m->values[v].elided = true;
+      producer[r.out] = p;
+      r.kind = S_NOP;
+      r.in0 = -1;
+    }
+    count_uses(m, m->steps);
+  }
+  // (2) Dropout / activation Reshape as aliases
+  if (m->fusion & ORE_FUSE_ALIAS) {
+    for (auto& s : m->steps) {
+      if (s.kind != S_COPY) continue;
+      Value& y = m->values[s.out];
+      y.alias_of = s.in0;  // resolved to the root at run time; requires a contiguous source
+      s.kind = S_NOP;
+    }
+  }
+  // (3) Concat in place: producers write channel slices of the concat buffer
+  if (m->fusion & ORE_FUSE_CONCAT) {
+    for (auto& s : m->steps) {
+      if (s.kind != S_CONCAT || s.axis != 1 || s.in0 == s.in1) continue;
+      Value &a = m->values[s.in0], &b = m->values[s.in1];
+      int pa = producer[s.in0], pb = producer[s.in1];
+      if (pa < 0 || pb < 0 || !strided_writer(m->steps[pa]) || !strided_writer(m->steps[pb])) continue;
+      if (a.uses != 1 || b.uses != 1 || a.is_output || b.is_output || a.alias_of >= 0 || b.alias_of >= 0) continue;
+      const Value& y = m->values[s.out];
+      a.alias_of = s.out; a.alias_off = 0; a.nstride = y.per_image();
+      b.alias_of = s.out; b.alias_off = a.per_image(); b.nstride = y.per_image();
+      s.kind = S_NOP;
+    }
+  }
+  // aliases of aliases must stay contiguous views (Reshape/Dropout of a channel slice)
+  for (auto& v : m->values) {
+    if (v.alias_of < 0 || v.nstride != 0) continue;
+    const Value& src = m->values[v.alias_of];
+    if (src.nstride != 0 && src.nstride != src.per_image())
+      return err(m, ORE_ERR_INVALID, "internal: alias of a strided view (" + v.name + ")");
+  }
+
+  // live intervals on root storage
+  auto root = [&](int id) {
+    while (m->values[id].alias_of >= 0) id = m->values[id].alias_of;
+    return id;
+  };
+  const int nsteps = int(m->steps.size());
+  for (int i = 0; i < nsteps; ++i) {
+    const Step& s = m->steps[i];
+    if (s.kind == S_NOP) continue;
+    for (int id : {s.in0, s.in1, s.in2}) {
+      if (id < 0 || m->values[id].is_const) continue;
+      Value& r = m->values[root(id)];
+      if (r.first < 0) r.first = i;
+      r.last = std::max(r.last, i);
+    }
+    if (s.out >= 0) {
+      Value& r = m->values[root(s.out)];
+      if (r.first < 0 || r.first > i) r.first = i;
+      r.last = std::max(r.last, i);
+    }
+  }
+  // the model output stays live to the end (it may be copied out after the last step)
+  if (m->output_value >= 0) m->values[root(m->output_value)].last = nsteps;
+
+  struct Slot { int64_t off, size; int first, last; };
+  std::vector<int> roots;
+  for (size_t id = 0; id < m->values.size(); ++id) {
+    Value& v = m->values[id];
+    if (v.is_const || v.is_input || v.alias_of >= 0 || v.elided || v.first < 0) continue;
+    roots.push_back(int(id));
+  }
+  std::sort(roots.begin(), roots.end(), [&](int a, int b) {
+    return m->values[a].per_image() > m->values[b].per_image();
+  });
+  std::vector<Slot> placed;
+  int64_t arena = 0;
+  for (int id : roots) {
+    Value& v = m->values[id];
+    const int64_t size = ((v.per_image() * m->max_batch * 4) + 255) / 256 * 256;
+    // first fit among the gaps left by placed slots whose lifetimes overlap this one
+    std::vector<std::pair<int64_t, int64_t>> busy;
+    for (auto& s : placed)
+      if ((m->fusion & ORE_KEEP_VALUES) || !(s.last < v.first || v.last < s.first)) busy.push_back({s.off, s.off + s.size});
+    std::sort(busy.begin(), busy.end());
+    int64_t off = 0;
+    for (auto& b : busy) {
+      if (off + size <= b.first) break;
+      off = std::max(off, b.second);
+    }
+    v.arena_off = off;
+    placed.push_back({off, size, v.first, v.last});
+    arena = std::max(arena, off + size);
+  }
+  if (size_t(arena) > m->arena_bytes) {
+    if (m->arena) (void)hipFree(m->arena);
+    m->arena = nullptr;
+    m->arena_bytes = 0;
+    if (arena > 0 && hipMalloc(reinterpret_cast<void**>(&m->arena), size_t(arena)) != hipSuccess)
+      return err(m, ORE_ERR_OOM, "arena allocation of " + std::to_string(arena) + " bytes failed");
+    m->arena_bytes = size_t(arena);
+  }
+  m->exec_steps.clear();
+  for (int i = 0; i < nsteps; ++i)
+    if (m->steps[i].kind != S_NOP) m->exec_steps.push_back(i);
+  return ORE_OK;
+}
+
+// storage of a value for the current run: pointer to image 0 and per-image stride
+struct Ref { float* p; int64_t nstride; };
+
+Ref ref_of(ore_model* m, int id) {
+  const Value& v = m->values[id];
+  if (v.is_const) return {v.cptr, 0};
+  if (v.alias_of >= 0) {
+    Ref base = ref_of(m, v.alias_of);
+    const int64_t ns = v.nstride ? v.nstride : base.nstride;
+    return {base.p + v.alias_off, ns};
+  }
+  if (v.is_input) return {const_cast<float*>(m->cur_in), v.per_image()};
+  if (v.is_output && m->out_bound) return {m->cur_out, v.per_image()};
+  return {reinterpret_cast<float*>(m->arena + v.arena_off), v.per_image()};
+}
+
+ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
+  ore_ctx* ctx = m->ctx;
+  const Ref y = ref_of(m, s.out);
+  switch (s.kind) {
+    case S_CONV: {
+      const Ref x = ref_of(m, s.in0);
+      const float* bias = s.in2 >= 0 ? m->values[s.in2].cptr : nullptr;
+      return run_conv(ctx, x.p, n, s.C, s.H, s.W, x.nstride, m->values[s.in1].cptr, s.M, s.kh, s.kw, false, bias,
+                      s.win, s.sh, s.sw, s.relu, y.p, y.nstride);
+    }
+    case S_MATMUL: {
+      const Ref x = ref_of(m, s.in0);
+      return run_conv(ctx, x.p, n, s.C, 1, 1, x.nstride, m->values[s.in1].cptr, s.M, 1, 1, true, nullptr, s.win, 1,
+                      1, false, y.p, y.nstride);
+    }
+    case S_MAXPOOL: {
+      const Ref x = ref_of(m, s.in0);
+      return run_maxpool(ctx, x.p, n, s.C, s.H, s.W, x.nstride, s.kh, s.kw, s.win, s.sh, s.sw, y.p, y.nstride);
+    }
+    default: break;
+  }
+  // contiguous ops through the public entry points
+  auto as_tensor = [&](int id, int64_t batch) {
+    const Value& v = m->values[id];
+    const Ref r = ref_of(m, id);
+    ore_tensor t{};
+    t.data = r.p;
+    t.ndim = v.ndim;
+    for (int i = 0; i < v.ndim; ++i) t.dims[i] = v.dims[i];
+    if (!v.is_const) t.dims[0] = batch;
+    t.nstride = v.is_const ? 0 : r.nstride;
+    return t;
+  };
+  ore_tensor X = as_tensor(s.in0, n), Y = as_tensor(s.out, n);
+  switch (s.kind) {
+    case S_RELU: return ore_relu_f32(ctx, &X, &Y);
+    case S_SOFTMAX: return ore_softmax_f32(ctx, &X, &Y);
+    case S_GAP: return ore_gap_f32(ctx, &X, &Y);
+    case S_COPY: return ore_dropout_f32(ctx, &X, &Y);
+    case S_ADD: {
+      ore_tensor B = as_tensor(s.in1, n);
+      return ore_add_f32(ctx, &X, &B, &Y);
+    }
+    case S_CONCAT: {
+      ore_tensor B = as_tensor(s.in1, n);
+      return ore_concat_f32(ctx, &X, &B, s.axis, &Y);
+    }
+    default: return err(m, ORE_ERR_INVALID, "internal: unexpected step kind");
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+ore_status ore_model_load(ore_ctx* ctx, const void* bytes, size_t len, int64_t max_batch, ore_model** out) {
+  if (!ctx || !bytes || !out || max_batch <= 0) return set_error(ctx, ORE_ERR_INVALID, "invalid argument");
+  ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+  Graph g;
+  std::string perr;
+  if (!parse_model(static_cast<const uint8_t*>(bytes), len, &g, &perr)) return set_error(ctx, ORE_ERR_PARSE, "%s", perr.c_str());
+  ore_model* m = new ore_model();
+  m->ctx = ctx;
+  m->max_batch = max_batch;
+  auto fail = [&](ore_status st) {
+    ore_model_destroy(m);
+    return st;
+  };
+  // initializers: shapes from graph.input when listed there (get_input_data_shape, utils.rs:53-97),
+  // else TensorProto.dims; f32 data uploaded once into one allocation.
+  std::map<std::string, const ValueInfo*> gin;
+  for (auto& vi : g.inputs) gin[vi.name] = &vi;
+  size_t total = 0;
+  for (auto& t : g.inits) total += (t.f32.size() * 4 + 255) / 256 * 256;
+  std::vector<char> host(total ? total : 1, 0);
+  if (total && hipMalloc(reinterpret_cast<void**>(&m->consts), total) != hipSuccess)
+    return fail(set_error(ctx, ORE_ERR_OOM, "initializer upload allocation failed"));
+  size_t off = 0;
+  for (auto& t : g.inits) {
+    int id = new_value(m, t.name);
+    Value& v = m->values[id];
+    v.is_const = true;
+    std::vector<int64_t> shape = t.dims;
+    auto it = gin.find(t.name);
+    if (it != gin.end() && !it->second->shape.empty()) shape = it->second->shape;
+    if (shape.size() > 4) return fail(set_error(ctx, ORE_ERR_UNSUPPORTED, "initializer '%s' rank > 4", t.name.c_str()));
+    v.ndim = int(shape.size());
+    for (size_t i = 0; i < shape.size(); ++i) v.dims[i] = shape[i];
+    if (!t.f32.empty()) {
+      if (int64_t(t.f32.size()) != v.numel_const())
+        return fail(set_error(ctx, ORE_ERR_INVALID, "initializer '%s' has %zu values for its shape", t.name.c_str(), t.f32.size()));
+      std::memcpy(host.data() + off, t.f32.data(), t.f32.size() * 4);
+      v.cptr = reinterpret_cast<float*>(reinterpret_cast<char*>(m->consts) + off);
+      off += (t.f32.size() * 4 + 255) / 256 * 256;
+    }
+    if (!t.i64.empty()) { v.i64 = t.i64; v.has_i64 = true; }
+  }
+  if (total) {
+    if (hipMemcpy(m->consts, host.data(), total, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(set_error(ctx, ORE_ERR_HIP, "initializer upload failed"));
+  }
+  // seeded input (manage_input_data, utils.rs:29-45): graph inputs that are not initializers
+  for (auto& vi : g.inputs) {
+    if (value_id(m, vi.name) >= 0) continue;
+    if (m->input_value >= 0) return fail(set_error(ctx, ORE_ERR_UNSUPPORTED, "more than one seeded model input"));
+    if (vi.shape.size() != 4) return fail(set_error(ctx, ORE_ERR_UNSUPPORTED, "model input '%s' must be 4-D", vi.name.c_str()));
+    int id = new_value(m, vi.name);
+    Value& v = m->values[id];
+    v.is_input = true;
+    v.ndim = 4;
+    v.dims[0] = 1;
+    for (int i = 1; i < 4; ++i) {
+      if (vi.shape[i] <= 0) return fail(set_error(ctx, ORE_ERR_UNSUPPORTED, "symbolic input dims are not supported"));
+      v.dims[i] = vi.shape[i];
+    }
+    m->input_value = id;
+  }
+  if (m->input_value < 0) return fail(set_error(ctx, ORE_ERR_UNSUPPORTED, "model has no seeded input"));
+  for (auto& n : g.nodes) {
+    Step s;
+    ore_status st = build_node(m, n, &s);
+    if (st) { std::string e = ctx->err; ore_model_destroy(m); return set_error(ctx, st, "%s", e.c_str()); }
+    m->base_steps.push_back(s);
+  }
+  if (g.outputs.empty()) return fail(set_error(ctx, ORE_ERR_INVALID, "model has no outputs"));
+  m->output_value = value_id(m, g.outputs[0].name);
+  if (m->output_value < 0 || m->values[m->output_value].is_const)
+    return fail(set_error(ctx, ORE_ERR_INVALID, "graph output '%s' is not produced", g.outputs[0].name.c_str()));
+  m->values[m->output_value].is_output = true;
+  if (ore_status st = plan(m)) { std::string e = ctx->err; ore_model_destroy(m); return set_error(ctx, st, "%s", e.c_str()); }
+  *out = m;
+  return ORE_OK;
+}
+
+ore_status ore_model_destroy(ore_model* m) {
+  if (!m) return ORE_OK;
+  (void)hipSetDevice(m->ctx->device);
+  (void)hipStreamSynchronize(m->ctx->stream);
+  for (auto e : m->events) (void)hipEventDestroy(e);
+  if (m->arena) (void)hipFree(m->arena);
+  if (m->consts) (void)hipFree(m->consts);
+  delete m;
+  return ORE_OK;
+}
+
+ore_status ore_model_set_fusion(ore_model* m, int32_t flags) {
+  if (!m) return set_error(nullptr, ORE_ERR_INVALID, "null model");
+  m->fusion = flags & (ORE_FUSE_ALL | ORE_KEEP_VALUES);
+  return plan(m);
+}
+
+ore_status ore_model_input_dims(ore_model* m, int64_t dims[4]) {
+  if (!m || !dims) return set_error(nullptr, ORE_ERR_INVALID, "null argument");
+  for (int i = 0; i < 4; ++i) dims[i] = m->values[m->input_value].dims[i];
+  return ORE_OK;
+}
+
+ore_status ore_model_output_elems(ore_model* m, int64_t* elems) {
+  if (!m || !elems) return set_error(nullptr, ORE_ERR_INVALID, "null argument");
+  *elems = m->values[m->output_value].per_image();
+  return ORE_OK;
+}
+
+ore_status ore_model_run(ore_model* m, const float* d_input, int64_t n, float* d_output) {
+  if (!m || !d_input || !d_output) return set_error(m ? m->ctx : nullptr, ORE_ERR_INVALID, "null argument");
+  ore_ctx* ctx = m->ctx;
+  if (n < 0 || n > m->max_batch) return set_error(ctx, ORE_ERR_INVALID, "batch %lld exceeds max_batch %lld", (long long)n, (long long)m->max_batch);
+  ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+  m->cur_in = d_input;
+  m->cur_out = d_output;
+  m->last_n = n;
+  const Value& ov = m->values[m->output_value];
+  // bind the output buffer directly when its producer writes a plain contiguous tensor
+  m->out_bound = ov.alias_of < 0 && !ov.elided;
+  if (m->timing && m->events.size() < m->exec_steps.size() + 1) {
+    for (auto e : m->events) (void)hipEventDestroy(e);
+    m->events.assign(m->exec_steps.size() + 1, nullptr);
+    for (auto& e : m->events) ORE_HIP_CHECK(ctx, hipEventCreate(&e));
+  }
+  for (size_t k = 0; k < m->exec_steps.size(); ++k) {
+    if (m->timing) ORE_HIP_CHECK(ctx, hipEventRecord(m->events[k], ctx->stream));
+    ore_status st = launch_step(m, m->steps[m->exec_steps[k]], n);
+    if (st) return st;
+  }
+  if (m->timing) ORE_HIP_CHECK(ctx, hipEventRecord(m->events[m->exec_steps.size()], ctx->stream));
+  if (!m->out_bound) {
+    const Ref r = ref_of(m, m->output_value);
+    const int64_t pe = ov.per_image();
+    if (r.nstride == pe) {
+      ORE_HIP_CHECK(ctx, hipMemcpyAsync(d_output, r.p, size_t(n * pe) * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    } else {
+      ORE_HIP_CHECK(ctx, hipMemcpy2DAsync(d_output, size_t(pe) * 4, r.p, size_t(r.nstride) * 4, size_t(pe) * 4, size_t(n),
+                                          hipMemcpyDeviceToDevice, ctx->stream));
+    }
+  }
+  return ORE_OK;
+}
+
+ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst, size_t cap, int64_t dims[4],
+                                int32_t* ndim) {
+  if (!m || !name) return set_error(nullptr, ORE_ERR_INVALID, "null argument");
+  ore_ctx* ctx = m->ctx;
+  int id = value_id(m, name);
+  if (id < 0) return set_error(ctx, ORE_ERR_INVALID, "no value named '%s'", name);
+  const Value& v = m->values[id];
+  if (v.elided) return set_error(ctx, ORE_ERR_INVALID, "value '%s' is fused away", name);
+  const int64_t n = v.is_const ? 1 : m->last_n;
+  if (dims) {
+    for (int i = 0; i < 4; ++i) dims[i] = v.dims[i];
+    if (!v.is_const) dims[0] = n;
+  }
+  if (ndim) *ndim = v.ndim;
+  const int64_t pe = v.is_const ? v.numel_const() : v.per_image();
+  if (!host_dst) return ORE_OK;
+  if (size_t(n * pe) > cap) return set_error(ctx, ORE_ERR_INVALID, "destination too small");
+  if (!v.is_const && v.first < 0 && !v.is_input) return set_error(ctx, ORE_ERR_INVALID, "value '%s' not materialised", name);
+  ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+  ORE_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  const Ref r = ref_of(m, id);
+  if (!r.p) return set_error(ctx, ORE_ERR_INVALID, "value '%s' has no f32 storage", name);
+  const int64_t ns = v.is_const ? pe : r.nstride;
+  ORE_HIP_CHECK(ctx, hipMemcpy2D(host_dst, size_t(pe) * 4, r.p, size_t(ns) * 4, size_t(pe) * 4, size_t(n),
+                                 hipMemcpyDeviceToHost));
+  return ORE_OK;
+}
+
+ore_status ore_model_enable_timing(ore_model* m, int32_t on) {
+  if (!m) return set_error(nullptr, ORE_ERR_INVALID, "null model");
+  m->timing = on != 0;
+  return ORE_OK;
+}
+
+int32_t ore_model_step_count(ore_model* m) { return m ? int32_t(m->exec_steps.size()) : 0; }
+
+ore_status ore_model_step_info(ore_model* m, int32_t i, const char** op, const char** name, double* flops, double* bytes) {
+  if (!m || i < 0 || size_t(i) >= m->exec_steps.size()) return set_error(nullptr, ORE_ERR_INVALID, "bad step index");
+  const Step& s = m->steps[m->exec_steps[i]];
+  static const char* kinds[] = {"Conv", "MaxPool", "Relu", "Add", "Softmax", "MatMul", "GlobalAveragePool", "Concat", "Copy", "Nop"};
+  if (op) *op = kinds[s.kind];
+  if (name) *name = s.name.c_str();
+  const double n = double(m->last_n);
+  if (flops) *flops = s.flops_per_img * n;
+  if (bytes) {
+    double b = s.bytes_per_img * n + s.bytes_fixed;
+    // fused epilogues/in-place writes move fewer bytes than the op-by-op accounting
+    *bytes = b;
+  }
+  return ORE_OK;
+}
+
+ore_status ore_model_step_times(ore_model* m, float* ms, int32_t cap) {
+  if (!m || !ms) return set_error(nullptr, ORE_ERR_INVALID, "null argument");
+  if (!m->timing || m->events.size() < m->exec_steps.size() + 1) return set_error(m->ctx, ORE_ERR_INVALID, "timing not enabled");
+  ORE_HIP_CHECK(m->ctx, hipEventSynchronize(m->events[m->exec_steps.size()]));
+  for (size_t k = 0; k < m->exec_steps.size() && int32_t(k) < cap; ++k)
+    ORE_HIP_CHECK(m->ctx, hipEventElapsedTime(&ms[k], m->events[k], m->events[k + 1]));
+  return ORE_OK;
+}
+
+}  // extern "C"

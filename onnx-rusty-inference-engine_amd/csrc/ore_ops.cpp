@@ -1,0 +1,410 @@
+// C ABI: context, memory, reference geometry and the per-op entry points that replace the
+// functions behind `node_inference` (model_inference.rs:137-161).
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "ore_internal.h"
+
+namespace {
+thread_local std::string g_global_err;
+}
+
+namespace ore {
+
+ore_status set_error(ore_ctx* ctx, ore_status st, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  g_global_err = buf;
+  return st;
+}
+
+// get_padding_size (convolution_op.rs:519-557 == max_pool_op.rs:363-401).  The reference
+// returns (pad_h, pad_w, pad_bottom, pad_top, pad_right, pad_left) into variables named
+// (pad_num_h, pad_num_w, pad_top, pad_bottom, pad_left, pad_right): the larger half lands on
+// the top/left, for SAME_UPPER and SAME_LOWER alike.
+static ore_status same_padding(ore_ctx* ctx, int64_t H, int64_t W, int64_t sh, int64_t sw, int64_t kh, int64_t kw,
+                               Window* w) {
+  const int64_t ph = (H % sh == 0) ? kh - sh : kh - (H % sh);
+  const int64_t pw = (W % sw == 0) ? kw - sw : kw - (W % sw);
+  if (ph < 0 || pw < 0)  // usize underflow in the reference
+    return set_error(ctx, ORE_ERR_UNSUPPORTED, "SAME padding with kernel smaller than stride/remainder");
+  w->pb = ph / 2;
+  w->pt = ph - w->pb;
+  w->pr = pw / 2;
+  w->pl = pw - w->pr;
+  return ORE_OK;
+}
+
+ore_status resolve_window(ore_ctx* ctx, int auto_pad, const int64_t* pads, int n_pads, int64_t H, int64_t W,
+                          int64_t kh, int64_t kw, int64_t sh, int64_t sw, Window* out) {
+  *out = Window{};
+  if (sh <= 0 || sw <= 0 || kh <= 0 || kw <= 0)
+    return set_error(ctx, ORE_ERR_INVALID, "non-positive kernel/stride");
+  switch (auto_pad) {
+    case ORE_PAD_SAME_UPPER:
+    case ORE_PAD_SAME_LOWER:
+      // H' = ceil(H / stride), computed in f32 as the reference does (:297-310)
+      out->Ho = int64_t(std::ceil(float(H) / float(sh)));
+      out->Wo = int64_t(std::ceil(float(W) / float(sw)));
+      return same_padding(ctx, H, W, sh, sw, kh, kw, out);
+    case ORE_PAD_NOTSET: {
+      if (n_pads < 4) return set_error(ctx, ORE_ERR_INVALID, "auto_pad NOTSET needs 4 pads");
+      out->pt = pads[0]; out->pl = pads[1]; out->pb = pads[2]; out->pr = pads[3];
+      if (out->pt < 0 || out->pl < 0 || out->pb < 0 || out->pr < 0)
+        return set_error(ctx, ORE_ERR_INVALID, "negative pads");
+      if (H + out->pt + out->pb < kh || W + out->pl + out->pr < kw)
+        return set_error(ctx, ORE_ERR_INVALID, "window larger than padded input");
+      out->Ho = (H - kh + out->pt + out->pb) / sh + 1;  // floor (:312-317)
+      out->Wo = (W - kw + out->pl + out->pr) / sw + 1;
+      return ORE_OK;
+    }
+    case ORE_PAD_VALID:
+      if (H < kh || W < kw) return set_error(ctx, ORE_ERR_INVALID, "window larger than input");
+      out->Ho = (H - kh) / sh + 1;
+      out->Wo = (W - kw) / sw + 1;
+      return ORE_OK;
+    default:
+      return set_error(ctx, ORE_ERR_UNSUPPORTED, "unknown auto_pad %d", auto_pad);
+  }
+}
+
+static int64_t nstride_of(const ore_tensor* t) {
+  if (t->nstride) return t->nstride;
+  int64_t s = 1;
+  for (int i = 1; i < t->ndim; ++i) s *= t->dims[i];
+  return s;
+}
+
+static int64_t numel(const ore_tensor* t) {
+  int64_t s = 1;
+  for (int i = 0; i < t->ndim; ++i) s *= t->dims[i];
+  return s;
+}
+
+static bool contiguous(const ore_tensor* t) {
+  if (!t->nstride) return true;
+  int64_t s = 1;
+  for (int i = 1; i < t->ndim; ++i) s *= t->dims[i];
+  return t->nstride == s;
+}
+
+static bool fits_i32(int64_t v) { return v >= 0 && v < (int64_t(1) << 31); }
+
+ore_status run_conv(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
+                    const float* w, int64_t M, int64_t kh, int64_t kw, bool w_kmajor, const float* bias,
+                    const Window& win, int64_t sh, int64_t sw, bool relu, float* y, int64_t y_nstride) {
+  if (N == 0) return ORE_OK;
+  ConvParams p{};
+  p.x = x; p.w = w; p.bias = bias; p.y = y;
+  p.N = int(N); p.C = int(C); p.H = int(H); p.W = int(W);
+  p.M = int(M); p.kh = int(kh); p.kw = int(kw); p.sh = int(sh); p.sw = int(sw);
+  p.pt = int(win.pt); p.pl = int(win.pl);
+  p.Ho = int(win.Ho); p.Wo = int(win.Wo);
+  p.K = int(C * kh * kw);
+  p.P = int(win.Ho * win.Wo);
+  p.Ntot = N * win.Ho * win.Wo;
+  p.x_nstride = x_nstride;
+  p.y_nstride = y_nstride;
+  p.relu = relu ? 1 : 0;
+  p.w_kmajor = w_kmajor ? 1 : 0;
+  p.is1x1 = (kh == 1 && kw == 1 && sh == 1 && sw == 1 && win.pt == 0 && win.pl == 0 && win.Ho == H && win.Wo == W);
+  if (!fits_i32(C * H * W) || !fits_i32(M * p.P) || !fits_i32(p.K * M) || !fits_i32(p.Ntot / 1) ||
+      (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))
+    return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
+  if (w_kmajor && !p.is1x1) return set_error(ctx, ORE_ERR_INVALID, "K-major weights need a 1x1 geometry");
+  launch_conv(p, ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
+}
+
+ore_status run_maxpool(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
+                       int64_t x_nstride, int64_t kh, int64_t kw, const Window& win, int64_t sh, int64_t sw,
+                       float* y, int64_t y_nstride) {
+  if (N == 0) return ORE_OK;
+  PoolParams p{};
+  p.x = x; p.y = y;
+  p.N = int(N); p.C = int(C); p.H = int(H); p.W = int(W);
+  p.kh = int(kh); p.kw = int(kw); p.sh = int(sh); p.sw = int(sw);
+  p.pt = int(win.pt); p.pl = int(win.pl);
+  p.Ho = int(win.Ho); p.Wo = int(win.Wo);
+  p.x_nstride = x_nstride; p.y_nstride = y_nstride;
+  launch_maxpool(p, ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
+}
+
+}  // namespace ore
+
+using namespace ore;
+
+// =================================================================================== C ABI
+extern "C" {
+
+int32_t ore_abi_version(void) { return ORE_ABI_VERSION; }
+
+const char* ore_last_error(ore_ctx* ctx) { return ctx ? ctx->err.c_str() : g_global_err.c_str(); }
+
+ore_status ore_ctx_create(int32_t device, ore_ctx** out) {
+  if (!out) return set_error(nullptr, ORE_ERR_INVALID, "null out");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) return set_error(nullptr, ORE_ERR_HIP, "no HIP device available");
+  if (device < 0 || device >= n) return set_error(nullptr, ORE_ERR_INVALID, "device %d out of range", device);
+  ORE_HIP_CHECK(nullptr, hipSetDevice(device));
+  ore_ctx* c = new ore_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return set_error(nullptr, ORE_ERR_HIP, "hipStreamCreate failed");
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return ORE_OK;
+}
+
+ore_status ore_ctx_destroy(ore_ctx* ctx) {
+  if (!ctx) return ORE_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->own_stream) {
+    (void)hipStreamSynchronize(ctx->own_stream);
+    (void)hipStreamDestroy(ctx->own_stream);
+  }
+  delete ctx;
+  return ORE_OK;
+}
+
+ore_status ore_ctx_set_stream(ore_ctx* ctx, void* s) {
+  if (!ctx) return set_error(nullptr, ORE_ERR_INVALID, "null ctx");
+  ctx->stream = reinterpret_cast<hipStream_t>(s);
+  return ORE_OK;
+}
+
+void* ore_ctx_get_stream(ore_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
+
+ore_status ore_sync(ore_ctx* ctx) {
+  if (!ctx) return set_error(nullptr, ORE_ERR_INVALID, "null ctx");
+  ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+  ORE_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return ORE_OK;
+}
+
+ore_status ore_malloc(ore_ctx* ctx, size_t bytes, void** dptr) {
+  if (!ctx || !dptr) return set_error(ctx, ORE_ERR_INVALID, "null argument");
+  ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+  if (hipMalloc(dptr, bytes ? bytes : 1) != hipSuccess) return set_error(ctx, ORE_ERR_OOM, "hipMalloc(%zu) failed", bytes);
+  return ORE_OK;
+}
+
+ore_status ore_free(ore_ctx* ctx, void* dptr) {
+  if (!ctx) return set_error(nullptr, ORE_ERR_INVALID, "null ctx");
+  if (dptr) ORE_HIP_CHECK(ctx, hipFree(dptr));
+  return ORE_OK;
+}
+
+ore_status ore_upload(ore_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return set_error(nullptr, ORE_ERR_INVALID, "null ctx");
+  ORE_HIP_CHECK(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  ORE_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return ORE_OK;
+}
+
+ore_status ore_download(ore_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return set_error(nullptr, ORE_ERR_INVALID, "null ctx");
+  ORE_HIP_CHECK(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  ORE_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return ORE_OK;
+}
+
+// ----------------------------------------------------------------------------- shapes
+static ore_status conv_geometry(ore_ctx* ctx, const int64_t xd[4], const int64_t wd[4], const ore_conv_attrs* a,
+                                Window* win) {
+  if (!a) return set_error(ctx, ORE_ERR_INVALID, "null conv attrs");
+  if (a->group != 1 || xd[1] != wd[1])  // assert at convolution_op.rs:252
+    return set_error(ctx, ORE_ERR_UNSUPPORTED, "Conv: group must be 1 and Cin must match the weights");
+  if (a->dilations[0] != 1 || a->dilations[1] != 1)
+    return set_error(ctx, ORE_ERR_UNSUPPORTED, "Conv: dilation > 1 is not supported by the reference path");
+  int auto_pad = a->auto_pad;
+  if (a->n_pads >= 4 && (a->pads[0] > 0 || a->pads[1] > 0 || a->pads[2] > 0 || a->pads[3] > 0))
+    auto_pad = ORE_PAD_NOTSET;  // convolution_op.rs:169-173
+  return resolve_window(ctx, auto_pad, a->pads, a->n_pads, xd[2], xd[3], wd[2], wd[3], a->strides[0],
+                        a->strides[1], win);
+}
+
+ore_status ore_conv_out_shape(const int64_t x_dims[4], const int64_t w_dims[4], const ore_conv_attrs* a,
+                              int64_t y_dims[4], int64_t pads_tlbr[4]) {
+  Window win;
+  ore_status st = conv_geometry(nullptr, x_dims, w_dims, a, &win);
+  if (st) return st;
+  y_dims[0] = x_dims[0]; y_dims[1] = w_dims[0]; y_dims[2] = win.Ho; y_dims[3] = win.Wo;
+  if (pads_tlbr) { pads_tlbr[0] = win.pt; pads_tlbr[1] = win.pl; pads_tlbr[2] = win.pb; pads_tlbr[3] = win.pr; }
+  return ORE_OK;
+}
+
+ore_status ore_pool_out_shape(const int64_t x_dims[4], const ore_pool_attrs* a, int64_t y_dims[4],
+                              int64_t pads_tlbr[4]) {
+  if (!a) return set_error(nullptr, ORE_ERR_INVALID, "null pool attrs");
+  Window win;
+  ore_status st = resolve_window(nullptr, a->auto_pad, a->pads, a->n_pads, x_dims[2], x_dims[3], a->kernel[0],
+                                 a->kernel[1], a->strides[0], a->strides[1], &win);
+  if (st) return st;
+  y_dims[0] = x_dims[0]; y_dims[1] = x_dims[1]; y_dims[2] = win.Ho; y_dims[3] = win.Wo;
+  if (pads_tlbr) { pads_tlbr[0] = win.pt; pads_tlbr[1] = win.pl; pads_tlbr[2] = win.pb; pads_tlbr[3] = win.pr; }
+  return ORE_OK;
+}
+
+// ----------------------------------------------------------------------------- ops
+ore_status ore_conv2d_f32(ore_ctx* ctx, const ore_tensor* x, const ore_tensor* w, const ore_tensor* bias,
+                          const ore_conv_attrs* a, ore_tensor* y) {
+  if (!ctx || !x || !w || !y || !a) return set_error(ctx, ORE_ERR_INVALID, "null argument");
+  if (x->ndim != 4 || w->ndim != 4 || y->ndim != 4) return set_error(ctx, ORE_ERR_INVALID, "Conv expects 4-D x, w, y");
+  if (!contiguous(w)) return set_error(ctx, ORE_ERR_INVALID, "Conv weights must be contiguous");
+  Window win;
+  ore_status st = conv_geometry(ctx, x->dims, w->dims, a, &win);
+  if (st) return st;
+  if (bias && (bias->ndim != 1 || bias->dims[0] != w->dims[0]))
+    return set_error(ctx, ORE_ERR_INVALID, "Bias array has the wrong shape");  // add_bias :710
+  if (y->dims[0] != x->dims[0] || y->dims[1] != w->dims[0] || y->dims[2] != win.Ho || y->dims[3] != win.Wo)
+    return set_error(ctx, ORE_ERR_INVALID, "Conv output dims mismatch: expected [%lld,%lld,%lld,%lld]",
+                     (long long)x->dims[0], (long long)w->dims[0], (long long)win.Ho, (long long)win.Wo);
+  return run_conv(ctx, x->data, x->dims[0], x->dims[1], x->dims[2], x->dims[3], nstride_of(x), w->data, w->dims[0],
+                  w->dims[2], w->dims[3], false, bias ? bias->data : nullptr, win, a->strides[0], a->strides[1],
+                  a->fuse_relu != 0, y->data, nstride_of(y));
+}
+
+ore_status ore_maxpool2d_f32(ore_ctx* ctx, const ore_tensor* x, const ore_pool_attrs* a, ore_tensor* y) {
+  if (!ctx || !x || !y || !a) return set_error(ctx, ORE_ERR_INVALID, "null argument");
+  if (x->ndim != 4 || y->ndim != 4) return set_error(ctx, ORE_ERR_INVALID, "MaxPool expects 4-D tensors");
+  Window win;
+  ore_status st = resolve_window(ctx, a->auto_pad, a->pads, a->n_pads, x->dims[2], x->dims[3], a->kernel[0],
+                                 a->kernel[1], a->strides[0], a->strides[1], &win);
+  if (st) return st;
+  if (y->dims[0] != x->dims[0] || y->dims[1] != x->dims[1] || y->dims[2] != win.Ho || y->dims[3] != win.Wo)
+    return set_error(ctx, ORE_ERR_INVALID, "MaxPool output dims mismatch");
+  return run_maxpool(ctx, x->data, x->dims[0], x->dims[1], x->dims[2], x->dims[3], nstride_of(x), a->kernel[0],
+                     a->kernel[1], win, a->strides[0], a->strides[1], y->data, nstride_of(y));
+}
+
+ore_status ore_relu_f32(ore_ctx* ctx, const ore_tensor* x, ore_tensor* y) {
+  if (!ctx || !x || !y) return set_error(ctx, ORE_ERR_INVALID, "null argument");
+  if (numel(x) != numel(y)) return set_error(ctx, ORE_ERR_INVALID, "Relu size mismatch");
+  if (!contiguous(x) || !contiguous(y)) return set_error(ctx, ORE_ERR_INVALID, "Relu expects contiguous tensors");
+  launch_relu(x->data, y->data, numel(x), ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
+}
+
+ore_status ore_add_f32(ore_ctx* ctx, const ore_tensor* a, const ore_tensor* b, ore_tensor* y) {
+  if (!ctx || !a || !b || !y) return set_error(ctx, ORE_ERR_INVALID, "null argument");
+  if (b->ndim > a->ndim || a->ndim > 4 || a->ndim < 1) return set_error(ctx, ORE_ERR_INVALID, "Add: rank mismatch");
+  if (!contiguous(a) || !contiguous(b) || !contiguous(y) || numel(a) != numel(y))
+    return set_error(ctx, ORE_ERR_INVALID, "Add expects contiguous, same-size a and y");
+  AddParams p{};
+  p.a = a->data; p.b = b->data; p.y = y->data;
+  int64_t bd[4] = {1, 1, 1, 1};
+  for (int i = 0; i < 4; ++i) p.d[i] = 1;
+  for (int i = 0; i < a->ndim; ++i) p.d[4 - a->ndim + i] = a->dims[i];
+  for (int i = 0; i < b->ndim; ++i) bd[4 - b->ndim + i] = b->dims[i];
+  int64_t s = 1;
+  for (int i = 3; i >= 0; --i) {
+    if (bd[i] != 1 && bd[i] != p.d[i]) return set_error(ctx, ORE_ERR_INVALID, "Add: shapes not broadcastable");
+    p.bs[i] = bd[i] == 1 ? 0 : s;
+    s *= bd[i];
+  }
+  if (numel(a) == 0) return ORE_OK;
+  launch_add_bcast(p, ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
+}
+
+ore_status ore_softmax_f32(ore_ctx* ctx, const ore_tensor* x, ore_tensor* y) {
+  if (!ctx || !x || !y) return set_error(ctx, ORE_ERR_INVALID, "null argument");
+  if (!contiguous(x) || !contiguous(y) || numel(x) != numel(y))
+    return set_error(ctx, ORE_ERR_INVALID, "Softmax expects contiguous same-size tensors");
+  const int64_t rows = x->dims[0];
+  if (rows == 0) return ORE_OK;
+  const int64_t D = numel(x) / rows;
+  if (D <= 0 || D >= (int64_t(1) << 31)) return set_error(ctx, ORE_ERR_INVALID, "Softmax row length");
+  launch_softmax(x->data, y->data, rows, int(D), ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
+}
+
+ore_status ore_matmul_f32(ore_ctx* ctx, const ore_tensor* a, const ore_tensor* b, ore_tensor* y) {
+  if (!ctx || !a || !b || !y) return set_error(ctx, ORE_ERR_INVALID, "null argument");
+  if (a->ndim != 2 || b->ndim != 2 || y->ndim != 2 || a->dims[1] != b->dims[0] || y->dims[0] != a->dims[0] ||
+      y->dims[1] != b->dims[1])
+    return set_error(ctx, ORE_ERR_INVALID, "MatMul expects a[M,K] . b[K,N] -> y[M,N]");
+  if (!contiguous(a) || !contiguous(b) || !contiguous(y))
+    return set_error(ctx, ORE_ERR_INVALID, "MatMul expects contiguous tensors");
+  // y[m][n] = sum_k a[m][k] b[k][n]  ==  1x1 conv over "images" m with Cin = K, Cout = N and
+  // K-major weights b: the MFMA implicit-GEMM kernel, columns = rows of a.
+  Window win;
+  win.Ho = 1; win.Wo = 1;
+  return run_conv(ctx, a->data, a->dims[0], a->dims[1], 1, 1, a->dims[1], b->data, b->dims[1], 1, 1, true,
+                  nullptr, win, 1, 1, false, y->data, y->dims[1]);
+}
+
+ore_status ore_gap_f32(ore_ctx* ctx, const ore_tensor* x, ore_tensor* y) {
+  if (!ctx || !x || !y) return set_error(ctx, ORE_ERR_INVALID, "null argument");
+  if (x->ndim != 4 || !contiguous(x) || !contiguous(y) || numel(y) != x->dims[0] * x->dims[1])
+    return set_error(ctx, ORE_ERR_INVALID, "GlobalAveragePool expects contiguous [N,C,H,W] -> [N,C,1,1]");
+  const int64_t HW = x->dims[2] * x->dims[3];
+  if (HW <= 0 || HW >= (int64_t(1) << 31)) return set_error(ctx, ORE_ERR_INVALID, "GAP spatial size");
+  launch_gap(x->data, y->data, x->dims[0] * x->dims[1], int(HW), ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
+}
+
+ore_status ore_concat_f32(ore_ctx* ctx, const ore_tensor* a, const ore_tensor* b, int64_t axis, ore_tensor* y) {
+  if (!ctx || !a || !b || !y) return set_error(ctx, ORE_ERR_INVALID, "null argument");
+  if (a->ndim != 4 || b->ndim != 4 || y->ndim != 4 || axis < 0 || axis > 3)
+    return set_error(ctx, ORE_ERR_INVALID, "Concat expects 4-D tensors and axis in [0,3]");
+  for (int i = 0; i < 4; ++i) {
+    const int64_t want = (i == axis) ? a->dims[i] + b->dims[i] : a->dims[i];
+    if ((i != axis && a->dims[i] != b->dims[i]) || y->dims[i] != want)
+      return set_error(ctx, ORE_ERR_INVALID, "Concat shape mismatch");
+  }
+  if (!contiguous(a) || !contiguous(b) || !contiguous(y))
+    return set_error(ctx, ORE_ERR_INVALID, "Concat expects contiguous tensors");
+  int64_t outer = 1, ia = 1, ib = 1;
+  for (int i = 0; i < axis; ++i) outer *= a->dims[i];
+  for (int i = int(axis); i < 4; ++i) { ia *= a->dims[i]; ib *= b->dims[i]; }
+  if (outer * (ia + ib) == 0) return ORE_OK;
+  launch_concat(a->data, b->data, y->data, outer, ia, ib, ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
+}
+
+ore_status ore_dropout_f32(ore_ctx* ctx, const ore_tensor* x, ore_tensor* y) {
+  if (!ctx || !x || !y) return set_error(ctx, ORE_ERR_INVALID, "null argument");
+  if (numel(x) != numel(y) || !contiguous(x) || !contiguous(y))
+    return set_error(ctx, ORE_ERR_INVALID, "Dropout size mismatch");
+  if (x->data == y->data) return ORE_OK;
+  ORE_HIP_CHECK(ctx, hipMemcpyAsync(y->data, x->data, size_t(numel(x)) * 4, hipMemcpyDeviceToDevice, ctx->stream));
+  return ORE_OK;
+}
+
+ore_status ore_reshape(const ore_tensor* x, const int64_t* shape, int32_t n_shape, ore_tensor* y) {
+  if (!x || !shape || !y) return set_error(nullptr, ORE_ERR_INVALID, "null argument");
+  if (n_shape != 2) return set_error(nullptr, ORE_ERR_UNSUPPORTED, "Reshape produces 2-D only (reshape_op.rs:87-91)");
+  if (!contiguous(x)) return set_error(nullptr, ORE_ERR_INVALID, "Reshape of a strided view");
+  int64_t ns[2] = {shape[0], shape[1]};
+  for (int i = 0; i < 2; ++i)
+    if (ns[i] == 0) ns[i] = x->dims[i];  // allowzero = 0 (:69-83)
+  if (ns[0] < 0 || ns[1] < 0 || ns[0] * ns[1] != numel(x))
+    return set_error(nullptr, ORE_ERR_INVALID, "Reshape element count mismatch");
+  *y = ore_tensor{};
+  y->data = x->data;
+  y->ndim = 2;
+  y->dims[0] = ns[0];
+  y->dims[1] = ns[1];
+  return ORE_OK;
+}
+
+}  // extern "C"

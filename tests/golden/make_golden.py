@@ -1,0 +1,63 @@
+"""Regenerates the committed golden fixtures of this directory from the C oracle (the CPU
+restatement of the reference, oracle/).  Run from the repo root:  python tests/golden/make_golden.py
+
+  squeezenet_synth_oracle.npz  synthetic SqueezeNet-1.0 (ore.squeezenet.build(224), seed 1234),
+                               input = [zoo image squeezenet_data_0.pb, synthetic_input(1, seed 0)],
+                               output = oracle softmax rows [2, 1000]
+  squeezenet_mini_oracle.npz   the same topology at 64x64 input, 4 seeded images; also every
+                               intermediate value of image 0 (for node-level parity)
+  mnist_oracle.npz             mnist-8.onnx on mnist_data_0.pb and 3 derived images
+
+The reference data files (mnist-8.onnx, *.pb) are copied verbatim from the reference repo's
+fixtures; the .npz files are outputs of oracle/ (pinned against mnist_output_0.pb).
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "onnx-rusty-inference-engine_amd"))
+
+import oracle  # noqa: E402
+from ore import onnx_wire, squeezenet  # noqa: E402
+
+
+def squeezenet_inputs():
+    zoo = onnx_wire.load_tensor(os.path.join(HERE, "squeezenet_data_0.pb")).to_numpy()
+    return np.concatenate([zoo, squeezenet.synthetic_input(1, 224, seed=0)]).astype(np.float32)
+
+
+def mini_inputs():
+    return squeezenet.synthetic_input(4, 64, seed=5)
+
+
+def mnist_inputs():
+    x = onnx_wire.load_tensor(os.path.join(HERE, "mnist_data_0.pb")).to_numpy()
+    rng = np.random.default_rng(9)
+    extra = rng.uniform(-30, 30, size=(3, 1, 28, 28)).astype(np.float32)
+    return np.concatenate([x, extra]).astype(np.float32)
+
+
+def main():
+    m = oracle.Model(squeezenet.build(224))
+    y = m.run(squeezenet_inputs(), 1000)
+    np.savez_compressed(os.path.join(HERE, "squeezenet_synth_oracle.npz"), output=y)
+
+    mini = squeezenet.build(64)
+    m = oracle.Model(mini)
+    x = mini_inputs()
+    y = m.run(x, 1000)
+    np.savez_compressed(os.path.join(HERE, "squeezenet_mini_oracle.npz"), output=y)
+
+    with open(os.path.join(HERE, "mnist-8.onnx"), "rb") as f:
+        m = oracle.Model(f.read())
+    y = m.run(mnist_inputs(), 10)
+    np.savez_compressed(os.path.join(HERE, "mnist_oracle.npz"), output=y)
+    print("wrote fixtures")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,192 @@
+"""Graph-level parity: the device walker (ore_model_*, replacing inference()/node_inference())
+against the reference's golden vectors and the oracle's committed fixtures.
+
+  MNIST-8 (real CNTK weights) vs mnist_output_0.pb: |d| <= 1e-6 * max|y| (1-4 ulp of the logits)
+  synthetic SqueezeNet-1.0 @224 vs oracle fixture: <= 1e-5 max-abs on the softmax probabilities
+  full-size properties at batch 256: rows sum to 1, per-image results bit-identical to the same
+  images run alone (no cross-image arithmetic), fused == unfused bit for bit."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+
+
+def _t(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
+
+
+def _np(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def _mnist_bytes():
+    with open(os.path.join(GOLD, "mnist-8.onnx"), "rb") as f:
+        return f.read()
+
+
+@pytest.fixture(scope="module")
+def squeeze224(gpu_ctx):
+    import ore
+    from ore import squeezenet
+    m = ore.Model(gpu_ctx, squeezenet.build(224), max_batch=256)
+    yield m
+    m.close()
+
+
+@pytest.mark.parametrize("fusion", [7, 0])
+def test_mnist_golden(gpu_ctx, fusion):
+    import ore
+    from ore import onnx_wire
+    m = ore.Model(gpu_ctx, _mnist_bytes(), max_batch=4)
+    m.set_fusion(fusion)
+    x = onnx_wire.load_tensor(os.path.join(GOLD, "mnist_data_0.pb")).to_numpy()
+    g = onnx_wire.load_tensor(os.path.join(GOLD, "mnist_output_0.pb")).to_numpy()
+    y = _np(m.run(_t(x)))
+    assert y.shape == (1, 10)
+    assert np.abs(y - g).max() <= 1e-6 * np.abs(g).max()
+    assert y.argmax() == g.argmax() == 2
+    m.close()
+
+
+def test_mnist_oracle_batch(gpu_ctx):
+    import ore
+    from golden.make_golden import mnist_inputs
+    ref = np.load(os.path.join(GOLD, "mnist_oracle.npz"))["output"]
+    m = ore.Model(gpu_ctx, _mnist_bytes(), max_batch=8)
+    y = _np(m.run(_t(mnist_inputs())))
+    assert np.abs(y - ref).max() <= 1e-6 * np.abs(ref).max()
+    m.close()
+
+
+def test_inference_entry_point():
+    """ore.inference() mirrors the reference's inference(model, input_data, names)."""
+    import ore
+    from ore import onnx_wire
+    x = onnx_wire.load_tensor(os.path.join(GOLD, "mnist_data_0.pb")).to_numpy().ravel()
+    g = onnx_wire.load_tensor(os.path.join(GOLD, "mnist_output_0.pb")).to_numpy()
+    y = ore.inference(_mnist_bytes(), x, ["Input3", "Parameter193"])
+    assert np.abs(y - g).max() <= 1e-6 * np.abs(g).max()
+
+
+def test_squeezenet_synth_vs_oracle(squeeze224):
+    from golden.make_golden import squeezenet_inputs
+    ref = np.load(os.path.join(GOLD, "squeezenet_synth_oracle.npz"))["output"]
+    y = _np(squeeze224.run(_t(squeezenet_inputs())))
+    assert y.shape == ref.shape == (2, 1000)
+    assert np.abs(y - ref).max() <= 1e-5
+    assert np.array_equal(y.argmax(1), ref.argmax(1))
+
+
+@pytest.mark.parametrize("fusion", [7, 0, 1, 2, 4])
+def test_squeezenet_mini_vs_oracle(gpu_ctx, fusion):
+    import ore
+    from ore import squeezenet
+    from golden.make_golden import mini_inputs
+    ref = np.load(os.path.join(GOLD, "squeezenet_mini_oracle.npz"))["output"]
+    m = ore.Model(gpu_ctx, squeezenet.build(64), max_batch=4)
+    m.set_fusion(fusion)
+    y = _np(m.run(_t(mini_inputs())))
+    assert np.abs(y - ref).max() <= 1e-5
+    m.close()
+
+
+def test_squeezenet_node_level_parity(gpu_ctx):
+    """Unfused run: every intermediate value vs the oracle op applied to the GPU's own input of
+    that node (isolates each op's error from the accumulated one)."""
+    import ore
+    import oracle
+    from ore import onnx_wire, squeezenet
+    from golden.make_golden import mini_inputs
+    mb = squeezenet.build(64)
+    model = onnx_wire.decode_model(mb)
+    inits = {t.name: t.to_numpy() for t in model.graph.initializer}
+    m = ore.Model(gpu_ctx, mb, max_batch=4)
+    m.set_fusion(ore.KEEP_VALUES)  # unfused, and no storage reuse so every value can be read back
+    xt = _t(mini_inputs()[:2])  # kept alive: read_value of the model input reads this buffer
+    _np(m.run(xt))
+    for node in model.graph.node:
+        a = node.attrs()
+        x = m.read_value(node.input[0])
+        y = m.read_value(node.output[0])
+        if node.op_type == "Conv":
+            w, b = inits[node.input[1]], inits[node.input[2]]
+            ref = oracle.conv2d(x, w, b, pads=a["pads"].ints, strides=a["strides"].ints)
+            scale = np.abs(ref).max() + 1.0
+            assert np.abs(y - ref).max() <= 1e-5 * scale, node.name
+        elif node.op_type == "Relu":
+            np.testing.assert_array_equal(y, oracle.relu(x))
+        elif node.op_type == "MaxPool":
+            ref = oracle.maxpool2d(x, a["kernel_shape"].ints, a["strides"].ints, auto_pad=a["auto_pad"].s.decode(),
+                                   pads=a["pads"].ints)
+            np.testing.assert_array_equal(y, ref)
+        elif node.op_type == "Concat":
+            np.testing.assert_array_equal(y, oracle.concat(x, m.read_value(node.input[1]), 1))
+        elif node.op_type == "Dropout":
+            np.testing.assert_array_equal(y, x)
+        elif node.op_type == "GlobalAveragePool":
+            np.testing.assert_array_equal(y, oracle.gap(x))
+        elif node.op_type == "Softmax":
+            assert np.abs(y - oracle.softmax(x)).max() <= 2e-7
+    m.close()
+
+
+def test_squeezenet_batch256_properties(squeeze224):
+    """Full benchmark size: size-independent properties (no oracle run at B=256)."""
+    import torch
+    from ore import squeezenet
+    x = squeezenet.synthetic_input(256, 224, seed=123)
+    xt = _t(x)
+    y = _np(squeeze224.run(xt))
+    assert y.shape == (256, 1000) and np.isfinite(y).all()
+    assert np.abs(y.sum(1) - 1.0).max() <= 1e-5
+    # image i of the batch == image i run alone, bit for bit (batch only tiles the N dim)
+    for i in (0, 1, 128, 255):
+        yi = _np(squeeze224.run(xt[i:i + 1].contiguous()))
+        assert np.array_equal(yi[0], y[i]), i
+    # fused and unfused graphs compute identical values
+    squeeze224.set_fusion(0)
+    y0 = _np(squeeze224.run(xt))
+    squeeze224.set_fusion(7)
+    assert np.array_equal(y0, y)
+    torch.cuda.synchronize()
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(HERE), "models", "squeezenet1.0-8.onnx")),
+                    reason="real squeezenet1.0-8.onnx is not in the repo (stripped from the reference mirror)")
+def test_real_squeezenet_golden(gpu_ctx):
+    import ore
+    from ore import onnx_wire
+    path = os.path.join(os.path.dirname(HERE), "models", "squeezenet1.0-8.onnx")
+    with open(path, "rb") as f:
+        m = ore.Model(gpu_ctx, f.read(), max_batch=1)
+    x = onnx_wire.load_tensor(os.path.join(GOLD, "squeezenet_data_0.pb")).to_numpy()
+    g = onnx_wire.load_tensor(os.path.join(GOLD, "squeezenet_output_0.pb")).to_numpy().reshape(1, -1)
+    y = _np(m.run(_t(x)))
+    assert np.abs(y - g).max() <= 1e-5
+
+
+def test_model_errors(gpu_ctx):
+    import ore
+    from ore import onnx_wire as w
+    def model(nodes, inits=(), extra_inputs=()):
+        return w.encode_model("t", nodes, [w.encode_tensor(n, a) for n, a in inits],
+                              [w.encode_value_info("x", (1, 2, 4, 4))] + list(extra_inputs),
+                              [w.encode_value_info("y", (1, 2, 4, 4))])
+    with pytest.raises(ore.OreError, match="NOT FOUND"):
+        ore.Model(gpu_ctx, model([w.encode_node("Sigmoid", ["x"], ["y"])]), 1)
+    with pytest.raises(ore.OreError, match="CONCATENATE"):
+        ore.Model(gpu_ctx, model([w.encode_node("Concat", ["x", "x"], ["y"], attrs=[w.encode_attr_int("bogus", 1)])]), 1)
+    wt = np.zeros((2, 2, 3, 3), np.float32)
+    with pytest.raises(ore.OreError, match="Auto Pad"):  # Conv accepts NOT_SET, not NOTSET
+        ore.Model(gpu_ctx, model([w.encode_node("Conv", ["x", "w"], ["y"], attrs=[
+            w.encode_attr_string("auto_pad", "NOTSET"), w.encode_attr_ints("strides", [1, 1])])], [("w", wt)]), 1)
+    with pytest.raises(ore.OreError):
+        ore.Model(gpu_ctx, b"\xff\xff\xff", 1)

@@ -1,0 +1,244 @@
+"""Per-op parity: every node_inference arm through the C ABI (libore.so, HIP on gfx950) against
+the CPU restatement of the reference (oracle/) on the same seeded inputs.
+
+Tolerances: bit-exact for Relu, MaxPool, Concat, Dropout, Reshape, Add (single rounding), GAP
+(same sequential order); Conv / MatMul within 2e-6 * sum|a*b| per output (the MFMA result is a
+k-ordered f32 fma chain, the reference sums per-channel 8-partial ndarray sums); Softmax within
+2e-7 absolute (expf ulp differences; same max and same 8-partial denominator order)."""
+import zlib
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
+
+
+def _np(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def _conv_bound(x, w, pads_tlbr, strides, Ho, Wo):
+    """sum |x| * |w| per output (float64), the scale of the rounding error of one output."""
+    import torch
+    xt = torch.from_numpy(np.abs(x).astype(np.float64))
+    wt = torch.from_numpy(np.abs(w).astype(np.float64))
+    t, l, b, r = pads_tlbr
+    xt = torch.nn.functional.pad(xt, (l, r, t, b))
+    y = torch.nn.functional.conv2d(xt, wt, stride=tuple(strides))
+    return y[:, :, :Ho, :Wo].numpy()
+
+
+CONV_CASES = [
+    # N, C, H, W, M, kh, kw, auto_pad, pads, strides, bias
+    (1, 3, 17, 19, 8, 3, 3, "NOTSET", [1, 1, 1, 1], [1, 1], True),
+    (2, 5, 16, 16, 40, 3, 3, "SAME_UPPER", None, [1, 1], True),
+    (3, 4, 15, 14, 24, 4, 4, "SAME_UPPER", None, [2, 2], False),   # asymmetric SAME split
+    (2, 4, 15, 14, 24, 4, 2, "SAME_LOWER", None, [2, 3], True),
+    (2, 7, 23, 23, 96, 7, 7, "VALID", None, [2, 2], True),          # conv1-like
+    (3, 96, 13, 13, 16, 1, 1, "VALID", None, [1, 1], True),         # squeeze (1x1 path)
+    (2, 16, 9, 9, 64, 1, 1, "NOTSET", [0, 0, 0, 0], [1, 1], True),  # expand1x1
+    (2, 16, 9, 9, 64, 3, 3, "NOTSET", [1, 1, 1, 1], [1, 1], True),  # expand3x3
+    (2, 64, 5, 5, 200, 1, 1, "VALID", None, [1, 1], True),          # conv10-like, M % 128 != 0
+    (1, 1, 28, 28, 8, 5, 5, "SAME_UPPER", None, [1, 1], False),     # MNIST conv 1
+    (1, 8, 14, 14, 16, 5, 5, "SAME_UPPER", None, [1, 1], False),    # MNIST conv 2
+    (2, 3, 11, 9, 33, 2, 3, "NOTSET", [2, 0, 1, 3], [3, 1], True),  # uneven explicit pads
+    (5, 17, 7, 7, 130, 3, 3, "NOTSET", [1, 1, 1, 1], [1, 1], False),
+    (2, 33, 6, 10, 48, 1, 1, "NOTSET", [1, 0, 0, 1], [1, 2], True),  # 1x1 with pads/stride -> generic path
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("fuse_relu", [False, True])
+def test_conv2d(gpu_ctx, case, fuse_relu):
+    import ore
+    N, C, H, W, M, kh, kw, auto_pad, pads, strides, with_bias = case
+    rng = np.random.default_rng(zlib.crc32(repr(case).encode()))
+    x = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    w = rng.standard_normal((M, C, kh, kw)).astype(np.float32)
+    b = rng.standard_normal((M,)).astype(np.float32) if with_bias else None
+    ref = oracle.conv2d(x, w, b, auto_pad=auto_pad, pads=pads, strides=strides)
+    if fuse_relu:
+        ref = oracle.relu(ref)
+    y = ore.convolution(gpu_ctx, _t(x), _t(w), _t(b) if b is not None else None, auto_pad=auto_pad, pads=pads,
+                        strides=strides, fuse_relu=fuse_relu)
+    got = _np(y)
+    assert got.shape == ref.shape
+    eff = auto_pad
+    if pads is not None and any(p > 0 for p in pads):
+        eff = "NOTSET"
+    p, Ho, Wo = oracle.resolve_window(eff, pads, H, W, kh, kw, strides[0], strides[1])
+    bound = _conv_bound(x, w, p, strides, Ho, Wo) + (np.abs(b)[None, :, None, None] if b is not None else 0)
+    err = np.abs(got.astype(np.float64) - ref.astype(np.float64))
+    assert np.all(err <= 2e-6 * bound + 1e-30), f"max err {err.max()} vs bound {(2e-6 * bound).max()}"
+
+
+def test_conv_integer_exact(gpu_ctx):
+    """Small-integer data: every partial sum is exact in f32, so GPU == oracle bit for bit."""
+    import ore
+    rng = np.random.default_rng(7)
+    x = rng.integers(-4, 5, size=(3, 12, 10, 11)).astype(np.float32)
+    w = rng.integers(-3, 4, size=(70, 12, 3, 3)).astype(np.float32)
+    b = rng.integers(-5, 6, size=(70,)).astype(np.float32)
+    ref = oracle.conv2d(x, w, b, auto_pad="SAME_UPPER", strides=(1, 1))
+    got = _np(ore.convolution(gpu_ctx, _t(x), _t(w), _t(b), auto_pad="SAME_UPPER", strides=(1, 1)))
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_conv_reference_kats(gpu_ctx):
+    """The reference's own conv test inputs (convolution_op.rs:729-832), integer-exact."""
+    import ore
+    x1 = np.arange(1, 31, dtype=np.float32).reshape(1, 1, 5, 6)
+    w1 = np.arange(1, 11, dtype=np.float32).reshape(1, 1, 5, 2)
+    x2 = np.arange(1, 61, dtype=np.float32).reshape(1, 2, 5, 6)
+    w2 = np.repeat(np.array([1, 2, 3, 4], dtype=np.float32), 12).reshape(2, 2, 3, 4)
+    x3 = np.arange(0, 35, dtype=np.float32).reshape(1, 1, 7, 5)
+    w3 = np.arange(1, 25, dtype=np.float32).reshape(2, 1, 3, 4)
+    for x, w in ((x1, w1), (x2, w2), (x3, w3)):
+        ref = oracle.conv2d(x, w, None, auto_pad="NOTSET", pads=[0, 0, 0, 0], strides=(1, 1))
+        got = _np(ore.convolution(gpu_ctx, _t(x), _t(w), None, auto_pad="NOTSET", pads=[0, 0, 0, 0],
+                                  strides=(1, 1)))
+        np.testing.assert_array_equal(got, ref)
+
+
+POOL_CASES = [
+    # N, C, H, W, k, s, auto_pad, pads
+    (2, 5, 9, 9, (3, 3), (2, 2), "VALID", None),
+    (1, 96, 109, 109, (3, 3), (2, 2), "NOTSET", [0, 0, 0, 0]),   # pool1
+    (2, 16, 54, 54, (3, 3), (2, 2), "NOTSET", [0, 0, 1, 1]),     # pool4 (ceil via pads)
+    (2, 16, 54, 54, (3, 3), (2, 2), "VALID", [0, 0, 1, 1]),      # pads ignored without NOTSET
+    (1, 8, 28, 28, (2, 2), (2, 2), "NOTSET", [0, 0, 0, 0]),      # MNIST pool 1
+    (1, 16, 14, 14, (3, 3), (3, 3), "NOTSET", [0, 0, 0, 0]),     # MNIST pool 2
+    (3, 4, 10, 7, (3, 2), (2, 1), "SAME_UPPER", None),
+    (3, 4, 10, 7, (4, 4), (3, 2), "SAME_LOWER", None),
+]
+
+
+@pytest.mark.parametrize("case", POOL_CASES)
+def test_maxpool(gpu_ctx, case):
+    import ore
+    N, C, H, W, k, s, auto_pad, pads = case
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal((N, C, H, W)) - 2.0).astype(np.float32)  # mostly negative: zero padding shows
+    ref = oracle.maxpool2d(x, k, s, auto_pad=auto_pad, pads=pads)
+    got = _np(ore.max_pool(gpu_ctx, _t(x), k, s, auto_pad=auto_pad, pads=pads))
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_relu_reference_kat(gpu_ctx):
+    """relu_op.rs:36-50: the only reference test with an expected array."""
+    import ore
+    x = np.arange(0, 35, dtype=np.float32)
+    x[17] = -17.0
+    x = x.reshape(1, 1, 7, 5)
+    expected = np.arange(0, 35, dtype=np.float32)
+    expected[17] = 0.0
+    got = _np(ore.relu(gpu_ctx, _t(x)))
+    np.testing.assert_array_equal(got.ravel(), expected)
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096, 4099, 1 << 20])
+def test_relu(gpu_ctx, n):
+    import ore
+    x = np.random.default_rng(n).standard_normal(n).astype(np.float32).reshape(1, 1, 1, n)
+    np.testing.assert_array_equal(_np(ore.relu(gpu_ctx, _t(x))), oracle.relu(x))
+
+
+def test_add(gpu_ctx):
+    import ore
+    rng = np.random.default_rng(11)
+    a = rng.standard_normal((3, 8, 5, 6)).astype(np.float32)
+    b = rng.standard_normal((8, 1, 1)).astype(np.float32)
+    np.testing.assert_array_equal(_np(ore.add(gpu_ctx, _t(a), _t(b))), oracle.add(a, b))
+    a2 = rng.standard_normal((4, 10)).astype(np.float32)
+    b2 = rng.standard_normal((1, 10)).astype(np.float32)
+    np.testing.assert_array_equal(_np(ore.add(gpu_ctx, _t(a2), _t(b2))), oracle.add(a2, b2))
+    with pytest.raises(ore.OreError):
+        ore.add(gpu_ctx, _t(a), _t(rng.standard_normal((3, 1, 1)).astype(np.float32)))
+
+
+def test_softmax_reference_kat(gpu_ctx):
+    import ore
+    x = np.array([118.85734, 5640.1426, 2., 3., 1000., 1001., 1002., 1003.], dtype=np.float32).reshape(1, 1, 2, 4)
+    got = _np(ore.softmax(gpu_ctx, _t(x)))
+    ref = oracle.softmax(x)
+    np.testing.assert_allclose(got, ref, atol=2e-7, rtol=0)
+
+
+@pytest.mark.parametrize("rows,d", [(1, 1000), (256, 1000), (3, 7), (5, 8), (2, 17), (4, 5000)])
+def test_softmax(gpu_ctx, rows, d):
+    import ore
+    x = (np.random.default_rng(d).standard_normal((rows, d, 1, 1)) * 5).astype(np.float32)
+    got = _np(ore.softmax(gpu_ctx, _t(x)))
+    ref = oracle.softmax(x)
+    assert np.abs(got - ref).max() <= 2e-7
+    assert np.array_equal(got.argmax(1), ref.argmax(1))
+
+
+@pytest.mark.parametrize("m,k,n", [(1, 256, 10), (37, 256, 10), (256, 256, 10), (5, 3, 129)])
+def test_matmul(gpu_ctx, m, k, n):
+    import ore
+    rng = np.random.default_rng(m * 7 + n)
+    a = rng.standard_normal((m, k)).astype(np.float32)
+    b = rng.standard_normal((k, n)).astype(np.float32)
+    ref = oracle.matmul(a, b)
+    got = _np(ore.mul(gpu_ctx, _t(a), _t(b)))
+    bound = np.abs(a).astype(np.float64) @ np.abs(b).astype(np.float64)
+    assert np.all(np.abs(got - ref) <= 2e-6 * bound + 1e-30)
+
+
+@pytest.mark.parametrize("shape", [(1, 2, 4, 4), (2, 1000, 13, 13), (3, 7, 1, 1), (2, 5, 129, 130)])
+def test_gap(gpu_ctx, shape):
+    import ore
+    x = np.random.default_rng(5).standard_normal(shape).astype(np.float32)
+    np.testing.assert_array_equal(_np(ore.global_average_pool(gpu_ctx, _t(x))), oracle.gap(x))
+
+
+@pytest.mark.parametrize("axis", [1, 2, 3, 0])
+def test_concat(gpu_ctx, axis):
+    import ore
+    rng = np.random.default_rng(axis)
+    sa = [2, 3, 4, 5]
+    sb = list(sa)
+    sb[axis] = 6
+    a = rng.standard_normal(sa).astype(np.float32)
+    b = rng.standard_normal(sb).astype(np.float32)
+    np.testing.assert_array_equal(_np(ore.concatenation(gpu_ctx, _t(a), _t(b), axis)), oracle.concat(a, b, axis))
+
+
+def test_dropout_reshape(gpu_ctx):
+    import ore
+    x = np.random.default_rng(1).standard_normal((4, 2, 2, 3)).astype(np.float32)
+    np.testing.assert_array_equal(_np(ore.drop_out(gpu_ctx, _t(x), 0.5)), x)
+    xt = _t(x)
+    y = ore.reshape(xt, [16, 3])   # reshape_op.rs:95-107
+    assert tuple(y.shape) == (16, 3) and y.data_ptr() == xt.data_ptr()
+    y0 = ore.reshape(xt, [0, 12])  # 0 copies the input dim
+    assert tuple(y0.shape) == (4, 12)
+    with pytest.raises(ore.OreError):
+        ore.reshape(xt, [5, 3])
+
+
+def test_error_behaviour(gpu_ctx):
+    import ore
+    x = _t(np.zeros((1, 3, 8, 8), np.float32))
+    w = _t(np.zeros((4, 2, 3, 3), np.float32))
+    with pytest.raises(ore.OreError, match="group"):          # Cin mismatch (assert, :252)
+        ore.convolution(gpu_ctx, x, w, strides=(1, 1))
+    w3 = _t(np.zeros((4, 3, 3, 3), np.float32))
+    with pytest.raises(ore.OreError):
+        ore.convolution(gpu_ctx, x, w3, strides=(1, 1), dilations=(2, 2))
+    with pytest.raises(ore.OreError):
+        ore.convolution(gpu_ctx, x, w3, strides=(1, 1), group=3)
+    with pytest.raises(ore.OreError):                          # bias of the wrong size (:710)
+        ore.convolution(gpu_ctx, x, w3, bias=_t(np.zeros(5, np.float32)), strides=(1, 1))
+    with pytest.raises(ore.OreError):                          # NOTSET without pads
+        ore.max_pool(gpu_ctx, x, (3, 3), (1, 1), auto_pad="NOTSET", pads=None)
