@@ -36,6 +36,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-step-timing", action="store_true", help="no per-kernel HIP events in the timed loop")
+    ap.add_argument("--layers", action="store_true", help="print per-kernel-step times to stderr")
     return ap.parse_args()
 
 
@@ -159,6 +160,12 @@ def main():
                 "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4), "traffic": None,
                 "per_launch_avg_us": round(1000.0 * conv["ms"] / conv["launches"], 2),
                 "algorithmic": "2*Cout*Ho*Wo*Cin*kh*kw per image (1.638 GFLOP/img)"}
+            if args.layers:
+                for info, ms in zip(infos, per_step_ms):
+                    tf = info["flops"] / (ms * 1e-3) / 1e12 if info["flops"] else 0.0
+                    gbs = info["bytes"] / (ms * 1e-3) / 1e9
+                    print(f"{info['name']:24s} {info['op']:18s} {1000 * ms:9.1f} us {tf:7.1f} TF/s {gbs:8.1f} GB/s",
+                          file=sys.stderr)
             result["breakdown_ms_per_step"] = {
                 k: {"ms": round(v["ms"], 4), "launches": v["launches"],
                     "TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["flops"] else None,

@@ -15,6 +15,8 @@ struct ore_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
+  float* scratch = nullptr;  // per-op weight packing (stream-ordered reuse)
+  size_t scratch_bytes = 0;
 };
 
 namespace ore {
@@ -79,9 +81,17 @@ ore_status resolve_window(ore_ctx* ctx, int auto_pad, const int64_t* pads, int n
                           int64_t kh, int64_t kw, int64_t sh, int64_t sw, Window* out);
 
 // ---------------------------------------------------------------- launches over resolved geometry
+// wp: weights packed by launch_pack_weights (row stride conv_packed_mp(M))
+// ktab: gather table (launch_ktab) for non-1x1 geometry
 ore_status run_conv(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
-                    const float* w, int64_t M, int64_t kh, int64_t kw, bool w_kmajor, const float* bias,
+                    const float* wp, const int2* ktab, int64_t M, int64_t kh, int64_t kw, const float* bias,
                     const Window& win, int64_t sh, int64_t sw, bool relu, float* y, int64_t y_nstride);
+// packs w (and the gather table for an input of H x W) into the context scratch buffer;
+// returns the packed weights (or null with the error set), *ktab receives the table
+float* pack_to_scratch(ore_ctx* ctx, const float* w, bool kmajor_src, int64_t M, int64_t K, int64_t kh, int64_t kw,
+                       int64_t H, int64_t W, const int2** ktab);
+// bytes of packed weights + gather table for one conv
+size_t packed_bytes(int64_t M, int64_t K);
 ore_status run_maxpool(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
                        int64_t x_nstride, int64_t kh, int64_t kw, const Window& win, int64_t sh, int64_t sw,
                        float* y, int64_t y_nstride);

@@ -7,7 +7,8 @@ namespace ore {
 
 struct ConvParams {
   const float* x;      // input  [N][C][H][W], image stride x_nstride
-  const float* w;      // weights [M][C*kh*kw] (ONNX layout) or [K][M] when w_kmajor
+  const float* wp;     // packed weights Wp[Kp][Mp] (launch_pack_weights)
+  const int2* ktab;    // gather table [Kp] (launch_ktab); unused by 1x1 geometry
   const float* bias;   // [M] or null
   float* y;            // output [N][..][Ho][Wo] starting at the channel slice; image stride y_nstride
   int N, C, H, W;
@@ -20,7 +21,7 @@ struct ConvParams {
   long long y_nstride;
   int relu;
   int is1x1;           // kh = kw = 1, stride 1, no padding, Ho*Wo == H*W
-  int w_kmajor;
+  int Mp;              // row stride of wp (conv_packed_mp(M))
   int mtiles, ntiles;  // filled by the launcher
 };
 
@@ -42,6 +43,11 @@ struct AddParams {
 };
 
 int conv_tile_config(int M);
+int conv_packed_mp(int M);  // padded M of the packed weights
+int conv_packed_kp(int K);  // padded K of the packed weights
+// w: ONNX conv weights [M][K] (kmajor_src = false) or MatMul B [K][M] (true) -> wp[Kp][Mp]
+void launch_pack_weights(const float* w, bool kmajor_src, int M, int K, float* wp, hipStream_t s);
+void launch_ktab(int2* ktab, int K, int kh, int kw, int H, int W, hipStream_t s);
 void launch_conv(const ConvParams& p, hipStream_t s);
 void launch_maxpool(const PoolParams& p, hipStream_t s);
 void launch_relu(const float* x, float* y, long long n, hipStream_t s);

@@ -67,7 +67,9 @@ struct Step {
   int64_t C = 0, H = 0, W = 0, M = 0, kh = 0, kw = 0, sh = 1, sw = 1;
   Window win;
   bool relu = false;
-  bool w_kmajor = false;
+  bool w_kmajor = false;  // MatMul: the constant operand is [K][M]
+  float* wp = nullptr;    // packed weights (K-major, padded) for S_CONV / S_MATMUL
+  const int2* ktab = nullptr;  // gather table (follows wp in the packed allocation)
   int64_t axis = 1;
   double flops_per_img = 0, bytes_per_img = 0, bytes_fixed = 0;
 };
@@ -85,6 +87,7 @@ struct ore_model {
   int input_value = -1;
   int output_value = -1;
   float* consts = nullptr;       // one device allocation for all f32 initializers
+  float* packed = nullptr;       // packed conv / matmul weights (one allocation)
   char* arena = nullptr;
   size_t arena_bytes = 0;
   // timing
@@ -549,13 +552,13 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
     case S_CONV: {
       const Ref x = ref_of(m, s.in0);
       const float* bias = s.in2 >= 0 ? m->values[s.in2].cptr : nullptr;
-      return run_conv(ctx, x.p, n, s.C, s.H, s.W, x.nstride, m->values[s.in1].cptr, s.M, s.kh, s.kw, false, bias,
-                      s.win, s.sh, s.sw, s.relu, y.p, y.nstride);
+      return run_conv(ctx, x.p, n, s.C, s.H, s.W, x.nstride, s.wp, s.ktab, s.M, s.kh, s.kw, bias, s.win, s.sh, s.sw, s.relu,
+                      y.p, y.nstride);
     }
     case S_MATMUL: {
       const Ref x = ref_of(m, s.in0);
-      return run_conv(ctx, x.p, n, s.C, 1, 1, x.nstride, m->values[s.in1].cptr, s.M, 1, 1, true, nullptr, s.win, 1,
-                      1, false, y.p, y.nstride);
+      return run_conv(ctx, x.p, n, s.C, 1, 1, x.nstride, s.wp, s.ktab, s.M, 1, 1, nullptr, s.win, 1, 1, false, y.p,
+                      y.nstride);
     }
     case S_MAXPOOL: {
       const Ref x = ref_of(m, s.in0);
@@ -666,6 +669,30 @@ ore_status ore_model_load(ore_ctx* ctx, const void* bytes, size_t len, int64_t m
     if (st) { std::string e = ctx->err; ore_model_destroy(m); return set_error(ctx, st, "%s", e.c_str()); }
     m->base_steps.push_back(s);
   }
+  // pack every conv / matmul weight once (K-major, zero padded) for the MFMA A tiles
+  {
+    size_t total_packed = 0;
+    for (auto& s : m->base_steps)
+      if (s.kind == S_CONV || s.kind == S_MATMUL)
+        total_packed += (packed_bytes(s.M, s.C * s.kh * s.kw) + 255) / 256 * 256;
+    if (total_packed) {
+      if (hipMalloc(reinterpret_cast<void**>(&m->packed), total_packed) != hipSuccess)
+        return fail(set_error(ctx, ORE_ERR_OOM, "packed weight allocation failed"));
+      size_t poff = 0;
+      for (auto& s : m->base_steps) {
+        if (s.kind != S_CONV && s.kind != S_MATMUL) continue;
+        const int64_t K = s.C * s.kh * s.kw;
+        s.wp = reinterpret_cast<float*>(reinterpret_cast<char*>(m->packed) + poff);
+        launch_pack_weights(m->values[s.in1].cptr, s.w_kmajor, int(s.M), int(K), s.wp, ctx->stream);
+        int2* kt = reinterpret_cast<int2*>(s.wp + size_t(conv_packed_mp(int(s.M))) * size_t(conv_packed_kp(int(K))));
+        launch_ktab(kt, int(K), int(s.kh), int(s.kw), int(s.H), int(s.W), ctx->stream);
+        s.ktab = kt;
+        poff += (packed_bytes(s.M, K) + 255) / 256 * 256;
+      }
+      if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
+        return fail(set_error(ctx, ORE_ERR_HIP, "weight packing failed"));
+    }
+  }
   if (g.outputs.empty()) return fail(set_error(ctx, ORE_ERR_INVALID, "model has no outputs"));
   m->output_value = value_id(m, g.outputs[0].name);
   if (m->output_value < 0 || m->values[m->output_value].is_const)
@@ -683,6 +710,7 @@ ore_status ore_model_destroy(ore_model* m) {
   for (auto e : m->events) (void)hipEventDestroy(e);
   if (m->arena) (void)hipFree(m->arena);
   if (m->consts) (void)hipFree(m->consts);
+  if (m->packed) (void)hipFree(m->packed);
   delete m;
   return ORE_OK;
 }

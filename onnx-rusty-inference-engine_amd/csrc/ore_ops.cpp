@@ -96,12 +96,44 @@ static bool contiguous(const ore_tensor* t) {
 
 static bool fits_i32(int64_t v) { return v >= 0 && v < (int64_t(1) << 31); }
 
+size_t packed_bytes(int64_t M, int64_t K) {
+  const size_t w = size_t(conv_packed_mp(int(M))) * size_t(conv_packed_kp(int(K))) * sizeof(float);
+  return w + size_t(conv_packed_kp(int(K))) * sizeof(int2);
+}
+
+float* pack_to_scratch(ore_ctx* ctx, const float* w, bool kmajor_src, int64_t M, int64_t K, int64_t kh, int64_t kw,
+                       int64_t H, int64_t W, const int2** ktab) {
+  const size_t need = packed_bytes(M, K);
+  if (need > ctx->scratch_bytes) {
+    if (ctx->scratch) {
+      (void)hipStreamSynchronize(ctx->stream);
+      (void)hipFree(ctx->scratch);
+    }
+    ctx->scratch = nullptr;
+    ctx->scratch_bytes = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->scratch), need) != hipSuccess) {
+      set_error(ctx, ORE_ERR_OOM, "weight scratch allocation (%zu bytes) failed", need);
+      return nullptr;
+    }
+    ctx->scratch_bytes = need;
+  }
+  launch_pack_weights(w, kmajor_src, int(M), int(K), ctx->scratch, ctx->stream);
+  int2* kt = reinterpret_cast<int2*>(ctx->scratch + size_t(conv_packed_mp(int(M))) * size_t(conv_packed_kp(int(K))));
+  launch_ktab(kt, int(K), int(kh), int(kw), int(H), int(W), ctx->stream);
+  if (hipGetLastError() != hipSuccess) {
+    set_error(ctx, ORE_ERR_HIP, "weight packing launch failed");
+    return nullptr;
+  }
+  *ktab = kt;
+  return ctx->scratch;
+}
+
 ore_status run_conv(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
-                    const float* w, int64_t M, int64_t kh, int64_t kw, bool w_kmajor, const float* bias,
+                    const float* wp, const int2* ktab, int64_t M, int64_t kh, int64_t kw, const float* bias,
                     const Window& win, int64_t sh, int64_t sw, bool relu, float* y, int64_t y_nstride) {
   if (N == 0) return ORE_OK;
   ConvParams p{};
-  p.x = x; p.w = w; p.bias = bias; p.y = y;
+  p.x = x; p.wp = wp; p.ktab = ktab; p.bias = bias; p.y = y;
   p.N = int(N); p.C = int(C); p.H = int(H); p.W = int(W);
   p.M = int(M); p.kh = int(kh); p.kw = int(kw); p.sh = int(sh); p.sw = int(sw);
   p.pt = int(win.pt); p.pl = int(win.pl);
@@ -112,12 +144,12 @@ ore_status run_conv(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t 
   p.x_nstride = x_nstride;
   p.y_nstride = y_nstride;
   p.relu = relu ? 1 : 0;
-  p.w_kmajor = w_kmajor ? 1 : 0;
+  p.Mp = conv_packed_mp(int(M));
   p.is1x1 = (kh == 1 && kw == 1 && sh == 1 && sw == 1 && win.pt == 0 && win.pl == 0 && win.Ho == H && win.Wo == W);
-  if (!fits_i32(C * H * W) || !fits_i32(M * p.P) || !fits_i32(p.K * M) || !fits_i32(p.Ntot / 1) ||
+  if (!fits_i32(C * H * W) || !fits_i32(M * p.P) || !fits_i32(p.K * M) || !fits_i32(p.Ntot + 256) ||
       (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))
     return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
-  if (w_kmajor && !p.is1x1) return set_error(ctx, ORE_ERR_INVALID, "K-major weights need a 1x1 geometry");
+  if (!p.is1x1 && !ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
   launch_conv(p, ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());
   return ORE_OK;
@@ -171,6 +203,9 @@ ore_status ore_ctx_create(int32_t device, ore_ctx** out) {
 ore_status ore_ctx_destroy(ore_ctx* ctx) {
   if (!ctx) return ORE_OK;
   (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  else (void)hipDeviceSynchronize();
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->own_stream) {
     (void)hipStreamSynchronize(ctx->own_stream);
     (void)hipStreamDestroy(ctx->own_stream);
@@ -272,8 +307,13 @@ ore_status ore_conv2d_f32(ore_ctx* ctx, const ore_tensor* x, const ore_tensor* w
   if (y->dims[0] != x->dims[0] || y->dims[1] != w->dims[0] || y->dims[2] != win.Ho || y->dims[3] != win.Wo)
     return set_error(ctx, ORE_ERR_INVALID, "Conv output dims mismatch: expected [%lld,%lld,%lld,%lld]",
                      (long long)x->dims[0], (long long)w->dims[0], (long long)win.Ho, (long long)win.Wo);
-  return run_conv(ctx, x->data, x->dims[0], x->dims[1], x->dims[2], x->dims[3], nstride_of(x), w->data, w->dims[0],
-                  w->dims[2], w->dims[3], false, bias ? bias->data : nullptr, win, a->strides[0], a->strides[1],
+  if (x->dims[0] == 0) return ORE_OK;
+  const int2* kt = nullptr;
+  float* wp = pack_to_scratch(ctx, w->data, false, w->dims[0], w->dims[1] * w->dims[2] * w->dims[3], w->dims[2],
+                              w->dims[3], x->dims[2], x->dims[3], &kt);
+  if (!wp) return ORE_ERR_OOM;
+  return run_conv(ctx, x->data, x->dims[0], x->dims[1], x->dims[2], x->dims[3], nstride_of(x), wp, kt, w->dims[0],
+                  w->dims[2], w->dims[3], bias ? bias->data : nullptr, win, a->strides[0], a->strides[1],
                   a->fuse_relu != 0, y->data, nstride_of(y));
 }
 
@@ -346,8 +386,12 @@ ore_status ore_matmul_f32(ore_ctx* ctx, const ore_tensor* a, const ore_tensor* b
   // K-major weights b: the MFMA implicit-GEMM kernel, columns = rows of a.
   Window win;
   win.Ho = 1; win.Wo = 1;
-  return run_conv(ctx, a->data, a->dims[0], a->dims[1], 1, 1, a->dims[1], b->data, b->dims[1], 1, 1, true,
-                  nullptr, win, 1, 1, false, y->data, y->dims[1]);
+  if (a->dims[0] == 0) return ORE_OK;
+  const int2* kt = nullptr;
+  float* wp = pack_to_scratch(ctx, b->data, true, b->dims[1], b->dims[0], 1, 1, 1, 1, &kt);
+  if (!wp) return ORE_ERR_OOM;
+  return run_conv(ctx, a->data, a->dims[0], a->dims[1], 1, 1, a->dims[1], wp, kt, b->dims[1], 1, 1, nullptr, win, 1, 1,
+                  false, y->data, y->dims[1]);
 }
 
 ore_status ore_gap_f32(ore_ctx* ctx, const ore_tensor* x, ore_tensor* y) {

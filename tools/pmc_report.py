@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Per-layer PMC table from tools/pmc.sh output (the last SqueezeNet pass of each counter pass).
+usage: python tools/pmc_report.py gpurun_out/pmc_TAG"""
+import csv
+import glob
+import os
+import sys
+from collections import OrderedDict, defaultdict
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "onnx-rusty-inference-engine_amd"))
+PER = 31
+
+
+def layer_names():
+    from ore import onnx_wire, squeezenet
+    m = onnx_wire.decode_model(squeezenet.build(224))
+    return [n.name for n in m.graph.node if n.op_type in ("Conv", "MaxPool", "GlobalAveragePool", "Softmax")]
+
+
+def load(d):
+    f = os.path.join(d, "run_counter_collection.csv")
+    if not os.path.exists(f):
+        return None
+    disp = OrderedDict()
+    for r in csv.DictReader(open(f)):
+        if "ore::" not in r["Kernel_Name"] or "pack_weights" in r["Kernel_Name"]:
+            continue
+        k = int(r["Dispatch_Id"])
+        e = disp.setdefault(k, {"name": r["Kernel_Name"], "dur": int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
+                                "vgpr": r["VGPR_Count"], "agpr": r["Accum_VGPR_Count"], "grid": int(r["Grid_Size"])})
+        e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    rows = list(disp.values())
+    return rows[len(rows) - PER:]
+
+
+def main():
+    base = sys.argv[1]
+    names = layer_names()
+    merged = [defaultdict(float) for _ in range(PER)]
+    for d in sorted(glob.glob(os.path.join(base, "p*"))):
+        if not os.path.isdir(d):
+            continue
+        rows = load(d)
+        if not rows:
+            continue
+        for i, r in enumerate(rows):
+            for k, v in r.items():
+                if k in ("name", "vgpr", "agpr"):
+                    merged[i][k] = v
+                elif k in ("dur", "grid"):
+                    merged[i].setdefault(k, v)
+                else:
+                    merged[i][k] = v
+    hdr = f"{'layer':22s} {'us':>7s} {'waves':>7s} {'valu/w':>7s} {'mfma/w':>7s} {'lds/w':>6s} {'vmr/w':>6s} {'vmw/w':>6s} {'mfma%':>6s} {'wait%':>6s} {'fetchMB':>8s} {'writeMB':>8s} {'l2hit':>6s} {'v/a':>7s}"
+    print(hdr)
+    for i in range(PER):
+        r = merged[i]
+        w = max(r.get("SQ_WAVES", 1), 1)
+        dur = r.get("dur", 1) / 1e3
+        busy = r.get("GRBM_GUI_ACTIVE", 0)
+        mf = r.get("SQ_VALU_MFMA_BUSY_CYCLES", 0)
+        # MFMA busy fraction: busy cycles summed over SIMDs (1024 SIMDs) vs kernel cycles
+        clk = busy / 8 if busy else dur * 1e3 * 2.1
+        mfpct = 100.0 * mf / (1024 * clk) if clk else 0
+        wc = r.get("SQ_WAVE_CYCLES", 0)
+        waitpct = 100.0 * r.get("SQ_WAIT_ANY", 0) / wc if wc else 0
+        hit, miss = r.get("TCC_HIT_sum", 0), r.get("TCC_MISS_sum", 0)
+        print(f"{names[i]:22s} {dur:7.1f} {w:7.0f} {r.get('SQ_INSTS_VALU', 0) / w:7.0f} {r.get('SQ_INSTS_MFMA', 0) / w:7.0f} "
+              f"{r.get('SQ_INSTS_LDS', 0) / w:6.0f} {r.get('SQ_INSTS_VMEM_RD', 0) / w:6.0f} {r.get('SQ_INSTS_VMEM_WR', 0) / w:6.0f} "
+              f"{mfpct:6.1f} {waitpct:6.1f} {2 * r.get('FETCH_SIZE', 0) / 1024:8.1f} {r.get('WRITE_SIZE', 0) / 1024:8.1f} "
+              f"{(100.0 * hit / (hit + miss)) if hit + miss else 0:6.1f} {r.get('vgpr', '')}/{r.get('agpr', '')}")
+
+
+if __name__ == "__main__":
+    main()
