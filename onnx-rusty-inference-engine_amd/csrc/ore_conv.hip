@@ -6,7 +6,7 @@
 //   Weights are packed once into K-major, zero-padded Wp[Kp][Mp] (Kp % 32 == 0, Mp % 128 == 0)
 //   so the A tile is a plain 16-B-vectorised copy with no bounds checks.
 //   B (the im2col of the input) is never materialised: each K tile gathers it straight from
-//   the NCHW input (B1X1: contiguous rows k*HW + pix; BGATHER: a per-layer (cin, r, s) offset
+//   the NCHW input (B1X1: contiguous rows k*x_ps + pix; BGATHER: a per-layer (cin, r, s) offset
 //   table read with scalar loads, plus per-column image/row/col bases).
 //   Block = 256 threads = 4 waves (WM x WN); block tile BM x BN x BK; LDS double-buffered, the
 //   next K tile prefetched into registers while the current one feeds the MFMAs.
@@ -15,6 +15,7 @@
 //   l&31 -> one register = two 128-B runs of consecutive output pixels.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "ore_kernels.h"
 
@@ -59,7 +60,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
   const int m0 = mt * BM;
   const int n0 = nt * BN;
   const int K = p.K;
-  const int HW = p.H * p.W;
+  const int XPS = p.x_ps;  // channel-plane stride of x (>= H*W: planes may be padded)
+  const int YPS = p.y_ps;  // channel-plane stride of y = columns iterated per image (>= Ho*Wo)
 
   for (int i = tid; i < BM; i += 256) sbias[i] = (p.bias && m0 + i < p.M) ? p.bias[m0 + i] : 0.0f;
   const int Kp = (K + 31) & ~31;
@@ -77,8 +79,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
   int ih0 = 0, iw0 = 0;
   {
     const int nn = bn_ok ? bn : 0;
-    const int img = nn / p.P;
-    const int pix = nn - img * p.P;
+    const int img = nn / YPS;
+    const int pix = nn - img * YPS;  // pix >= Ho*Wo: a pad column, computed and never read
     xoff = img * (int)p.x_nstride;
     if (BMODE == B1X1) {
       xoff += pix;
@@ -104,7 +106,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
       const int kk = tid / (BM / 4), mm = (tid % (BM / 4)) * 4;                                      \
       if (AF4 >= 256 || tid < AF4)                                                                   \
         RA0 = *reinterpret_cast<const float4*>(wp + (unsigned)((k0_ + kk) * p.Mp + m0 + mm));       \
-      if (AVEC > 1) {                                                                                \
+      if (AVEC > 1 && (AF4 >= 512 || tid + 256 < AF4)) {                                             \
         const int e1 = tid + 256, kk1 = e1 / (BM / 4), mm1 = (e1 % (BM / 4)) * 4;                    \
         RA1 = *reinterpret_cast<const float4*>(wp + (unsigned)((k0_ + kk1) * p.Mp + m0 + mm1));     \
       }                                                                                              \
@@ -115,7 +117,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
       int off;                                                                                       \
       if (BMODE == B1X1) {                                                                           \
         ok = bn_ok & (k < K);                                                                        \
-        off = xoff + k * HW;                                                                         \
+        off = xoff + k * XPS;                                                                        \
       } else {                                                                                       \
         const int2 e = BMODE == BGATHER_LDS ? ktab_s[k] : ktab[__builtin_amdgcn_readfirstlane(k)];  \
         const int r = e.y >> 16, s = e.y & 0xffff;                                                   \
@@ -131,7 +133,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
     {                                                                                                \
       const int kk = tid / (BM / 4), mm = (tid % (BM / 4)) * 4;                                      \
       if (AF4 >= 256 || tid < AF4) *reinterpret_cast<float4*>(&As[BUF][kk][mm]) = RA0;              \
-      if (AVEC > 1) {                                                                                \
+      if (AVEC > 1 && (AF4 >= 512 || tid + 256 < AF4)) {                                             \
         const int e1 = tid + 256, kk1 = e1 / (BM / 4), mm1 = (e1 % (BM / 4)) * 4;                    \
         *reinterpret_cast<float4*>(&As[BUF][kk1][mm1]) = RA1;                                       \
       }                                                                                              \
@@ -200,8 +202,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
   for (int j = 0; j < FN; ++j) {
     const int n = n0 + wn0 + j * 32 + lcol;
     if (n >= p.Ntot) continue;
-    const int img = n / p.P;
-    const int pix = n - img * p.P;
+    const int img = n / YPS;
+    const int pix = n - img * YPS;
     const unsigned yb = (unsigned)(img * (int)p.y_nstride + pix);
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
         if (m0 + ml < p.M) {
           float v = acc[i][j][e] + sbias[ml];
           if (p.relu) v = fmaxf(v, 0.0f);
-          y[yb + (unsigned)((m0 + ml) * p.P)] = v;
+          y[yb + (unsigned)((m0 + ml) * YPS)] = v;
         }
       }
     }
@@ -219,24 +221,24 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
 }
 
 // ------------------------------------------------------------------ gather table
-// ktab[k] = {c*H*W + r*W + s, (r << 16) | s} for k = (c, r, s) < K; padded entries (k >= K)
+// ktab[k] = {c*x_ps + r*W + s, (r << 16) | s} for k = (c, r, s) < K; padded entries (k >= K)
 // carry r = 1 << 14 so the bounds test of the gather fails and they read as zero.
-__global__ __launch_bounds__(256) void ktab_kernel(int2* __restrict__ ktab, int K, int Kp, int kh, int kw, int H,
+__global__ __launch_bounds__(256) void ktab_kernel(int2* __restrict__ ktab, int K, int Kp, int kh, int kw, int ps,
                                                    int W) {
   for (int k = blockIdx.x * 256 + threadIdx.x; k < Kp; k += gridDim.x * 256) {
     int2 e = make_int2(0, (1 << 14) << 16);
     if (k < K) {
       const int KK = kh * kw;
       const int c = k / KK, rs = k - c * KK, r = rs / kw, s = rs - r * kw;
-      e = make_int2(c * H * W + r * W + s, (r << 16) | s);
+      e = make_int2(c * ps + r * W + s, (r << 16) | s);
     }
     ktab[k] = e;
   }
 }
 
-void launch_ktab(int2* ktab, int K, int kh, int kw, int H, int W, hipStream_t s) {
+void launch_ktab(int2* ktab, int K, int kh, int kw, int x_ps, int W, hipStream_t s) {
   const int Kp = conv_packed_kp(K);
-  hipLaunchKernelGGL(ktab_kernel, dim3((Kp + 255) / 256), dim3(256), 0, s, ktab, K, Kp, kh, kw, H, W);
+  hipLaunchKernelGGL(ktab_kernel, dim3((Kp + 255) / 256), dim3(256), 0, s, ktab, K, Kp, kh, kw, x_ps, W);
 }
 
 // ------------------------------------------------------------------ weight packing
@@ -278,16 +280,34 @@ static void launch_conv_cfg(const ConvParams& p0, hipStream_t s) {
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BGATHER>), grid, block, 0, s, p);
 }
 
+// Block tiles, chosen per layer to minimise the padded output channels (MFMA work on rows
+// >= M is wasted): BM = 128 (2x2 waves of 64x64), 96 (1x4 waves of 96x32), 64 (2x2 of 32x64),
+// 32 (1x4 of 32x64).  Ties go to the larger tile (more reuse of each B element).
 int conv_tile_config(int M) {
-  if (M >= 128) return 2;
-  if (M > 32) return 1;
-  return 0;
+  static const int bms[4] = {128, 96, 64, 32};
+  int best = 0;
+  long long best_rows = 1LL << 60;
+  for (int i = 0; i < 4; ++i) {
+    const long long rows = (long long)((M + bms[i] - 1) / bms[i]) * bms[i];
+    if (rows < best_rows) { best_rows = rows; best = i; }
+  }
+  return best;
 }
 
 void launch_conv(const ConvParams& p, hipStream_t s) {
-  switch (conv_tile_config(p.M)) {
-    case 2: launch_conv_cfg<128, 128, 2, 2, 16>(p, s); break;
-    case 1: launch_conv_cfg<64, 128, 2, 2, 16>(p, s); break;
+  static int forced = -2;
+  if (forced == -2) {
+    const char* e = getenv("ORE_CONV_CFG");  // tuning knob: force a tile config (0..3)
+    forced = e ? atoi(e) : -1;
+  }
+  int cfg = conv_tile_config(p.M);
+  // short-K layers (SqueezeNet's expand1x1, K <= 64) are epilogue/write bound: the 1x4-wave
+  // 96-row tile measured fastest for them even with padded rows (tools/bench_ops.py)
+  if (p.K <= 64 && p.M >= 64 && p.is1x1) cfg = 1;
+  switch (forced >= 0 ? forced : cfg) {
+    case 0: launch_conv_cfg<128, 128, 2, 2, 16>(p, s); break;
+    case 1: launch_conv_cfg<96, 128, 1, 4, 16>(p, s); break;
+    case 2: launch_conv_cfg<64, 128, 2, 2, 16>(p, s); break;
     default: launch_conv_cfg<32, 256, 1, 4, 16>(p, s); break;
   }
 }

@@ -16,7 +16,8 @@ struct ConvParams {
   int Ho, Wo;
   int K;               // C*kh*kw
   int P;               // Ho*Wo
-  long long Ntot;      // N*P
+  int x_ps, y_ps;      // channel-plane strides (>= H*W, >= Ho*Wo); y_ps columns are computed per image
+  long long Ntot;      // N*y_ps
   long long x_nstride;
   long long y_nstride;
   int relu;
@@ -31,6 +32,7 @@ struct PoolParams {
   int N, C, H, W;
   int kh, kw, sh, sw, pt, pl;
   int Ho, Wo;
+  int x_ps, y_ps;      // channel-plane strides
   long long x_nstride, y_nstride;
 };
 
@@ -47,7 +49,7 @@ int conv_packed_mp(int M);  // padded M of the packed weights
 int conv_packed_kp(int K);  // padded K of the packed weights
 // w: ONNX conv weights [M][K] (kmajor_src = false) or MatMul B [K][M] (true) -> wp[Kp][Mp]
 void launch_pack_weights(const float* w, bool kmajor_src, int M, int K, float* wp, hipStream_t s);
-void launch_ktab(int2* ktab, int K, int kh, int kw, int H, int W, hipStream_t s);
+void launch_ktab(int2* ktab, int K, int kh, int kw, int x_ps, int W, hipStream_t s);
 void launch_conv(const ConvParams& p, hipStream_t s);
 void launch_maxpool(const PoolParams& p, hipStream_t s);
 void launch_relu(const float* x, float* y, long long n, hipStream_t s);

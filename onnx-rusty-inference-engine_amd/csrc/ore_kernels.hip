@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "ore_kernels.h"
 
@@ -24,21 +25,27 @@ namespace ore {
 // inside a plane.  The window reads zeros outside the image (the reference pads with 0,
 // max_pool_op.rs:265-276) and starts from -FLT_MAX (:337).  HBM-bound: in + out bytes.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void maxpool_kernel(PoolParams p) {
-  const int plane = blockIdx.x;  // n * C + c
+template <int KH, int KW>  // 0 = runtime window size
+__global__ __launch_bounds__(256) void maxpool_kernel(PoolParams p, int chunks) {
+  // 1-D grid, chunk index fastest: consecutive blocks stream consecutive parts of one plane
+  const int plane = blockIdx.x / chunks;  // n * C + c
+  const int chunk = blockIdx.x - plane * chunks;
   const int n = plane / p.C, c = plane - n * p.C;
-  const float* __restrict__ xp = p.x + (long long)n * p.x_nstride + (long long)c * p.H * p.W;
-  float* __restrict__ yp = p.y + (long long)n * p.y_nstride + (long long)c * p.Ho * p.Wo;
+  const float* __restrict__ xp = p.x + (long long)n * p.x_nstride + (long long)c * p.x_ps;
+  float* __restrict__ yp = p.y + (long long)n * p.y_nstride + (long long)c * p.y_ps;
   const int P = p.Ho * p.Wo;
-  for (int idx = blockIdx.y * 256 + threadIdx.x; idx < P; idx += gridDim.y * 256) {
+  for (int idx = chunk * 256 + threadIdx.x; idx < P; idx += chunks * 256) {
     const int oh = idx / p.Wo, ow = idx - oh * p.Wo;
     const int ih0 = oh * p.sh - p.pt, iw0 = ow * p.sw - p.pl;
     float m = -FLT_MAX;
-    for (int r = 0; r < p.kh; ++r) {
+    const int kh = KH ? KH : p.kh, kw = KW ? KW : p.kw;
+#pragma unroll
+    for (int r = 0; r < kh; ++r) {
       const int ih = ih0 + r;
       const bool rok = (unsigned)ih < (unsigned)p.H;
       const float* row = xp + ih * p.W;
-      for (int s = 0; s < p.kw; ++s) {
+#pragma unroll
+      for (int s = 0; s < kw; ++s) {
         const int iw = iw0 + s;
         const float v = (rok && (unsigned)iw < (unsigned)p.W) ? row[iw] : 0.0f;
         m = fmaxf(m, v);
@@ -48,42 +55,73 @@ __global__ __launch_bounds__(256) void maxpool_kernel(PoolParams p) {
   }
 }
 
-// Specialisation for the 3x3 windows of SqueezeNet/MNIST (fully unrolled).
-__global__ __launch_bounds__(256) void maxpool3x3_kernel(PoolParams p) {
+// LDS-staged MaxPool: one block per (plane, band of output rows).  The band's input rows are
+// one contiguous chunk of the plane, copied to LDS with coalesced loads (each input element
+// leaves HBM once); the windows are then evaluated from LDS.  Zero padding / -FLT_MAX start as
+// above.
+constexpr int POOL_LDS_FLOATS = 8192;  // 32 KiB per block
+
+__global__ __launch_bounds__(256) void maxpool_lds_kernel(PoolParams p, int band_rows) {
+  __shared__ float tile[POOL_LDS_FLOATS];
   const int plane = blockIdx.x;
   const int n = plane / p.C, c = plane - n * p.C;
-  const float* __restrict__ xp = p.x + (long long)n * p.x_nstride + (long long)c * p.H * p.W;
-  float* __restrict__ yp = p.y + (long long)n * p.y_nstride + (long long)c * p.Ho * p.Wo;
-  const int P = p.Ho * p.Wo;
-  for (int idx = blockIdx.y * 256 + threadIdx.x; idx < P; idx += gridDim.y * 256) {
-    const int oh = idx / p.Wo, ow = idx - oh * p.Wo;
+  const float* __restrict__ xp = p.x + (long long)n * p.x_nstride + (long long)c * p.x_ps;
+  float* __restrict__ yp = p.y + (long long)n * p.y_nstride + (long long)c * p.y_ps;
+  const int oh0 = blockIdx.y * band_rows;
+  const int oh1 = min(p.Ho, oh0 + band_rows);
+  const int ih_lo = max(0, oh0 * p.sh - p.pt);
+  const int ih_hi = min(p.H, (oh1 - 1) * p.sh - p.pt + p.kh);
+  const int cnt = (ih_hi - ih_lo) * p.W;
+  const float* __restrict__ src = xp + ih_lo * p.W;
+  for (int i = threadIdx.x; i < cnt; i += 256) tile[i] = src[i];
+  __syncthreads();
+  const int nout = (oh1 - oh0) * p.Wo;
+  for (int idx = threadIdx.x; idx < nout; idx += 256) {
+    const int dr = idx / p.Wo, ow = idx - dr * p.Wo;
+    const int oh = oh0 + dr;
     const int ih0 = oh * p.sh - p.pt, iw0 = ow * p.sw - p.pl;
     float m = -FLT_MAX;
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
+    for (int r = 0; r < p.kh; ++r) {
       const int ih = ih0 + r;
       const bool rok = (unsigned)ih < (unsigned)p.H;
-#pragma unroll
-      for (int s = 0; s < 3; ++s) {
+      const float* row = tile + (ih - ih_lo) * p.W;
+      for (int s = 0; s < p.kw; ++s) {
         const int iw = iw0 + s;
-        const float v = (rok && (unsigned)iw < (unsigned)p.W) ? xp[ih * p.W + iw] : 0.0f;
+        const float v = (rok && (unsigned)iw < (unsigned)p.W) ? row[iw] : 0.0f;
         m = fmaxf(m, v);
       }
     }
-    yp[idx] = m;
+    yp[oh * p.Wo + ow] = m;
   }
+}
+
+static int pool_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ORE_POOL_VARIANT");  // tuning knob: 0 direct (default), 1 LDS-staged
+    v = e ? atoi(e) : 0;
+  }
+  return v;
 }
 
 void launch_maxpool(const PoolParams& p, hipStream_t s) {
   const long long planes = (long long)p.N * p.C;
   const int P = p.Ho * p.Wo;
-  int gy = (P + 255) / 256;
-  if (gy > 64) gy = 64;
   if (planes <= 0 || P <= 0) return;
+  const int rows_fit = POOL_LDS_FLOATS / p.W;
+  if (pool_variant() == 1 && rows_fit >= p.kh) {
+    int band = (rows_fit - p.kh) / p.sh + 1;
+    if (band > p.Ho) band = p.Ho;
+    const int nb = (p.Ho + band - 1) / band;
+    hipLaunchKernelGGL(maxpool_lds_kernel, dim3((unsigned)planes, nb), dim3(256), 0, s, p, band);
+    return;
+  }
+  int chunks = (P + 255) / 256;
+  if (chunks > 64) chunks = 64;
   if (p.kh == 3 && p.kw == 3)
-    hipLaunchKernelGGL(maxpool3x3_kernel, dim3((unsigned)planes, gy), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((maxpool_kernel<3, 3>), dim3((unsigned)(planes * chunks)), dim3(256), 0, s, p, chunks);
   else
-    hipLaunchKernelGGL(maxpool_kernel, dim3((unsigned)planes, gy), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((maxpool_kernel<0, 0>), dim3((unsigned)(planes * chunks)), dim3(256), 0, s, p, chunks);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -40,13 +40,16 @@ struct Value {
   std::vector<int64_t> i64;        // const int64 host data
   bool has_i64 = false;
   int alias_of = -1;               // view into another value's storage
-  int64_t alias_off = 0;           // per-image element offset inside the base
-  int64_t nstride = 0;             // per-image stride of the storage (0 = own size)
+  int64_t alias_ch = 0;            // concat slice: first channel inside the base
+  bool slice = false;              // alias is a channel slice of its base (Concat in place)
+  int64_t ps = 0;                  // 4-D activations: channel-plane stride (>= H*W; padded planes)
   bool elided = false;             // produced and consumed inside one fused kernel
   int64_t arena_off = -1;          // byte offset in the arena (root values)
   int first = -1, last = -1;       // live interval in step indices
   int uses = 0;                    // consumer count (node inputs)
 
+  // elements between images in this value's own storage (roots)
+  int64_t image_stride() const { return (ndim == 4 && ps) ? dims[1] * ps : per_image(); }
   int64_t per_image() const {
     int64_t s = 1;
     for (int i = 1; i < ndim; ++i) s *= dims[i];
@@ -406,7 +409,8 @@ bool strided_writer(const Step& s) { return s.kind == S_CONV || s.kind == S_MAXP
 ore_status plan(ore_model* m) {
   m->steps = m->base_steps;
   for (auto& v : m->values) {
-    v.alias_of = -1; v.alias_off = 0; v.nstride = 0; v.elided = false; v.arena_off = -1; v.first = v.last = -1;
+    v.alias_of = -1; v.alias_ch = 0; v.slice = false; v.ps = 0; v.elided = false; v.arena_off = -1;
+    v.first = v.last = -1;
   }
   count_uses(m, m->steps);
   std::vector<int> producer(m->values.size(), -1);
@@ -449,24 +453,53 @@ ore_status plan(ore_model* m) {
       if (pa < 0 || pb < 0 || !strided_writer(m->steps[pa]) || !strided_writer(m->steps[pb])) continue;
       if (a.uses != 1 || b.uses != 1 || a.is_output || b.is_output || a.alias_of >= 0 || b.alias_of >= 0) continue;
       const Value& y = m->values[s.out];
-      a.alias_of = s.out; a.alias_off = 0; a.nstride = y.per_image();
-      b.alias_of = s.out; b.alias_off = a.per_image(); b.nstride = y.per_image();
+      (void)y;
+      a.alias_of = s.out; a.alias_ch = 0; a.slice = true;
+      b.alias_of = s.out; b.alias_ch = a.dims[1]; b.slice = true;
       s.kind = S_NOP;
     }
   }
   // aliases of aliases must stay contiguous views (Reshape/Dropout of a channel slice)
   for (auto& v : m->values) {
-    if (v.alias_of < 0 || v.nstride != 0) continue;
-    const Value& src = m->values[v.alias_of];
-    if (src.nstride != 0 && src.nstride != src.per_image())
+    if (v.alias_of < 0 || v.slice) continue;
+    if (m->values[v.alias_of].slice)
       return err(m, ORE_ERR_INVALID, "internal: alias of a strided view (" + v.name + ")");
   }
-
-  // live intervals on root storage
   auto root = [&](int id) {
     while (m->values[id].alias_of >= 0) id = m->values[id].alias_of;
     return id;
   };
+
+  // layout: an activation touched only by Conv / MaxPool kernels gets channel planes padded to
+  // a multiple of 32 floats (128-B aligned rows for the conv epilogue and the 1x1 gathers) when
+  // that costs <= 5% extra columns; everything else stays dense NCHW.
+  {
+    std::vector<char> dense(m->values.size(), 0);
+    for (const Step& st : m->steps) {
+      if (st.kind == S_NOP) continue;
+      const bool ok = st.kind == S_CONV || st.kind == S_MAXPOOL;
+      for (int id : {st.in0, st.in2, st.out})
+        if (id >= 0 && !m->values[id].is_const && !ok) dense[root(id)] = 1;
+      if (st.in1 >= 0 && !m->values[st.in1].is_const) dense[root(st.in1)] = 1;
+    }
+    for (size_t id = 0; id < m->values.size(); ++id) {
+      Value& v = m->values[id];
+      if (v.is_const || v.ndim != 4 || v.alias_of >= 0) continue;
+      const int64_t P = v.dims[2] * v.dims[3];
+      const int64_t Pp = (P + 31) / 32 * 32;
+      const bool pad = (m->fusion & ORE_FUSE_CONCAT) && !dense[id] && !v.is_input && !v.is_output && Pp - P <= P / 20;
+      v.ps = pad ? Pp : P;
+    }
+    for (auto& v : m->values)  // views inherit the plane stride of their root
+      if (v.alias_of >= 0 && v.ndim == 4) {
+        const Value& r = m->values[root(int(&v - &m->values[0]))];
+        v.ps = r.ps;
+        if (!v.slice && r.ps != r.dims[2] * r.dims[3])
+          return err(m, ORE_ERR_INVALID, "internal: dense alias of a padded value (" + v.name + ")");
+      }
+  }
+
+  // live intervals on root storage
   const int nsteps = int(m->steps.size());
   for (int i = 0; i < nsteps; ++i) {
     const Step& s = m->steps[i];
@@ -494,13 +527,13 @@ ore_status plan(ore_model* m) {
     roots.push_back(int(id));
   }
   std::sort(roots.begin(), roots.end(), [&](int a, int b) {
-    return m->values[a].per_image() > m->values[b].per_image();
+    return m->values[a].image_stride() > m->values[b].image_stride();
   });
   std::vector<Slot> placed;
   int64_t arena = 0;
   for (int id : roots) {
     Value& v = m->values[id];
-    const int64_t size = ((v.per_image() * m->max_batch * 4) + 255) / 256 * 256;
+    const int64_t size = ((v.image_stride() * m->max_batch * 4) + 255) / 256 * 256;
     // first fit among the gaps left by placed slots whose lifetimes overlap this one
     std::vector<std::pair<int64_t, int64_t>> busy;
     for (auto& s : placed)
@@ -526,23 +559,32 @@ ore_status plan(ore_model* m) {
   m->exec_steps.clear();
   for (int i = 0; i < nsteps; ++i)
     if (m->steps[i].kind != S_NOP) m->exec_steps.push_back(i);
+  // gather tables depend on the input's plane stride
+  for (const Step& st : m->steps) {
+    if (st.kind != S_CONV || !st.ktab) continue;
+    const Value& xv = m->values[st.in0];
+    launch_ktab(const_cast<int2*>(st.ktab), int(st.C * st.kh * st.kw), int(st.kh), int(st.kw), int(xv.ps ? xv.ps : st.H * st.W),
+                int(st.W), m->ctx->stream);
+  }
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
+    return err(m, ORE_ERR_HIP, "gather table build failed");
   return ORE_OK;
 }
 
 // storage of a value for the current run: pointer to image 0 and per-image stride
-struct Ref { float* p; int64_t nstride; };
+struct Ref { float* p; int64_t nstride; int64_t ps; };
 
 Ref ref_of(ore_model* m, int id) {
   const Value& v = m->values[id];
-  if (v.is_const) return {v.cptr, 0};
+  if (v.is_const) return {v.cptr, 0, 0};
   if (v.alias_of >= 0) {
     Ref base = ref_of(m, v.alias_of);
-    const int64_t ns = v.nstride ? v.nstride : base.nstride;
-    return {base.p + v.alias_off, ns};
+    if (v.slice) return {base.p + v.alias_ch * base.ps, base.nstride, base.ps};
+    return base;
   }
-  if (v.is_input) return {const_cast<float*>(m->cur_in), v.per_image()};
-  if (v.is_output && m->out_bound) return {m->cur_out, v.per_image()};
-  return {reinterpret_cast<float*>(m->arena + v.arena_off), v.per_image()};
+  if (v.is_input) return {const_cast<float*>(m->cur_in), v.image_stride(), v.ps};
+  if (v.is_output && m->out_bound) return {m->cur_out, v.image_stride(), v.ps};
+  return {reinterpret_cast<float*>(m->arena + v.arena_off), v.image_stride(), v.ps};
 }
 
 ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
@@ -553,7 +595,7 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       const Ref x = ref_of(m, s.in0);
       const float* bias = s.in2 >= 0 ? m->values[s.in2].cptr : nullptr;
       return run_conv(ctx, x.p, n, s.C, s.H, s.W, x.nstride, s.wp, s.ktab, s.M, s.kh, s.kw, bias, s.win, s.sh, s.sw, s.relu,
-                      y.p, y.nstride);
+                      y.p, y.nstride, x.ps, y.ps);
     }
     case S_MATMUL: {
       const Ref x = ref_of(m, s.in0);
@@ -562,7 +604,8 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
     }
     case S_MAXPOOL: {
       const Ref x = ref_of(m, s.in0);
-      return run_maxpool(ctx, x.p, n, s.C, s.H, s.W, x.nstride, s.kh, s.kw, s.win, s.sh, s.sw, y.p, y.nstride);
+      return run_maxpool(ctx, x.p, n, s.C, s.H, s.W, x.nstride, s.kh, s.kw, s.win, s.sh, s.sw, y.p, y.nstride, x.ps,
+                         y.ps);
     }
     default: break;
   }
@@ -684,9 +727,7 @@ ore_status ore_model_load(ore_ctx* ctx, const void* bytes, size_t len, int64_t m
         const int64_t K = s.C * s.kh * s.kw;
         s.wp = reinterpret_cast<float*>(reinterpret_cast<char*>(m->packed) + poff);
         launch_pack_weights(m->values[s.in1].cptr, s.w_kmajor, int(s.M), int(K), s.wp, ctx->stream);
-        int2* kt = reinterpret_cast<int2*>(s.wp + size_t(conv_packed_mp(int(s.M))) * size_t(conv_packed_kp(int(K))));
-        launch_ktab(kt, int(K), int(s.kh), int(s.kw), int(s.H), int(s.W), ctx->stream);
-        s.ktab = kt;
+        s.ktab = reinterpret_cast<int2*>(s.wp + size_t(conv_packed_mp(int(s.M))) * size_t(conv_packed_kp(int(K))));
         poff += (packed_bytes(s.M, K) + 255) / 256 * 256;
       }
       if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
@@ -785,12 +826,25 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
   const int64_t pe = v.is_const ? v.numel_const() : v.per_image();
   if (!host_dst) return ORE_OK;
   if (size_t(n * pe) > cap) return set_error(ctx, ORE_ERR_INVALID, "destination too small");
-  if (!v.is_const && v.first < 0 && !v.is_input) return set_error(ctx, ORE_ERR_INVALID, "value '%s' not materialised", name);
+  {
+    int rid = id;
+    while (m->values[rid].alias_of >= 0) rid = m->values[rid].alias_of;
+    const Value& rv = m->values[rid];
+    if (!rv.is_const && rv.first < 0 && !rv.is_input)
+      return set_error(ctx, ORE_ERR_INVALID, "value '%s' not materialised", name);
+  }
   ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
   ORE_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
   const Ref r = ref_of(m, id);
   if (!r.p) return set_error(ctx, ORE_ERR_INVALID, "value '%s' has no f32 storage", name);
   const int64_t ns = v.is_const ? pe : r.nstride;
+  if (!v.is_const && v.ndim == 4 && r.ps && r.ps != v.dims[2] * v.dims[3]) {  // padded planes
+    const int64_t P = v.dims[2] * v.dims[3];
+    for (int64_t i = 0; i < n; ++i)
+      ORE_HIP_CHECK(ctx, hipMemcpy2D(host_dst + i * pe, size_t(P) * 4, r.p + i * ns, size_t(r.ps) * 4, size_t(P) * 4,
+                                     size_t(v.dims[1]), hipMemcpyDeviceToHost));
+    return ORE_OK;
+  }
   ORE_HIP_CHECK(ctx, hipMemcpy2D(host_dst, size_t(pe) * 4, r.p, size_t(ns) * 4, size_t(pe) * 4, size_t(n),
                                  hipMemcpyDeviceToHost));
   return ORE_OK;

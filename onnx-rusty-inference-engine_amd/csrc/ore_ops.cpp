@@ -119,7 +119,7 @@ float* pack_to_scratch(ore_ctx* ctx, const float* w, bool kmajor_src, int64_t M,
   }
   launch_pack_weights(w, kmajor_src, int(M), int(K), ctx->scratch, ctx->stream);
   int2* kt = reinterpret_cast<int2*>(ctx->scratch + size_t(conv_packed_mp(int(M))) * size_t(conv_packed_kp(int(K))));
-  launch_ktab(kt, int(K), int(kh), int(kw), int(H), int(W), ctx->stream);
+  launch_ktab(kt, int(K), int(kh), int(kw), int(H * W), int(W), ctx->stream);
   if (hipGetLastError() != hipSuccess) {
     set_error(ctx, ORE_ERR_HIP, "weight packing launch failed");
     return nullptr;
@@ -130,8 +130,11 @@ float* pack_to_scratch(ore_ctx* ctx, const float* w, bool kmajor_src, int64_t M,
 
 ore_status run_conv(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
                     const float* wp, const int2* ktab, int64_t M, int64_t kh, int64_t kw, const float* bias,
-                    const Window& win, int64_t sh, int64_t sw, bool relu, float* y, int64_t y_nstride) {
+                    const Window& win, int64_t sh, int64_t sw, bool relu, float* y, int64_t y_nstride,
+                    int64_t x_ps, int64_t y_ps) {
   if (N == 0) return ORE_OK;
+  if (x_ps == 0) x_ps = H * W;
+  if (y_ps == 0) y_ps = win.Ho * win.Wo;
   ConvParams p{};
   p.x = x; p.wp = wp; p.ktab = ktab; p.bias = bias; p.y = y;
   p.N = int(N); p.C = int(C); p.H = int(H); p.W = int(W);
@@ -140,13 +143,17 @@ ore_status run_conv(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t 
   p.Ho = int(win.Ho); p.Wo = int(win.Wo);
   p.K = int(C * kh * kw);
   p.P = int(win.Ho * win.Wo);
-  p.Ntot = N * win.Ho * win.Wo;
+  p.x_ps = int(x_ps);
+  p.y_ps = int(y_ps);
+  p.Ntot = N * y_ps;
   p.x_nstride = x_nstride;
   p.y_nstride = y_nstride;
   p.relu = relu ? 1 : 0;
   p.Mp = conv_packed_mp(int(M));
-  p.is1x1 = (kh == 1 && kw == 1 && sh == 1 && sw == 1 && win.pt == 0 && win.pl == 0 && win.Ho == H && win.Wo == W);
-  if (!fits_i32(C * H * W) || !fits_i32(M * p.P) || !fits_i32(p.K * M) || !fits_i32(p.Ntot + 256) ||
+  p.is1x1 = (kh == 1 && kw == 1 && sh == 1 && sw == 1 && win.pt == 0 && win.pl == 0 && win.Ho == H && win.Wo == W &&
+             x_ps == y_ps);
+  if (x_ps < H * W || y_ps < win.Ho * win.Wo) return set_error(ctx, ORE_ERR_INVALID, "plane stride below plane size");
+  if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(p.K * M) || !fits_i32(p.Ntot + 256) ||
       (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))
     return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
   if (!p.is1x1 && !ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
@@ -157,9 +164,11 @@ ore_status run_conv(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t 
 
 ore_status run_maxpool(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
                        int64_t x_nstride, int64_t kh, int64_t kw, const Window& win, int64_t sh, int64_t sw,
-                       float* y, int64_t y_nstride) {
+                       float* y, int64_t y_nstride, int64_t x_ps, int64_t y_ps) {
   if (N == 0) return ORE_OK;
   PoolParams p{};
+  p.x_ps = int(x_ps ? x_ps : H * W);
+  p.y_ps = int(y_ps ? y_ps : win.Ho * win.Wo);
   p.x = x; p.y = y;
   p.N = int(N); p.C = int(C); p.H = int(H); p.W = int(W);
   p.kh = int(kh); p.kw = int(kw); p.sh = int(sh); p.sw = int(sw);

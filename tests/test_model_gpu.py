@@ -138,6 +138,34 @@ def test_squeezenet_node_level_parity(gpu_ctx):
     m.close()
 
 
+@pytest.mark.parametrize("hw", [64, 224])
+def test_fused_padded_layout_values(gpu_ctx, hw):
+    """Fused graph (conv->relu epilogue, concat in place, 128-B padded channel planes): every
+    value it materialises equals the unfused dense run's value bit for bit."""
+    import ore
+    from ore import onnx_wire, squeezenet
+    mb = squeezenet.build(hw)
+    model = onnx_wire.decode_model(mb)
+    xt = _t(squeezenet.synthetic_input(3, hw, seed=31))
+    ref = ore.Model(gpu_ctx, mb, max_batch=3)
+    ref.set_fusion(ore.KEEP_VALUES)
+    _np(ref.run(xt))
+    fused = ore.Model(gpu_ctx, mb, max_batch=3)
+    fused.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+    _np(fused.run(xt))
+    checked = 0
+    for node in model.graph.node:
+        try:
+            y = fused.read_value(node.output[0])
+        except ore.OreError:
+            continue  # fused away (conv output feeding its relu)
+        np.testing.assert_array_equal(y, ref.read_value(node.output[0]), err_msg=node.output[0])
+        checked += 1
+    assert checked >= 39
+    ref.close()
+    fused.close()
+
+
 def test_squeezenet_batch256_properties(squeeze224):
     """Full benchmark size: size-independent properties (no oracle run at B=256)."""
     import torch

@@ -52,7 +52,7 @@ def main():
                     merged[i].setdefault(k, v)
                 else:
                     merged[i][k] = v
-    hdr = f"{'layer':22s} {'us':>7s} {'waves':>7s} {'valu/w':>7s} {'mfma/w':>7s} {'lds/w':>6s} {'vmr/w':>6s} {'vmw/w':>6s} {'mfma%':>6s} {'wait%':>6s} {'fetchMB':>8s} {'writeMB':>8s} {'l2hit':>6s} {'v/a':>7s}"
+    hdr = f"{'layer':22s} {'us':>7s} {'waves':>7s} {'valu/w':>7s} {'mfma/w':>7s} {'lds/w':>6s} {'vmr/w':>6s} {'vmw/w':>6s} {'mfma%':>6s} {'wait%':>6s} {'fetchMB':>8s} {'writeMB':>8s} {'GHz':>5s} {'v/a':>7s}"
     print(hdr)
     for i in range(PER):
         r = merged[i]
@@ -69,7 +69,7 @@ def main():
         print(f"{names[i]:22s} {dur:7.1f} {w:7.0f} {r.get('SQ_INSTS_VALU', 0) / w:7.0f} {r.get('SQ_INSTS_MFMA', 0) / w:7.0f} "
               f"{r.get('SQ_INSTS_LDS', 0) / w:6.0f} {r.get('SQ_INSTS_VMEM_RD', 0) / w:6.0f} {r.get('SQ_INSTS_VMEM_WR', 0) / w:6.0f} "
               f"{mfpct:6.1f} {waitpct:6.1f} {2 * r.get('FETCH_SIZE', 0) / 1024:8.1f} {r.get('WRITE_SIZE', 0) / 1024:8.1f} "
-              f"{(100.0 * hit / (hit + miss)) if hit + miss else 0:6.1f} {r.get('vgpr', '')}/{r.get('agpr', '')}")
+              f"{(busy / 8 / (dur * 1e3)) if busy else 0:5.2f} {r.get('vgpr', '')}/{r.get('agpr', '')}")
 
 
 if __name__ == "__main__":
