@@ -22,6 +22,7 @@
 namespace ore {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));  // first-class vector (no struct copies)
 
 enum { B1X1 = 0, BGATHER = 1, BGATHER_LDS = 2 };  // BGATHER_LDS: whole gather table in LDS
 
@@ -266,6 +267,282 @@ void launch_pack_weights(const float* w, bool kmajor_src, int M, int K, float* w
                      kmajor_src ? 1 : 0);
 }
 
+// ------------------------------------------------------------------ window-staged implicit GEMM
+// For k > 1 / strided convs on planes large enough to tile per image (conv1, the 54^2 and 27^2
+// 3x3 layers).  A block owns BM output channels x BN consecutive output pixels of ONE image.
+// K is walked in stages of `bch` input channels (ks = bch*kh*kw rounded up to even):
+//   * A stage: rows [stage*ks, stage*ks + ks) of the stage-major packed weights -> LDS.
+//   * B stage: the input rows those BN pixels touch (wr rows x ww columns per channel, zero
+//     outside the image) are copied ONCE into an LDS window by row-coalesced loads.
+// B fragments are then read straight from the window: lane address = per-column base
+// ((oh - oh_first)*sh*ww + ow*sw) + koff[k] (c*wr*ww + r*ww + s, an LDS table), so there is no
+// per-element bounds arithmetic and no im2col tile.  Stage s+1 is prefetched into registers
+// while stage s feeds the MFMAs.
+constexpr int WIN_MAXA = 6;   // float4 A loads per thread per stage
+constexpr int WIN_MAXW = 12;  // window loads per lane per stage
+constexpr int WIN_MAXROWS = 64;
+
+template <int BM, int BN, int WM, int WN, int WQ>  // WQ = ceil(ww / 64): loads per lane per window row
+__global__ __launch_bounds__(256, 2) void conv_win_kernel(ConvParams p) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 32, FN = TN / 32;
+  constexpr int RSLOTS = WIN_MAXW / WQ;  // window rows per wave per stage
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int KS = p.ks, BCH = p.bch, WR = p.wr, WWD = p.ww;
+  const int AFL = KS * BM;          // floats of one A stage
+  const int WFL = BCH * WR * WWD;   // floats of one window stage
+  float* As = smem;                 // [2][KS][BM]
+  float* Ws = smem + 2 * AFL;       // [2][BCH][WR][WW]
+  int* koff = reinterpret_cast<int*>(Ws + 2 * WFL);   // [KS + 8] window offset of each k (0 past KS)
+  int2* rowtab = reinterpret_cast<int2*>(koff + KS + 8);  // [WIN_MAXROWS] {input offset, channel}
+  float* sbias = reinterpret_cast<float*>(rowtab + WIN_MAXROWS);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm0 = (wave / WN) * TM, wn0 = (wave % WN) * TN;
+  const int lrow = lane >> 5, lcol = lane & 31;
+
+  const int nwg = p.mtiles * p.ntiles;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, rr8 = nwg & 7;
+  const int wgid = (xcd < rr8 ? xcd * (q + 1) : rr8 * (q + 1) + (xcd - rr8) * q) + (bid >> 3);
+  const int mt = wgid % p.mtiles, nt = wgid / p.mtiles;
+  const int m0 = mt * BM;
+  const int img = nt / p.tiles_per_img;
+  const int p0 = (nt - img * p.tiles_per_img) * BN;
+  const int oh_first = p0 / p.Wo;
+  const int ihb = oh_first * p.sh - p.pt;  // input row of window row 0
+
+  const int KK = p.kh * p.kw;
+  for (int i = tid; i < KS + 8; i += 256) {
+    int off = 0;
+    if (i < BCH * KK) {
+      const int c = i / KK, rs = i - c * KK, r = rs / p.kw, sx = rs - r * p.kw;
+      off = (c * WR + r) * WWD + sx;
+    }
+    koff[i] = off;
+  }
+  const int wrows = BCH * WR;
+  for (int i = tid; i < WIN_MAXROWS; i += 256) {
+    // window row i = (channel c, row r): input offset relative to channel c0 of the stage;
+    // offset -1 marks rows outside the image (zero filled); c decides stage-tail rows
+    int off = -1, c = 1 << 20;
+    if (i < wrows) {
+      c = i / WR;
+      const int ih = ihb + (i - c * WR);
+      if ((unsigned)ih < (unsigned)p.H) off = c * p.x_ps + ih * p.W;
+    }
+    rowtab[i] = make_int2(off, c);
+  }
+  for (int i = tid; i < BM; i += 256) sbias[i] = (p.bias && m0 + i < p.M) ? p.bias[m0 + i] : 0.0f;
+
+  int bbase[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    int pc = p0 + wn0 + j * 32 + lcol;
+    if (pc > p.P - 1) pc = p.P - 1;  // pad columns read any valid window address
+    const int oh = pc / p.Wo, ow = pc - oh * p.Wo;
+    bbase[j] = (oh - oh_first) * p.sh * WWD + ow * p.sw;
+  }
+
+  const float* __restrict__ x = p.x;
+  const float* __restrict__ wp = p.wp;
+  const int ximg = img * (int)p.x_nstride;
+  __syncthreads();  // koff / rowtab / sbias
+  // this wave's window rows (row = wave + 4 r) for the whole block: wave-uniform, kept in SGPRs
+  int wroff[RSLOTS], wrch[RSLOTS];
+#pragma unroll
+  for (int r = 0; r < RSLOTS; ++r) {
+    const int row = wave + 4 * r;
+    const int2 rt = rowtab[row < WIN_MAXROWS ? row : 0];
+    wroff[r] = __builtin_amdgcn_readfirstlane(rt.x);
+    wrch[r] = __builtin_amdgcn_readfirstlane(rt.y);
+  }
+
+#define ORE_WIN_LOAD(RA, RW, ROK, ST)                                                                \
+  {                                                                                                  \
+    const int st_ = (ST);                                                                            \
+    const float* ws_ = wp + (unsigned)(st_ * KS * p.Mp + m0);                                        \
+    _Pragma("unroll") for (int j = 0; j < WIN_MAXA; ++j) {                                           \
+      const int e = (tid + j * 256 < AFL / 4) ? tid + j * 256 : 0; /* tail lanes reload element 0 */ \
+      const int kk = e / (BM / 4), mm = (e - kk * (BM / 4)) * 4;                                     \
+      RA[j] = *reinterpret_cast<const floatx4*>(ws_ + (unsigned)(kk * p.Mp + mm));                   \
+    }                                                                                                \
+    const int cbase_ = ximg + st_ * BCH * p.x_ps;                                                    \
+    const int cleft_ = p.C - st_ * BCH;  /* channels left in this stage */                           \
+    _Pragma("unroll") for (int r = 0; r < RSLOTS; ++r) {                                             \
+      const int row = wave + 4 * r;                                                                  \
+      if (row < wrows) { /* wave-uniform */                                                          \
+        const int roff = wroff[r];                                                                   \
+        const bool rok_ = (roff >= 0) & (wrch[r] < cleft_);                                          \
+        _Pragma("unroll") for (int qq = 0; qq < WQ; ++qq) {                                          \
+          const int col = lane + 64 * qq, iw = col - p.pl;                                           \
+          const bool ok = rok_ & (col < WWD) & ((unsigned)iw < (unsigned)p.W);                       \
+          RW[r * WQ + qq] = x[(unsigned)(ok ? cbase_ + roff + iw : 0)];                              \
+          ROK[r * WQ + qq] = ok;                                                                     \
+        }                                                                                            \
+      }                                                                                              \
+    }                                                                                                \
+  }
+#define ORE_WIN_STORE(RA, RW, ROK, BUF)                                                              \
+  {                                                                                                  \
+    float* a_ = As + (BUF) * AFL;                                                                    \
+    _Pragma("unroll") for (int j = 0; j < WIN_MAXA; ++j) {                                           \
+      const int e = tid + j * 256;                                                                   \
+      if (e < AFL / 4) *reinterpret_cast<floatx4*>(a_ + e * 4) = RA[j];                              \
+    }                                                                                                \
+    float* w_ = Ws + (BUF) * WFL;                                                                    \
+    _Pragma("unroll") for (int r = 0; r < RSLOTS; ++r) {                                             \
+      const int row = wave + 4 * r;                                                                  \
+      _Pragma("unroll") for (int qq = 0; qq < WQ; ++qq) {                                            \
+        const int col = lane + 64 * qq;                                                              \
+        if (row < wrows && col < WWD) w_[row * WWD + col] = ROK[r * WQ + qq] ? RW[r * WQ + qq] : 0.0f; \
+      }                                                                                              \
+    }                                                                                                \
+  }
+
+  floatx16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  {
+    floatx4 ra[WIN_MAXA];
+    float rw[WIN_MAXW];
+    bool rok[WIN_MAXW];
+    ORE_WIN_LOAD(ra, rw, rok, 0);
+    ORE_WIN_STORE(ra, rw, rok, 0);
+  }
+  __syncthreads();
+  const int nst = p.nst;
+  // Inner loop: 4 k values (two MFMA k-steps) per trip, software-pipelined: the fragments of
+  // trip t+1 are read from LDS while trip t's MFMAs run, and the koff entries two trips ahead
+  // (KS % 4 == 0; koff is padded with 8 zero entries so the look-ahead never leaves the table).
+#ifdef ORE_EXP_REGONLY  /* timing experiment: fragments without LDS reads */
+#define ORE_WIN_FRAGS(AF0, AF1, BF0, BF1, KQ, KK)                                                    \
+  {                                                                                                  \
+    _Pragma("unroll") for (int i = 0; i < FM; ++i) { AF0[i] = (float)(KK) + i; AF1[i] = (float)(KK) - i; } \
+    _Pragma("unroll") for (int j = 0; j < FN; ++j) { BF0[j] = (float)(KQ).x + j; BF1[j] = (float)(KQ).y - j; } \
+  }
+#else
+#define ORE_WIN_FRAGS(AF0, AF1, BF0, BF1, KQ, KK)                                                    \
+  {                                                                                                  \
+    const int lo0_ = lrow ? (KQ).y : (KQ).x, lo1_ = lrow ? (KQ).w : (KQ).z;                           \
+    _Pragma("unroll") for (int i = 0; i < FM; ++i) {                                                 \
+      AF0[i] = a_[((KK) + lrow) * BM + wm0 + i * 32 + lcol];                                         \
+      AF1[i] = a_[((KK) + 2 + lrow) * BM + wm0 + i * 32 + lcol];                                     \
+    }                                                                                                \
+    _Pragma("unroll") for (int j = 0; j < FN; ++j) {                                                 \
+      BF0[j] = w_[bbase[j] + lo0_];                                                                  \
+      BF1[j] = w_[bbase[j] + lo1_];                                                                  \
+    }                                                                                                \
+  }
+#endif
+#define ORE_WIN_MFMAS(AF0, AF1, BF0, BF1)                                                            \
+  {                                                                                                  \
+    _Pragma("unroll") for (int i = 0; i < FM; ++i)                                                   \
+    _Pragma("unroll") for (int j = 0; j < FN; ++j)                                                   \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(AF0[i], BF0[j], acc[i][j], 0, 0, 0);          \
+    _Pragma("unroll") for (int i = 0; i < FM; ++i)                                                   \
+    _Pragma("unroll") for (int j = 0; j < FN; ++j)                                                   \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(AF1[i], BF1[j], acc[i][j], 0, 0, 0);          \
+  }
+  // two trips per iteration with ping-pong fragment registers (no copies); an odd trip count
+  // leaves one trip for the tail.  Fragment reads past the last trip are clamped dummies.
+#define ORE_WIN_COMPUTE(BUF)                                                                         \
+  {                                                                                                  \
+    const float* a_ = As + (BUF) * AFL;                                                              \
+    const float* w_ = Ws + (BUF) * WFL;                                                              \
+    const int4* kq_ = reinterpret_cast<const int4*>(koff);                                           \
+    const int trips_ = KS >> 2, last_ = KS - 4;                                                      \
+    float ca0[FM], ca1[FM], cb0[FN], cb1[FN], na0[FM], na1[FM], nb0[FN], nb1[FN];                    \
+    int4 kq1 = kq_[1];                                                                               \
+    {                                                                                                \
+      const int4 kq0 = kq_[0];                                                                       \
+      ORE_WIN_FRAGS(ca0, ca1, cb0, cb1, kq0, 0);                                                     \
+    }                                                                                                \
+    int t_ = 0;                                                                                      \
+    for (; t_ + 2 <= trips_; t_ += 2) {                                                              \
+      const int4 kq2 = kq_[t_ + 2];                                                                  \
+      ORE_WIN_FRAGS(na0, na1, nb0, nb1, kq1, 4 * t_ + 4);                                            \
+      __builtin_amdgcn_sched_barrier(0);                                                             \
+      ORE_WIN_MFMAS(ca0, ca1, cb0, cb1);                                                             \
+      __builtin_amdgcn_sched_barrier(0);                                                             \
+      kq1 = kq_[t_ + 3];                                                                             \
+      ORE_WIN_FRAGS(ca0, ca1, cb0, cb1, kq2, (4 * t_ + 8 <= last_ ? 4 * t_ + 8 : last_));            \
+      __builtin_amdgcn_sched_barrier(0);                                                             \
+      ORE_WIN_MFMAS(na0, na1, nb0, nb1);                                                             \
+      __builtin_amdgcn_sched_barrier(0);                                                             \
+    }                                                                                                \
+    if (t_ < trips_) ORE_WIN_MFMAS(ca0, ca1, cb0, cb1);                                              \
+  }
+  for (int st = 0; st < nst - 1; ++st) {
+    const int buf = st & 1;
+#ifndef ORE_EXP_NOLOAD  // timing experiments only (tools/build_exp.sh)
+    floatx4 ra[WIN_MAXA];
+    float rw[WIN_MAXW];
+    bool rok[WIN_MAXW];
+    ORE_WIN_LOAD(ra, rw, rok, st + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    ORE_WIN_COMPUTE(buf);
+    ORE_WIN_STORE(ra, rw, rok, buf ^ 1);
+#else
+    ORE_WIN_COMPUTE(0);
+#endif
+#ifndef ORE_EXP_NOSYNC
+    __syncthreads();
+#endif
+  }
+  ORE_WIN_COMPUTE((nst - 1) & 1);
+#undef ORE_WIN_LOAD
+#undef ORE_WIN_STORE
+#undef ORE_WIN_COMPUTE
+#undef ORE_WIN_FRAGS
+#undef ORE_WIN_MFMAS
+
+  // epilogue: columns are pixels p0 + n of image img (plane stride y_ps; pixels >= P skipped)
+  float* __restrict__ y = p.y;
+  const unsigned yimg = (unsigned)(img * (int)p.y_nstride);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int pix = p0 + wn0 + j * 32 + lcol;
+    if (pix >= p.P) continue;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int ml = wm0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lrow;
+        if (m0 + ml < p.M) {
+          float v = acc[i][j][e] + sbias[ml];
+          if (p.relu) v = fmaxf(v, 0.0f);
+#ifdef ORE_EXP_NOEPI
+          if (v == 1234.5678f)
+#endif
+          y[yimg + (unsigned)((m0 + ml) * p.y_ps + pix)] = v;
+        }
+      }
+    }
+  }
+}
+
+// window-staged packing: row stage*ks + (c - c0)*kh*kw + r*kw + s, zero for padded rows
+__global__ __launch_bounds__(256) void pack_win_kernel(const float* __restrict__ w, float* __restrict__ wp, int M,
+                                                       int C, int KK, int Mp, int bch, int ks, int nst) {
+  const long long total = (long long)nst * ks * Mp;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int row = (int)(i / Mp), m = (int)(i - (long long)row * Mp);
+    const int st = row / ks, kk = row - st * ks;
+    float v = 0.0f;
+    if (kk < bch * KK && m < M) {
+      const int c = st * bch + kk / KK, rs = kk - (kk / KK) * KK;
+      if (c < C) v = w[((long long)m * C + c) * KK + rs];
+    }
+    wp[i] = v;
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int BK>
 static void launch_conv_cfg(const ConvParams& p0, hipStream_t s) {
   ConvParams p = p0;
@@ -294,17 +571,114 @@ int conv_tile_config(int M) {
   return best;
 }
 
-void launch_conv(const ConvParams& p, hipStream_t s) {
-  static int forced = -2;
-  if (forced == -2) {
-    const char* e = getenv("ORE_CONV_CFG");  // tuning knob: force a tile config (0..3)
-    forced = e ? atoi(e) : -1;
-  }
-  int cfg = conv_tile_config(p.M);
-  // short-K layers (SqueezeNet's expand1x1, K <= 64) are epilogue/write bound: the 1x4-wave
+static const int CFG_BM[4] = {128, 96, 64, 32};
+static const int CFG_BN[4] = {128, 128, 128, 256};
+
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
+                   bool is1x1) {
+  (void)H; (void)W; (void)pt;
+  ConvPlan pln{};
+  pln.cfg = conv_tile_config(M);
+  const int K = C * kh * kw;
+  // short-K 1x1 layers (SqueezeNet's expand1x1, K <= 64) are epilogue/write bound: the 1x4-wave
   // 96-row tile measured fastest for them even with padded rows (tools/bench_ops.py)
-  if (p.K <= 64 && p.M >= 64 && p.is1x1) cfg = 1;
-  switch (forced >= 0 ? forced : cfg) {
+  if (K <= 64 && M >= 64 && is1x1) pln.cfg = 1;
+  const int forced = env_int("ORE_CONV_CFG", -1);  // tuning knob
+  if (forced >= 0 && forced < 4) pln.cfg = forced;
+  pln.Mp = conv_packed_mp(M);
+  pln.krows = conv_packed_kp(K);
+  pln.window = 0;
+  const int P = Ho * Wo;
+  // The window-staged kernel is opt-in (ORE_CONV_WINDOW=1): on the SqueezeNet layers it measured
+  // 5-45 % slower than the gather kernel (its 49-59 KB LDS stages allow 2-3 blocks per CU against
+  // the gather kernel's 4; profiles/r01f_window_vs_gather.txt).
+  if (is1x1 || env_int("ORE_CONV_WINDOW", 0) == 0 || P < 512) return pln;
+  const int BM = CFG_BM[pln.cfg], BN = CFG_BN[pln.cfg];
+  const int tiles = (P + BN - 1) / BN;
+  if ((long long)tiles * BN > (long long)P * 11 / 10) return pln;  // > 10% pad columns
+  int span = 1;
+  for (int t = 0; t < tiles; ++t) {
+    const int p0 = t * BN, p1 = (p0 + BN - 1 < P - 1) ? p0 + BN - 1 : P - 1;
+    const int sp = p1 / Wo - p0 / Wo + 1;
+    if (sp > span) span = sp;
+  }
+  const int wr = (span - 1) * sh + kh;
+  const int ww = (Wo - 1) * sw + kw;
+  const int wq = (ww + 63) / 64;
+  if (wq > 4) return pln;
+  const int KK = kh * kw;
+  const size_t lds_max = (size_t)env_int("ORE_WIN_LDS_KB", 64) * 1024;  // tuning knob
+  int best = 0;
+  for (int bch = C; bch >= 1; --bch) {
+    const int ks = (bch * KK + 3) & ~3;
+    const size_t lds = ((size_t)2 * ks * BM + (size_t)2 * bch * wr * ww) * 4 + (size_t)(ks + 8) * 4 +
+                       (size_t)WIN_MAXROWS * 8 + (size_t)BM * 4;
+    const int rows = bch * wr;
+    if (lds > lds_max || rows > WIN_MAXROWS || ((rows + 3) / 4) * wq > WIN_MAXW || ks * BM / 4 > WIN_MAXA * 256)
+      continue;
+    if (!best) best = bch;
+    if (C % bch == 0 && 2 * bch >= best) { best = bch; break; }
+  }
+  if (!best) return pln;
+  pln.window = 1;
+  pln.bch = best;
+  pln.ks = (best * KK + 3) & ~3;
+  pln.nst = (C + best - 1) / best;
+  pln.wr = wr;
+  pln.ww = ww;
+  pln.wq = wq;
+  pln.krows = pln.nst * pln.ks;
+  pln.lds = ((size_t)2 * pln.ks * BM + (size_t)2 * best * wr * ww) * 4 + (size_t)(pln.ks + 8) * 4 +
+            (size_t)WIN_MAXROWS * 8 + (size_t)BM * 4;
+  return pln;
+}
+
+size_t conv_packed_bytes(const ConvPlan& pln) { return (size_t)pln.krows * pln.Mp * sizeof(float); }
+
+void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, const ConvPlan& pln, float* wp,
+                 hipStream_t s) {
+  if (!pln.window) {
+    launch_pack_weights(w, kmajor_src, M, C * kh * kw, wp, s);
+    return;
+  }
+  const long long total = (long long)pln.krows * pln.Mp;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pack_win_kernel, dim3((unsigned)blocks), dim3(256), 0, s, w, wp, M, C, kh * kw, pln.Mp, pln.bch,
+                     pln.ks, pln.nst);
+}
+
+template <int BM, int BN, int WM, int WN>
+static void launch_win_cfg(const ConvParams& p0, const ConvPlan& pln, hipStream_t s) {
+  ConvParams p = p0;
+  p.bch = pln.bch; p.ks = pln.ks; p.nst = pln.nst; p.wr = pln.wr; p.ww = pln.ww;
+  p.tiles_per_img = (p.P + BN - 1) / BN;
+  p.mtiles = (p.M + BM - 1) / BM;
+  p.ntiles = p.N * p.tiles_per_img;
+  dim3 grid(p.mtiles * p.ntiles), block(256);
+  switch (pln.wq) {
+    case 1: hipLaunchKernelGGL((conv_win_kernel<BM, BN, WM, WN, 1>), grid, block, pln.lds, s, p); break;
+    case 2: hipLaunchKernelGGL((conv_win_kernel<BM, BN, WM, WN, 2>), grid, block, pln.lds, s, p); break;
+    default: hipLaunchKernelGGL((conv_win_kernel<BM, BN, WM, WN, 4>), grid, block, pln.lds, s, p); break;
+  }
+}
+
+void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
+  if (pln.window) {
+    switch (pln.cfg) {
+      case 0: launch_win_cfg<128, 128, 2, 2>(p, pln, s); break;
+      case 1: launch_win_cfg<96, 128, 1, 4>(p, pln, s); break;
+      case 2: launch_win_cfg<64, 128, 2, 2>(p, pln, s); break;
+      default: launch_win_cfg<32, 256, 1, 4>(p, pln, s); break;
+    }
+    return;
+  }
+  switch (pln.cfg) {
     case 0: launch_conv_cfg<128, 128, 2, 2, 16>(p, s); break;
     case 1: launch_conv_cfg<96, 128, 1, 4, 16>(p, s); break;
     case 2: launch_conv_cfg<64, 128, 2, 2, 16>(p, s); break;

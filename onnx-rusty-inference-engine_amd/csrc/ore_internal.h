@@ -81,18 +81,21 @@ ore_status resolve_window(ore_ctx* ctx, int auto_pad, const int64_t* pads, int n
                           int64_t kh, int64_t kw, int64_t sh, int64_t sw, Window* out);
 
 // ---------------------------------------------------------------- launches over resolved geometry
-// wp: weights packed by launch_pack_weights (row stride conv_packed_mp(M))
-// ktab: gather table (launch_ktab) for non-1x1 geometry
-ore_status run_conv(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
-                    const float* wp, const int2* ktab, int64_t M, int64_t kh, int64_t kw, const float* bias,
-                    const Window& win, int64_t sh, int64_t sw, bool relu, float* y, int64_t y_nstride,
-                    int64_t x_ps = 0, int64_t y_ps = 0);  // plane strides, 0 = dense (H*W, Ho*Wo)
+// Kernel plan of a conv (or MatMul as a 1x1 conv) over resolved geometry.
+ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
+                   const Window& win);
+// wp: weights packed by launch_pack for plan `pln`
+// ktab: gather table (launch_ktab) for non-1x1 geometry on the gather kernel
+ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
+                    int64_t x_nstride, const float* wp, const int2* ktab, int64_t M, int64_t kh, int64_t kw,
+                    const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, float* y,
+                    int64_t y_nstride, int64_t x_ps = 0, int64_t y_ps = 0);  // plane strides, 0 = dense
 // packs w (and the gather table for an input of H x W) into the context scratch buffer;
 // returns the packed weights (or null with the error set), *ktab receives the table
-float* pack_to_scratch(ore_ctx* ctx, const float* w, bool kmajor_src, int64_t M, int64_t K, int64_t kh, int64_t kw,
-                       int64_t H, int64_t W, const int2** ktab);
+float* pack_to_scratch(ore_ctx* ctx, const ConvPlan& pln, const float* w, bool kmajor_src, int64_t M, int64_t C,
+                       int64_t kh, int64_t kw, int64_t H, int64_t W, const int2** ktab);
 // bytes of packed weights + gather table for one conv
-size_t packed_bytes(int64_t M, int64_t K);
+size_t packed_bytes(const ConvPlan& pln);
 ore_status run_maxpool(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
                        int64_t x_nstride, int64_t kh, int64_t kw, const Window& win, int64_t sh, int64_t sw,
                        float* y, int64_t y_nstride, int64_t x_ps = 0, int64_t y_ps = 0);

@@ -24,6 +24,18 @@ struct ConvParams {
   int is1x1;           // kh = kw = 1, stride 1, no padding, Ho*Wo == H*W
   int Mp;              // row stride of wp (conv_packed_mp(M))
   int mtiles, ntiles;  // filled by the launcher
+  // window-staged kernel (filled by the launcher from the ConvPlan)
+  int bch, ks, nst, wr, ww, tiles_per_img;
+};
+
+// Per-layer kernel choice and weight layout (see plan_conv in ore_conv.hip).
+struct ConvPlan {
+  int window;          // 1: conv_win_kernel (stage-major packed weights), 0: conv_gemm_kernel
+  int cfg;             // block tile (0: 128x128, 1: 96x128, 2: 64x128, 3: 32x256)
+  int bch, ks, nst;    // window: channels / K rows per stage, stages
+  int wr, ww, wq;      // window rows, columns, loads per lane per row
+  int Mp, krows;       // packed weights are krows x Mp floats
+  size_t lds;          // dynamic LDS bytes of the window kernel
 };
 
 struct PoolParams {
@@ -50,7 +62,13 @@ int conv_packed_kp(int K);  // padded K of the packed weights
 // w: ONNX conv weights [M][K] (kmajor_src = false) or MatMul B [K][M] (true) -> wp[Kp][Mp]
 void launch_pack_weights(const float* w, bool kmajor_src, int M, int K, float* wp, hipStream_t s);
 void launch_ktab(int2* ktab, int K, int kh, int kw, int x_ps, int W, hipStream_t s);
-void launch_conv(const ConvParams& p, hipStream_t s);
+ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
+                   bool is1x1);
+size_t conv_packed_bytes(const ConvPlan& pln);
+// packs ONNX weights [M][C][kh][kw] (or MatMul [K][M]) in the layout the plan's kernel reads
+void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, const ConvPlan& pln, float* wp,
+                 hipStream_t s);
+void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s);
 void launch_maxpool(const PoolParams& p, hipStream_t s);
 void launch_relu(const float* x, float* y, long long n, hipStream_t s);
 void launch_add_bcast(const AddParams& p, hipStream_t s);

@@ -71,8 +71,9 @@ struct Step {
   Window win;
   bool relu = false;
   bool w_kmajor = false;  // MatMul: the constant operand is [K][M]
-  float* wp = nullptr;    // packed weights (K-major, padded) for S_CONV / S_MATMUL
-  const int2* ktab = nullptr;  // gather table (follows wp in the packed allocation)
+  ConvPlan plan{};        // kernel choice and weight layout for S_CONV / S_MATMUL
+  float* wp = nullptr;    // packed weights (layout per plan) for S_CONV / S_MATMUL
+  const int2* ktab = nullptr;  // gather table (follows wp in the packed allocation; gather kernel only)
   int64_t axis = 1;
   double flops_per_img = 0, bytes_per_img = 0, bytes_fixed = 0;
 };
@@ -594,12 +595,12 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
     case S_CONV: {
       const Ref x = ref_of(m, s.in0);
       const float* bias = s.in2 >= 0 ? m->values[s.in2].cptr : nullptr;
-      return run_conv(ctx, x.p, n, s.C, s.H, s.W, x.nstride, s.wp, s.ktab, s.M, s.kh, s.kw, bias, s.win, s.sh, s.sw, s.relu,
+      return run_conv(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, s.wp, s.ktab, s.M, s.kh, s.kw, bias, s.win, s.sh, s.sw, s.relu,
                       y.p, y.nstride, x.ps, y.ps);
     }
     case S_MATMUL: {
       const Ref x = ref_of(m, s.in0);
-      return run_conv(ctx, x.p, n, s.C, 1, 1, x.nstride, s.wp, s.ktab, s.M, 1, 1, nullptr, s.win, 1, 1, false, y.p,
+      return run_conv(ctx, s.plan, x.p, n, s.C, 1, 1, x.nstride, s.wp, s.ktab, s.M, 1, 1, nullptr, s.win, 1, 1, false, y.p,
                       y.nstride);
     }
     case S_MAXPOOL: {
@@ -715,20 +716,27 @@ ore_status ore_model_load(ore_ctx* ctx, const void* bytes, size_t len, int64_t m
   // pack every conv / matmul weight once (K-major, zero padded) for the MFMA A tiles
   {
     size_t total_packed = 0;
-    for (auto& s : m->base_steps)
-      if (s.kind == S_CONV || s.kind == S_MATMUL)
-        total_packed += (packed_bytes(s.M, s.C * s.kh * s.kw) + 255) / 256 * 256;
+    for (auto& s : m->base_steps) {
+      if (s.kind == S_CONV)
+        s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win);
+      else if (s.kind == S_MATMUL)
+        s.plan = conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win);
+      else
+        continue;
+      total_packed += (packed_bytes(s.plan) + 255) / 256 * 256;
+    }
     if (total_packed) {
       if (hipMalloc(reinterpret_cast<void**>(&m->packed), total_packed) != hipSuccess)
         return fail(set_error(ctx, ORE_ERR_OOM, "packed weight allocation failed"));
       size_t poff = 0;
       for (auto& s : m->base_steps) {
         if (s.kind != S_CONV && s.kind != S_MATMUL) continue;
-        const int64_t K = s.C * s.kh * s.kw;
-        s.wp = reinterpret_cast<float*>(reinterpret_cast<char*>(m->packed) + poff);
-        launch_pack_weights(m->values[s.in1].cptr, s.w_kmajor, int(s.M), int(K), s.wp, ctx->stream);
-        s.ktab = reinterpret_cast<int2*>(s.wp + size_t(conv_packed_mp(int(s.M))) * size_t(conv_packed_kp(int(K))));
-        poff += (packed_bytes(s.M, K) + 255) / 256 * 256;
+        char* base = reinterpret_cast<char*>(m->packed) + poff;
+        s.wp = reinterpret_cast<float*>(base);
+        launch_pack(m->values[s.in1].cptr, s.w_kmajor, int(s.M), int(s.C), int(s.kh), int(s.kw), s.plan, s.wp,
+                    ctx->stream);
+        s.ktab = s.plan.window ? nullptr : reinterpret_cast<int2*>(base + conv_packed_bytes(s.plan));
+        poff += (packed_bytes(s.plan) + 255) / 256 * 256;
       }
       if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
         return fail(set_error(ctx, ORE_ERR_HIP, "weight packing failed"));

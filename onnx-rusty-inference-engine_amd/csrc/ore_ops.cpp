@@ -96,14 +96,19 @@ static bool contiguous(const ore_tensor* t) {
 
 static bool fits_i32(int64_t v) { return v >= 0 && v < (int64_t(1) << 31); }
 
-size_t packed_bytes(int64_t M, int64_t K) {
-  const size_t w = size_t(conv_packed_mp(int(M))) * size_t(conv_packed_kp(int(K))) * sizeof(float);
-  return w + size_t(conv_packed_kp(int(K))) * sizeof(int2);
+ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
+                   const Window& win) {
+  return plan_conv(int(M), int(C), int(H), int(W), int(kh), int(kw), int(sh), int(sw), int(win.pt), int(win.pl),
+                   int(win.Ho), int(win.Wo), kh == 1 && kw == 1);
 }
 
-float* pack_to_scratch(ore_ctx* ctx, const float* w, bool kmajor_src, int64_t M, int64_t K, int64_t kh, int64_t kw,
-                       int64_t H, int64_t W, const int2** ktab) {
-  const size_t need = packed_bytes(M, K);
+size_t packed_bytes(const ConvPlan& pln) {
+  return conv_packed_bytes(pln) + size_t(pln.window ? 0 : pln.krows) * sizeof(int2);
+}
+
+float* pack_to_scratch(ore_ctx* ctx, const ConvPlan& pln, const float* w, bool kmajor_src, int64_t M, int64_t C,
+                       int64_t kh, int64_t kw, int64_t H, int64_t W, const int2** ktab) {
+  const size_t need = packed_bytes(pln);
   if (need > ctx->scratch_bytes) {
     if (ctx->scratch) {
       (void)hipStreamSynchronize(ctx->stream);
@@ -117,9 +122,12 @@ float* pack_to_scratch(ore_ctx* ctx, const float* w, bool kmajor_src, int64_t M,
     }
     ctx->scratch_bytes = need;
   }
-  launch_pack_weights(w, kmajor_src, int(M), int(K), ctx->scratch, ctx->stream);
-  int2* kt = reinterpret_cast<int2*>(ctx->scratch + size_t(conv_packed_mp(int(M))) * size_t(conv_packed_kp(int(K))));
-  launch_ktab(kt, int(K), int(kh), int(kw), int(H * W), int(W), ctx->stream);
+  launch_pack(w, kmajor_src, int(M), int(C), int(kh), int(kw), pln, ctx->scratch, ctx->stream);
+  int2* kt = nullptr;
+  if (!pln.window) {
+    kt = reinterpret_cast<int2*>(reinterpret_cast<char*>(ctx->scratch) + conv_packed_bytes(pln));
+    launch_ktab(kt, int(C * kh * kw), int(kh), int(kw), int(H * W), int(W), ctx->stream);
+  }
   if (hipGetLastError() != hipSuccess) {
     set_error(ctx, ORE_ERR_HIP, "weight packing launch failed");
     return nullptr;
@@ -128,10 +136,10 @@ float* pack_to_scratch(ore_ctx* ctx, const float* w, bool kmajor_src, int64_t M,
   return ctx->scratch;
 }
 
-ore_status run_conv(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
-                    const float* wp, const int2* ktab, int64_t M, int64_t kh, int64_t kw, const float* bias,
-                    const Window& win, int64_t sh, int64_t sw, bool relu, float* y, int64_t y_nstride,
-                    int64_t x_ps, int64_t y_ps) {
+ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
+                    int64_t x_nstride, const float* wp, const int2* ktab, int64_t M, int64_t kh, int64_t kw,
+                    const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, float* y,
+                    int64_t y_nstride, int64_t x_ps, int64_t y_ps) {
   if (N == 0) return ORE_OK;
   if (x_ps == 0) x_ps = H * W;
   if (y_ps == 0) y_ps = win.Ho * win.Wo;
@@ -149,15 +157,15 @@ ore_status run_conv(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t 
   p.x_nstride = x_nstride;
   p.y_nstride = y_nstride;
   p.relu = relu ? 1 : 0;
-  p.Mp = conv_packed_mp(int(M));
+  p.Mp = pln.Mp;
   p.is1x1 = (kh == 1 && kw == 1 && sh == 1 && sw == 1 && win.pt == 0 && win.pl == 0 && win.Ho == H && win.Wo == W &&
              x_ps == y_ps);
   if (x_ps < H * W || y_ps < win.Ho * win.Wo) return set_error(ctx, ORE_ERR_INVALID, "plane stride below plane size");
-  if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(p.K * M) || !fits_i32(p.Ntot + 256) ||
-      (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))
+  if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(int64_t(pln.krows) * pln.Mp) ||
+      !fits_i32(p.Ntot + 256) || (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))
     return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
-  if (!p.is1x1 && !ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
-  launch_conv(p, ctx->stream);
+  if (!pln.window && !p.is1x1 && !ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
+  launch_conv(p, pln, ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());
   return ORE_OK;
 }
@@ -318,10 +326,12 @@ ore_status ore_conv2d_f32(ore_ctx* ctx, const ore_tensor* x, const ore_tensor* w
                      (long long)x->dims[0], (long long)w->dims[0], (long long)win.Ho, (long long)win.Wo);
   if (x->dims[0] == 0) return ORE_OK;
   const int2* kt = nullptr;
-  float* wp = pack_to_scratch(ctx, w->data, false, w->dims[0], w->dims[1] * w->dims[2] * w->dims[3], w->dims[2],
-                              w->dims[3], x->dims[2], x->dims[3], &kt);
+  const ConvPlan pln = conv_plan(w->dims[0], w->dims[1], x->dims[2], x->dims[3], w->dims[2], w->dims[3], a->strides[0],
+                                 a->strides[1], win);
+  float* wp = pack_to_scratch(ctx, pln, w->data, false, w->dims[0], w->dims[1], w->dims[2], w->dims[3], x->dims[2],
+                              x->dims[3], &kt);
   if (!wp) return ORE_ERR_OOM;
-  return run_conv(ctx, x->data, x->dims[0], x->dims[1], x->dims[2], x->dims[3], nstride_of(x), wp, kt, w->dims[0],
+  return run_conv(ctx, pln, x->data, x->dims[0], x->dims[1], x->dims[2], x->dims[3], nstride_of(x), wp, kt, w->dims[0],
                   w->dims[2], w->dims[3], bias ? bias->data : nullptr, win, a->strides[0], a->strides[1],
                   a->fuse_relu != 0, y->data, nstride_of(y));
 }
@@ -397,9 +407,10 @@ ore_status ore_matmul_f32(ore_ctx* ctx, const ore_tensor* a, const ore_tensor* b
   win.Ho = 1; win.Wo = 1;
   if (a->dims[0] == 0) return ORE_OK;
   const int2* kt = nullptr;
-  float* wp = pack_to_scratch(ctx, b->data, true, b->dims[1], b->dims[0], 1, 1, 1, 1, &kt);
+  const ConvPlan pln = conv_plan(b->dims[1], b->dims[0], 1, 1, 1, 1, 1, 1, win);
+  float* wp = pack_to_scratch(ctx, pln, b->data, true, b->dims[1], b->dims[0], 1, 1, 1, 1, &kt);
   if (!wp) return ORE_ERR_OOM;
-  return run_conv(ctx, a->data, a->dims[0], a->dims[1], 1, 1, a->dims[1], wp, kt, b->dims[1], 1, 1, nullptr, win, 1, 1,
+  return run_conv(ctx, pln, a->data, a->dims[0], a->dims[1], 1, 1, a->dims[1], wp, kt, b->dims[1], 1, 1, nullptr, win, 1, 1,
                   false, y->data, y->dims[1]);
 }
 

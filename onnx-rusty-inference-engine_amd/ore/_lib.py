@@ -9,7 +9,8 @@ import ctypes
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libore.so")
+# ORE_LIB selects another build of the same library (tools/build_exp.sh timing variants)
+LIB_PATH = os.environ.get("ORE_LIB") or os.path.join(PKG_ROOT, "lib", "libore.so")
 
 ORE_OK = 0
 STATUS_NAMES = {0: "ORE_OK", 1: "ORE_ERR_INVALID", 2: "ORE_ERR_UNSUPPORTED", 3: "ORE_ERR_HIP",

@@ -53,13 +53,26 @@ CONV_CASES = [
     (2, 3, 11, 9, 33, 2, 3, "NOTSET", [2, 0, 1, 3], [3, 1], True),  # uneven explicit pads
     (5, 17, 7, 7, 130, 3, 3, "NOTSET", [1, 1, 1, 1], [1, 1], False),
     (2, 33, 6, 10, 48, 1, 1, "NOTSET", [1, 0, 0, 1], [1, 2], True),  # 1x1 with pads/stride -> generic path
+    # planes >= 512 pixels: window-staged kernel (plan_conv in ore_conv.hip)
+    (2, 16, 54, 54, 64, 3, 3, "NOTSET", [1, 1, 1, 1], [1, 1], True),     # fire2 expand3x3
+    (2, 32, 54, 54, 128, 3, 3, "NOTSET", [1, 1, 1, 1], [1, 1], False),   # fire4 expand3x3
+    (2, 48, 27, 27, 192, 3, 3, "NOTSET", [1, 1, 1, 1], [1, 1], True),    # fire6 expand3x3
+    (1, 64, 27, 27, 256, 3, 3, "NOTSET", [1, 1, 1, 1], [1, 1], True),    # fire8 expand3x3
+    (1, 3, 224, 224, 96, 7, 7, "VALID", None, [2, 2], True),             # conv1, 4 loads per window row
+    (2, 3, 64, 64, 96, 7, 7, "VALID", None, [2, 2], True),
+    (2, 13, 40, 37, 20, 3, 3, "SAME_UPPER", None, [1, 1], True),         # 32x256 tile, ragged channel stage
+    (2, 7, 30, 150, 33, 5, 3, "NOTSET", [2, 1, 0, 3], [1, 2], False),    # 3 loads per row, uneven pads
+    (3, 5, 33, 31, 40, 2, 4, "SAME_LOWER", None, [1, 1], True),
 ]
 
 
+@pytest.mark.parametrize("window", ["0", "1"])
 @pytest.mark.parametrize("case", CONV_CASES)
 @pytest.mark.parametrize("fuse_relu", [False, True])
-def test_conv2d(gpu_ctx, case, fuse_relu):
+def test_conv2d(gpu_ctx, case, fuse_relu, window, monkeypatch):
+    """window=1 routes planes >= 512 pixels to the (opt-in) window-staged kernel."""
     import ore
+    monkeypatch.setenv("ORE_CONV_WINDOW", window)
     N, C, H, W, M, kh, kw, auto_pad, pads, strides, with_bias = case
     rng = np.random.default_rng(zlib.crc32(repr(case).encode()))
     x = rng.standard_normal((N, C, H, W)).astype(np.float32)
@@ -90,6 +103,21 @@ def test_conv_integer_exact(gpu_ctx):
     b = rng.integers(-5, 6, size=(70,)).astype(np.float32)
     ref = oracle.conv2d(x, w, b, auto_pad="SAME_UPPER", strides=(1, 1))
     got = _np(ore.convolution(gpu_ctx, _t(x), _t(w), _t(b), auto_pad="SAME_UPPER", strides=(1, 1)))
+    np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("window", ["1", "0"])
+def test_conv_integer_exact_window(gpu_ctx, window, monkeypatch):
+    """Window-eligible geometry on both conv kernels (ORE_CONV_WINDOW=0 forces the gather
+    kernel): small-integer data, so both equal the oracle bit for bit."""
+    import ore
+    monkeypatch.setenv("ORE_CONV_WINDOW", window)
+    rng = np.random.default_rng(11)
+    x = rng.integers(-4, 5, size=(2, 19, 30, 29)).astype(np.float32)
+    w = rng.integers(-3, 4, size=(100, 19, 3, 3)).astype(np.float32)
+    b = rng.integers(-5, 6, size=(100,)).astype(np.float32)
+    ref = oracle.conv2d(x, w, b, pads=[1, 1, 1, 1], strides=(1, 1))
+    got = _np(ore.convolution(gpu_ctx, _t(x), _t(w), _t(b), pads=[1, 1, 1, 1], strides=(1, 1)))
     np.testing.assert_array_equal(got, ref)
 
 

@@ -24,7 +24,7 @@ def load(d):
         return None
     disp = OrderedDict()
     for r in csv.DictReader(open(f)):
-        if "ore::" not in r["Kernel_Name"] or "pack_weights" in r["Kernel_Name"]:
+        if "ore::" not in r["Kernel_Name"] or "pack_" in r["Kernel_Name"] or "ktab" in r["Kernel_Name"]:
             continue
         k = int(r["Dispatch_Id"])
         e = disp.setdefault(k, {"name": r["Kernel_Name"], "dur": int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
