@@ -94,7 +94,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
   }
   const float* __restrict__ x = p.x;
   const float* __restrict__ wp = p.wp;
-  const int2* __restrict__ ktab = p.ktab;
+  // the gather table through the constant address space: k is wave-uniform, so the entries
+  // come in by scalar loads (s_load) into SGPRs instead of LDS / vector round trips
+  typedef const __attribute__((address_space(4))) long long* ktab_cptr;  // int2 {x, y} as one 64-bit word
+  const ktab_cptr ktab = (ktab_cptr)p.ktab;
 
   static_assert(AVEC <= 2, "A tile prefetch holds at most two float4 per thread");
 
@@ -120,7 +123,14 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
         ok = bn_ok & (k < K);                                                                        \
         off = xoff + k * XPS;                                                                        \
       } else {                                                                                       \
-        const int2 e = BMODE == BGATHER_LDS ? ktab_s[k] : ktab[__builtin_amdgcn_readfirstlane(k)];  \
+        int2 e;                                                                                      \
+        if (BMODE == BGATHER_LDS) {                                                                  \
+          e = ktab_s[k];                                                                             \
+        } else {                                                                                     \
+          const long long w_ = ktab[k];                                                              \
+          e.x = (int)w_;                                                                             \
+          e.y = (int)(w_ >> 32);                                                                     \
+        }                                                                                            \
         const int r = e.y >> 16, s = e.y & 0xffff;                                                   \
         ok = bn_ok & ((unsigned)(ih0 + r) < (unsigned)p.H) & ((unsigned)(iw0 + s) < (unsigned)p.W);  \
         off = xoff + e.x;                                                                            \
@@ -183,6 +193,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
   // steady state: prefetch tile t+1 into registers, MFMAs on tile t, publish t+1 to LDS
   for (int t = 0; t < ntk - 1; ++t) {
     const int buf = t & 1;
+#ifndef ORE_EXP_NOLOAD  // timing experiments only (tools/build_exp.sh)
     float4 ra0, ra1;
     float rb[BLOADS];
     bool rok[BLOADS];
@@ -190,7 +201,12 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
     __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
     ORE_COMPUTE_TILE(buf);
     ORE_STORE_TILE(ra0, ra1, rb, rok, buf ^ 1);
+#else
+    ORE_COMPUTE_TILE(0);
+#endif
+#ifndef ORE_EXP_NOSYNC
     __syncthreads();
+#endif
   }
   ORE_COMPUTE_TILE((ntk - 1) & 1);
 #undef ORE_COMPUTE_TILE
@@ -214,6 +230,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
         if (m0 + ml < p.M) {
           float v = acc[i][j][e] + sbias[ml];
           if (p.relu) v = fmaxf(v, 0.0f);
+#ifdef ORE_EXP_NOEPI
+          if (v == 1234.5678f)
+#endif
           y[yb + (unsigned)((m0 + ml) * YPS)] = v;
         }
       }
@@ -543,6 +562,11 @@ __global__ __launch_bounds__(256) void pack_win_kernel(const float* __restrict__
   }
 }
 
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
 template <int BM, int BN, int WM, int WN, int BK>
 static void launch_conv_cfg(const ConvParams& p0, hipStream_t s) {
   ConvParams p = p0;
@@ -551,7 +575,7 @@ static void launch_conv_cfg(const ConvParams& p0, hipStream_t s) {
   dim3 grid(p.mtiles * p.ntiles), block(256);
   if (p.is1x1)
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, B1X1>), grid, block, 0, s, p);
-  else if (conv_packed_kp(p.K) <= KTAB_LDS)
+  else if (conv_packed_kp(p.K) <= KTAB_LDS && env_int("ORE_KTAB_LDS", 0))
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BGATHER_LDS>), grid, block, 0, s, p);
   else
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BGATHER>), grid, block, 0, s, p);
@@ -574,10 +598,6 @@ int conv_tile_config(int M) {
 static const int CFG_BM[4] = {128, 96, 64, 32};
 static const int CFG_BN[4] = {128, 128, 128, 256};
 
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
 
 ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
                    bool is1x1) {

@@ -95,25 +95,169 @@ __global__ __launch_bounds__(256) void maxpool_lds_kernel(PoolParams p, int band
   }
 }
 
-static int pool_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ORE_POOL_VARIANT");  // tuning knob: 0 direct (default), 1 LDS-staged
-    v = e ? atoi(e) : 0;
+// Column-strip MaxPool: one thread per (plane, output column, band of RB output rows).  The
+// thread walks down its band; each input row is reduced across the KW window columns once
+// and the row maxima shared by consecutive windows (KH > SH) stay in registers, so an output
+// row costs SH*KW loads instead of KH*KW.  Lanes are consecutive output columns (then the next
+// plane's), so loads are stride-SW and stores are coalesced.  Zero padding / -FLT_MAX start as
+// above; max is exact, so the regrouping is bit-identical.
+template <int KH, int KW, int SH, int RB>
+__global__ __launch_bounds__(256) void maxpool_strip_kernel(PoolParams p, long long cols) {
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= cols) return;
+  const long long plane = t / p.Wo;
+  const int ow = (int)(t - plane * p.Wo);
+  const int n = (int)(plane / p.C), c = (int)(plane - (long long)n * p.C);
+  const float* __restrict__ xp = p.x + (long long)n * p.x_nstride + (long long)c * p.x_ps;
+  float* __restrict__ yp = p.y + (long long)n * p.y_nstride + (long long)c * p.y_ps;
+  const int oh0 = blockIdx.y * RB;
+  const int oh1 = min(p.Ho, oh0 + RB);
+  const int iw0 = ow * p.sw - p.pl;
+  bool cok[KW];
+#pragma unroll
+  for (int s = 0; s < KW; ++s) cok[s] = (unsigned)(iw0 + s) < (unsigned)p.W;
+  constexpr int KEEP = KH > SH ? KH - SH : 0;
+  float keep[KEEP > 0 ? KEEP : 1];
+#define ORE_ROWMAX(DST, IH)                                                       \
+  {                                                                               \
+    const int ih_ = (IH);                                                         \
+    const bool rok_ = (unsigned)ih_ < (unsigned)p.H;                              \
+    const float* row_ = xp + (rok_ ? ih_ : 0) * p.W;                              \
+    float m_ = -FLT_MAX;                                                          \
+    _Pragma("unroll") for (int s = 0; s < KW; ++s) {                              \
+      const float v_ = (rok_ && cok[s]) ? row_[iw0 + s] : 0.0f;                   \
+      m_ = fmaxf(m_, v_);                                                         \
+    }                                                                             \
+    DST = m_;                                                                     \
   }
-  return v;
+  int ih = oh0 * SH - p.pt;
+#pragma unroll
+  for (int r = 0; r < KEEP; ++r) ORE_ROWMAX(keep[r], ih + r);
+#pragma unroll 2
+  for (int oh = oh0; oh < oh1; ++oh) {
+    float m = -FLT_MAX;
+#pragma unroll
+    for (int r = 0; r < KEEP; ++r) m = fmaxf(m, keep[r]);
+    float fresh[KH - KEEP];
+#pragma unroll
+    for (int r = 0; r < KH - KEEP; ++r) {
+      ORE_ROWMAX(fresh[r], ih + KEEP + r);
+      m = fmaxf(m, fresh[r]);
+    }
+    yp[oh * p.Wo + ow] = m;
+    // rows ih+SH .. ih+KH-1 open the next window
+#pragma unroll
+    for (int r = 0; r < KEEP; ++r) keep[r] = (r + SH < KEEP) ? keep[r + SH] : fresh[r + SH - KEEP];
+    ih += SH;
+  }
+#undef ORE_ROWMAX
 }
+
+// Plane-staged MaxPool: one block per group of PB consecutive (n, c) planes.  The planes are
+// copied to LDS with coalesced loads (every input element leaves HBM once, 8 loads in flight per
+// thread), then every output window is evaluated from LDS and stored coalesced.
+template <int KH, int KW>
+__global__ __launch_bounds__(256) void maxpool_planes_kernel(PoolParams p, int pb, long long planes) {
+  extern __shared__ float tile[];  // [pb][H*W]
+  const int HW = p.H * p.W;
+  const long long q0 = (long long)blockIdx.x * pb;
+  const int nq = (int)min((long long)pb, planes - q0);
+  const int tid = threadIdx.x;
+  for (int q = 0; q < nq; ++q) {
+    const long long pl = q0 + q;
+    const int n = (int)(pl / p.C), c = (int)(pl - (long long)n * p.C);
+    const float* __restrict__ xq = p.x + (long long)n * p.x_nstride + (long long)c * p.x_ps;
+    float* tq = tile + q * HW;
+    int i = tid;
+    for (; i + 7 * 256 < HW; i += 8 * 256) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = xq[i + u * 256];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) tq[i + u * 256] = v[u];
+    }
+    for (; i < HW; i += 256) tq[i] = xq[i];
+  }
+  __syncthreads();
+  const int P = p.Ho * p.Wo;
+  const int kh = KH ? KH : p.kh, kw = KW ? KW : p.kw;
+  for (int q = 0; q < nq; ++q) {
+    const long long pl = q0 + q;
+    const int n = (int)(pl / p.C), c = (int)(pl - (long long)n * p.C);
+    float* __restrict__ yq = p.y + (long long)n * p.y_nstride + (long long)c * p.y_ps;
+    const float* tq = tile + q * HW;
+    for (int o = tid; o < P; o += 256) {
+      const int oh = o / p.Wo, ow = o - oh * p.Wo;
+      const int ih0 = oh * p.sh - p.pt, iw0 = ow * p.sw - p.pl;
+      float m = -FLT_MAX;
+#pragma unroll
+      for (int r = 0; r < kh; ++r) {
+        const int ih = ih0 + r;
+        const bool rok = (unsigned)ih < (unsigned)p.H;
+#pragma unroll
+        for (int s2 = 0; s2 < kw; ++s2) {
+          const int iw = iw0 + s2;
+          const float v = (rok && (unsigned)iw < (unsigned)p.W) ? tq[ih * p.W + iw] : 0.0f;
+          m = fmaxf(m, v);
+        }
+      }
+      yq[o] = m;
+    }
+  }
+}
+
+// tuning knobs, read per launch so tests can switch them: ORE_POOL_VARIANT 0 auto, 1 band
+// LDS-staged, 2 direct, 3 column strip, 4 plane-staged; ORE_POOL_LDS_KB (planes per block of
+// variant 4 = budget / plane bytes); ORE_POOL_RB (output rows per thread of variant 3)
+static int env_knob(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+static int pool_variant() { return env_knob("ORE_POOL_VARIANT", 0); }
 
 void launch_maxpool(const PoolParams& p, hipStream_t s) {
   const long long planes = (long long)p.N * p.C;
   const int P = p.Ho * p.Wo;
   if (planes <= 0 || P <= 0) return;
-  const int rows_fit = POOL_LDS_FLOATS / p.W;
-  if (pool_variant() == 1 && rows_fit >= p.kh) {
+  const long long plane_bytes = (long long)p.H * p.W * 4;
+  int v = pool_variant();
+  if (v == 0) {
+    // measured on the SqueezeNet pools (batch 256): one plane per block from LDS for planes of
+    // 8-48 KB (pool1 485 -> 367 us, pool3 318 -> 227 us); 27x27 planes keep the direct kernel
+    v = (plane_bytes >= 8 * 1024 && plane_bytes <= 48 * 1024) ? 4
+        : (plane_bytes > 48 * 1024 && p.kh == 3 && p.kw == 3 && p.sh == 2) ? 3 : 2;
+  }
+  if (v == 1 && POOL_LDS_FLOATS / p.W >= p.kh) {
+    const int rows_fit = POOL_LDS_FLOATS / p.W;
     int band = (rows_fit - p.kh) / p.sh + 1;
     if (band > p.Ho) band = p.Ho;
     const int nb = (p.Ho + band - 1) / band;
     hipLaunchKernelGGL(maxpool_lds_kernel, dim3((unsigned)planes, nb), dim3(256), 0, s, p, band);
+    return;
+  }
+  if (v == 4 && plane_bytes <= 64 * 1024) {
+    int lds_kb = env_knob("ORE_POOL_LDS_KB", 0);
+    if (lds_kb > 64) lds_kb = 64;
+    int pb = lds_kb ? (int)((long long)lds_kb * 1024 / plane_bytes) : 1;
+    if (pb < 1) pb = 1;
+    const long long nblk = (planes + pb - 1) / pb;
+    const size_t lds = (size_t)(pb * plane_bytes);
+    if (p.kh == 3 && p.kw == 3)
+      hipLaunchKernelGGL((maxpool_planes_kernel<3, 3>), dim3((unsigned)nblk), dim3(256), lds, s, p, pb, planes);
+    else
+      hipLaunchKernelGGL((maxpool_planes_kernel<0, 0>), dim3((unsigned)nblk), dim3(256), lds, s, p, pb, planes);
+    return;
+  }
+  if (v == 3 && p.kh == 3 && p.kw == 3 && p.sh == 2) {
+    const int RB = env_knob("ORE_POOL_RB", 16);
+    const long long cols = planes * p.Wo;
+    const dim3 grid((unsigned)((cols + 255) / 256), (unsigned)((p.Ho + RB - 1) / RB));
+    if (RB <= 4)
+      hipLaunchKernelGGL((maxpool_strip_kernel<3, 3, 2, 4>), grid, dim3(256), 0, s, p, cols);
+    else if (RB <= 8)
+      hipLaunchKernelGGL((maxpool_strip_kernel<3, 3, 2, 8>), grid, dim3(256), 0, s, p, cols);
+    else
+      hipLaunchKernelGGL((maxpool_strip_kernel<3, 3, 2, 16>), grid, dim3(256), 0, s, p, cols);
     return;
   }
   int chunks = (P + 255) / 256;

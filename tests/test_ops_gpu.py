@@ -147,12 +147,21 @@ POOL_CASES = [
     (1, 16, 14, 14, (3, 3), (3, 3), "NOTSET", [0, 0, 0, 0]),     # MNIST pool 2
     (3, 4, 10, 7, (3, 2), (2, 1), "SAME_UPPER", None),
     (3, 4, 10, 7, (4, 4), (3, 2), "SAME_LOWER", None),
+    # 3x3 stride-2 rows: the column-strip kernel (bands of 8 output rows)
+    (3, 7, 27, 27, (3, 3), (2, 2), "NOTSET", [0, 0, 0, 0]),      # pool8 shape, 13 columns per plane
+    (2, 3, 20, 17, (3, 3), (2, 1), "SAME_LOWER", None),
+    (2, 5, 35, 30, (3, 3), (2, 3), "NOTSET", [1, 2, 1, 0]),
+    (1, 2, 40, 9, (3, 3), (2, 2), "SAME_UPPER", None),
 ]
 
 
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4"])
 @pytest.mark.parametrize("case", POOL_CASES)
-def test_maxpool(gpu_ctx, case):
+def test_maxpool(gpu_ctx, case, variant, monkeypatch):
+    """Every MaxPool kernel (ORE_POOL_VARIANT: auto, band-LDS, direct, column strip, plane-LDS;
+    a variant that does not apply to a shape falls through to the direct kernel)."""
     import ore
+    monkeypatch.setenv("ORE_POOL_VARIANT", variant)
     N, C, H, W, k, s, auto_pad, pads = case
     rng = np.random.default_rng(3)
     x = (rng.standard_normal((N, C, H, W)) - 2.0).astype(np.float32)  # mostly negative: zero padding shows
