@@ -24,6 +24,12 @@ namespace ore {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));  // first-class vector (no struct copies)
 
+#ifdef ORE_EXP_SETPRIO  // timing experiment: raise wave priority around MFMA clusters
+#define ORE_PRIO(X) __builtin_amdgcn_s_setprio(X)
+#else
+#define ORE_PRIO(X)
+#endif
+
 enum { B1X1 = 0, BGATHER = 1, BGATHER_LDS = 2 };  // BGATHER_LDS: whole gather table in LDS
 
 constexpr int KTAB_LDS = 1024;  // gather-table entries staged in LDS (larger K reads it from global)
@@ -39,8 +45,13 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
   constexpr int AVEC = (AF4 + 255) / 256;    // float4 A loads per thread per tile
   static_assert(WM * WN == 4 && FM >= 1 && FN >= 1 && BK % BROWS == 0 && AVEC >= 1, "tile");
 
-  __shared__ __attribute__((aligned(16))) float As[2][BK][AS];
-  __shared__ float Bs[2][BK][BN];
+  // one LDS array: the A/B double buffers of the main loop, reused by the epilogue's per-wave
+  // [32][TN] output staging (all LDS in one __shared__ object, cdna_hip_programming.md §5)
+  constexpr int MAIN_FLOATS = 2 * BK * AS + 2 * BK * BN;
+  constexpr int EPI_FLOATS = 4 * 32 * TN;
+  __shared__ __attribute__((aligned(16))) float smem[MAIN_FLOATS > EPI_FLOATS ? MAIN_FLOATS : EPI_FLOATS];
+  float(*As)[BK][AS] = reinterpret_cast<float(*)[BK][AS]>(smem);
+  float(*Bs)[BK][BN] = reinterpret_cast<float(*)[BK][BN]>(smem + 2 * BK * AS);
   __shared__ float sbias[BM];
   __shared__ int2 ktab_s[BMODE == BGATHER_LDS ? KTAB_LDS : 1];
 
@@ -99,21 +110,17 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
   typedef const __attribute__((address_space(4))) long long* ktab_cptr;  // int2 {x, y} as one 64-bit word
   const ktab_cptr ktab = (ktab_cptr)p.ktab;
 
-  static_assert(AVEC <= 2, "A tile prefetch holds at most two float4 per thread");
 
   // Branch-free loads: every lane loads (masked lanes from x[0]) and selects 0 afterwards, so
   // the whole tile's loads issue back to back.
-#define ORE_LOAD_TILE(RA0, RA1, RB, ROK, K0)                                                                         \
+#define ORE_LOAD_TILE(RA, RB, ROK, K0)                                                               \
   {                                                                                                  \
     const int k0_ = (K0);                                                                            \
-    {                                                                                                \
-      const int kk = tid / (BM / 4), mm = (tid % (BM / 4)) * 4;                                      \
-      if (AF4 >= 256 || tid < AF4)                                                                   \
-        RA0 = *reinterpret_cast<const float4*>(wp + (unsigned)((k0_ + kk) * p.Mp + m0 + mm));       \
-      if (AVEC > 1 && (AF4 >= 512 || tid + 256 < AF4)) {                                             \
-        const int e1 = tid + 256, kk1 = e1 / (BM / 4), mm1 = (e1 % (BM / 4)) * 4;                    \
-        RA1 = *reinterpret_cast<const float4*>(wp + (unsigned)((k0_ + kk1) * p.Mp + m0 + mm1));     \
-      }                                                                                              \
+    _Pragma("unroll") for (int v_ = 0; v_ < AVEC; ++v_) {                                            \
+      /* the A tile's tail float4s (AF4 % 256 != 0) reload element 0 and are not stored */           \
+      const int e_ = (AF4 % 256 == 0 || tid + v_ * 256 < AF4) ? tid + v_ * 256 : 0;                  \
+      const int kk = e_ / (BM / 4), mm = (e_ % (BM / 4)) * 4;                                        \
+      RA[v_] = *reinterpret_cast<const floatx4*>(wp + (unsigned)((k0_ + kk) * p.Mp + m0 + mm));      \
     }                                                                                                \
     _Pragma("unroll") for (int j = 0; j < BLOADS; ++j) {                                             \
       const int k = k0_ + krow + j * BROWS;                                                          \
@@ -139,15 +146,12 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
       ROK[j] = ok;  /* the zero select happens at the LDS store, after the MFMAs */                  \
     }                                                                                                \
   }
-#define ORE_STORE_TILE(RA0, RA1, RB, ROK, BUF)                                                                       \
+#define ORE_STORE_TILE(RA, RB, ROK, BUF)                                                             \
   {                                                                                                  \
-    {                                                                                                \
-      const int kk = tid / (BM / 4), mm = (tid % (BM / 4)) * 4;                                      \
-      if (AF4 >= 256 || tid < AF4) *reinterpret_cast<float4*>(&As[BUF][kk][mm]) = RA0;              \
-      if (AVEC > 1 && (AF4 >= 512 || tid + 256 < AF4)) {                                             \
-        const int e1 = tid + 256, kk1 = e1 / (BM / 4), mm1 = (e1 % (BM / 4)) * 4;                    \
-        *reinterpret_cast<float4*>(&As[BUF][kk1][mm1]) = RA1;                                       \
-      }                                                                                              \
+    _Pragma("unroll") for (int v_ = 0; v_ < AVEC; ++v_) {                                            \
+      const int e_ = tid + v_ * 256;                                                                 \
+      const int kk = e_ / (BM / 4), mm = (e_ % (BM / 4)) * 4;                                        \
+      if (AF4 % 256 == 0 || e_ < AF4) *reinterpret_cast<floatx4*>(&As[BUF][kk][mm]) = RA[v_];        \
     }                                                                                                \
     _Pragma("unroll") for (int j = 0; j < BLOADS; ++j)                                               \
       Bs[BUF][krow + j * BROWS][bcol] = ROK[j] ? RB[j] : 0.0f;                                       \
@@ -163,11 +167,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
 
   const int ntk = (K + BK - 1) / BK;
   {
-    float4 ra0, ra1;
+    floatx4 ra[AVEC];
     float rb[BLOADS];
     bool rok[BLOADS];
-    ORE_LOAD_TILE(ra0, ra1, rb, rok, 0);
-    ORE_STORE_TILE(ra0, ra1, rb, rok, 0);
+    ORE_LOAD_TILE(ra, rb, rok, 0);
+    ORE_STORE_TILE(ra, rb, rok, 0);
   }
   __syncthreads();
   const int lrow = lane >> 5, lcol = lane & 31;
@@ -185,22 +189,24 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
         _Pragma("unroll") for (int j = 0; j < FN; ++j)                                               \
           bf[cur ^ 1][j] = Bs[BUF][kk + 2 + lrow][wn0 + j * 32 + lcol];                              \
       }                                                                                              \
+      ORE_PRIO(1);                                                                                   \
       _Pragma("unroll") for (int i = 0; i < FM; ++i)                                                 \
       _Pragma("unroll") for (int j = 0; j < FN; ++j)                                                 \
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0); \
+      ORE_PRIO(0);                                                                                   \
     }                                                                                                \
   }
   // steady state: prefetch tile t+1 into registers, MFMAs on tile t, publish t+1 to LDS
   for (int t = 0; t < ntk - 1; ++t) {
     const int buf = t & 1;
 #ifndef ORE_EXP_NOLOAD  // timing experiments only (tools/build_exp.sh)
-    float4 ra0, ra1;
+    floatx4 ra[AVEC];
     float rb[BLOADS];
     bool rok[BLOADS];
-    ORE_LOAD_TILE(ra0, ra1, rb, rok, (t + 1) * BK);
+    ORE_LOAD_TILE(ra, rb, rok, (t + 1) * BK);
     __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
     ORE_COMPUTE_TILE(buf);
-    ORE_STORE_TILE(ra0, ra1, rb, rok, buf ^ 1);
+    ORE_STORE_TILE(ra, rb, rok, buf ^ 1);
 #else
     ORE_COMPUTE_TILE(0);
 #endif
@@ -213,8 +219,54 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
 #undef ORE_LOAD_TILE
 #undef ORE_STORE_TILE
 
-  // ---- epilogue: + bias, optional Relu, scatter to NCHW (possibly a channel slice)
+  // ---- epilogue: + bias, optional Relu, store to NCHW (possibly a channel slice)
   float* __restrict__ y = p.y;
+  if (p.vec_out) {
+    // 16-B stores: each wave stages 32 output rows x TN pixels in its own LDS slice (column
+    // halves swapped every 4 rows so the two lane halves' writes hit different banks), then
+    // writes whole pixel runs with float4 stores.  Host guarantees y_ps % 4 == 0, 16-B aligned
+    // image/plane bases and Ntot % 4 == 0, so no float4 straddles an image.
+    __syncthreads();  // every wave is done with the A/B tiles
+    float* stg = smem + wave * (32 * TN);
+    constexpr int V4 = TN / 4;            // float4 per staged row
+    constexpr int RPI = 64 / V4;          // rows per wave-instruction
+    // staging address of (row r, column c): rows r and r + 4 (the two lane halves of one MFMA
+    // output register) land in opposite halves of the 64 banks
+#define ORE_STG(R, C) (TN >= 64 ? (R) * TN + ((C) ^ ((((R) >> 2) & 1) * 32)) : ((R) ^ (((R) >> 2) & 1)) * TN + (C))
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int r = (e & 3) + 8 * (e >> 2) + 4 * lrow;
+          float v = acc[i][j][e] + sbias[wm0 + i * 32 + r];
+          if (p.relu) v = fmaxf(v, 0.0f);
+          stg[ORE_STG(r, j * 32 + lcol)] = v;
+        }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int c4 = (lane % V4) * 4;
+      const int n = n0 + wn0 + c4;
+      const int img = n / YPS;
+      const int pix = n - img * YPS;
+      const bool nok = n < p.Ntot;
+#pragma unroll
+      for (int rr = 0; rr < 32; rr += RPI) {
+        const int r = rr + lane / V4;
+        const int m = m0 + wm0 + i * 32 + r;
+        const floatx4 v = *reinterpret_cast<const floatx4*>(stg + ORE_STG(r, c4));
+        if (nok && m < p.M)
+          *reinterpret_cast<floatx4*>(y + (unsigned)(img * (int)p.y_nstride + m * YPS + pix)) = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+#undef ORE_STG
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = n0 + wn0 + j * 32 + lcol;
@@ -698,11 +750,12 @@ void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
     }
     return;
   }
+  const bool bk32 = env_int("ORE_CONV_BK", 16) == 32;  // tuning knob
   switch (pln.cfg) {
-    case 0: launch_conv_cfg<128, 128, 2, 2, 16>(p, s); break;
-    case 1: launch_conv_cfg<96, 128, 1, 4, 16>(p, s); break;
-    case 2: launch_conv_cfg<64, 128, 2, 2, 16>(p, s); break;
-    default: launch_conv_cfg<32, 256, 1, 4, 16>(p, s); break;
+    case 0: if (bk32) launch_conv_cfg<128, 128, 2, 2, 32>(p, s); else launch_conv_cfg<128, 128, 2, 2, 16>(p, s); break;
+    case 1: if (bk32) launch_conv_cfg<96, 128, 1, 4, 32>(p, s); else launch_conv_cfg<96, 128, 1, 4, 16>(p, s); break;
+    case 2: if (bk32) launch_conv_cfg<64, 128, 2, 2, 32>(p, s); else launch_conv_cfg<64, 128, 2, 2, 16>(p, s); break;
+    default: if (bk32) launch_conv_cfg<32, 256, 1, 4, 32>(p, s); else launch_conv_cfg<32, 256, 1, 4, 16>(p, s); break;
   }
 }
 

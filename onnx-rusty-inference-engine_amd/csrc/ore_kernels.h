@@ -24,6 +24,7 @@ struct ConvParams {
   int is1x1;           // kh = kw = 1, stride 1, no padding, Ho*Wo == H*W
   int Mp;              // row stride of wp (conv_packed_mp(M))
   int mtiles, ntiles;  // filled by the launcher
+  int vec_out;         // 16-B epilogue stores (y_ps, y_nstride % 4 == 0 and a 16-B aligned y)
   // window-staged kernel (filled by the launcher from the ConvPlan)
   int bch, ks, nst, wr, ww, tiles_per_img;
 };
