@@ -23,6 +23,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "SqueezeNet-1.0 fp32 images/s at batch 256, 1/2/4/8 MI355X; max-abs diff vs CPU"
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
+PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: f16/bf16 MFMA dense peak (no sparsity)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec peak
 
 
@@ -37,6 +38,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-step-timing", action="store_true", help="no per-kernel HIP events in the timed loop")
     ap.add_argument("--layers", action="store_true", help="print per-kernel-step times to stderr")
+    ap.add_argument("--precision", choices=["f32", "f16"], default="f32",
+                    help="f16: the fp16 variant (SURVEY.md §8(f)3, config 5); the headline metric is f32")
     return ap.parse_args()
 
 
@@ -91,7 +94,8 @@ def main():
     B = args.batch
     model_bytes = squeezenet.build(args.hw)
     ctx = ore.Context(local)
-    model = ore.Model(ctx, model_bytes, max_batch=B)
+    model = ore.Model(ctx, model_bytes, max_batch=B, precision=args.precision)
+    f16 = args.precision == "f16"
     g = torch.Generator(device=f"cuda:{local}")
     g.manual_seed(1000 + rank)
     x = (torch.rand((B, 3, args.hw, args.hw), generator=g, device=f"cuda:{local}") * 100.0 - 50.0).contiguous()
@@ -135,10 +139,11 @@ def main():
         result = {
             "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (seeded U(-50,50) 3x224x224 images; seeded He-normal SqueezeNet-1.0 weights)",
-            "config": {"workload": f"SqueezeNet-1.0 (66 nodes, 818.9 MMAC/img) fp32 inference, batch {B} per GPU, "
-                                   f"3x{args.hw}x{args.hw}",
+            "config": {"workload": f"SqueezeNet-1.0 (66 nodes, 818.9 MMAC/img) "
+                                   f"{'fp16 (config 5: f16 activations/weights, f32 accumulate)' if f16 else 'fp32'} "
+                                   f"inference, batch {B} per GPU, 3x{args.hw}x{args.hw}",
                        "model": "squeezenet1.0-8 topology, synthetic weights", "global_batch": world * B,
                        "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}",
                        "collective": "RCCL all_gather of [256,1000] logits per step" if world > 1 else None},
@@ -154,10 +159,13 @@ def main():
                 c["launches"] += 1
             conv = classes.get("Conv", {"ms": 1e-9, "flops": 0.0, "launches": 1})
             achieved = conv["flops"] / (conv["ms"] * 1e-3) / 1e12
+            peak = PEAK_F16_MFMA_TFLOPS if f16 else PEAK_F32_MFMA_TFLOPS
+            kname = ("conv_f16_kernel (implicit-GEMM MFMA 32x32x16 f16, f32 accumulate" if f16 else
+                     "conv_gemm_kernel (implicit-GEMM MFMA 32x32x2 f32") + ", 26 launches/step)"
             result["roofline"] = {
-                "bound": "mfma", "kernel": "conv_gemm_kernel (implicit-GEMM MFMA 32x32x2 f32, 26 launches/step)",
-                "achieved": round(achieved, 2), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4), "traffic": None,
+                "bound": "mfma", "kernel": kname,
+                "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": None,
                 "per_launch_avg_us": round(1000.0 * conv["ms"] / conv["launches"], 2),
                 "algorithmic": "2*Cout*Ho*Wo*Cin*kh*kw per image (1.638 GFLOP/img)"}
             if args.layers:
@@ -177,7 +185,9 @@ def main():
             xs = x[:2].cpu().numpy()
             ref = oracle.Model(model_bytes).run(xs, 1000)
             result["max_abs_diff_vs_cpu"] = float(np.abs(out[:2].cpu().numpy() - ref).max())
-            result["max_abs_sample"] = "2 images of the timed batch vs oracle (C restatement of the reference)"
+            result["max_abs_sample"] = "2 images of the timed batch vs oracle (C restatement of the reference, f32)"
+            if f16:
+                result["top1_agrees_with_cpu"] = bool((out[:2].cpu().numpy().argmax(1) == ref.argmax(1)).all())
             if not args.no_cpu_baseline:
                 threads = args.cpu_threads or min(16, os.cpu_count() or 1)
                 result["cpu_baseline"] = cpu_baseline(model_bytes, args.hw, threads)

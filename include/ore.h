@@ -141,6 +141,15 @@ ore_status ore_reshape(const ore_tensor* x, const int64_t* shape, int32_t n_shap
  * Unsupported ops/attributes fail here (the reference panics when it reaches them). */
 ore_status ore_model_load(ore_ctx* ctx, const void* onnx_bytes, size_t len, int64_t max_batch,
                           ore_model** out);
+/* Load flags.  ORE_LOAD_F16: the fp16 variant (no reference
+ * counterpart -- the reference is f32 only): Conv weights and the activations of Conv / MaxPool /
+ * Relu / Concat / Dropout are f16, Conv accumulates in f32 on the f16 matrix cores (bias and Relu
+ * in f32, rounded once), GlobalAveragePool sums f16 inputs in f32, and Softmax, Add and MatMul
+ * stay f32 (Add / MatMul / Softmax on an f16 value is rejected).  The model input and
+ * graph.output[0] stay f32 (an f16 graph output is rejected). */
+#define ORE_LOAD_F16 1
+ore_status ore_model_load_ex(ore_ctx* ctx, const void* onnx_bytes, size_t len, int64_t max_batch, int32_t flags,
+                             ore_model** out);
 ore_status ore_model_destroy(ore_model* m);
 /* flags: bit 0 = fuse Conv->Relu, bit 1 = Concat in place, bit 2 = alias Dropout/Reshape.
  * ORE_FUSE_ALL is the default; 0 runs every node as its own kernel (op-by-op parity). */

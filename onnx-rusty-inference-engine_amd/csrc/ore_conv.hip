@@ -329,8 +329,8 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
 int conv_packed_mp(int M) { return (M + 127) / 128 * 128; }
 int conv_packed_kp(int K) { return (K + 31) / 32 * 32; }
 
-void launch_pack_weights(const float* w, bool kmajor_src, int M, int K, float* wp, hipStream_t s) {
-  const int Mp = conv_packed_mp(M), Kp = conv_packed_kp(K);
+void launch_pack_weights(const float* w, bool kmajor_src, int M, int K, int Mp, float* wp, hipStream_t s) {
+  const int Kp = conv_packed_kp(K);
   long long total = (long long)Mp * Kp;
   long long blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
@@ -652,9 +652,10 @@ static const int CFG_BN[4] = {128, 128, 128, 256};
 
 
 ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
-                   bool is1x1) {
+                   bool is1x1, bool f16) {
   (void)H; (void)W; (void)pt;
   ConvPlan pln{};
+  pln.f16 = f16 ? 1 : 0;
   pln.cfg = conv_tile_config(M);
   const int K = C * kh * kw;
   // short-K 1x1 layers (SqueezeNet's expand1x1, K <= 64) are epilogue/write bound: the 1x4-wave
@@ -662,9 +663,15 @@ ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, i
   if (K <= 64 && M >= 64 && is1x1) pln.cfg = 1;
   const int forced = env_int("ORE_CONV_CFG", -1);  // tuning knob
   if (forced >= 0 && forced < 4) pln.cfg = forced;
+  // packed rows cover every block tile's rows (the 96-row tile can pass roundup(M, 128))
   pln.Mp = conv_packed_mp(M);
+  {
+    const int bm = CFG_BM[pln.cfg], rows = (M + bm - 1) / bm * bm;
+    if (rows > pln.Mp) pln.Mp = rows;
+  }
   pln.krows = conv_packed_kp(K);
   pln.window = 0;
+  if (f16) return pln;
   const int P = Ho * Wo;
   // The window-staged kernel is opt-in (ORE_CONV_WINDOW=1): on the SqueezeNet layers it measured
   // 5-45 % slower than the gather kernel (its 49-59 KB LDS stages allow 2-3 blocks per CU against
@@ -710,12 +717,18 @@ ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, i
   return pln;
 }
 
-size_t conv_packed_bytes(const ConvPlan& pln) { return (size_t)pln.krows * pln.Mp * sizeof(float); }
+size_t conv_packed_bytes(const ConvPlan& pln) {
+  return (size_t)pln.krows * pln.Mp * (pln.f16 ? sizeof(_Float16) : sizeof(float));
+}
 
 void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, const ConvPlan& pln, float* wp,
                  hipStream_t s) {
+  if (pln.f16) {
+    launch_pack_weights_f16(w, kmajor_src, M, C * kh * kw, pln.Mp, wp, s);
+    return;
+  }
   if (!pln.window) {
-    launch_pack_weights(w, kmajor_src, M, C * kh * kw, wp, s);
+    launch_pack_weights(w, kmajor_src, M, C * kh * kw, pln.Mp, wp, s);
     return;
   }
   const long long total = (long long)pln.krows * pln.Mp;
@@ -741,6 +754,10 @@ static void launch_win_cfg(const ConvParams& p0, const ConvPlan& pln, hipStream_
 }
 
 void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
+  if (pln.f16) {
+    launch_conv_f16(p, pln.cfg, s);
+    return;
+  }
   if (pln.window) {
     switch (pln.cfg) {
       case 0: launch_win_cfg<128, 128, 2, 2>(p, pln, s); break;

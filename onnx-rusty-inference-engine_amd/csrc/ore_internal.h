@@ -83,13 +83,14 @@ ore_status resolve_window(ore_ctx* ctx, int auto_pad, const int64_t* pads, int n
 // ---------------------------------------------------------------- launches over resolved geometry
 // Kernel plan of a conv (or MatMul as a 1x1 conv) over resolved geometry.
 ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
-                   const Window& win);
+                   const Window& win, bool f16 = false);
 // wp: weights packed by launch_pack for plan `pln`
 // ktab: gather table (launch_ktab) for non-1x1 geometry on the gather kernel
 ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
                     int64_t x_nstride, const float* wp, const int2* ktab, int64_t M, int64_t kh, int64_t kw,
                     const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, float* y,
-                    int64_t y_nstride, int64_t x_ps = 0, int64_t y_ps = 0);  // plane strides, 0 = dense
+                    int64_t y_nstride, int64_t x_ps = 0, int64_t y_ps = 0,  // plane strides, 0 = dense
+                    int x_es = 4);  // input element bytes (2: f16; only with an f16 plan, whose output is f16)
 // packs w (and the gather table for an input of H x W) into the context scratch buffer;
 // returns the packed weights (or null with the error set), *ktab receives the table
 float* pack_to_scratch(ore_ctx* ctx, const ConvPlan& pln, const float* w, bool kmajor_src, int64_t M, int64_t C,
@@ -98,6 +99,7 @@ float* pack_to_scratch(ore_ctx* ctx, const ConvPlan& pln, const float* w, bool k
 size_t packed_bytes(const ConvPlan& pln);
 ore_status run_maxpool(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
                        int64_t x_nstride, int64_t kh, int64_t kw, const Window& win, int64_t sh, int64_t sw,
-                       float* y, int64_t y_nstride, int64_t x_ps = 0, int64_t y_ps = 0);
+                       float* y, int64_t y_nstride, int64_t x_ps = 0, int64_t y_ps = 0,
+                       int es = 4);  // element bytes of x and y
 
 }  // namespace ore

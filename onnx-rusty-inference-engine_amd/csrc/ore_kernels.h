@@ -25,12 +25,14 @@ struct ConvParams {
   int Mp;              // row stride of wp (conv_packed_mp(M))
   int mtiles, ntiles;  // filled by the launcher
   int vec_out;         // 16-B epilogue stores (y_ps, y_nstride % 4 == 0 and a 16-B aligned y)
+  int x_f32;           // f16 kernel: the input is f32 (rounded to f16 while staging)
   // window-staged kernel (filled by the launcher from the ConvPlan)
   int bch, ks, nst, wr, ww, tiles_per_img;
 };
 
 // Per-layer kernel choice and weight layout (see plan_conv in ore_conv.hip).
 struct ConvPlan {
+  int f16;             // 1: conv_f16_kernel (f16 weights Wh[Mp][Kp] and f16 output)
   int window;          // 1: conv_win_kernel (stage-major packed weights), 0: conv_gemm_kernel
   int cfg;             // block tile (0: 128x128, 1: 96x128, 2: 64x128, 3: 32x256)
   int bch, ks, nst;    // window: channels / K rows per stage, stages
@@ -40,13 +42,14 @@ struct ConvPlan {
 };
 
 struct PoolParams {
-  const float* x;
+  const float* x;      // element type per es (f32 or f16 storage)
   float* y;
   int N, C, H, W;
   int kh, kw, sh, sw, pt, pl;
   int Ho, Wo;
-  int x_ps, y_ps;      // channel-plane strides
+  int x_ps, y_ps;      // channel-plane strides (elements)
   long long x_nstride, y_nstride;
+  int es;              // element bytes: 4 (f32) or 2 (f16)
 };
 
 struct AddParams {
@@ -61,10 +64,12 @@ int conv_tile_config(int M);
 int conv_packed_mp(int M);  // padded M of the packed weights
 int conv_packed_kp(int K);  // padded K of the packed weights
 // w: ONNX conv weights [M][K] (kmajor_src = false) or MatMul B [K][M] (true) -> wp[Kp][Mp]
-void launch_pack_weights(const float* w, bool kmajor_src, int M, int K, float* wp, hipStream_t s);
+void launch_pack_weights(const float* w, bool kmajor_src, int M, int K, int Mp, float* wp, hipStream_t s);
 void launch_ktab(int2* ktab, int K, int kh, int kw, int x_ps, int W, hipStream_t s);
 ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
-                   bool is1x1);
+                   bool is1x1, bool f16 = false);
+void launch_pack_weights_f16(const float* w, bool kmajor_src, int M, int K, int Mp, void* wh, hipStream_t s);
+void launch_conv_f16(const ConvParams& p, int cfg, hipStream_t s);
 size_t conv_packed_bytes(const ConvPlan& pln);
 // packs ONNX weights [M][C][kh][kw] (or MatMul [K][M]) in the layout the plan's kernel reads
 void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, const ConvPlan& pln, float* wp,
@@ -72,10 +77,11 @@ void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, 
 void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s);
 void launch_maxpool(const PoolParams& p, hipStream_t s);
 void launch_relu(const float* x, float* y, long long n, hipStream_t s);
+void launch_relu_f16(const void* x, void* y, long long n, hipStream_t s);
 void launch_add_bcast(const AddParams& p, hipStream_t s);
 void launch_softmax(const float* x, float* y, long long rows, int D, hipStream_t s);
-void launch_gap(const float* x, float* y, long long rows, int HW, hipStream_t s);
-void launch_concat(const float* a, const float* b, float* y, long long outer, long long ia, long long ib,
+void launch_gap(const void* x, int es, float* y, long long rows, int HW, hipStream_t s);  // es: 4 f32, 2 f16 input
+void launch_concat(const void* a, const void* b, void* y, int es, long long outer, long long ia, long long ib,
                    hipStream_t s);
 
 }  // namespace ore

@@ -25,14 +25,14 @@ namespace ore {
 // inside a plane.  The window reads zeros outside the image (the reference pads with 0,
 // max_pool_op.rs:265-276) and starts from -FLT_MAX (:337).  HBM-bound: in + out bytes.
 // ------------------------------------------------------------------------------------------
-template <int KH, int KW>  // 0 = runtime window size
+template <typename T, int KH, int KW>  // T: float or _Float16 (element type of x and y); 0 = runtime window
 __global__ __launch_bounds__(256) void maxpool_kernel(PoolParams p, int chunks) {
   // 1-D grid, chunk index fastest: consecutive blocks stream consecutive parts of one plane
   const int plane = blockIdx.x / chunks;  // n * C + c
   const int chunk = blockIdx.x - plane * chunks;
   const int n = plane / p.C, c = plane - n * p.C;
-  const float* __restrict__ xp = p.x + (long long)n * p.x_nstride + (long long)c * p.x_ps;
-  float* __restrict__ yp = p.y + (long long)n * p.y_nstride + (long long)c * p.y_ps;
+  const T* __restrict__ xp = reinterpret_cast<const T*>(p.x) + (long long)n * p.x_nstride + (long long)c * p.x_ps;
+  T* __restrict__ yp = reinterpret_cast<T*>(p.y) + (long long)n * p.y_nstride + (long long)c * p.y_ps;
   const int P = p.Ho * p.Wo;
   for (int idx = chunk * 256 + threadIdx.x; idx < P; idx += chunks * 256) {
     const int oh = idx / p.Wo, ow = idx - oh * p.Wo;
@@ -43,15 +43,15 @@ __global__ __launch_bounds__(256) void maxpool_kernel(PoolParams p, int chunks) 
     for (int r = 0; r < kh; ++r) {
       const int ih = ih0 + r;
       const bool rok = (unsigned)ih < (unsigned)p.H;
-      const float* row = xp + ih * p.W;
+      const T* row = xp + ih * p.W;
 #pragma unroll
       for (int s = 0; s < kw; ++s) {
         const int iw = iw0 + s;
-        const float v = (rok && (unsigned)iw < (unsigned)p.W) ? row[iw] : 0.0f;
+        const float v = (rok && (unsigned)iw < (unsigned)p.W) ? (float)row[iw] : 0.0f;
         m = fmaxf(m, v);
       }
     }
-    yp[idx] = m;
+    yp[idx] = (T)m;  // max of the inputs (or 0): exact in T
   }
 }
 
@@ -101,15 +101,15 @@ __global__ __launch_bounds__(256) void maxpool_lds_kernel(PoolParams p, int band
 // row costs SH*KW loads instead of KH*KW.  Lanes are consecutive output columns (then the next
 // plane's), so loads are stride-SW and stores are coalesced.  Zero padding / -FLT_MAX start as
 // above; max is exact, so the regrouping is bit-identical.
-template <int KH, int KW, int SH, int RB>
+template <typename T, int KH, int KW, int SH, int RB>
 __global__ __launch_bounds__(256) void maxpool_strip_kernel(PoolParams p, long long cols) {
   const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
   if (t >= cols) return;
   const long long plane = t / p.Wo;
   const int ow = (int)(t - plane * p.Wo);
   const int n = (int)(plane / p.C), c = (int)(plane - (long long)n * p.C);
-  const float* __restrict__ xp = p.x + (long long)n * p.x_nstride + (long long)c * p.x_ps;
-  float* __restrict__ yp = p.y + (long long)n * p.y_nstride + (long long)c * p.y_ps;
+  const T* __restrict__ xp = reinterpret_cast<const T*>(p.x) + (long long)n * p.x_nstride + (long long)c * p.x_ps;
+  T* __restrict__ yp = reinterpret_cast<T*>(p.y) + (long long)n * p.y_nstride + (long long)c * p.y_ps;
   const int oh0 = blockIdx.y * RB;
   const int oh1 = min(p.Ho, oh0 + RB);
   const int iw0 = ow * p.sw - p.pl;
@@ -122,10 +122,10 @@ __global__ __launch_bounds__(256) void maxpool_strip_kernel(PoolParams p, long l
   {                                                                               \
     const int ih_ = (IH);                                                         \
     const bool rok_ = (unsigned)ih_ < (unsigned)p.H;                              \
-    const float* row_ = xp + (rok_ ? ih_ : 0) * p.W;                              \
+    const T* row_ = xp + (rok_ ? ih_ : 0) * p.W;                                  \
     float m_ = -FLT_MAX;                                                          \
     _Pragma("unroll") for (int s = 0; s < KW; ++s) {                              \
-      const float v_ = (rok_ && cok[s]) ? row_[iw0 + s] : 0.0f;                   \
+      const float v_ = (rok_ && cok[s]) ? (float)row_[iw0 + s] : 0.0f;            \
       m_ = fmaxf(m_, v_);                                                         \
     }                                                                             \
     DST = m_;                                                                     \
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void maxpool_strip_kernel(PoolParams p, long l
       ORE_ROWMAX(fresh[r], ih + KEEP + r);
       m = fmaxf(m, fresh[r]);
     }
-    yp[oh * p.Wo + ow] = m;
+    yp[oh * p.Wo + ow] = (T)m;
     // rows ih+SH .. ih+KH-1 open the next window
 #pragma unroll
     for (int r = 0; r < KEEP; ++r) keep[r] = (r + SH < KEEP) ? keep[r + SH] : fresh[r + SH - KEEP];
@@ -156,9 +156,10 @@ __global__ __launch_bounds__(256) void maxpool_strip_kernel(PoolParams p, long l
 // Plane-staged MaxPool: one block per group of PB consecutive (n, c) planes.  The planes are
 // copied to LDS with coalesced loads (every input element leaves HBM once, 8 loads in flight per
 // thread), then every output window is evaluated from LDS and stored coalesced.
-template <int KH, int KW>
+template <typename T, int KH, int KW>
 __global__ __launch_bounds__(256) void maxpool_planes_kernel(PoolParams p, int pb, long long planes) {
-  extern __shared__ float tile[];  // [pb][H*W]
+  extern __shared__ __attribute__((aligned(16))) char tile_raw[];
+  T* tile = reinterpret_cast<T*>(tile_raw);  // [pb][H*W]
   const int HW = p.H * p.W;
   const long long q0 = (long long)blockIdx.x * pb;
   const int nq = (int)min((long long)pb, planes - q0);
@@ -166,11 +167,11 @@ __global__ __launch_bounds__(256) void maxpool_planes_kernel(PoolParams p, int p
   for (int q = 0; q < nq; ++q) {
     const long long pl = q0 + q;
     const int n = (int)(pl / p.C), c = (int)(pl - (long long)n * p.C);
-    const float* __restrict__ xq = p.x + (long long)n * p.x_nstride + (long long)c * p.x_ps;
-    float* tq = tile + q * HW;
+    const T* __restrict__ xq = reinterpret_cast<const T*>(p.x) + (long long)n * p.x_nstride + (long long)c * p.x_ps;
+    T* tq = tile + q * HW;
     int i = tid;
     for (; i + 7 * 256 < HW; i += 8 * 256) {
-      float v[8];
+      T v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) v[u] = xq[i + u * 256];
 #pragma unroll
@@ -184,8 +185,8 @@ __global__ __launch_bounds__(256) void maxpool_planes_kernel(PoolParams p, int p
   for (int q = 0; q < nq; ++q) {
     const long long pl = q0 + q;
     const int n = (int)(pl / p.C), c = (int)(pl - (long long)n * p.C);
-    float* __restrict__ yq = p.y + (long long)n * p.y_nstride + (long long)c * p.y_ps;
-    const float* tq = tile + q * HW;
+    T* __restrict__ yq = reinterpret_cast<T*>(p.y) + (long long)n * p.y_nstride + (long long)c * p.y_ps;
+    const T* tq = tile + q * HW;
     for (int o = tid; o < P; o += 256) {
       const int oh = o / p.Wo, ow = o - oh * p.Wo;
       const int ih0 = oh * p.sh - p.pt, iw0 = ow * p.sw - p.pl;
@@ -197,11 +198,11 @@ __global__ __launch_bounds__(256) void maxpool_planes_kernel(PoolParams p, int p
 #pragma unroll
         for (int s2 = 0; s2 < kw; ++s2) {
           const int iw = iw0 + s2;
-          const float v = (rok && (unsigned)iw < (unsigned)p.W) ? tq[ih * p.W + iw] : 0.0f;
+          const float v = (rok && (unsigned)iw < (unsigned)p.W) ? (float)tq[ih * p.W + iw] : 0.0f;
           m = fmaxf(m, v);
         }
       }
-      yq[o] = m;
+      yq[o] = (T)m;
     }
   }
 }
@@ -215,19 +216,27 @@ static int env_knob(const char* name, int dflt) {
 }
 static int pool_variant() { return env_knob("ORE_POOL_VARIANT", 0); }
 
-void launch_maxpool(const PoolParams& p, hipStream_t s) {
+template <typename T>
+static void launch_maxpool_t(const PoolParams& p, hipStream_t s) {
   const long long planes = (long long)p.N * p.C;
   const int P = p.Ho * p.Wo;
   if (planes <= 0 || P <= 0) return;
-  const long long plane_bytes = (long long)p.H * p.W * 4;
+  const long long plane_bytes = (long long)p.H * p.W * (long long)sizeof(T);
   int v = pool_variant();
   if (v == 0) {
     // measured on the SqueezeNet pools (batch 256): one plane per block from LDS for planes of
-    // 8-48 KB (pool1 485 -> 367 us, pool3 318 -> 227 us); 27x27 planes keep the direct kernel
-    v = (plane_bytes >= 8 * 1024 && plane_bytes <= 48 * 1024) ? 4
-        : (plane_bytes > 48 * 1024 && p.kh == 3 && p.kw == 3 && p.sh == 2) ? 3 : 2;
+    // >= 2048 elements up to 48 KB (f32 pool1 485 -> 367 us, pool3 318 -> 227 us; f16 pool1 617 ->
+    // 204, pool3 380 -> 186); 27x27 planes: the direct kernel for f32 (150 us vs strip 171), the
+    // column strip for f16 (120 us vs direct 169)
+    const bool s332 = p.kh == 3 && p.kw == 3 && p.sh == 2;
+    if ((long long)p.H * p.W >= 2048 && plane_bytes <= 48 * 1024)
+      v = 4;
+    else if (s332 && (plane_bytes > 48 * 1024 || sizeof(T) == 2))
+      v = 3;
+    else
+      v = 2;
   }
-  if (v == 1 && POOL_LDS_FLOATS / p.W >= p.kh) {
+  if (v == 1 && sizeof(T) == 4 && POOL_LDS_FLOATS / p.W >= p.kh) {
     const int rows_fit = POOL_LDS_FLOATS / p.W;
     int band = (rows_fit - p.kh) / p.sh + 1;
     if (band > p.Ho) band = p.Ho;
@@ -243,9 +252,9 @@ void launch_maxpool(const PoolParams& p, hipStream_t s) {
     const long long nblk = (planes + pb - 1) / pb;
     const size_t lds = (size_t)(pb * plane_bytes);
     if (p.kh == 3 && p.kw == 3)
-      hipLaunchKernelGGL((maxpool_planes_kernel<3, 3>), dim3((unsigned)nblk), dim3(256), lds, s, p, pb, planes);
+      hipLaunchKernelGGL((maxpool_planes_kernel<T, 3, 3>), dim3((unsigned)nblk), dim3(256), lds, s, p, pb, planes);
     else
-      hipLaunchKernelGGL((maxpool_planes_kernel<0, 0>), dim3((unsigned)nblk), dim3(256), lds, s, p, pb, planes);
+      hipLaunchKernelGGL((maxpool_planes_kernel<T, 0, 0>), dim3((unsigned)nblk), dim3(256), lds, s, p, pb, planes);
     return;
   }
   if (v == 3 && p.kh == 3 && p.kw == 3 && p.sh == 2) {
@@ -253,19 +262,26 @@ void launch_maxpool(const PoolParams& p, hipStream_t s) {
     const long long cols = planes * p.Wo;
     const dim3 grid((unsigned)((cols + 255) / 256), (unsigned)((p.Ho + RB - 1) / RB));
     if (RB <= 4)
-      hipLaunchKernelGGL((maxpool_strip_kernel<3, 3, 2, 4>), grid, dim3(256), 0, s, p, cols);
+      hipLaunchKernelGGL((maxpool_strip_kernel<T, 3, 3, 2, 4>), grid, dim3(256), 0, s, p, cols);
     else if (RB <= 8)
-      hipLaunchKernelGGL((maxpool_strip_kernel<3, 3, 2, 8>), grid, dim3(256), 0, s, p, cols);
+      hipLaunchKernelGGL((maxpool_strip_kernel<T, 3, 3, 2, 8>), grid, dim3(256), 0, s, p, cols);
     else
-      hipLaunchKernelGGL((maxpool_strip_kernel<3, 3, 2, 16>), grid, dim3(256), 0, s, p, cols);
+      hipLaunchKernelGGL((maxpool_strip_kernel<T, 3, 3, 2, 16>), grid, dim3(256), 0, s, p, cols);
     return;
   }
   int chunks = (P + 255) / 256;
   if (chunks > 64) chunks = 64;
   if (p.kh == 3 && p.kw == 3)
-    hipLaunchKernelGGL((maxpool_kernel<3, 3>), dim3((unsigned)(planes * chunks)), dim3(256), 0, s, p, chunks);
+    hipLaunchKernelGGL((maxpool_kernel<T, 3, 3>), dim3((unsigned)(planes * chunks)), dim3(256), 0, s, p, chunks);
   else
-    hipLaunchKernelGGL((maxpool_kernel<0, 0>), dim3((unsigned)(planes * chunks)), dim3(256), 0, s, p, chunks);
+    hipLaunchKernelGGL((maxpool_kernel<T, 0, 0>), dim3((unsigned)(planes * chunks)), dim3(256), 0, s, p, chunks);
+}
+
+void launch_maxpool(const PoolParams& p, hipStream_t s) {
+  if (p.es == 2)
+    launch_maxpool_t<_Float16>(p, s);
+  else
+    launch_maxpool_t<float>(p, s);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -295,6 +311,14 @@ __global__ __launch_bounds__(256) void relu_scalar_kernel(const float* __restric
     y[i] = fmaxf(x[i], 0.0f);
 }
 
+__global__ __launch_bounds__(256) void relu_f16_kernel(const _Float16* __restrict__ x, _Float16* __restrict__ y,
+                                                       long long n) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const _Float16 v = x[i];
+    y[i] = v > (_Float16)0 ? v : (_Float16)0;  // max(x, 0); -0 and NaN as f32 fmaxf would give
+  }
+}
+
 static unsigned stream_blocks(long long work) {
   long long b = (work + 255) / 256;
   if (b > 256 * 8) b = 256 * 8;
@@ -308,6 +332,11 @@ void launch_relu(const float* x, float* y, long long n, hipStream_t s) {
     hipLaunchKernelGGL(relu_kernel, dim3(stream_blocks(n >> 2)), dim3(256), 0, s, x, y, n);
   else
     hipLaunchKernelGGL(relu_scalar_kernel, dim3(stream_blocks(n)), dim3(256), 0, s, x, y, n);
+}
+
+void launch_relu_f16(const void* x, void* y, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(relu_f16_kernel, dim3(stream_blocks(n)), dim3(256), 0, s, static_cast<const _Float16*>(x),
+                     static_cast<_Float16*>(y), n);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -382,14 +411,15 @@ void launch_softmax(const float* x, float* y, long long rows, int D, hipStream_t
 // GlobalAveragePool: 64 (image, channel) rows per block are staged through LDS with coalesced
 // loads, then each lane sums its row sequentially (the reference's order) and divides.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void gap_kernel(const float* __restrict__ x, float* __restrict__ y,
+template <typename T>  // input element type (f32 sums either way)
+__global__ __launch_bounds__(256) void gap_kernel(const T* __restrict__ x, float* __restrict__ y,
                                                   long long rows, int HW) {
   extern __shared__ float tile[];  // 64 * HW floats
   const long long r0 = (long long)blockIdx.x * 64;
   const long long nr = rows - r0 < 64 ? rows - r0 : 64;
   const long long base = r0 * HW;
   const long long cnt = nr * HW;
-  for (long long i = threadIdx.x; i < cnt; i += 256) tile[i] = x[base + i];
+  for (long long i = threadIdx.x; i < cnt; i += 256) tile[i] = (float)x[base + i];
   __syncthreads();
   if (threadIdx.x < nr) {
     const float* tr = tile + (long long)threadIdx.x * HW;
@@ -399,31 +429,41 @@ __global__ __launch_bounds__(256) void gap_kernel(const float* __restrict__ x, f
   }
 }
 
-__global__ __launch_bounds__(64) void gap_big_kernel(const float* __restrict__ x, float* __restrict__ y,
+template <typename T>
+__global__ __launch_bounds__(64) void gap_big_kernel(const T* __restrict__ x, float* __restrict__ y,
                                                      long long rows, int HW) {
   const long long r = (long long)blockIdx.x * 64 + threadIdx.x;
   if (r >= rows) return;
-  const float* tr = x + r * HW;
+  const T* tr = x + r * HW;
   float s = 0.0f;
-  for (int i = 0; i < HW; ++i) s = s + tr[i];
+  for (int i = 0; i < HW; ++i) s = s + (float)tr[i];
   y[r] = s / (float)HW;
 }
 
-void launch_gap(const float* x, float* y, long long rows, int HW, hipStream_t s) {
+template <typename T>
+static void launch_gap_t(const T* x, float* y, long long rows, int HW, hipStream_t s) {
   if (rows <= 0) return;
   const unsigned blocks = (unsigned)((rows + 63) / 64);
   const size_t lds = (size_t)64 * HW * sizeof(float);
   if (lds <= 64 * 1024)
-    hipLaunchKernelGGL(gap_kernel, dim3(blocks), dim3(256), lds, s, x, y, rows, HW);
+    hipLaunchKernelGGL(gap_kernel<T>, dim3(blocks), dim3(256), lds, s, x, y, rows, HW);
   else
-    hipLaunchKernelGGL(gap_big_kernel, dim3(blocks), dim3(64), 0, s, x, y, rows, HW);
+    hipLaunchKernelGGL(gap_big_kernel<T>, dim3(blocks), dim3(64), 0, s, x, y, rows, HW);
+}
+
+void launch_gap(const void* x, int es, float* y, long long rows, int HW, hipStream_t s) {
+  if (es == 2)
+    launch_gap_t(static_cast<const _Float16*>(x), y, rows, HW, s);
+  else
+    launch_gap_t(static_cast<const float*>(x), y, rows, HW, s);
 }
 
 // ------------------------------------------------------------------------------------------
 // Concat of two row-major tensors along an axis: outer blocks of (inner_a | inner_b).
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void concat_kernel(const float* __restrict__ a, const float* __restrict__ b,
-                                                     float* __restrict__ y, long long outer,
+template <typename T>
+__global__ __launch_bounds__(256) void concat_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                     T* __restrict__ y, long long outer,
                                                      long long ia, long long ib) {
   const long long row = ia + ib;
   const long long total = outer * row;
@@ -434,10 +474,15 @@ __global__ __launch_bounds__(256) void concat_kernel(const float* __restrict__ a
   }
 }
 
-void launch_concat(const float* a, const float* b, float* y, long long outer, long long ia, long long ib,
+void launch_concat(const void* a, const void* b, void* y, int es, long long outer, long long ia, long long ib,
                    hipStream_t s) {
-  hipLaunchKernelGGL(concat_kernel, dim3(stream_blocks(outer * (ia + ib))), dim3(256), 0, s, a, b, y,
-                     outer, ia, ib);
+  const dim3 grid(stream_blocks(outer * (ia + ib)));
+  if (es == 2)
+    hipLaunchKernelGGL(concat_kernel<_Float16>, grid, dim3(256), 0, s, static_cast<const _Float16*>(a),
+                       static_cast<const _Float16*>(b), static_cast<_Float16*>(y), outer, ia, ib);
+  else
+    hipLaunchKernelGGL(concat_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(a),
+                       static_cast<const float*>(b), static_cast<float*>(y), outer, ia, ib);
 }
 
 }  // namespace ore

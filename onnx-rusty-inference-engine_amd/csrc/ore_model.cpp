@@ -43,6 +43,7 @@ struct Value {
   int64_t alias_ch = 0;            // concat slice: first channel inside the base
   bool slice = false;              // alias is a channel slice of its base (Concat in place)
   int64_t ps = 0;                  // 4-D activations: channel-plane stride (>= H*W; padded planes)
+  int es = 4;                      // element bytes: 4 f32, 2 f16 (f16 models, ORE_LOAD_F16)
   bool elided = false;             // produced and consumed inside one fused kernel
   int64_t arena_off = -1;          // byte offset in the arena (root values)
   int first = -1, last = -1;       // live interval in step indices
@@ -84,6 +85,7 @@ struct ore_model {
   ore_ctx* ctx = nullptr;
   int64_t max_batch = 0;
   int32_t fusion = ORE_FUSE_ALL;
+  bool f16 = false;              // ORE_LOAD_F16: f16 conv/pool activations, f32 accumulation
   std::vector<Value> values;
   std::map<std::string, int> by_name;
   std::vector<Step> base_steps;  // unfused, one per node
@@ -106,6 +108,26 @@ struct ore_model {
 };
 
 namespace {
+
+// IEEE binary16 -> binary32 (exact)
+float half_bits_to_float(uint16_t h) {
+  const uint32_t sign = uint32_t(h & 0x8000) << 16;
+  uint32_t exp = (h >> 10) & 0x1f, man = h & 0x3ff, bits;
+  if (exp == 0x1f) {
+    bits = sign | 0x7f800000u | (man << 13);
+  } else if (exp != 0) {
+    bits = sign | ((exp + 112) << 23) | (man << 13);
+  } else if (man == 0) {
+    bits = sign;
+  } else {  // subnormal: renormalise
+    int e = -1;
+    do { man <<= 1; ++e; } while (!(man & 0x400));
+    bits = sign | (uint32_t(112 - e) << 23) | ((man & 0x3ff) << 13);
+  }
+  float f;
+  std::memcpy(&f, &bits, 4);
+  return f;
+}
 
 ore_status err(ore_model* m, ore_status st, const std::string& msg) {
   return set_error(m->ctx, st, "%s", msg.c_str());
@@ -186,11 +208,13 @@ ore_status build_conv(ore_model* m, const Node& n, Step* s) {
   s->win.Ho = yd[2]; s->win.Wo = yd[3];
   const double P = double(yd[2] * yd[3]);
   s->flops_per_img = 2.0 * double(s->M) * P * double(s->C * s->kh * s->kw);
-  s->bytes_per_img = 4.0 * (double(s->C * s->H * s->W) + double(s->M) * P);
-  s->bytes_fixed = 4.0 * double(Wt.numel_const() + (b >= 0 ? s->M : 0));
+  const int yes = m->f16 ? 2 : 4;
+  s->bytes_per_img = double(X.es) * double(s->C * s->H * s->W) + double(yes) * double(s->M) * P;
+  s->bytes_fixed = double(yes) * double(Wt.numel_const()) + 4.0 * double(b >= 0 ? s->M : 0);
   int y = new_value(m, n.outputs[0]);
   Value& Y = m->values[y];
   Y.ndim = 4; Y.dims[0] = 1; Y.dims[1] = yd[1]; Y.dims[2] = yd[2]; Y.dims[3] = yd[3];
+  Y.es = yes;
   s->out = y;
   return ORE_OK;
 }
@@ -234,10 +258,12 @@ ore_status build_maxpool(ore_model* m, const Node& n, Step* s) {
   s->kh = a.kernel[0]; s->kw = a.kernel[1]; s->sh = a.strides[0]; s->sw = a.strides[1];
   s->win.pt = p[0]; s->win.pl = p[1]; s->win.pb = p[2]; s->win.pr = p[3];
   s->win.Ho = yd[2]; s->win.Wo = yd[3];
-  s->bytes_per_img = 4.0 * double(X.per_image() + s->C * yd[2] * yd[3]);
+  s->bytes_per_img = double(X.es) * double(X.per_image() + s->C * yd[2] * yd[3]);
+  const int xes = X.es;
   int y = new_value(m, n.outputs[0]);
   Value& Y = m->values[y];
   Y.ndim = 4; Y.dims[0] = 1; Y.dims[1] = yd[1]; Y.dims[2] = yd[2]; Y.dims[3] = yd[3];
+  Y.es = xes;
   s->out = y;
   return ORE_OK;
 }
@@ -253,8 +279,9 @@ ore_status build_unary4(ore_model* m, const Node& n, Step* s, StepKind kind) {
   Value& Y = m->values[y];
   Y.ndim = X.ndim;
   for (int i = 0; i < 4; ++i) Y.dims[i] = X.dims[i];
+  Y.es = X.es;
   s->out = y;
-  s->bytes_per_img = 8.0 * double(X.per_image());
+  s->bytes_per_img = 2.0 * X.es * double(X.per_image());
   return ORE_OK;
 }
 
@@ -277,7 +304,8 @@ ore_status build_node(ore_model* m, const Node& n, Step* s) {
     Value& Y = m->values[s->out];
     const Value& X = m->values[s->in0];
     Y.dims[2] = 1; Y.dims[3] = 1;
-    s->bytes_per_img = 4.0 * double(X.per_image() + X.dims[1]);
+    Y.es = 4;  // f32 sums and output either way
+    s->bytes_per_img = double(X.es) * double(X.per_image()) + 4.0 * double(X.dims[1]);
     return ORE_OK;
   }
   if (op == "Softmax") {  // softmax_wrapper flattens to (N, C*H*W), axis 1 (:46-51)
@@ -286,6 +314,7 @@ ore_status build_node(ore_model* m, const Node& n, Step* s) {
     Value& Y = m->values[s->out];
     const Value& X = m->values[s->in0];
     Y.ndim = 2; Y.dims[0] = 1; Y.dims[1] = X.per_image(); Y.dims[2] = Y.dims[3] = 0;
+    if (X.es != 4) return err(m, ORE_ERR_UNSUPPORTED, "Softmax '" + n.name + "': f16 input (f16 models end in f32 after GlobalAveragePool)");
     return ORE_OK;
   }
   if (op == "Concat") {  // concatenate_op.rs:22-32
@@ -303,14 +332,16 @@ ore_status build_node(ore_model* m, const Node& n, Step* s) {
     const Value A = m->values[a], B = m->values[b];
     for (int i = 1; i < 4; ++i)
       if (i != axis && A.dims[i] != B.dims[i]) return err(m, ORE_ERR_INVALID, "Concat '" + n.name + "': shape mismatch");
+    if (A.es != B.es) return err(m, ORE_ERR_UNSUPPORTED, "Concat '" + n.name + "': inputs of different precision");
     s->kind = S_CONCAT; s->in0 = a; s->in1 = b; s->axis = axis;
     int y = new_value(m, n.outputs[0]);
     Value& Y = m->values[y];
     Y.ndim = 4;
     for (int i = 0; i < 4; ++i) Y.dims[i] = A.dims[i];
     Y.dims[axis] = A.dims[axis] + B.dims[axis];
+    Y.es = A.es;
     s->out = y;
-    s->bytes_per_img = 8.0 * double(Y.per_image());
+    s->bytes_per_img = 2.0 * A.es * double(Y.per_image());
     return ORE_OK;
   }
   if (op == "Add") {  // add_op.rs:16-107
@@ -321,6 +352,7 @@ ore_status build_node(ore_model* m, const Node& n, Step* s) {
       return err(m, ORE_ERR_UNSUPPORTED, "Cannot retrieve input 2 for Add operation");
     const Value A = m->values[a], B = m->values[b];
     if (A.is_const) return err(m, ORE_ERR_UNSUPPORTED, "Add '" + n.name + "': constant first input not supported");
+    if (A.es != 4) return err(m, ORE_ERR_UNSUPPORTED, "Add '" + n.name + "': f16 input is not supported (f32 op)");
     if (!((A.ndim == 4 && B.ndim == 3) || (A.ndim == 2 && B.ndim == 2)))
       return err(m, ORE_ERR_UNSUPPORTED, "Add '" + n.name + "': supports 4-D + 3-D or 2-D + 2-D");
     for (int i = 0; i < B.ndim; ++i) {  // right-aligned broadcast; the batch axis of A is 1 here
@@ -369,6 +401,7 @@ ore_status build_node(ore_model* m, const Node& n, Step* s) {
     int y = new_value(m, n.outputs[0]);
     Value& Y = m->values[y];
     Y.ndim = 2; Y.dims[0] = 1; Y.dims[1] = ns[1];
+    Y.es = X.es;
     s->out = y;
     s->bytes_per_img = 8.0 * double(X.per_image());
     return ORE_OK;
@@ -382,6 +415,7 @@ ore_status build_node(ore_model* m, const Node& n, Step* s) {
     if (A.is_const || !B.is_const || !B.cptr)
       return err(m, ORE_ERR_UNSUPPORTED, "MatMul '" + n.name + "': expects activation . constant");
     if (A.dims[1] != B.dims[0]) return err(m, ORE_ERR_INVALID, "MatMul '" + n.name + "': inner dims differ");
+    if (A.es != 4) return err(m, ORE_ERR_UNSUPPORTED, "MatMul '" + n.name + "': f16 input is not supported (f32 op)");
     s->kind = S_MATMUL; s->in0 = a; s->in1 = b;
     s->C = A.dims[1]; s->M = B.dims[1]; s->w_kmajor = true;
     s->win.Ho = 1; s->win.Wo = 1; s->H = 1; s->W = 1; s->kh = 1; s->kw = 1;
@@ -534,7 +568,7 @@ ore_status plan(ore_model* m) {
   int64_t arena = 0;
   for (int id : roots) {
     Value& v = m->values[id];
-    const int64_t size = ((v.image_stride() * m->max_batch * 4) + 255) / 256 * 256;
+    const int64_t size = ((v.image_stride() * m->max_batch * v.es) + 255) / 256 * 256;
     // first fit among the gaps left by placed slots whose lifetimes overlap this one
     std::vector<std::pair<int64_t, int64_t>> busy;
     for (auto& s : placed)
@@ -573,19 +607,54 @@ ore_status plan(ore_model* m) {
 }
 
 // storage of a value for the current run: pointer to image 0 and per-image stride
-struct Ref { float* p; int64_t nstride; int64_t ps; };
+struct Ref { float* p; int64_t nstride; int64_t ps; int es; };  // p: storage of es-byte elements
 
 Ref ref_of(ore_model* m, int id) {
   const Value& v = m->values[id];
-  if (v.is_const) return {v.cptr, 0, 0};
+  if (v.is_const) return {v.cptr, 0, 0, 4};
   if (v.alias_of >= 0) {
     Ref base = ref_of(m, v.alias_of);
-    if (v.slice) return {base.p + v.alias_ch * base.ps, base.nstride, base.ps};
+    if (v.slice)
+      return {reinterpret_cast<float*>(reinterpret_cast<char*>(base.p) + v.alias_ch * base.ps * base.es), base.nstride,
+              base.ps, base.es};
     return base;
   }
-  if (v.is_input) return {const_cast<float*>(m->cur_in), v.image_stride(), v.ps};
-  if (v.is_output && m->out_bound) return {m->cur_out, v.image_stride(), v.ps};
-  return {reinterpret_cast<float*>(m->arena + v.arena_off), v.image_stride(), v.ps};
+  if (v.is_input) return {const_cast<float*>(m->cur_in), v.image_stride(), v.ps, v.es};
+  if (v.is_output && m->out_bound) return {m->cur_out, v.image_stride(), v.ps, v.es};
+  return {reinterpret_cast<float*>(m->arena + v.arena_off), v.image_stride(), v.ps, v.es};
+}
+
+// contiguous steps on f16 values (f16 models): Relu, GAP (f32 out), Concat, Dropout/Reshape copies
+ore_status launch_step_f16(ore_model* m, const Step& s, int64_t n) {
+  ore_ctx* ctx = m->ctx;
+  const Value& X = m->values[s.in0];
+  const Ref x = ref_of(m, s.in0), y = ref_of(m, s.out);
+  if (x.nstride != X.per_image() || (X.ndim == 4 && x.ps && x.ps != X.dims[2] * X.dims[3]))
+    return err(m, ORE_ERR_INVALID, "internal: f16 step on a strided view");
+  const int64_t count = n * X.per_image();
+  if (count == 0) return ORE_OK;
+  switch (s.kind) {
+    case S_RELU: launch_relu_f16(x.p, y.p, count, ctx->stream); break;
+    case S_GAP: launch_gap(x.p, 2, y.p, n * X.dims[1], int(X.dims[2] * X.dims[3]), ctx->stream); break;
+    case S_COPY:
+      if (x.p != y.p)
+        ORE_HIP_CHECK(ctx, hipMemcpyAsync(y.p, x.p, size_t(count) * 2, hipMemcpyDeviceToDevice, ctx->stream));
+      break;
+    case S_CONCAT: {
+      const Value& B = m->values[s.in1];
+      const Ref b = ref_of(m, s.in1);
+      if (b.nstride != B.per_image() || (b.ps && b.ps != B.dims[2] * B.dims[3]))
+        return err(m, ORE_ERR_INVALID, "internal: f16 concat of a strided view");
+      int64_t outer = n, ia = 1, ib = 1;
+      for (int i = 1; i < int(s.axis); ++i) outer *= X.dims[i];
+      for (int i = int(s.axis); i < 4; ++i) { ia *= X.dims[i]; ib *= B.dims[i]; }
+      launch_concat(x.p, b.p, y.p, 2, outer, ia, ib, ctx->stream);
+      break;
+    }
+    default: return err(m, ORE_ERR_UNSUPPORTED, "internal: step '" + s.name + "' has no f16 kernel");
+  }
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
 }
 
 ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
@@ -596,7 +665,7 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       const Ref x = ref_of(m, s.in0);
       const float* bias = s.in2 >= 0 ? m->values[s.in2].cptr : nullptr;
       return run_conv(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, s.wp, s.ktab, s.M, s.kh, s.kw, bias, s.win, s.sh, s.sw, s.relu,
-                      y.p, y.nstride, x.ps, y.ps);
+                      y.p, y.nstride, x.ps, y.ps, x.es);
     }
     case S_MATMUL: {
       const Ref x = ref_of(m, s.in0);
@@ -606,10 +675,11 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
     case S_MAXPOOL: {
       const Ref x = ref_of(m, s.in0);
       return run_maxpool(ctx, x.p, n, s.C, s.H, s.W, x.nstride, s.kh, s.kw, s.win, s.sh, s.sw, y.p, y.nstride, x.ps,
-                         y.ps);
+                         y.ps, x.es);
     }
     default: break;
   }
+  if (m->values[s.in0].es == 2) return launch_step_f16(m, s, n);
   // contiguous ops through the public entry points
   auto as_tensor = [&](int id, int64_t batch) {
     const Value& v = m->values[id];
@@ -645,7 +715,13 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
 extern "C" {
 
 ore_status ore_model_load(ore_ctx* ctx, const void* bytes, size_t len, int64_t max_batch, ore_model** out) {
+  return ore_model_load_ex(ctx, bytes, len, max_batch, 0, out);
+}
+
+ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_t max_batch, int32_t flags,
+                             ore_model** out) {
   if (!ctx || !bytes || !out || max_batch <= 0) return set_error(ctx, ORE_ERR_INVALID, "invalid argument");
+  if (flags & ~ORE_LOAD_F16) return set_error(ctx, ORE_ERR_INVALID, "unknown load flags 0x%x", unsigned(flags));
   ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
   Graph g;
   std::string perr;
@@ -653,6 +729,7 @@ ore_status ore_model_load(ore_ctx* ctx, const void* bytes, size_t len, int64_t m
   ore_model* m = new ore_model();
   m->ctx = ctx;
   m->max_batch = max_batch;
+  m->f16 = (flags & ORE_LOAD_F16) != 0;
   auto fail = [&](ore_status st) {
     ore_model_destroy(m);
     return st;
@@ -718,7 +795,7 @@ ore_status ore_model_load(ore_ctx* ctx, const void* bytes, size_t len, int64_t m
     size_t total_packed = 0;
     for (auto& s : m->base_steps) {
       if (s.kind == S_CONV)
-        s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win);
+        s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, m->f16);
       else if (s.kind == S_MATMUL)
         s.plan = conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win);
       else
@@ -747,6 +824,9 @@ ore_status ore_model_load(ore_ctx* ctx, const void* bytes, size_t len, int64_t m
   if (m->output_value < 0 || m->values[m->output_value].is_const)
     return fail(set_error(ctx, ORE_ERR_INVALID, "graph output '%s' is not produced", g.outputs[0].name.c_str()));
   m->values[m->output_value].is_output = true;
+  if (m->values[m->output_value].es != 4)
+    return fail(set_error(ctx, ORE_ERR_UNSUPPORTED, "f16 model: graph output '%s' must be f32 (end with GlobalAveragePool / Softmax)",
+                          g.outputs[0].name.c_str()));
   if (ore_status st = plan(m)) { std::string e = ctx->err; ore_model_destroy(m); return set_error(ctx, st, "%s", e.c_str()); }
   *out = m;
   return ORE_OK;
@@ -846,6 +926,24 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
   const Ref r = ref_of(m, id);
   if (!r.p) return set_error(ctx, ORE_ERR_INVALID, "value '%s' has no f32 storage", name);
   const int64_t ns = v.is_const ? pe : r.nstride;
+  if (r.es == 2) {  // f16 storage: download the halves (padded planes included), convert on the host
+    const bool padded = v.ndim == 4 && r.ps && r.ps != v.dims[2] * v.dims[3];
+    const int64_t rows = padded ? n * v.dims[1] : n;
+    const int64_t row_elems = padded ? v.dims[2] * v.dims[3] : pe;
+    const int64_t pitch = padded ? r.ps : ns;
+    std::vector<uint16_t> tmp(size_t(rows * row_elems));
+    if (padded) {
+      for (int64_t i = 0; i < n; ++i)
+        ORE_HIP_CHECK(ctx, hipMemcpy2D(tmp.data() + i * pe, size_t(row_elems) * 2,
+                                       reinterpret_cast<const char*>(r.p) + i * ns * 2, size_t(pitch) * 2,
+                                       size_t(row_elems) * 2, size_t(v.dims[1]), hipMemcpyDeviceToHost));
+    } else {
+      ORE_HIP_CHECK(ctx, hipMemcpy2D(tmp.data(), size_t(pe) * 2, r.p, size_t(pitch) * 2, size_t(pe) * 2, size_t(n),
+                                     hipMemcpyDeviceToHost));
+    }
+    for (size_t i = 0; i < tmp.size(); ++i) host_dst[i] = half_bits_to_float(tmp[i]);
+    return ORE_OK;
+  }
   if (!v.is_const && v.ndim == 4 && r.ps && r.ps != v.dims[2] * v.dims[3]) {  // padded planes
     const int64_t P = v.dims[2] * v.dims[3];
     for (int64_t i = 0; i < n; ++i)

@@ -98,9 +98,9 @@ static bool contiguous(const ore_tensor* t) {
 static bool fits_i32(int64_t v) { return v >= 0 && v < (int64_t(1) << 31); }
 
 ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
-                   const Window& win) {
+                   const Window& win, bool f16) {
   return plan_conv(int(M), int(C), int(H), int(W), int(kh), int(kw), int(sh), int(sw), int(win.pt), int(win.pl),
-                   int(win.Ho), int(win.Wo), kh == 1 && kw == 1);
+                   int(win.Ho), int(win.Wo), kh == 1 && kw == 1, f16);
 }
 
 size_t packed_bytes(const ConvPlan& pln) {
@@ -140,8 +140,9 @@ float* pack_to_scratch(ore_ctx* ctx, const ConvPlan& pln, const float* w, bool k
 ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
                     int64_t x_nstride, const float* wp, const int2* ktab, int64_t M, int64_t kh, int64_t kw,
                     const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, float* y,
-                    int64_t y_nstride, int64_t x_ps, int64_t y_ps) {
+                    int64_t y_nstride, int64_t x_ps, int64_t y_ps, int x_es) {
   if (N == 0) return ORE_OK;
+  if (!pln.f16 && x_es != 4) return set_error(ctx, ORE_ERR_INVALID, "internal: f32 conv on f16 input");
   if (x_ps == 0) x_ps = H * W;
   if (y_ps == 0) y_ps = win.Ho * win.Wo;
   ConvParams p{};
@@ -159,6 +160,7 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
   p.y_nstride = y_nstride;
   p.relu = relu ? 1 : 0;
   p.Mp = pln.Mp;
+  p.x_f32 = x_es == 4 ? 1 : 0;
   p.vec_out = (y_ps % 4 == 0 && y_nstride % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
   if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;  // tuning knob
   p.is1x1 = (kh == 1 && kw == 1 && sh == 1 && sw == 1 && win.pt == 0 && win.pl == 0 && win.Ho == H && win.Wo == W &&
@@ -175,9 +177,10 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
 
 ore_status run_maxpool(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
                        int64_t x_nstride, int64_t kh, int64_t kw, const Window& win, int64_t sh, int64_t sw,
-                       float* y, int64_t y_nstride, int64_t x_ps, int64_t y_ps) {
+                       float* y, int64_t y_nstride, int64_t x_ps, int64_t y_ps, int es) {
   if (N == 0) return ORE_OK;
   PoolParams p{};
+  p.es = es;
   p.x_ps = int(x_ps ? x_ps : H * W);
   p.y_ps = int(y_ps ? y_ps : win.Ho * win.Wo);
   p.x = x; p.y = y;
@@ -423,7 +426,7 @@ ore_status ore_gap_f32(ore_ctx* ctx, const ore_tensor* x, ore_tensor* y) {
     return set_error(ctx, ORE_ERR_INVALID, "GlobalAveragePool expects contiguous [N,C,H,W] -> [N,C,1,1]");
   const int64_t HW = x->dims[2] * x->dims[3];
   if (HW <= 0 || HW >= (int64_t(1) << 31)) return set_error(ctx, ORE_ERR_INVALID, "GAP spatial size");
-  launch_gap(x->data, y->data, x->dims[0] * x->dims[1], int(HW), ctx->stream);
+  launch_gap(x->data, 4, y->data, x->dims[0] * x->dims[1], int(HW), ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());
   return ORE_OK;
 }
@@ -443,7 +446,7 @@ ore_status ore_concat_f32(ore_ctx* ctx, const ore_tensor* a, const ore_tensor* b
   for (int i = 0; i < axis; ++i) outer *= a->dims[i];
   for (int i = int(axis); i < 4; ++i) { ia *= a->dims[i]; ib *= b->dims[i]; }
   if (outer * (ia + ib) == 0) return ORE_OK;
-  launch_concat(a->data, b->data, y->data, outer, ia, ib, ctx->stream);
+  launch_concat(a->data, b->data, y->data, 4, outer, ia, ib, ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());
   return ORE_OK;
 }

@@ -17,6 +17,7 @@ STATUS_NAMES = {0: "ORE_OK", 1: "ORE_ERR_INVALID", 2: "ORE_ERR_UNSUPPORTED", 3: 
                 4: "ORE_ERR_OOM", 5: "ORE_ERR_PARSE"}
 
 FUSE_CONV_RELU, FUSE_CONCAT, FUSE_ALIAS, FUSE_ALL, KEEP_VALUES = 1, 2, 4, 7, 8
+LOAD_F16 = 1  # ore_model_load_ex flag: the fp16 variant
 PAD = {"NOTSET": 0, "NOT_SET": 0, "SAME_UPPER": 1, "SAME_LOWER": 2, "VALID": 3}
 
 # every symbol include/ore.h declares (checked by tests/test_abi.py on CPU)
@@ -25,7 +26,7 @@ EXPORTED = [
     "ore_sync", "ore_last_error", "ore_malloc", "ore_free", "ore_upload", "ore_download",
     "ore_conv_out_shape", "ore_pool_out_shape", "ore_conv2d_f32", "ore_maxpool2d_f32", "ore_relu_f32",
     "ore_add_f32", "ore_softmax_f32", "ore_matmul_f32", "ore_gap_f32", "ore_concat_f32", "ore_dropout_f32",
-    "ore_reshape", "ore_model_load", "ore_model_destroy", "ore_model_set_fusion", "ore_model_input_dims",
+    "ore_reshape", "ore_model_load", "ore_model_load_ex", "ore_model_destroy", "ore_model_set_fusion", "ore_model_input_dims",
     "ore_model_output_elems", "ore_model_run", "ore_model_read_value", "ore_model_enable_timing",
     "ore_model_step_count", "ore_model_step_info", "ore_model_step_times",
 ]
@@ -92,6 +93,7 @@ def load():
         "ore_dropout_f32": (i32, [vp, T, T]),
         "ore_reshape": (i32, [T, I64P, i32, T]),
         "ore_model_load": (i32, [vp, ctypes.c_char_p, ctypes.c_size_t, i64, ctypes.POINTER(vp)]),
+        "ore_model_load_ex": (i32, [vp, ctypes.c_char_p, ctypes.c_size_t, i64, i32, ctypes.POINTER(vp)]),
         "ore_model_destroy": (i32, [vp]),
         "ore_model_set_fusion": (i32, [vp, i32]),
         "ore_model_input_dims": (i32, [vp, I64P]),

@@ -16,7 +16,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import ConvAttrs, OreError, PoolAttrs, Tensor, check, load
+from ._lib import LOAD_F16, ConvAttrs, OreError, PoolAttrs, Tensor, check, load
 
 __all__ = ["Context", "Model", "OreError", "convolution", "max_pool", "relu", "add", "softmax", "mul",
            "global_average_pool", "concatenation", "drop_out", "reshape", "inference", "conv_out_shape",
@@ -217,10 +217,16 @@ def reshape(x, shape: Sequence[int]):
 class Model:
     """ore_model: the device-resident walker over one ONNX graph."""
 
-    def __init__(self, ctx: Context, onnx_bytes: bytes, max_batch: int):
+    def __init__(self, ctx: Context, onnx_bytes: bytes, max_batch: int, precision: str = "f32"):
+        """precision "f16": the fp16 variant (ORE_LOAD_F16, include/ore.h); input/output stay f32."""
+        if precision not in ("f32", "f16"):
+            raise OreError(1, f"precision must be 'f32' or 'f16', not {precision!r}")
         self.ctx = ctx
+        self.precision = precision
         h = ctypes.c_void_p()
-        check(load().ore_model_load(ctx.h, onnx_bytes, len(onnx_bytes), int(max_batch), ctypes.byref(h)), ctx.h)
+        flags = LOAD_F16 if precision == "f16" else 0
+        check(load().ore_model_load_ex(ctx.h, onnx_bytes, len(onnx_bytes), int(max_batch), flags, ctypes.byref(h)),
+              ctx.h)
         self.h = h
         self.max_batch = max_batch
         d = (ctypes.c_int64 * 4)()

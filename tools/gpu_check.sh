@@ -2,7 +2,7 @@
 # One GPU-box pass: smoke, GPU parity tests, a short bench, a rocprofv3 kernel-trace summary.
 # Every GPU step has its own time limit; a crash/abort/timeout ends the script (no retries).
 # Usage (from the repo root on the box): bash tools/gpu_check.sh [tag] [stages...]
-# stages: smoke tests bench prof (default: all)
+# stages: smoke tests bench bench16 prof (default: smoke tests bench prof)
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd "$ROOT"
@@ -27,6 +27,11 @@ fi
 if has bench; then
   timeout -k 10 600 python3 bench.py > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"
   rc=$?; echo "bench rc=$rc"; cat "$OUT/bench_$TAG.json"; tail -5 "$OUT/bench_$TAG.err"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+fi
+if has bench16; then
+  timeout -k 10 600 python3 bench.py --precision f16 --no-cpu-baseline > "$OUT/bench16_$TAG.json" 2> "$OUT/bench16_$TAG.err"
+  rc=$?; echo "bench16 rc=$rc"; cat "$OUT/bench16_$TAG.json"; tail -5 "$OUT/bench16_$TAG.err"
   if [ $rc -ne 0 ]; then exit $rc; fi
 fi
 if has prof; then
