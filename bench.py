@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-step-timing", action="store_true", help="no per-kernel HIP events in the timed loop")
     ap.add_argument("--layers", action="store_true", help="print per-kernel-step times to stderr")
+    ap.add_argument("--no-b1", action="store_true", help="skip the batch-1 latency probe")
     ap.add_argument("--precision", choices=["f32", "f16"], default="f32",
                     help="f16: the fp16 variant (SURVEY.md §8(f)3, config 5); the headline metric is f32")
     return ap.parse_args()
@@ -71,6 +72,38 @@ def cpu_baseline(model_bytes, hw, threads):
             "sample": f"{threads} SqueezeNet-1.0 224x224 images, one batch-1 inference() per thread, "
                       f"reference cost structure (oracle faithful mode); single-image latency "
                       f"{float(np.median(done)):.2f} s"}
+
+
+def b1_latency(model_bytes, hw, local, precision, iters=200):
+    """Batch-1 latency (SURVEY.md §8(d) B = 1 config): one image per synchronous call, issued
+    as plain launches, as one HIP-graph replay, and as a graph with the fire modules' expand
+    branches on two streams (ore_model_set_streams).  Milliseconds per image."""
+    import torch
+    import ore
+    s = torch.cuda.Stream(device=f"cuda:{local}")
+    ctx = ore.Context(local, use_torch_stream=False)
+    ctx.set_stream(s.cuda_stream)
+    x = (torch.rand((1, 3, hw, hw), device=f"cuda:{local}") * 100.0 - 50.0).contiguous()
+    res = {}
+    for label, streams, graph in (("plain_ms", 1, False), ("graph_ms", 1, True), ("graph_2streams_ms", 2, True)):
+        m = ore.Model(ctx, model_bytes, max_batch=1, precision=precision)
+        m.set_streams(streams)
+        out = torch.empty((1, m.output_elems), device=f"cuda:{local}")
+        torch.cuda.synchronize()
+        if graph:
+            m.capture(x, out)
+        call = m.replay if graph else (lambda: m.run_into(x, out))
+        for _ in range(10):
+            call()
+        s.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            call()
+            s.synchronize()
+        res[label] = round(1000.0 * (time.perf_counter() - t0) / iters, 4)
+        m.close()
+    ctx.close()
+    return res
 
 
 def main():
@@ -188,6 +221,8 @@ def main():
             result["max_abs_sample"] = "2 images of the timed batch vs oracle (C restatement of the reference, f32)"
             if f16:
                 result["top1_agrees_with_cpu"] = bool((out[:2].cpu().numpy().argmax(1) == ref.argmax(1)).all())
+            if not args.no_b1:
+                result["b1_latency_ms"] = b1_latency(model_bytes, args.hw, local, args.precision)
             if not args.no_cpu_baseline:
                 threads = args.cpu_threads or min(16, os.cpu_count() or 1)
                 result["cpu_baseline"] = cpu_baseline(model_bytes, args.hw, threads)

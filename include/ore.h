@@ -174,6 +174,17 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
                                 int64_t dims[4], int32_t* ndim);
 /* Per-node timing with HIP events on the context stream (enable, run, then query).
  * ore_model_node_count/ore_model_node_info describe the executed kernel steps. */
+/* Branch concurrency (the reference runs the two expand branches of a fire
+ * module on threads, multithreading.rs:20-62): with 2 streams, adjacent independent steps (no
+ * data dependence, no overlapping storage) run on a side stream beside the main one, joined by
+ * events.  Pays off at small batch, where one conv does not fill the GPU.  Default 1. */
+ore_status ore_model_set_streams(ore_model* m, int32_t streams);
+/* Capture one ore_model_run(d_input, n, d_output) into a HIP graph (launch-bound small batches:
+ * one graph launch replaces ~30 kernel launches); replay it with ore_model_graph_launch on the
+ * context stream.  The graph keeps the buffers and batch it was captured with; re-capture after
+ * ore_model_set_fusion / set_streams.  Needs a non-null context stream. */
+ore_status ore_model_graph_capture(ore_model* m, const float* d_input, int64_t n, float* d_output);
+ore_status ore_model_graph_launch(ore_model* m);
 ore_status ore_model_enable_timing(ore_model* m, int32_t on);
 int32_t ore_model_step_count(ore_model* m);
 ore_status ore_model_step_info(ore_model* m, int32_t i, const char** op, const char** name, double* flops,

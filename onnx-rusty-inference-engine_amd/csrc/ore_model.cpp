@@ -99,6 +99,16 @@ struct ore_model {
   // timing
   bool timing = false;
   std::vector<hipEvent_t> events;
+  // branch concurrency (ore_model_set_streams): exec_steps[k] with pair_next[k] runs on the side
+  // stream beside exec_steps[k + 1] (the two expand convs of a fire module: the reference's
+  // branch threads, multithreading.rs:20-62)
+  int streams = 1;
+  std::vector<char> pair_next;
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // captured run (ore_model_graph_capture)
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t graph_exec = nullptr;
   std::vector<int> exec_steps;   // indices into steps of launched (non-NOP) steps
   // run-time binding
   const float* cur_in = nullptr;
@@ -594,6 +604,43 @@ ore_status plan(ore_model* m) {
   m->exec_steps.clear();
   for (int i = 0; i < nsteps; ++i)
     if (m->steps[i].kind != S_NOP) m->exec_steps.push_back(i);
+  // independent neighbours: B reads nothing A writes, and no byte range A or B writes overlaps
+  // one the other reads or writes (arena slots are shared by liveness, so check the memory)
+  m->pair_next.assign(m->exec_steps.size(), 0);
+  {
+    auto span = [&](int id, int64_t* lo, int64_t* hi) {  // arena byte range of a value's root
+      const int r = root(id);
+      const Value& v = m->values[r];
+      if (v.is_const || v.arena_off < 0) return false;
+      *lo = v.arena_off;
+      *hi = v.arena_off + v.image_stride() * m->max_batch * v.es;
+      return true;
+    };
+    auto overlap = [&](int a, int b) {
+      if (a < 0 || b < 0) return false;
+      if (m->values[a].is_const || m->values[b].is_const) return false;
+      const int ra = root(a), rb = root(b);
+      if (m->values[ra].is_input || m->values[rb].is_input) return false;  // never written
+      if (ra == rb) {  // channel slices of one buffer: disjoint unless the same slice
+        const Value &va = m->values[a], &vb = m->values[b];
+        if (va.slice && vb.slice) return va.alias_ch < vb.alias_ch + vb.dims[1] && vb.alias_ch < va.alias_ch + va.dims[1];
+        return true;
+      }
+      if (m->values[ra].is_output || m->values[rb].is_output) return true;  // conservative (may live in the arena)
+      int64_t a0, a1, b0, b1;
+      if (!span(a, &a0, &a1) || !span(b, &b0, &b1)) return false;
+      return a0 < b1 && b0 < a1;
+    };
+    for (size_t k = 0; k + 1 < m->exec_steps.size(); ++k) {
+      if (k > 0 && m->pair_next[k - 1]) continue;  // pairs only
+      const Step &A = m->steps[m->exec_steps[k]], &B = m->steps[m->exec_steps[k + 1]];
+      bool ok = A.out >= 0 && B.out >= 0;
+      for (int bi : {B.in0, B.in1, B.in2}) ok = ok && !overlap(bi, A.out);
+      for (int ai : {A.in0, A.in1, A.in2}) ok = ok && !overlap(ai, B.out);
+      ok = ok && !overlap(A.out, B.out);
+      m->pair_next[k] = ok ? 1 : 0;
+    }
+  }
   // gather tables depend on the input's plane stride
   for (const Step& st : m->steps) {
     if (st.kind != S_CONV || !st.ktab) continue;
@@ -837,6 +884,11 @@ ore_status ore_model_destroy(ore_model* m) {
   (void)hipSetDevice(m->ctx->device);
   (void)hipStreamSynchronize(m->ctx->stream);
   for (auto e : m->events) (void)hipEventDestroy(e);
+  if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
+  if (m->graph) (void)hipGraphDestroy(m->graph);
+  if (m->side) (void)hipStreamDestroy(m->side);
+  if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
+  if (m->ev_join) (void)hipEventDestroy(m->ev_join);
   if (m->arena) (void)hipFree(m->arena);
   if (m->consts) (void)hipFree(m->consts);
   if (m->packed) (void)hipFree(m->packed);
@@ -878,8 +930,30 @@ ore_status ore_model_run(ore_model* m, const float* d_input, int64_t n, float* d
     m->events.assign(m->exec_steps.size() + 1, nullptr);
     for (auto& e : m->events) ORE_HIP_CHECK(ctx, hipEventCreate(&e));
   }
+  const bool branches = m->streams > 1 && !m->timing;
+  if (branches && !m->side) {
+    ORE_HIP_CHECK(ctx, hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking));
+    ORE_HIP_CHECK(ctx, hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
+    ORE_HIP_CHECK(ctx, hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming));
+  }
   for (size_t k = 0; k < m->exec_steps.size(); ++k) {
     if (m->timing) ORE_HIP_CHECK(ctx, hipEventRecord(m->events[k], ctx->stream));
+    if (branches && m->pair_next[k]) {
+      // fork: step k on the side stream, step k + 1 on the main stream, then join
+      ORE_HIP_CHECK(ctx, hipEventRecord(m->ev_fork, ctx->stream));
+      ORE_HIP_CHECK(ctx, hipStreamWaitEvent(m->side, m->ev_fork, 0));
+      hipStream_t main = ctx->stream;
+      ctx->stream = m->side;
+      ore_status st = launch_step(m, m->steps[m->exec_steps[k]], n);
+      ctx->stream = main;
+      if (st) return st;
+      ORE_HIP_CHECK(ctx, hipEventRecord(m->ev_join, m->side));
+      st = launch_step(m, m->steps[m->exec_steps[k + 1]], n);
+      if (st) return st;
+      ORE_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->stream, m->ev_join, 0));
+      ++k;
+      continue;
+    }
     ore_status st = launch_step(m, m->steps[m->exec_steps[k]], n);
     if (st) return st;
   }
@@ -953,6 +1027,46 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
   }
   ORE_HIP_CHECK(ctx, hipMemcpy2D(host_dst, size_t(pe) * 4, r.p, size_t(ns) * 4, size_t(pe) * 4, size_t(n),
                                  hipMemcpyDeviceToHost));
+  return ORE_OK;
+}
+
+ore_status ore_model_set_streams(ore_model* m, int32_t streams) {
+  if (!m || streams < 1 || streams > 2) return set_error(m ? m->ctx : nullptr, ORE_ERR_INVALID, "streams must be 1 or 2");
+  m->streams = streams;
+  return ORE_OK;
+}
+
+ore_status ore_model_graph_capture(ore_model* m, const float* d_input, int64_t n, float* d_output) {
+  if (!m || !d_input || !d_output) return set_error(m ? m->ctx : nullptr, ORE_ERR_INVALID, "null argument");
+  ore_ctx* ctx = m->ctx;
+  if (m->timing) return set_error(ctx, ORE_ERR_INVALID, "disable step timing before capturing a graph");
+  if (!ctx->stream) return set_error(ctx, ORE_ERR_INVALID, "graph capture needs a non-null context stream");
+  ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+  if (m->graph_exec) { (void)hipGraphExecDestroy(m->graph_exec); m->graph_exec = nullptr; }
+  if (m->graph) { (void)hipGraphDestroy(m->graph); m->graph = nullptr; }
+  if (m->streams > 1 && !m->side) {  // created outside the capture
+    ORE_HIP_CHECK(ctx, hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking));
+    ORE_HIP_CHECK(ctx, hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
+    ORE_HIP_CHECK(ctx, hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming));
+  }
+  ORE_HIP_CHECK(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+  ore_status st = ore_model_run(m, d_input, n, d_output);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+  if (st) {
+    if (g) (void)hipGraphDestroy(g);
+    return st;
+  }
+  if (e != hipSuccess) return set_error(ctx, ORE_ERR_HIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
+  m->graph = g;
+  ORE_HIP_CHECK(ctx, hipGraphInstantiate(&m->graph_exec, m->graph, nullptr, nullptr, 0));
+  return ORE_OK;
+}
+
+ore_status ore_model_graph_launch(ore_model* m) {
+  if (!m) return set_error(nullptr, ORE_ERR_INVALID, "null model");
+  if (!m->graph_exec) return set_error(m->ctx, ORE_ERR_INVALID, "no captured graph (ore_model_graph_capture)");
+  ORE_HIP_CHECK(m->ctx, hipGraphLaunch(m->graph_exec, m->ctx->stream));
   return ORE_OK;
 }
 

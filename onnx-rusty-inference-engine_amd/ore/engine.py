@@ -265,6 +265,27 @@ class Model:
                                           dims, ctypes.byref(nd)), self.ctx.h)
         return buf
 
+    def set_streams(self, streams: int):
+        """2: run independent neighbouring steps (the fire modules' expand branches) on a side
+        stream (ore_model_set_streams)."""
+        check(load().ore_model_set_streams(self.h, int(streams)), self.ctx.h)
+
+    def capture(self, x, out):
+        """Capture run_into(x, out) as a HIP graph on the context stream (ore_model_graph_capture);
+        replay() re-runs it on whatever x / out hold then."""
+        n = x.shape[0]
+        if tuple(x.shape[1:]) != self.input_dims or not (x.is_contiguous() and out.is_contiguous()) \
+                or out.numel() < n * self.output_elems:
+            raise OreError(1, "bad input/output buffers")
+        self._graph_bufs = (x, out)  # the graph holds these pointers
+        check(load().ore_model_graph_capture(self.h, ctypes.c_void_p(x.data_ptr()), int(n),
+                                             ctypes.c_void_p(out.data_ptr())), self.ctx.h)
+        return out
+
+    def replay(self):
+        check(load().ore_model_graph_launch(self.h), self.ctx.h)
+        return self._graph_bufs[1]
+
     def enable_timing(self, on: bool = True):
         check(load().ore_model_enable_timing(self.h, 1 if on else 0), self.ctx.h)
 
