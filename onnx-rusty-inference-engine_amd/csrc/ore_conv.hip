@@ -24,17 +24,23 @@ namespace ore {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));  // first-class vector (no struct copies)
 
+#ifdef ORE_EXP_BFIXED  // timing experiment: B loads without the gather index math
+#define ORE_EXP_BFIXED_HOOK ok = bn_ok; off = (xoff > 0 ? xoff : 0) + ((k >> 4) & 1) * XPS;  /* channel 0/1, clamped: in bounds */
+#else
+#define ORE_EXP_BFIXED_HOOK
+#endif
 #ifdef ORE_EXP_SETPRIO  // timing experiment: raise wave priority around MFMA clusters
 #define ORE_PRIO(X) __builtin_amdgcn_s_setprio(X)
 #else
 #define ORE_PRIO(X)
 #endif
 
-enum { B1X1 = 0, BGATHER = 1, BGATHER_LDS = 2 };  // BGATHER_LDS: whole gather table in LDS
+enum { B1X1 = 0, BGATHER = 1 };
 
-constexpr int KTAB_LDS = 1024;  // gather-table entries staged in LDS (larger K reads it from global)
-
-template <int BM, int BN, int WM, int WN, int BK, int BMODE>
+// DMA: the B tile goes global -> LDS by buffer_load ... lds (no VGPR staging, no LDS store
+// pass); a tap outside the image gets an out-of-range offset, which the buffer bounds check
+// turns into a 0 -- the reference's zero padding -- with no select.
+template <int BM, int BN, int WM, int WN, int BK, int BMODE, int DMA>
 __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 32, FN = TN / 32;
@@ -53,7 +59,6 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
   float(*As)[BK][AS] = reinterpret_cast<float(*)[BK][AS]>(smem);
   float(*Bs)[BK][BN] = reinterpret_cast<float(*)[BK][BN]>(smem + 2 * BK * AS);
   __shared__ float sbias[BM];
-  __shared__ int2 ktab_s[BMODE == BGATHER_LDS ? KTAB_LDS : 1];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -76,9 +81,6 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
   const int YPS = p.y_ps;  // channel-plane stride of y = columns iterated per image (>= Ho*Wo)
 
   for (int i = tid; i < BM; i += 256) sbias[i] = (p.bias && m0 + i < p.M) ? p.bias[m0 + i] : 0.0f;
-  const int Kp = (K + 31) & ~31;
-  if (BMODE == BGATHER_LDS)
-    for (int i = tid; i < Kp; i += 256) ktab_s[i] = p.ktab[i];
   __syncthreads();
 
   // ---- this thread's B column (Ntot < 2^31 is checked on the host)
@@ -105,6 +107,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
   }
   const float* __restrict__ x = p.x;
   const float* __restrict__ wp = p.wp;
+  // DMA: buffer resource over x's valid extent (bytes < 2^32, checked on the host); each wave
+  // writes 64 consecutive columns of one B row
+  const __amdgpu_buffer_rsrc_t xrsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
+  const int wcol0 = bcol & ~63;
   // the gather table through the constant address space: k is wave-uniform, so the entries
   // come in by scalar loads (s_load) into SGPRs instead of LDS / vector round trips
   typedef const __attribute__((address_space(4))) long long* ktab_cptr;  // int2 {x, y} as one 64-bit word
@@ -113,7 +120,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
 
   // Branch-free loads: every lane loads (masked lanes from x[0]) and selects 0 afterwards, so
   // the whole tile's loads issue back to back.
-#define ORE_LOAD_TILE(RA, RB, ROK, K0)                                                               \
+#define ORE_LOAD_TILE(RA, RB, ROK, K0, DBUF)                                                         \
   {                                                                                                  \
     const int k0_ = (K0);                                                                            \
     _Pragma("unroll") for (int v_ = 0; v_ < AVEC; ++v_) {                                            \
@@ -130,20 +137,21 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
         ok = bn_ok & (k < K);                                                                        \
         off = xoff + k * XPS;                                                                        \
       } else {                                                                                       \
-        int2 e;                                                                                      \
-        if (BMODE == BGATHER_LDS) {                                                                  \
-          e = ktab_s[k];                                                                             \
-        } else {                                                                                     \
-          const long long w_ = ktab[k];                                                              \
-          e.x = (int)w_;                                                                             \
-          e.y = (int)(w_ >> 32);                                                                     \
-        }                                                                                            \
-        const int r = e.y >> 16, s = e.y & 0xffff;                                                   \
+        const long long w_ = ktab[k];                                                                \
+        const int ex_ = (int)w_, ey_ = (int)(w_ >> 32);                                              \
+        const int r = ey_ >> 16, s = ey_ & 0xffff;                                                   \
         ok = bn_ok & ((unsigned)(ih0 + r) < (unsigned)p.H) & ((unsigned)(iw0 + s) < (unsigned)p.W);  \
-        off = xoff + e.x;                                                                            \
+        off = xoff + ex_;                                                                            \
       }                                                                                              \
-      RB[j] = x[(unsigned)(ok ? off : 0)];                                                           \
-      ROK[j] = ok;  /* the zero select happens at the LDS store, after the MFMAs */                  \
+      ORE_EXP_BFIXED_HOOK                                                                            \
+      if (DMA) {                                                                                     \
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                    \
+            xrsrc, (__attribute__((address_space(3))) void*)&Bs[(DBUF)][krow + j * BROWS][wcol0], 4,  \
+            ok ? off * 4 : (int)0x80000000, 0, 0, 0);                                                \
+      } else {                                                                                       \
+        RB[j] = x[(unsigned)(ok ? off : 0)];                                                         \
+        ROK[j] = ok; /* the zero select happens at the LDS store, after the MFMAs */                 \
+      }                                                                                              \
     }                                                                                                \
   }
 #define ORE_STORE_TILE(RA, RB, ROK, BUF)                                                             \
@@ -153,8 +161,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
       const int kk = e_ / (BM / 4), mm = (e_ % (BM / 4)) * 4;                                        \
       if (AF4 % 256 == 0 || e_ < AF4) *reinterpret_cast<floatx4*>(&As[BUF][kk][mm]) = RA[v_];        \
     }                                                                                                \
-    _Pragma("unroll") for (int j = 0; j < BLOADS; ++j)                                               \
-      Bs[BUF][krow + j * BROWS][bcol] = ROK[j] ? RB[j] : 0.0f;                                       \
+    if (!DMA)                                                                                        \
+      _Pragma("unroll") for (int j = 0; j < BLOADS; ++j)                                             \
+        Bs[BUF][krow + j * BROWS][bcol] = ROK[j] ? RB[j] : 0.0f;                                     \
   }
 
   floatx16 acc[FM][FN];
@@ -170,9 +179,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
     floatx4 ra[AVEC];
     float rb[BLOADS];
     bool rok[BLOADS];
-    ORE_LOAD_TILE(ra, rb, rok, 0);
+    ORE_LOAD_TILE(ra, rb, rok, 0, 0);
     ORE_STORE_TILE(ra, rb, rok, 0);
   }
+  if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the B tile has landed in LDS
   __syncthreads();
   const int lrow = lane >> 5, lcol = lane & 31;
 // fragments for k-step kk+2 are read from LDS before the MFMAs of k-step kk are issued
@@ -203,7 +213,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
     floatx4 ra[AVEC];
     float rb[BLOADS];
     bool rok[BLOADS];
-    ORE_LOAD_TILE(ra, rb, rok, (t + 1) * BK);
+    ORE_LOAD_TILE(ra, rb, rok, (t + 1) * BK, buf ^ 1);
     __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
     ORE_COMPUTE_TILE(buf);
     ORE_STORE_TILE(ra, rb, rok, buf ^ 1);
@@ -211,6 +221,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
     ORE_COMPUTE_TILE(0);
 #endif
 #ifndef ORE_EXP_NOSYNC
+    if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 #endif
   }
@@ -619,18 +630,25 @@ static int env_int(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
-template <int BM, int BN, int WM, int WN, int BK>
+template <int BM, int BN, int WM, int WN>
 static void launch_conv_cfg(const ConvParams& p0, hipStream_t s) {
+  constexpr int BK = 16;
   ConvParams p = p0;
   p.mtiles = (p.M + BM - 1) / BM;
   p.ntiles = (int)((p.Ntot + BN - 1) / BN);
   dim3 grid(p.mtiles * p.ntiles), block(256);
-  if (p.is1x1)
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, B1X1>), grid, block, 0, s, p);
-  else if (conv_packed_kp(p.K) <= KTAB_LDS && env_int("ORE_KTAB_LDS", 0))
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BGATHER_LDS>), grid, block, 0, s, p);
-  else
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BGATHER>), grid, block, 0, s, p);
+  const bool dma = p.x_bytes > 0 && env_int("ORE_CONV_DMA", 1) != 0;  // tuning knob
+  if (p.is1x1) {
+    if (dma)
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, B1X1, 1>), grid, block, 0, s, p);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, B1X1, 0>), grid, block, 0, s, p);
+  } else {
+    if (dma)
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BGATHER, 1>), grid, block, 0, s, p);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BGATHER, 0>), grid, block, 0, s, p);
+  }
 }
 
 // Block tiles, chosen per layer to minimise the padded output channels (MFMA work on rows
@@ -767,12 +785,11 @@ void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
     }
     return;
   }
-  const bool bk32 = env_int("ORE_CONV_BK", 16) == 32;  // tuning knob
   switch (pln.cfg) {
-    case 0: if (bk32) launch_conv_cfg<128, 128, 2, 2, 32>(p, s); else launch_conv_cfg<128, 128, 2, 2, 16>(p, s); break;
-    case 1: if (bk32) launch_conv_cfg<96, 128, 1, 4, 32>(p, s); else launch_conv_cfg<96, 128, 1, 4, 16>(p, s); break;
-    case 2: if (bk32) launch_conv_cfg<64, 128, 2, 2, 32>(p, s); else launch_conv_cfg<64, 128, 2, 2, 16>(p, s); break;
-    default: if (bk32) launch_conv_cfg<32, 256, 1, 4, 32>(p, s); else launch_conv_cfg<32, 256, 1, 4, 16>(p, s); break;
+    case 0: launch_conv_cfg<128, 128, 2, 2>(p, s); break;
+    case 1: launch_conv_cfg<96, 128, 1, 4>(p, s); break;
+    case 2: launch_conv_cfg<64, 128, 2, 2>(p, s); break;
+    default: launch_conv_cfg<32, 256, 1, 4>(p, s); break;
   }
 }
 

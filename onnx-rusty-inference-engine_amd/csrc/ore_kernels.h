@@ -26,6 +26,7 @@ struct ConvParams {
   int mtiles, ntiles;  // filled by the launcher
   int vec_out;         // 16-B epilogue stores (y_ps, y_nstride % 4 == 0 and a 16-B aligned y)
   int x_f32;           // f16 kernel: the input is f32 (rounded to f16 while staging)
+  long long x_bytes;   // bytes from x to the end of its last valid element (0: no buffer DMA path)
   // window-staged kernel (filled by the launcher from the ConvPlan)
   int bch, ks, nst, wr, ww, tiles_per_img;
 };

@@ -161,6 +161,10 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
   p.relu = relu ? 1 : 0;
   p.Mp = pln.Mp;
   p.x_f32 = x_es == 4 ? 1 : 0;
+  {  // extent of x for the B-tile DMA path's buffer resource (32-bit byte offsets)
+    const int64_t extent = ((N - 1) * x_nstride + C * x_ps) * int64_t(x_es);
+    p.x_bytes = (extent > 0 && extent < (int64_t(1) << 31)) ? extent : 0;
+  }
   p.vec_out = (y_ps % 4 == 0 && y_nstride % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
   if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;  // tuning knob
   p.is1x1 = (kh == 1 && kw == 1 && sh == 1 && sw == 1 && win.pt == 0 && win.pl == 0 && win.Ho == H && win.Wo == W &&
