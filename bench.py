@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--no-step-timing", action="store_true", help="no per-kernel HIP events in the timed loop")
     ap.add_argument("--layers", action="store_true", help="print per-kernel-step times to stderr")
     ap.add_argument("--no-b1", action="store_true", help="skip the batch-1 latency probe")
+    ap.add_argument("--no-autotune", action="store_true", help="keep the heuristic per-layer conv tiles")
     ap.add_argument("--precision", choices=["f32", "f16"], default="f32",
                     help="f16: the fp16 variant (SURVEY.md §8(f)3, config 5); the headline metric is f32")
     return ap.parse_args()
@@ -136,6 +137,9 @@ def main():
     gathered = torch.empty((world * B, model.output_elems), dtype=torch.float32, device=f"cuda:{local}") \
         if world > 1 else out
 
+    if not args.no_autotune:  # per-layer conv tile search, outside the timed region
+        model.autotune(x, out)
+
     def step():
         model.run_into(x, out)
         if world > 1:
@@ -181,6 +185,9 @@ def main():
                        "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}",
                        "collective": "RCCL all_gather of [256,1000] logits per step" if world > 1 else None},
         }
+        result["conv_tiles"] = {"autotuned": not args.no_autotune,
+                                "tile_per_conv": [["128x128", "96x128", "64x128", "32x256"][t]
+                                                  for t in model.tiles() if t >= 0]}
         if timing:
             per_step_ms /= args.steps
             classes = {}

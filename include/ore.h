@@ -174,6 +174,13 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
                                 int64_t dims[4], int32_t* ndim);
 /* Per-node timing with HIP events on the context stream (enable, run, then query).
  * ore_model_node_count/ore_model_node_info describe the executed kernel steps. */
+/* Measure every Conv step's candidate block tiles (128x128, 96x128, 64x128, 32x256) on a real
+ * run of n images (d_input / d_output as for ore_model_run) and keep the fastest per layer (like
+ * a benchmark-mode convolution search).  Results do not depend on the tile.  Synchronous.
+ * reps: timed launches per candidate (<= 0: 3).  The choice survives ore_model_set_fusion. */
+ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, float* d_output, int32_t reps);
+/* Block tile chosen for exec step i (-1 for non-conv steps). */
+int32_t ore_model_step_tile(ore_model* m, int32_t i);
 /* Branch concurrency (the reference runs the two expand branches of a fire
  * module on threads, multithreading.rs:20-62): with 2 streams, adjacent independent steps (no
  * data dependence, no overlapping storage) run on a side stream beside the main one, joined by

@@ -681,10 +681,11 @@ ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, i
   if (K <= 64 && M >= 64 && is1x1) pln.cfg = 1;
   const int forced = env_int("ORE_CONV_CFG", -1);  // tuning knob
   if (forced >= 0 && forced < 4) pln.cfg = forced;
-  // packed rows cover every block tile's rows (the 96-row tile can pass roundup(M, 128))
+  // packed rows cover every block tile's rows (the 96-row tile can pass roundup(M, 128)), so
+  // the tile can be changed after packing (ore_model_autotune)
   pln.Mp = conv_packed_mp(M);
-  {
-    const int bm = CFG_BM[pln.cfg], rows = (M + bm - 1) / bm * bm;
+  for (int c = 0; c < 4; ++c) {
+    const int bm = CFG_BM[c], rows = (M + bm - 1) / bm * bm;
     if (rows > pln.Mp) pln.Mp = rows;
   }
   pln.krows = conv_packed_kp(K);

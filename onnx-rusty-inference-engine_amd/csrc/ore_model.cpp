@@ -1030,6 +1030,63 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
   return ORE_OK;
 }
 
+ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, float* d_output, int32_t reps) {
+  if (!m || !d_input || !d_output) return set_error(m ? m->ctx : nullptr, ORE_ERR_INVALID, "null argument");
+  ore_ctx* ctx = m->ctx;
+  if (n < 1 || n > m->max_batch) return set_error(ctx, ORE_ERR_INVALID, "batch out of range");
+  if (reps < 1) reps = 3;
+  ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+  m->cur_in = d_input;
+  m->cur_out = d_output;
+  m->last_n = n;
+  const Value& ov = m->values[m->output_value];
+  m->out_bound = ov.alias_of < 0 && !ov.elided;
+  hipEvent_t e0, e1;
+  ORE_HIP_CHECK(ctx, hipEventCreate(&e0));
+  ORE_HIP_CHECK(ctx, hipEventCreate(&e1));
+  ore_status st = ORE_OK;
+  // steps run in order so every conv sees its real input geometry; each candidate block tile
+  // is timed on the step's own buffers and the fastest kept (results do not depend on the tile:
+  // every output is the same k-ordered MFMA chain)
+  for (size_t k = 0; k < m->exec_steps.size() && !st; ++k) {
+    Step& s = m->steps[m->exec_steps[k]];
+    if (s.kind != S_CONV || s.plan.window) {
+      st = launch_step(m, s, n);
+      continue;
+    }
+    int best = s.plan.cfg;
+    float best_ms = 1e30f;
+    for (int c = 0; c < 4 && !st; ++c) {
+      s.plan.cfg = c;
+      st = launch_step(m, s, n);  // warm-up
+      if (st) break;
+      if (hipEventRecord(e0, ctx->stream) != hipSuccess) { st = set_error(ctx, ORE_ERR_HIP, "event record"); break; }
+      for (int r = 0; r < reps && !st; ++r) st = launch_step(m, s, n);
+      if (st) break;
+      float ms = 0.f;
+      if (hipEventRecord(e1, ctx->stream) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+          hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
+        st = set_error(ctx, ORE_ERR_HIP, "autotune timing failed");
+        break;
+      }
+      if (ms < best_ms) { best_ms = ms; best = c; }
+    }
+    s.plan.cfg = best;
+    m->base_steps[m->exec_steps[k]].plan.cfg = best;  // steps are a per-plan copy of base_steps
+    if (!st) st = launch_step(m, s, n);                // leave the real output for the next step
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (!st && hipStreamSynchronize(ctx->stream) != hipSuccess) st = set_error(ctx, ORE_ERR_HIP, "autotune sync");
+  return st;
+}
+
+int32_t ore_model_step_tile(ore_model* m, int32_t i) {
+  if (!m || i < 0 || size_t(i) >= m->exec_steps.size()) return -1;
+  const Step& s = m->steps[m->exec_steps[i]];
+  return (s.kind == S_CONV || s.kind == S_MATMUL) ? s.plan.cfg : -1;
+}
+
 ore_status ore_model_set_streams(ore_model* m, int32_t streams) {
   if (!m || streams < 1 || streams > 2) return set_error(m ? m->ctx : nullptr, ORE_ERR_INVALID, "streams must be 1 or 2");
   m->streams = streams;

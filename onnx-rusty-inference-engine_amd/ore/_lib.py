@@ -27,7 +27,8 @@ EXPORTED = [
     "ore_conv_out_shape", "ore_pool_out_shape", "ore_conv2d_f32", "ore_maxpool2d_f32", "ore_relu_f32",
     "ore_add_f32", "ore_softmax_f32", "ore_matmul_f32", "ore_gap_f32", "ore_concat_f32", "ore_dropout_f32",
     "ore_reshape", "ore_model_load", "ore_model_load_ex", "ore_model_destroy", "ore_model_set_fusion", "ore_model_input_dims",
-    "ore_model_output_elems", "ore_model_run", "ore_model_read_value", "ore_model_set_streams",
+    "ore_model_output_elems", "ore_model_run", "ore_model_read_value", "ore_model_autotune",
+    "ore_model_step_tile", "ore_model_set_streams",
     "ore_model_graph_capture", "ore_model_graph_launch", "ore_model_enable_timing",
     "ore_model_step_count", "ore_model_step_info", "ore_model_step_times",
 ]
@@ -103,6 +104,8 @@ def load():
         "ore_model_read_value": (i32, [vp, cs, vp, ctypes.c_size_t, I64P, ctypes.POINTER(i32)]),
         "ore_model_enable_timing": (i32, [vp, i32]),
         "ore_model_set_streams": (i32, [vp, i32]),
+        "ore_model_autotune": (i32, [vp, vp, i64, vp, i32]),
+        "ore_model_step_tile": (i32, [vp, i32]),
         "ore_model_graph_capture": (i32, [vp, vp, i64, vp]),
         "ore_model_graph_launch": (i32, [vp]),
         "ore_model_step_count": (i32, [vp]),

@@ -265,6 +265,17 @@ class Model:
                                           dims, ctypes.byref(nd)), self.ctx.h)
         return buf
 
+    def autotune(self, x, out, reps: int = 3):
+        """Per-layer block-tile search on a real run (ore_model_autotune); synchronous."""
+        if tuple(x.shape[1:]) != self.input_dims or not (x.is_contiguous() and out.is_contiguous()):
+            raise OreError(1, "bad input/output buffers")
+        check(load().ore_model_autotune(self.h, ctypes.c_void_p(x.data_ptr()), int(x.shape[0]),
+                                        ctypes.c_void_p(out.data_ptr()), int(reps)), self.ctx.h)
+
+    def tiles(self):
+        """Block tile per exec step (-1 for non-conv steps)."""
+        return [load().ore_model_step_tile(self.h, i) for i in range(load().ore_model_step_count(self.h))]
+
     def set_streams(self, streams: int):
         """2: run independent neighbouring steps (the fire modules' expand branches) on a side
         stream (ore_model_set_streams)."""

@@ -187,6 +187,28 @@ def test_squeezenet_batch256_properties(squeeze224):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("precision", ["f32", "f16"])
+def test_autotune_keeps_results(gpu_ctx, precision):
+    """ore_model_autotune only changes block tiles: outputs stay bit-identical."""
+    import torch
+    import ore
+    from ore import squeezenet
+    m = ore.Model(gpu_ctx, squeezenet.build(224), max_batch=8, precision=precision)
+    x = _t(squeezenet.synthetic_input(8, 224, seed=21))
+    before = _np(m.run(x))
+    tiles0 = m.tiles()
+    out = torch.empty_like(torch.from_numpy(before)).cuda()
+    m.autotune(x, out, reps=2)
+    np.testing.assert_array_equal(_np(out), before)  # the autotune pass leaves a real result
+    np.testing.assert_array_equal(_np(m.run(x)), before)
+    tiles1 = m.tiles()
+    assert len(tiles1) == len(tiles0) and sum(t >= 0 for t in tiles1) == 26
+    m.set_fusion(0)  # the choice survives re-planning
+    assert [t for t in m.tiles() if t >= 0] == [t for t in tiles1 if t >= 0]
+    np.testing.assert_array_equal(_np(m.run(x)), before)
+    m.close()
+
+
 @pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(HERE), "models", "squeezenet1.0-8.onnx")),
                     reason="real squeezenet1.0-8.onnx is not in the repo (stripped from the reference mirror)")
 def test_real_squeezenet_golden(gpu_ctx):
