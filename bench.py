@@ -202,10 +202,20 @@ def main():
             peak = PEAK_F16_MFMA_TFLOPS if f16 else PEAK_F32_MFMA_TFLOPS
             kname = ("conv_f16_kernel (implicit-GEMM MFMA 32x32x16 f16, f32 accumulate" if f16 else
                      "conv_gemm_kernel (implicit-GEMM MFMA 32x32x2 f32") + ", 26 launches/step)"
+            # HBM bytes per conv launch from the PMC passes of tools/pmc.sh (FETCH_SIZE x2 +
+            # WRITE_SIZE, separate --pmc runs; counters cannot be read inside this timed run)
+            traffic, tsrc = None, None
+            tfile = os.path.join(REPO, "profiles", f"pmc_traffic_{args.precision}.json")
+            if os.path.exists(tfile):
+                with open(tfile) as f:
+                    tj = json.load(f)
+                traffic, tsrc = round(tj["hbm_bytes_per_launch"]), f"profiles/pmc_traffic_{args.precision}.json"
             result["roofline"] = {
                 "bound": "mfma", "kernel": kname,
                 "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": None,
+                "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                "traffic_source": tsrc,
+                "algorithmic_bytes_per_launch": round(conv["bytes"] / max(conv["launches"], 1)),
                 "per_launch_avg_us": round(1000.0 * conv["ms"] / conv["launches"], 2),
                 "algorithmic": "2*Cout*Ho*Wo*Cin*kh*kw per image (1.638 GFLOP/img)"}
             if args.layers:

@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Per-layer PMC table from tools/pmc.sh output (the last SqueezeNet pass of each counter pass).
-usage: python tools/pmc_report.py gpurun_out/pmc_TAG"""
+usage: python tools/pmc_report.py gpurun_out/pmc_TAG [--json profiles/pmc_traffic_f32.json]
+
+--json writes the HBM traffic per launch of the conv kernel class (FETCH_SIZE x2 + WRITE_SIZE,
+the guide's gfx950 correction), which bench.py reports as roofline.traffic."""
 import csv
 import glob
 import os
@@ -36,6 +39,7 @@ def load(d):
 
 def main():
     base = sys.argv[1]
+    json_out = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
     names = layer_names()
     merged = [defaultdict(float) for _ in range(PER)]
     for d in sorted(glob.glob(os.path.join(base, "p*"))):
@@ -70,6 +74,17 @@ def main():
               f"{r.get('SQ_INSTS_LDS', 0) / w:6.0f} {r.get('SQ_INSTS_VMEM_RD', 0) / w:6.0f} {r.get('SQ_INSTS_VMEM_WR', 0) / w:6.0f} "
               f"{mfpct:6.1f} {waitpct:6.1f} {2 * r.get('FETCH_SIZE', 0) / 1024:8.1f} {r.get('WRITE_SIZE', 0) / 1024:8.1f} "
               f"{(busy / 8 / (dur * 1e3)) if busy else 0:5.2f} {r.get('vgpr', '')}/{r.get('agpr', '')}")
+    if json_out:
+        import json
+        conv = [r for r in merged if "conv" in str(r.get("name", ""))]
+        fetch = sum(2 * r.get("FETCH_SIZE", 0) * 1024 for r in conv)  # KB -> B, x2 gfx950 correction
+        write = sum(r.get("WRITE_SIZE", 0) * 1024 for r in conv)
+        out = {"kernel_class": "conv", "launches": len(conv), "hbm_bytes_per_launch": (fetch + write) / max(len(conv), 1),
+               "fetch_bytes_per_launch": fetch / max(len(conv), 1), "write_bytes_per_launch": write / max(len(conv), 1),
+               "source": base, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, FETCH_SIZE x2 (gfx950)"}
+        with open(json_out, "w") as f:
+            json.dump(out, f, indent=1)
+        print(f"wrote {json_out}: {out['hbm_bytes_per_launch'] / 1e6:.1f} MB per conv launch")
 
 
 if __name__ == "__main__":
