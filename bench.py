@@ -197,7 +197,7 @@ def main():
                 c["flops"] += info["flops"]
                 c["bytes"] += info["bytes"]
                 c["launches"] += 1
-            conv = classes.get("Conv", {"ms": 1e-9, "flops": 0.0, "launches": 1})
+            conv = classes.get("Conv", {"ms": 1e-9, "flops": 0.0, "bytes": 0.0, "launches": 1})
             achieved = conv["flops"] / (conv["ms"] * 1e-3) / 1e12
             peak = PEAK_F16_MFMA_TFLOPS if f16 else PEAK_F32_MFMA_TFLOPS
             kname = ("conv_f16_kernel (implicit-GEMM MFMA 32x32x16 f16, f32 accumulate" if f16 else
