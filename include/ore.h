@@ -157,6 +157,12 @@ ore_status ore_model_destroy(ore_model* m);
 #define ORE_FUSE_CONCAT 2
 #define ORE_FUSE_ALIAS 4
 #define ORE_FUSE_ALL 7
+/* bit 4 (opt-in, not in ORE_FUSE_ALL): a 3x3 MaxPool whose only consumer is a 1x1 stride-1 Conv
+ * runs inside that conv's operand gather (each B element = the window max of the pre-pool
+ * tensor); the pooled tensor is never written.  Max is exact, so results are bit-identical.
+ * Measured slower than the separate plane-staged pool on SqueezeNet (9 loads per operand
+ * element lose the pool kernel's row reuse: +150 us per step at batch 256). */
+#define ORE_FUSE_POOL_CONV 16
 /* debug: give every value its own storage (no liveness reuse) so any value can be read back */
 #define ORE_KEEP_VALUES 8
 ore_status ore_model_set_fusion(ore_model* m, int32_t flags);

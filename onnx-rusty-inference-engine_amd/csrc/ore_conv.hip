@@ -14,6 +14,7 @@
 //   B[k=l>>5][l&31]; accumulator register e of lane l is row (e&3)+8*(e>>2)+4*(l>>5), column
 //   l&31 -> one register = two 128-B runs of consecutive output pixels.
 #include <hip/hip_runtime.h>
+#include <float.h>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -35,7 +36,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));  // first-class vecto
 #define ORE_PRIO(X)
 #endif
 
-enum { B1X1 = 0, BGATHER = 1 };
+enum { B1X1 = 0, BGATHER = 1, BPOOL = 2 };  // BPOOL: B = 3x3 window max of the pre-pool tensor
 
 // DMA: the B tile goes global -> LDS by buffer_load ... lds (no VGPR staging, no LDS store
 // pass); a tap outside the image gets an out-of-range offset, which the buffer bounds check
@@ -91,6 +92,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
   // element offsets fit in 32 bits (checked on the host): uniform base + 32-bit lane offset
   int xoff;
   int ih0 = 0, iw0 = 0;
+  int pmask = 0;  // BPOOL: bit r*3+s set when window tap (r, s) is inside the pre-pool plane
   {
     const int nn = bn_ok ? bn : 0;
     const int img = nn / YPS;
@@ -98,6 +100,16 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
     xoff = img * (int)p.x_nstride;
     if (BMODE == B1X1) {
       xoff += pix;
+    } else if (BMODE == BPOOL) {
+      const int oh = pix / p.Wo, ow = pix - oh * p.Wo;
+      ih0 = oh * p.pool_sh - p.pool_pt;
+      iw0 = ow * p.pool_sw - p.pool_pl;
+      xoff += ih0 * p.pool_W + iw0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+          if ((unsigned)(ih0 + r) < (unsigned)p.pool_H && (unsigned)(iw0 + s) < (unsigned)p.pool_W) pmask |= 1 << (r * 3 + s);
     } else {
       const int oh = pix / p.Wo, ow = pix - oh * p.Wo;
       ih0 = oh * p.sh - p.pt;
@@ -133,7 +145,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
       const int k = k0_ + krow + j * BROWS;                                                          \
       bool ok;                                                                                       \
       int off;                                                                                       \
-      if (BMODE == B1X1) {                                                                           \
+      if (BMODE == B1X1 || BMODE == BPOOL) {                                                         \
         ok = bn_ok & (k < K);                                                                        \
         off = xoff + k * XPS;                                                                        \
       } else {                                                                                       \
@@ -144,7 +156,17 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
         off = xoff + ex_;                                                                            \
       }                                                                                              \
       ORE_EXP_BFIXED_HOOK                                                                            \
-      if (DMA) {                                                                                     \
+      if (BMODE == BPOOL) {                                                                          \
+        /* the reference's MaxPool: start at -FLT_MAX, taps outside the plane read 0 */              \
+        float m_ = -FLT_MAX;                                                                         \
+        _Pragma("unroll") for (int t_ = 0; t_ < 9; ++t_) {                                           \
+          const bool in_ = ok & (((pmask >> t_) & 1) != 0);                                          \
+          const float v_ = x[(unsigned)(in_ ? off + (t_ / 3) * p.pool_W + (t_ % 3) : 0)];             \
+          m_ = fmaxf(m_, in_ ? v_ : 0.0f);                                                           \
+        }                                                                                            \
+        RB[j] = m_;                                                                                  \
+        ROK[j] = ok;                                                                                 \
+      } else if (DMA) {                                                                              \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                    \
             xrsrc, (__attribute__((address_space(3))) void*)&Bs[(DBUF)][krow + j * BROWS][wcol0], 4,  \
             ok ? off * 4 : (int)0x80000000, 0, 0, 0);                                                \
@@ -638,7 +660,9 @@ static void launch_conv_cfg(const ConvParams& p0, hipStream_t s) {
   p.ntiles = (int)((p.Ntot + BN - 1) / BN);
   dim3 grid(p.mtiles * p.ntiles), block(256);
   const bool dma = p.x_bytes > 0 && env_int("ORE_CONV_DMA", 1) != 0;  // tuning knob
-  if (p.is1x1) {
+  if (p.pool) {
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BPOOL, 0>), grid, block, 0, s, p);
+  } else if (p.is1x1) {
     if (dma)
       hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, B1X1, 1>), grid, block, 0, s, p);
     else

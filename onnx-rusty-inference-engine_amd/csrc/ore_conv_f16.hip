@@ -19,7 +19,7 @@ namespace ore {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16h __attribute__((ext_vector_type(16)));
 
-enum { H1X1 = 0, HGATHER = 1 };
+enum { H1X1 = 0, HGATHER = 1, HPOOL = 2 };  // HPOOL: B = 3x3 window max of the pre-pool tensor
 
 template <int BM, int BN, int WM, int WN, int XF32, int BMODE>
 __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
@@ -61,6 +61,7 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
   const int bn = n0 + bcol;
   const bool bn_ok = bn < p.Ntot;
   int xoff, ih0 = 0, iw0 = 0;
+  int pmask = 0;
   {
     const int nn = bn_ok ? bn : 0;
     const int img = nn / YPS;
@@ -68,6 +69,16 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
     xoff = img * (int)p.x_nstride;
     if (BMODE == H1X1) {
       xoff += pix;
+    } else if (BMODE == HPOOL) {
+      const int oh = pix / p.Wo, ow = pix - oh * p.Wo;
+      ih0 = oh * p.pool_sh - p.pool_pt;
+      iw0 = ow * p.pool_sw - p.pool_pl;
+      xoff += ih0 * p.pool_W + iw0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+          if ((unsigned)(ih0 + r) < (unsigned)p.pool_H && (unsigned)(iw0 + s) < (unsigned)p.pool_W) pmask |= 1 << (r * 3 + s);
     } else {
       const int oh = pix / p.Wo, ow = pix - oh * p.Wo;
       ih0 = oh * p.sh - p.pt;
@@ -94,7 +105,7 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
         const int k = kg_ + e_;                                                                      \
         bool ok;                                                                                     \
         int off;                                                                                     \
-        if (BMODE == H1X1) {                                                                         \
+        if (BMODE == H1X1 || BMODE == HPOOL) {                                                       \
           ok = bn_ok & (k < K);                                                                      \
           off = xoff + k * XPS;                                                                      \
         } else {                                                                                     \
@@ -104,7 +115,17 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
           ok = bn_ok & ((unsigned)(ih0 + r) < (unsigned)p.H) & ((unsigned)(iw0 + s) < (unsigned)p.W); \
           off = xoff + ex_;                                                                          \
         }                                                                                            \
-        RB[u_ * 8 + e_] = x[(unsigned)(ok ? off : 0)];                                               \
+        if (BMODE == HPOOL) {                                                                        \
+          float m_ = -3.402823466e38f;                                                               \
+          _Pragma("unroll") for (int t_ = 0; t_ < 9; ++t_) {                                         \
+            const bool in_ = ok & (((pmask >> t_) & 1) != 0);                                        \
+            const float v_ = (float)x[(unsigned)(in_ ? off + (t_ / 3) * p.pool_W + (t_ % 3) : 0)];    \
+            m_ = fmaxf(m_, in_ ? v_ : 0.0f);                                                         \
+          }                                                                                          \
+          RB[u_ * 8 + e_] = (XT)m_;                                                                  \
+        } else {                                                                                     \
+          RB[u_ * 8 + e_] = x[(unsigned)(ok ? off : 0)];                                             \
+        }                                                                                            \
         ROK[u_ * 8 + e_] = ok;                                                                       \
       }                                                                                              \
     }                                                                                                \
@@ -222,7 +243,12 @@ static void launch_f16_cfg(const ConvParams& p0, hipStream_t s) {
   p.ntiles = (int)((p.Ntot + BN - 1) / BN);
   dim3 grid((unsigned)(p.mtiles * p.ntiles)), block(256);
   const bool xf32 = p.x_f32 != 0;
-  if (p.is1x1) {
+  if (p.pool) {
+    if (xf32)
+      hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, WN, 1, HPOOL>), grid, block, 0, s, p);
+    else
+      hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, WN, 0, HPOOL>), grid, block, 0, s, p);
+  } else if (p.is1x1) {
     if (xf32)
       hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, WN, 1, H1X1>), grid, block, 0, s, p);
     else

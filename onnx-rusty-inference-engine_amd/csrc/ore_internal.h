@@ -91,6 +91,12 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
                     const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, float* y,
                     int64_t y_nstride, int64_t x_ps = 0, int64_t y_ps = 0,  // plane strides, 0 = dense
                     int x_es = 4);  // input element bytes (2: f16; only with an f16 plan, whose output is f16)
+// 1x1 conv over the 3x3 MaxPool (window pwin, strides psh/psw) of x [C][pH][pW] (plane stride x_ps):
+// the pooled tensor is never materialised (ORE_FUSE_POOL_CONV)
+ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t pH,
+                         int64_t pW, int64_t x_nstride, int64_t x_ps, const Window& pwin, int64_t psh, int64_t psw,
+                         const float* wp, int64_t M, const float* bias, bool relu, float* y, int64_t y_nstride,
+                         int64_t y_ps, int x_es);
 // packs w (and the gather table for an input of H x W) into the context scratch buffer;
 // returns the packed weights (or null with the error set), *ktab receives the table
 float* pack_to_scratch(ore_ctx* ctx, const ConvPlan& pln, const float* w, bool kmajor_src, int64_t M, int64_t C,

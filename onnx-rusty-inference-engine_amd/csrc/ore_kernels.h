@@ -27,6 +27,10 @@ struct ConvParams {
   int vec_out;         // 16-B epilogue stores (y_ps, y_nstride % 4 == 0 and a 16-B aligned y)
   int x_f32;           // f16 kernel: the input is f32 (rounded to f16 while staging)
   long long x_bytes;   // bytes from x to the end of its last valid element (0: no buffer DMA path)
+  // fused MaxPool (ORE_FUSE_POOL_CONV): x is the PRE-pool tensor [pool_H][pool_W] planes and the
+  // conv (1x1) reads each B element as the 3x3 window max at stride (pool_sh, pool_sw)
+  int pool;            // 1: BPOOL operand mode
+  int pool_sh, pool_sw, pool_pt, pool_pl, pool_H, pool_W;
   // window-staged kernel (filled by the launcher from the ConvPlan)
   int bch, ks, nst, wr, ww, tiles_per_img;
 };

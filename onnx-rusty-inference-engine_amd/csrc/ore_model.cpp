@@ -72,6 +72,10 @@ struct Step {
   Window win;
   bool relu = false;
   bool w_kmajor = false;  // MatMul: the constant operand is [K][M]
+  // fused MaxPool (ORE_FUSE_POOL_CONV): in0 is the pool's input; pool geometry below
+  bool pool = false;
+  int64_t pH = 0, pW = 0, psh = 1, psw = 1;
+  Window pwin;
   ConvPlan plan{};        // kernel choice and weight layout for S_CONV / S_MATMUL
   float* wp = nullptr;    // packed weights (layout per plan) for S_CONV / S_MATMUL
   const int2* ktab = nullptr;  // gather table (follows wp in the packed allocation; gather kernel only)
@@ -480,6 +484,30 @@ ore_status plan(ore_model* m) {
     }
     count_uses(m, m->steps);
   }
+  // (1b) 3x3 MaxPool -> its only consumer, a plain 1x1 Conv: the pool runs in the conv's gather
+  if (m->fusion & ORE_FUSE_POOL_CONV) {
+    for (size_t i = 0; i < m->steps.size(); ++i) {
+      Step& pl = m->steps[i];
+      if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3) continue;
+      const int v = pl.out;
+      if (m->values[v].uses != 1 || m->values[v].is_output) continue;
+      int ci = -1;
+      for (size_t j = i + 1; j < m->steps.size(); ++j)
+        if (m->steps[j].kind != S_NOP && m->steps[j].in0 == v) { ci = int(j); break; }
+      if (ci < 0) continue;
+      Step& cv = m->steps[ci];
+      if (cv.kind != S_CONV || cv.pool || cv.kh != 1 || cv.kw != 1 || cv.sh != 1 || cv.sw != 1 || cv.win.pt != 0 ||
+          cv.win.pl != 0 || cv.win.Ho != cv.H || cv.win.Wo != cv.W || cv.plan.window)
+        continue;
+      cv.pool = true;
+      cv.in0 = pl.in0;
+      cv.pH = pl.H; cv.pW = pl.W; cv.psh = pl.sh; cv.psw = pl.sw; cv.pwin = pl.win;
+      m->values[v].elided = true;
+      pl.kind = S_NOP;
+      pl.in0 = -1;
+    }
+    count_uses(m, m->steps);
+  }
   // (2) Dropout / activation Reshape as aliases
   if (m->fusion & ORE_FUSE_ALIAS) {
     for (auto& s : m->steps) {
@@ -711,6 +739,9 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
     case S_CONV: {
       const Ref x = ref_of(m, s.in0);
       const float* bias = s.in2 >= 0 ? m->values[s.in2].cptr : nullptr;
+      if (s.pool)
+        return run_conv_pool(ctx, s.plan, x.p, n, s.C, s.pH, s.pW, x.nstride, x.ps, s.pwin, s.psh, s.psw, s.wp, s.M, bias,
+                             s.relu, y.p, y.nstride, y.ps, x.es);
       return run_conv(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, s.wp, s.ktab, s.M, s.kh, s.kw, bias, s.win, s.sh, s.sw, s.relu,
                       y.p, y.nstride, x.ps, y.ps, x.es);
     }
@@ -898,7 +929,7 @@ ore_status ore_model_destroy(ore_model* m) {
 
 ore_status ore_model_set_fusion(ore_model* m, int32_t flags) {
   if (!m) return set_error(nullptr, ORE_ERR_INVALID, "null model");
-  m->fusion = flags & (ORE_FUSE_ALL | ORE_KEEP_VALUES);
+  m->fusion = flags & (ORE_FUSE_ALL | ORE_FUSE_POOL_CONV | ORE_KEEP_VALUES);
   return plan(m);
 }
 

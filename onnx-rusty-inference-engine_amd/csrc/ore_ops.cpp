@@ -179,6 +179,46 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
   return ORE_OK;
 }
 
+ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t pH,
+                         int64_t pW, int64_t x_nstride, int64_t x_ps, const Window& pwin, int64_t psh, int64_t psw,
+                         const float* wp, int64_t M, const float* bias, bool relu, float* y, int64_t y_nstride,
+                         int64_t y_ps, int x_es) {
+  if (N == 0) return ORE_OK;
+  if (x_ps == 0) x_ps = pH * pW;
+  const int64_t P = pwin.Ho * pwin.Wo;
+  if (y_ps == 0) y_ps = P;
+  if (!pln.f16 && x_es != 4) return set_error(ctx, ORE_ERR_INVALID, "internal: f32 conv on f16 input");
+  ConvParams p{};
+  p.x = x; p.wp = wp; p.ktab = nullptr; p.bias = bias; p.y = y;
+  p.N = int(N); p.C = int(C); p.H = int(pwin.Ho); p.W = int(pwin.Wo);
+  p.M = int(M); p.kh = 1; p.kw = 1; p.sh = 1; p.sw = 1; p.pt = 0; p.pl = 0;
+  p.Ho = int(pwin.Ho); p.Wo = int(pwin.Wo);
+  p.K = int(C);
+  p.P = int(P);
+  p.x_ps = int(x_ps);
+  p.y_ps = int(y_ps);
+  p.Ntot = N * y_ps;
+  p.x_nstride = x_nstride;
+  p.y_nstride = y_nstride;
+  p.relu = relu ? 1 : 0;
+  p.is1x1 = 0;
+  p.Mp = pln.Mp;
+  p.x_f32 = x_es == 4 ? 1 : 0;
+  p.x_bytes = 0;  // register path: the window max needs the values
+  p.vec_out = (y_ps % 4 == 0 && y_nstride % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
+  if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;
+  p.pool = 1;
+  p.pool_sh = int(psh); p.pool_sw = int(psw); p.pool_pt = int(pwin.pt); p.pool_pl = int(pwin.pl);
+  p.pool_H = int(pH); p.pool_W = int(pW);
+  if (x_ps < pH * pW || y_ps < P) return set_error(ctx, ORE_ERR_INVALID, "plane stride below plane size");
+  if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(int64_t(pln.krows) * pln.Mp) ||
+      !fits_i32(p.Ntot + 256))
+    return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
+  launch_conv(p, pln, ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
+}
+
 ore_status run_maxpool(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
                        int64_t x_nstride, int64_t kh, int64_t kw, const Window& win, int64_t sh, int64_t sw,
                        float* y, int64_t y_nstride, int64_t x_ps, int64_t y_ps, int es) {

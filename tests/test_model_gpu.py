@@ -41,7 +41,7 @@ def squeeze224(gpu_ctx):
     m.close()
 
 
-@pytest.mark.parametrize("fusion", [7, 0])
+@pytest.mark.parametrize("fusion", [23, 7, 0])  # 23 = default set + the opt-in pool fusion
 def test_mnist_golden(gpu_ctx, fusion):
     import ore
     from ore import onnx_wire
@@ -85,7 +85,7 @@ def test_squeezenet_synth_vs_oracle(squeeze224):
     assert np.array_equal(y.argmax(1), ref.argmax(1))
 
 
-@pytest.mark.parametrize("fusion", [7, 0, 1, 2, 4])
+@pytest.mark.parametrize("fusion", [23, 16, 7, 0, 1, 2, 4])
 def test_squeezenet_mini_vs_oracle(gpu_ctx, fusion):
     import ore
     from ore import squeezenet
@@ -185,6 +185,32 @@ def test_squeezenet_batch256_properties(squeeze224):
     squeeze224.set_fusion(7)
     assert np.array_equal(y0, y)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("precision", ["f32", "f16"])
+@pytest.mark.parametrize("hw", [64, 224])
+def test_pool_conv_fusion_bit_identical(gpu_ctx, precision, hw):
+    """ORE_FUSE_POOL_CONV (the 3x3 pools computed inside the squeeze convs' gathers) changes no
+    bit of any result; all tiles of the fused kernel agree too."""
+    import os
+    import ore
+    from ore import squeezenet
+    mb = squeezenet.build(hw)
+    x = _t(squeezenet.synthetic_input(3, hw, seed=13))
+    outs = []
+    pf = ore.FUSE_ALL | ore.FUSE_POOL_CONV
+    for fusion, cfg in ((pf, None), (ore.FUSE_ALL, None), (pf, "2"), (pf, "3"), (pf, "1"), (pf, "0")):
+        if cfg is not None:
+            os.environ["ORE_CONV_CFG"] = cfg
+        try:
+            m = ore.Model(gpu_ctx, mb, max_batch=3, precision=precision)
+            m.set_fusion(fusion)
+            outs.append(_np(m.run(x)))
+            m.close()
+        finally:
+            os.environ.pop("ORE_CONV_CFG", None)
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])
 
 
 @pytest.mark.parametrize("precision", ["f32", "f16"])
