@@ -208,7 +208,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
   __syncthreads();
   const int lrow = lane >> 5, lcol = lane & 31;
 // fragments for k-step kk+2 are read from LDS before the MFMAs of k-step kk are issued
-#define ORE_COMPUTE_TILE(BUF)                                                                        \
+// KEND: k-steps of this tile that carry data (BK except on the last tile, where the zero rows
+// past K are skipped: conv1's K = 147 pads to 160)
+#define ORE_COMPUTE_TILE(BUF, KEND)                                                                  \
   {                                                                                                  \
     float af[2][FM], bf[2][FN];                                                                      \
     _Pragma("unroll") for (int i = 0; i < FM; ++i) af[0][i] = As[BUF][lrow][wm0 + i * 32 + lcol];    \
@@ -222,9 +224,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
           bf[cur ^ 1][j] = Bs[BUF][kk + 2 + lrow][wn0 + j * 32 + lcol];                              \
       }                                                                                              \
       ORE_PRIO(1);                                                                                   \
-      _Pragma("unroll") for (int i = 0; i < FM; ++i)                                                 \
-      _Pragma("unroll") for (int j = 0; j < FN; ++j)                                                 \
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0); \
+      if (kk < (KEND)) {                                                                             \
+        _Pragma("unroll") for (int i = 0; i < FM; ++i)                                               \
+        _Pragma("unroll") for (int j = 0; j < FN; ++j)                                               \
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0); \
+      }                                                                                              \
       ORE_PRIO(0);                                                                                   \
     }                                                                                                \
   }
@@ -237,17 +241,20 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
     bool rok[BLOADS];
     ORE_LOAD_TILE(ra, rb, rok, (t + 1) * BK, buf ^ 1);
     __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
-    ORE_COMPUTE_TILE(buf);
+    ORE_COMPUTE_TILE(buf, BK);
     ORE_STORE_TILE(ra, rb, rok, buf ^ 1);
 #else
-    ORE_COMPUTE_TILE(0);
+    ORE_COMPUTE_TILE(0, BK);
 #endif
 #ifndef ORE_EXP_NOSYNC
     if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 #endif
   }
-  ORE_COMPUTE_TILE((ntk - 1) & 1);
+  {
+    const int kend = __builtin_amdgcn_readfirstlane((K - (ntk - 1) * BK + 1) & ~1);
+    ORE_COMPUTE_TILE((ntk - 1) & 1, kend);
+  }
 #undef ORE_COMPUTE_TILE
 #undef ORE_LOAD_TILE
 #undef ORE_STORE_TILE
