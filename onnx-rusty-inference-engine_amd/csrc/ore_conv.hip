@@ -36,13 +36,22 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));  // first-class vecto
 #define ORE_PRIO(X)
 #endif
 
+#ifndef ORE_NO_FRAG_PIN
+#define ORE_FRAG_PIN __builtin_amdgcn_sched_barrier(0)
+#else
+#define ORE_FRAG_PIN
+#endif
+#ifndef ORE_CONV_MINBLOCKS
+#define ORE_CONV_MINBLOCKS 2  // __launch_bounds__ minimum blocks per CU (VGPR budget)
+#endif
+
 enum { B1X1 = 0, BGATHER = 1, BPOOL = 2 };  // BPOOL: B = 3x3 window max of the pre-pool tensor
 
 // DMA: the B tile goes global -> LDS by buffer_load ... lds (no VGPR staging, no LDS store
 // pass); a tap outside the image gets an out-of-range offset, which the buffer bounds check
 // turns into a 0 -- the reference's zero padding -- with no select.
 template <int BM, int BN, int WM, int WN, int BK, int BMODE, int DMA>
-__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
+__global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(ConvParams p) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 32, FN = TN / 32;
   constexpr int AS = BM + 4;                 // LDS row stride of the A tile (16-B aligned rows)
@@ -223,6 +232,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvParams p) {
         _Pragma("unroll") for (int j = 0; j < FN; ++j)                                               \
           bf[cur ^ 1][j] = Bs[BUF][kk + 2 + lrow][wn0 + j * 32 + lcol];                              \
       }                                                                                              \
+      ORE_FRAG_PIN; /* next k-step's fragment reads stay ahead of this k-step's MFMAs */             \
       ORE_PRIO(1);                                                                                   \
       if (kk < (KEND)) {                                                                             \
         _Pragma("unroll") for (int i = 0; i < FM; ++i)                                               \
