@@ -186,8 +186,7 @@ def main():
                        "collective": "RCCL all_gather of [256,1000] logits per step" if world > 1 else None},
         }
         result["conv_tiles"] = {"autotuned": not args.no_autotune,
-                                "tile_per_conv": [["128x128", "96x128", "64x128", "32x256"][t]
-                                                  for t in model.tiles() if t >= 0]}
+                                "tile_per_conv": [ore.Model.TILE_NAMES[t] for t in model.tiles() if t >= 0]}
         if timing:
             per_step_ms /= args.steps
             classes = {}

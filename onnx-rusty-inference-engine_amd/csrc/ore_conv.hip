@@ -721,7 +721,7 @@ ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, i
   // 96-row tile measured fastest for them even with padded rows (tools/bench_ops.py)
   if (K <= 64 && M >= 64 && is1x1) pln.cfg = 1;
   const int forced = env_int("ORE_CONV_CFG", -1);  // tuning knob
-  if (forced >= 0 && forced < 4) pln.cfg = forced;
+  if (forced >= 0 && forced < (f16 ? CONV_TILES_F16 : CONV_TILES_F32)) pln.cfg = forced;
   // packed rows cover every block tile's rows (the 96-row tile can pass roundup(M, 128)), so
   // the tile can be changed after packing (ore_model_autotune)
   pln.Mp = conv_packed_mp(M);
@@ -737,6 +737,7 @@ ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, i
   // 5-45 % slower than the gather kernel (its 49-59 KB LDS stages allow 2-3 blocks per CU against
   // the gather kernel's 4; profiles/r01f_window_vs_gather.txt).
   if (is1x1 || env_int("ORE_CONV_WINDOW", 0) == 0 || P < 512) return pln;
+  if (pln.cfg >= 4) return pln;  // the direct kernel has no window variant
   const int BM = CFG_BM[pln.cfg], BN = CFG_BN[pln.cfg];
   const int tiles = (P + BN - 1) / BN;
   if ((long long)tiles * BN > (long long)P * 11 / 10) return pln;  // > 10% pad columns
@@ -816,6 +817,16 @@ static void launch_win_cfg(const ConvParams& p0, const ConvPlan& pln, hipStream_
 void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
   if (pln.f16) {
     launch_conv_f16(p, pln.cfg, s);
+    return;
+  }
+  if (pln.cfg >= 4) {
+    if (p.x_bytes > 0) {
+      launch_conv_direct(p, pln.cfg, s);
+      return;
+    }
+    ConvPlan q = pln;  // buffer resource unavailable (> 2 GiB input): the LDS-staged kernel
+    q.cfg = 0;
+    launch_conv(p, q, s);
     return;
   }
   if (pln.window) {

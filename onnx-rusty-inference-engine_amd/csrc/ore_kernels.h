@@ -80,6 +80,11 @@ size_t conv_packed_bytes(const ConvPlan& pln);
 void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, const ConvPlan& pln, float* wp,
                  hipStream_t s);
 void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s);
+// LDS-free, barrier-free variant (ore_conv_direct.hip): tiles 4-7 (needs p.x_bytes > 0)
+void launch_conv_direct(const ConvParams& p, int tile, hipStream_t s);
+constexpr int CONV_TILES_F32 = 8;  // 0-3 conv_gemm_kernel, 4-7 conv_direct_kernel (ORE_CONV_CFG only)
+constexpr int CONV_TILES_F16 = 4;
+constexpr int CONV_TILES_AUTOTUNE = 4;  // the direct tiles measured 15-80 % slower on every SqueezeNet layer
 void launch_maxpool(const PoolParams& p, hipStream_t s);
 void launch_relu(const float* x, float* y, long long n, hipStream_t s);
 void launch_relu_f16(const void* x, void* y, long long n, hipStream_t s);

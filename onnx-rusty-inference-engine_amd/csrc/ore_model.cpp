@@ -1087,7 +1087,8 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
     }
     int best = s.plan.cfg;
     float best_ms = 1e30f;
-    for (int c = 0; c < 4 && !st; ++c) {
+    const int ntiles = CONV_TILES_AUTOTUNE;
+    for (int c = 0; c < ntiles && !st; ++c) {
       s.plan.cfg = c;
       st = launch_step(m, s, n);  // warm-up
       if (st) break;

@@ -272,8 +272,11 @@ class Model:
         check(load().ore_model_autotune(self.h, ctypes.c_void_p(x.data_ptr()), int(x.shape[0]),
                                         ctypes.c_void_p(out.data_ptr()), int(reps)), self.ctx.h)
 
+    TILE_NAMES = ["128x128", "96x128", "64x128", "32x256",
+                  "direct 128x128", "direct 96x128", "direct 64x128", "direct 128x64"]
+
     def tiles(self):
-        """Block tile per exec step (-1 for non-conv steps)."""
+        """Block tile per exec step (-1 for non-conv steps); names in TILE_NAMES."""
         return [load().ore_model_step_tile(self.h, i) for i in range(load().ore_model_step_count(self.h))]
 
     def set_streams(self, streams: int):

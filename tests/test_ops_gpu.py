@@ -94,6 +94,27 @@ def test_conv2d(gpu_ctx, case, fuse_relu, window, monkeypatch):
     assert np.all(err <= 2e-6 * bound + 1e-30), f"max err {err.max()} vs bound {(2e-6 * bound).max()}"
 
 
+@pytest.mark.parametrize("tile", ["4", "5", "6", "7"])
+@pytest.mark.parametrize("case", CONV_CASES[::2] + CONV_CASES[14:16])
+def test_conv2d_direct_bit_identical(gpu_ctx, case, tile, monkeypatch):
+    """The LDS-free direct kernel (tiles 4-7) runs the same k-ordered MFMA chain per output as
+    the LDS-staged kernel (tile 0): bit-identical outputs, and within tolerance of the oracle."""
+    import ore
+    N, C, H, W, M, kh, kw, auto_pad, pads, strides, with_bias = case
+    rng = np.random.default_rng(zlib.crc32(repr(case).encode()) ^ 0x5a5a)
+    x = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    w = rng.standard_normal((M, C, kh, kw)).astype(np.float32)
+    b = rng.standard_normal((M,)).astype(np.float32) if with_bias else None
+    outs = []
+    for t in ("0", tile):
+        monkeypatch.setenv("ORE_CONV_CFG", t)
+        outs.append(_np(ore.convolution(gpu_ctx, _t(x), _t(w), _t(b) if b is not None else None, auto_pad=auto_pad,
+                                        pads=pads, strides=strides, fuse_relu=True)))
+    np.testing.assert_array_equal(outs[1], outs[0])
+    ref = oracle.relu(oracle.conv2d(x, w, b, auto_pad=auto_pad, pads=pads, strides=strides))
+    assert np.abs(outs[1] - ref).max() <= 1e-4 * (np.abs(ref).max() + 1.0)
+
+
 def test_conv_integer_exact(gpu_ctx):
     """Small-integer data: every partial sum is exact in f32, so GPU == oracle bit for bit."""
     import ore
