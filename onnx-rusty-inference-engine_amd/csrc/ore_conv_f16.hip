@@ -34,7 +34,9 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
   static_assert(WM * WN == 4 && FM >= 1 && FN >= 1 && (BN * 4) % 256 == 0 && 256 % BN == 0, "tile");
   typedef typename std::conditional<XF32, float, _Float16>::type XT;
 
-  __shared__ __attribute__((aligned(16))) _Float16 smem[2 * (BM + BN) * LR];
+  // operand tiles; the epilogue reuses the array for a per-wave [32][TN] f32 staging tile
+  constexpr int MAIN_HALVES = 2 * (BM + BN) * LR, EPI_HALVES = 4 * 32 * TN * 2;
+  __shared__ __attribute__((aligned(16))) _Float16 smem[MAIN_HALVES > EPI_HALVES ? MAIN_HALVES : EPI_HALVES];
   __shared__ float sbias[BM];
   _Float16(*As)[BM][LR] = reinterpret_cast<_Float16(*)[BM][LR]>(smem);
   _Float16(*Bs)[BN][LR] = reinterpret_cast<_Float16(*)[BN][LR]>(smem + 2 * BM * LR);
@@ -194,6 +196,50 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
 
   // epilogue: + bias (f32), optional Relu, round to f16, store NCHW (possibly a channel slice)
   _Float16* __restrict__ y = reinterpret_cast<_Float16*>(p.y);
+  if (p.vec_out) {
+    // 16-B stores of 8 pixels: each wave stages 32 rows x TN pixels (f32) in its own LDS slice
+    // (rows r and r + 4 in opposite bank halves), then converts and writes whole pixel runs.
+    // Host guarantees y_ps % 8 == 0, y_nstride % 8 == 0 and a 16-B aligned y.
+    __syncthreads();  // every wave is done with the A/B tiles
+    float* stg = reinterpret_cast<float*>(smem) + wave * (32 * TN);
+    constexpr int V8 = TN / 8;   // 8-pixel groups per staged row
+    constexpr int RPI = 64 / V8; // rows per wave-instruction
+#define ORE_HSTG(R, C) (TN >= 64 ? (R) * TN + ((C) ^ ((((R) >> 2) & 1) * 32)) : ((R) ^ (((R) >> 2) & 1)) * TN + (C))
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int r = (e & 3) + 8 * (e >> 2) + 4 * lrow;
+          float v = acc[i][j][e] + sbias[wm0 + i * 32 + r];
+          if (p.relu) v = fmaxf(v, 0.0f);
+          stg[ORE_HSTG(r, j * 32 + lcol)] = v;
+        }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int c8 = (lane % V8) * 8;
+      const int n = n0 + wn0 + c8;
+      const int img = n / YPS;
+      const int pix = n - img * YPS;
+      const bool nok = n < p.Ntot;
+#pragma unroll
+      for (int rr = 0; rr < 32; rr += RPI) {
+        const int r = rr + lane / V8;
+        const int m = m0 + wm0 + i * 32 + r;
+        half8 h;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) h[u] = (_Float16)stg[ORE_HSTG(r, c8 + u)];
+        if (nok && m < p.M) *reinterpret_cast<half8*>(y + (unsigned)(img * (int)p.y_nstride + m * YPS + pix)) = h;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+#undef ORE_HSTG
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = n0 + wn0 + j * 32 + lcol;

@@ -165,7 +165,10 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
     const int64_t extent = ((N - 1) * x_nstride + C * x_ps) * int64_t(x_es);
     p.x_bytes = (extent > 0 && extent < (int64_t(1) << 31)) ? extent : 0;
   }
-  p.vec_out = (y_ps % 4 == 0 && y_nstride % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
+  {  // 16-B epilogue stores: 4 floats or 8 halves per store
+    const int64_t g = pln.f16 ? 8 : 4;
+    p.vec_out = (y_ps % g == 0 && y_nstride % g == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
+  }
   if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;  // tuning knob
   p.is1x1 = (kh == 1 && kw == 1 && sh == 1 && sw == 1 && win.pt == 0 && win.pl == 0 && win.Ho == H && win.Wo == W &&
              x_ps == y_ps);
@@ -205,7 +208,10 @@ ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int6
   p.Mp = pln.Mp;
   p.x_f32 = x_es == 4 ? 1 : 0;
   p.x_bytes = 0;  // register path: the window max needs the values
-  p.vec_out = (y_ps % 4 == 0 && y_nstride % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
+  {
+    const int64_t g = pln.f16 ? 8 : 4;
+    p.vec_out = (y_ps % g == 0 && y_nstride % g == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
+  }
   if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;
   p.pool = 1;
   p.pool_sh = int(psh); p.pool_sw = int(psw); p.pool_pt = int(pwin.pt); p.pool_pl = int(pwin.pl);
