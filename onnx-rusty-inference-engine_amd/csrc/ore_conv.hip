@@ -41,6 +41,12 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));  // first-class vecto
 #else
 #define ORE_FRAG_PIN
 #endif
+#ifndef ORE_VEC_EPI_ON
+#define ORE_VEC_EPI_ON 1
+#endif
+// the LDS-staged 16-B epilogue costs VGPRs (128x128: 135 vs 104-117 without it); the
+// warp-specialised variant keeps the scalar epilogue for its 2 blocks/CU
+#define ORE_WS_VEC_EPI (ORE_VEC_EPI_ON && !WS)
 #ifndef ORE_CONV_MINBLOCKS
 #define ORE_CONV_MINBLOCKS 2  // __launch_bounds__ minimum blocks per CU (VGPR budget)
 #endif
@@ -50,8 +56,11 @@ enum { B1X1 = 0, BGATHER = 1, BPOOL = 2 };  // BPOOL: B = 3x3 window max of the 
 // DMA: the B tile goes global -> LDS by buffer_load ... lds (no VGPR staging, no LDS store
 // pass); a tap outside the image gets an out-of-range offset, which the buffer bounds check
 // turns into a 0 -- the reference's zero padding -- with no select.
-template <int BM, int BN, int WM, int WN, int BK, int BMODE, int DMA>
-__global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(ConvParams p) {
+// WS (warp-specialised): 512 threads; waves 0-3 only read LDS and issue MFMAs, waves 4-7 only
+// gather the next K tile into the other LDS buffer.  Both roles meet at the same barrier once
+// per K tile, so the MFMA waves' instruction stream carries no global loads or gather math.
+template <int BM, int BN, int WM, int WN, int BK, int BMODE, int DMA, int WS = 0>
+__global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_kernel(ConvParams p) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 32, FN = TN / 32;
   constexpr int AS = BM + 4;                 // LDS row stride of the A tile (16-B aligned rows)
@@ -63,14 +72,16 @@ __global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(Conv
 
   // one LDS array: the A/B double buffers of the main loop, reused by the epilogue's per-wave
   // [32][TN] output staging (all LDS in one __shared__ object, cdna_hip_programming.md §5)
-  constexpr int MAIN_FLOATS = 2 * BK * AS + 2 * BK * BN;
+  constexpr int NBUF = WS ? 3 : 2;  // WS: the loaders keep one K tile in flight across the barrier
+  constexpr int MAIN_FLOATS = NBUF * BK * AS + NBUF * BK * BN;
   constexpr int EPI_FLOATS = 4 * 32 * TN;
   __shared__ __attribute__((aligned(16))) float smem[MAIN_FLOATS > EPI_FLOATS ? MAIN_FLOATS : EPI_FLOATS];
   float(*As)[BK][AS] = reinterpret_cast<float(*)[BK][AS]>(smem);
-  float(*Bs)[BK][BN] = reinterpret_cast<float(*)[BK][BN]>(smem + 2 * BK * AS);
+  float(*Bs)[BK][BN] = reinterpret_cast<float(*)[BK][BN]>(smem + NBUF * BK * AS);
   __shared__ float sbias[BM];
 
-  const int tid = threadIdx.x;
+  const int tid = WS ? (threadIdx.x & 255) : threadIdx.x;  // WS: both roles index 0..255
+  const bool loader = WS && threadIdx.x >= 256;              // wave-uniform role
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm0 = (wave / WN) * TM;
@@ -206,15 +217,22 @@ __global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(Conv
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
   const int ntk = (K + BK - 1) / BK;
-  {
+  if (!WS || loader) {
     floatx4 ra[AVEC];
     float rb[BLOADS];
     bool rok[BLOADS];
     ORE_LOAD_TILE(ra, rb, rok, 0, 0);
     ORE_STORE_TILE(ra, rb, rok, 0);
+    if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the B tile has landed in LDS
   }
-  if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the B tile has landed in LDS
   __syncthreads();
+  // WS loaders: K tile 1 in flight (A in registers, B by LDS-DMA into buffer 1)
+  floatx4 wra[WS ? AVEC : 1];
+  {
+    float rb[BLOADS];
+    bool rok[BLOADS];
+    if (WS && loader && ntk > 1) ORE_LOAD_TILE(wra, rb, rok, BK, 1);
+  }
   const int lrow = lane >> 5, lcol = lane & 31;
 // fragments for k-step kk+2 are read from LDS before the MFMAs of k-step kk are issued
 // KEND: k-steps of this tile that carry data (BK except on the last tile, where the zero rows
@@ -242,6 +260,34 @@ __global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(Conv
       ORE_PRIO(0);                                                                                   \
     }                                                                                                \
   }
+  if (WS) {
+    // three LDS buffers: while the MFMA waves consume tile t (buffer t % 3) the loaders retire
+    // tile t + 1 (its LDS-DMA + the A store) and issue tile t + 2, which stays in flight across
+    // the barrier (raw s_barrier, counted waits: cdna_hip_programming.md "Pipelining across
+    // barriers").  Buffer (t + 2) % 3 was last read in tile t - 1, before the previous barrier.
+    static_assert(!WS || DMA, "the warp-specialised loop streams B by LDS-DMA");
+    const int kend = __builtin_amdgcn_readfirstlane((K - (ntk - 1) * BK + 1) & ~1);
+    for (int t = 0; t < ntk; ++t) {
+      const int buf = t % 3;
+      if (loader) {
+        if (t + 1 < ntk) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t + 1: A registers + B DMA landed
+          float rb[BLOADS];
+          bool rok[BLOADS];
+          ORE_STORE_TILE(wra, rb, rok, (t + 1) % 3);
+          if (t + 2 < ntk) ORE_LOAD_TILE(wra, rb, rok, (t + 2) * BK, (t + 2) % 3);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the A stores are in LDS
+      } else {
+        ORE_COMPUTE_TILE(buf, t + 1 < ntk ? BK : kend);
+        // every read of buffer t % 3 has returned before the barrier: the loaders refill it in
+        // tile t + 1 (the asm's memory clobber also keeps the reads from sinking past it)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+    if (loader) return;  // no block barrier follows: the epilogue is per wave
+  } else {
   // steady state: prefetch tile t+1 into registers, MFMAs on tile t, publish t+1 to LDS
   for (int t = 0; t < ntk - 1; ++t) {
     const int buf = t & 1;
@@ -265,18 +311,19 @@ __global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(Conv
     const int kend = __builtin_amdgcn_readfirstlane((K - (ntk - 1) * BK + 1) & ~1);
     ORE_COMPUTE_TILE((ntk - 1) & 1, kend);
   }
+  }  // !WS
 #undef ORE_COMPUTE_TILE
 #undef ORE_LOAD_TILE
 #undef ORE_STORE_TILE
 
   // ---- epilogue: + bias, optional Relu, store to NCHW (possibly a channel slice)
   float* __restrict__ y = p.y;
-  if (p.vec_out) {
+  if (ORE_WS_VEC_EPI && p.vec_out) {
     // 16-B stores: each wave stages 32 output rows x TN pixels in its own LDS slice (column
     // halves swapped every 4 rows so the two lane halves' writes hit different banks), then
     // writes whole pixel runs with float4 stores.  Host guarantees y_ps % 4 == 0, 16-B aligned
     // image/plane bases and Ntot % 4 == 0, so no float4 straddles an image.
-    __syncthreads();  // every wave is done with the A/B tiles
+    if (!WS) __syncthreads();  // every wave is done with the A/B tiles (WS: the loop's last barrier)
     float* stg = smem + wave * (32 * TN);
     constexpr int V4 = TN / 4;            // float4 per staged row
     constexpr int RPI = 64 / V4;          // rows per wave-instruction
@@ -669,7 +716,7 @@ static int env_int(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int WS = 0>
 static void launch_conv_cfg(const ConvParams& p0, hipStream_t s) {
   constexpr int BK = 16;
   ConvParams p = p0;
@@ -677,6 +724,14 @@ static void launch_conv_cfg(const ConvParams& p0, hipStream_t s) {
   p.ntiles = (int)((p.Ntot + BN - 1) / BN);
   dim3 grid(p.mtiles * p.ntiles), block(256);
   const bool dma = p.x_bytes > 0 && env_int("ORE_CONV_DMA", 1) != 0;  // tuning knob
+  if (WS && dma && !p.pool) {  // the warp-specialised loop streams B by LDS-DMA
+    const dim3 wblock(512);
+    if (p.is1x1)
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, B1X1, 1, 1>), grid, wblock, 0, s, p);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BGATHER, 1, 1>), grid, wblock, 0, s, p);
+    return;
+  }
   if (p.pool) {
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BPOOL, 0>), grid, block, 0, s, p);
   } else if (p.is1x1) {
@@ -817,6 +872,15 @@ static void launch_win_cfg(const ConvParams& p0, const ConvPlan& pln, hipStream_
 void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
   if (pln.f16) {
     launch_conv_f16(p, pln.cfg, s);
+    return;
+  }
+  if (pln.cfg >= 8) {  // warp-specialised variants of tiles 0-3
+    switch (pln.cfg) {
+      case 8: launch_conv_cfg<128, 128, 2, 2, 1>(p, s); break;
+      case 9: launch_conv_cfg<96, 128, 1, 4, 1>(p, s); break;
+      case 10: launch_conv_cfg<64, 128, 2, 2, 1>(p, s); break;
+      default: launch_conv_cfg<32, 256, 1, 4, 1>(p, s); break;
+    }
     return;
   }
   if (pln.cfg >= 4) {

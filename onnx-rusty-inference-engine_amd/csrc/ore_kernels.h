@@ -82,7 +82,8 @@ void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, 
 void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s);
 // LDS-free, barrier-free variant (ore_conv_direct.hip): tiles 4-7 (needs p.x_bytes > 0)
 void launch_conv_direct(const ConvParams& p, int tile, hipStream_t s);
-constexpr int CONV_TILES_F32 = 8;  // 0-3 conv_gemm_kernel, 4-7 conv_direct_kernel (ORE_CONV_CFG only)
+constexpr int CONV_TILES_F32 = 12;  // 0-3 conv_gemm_kernel, 4-7 conv_direct_kernel (ORE_CONV_CFG only),
+                                    // 8-11 conv_gemm_kernel warp-specialised (512 threads)
 constexpr int CONV_TILES_F16 = 4;
 constexpr int CONV_TILES_AUTOTUNE = 4;  // the direct tiles measured 15-80 % slower on every SqueezeNet layer
 void launch_maxpool(const PoolParams& p, hipStream_t s);

@@ -94,11 +94,12 @@ def test_conv2d(gpu_ctx, case, fuse_relu, window, monkeypatch):
     assert np.all(err <= 2e-6 * bound + 1e-30), f"max err {err.max()} vs bound {(2e-6 * bound).max()}"
 
 
-@pytest.mark.parametrize("tile", ["4", "5", "6", "7"])
+@pytest.mark.parametrize("tile", ["4", "5", "6", "7", "8", "9", "10", "11"])
 @pytest.mark.parametrize("case", CONV_CASES[::2] + CONV_CASES[14:16])
 def test_conv2d_direct_bit_identical(gpu_ctx, case, tile, monkeypatch):
-    """The LDS-free direct kernel (tiles 4-7) runs the same k-ordered MFMA chain per output as
-    the LDS-staged kernel (tile 0): bit-identical outputs, and within tolerance of the oracle."""
+    """The LDS-free direct kernel (tiles 4-7) and the warp-specialised kernel (tiles 8-11) run
+    the same k-ordered MFMA chain per output as the LDS-staged kernel (tile 0): bit-identical
+    outputs, and within tolerance of the oracle."""
     import ore
     N, C, H, W, M, kh, kw, auto_pad, pads, strides, with_bias = case
     rng = np.random.default_rng(zlib.crc32(repr(case).encode()) ^ 0x5a5a)
