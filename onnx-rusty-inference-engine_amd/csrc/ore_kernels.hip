@@ -169,7 +169,25 @@ __global__ __launch_bounds__(256) void maxpool_planes_kernel(PoolParams p, int p
     const int n = (int)(pl / p.C), c = (int)(pl - (long long)n * p.C);
     const T* __restrict__ xq = reinterpret_cast<const T*>(p.x) + (long long)n * p.x_nstride + (long long)c * p.x_ps;
     T* tq = tile + q * HW;
-    int i = tid;
+    int i0 = 0;  // elements copied by the 16-B path
+    if (((reinterpret_cast<uintptr_t>(xq) | reinterpret_cast<uintptr_t>(tq)) & 15) == 0) {
+      // 16-B copies (4 floats / 8 halves per lane), 4 in flight per thread
+      constexpr int EV = 16 / (int)sizeof(T);
+      const int nv = HW / EV;
+      const uint4* __restrict__ xv = reinterpret_cast<const uint4*>(xq);
+      uint4* tv = reinterpret_cast<uint4*>(tq);
+      int i = tid;
+      for (; i + 3 * 256 < nv; i += 4 * 256) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = xv[i + u * 256];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) tv[i + u * 256] = v[u];
+      }
+      for (; i < nv; i += 256) tv[i] = xv[i];
+      i0 = nv * EV;
+    }
+    int i = i0 + tid;
     for (; i + 7 * 256 < HW; i += 8 * 256) {
       T v[8];
 #pragma unroll
