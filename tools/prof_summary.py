@@ -1,9 +1,14 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 --kernel-trace --stats run of bench.py: per-kernel-class launches and
 average duration, next to bench.py's own HIP-event figure (roofline.per_launch_avg_us).
-usage: python tools/prof_summary.py <run_kernel_stats.csv> [bench_json] > profiles/rNN_prof_summary.txt"""
+usage: python tools/prof_summary.py <run_kernel_stats.csv> [bench_json] > profiles/rNN_prof_summary.txt
+
+With run_kernel_trace.csv beside the stats file, the classes are also computed over the timed
+steps only (the last `steps` x 31 dispatches of the run: autotune candidates and warm-up runs
+excluded), which is what bench.py's per_launch_avg_us measures."""
 import csv
 import json
+import os
 import sys
 
 CLASSES = [("conv (f32 MFMA)", "conv_gemm_kernel"), ("conv (f16 MFMA)", "conv_f16_kernel"),
@@ -21,8 +26,20 @@ def main():
         calls = sum(int(r["Calls"]) for r in sel)
         tot = sum(float(r["TotalDurationNs"]) for r in sel)
         print(f"{label:24s} {calls:9d} {tot / 1e6:10.3f} {tot / calls / 1e3:9.2f}")
-    if len(sys.argv) > 2:
-        b = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+    trace = os.path.join(os.path.dirname(sys.argv[1]), "run_kernel_trace.csv")
+    bench = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1]) if len(sys.argv) > 2 else None
+    if os.path.exists(trace) and bench:
+        disp = [r for r in csv.DictReader(open(trace)) if "ore::" in r["Kernel_Name"]]
+        disp.sort(key=lambda r: int(r["Dispatch_Id"]))
+        last = disp[-31 * int(bench["steps"]):]
+        print(f"\ntimed steps only (last {len(last)} dispatches = {bench['steps']} steps x 31):")
+        for label, key in CLASSES:
+            sel = [r for r in last if key in r["Kernel_Name"]]
+            if sel:
+                tot = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in sel)
+                print(f"{label:24s} {len(sel):9d} {tot / 1e6:10.3f} {tot / len(sel) / 1e3:9.2f}")
+    if bench:
+        b = bench
         r = b.get("roofline", {})
         print(f"\nbench.py (HIP events, same run): conv per_launch_avg_us = {r.get('per_launch_avg_us')}, "
               f"achieved {r.get('achieved')} {r.get('unit')} = {r.get('frac')} of {r.get('peak')}")
