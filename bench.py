@@ -32,7 +32,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU per step (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: this many images per step split over the GPUs (SURVEY §8(d) B=2048)")
     ap.add_argument("--hw", type=int, default=224)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
@@ -126,7 +128,10 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    B = args.batch
+    strong = args.global_batch > 0
+    if strong and args.global_batch % world:
+        raise SystemExit(f"--global-batch {args.global_batch} does not split over {world} GPUs")
+    B = args.global_batch // world if strong else args.batch
     model_bytes = squeezenet.build(args.hw)
     ctx = ore.Context(local)
     model = ore.Model(ctx, model_bytes, max_batch=B, precision=args.precision)
@@ -177,14 +182,14 @@ def main():
         result = {
             "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (seeded U(-50,50) 3x224x224 images; seeded He-normal SqueezeNet-1.0 weights)",
             "config": {"workload": f"SqueezeNet-1.0 (66 nodes, 818.9 MMAC/img) "
                                    f"{'fp16 (config 5: f16 activations/weights, f32 accumulate)' if f16 else 'fp32'} "
                                    f"inference, batch {B} per GPU, 3x{args.hw}x{args.hw}",
                        "model": "squeezenet1.0-8 topology, synthetic weights", "global_batch": world * B,
                        "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}",
-                       "collective": "RCCL all_gather of [256,1000] logits per step" if world > 1 else None},
+                       "collective": f"RCCL all_gather of [{B},1000] logits per step" if world > 1 else None},
         }
         result["conv_tiles"] = {"autotuned": not args.no_autotune,
                                 "tile_per_conv": [ore.Model.TILE_NAMES[t] for t in model.tiles() if t >= 0]}
