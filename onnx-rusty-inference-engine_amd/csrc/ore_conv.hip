@@ -766,10 +766,11 @@ static const int CFG_BN[4] = {128, 128, 128, 256};
 
 
 ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
-                   bool is1x1, bool f16) {
+                   bool is1x1, bool f16, int xmode) {
   (void)H; (void)W; (void)pt;
   ConvPlan pln{};
   pln.f16 = f16 ? 1 : 0;
+  pln.xmode = f16 ? xmode : 0;
   pln.cfg = conv_tile_config(M);
   const int K = C * kh * kw;
   // short-K 1x1 layers (SqueezeNet's expand1x1, K <= 64) are epilogue/write bound: the 1x4-wave
@@ -840,7 +841,8 @@ size_t conv_packed_bytes(const ConvPlan& pln) {
 void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, const ConvPlan& pln, float* wp,
                  hipStream_t s) {
   if (pln.f16) {
-    launch_pack_weights_f16(w, kmajor_src, M, C * kh * kw, pln.Mp, wp, s);
+    (void)kmajor_src;  // f16 plans are convs only (MatMul stays f32)
+    launch_pack_weights_f16(w, pln.xmode, M, C, kh, kw, pln.Mp, wp, s);
     return;
   }
   if (!pln.window) {
@@ -871,7 +873,7 @@ static void launch_win_cfg(const ConvParams& p0, const ConvPlan& pln, hipStream_
 
 void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
   if (pln.f16) {
-    launch_conv_f16(p, pln.cfg, s);
+    launch_conv_f16(p, pln.cfg, pln.xmode, s);
     return;
   }
   if (pln.cfg >= 8) {  // warp-specialised variants of tiles 0-3

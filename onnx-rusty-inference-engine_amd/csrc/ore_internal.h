@@ -83,7 +83,7 @@ ore_status resolve_window(ore_ctx* ctx, int auto_pad, const int64_t* pads, int n
 // ---------------------------------------------------------------- launches over resolved geometry
 // Kernel plan of a conv (or MatMul as a 1x1 conv) over resolved geometry.
 ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
-                   const Window& win, bool f16 = false);
+                   const Window& win, bool f16 = false, int xmode = 0);
 // wp: weights packed by launch_pack for plan `pln`
 // ktab: gather table (launch_ktab) for non-1x1 geometry on the gather kernel
 ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
@@ -91,6 +91,12 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
                     const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, float* y,
                     int64_t y_nstride, int64_t x_ps = 0, int64_t y_ps = 0,  // plane strides, 0 = dense
                     int x_es = 4);  // input element bytes (2: f16; only with an f16 plan, whose output is f16)
+// f16 plan (f16 models): y is NHWC f16 with pixel stride y_ps; x is the f32 NCHW model input
+// (F16_X_NCHW32, plane stride x_ps) or NHWC f16 with pixel stride x_ps.  ktab per plan.xmode.
+ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_t N, int64_t C, int64_t H, int64_t W,
+                        int64_t x_nstride, int64_t x_ps, const void* wp, const int2* ktab, int64_t M, int64_t kh,
+                        int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, void* y,
+                        int64_t y_nstride, int64_t y_ps);
 // 1x1 conv over the 3x3 MaxPool (window pwin, strides psh/psw) of x [C][pH][pW] (plane stride x_ps):
 // the pooled tensor is never materialised (ORE_FUSE_POOL_CONV)
 ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t pH,
@@ -107,5 +113,9 @@ ore_status run_maxpool(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64
                        int64_t x_nstride, int64_t kh, int64_t kw, const Window& win, int64_t sh, int64_t sw,
                        float* y, int64_t y_nstride, int64_t x_ps = 0, int64_t y_ps = 0,
                        int es = 4);  // element bytes of x and y
+// MaxPool over NHWC f16 (f16 models); x_cs / y_cs: pixel strides
+ore_status run_maxpool_nhwc(ore_ctx* ctx, const void* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
+                            int64_t x_cs, int64_t kh, int64_t kw, const Window& win, int64_t sh, int64_t sw, void* y,
+                            int64_t y_nstride, int64_t y_cs);
 
 }  // namespace ore

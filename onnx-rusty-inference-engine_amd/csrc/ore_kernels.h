@@ -25,10 +25,12 @@ struct ConvParams {
   int Mp;              // row stride of wp (conv_packed_mp(M))
   int mtiles, ntiles;  // filled by the launcher
   int vec_out;         // 16-B epilogue stores (y_ps, y_nstride % 4 == 0 and a 16-B aligned y)
-  int x_f32;           // f16 kernel: the input is f32 (rounded to f16 while staging)
+  int x_f32;           // f16 kernel: the input is the f32 NCHW model input (rounded to f16 while staging);
+                       // otherwise f16 NHWC with pixel stride x_ps (f16 kernels always write NHWC,
+                       // pixel stride y_ps, columns dense over Ho*Wo: Ntot = N*P)
   long long x_bytes;   // bytes from x to the end of its last valid element (0: no buffer DMA path)
-  // fused MaxPool (ORE_FUSE_POOL_CONV): x is the PRE-pool tensor [pool_H][pool_W] planes and the
-  // conv (1x1) reads each B element as the 3x3 window max at stride (pool_sh, pool_sw)
+  // fused MaxPool (ORE_FUSE_POOL_CONV, f32 only): x is the PRE-pool tensor [pool_H][pool_W] planes
+  // and the conv (1x1) reads each B element as the 3x3 window max at stride (pool_sh, pool_sw)
   int pool;            // 1: BPOOL operand mode
   int pool_sh, pool_sw, pool_pt, pool_pl, pool_H, pool_W;
   // window-staged kernel (filled by the launcher from the ConvPlan)
@@ -37,7 +39,8 @@ struct ConvParams {
 
 // Per-layer kernel choice and weight layout (see plan_conv in ore_conv.hip).
 struct ConvPlan {
-  int f16;             // 1: conv_f16_kernel (f16 weights Wh[Mp][Kp] and f16 output)
+  int f16;             // 1: conv_f16_kernel (f16 weights Wh[Mp][Kp] and f16 NHWC output)
+  int xmode;           // f16: F16_X_NCHW32 / F16_X_NHWC_ELEM / F16_X_NHWC_VEC (operand gather, k order)
   int window;          // 1: conv_win_kernel (stage-major packed weights), 0: conv_gemm_kernel
   int cfg;             // block tile (0: 128x128, 1: 96x128, 2: 64x128, 3: 32x256)
   int bch, ks, nst;    // window: channels / K rows per stage, stages
@@ -57,6 +60,17 @@ struct PoolParams {
   int es;              // element bytes: 4 (f32) or 2 (f16)
 };
 
+// MaxPool over channels-last f16 (f16 models): element (n, c, h, w) at n*nstride + (h*W + w)*cs + c
+struct NhwcPoolParams {
+  const _Float16* x;
+  _Float16* y;
+  int N, C, H, W;
+  int kh, kw, sh, sw, pt, pl;
+  int Ho, Wo;
+  int x_cs, y_cs;      // pixel strides (elements, >= C)
+  long long x_nstride, y_nstride;
+};
+
 struct AddParams {
   const float* a;
   const float* b;
@@ -72,9 +86,24 @@ int conv_packed_kp(int K);  // padded K of the packed weights
 void launch_pack_weights(const float* w, bool kmajor_src, int M, int K, int Mp, float* wp, hipStream_t s);
 void launch_ktab(int2* ktab, int K, int kh, int kw, int x_ps, int W, hipStream_t s);
 ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
-                   bool is1x1, bool f16 = false);
-void launch_pack_weights_f16(const float* w, bool kmajor_src, int M, int K, int Mp, void* wh, hipStream_t s);
-void launch_conv_f16(const ConvParams& p, int cfg, hipStream_t s);
+                   bool is1x1, bool f16 = false, int xmode = 0);
+// f16 conv operand modes (ConvPlan::xmode), chosen by the input's layout:
+enum {
+  F16_X_NCHW32 = 0,     // f32 NCHW model input, per-element gather, k order (c, r, s) (the reference's)
+  F16_X_NHWC_ELEM = 1,  // f16 NHWC input with C % 8 != 0: per-element gather, k order (r, s, c)
+  F16_X_NHWC_VEC = 2,   // f16 NHWC input, C % 8 == 0: one 16-B load per (pixel, 8 channels), k order (r, s, c)
+};
+// Wh[Mp][Kp] = f16(W[M][C][kh][kw]) in the k order of `xmode` (MatMul stays f32)
+void launch_pack_weights_f16(const float* w, int xmode, int M, int C, int kh, int kw, int Mp, void* wh, hipStream_t s);
+// gather tables of the f16 conv: per k for F16_X_NCHW32 (launch_ktab) / F16_X_NHWC_ELEM, per group of 8 k
+// for F16_X_NHWC_VEC; cs = the input's pixel stride
+void launch_ktab_nhwc(int2* ktab, int C, int kh, int kw, int cs, int W, bool vec, hipStream_t s);
+void launch_maxpool_nhwc(const NhwcPoolParams& p, hipStream_t s);
+// GlobalAveragePool of NHWC f16 -> f32 y[n][c]
+void launch_gap_nhwc(const void* x, float* y, int N, int C, int HW, int cs, long long nstride, hipStream_t s);
+// Concat along channels of two dense NHWC f16 values (pixels = N*H*W)
+void launch_concat_nhwc(const void* a, const void* b, void* y, long long pixels, int Ca, int Cb, hipStream_t s);
+void launch_conv_f16(const ConvParams& p, int cfg, int xmode, hipStream_t s);
 size_t conv_packed_bytes(const ConvPlan& pln);
 // packs ONNX weights [M][C][kh][kw] (or MatMul [K][M]) in the layout the plan's kernel reads
 void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, const ConvPlan& pln, float* wp,

@@ -42,15 +42,20 @@ struct Value {
   int alias_of = -1;               // view into another value's storage
   int64_t alias_ch = 0;            // concat slice: first channel inside the base
   bool slice = false;              // alias is a channel slice of its base (Concat in place)
-  int64_t ps = 0;                  // 4-D activations: channel-plane stride (>= H*W; padded planes)
+  int64_t ps = 0;                  // 4-D activations: channel-plane stride (>= H*W; padded planes),
+                                   // or for nhwc values the pixel stride (the root's channel count)
   int es = 4;                      // element bytes: 4 f32, 2 f16 (f16 models, ORE_LOAD_F16)
+  bool nhwc = false;               // channels-last storage (every 4-D f16 activation)
   bool elided = false;             // produced and consumed inside one fused kernel
   int64_t arena_off = -1;          // byte offset in the arena (root values)
   int first = -1, last = -1;       // live interval in step indices
   int uses = 0;                    // consumer count (node inputs)
 
   // elements between images in this value's own storage (roots)
-  int64_t image_stride() const { return (ndim == 4 && ps) ? dims[1] * ps : per_image(); }
+  int64_t image_stride() const {
+    if (ndim != 4 || !ps) return per_image();
+    return nhwc ? dims[2] * dims[3] * ps : dims[1] * ps;
+  }
   int64_t per_image() const {
     int64_t s = 1;
     for (int i = 1; i < ndim; ++i) s *= dims[i];
@@ -347,6 +352,8 @@ ore_status build_node(ore_model* m, const Node& n, Step* s) {
     for (int i = 1; i < 4; ++i)
       if (i != axis && A.dims[i] != B.dims[i]) return err(m, ORE_ERR_INVALID, "Concat '" + n.name + "': shape mismatch");
     if (A.es != B.es) return err(m, ORE_ERR_UNSUPPORTED, "Concat '" + n.name + "': inputs of different precision");
+    if (A.es == 2 && axis != 1)
+      return err(m, ORE_ERR_UNSUPPORTED, "Concat '" + n.name + "': f16 (channels-last) activations concatenate along axis 1 only");
     s->kind = S_CONCAT; s->in0 = a; s->in1 = b; s->axis = axis;
     int y = new_value(m, n.outputs[0]);
     Value& Y = m->values[y];
@@ -411,6 +418,8 @@ ore_status build_node(ore_model* m, const Node& n, Step* s) {
     }
     if (ns[0] != 1 || ns[1] != X.per_image())
       return err(m, ORE_ERR_UNSUPPORTED, "Reshape '" + n.name + "': activation reshape must be [1 or 0, C*H*W] per image");
+    if (X.es == 2 && X.dims[2] * X.dims[3] != 1)
+      return err(m, ORE_ERR_UNSUPPORTED, "Reshape '" + n.name + "': f16 activations are channels-last; flattening one is not supported");
     s->kind = S_COPY; s->in0 = x;
     int y = new_value(m, n.outputs[0]);
     Value& Y = m->values[y];
@@ -459,6 +468,7 @@ ore_status plan(ore_model* m) {
   m->steps = m->base_steps;
   for (auto& v : m->values) {
     v.alias_of = -1; v.alias_ch = 0; v.slice = false; v.ps = 0; v.elided = false; v.arena_off = -1;
+    v.nhwc = !v.is_const && v.es == 2 && v.ndim == 4;
     v.first = v.last = -1;
   }
   count_uses(m, m->steps);
@@ -485,7 +495,7 @@ ore_status plan(ore_model* m) {
     count_uses(m, m->steps);
   }
   // (1b) 3x3 MaxPool -> its only consumer, a plain 1x1 Conv: the pool runs in the conv's gather
-  if (m->fusion & ORE_FUSE_POOL_CONV) {
+  if ((m->fusion & ORE_FUSE_POOL_CONV) && !m->f16) {
     for (size_t i = 0; i < m->steps.size(); ++i) {
       Step& pl = m->steps[i];
       if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3) continue;
@@ -558,6 +568,10 @@ ore_status plan(ore_model* m) {
     for (size_t id = 0; id < m->values.size(); ++id) {
       Value& v = m->values[id];
       if (v.is_const || v.ndim != 4 || v.alias_of >= 0) continue;
+      if (v.nhwc) {  // channels-last f16: dense pixels of dims[1] channels
+        v.ps = v.dims[1];
+        continue;
+      }
       const int64_t P = v.dims[2] * v.dims[3];
       const int64_t Pp = (P + 31) / 32 * 32;
       const bool pad = (m->fusion & ORE_FUSE_CONCAT) && !dense[id] && !v.is_input && !v.is_output && Pp - P <= P / 20;
@@ -567,7 +581,8 @@ ore_status plan(ore_model* m) {
       if (v.alias_of >= 0 && v.ndim == 4) {
         const Value& r = m->values[root(int(&v - &m->values[0]))];
         v.ps = r.ps;
-        if (!v.slice && r.ps != r.dims[2] * r.dims[3])
+        if (v.nhwc != r.nhwc) return err(m, ORE_ERR_INVALID, "internal: view of a different layout (" + v.name + ")");
+        if (!v.slice && r.ps != (r.nhwc ? r.dims[1] : r.dims[2] * r.dims[3]))
           return err(m, ORE_ERR_INVALID, "internal: dense alias of a padded value (" + v.name + ")");
       }
   }
@@ -673,8 +688,13 @@ ore_status plan(ore_model* m) {
   for (const Step& st : m->steps) {
     if (st.kind != S_CONV || !st.ktab) continue;
     const Value& xv = m->values[st.in0];
-    launch_ktab(const_cast<int2*>(st.ktab), int(st.C * st.kh * st.kw), int(st.kh), int(st.kw), int(xv.ps ? xv.ps : st.H * st.W),
-                int(st.W), m->ctx->stream);
+    int2* kt = const_cast<int2*>(st.ktab);
+    if (st.plan.f16 && st.plan.xmode != F16_X_NCHW32)
+      launch_ktab_nhwc(kt, int(st.C), int(st.kh), int(st.kw), int(xv.ps), int(st.W), st.plan.xmode == F16_X_NHWC_VEC,
+                       m->ctx->stream);
+    else
+      launch_ktab(kt, int(st.C * st.kh * st.kw), int(st.kh), int(st.kw), int(xv.ps ? xv.ps : st.H * st.W), int(st.W),
+                  m->ctx->stream);
   }
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
     return err(m, ORE_ERR_HIP, "gather table build failed");
@@ -689,9 +709,9 @@ Ref ref_of(ore_model* m, int id) {
   if (v.is_const) return {v.cptr, 0, 0, 4};
   if (v.alias_of >= 0) {
     Ref base = ref_of(m, v.alias_of);
-    if (v.slice)
-      return {reinterpret_cast<float*>(reinterpret_cast<char*>(base.p) + v.alias_ch * base.ps * base.es), base.nstride,
-              base.ps, base.es};
+    if (v.slice)  // NCHW: the slice's first plane; NHWC: its first channel inside each pixel
+      return {reinterpret_cast<float*>(reinterpret_cast<char*>(base.p) + v.alias_ch * (v.nhwc ? 1 : base.ps) * base.es),
+              base.nstride, base.ps, base.es};
     return base;
   }
   if (v.is_input) return {const_cast<float*>(m->cur_in), v.image_stride(), v.ps, v.es};
@@ -699,31 +719,33 @@ Ref ref_of(ore_model* m, int id) {
   return {reinterpret_cast<float*>(m->arena + v.arena_off), v.image_stride(), v.ps, v.es};
 }
 
-// contiguous steps on f16 values (f16 models): Relu, GAP (f32 out), Concat, Dropout/Reshape copies
+// steps on NHWC f16 values (f16 models): Relu, GAP (f32 out), Concat (channels), Dropout copies
 ore_status launch_step_f16(ore_model* m, const Step& s, int64_t n) {
   ore_ctx* ctx = m->ctx;
   const Value& X = m->values[s.in0];
   const Ref x = ref_of(m, s.in0), y = ref_of(m, s.out);
-  if (x.nstride != X.per_image() || (X.ndim == 4 && x.ps && x.ps != X.dims[2] * X.dims[3]))
-    return err(m, ORE_ERR_INVALID, "internal: f16 step on a strided view");
   const int64_t count = n * X.per_image();
   if (count == 0) return ORE_OK;
+  if (s.kind == S_GAP) {
+    launch_gap_nhwc(x.p, reinterpret_cast<float*>(y.p), int(n), int(X.dims[1]), int(X.dims[2] * X.dims[3]), int(x.ps),
+                    x.nstride, ctx->stream);
+    ORE_HIP_CHECK(ctx, hipGetLastError());
+    return ORE_OK;
+  }
+  if (x.nstride != X.per_image() || y.nstride != m->values[s.out].per_image())
+    return err(m, ORE_ERR_INVALID, "internal: f16 step on a strided view");
   switch (s.kind) {
     case S_RELU: launch_relu_f16(x.p, y.p, count, ctx->stream); break;
-    case S_GAP: launch_gap(x.p, 2, y.p, n * X.dims[1], int(X.dims[2] * X.dims[3]), ctx->stream); break;
     case S_COPY:
       if (x.p != y.p)
         ORE_HIP_CHECK(ctx, hipMemcpyAsync(y.p, x.p, size_t(count) * 2, hipMemcpyDeviceToDevice, ctx->stream));
       break;
-    case S_CONCAT: {
+    case S_CONCAT: {  // axis 1 (build_node): per pixel, a's channels then b's
       const Value& B = m->values[s.in1];
       const Ref b = ref_of(m, s.in1);
-      if (b.nstride != B.per_image() || (b.ps && b.ps != B.dims[2] * B.dims[3]))
+      if (b.nstride != B.per_image() || s.axis != 1)
         return err(m, ORE_ERR_INVALID, "internal: f16 concat of a strided view");
-      int64_t outer = n, ia = 1, ib = 1;
-      for (int i = 1; i < int(s.axis); ++i) outer *= X.dims[i];
-      for (int i = int(s.axis); i < 4; ++i) { ia *= X.dims[i]; ib *= B.dims[i]; }
-      launch_concat(x.p, b.p, y.p, 2, outer, ia, ib, ctx->stream);
+      launch_concat_nhwc(x.p, b.p, y.p, n * X.dims[2] * X.dims[3], int(X.dims[1]), int(B.dims[1]), ctx->stream);
       break;
     }
     default: return err(m, ORE_ERR_UNSUPPORTED, "internal: step '" + s.name + "' has no f16 kernel");
@@ -739,6 +761,9 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
     case S_CONV: {
       const Ref x = ref_of(m, s.in0);
       const float* bias = s.in2 >= 0 ? m->values[s.in2].cptr : nullptr;
+      if (s.plan.f16)
+        return run_conv_f16(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.ktab, s.M, s.kh, s.kw, bias,
+                            s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps);
       if (s.pool)
         return run_conv_pool(ctx, s.plan, x.p, n, s.C, s.pH, s.pW, x.nstride, x.ps, s.pwin, s.psh, s.psw, s.wp, s.M, bias,
                              s.relu, y.p, y.nstride, y.ps, x.es);
@@ -752,6 +777,9 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
     }
     case S_MAXPOOL: {
       const Ref x = ref_of(m, s.in0);
+      if (x.es == 2)
+        return run_maxpool_nhwc(ctx, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.kh, s.kw, s.win, s.sh, s.sw, y.p,
+                                y.nstride, y.ps);
       return run_maxpool(ctx, x.p, n, s.C, s.H, s.W, x.nstride, s.kh, s.kw, s.win, s.sh, s.sw, y.p, y.nstride, x.ps,
                          y.ps, x.es);
     }
@@ -872,8 +900,12 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
   {
     size_t total_packed = 0;
     for (auto& s : m->base_steps) {
-      if (s.kind == S_CONV)
-        s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, m->f16);
+      if (s.kind == S_CONV) {
+        // f16 operand mode by the input's layout: the f32 NCHW model input, or NHWC f16 (16-B
+        // channel groups when C % 8 == 0)
+        const int xmode = m->values[s.in0].es == 4 ? F16_X_NCHW32 : s.C % 8 == 0 ? F16_X_NHWC_VEC : F16_X_NHWC_ELEM;
+        s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, m->f16, xmode);
+      }
       else if (s.kind == S_MATMUL)
         s.plan = conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win);
       else
@@ -1031,21 +1063,20 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
   const Ref r = ref_of(m, id);
   if (!r.p) return set_error(ctx, ORE_ERR_INVALID, "value '%s' has no f32 storage", name);
   const int64_t ns = v.is_const ? pe : r.nstride;
-  if (r.es == 2) {  // f16 storage: download the halves (padded planes included), convert on the host
-    const bool padded = v.ndim == 4 && r.ps && r.ps != v.dims[2] * v.dims[3];
-    const int64_t rows = padded ? n * v.dims[1] : n;
-    const int64_t row_elems = padded ? v.dims[2] * v.dims[3] : pe;
-    const int64_t pitch = padded ? r.ps : ns;
-    std::vector<uint16_t> tmp(size_t(rows * row_elems));
-    if (padded) {
+  if (r.es == 2) {  // f16 storage: download the halves, convert (and, channels-last, transpose) on the host
+    std::vector<uint16_t> tmp(size_t(n * pe));
+    if (v.nhwc) {  // per image: H*W pixels of C channels at pixel stride ps -> NCHW
+      const int64_t C = v.dims[1], HW = v.dims[2] * v.dims[3];
       for (int64_t i = 0; i < n; ++i)
-        ORE_HIP_CHECK(ctx, hipMemcpy2D(tmp.data() + i * pe, size_t(row_elems) * 2,
-                                       reinterpret_cast<const char*>(r.p) + i * ns * 2, size_t(pitch) * 2,
-                                       size_t(row_elems) * 2, size_t(v.dims[1]), hipMemcpyDeviceToHost));
-    } else {
-      ORE_HIP_CHECK(ctx, hipMemcpy2D(tmp.data(), size_t(pe) * 2, r.p, size_t(pitch) * 2, size_t(pe) * 2, size_t(n),
-                                     hipMemcpyDeviceToHost));
+        ORE_HIP_CHECK(ctx, hipMemcpy2D(tmp.data() + i * pe, size_t(C) * 2, reinterpret_cast<const char*>(r.p) + i * ns * 2,
+                                       size_t(r.ps) * 2, size_t(C) * 2, size_t(HW), hipMemcpyDeviceToHost));
+      for (int64_t i = 0; i < n; ++i)
+        for (int64_t q = 0; q < HW; ++q)
+          for (int64_t c = 0; c < C; ++c) host_dst[i * pe + c * HW + q] = half_bits_to_float(tmp[size_t(i * pe + q * C + c)]);
+      return ORE_OK;
     }
+    ORE_HIP_CHECK(ctx, hipMemcpy2D(tmp.data(), size_t(pe) * 2, r.p, size_t(ns) * 2, size_t(pe) * 2, size_t(n),
+                                   hipMemcpyDeviceToHost));
     for (size_t i = 0; i < tmp.size(); ++i) host_dst[i] = half_bits_to_float(tmp[i]);
     return ORE_OK;
   }

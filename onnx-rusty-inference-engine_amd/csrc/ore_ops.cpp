@@ -98,9 +98,9 @@ static bool contiguous(const ore_tensor* t) {
 static bool fits_i32(int64_t v) { return v >= 0 && v < (int64_t(1) << 31); }
 
 ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
-                   const Window& win, bool f16) {
+                   const Window& win, bool f16, int xmode) {
   return plan_conv(int(M), int(C), int(H), int(W), int(kh), int(kw), int(sh), int(sw), int(win.pt), int(win.pl),
-                   int(win.Ho), int(win.Wo), kh == 1 && kw == 1, f16);
+                   int(win.Ho), int(win.Wo), kh == 1 && kw == 1, f16, xmode);
 }
 
 size_t packed_bytes(const ConvPlan& pln) {
@@ -142,7 +142,7 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
                     const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, float* y,
                     int64_t y_nstride, int64_t x_ps, int64_t y_ps, int x_es) {
   if (N == 0) return ORE_OK;
-  if (!pln.f16 && x_es != 4) return set_error(ctx, ORE_ERR_INVALID, "internal: f32 conv on f16 input");
+  if (pln.f16 || x_es != 4) return set_error(ctx, ORE_ERR_INVALID, "internal: run_conv takes f32 plans and inputs");
   if (x_ps == 0) x_ps = H * W;
   if (y_ps == 0) y_ps = win.Ho * win.Wo;
   ConvParams p{};
@@ -160,15 +160,13 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
   p.y_nstride = y_nstride;
   p.relu = relu ? 1 : 0;
   p.Mp = pln.Mp;
-  p.x_f32 = x_es == 4 ? 1 : 0;
+  p.x_f32 = 1;
   {  // extent of x for the B-tile DMA path's buffer resource (32-bit byte offsets)
     const int64_t extent = ((N - 1) * x_nstride + C * x_ps) * int64_t(x_es);
     p.x_bytes = (extent > 0 && extent < (int64_t(1) << 31)) ? extent : 0;
   }
-  {  // 16-B epilogue stores: 4 floats or 8 halves per store
-    const int64_t g = pln.f16 ? 8 : 4;
-    p.vec_out = (y_ps % g == 0 && y_nstride % g == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
-  }
+  // 16-B epilogue stores of 4 floats
+  p.vec_out = (y_ps % 4 == 0 && y_nstride % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
   if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;  // tuning knob
   p.is1x1 = (kh == 1 && kw == 1 && sh == 1 && sw == 1 && win.pt == 0 && win.pl == 0 && win.Ho == H && win.Wo == W &&
              x_ps == y_ps);
@@ -190,7 +188,7 @@ ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int6
   if (x_ps == 0) x_ps = pH * pW;
   const int64_t P = pwin.Ho * pwin.Wo;
   if (y_ps == 0) y_ps = P;
-  if (!pln.f16 && x_es != 4) return set_error(ctx, ORE_ERR_INVALID, "internal: f32 conv on f16 input");
+  if (pln.f16 || x_es != 4) return set_error(ctx, ORE_ERR_INVALID, "internal: the pooled 1x1 conv is f32 only");
   ConvParams p{};
   p.x = x; p.wp = wp; p.ktab = nullptr; p.bias = bias; p.y = y;
   p.N = int(N); p.C = int(C); p.H = int(pwin.Ho); p.W = int(pwin.Wo);
@@ -206,12 +204,9 @@ ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int6
   p.relu = relu ? 1 : 0;
   p.is1x1 = 0;
   p.Mp = pln.Mp;
-  p.x_f32 = x_es == 4 ? 1 : 0;
+  p.x_f32 = 1;
   p.x_bytes = 0;  // register path: the window max needs the values
-  {
-    const int64_t g = pln.f16 ? 8 : 4;
-    p.vec_out = (y_ps % g == 0 && y_nstride % g == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
-  }
+  p.vec_out = (y_ps % 4 == 0 && y_nstride % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
   if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;
   p.pool = 1;
   p.pool_sh = int(psh); p.pool_sw = int(psw); p.pool_pt = int(pwin.pt); p.pool_pl = int(pwin.pl);
@@ -221,6 +216,65 @@ ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int6
       !fits_i32(p.Ntot + 256))
     return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
   launch_conv(p, pln, ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
+}
+
+ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_t N, int64_t C, int64_t H, int64_t W,
+                        int64_t x_nstride, int64_t x_ps, const void* wp, const int2* ktab, int64_t M, int64_t kh,
+                        int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, void* y,
+                        int64_t y_nstride, int64_t y_ps) {
+  if (N == 0) return ORE_OK;
+  if (!pln.f16) return set_error(ctx, ORE_ERR_INVALID, "internal: run_conv_f16 needs an f16 plan");
+  const bool nchw = pln.xmode == F16_X_NCHW32;
+  if (x_ps == 0) x_ps = nchw ? H * W : C;
+  if (y_ps == 0) y_ps = M;
+  if (nchw ? x_ps < H * W : x_ps < C) return set_error(ctx, ORE_ERR_INVALID, "input stride below its extent");
+  if (y_ps < M) return set_error(ctx, ORE_ERR_INVALID, "output pixel stride below the channel count");
+  if (pln.xmode == F16_X_NHWC_VEC &&
+      (C % 8 || x_ps % 8 || x_nstride % 8 || (reinterpret_cast<uintptr_t>(x) & 15)))
+    return set_error(ctx, ORE_ERR_INVALID, "internal: 16-B NHWC gather needs C, strides %% 8 == 0 and an aligned input");
+  if (!ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
+  ConvParams p{};
+  p.x = static_cast<const float*>(x); p.wp = static_cast<const float*>(wp); p.ktab = ktab; p.bias = bias;
+  p.y = static_cast<float*>(y);
+  p.N = int(N); p.C = int(C); p.H = int(H); p.W = int(W);
+  p.M = int(M); p.kh = int(kh); p.kw = int(kw); p.sh = int(sh); p.sw = int(sw);
+  p.pt = int(win.pt); p.pl = int(win.pl);
+  p.Ho = int(win.Ho); p.Wo = int(win.Wo);
+  p.K = int(C * kh * kw);
+  p.P = int(win.Ho * win.Wo);
+  p.x_ps = int(x_ps);
+  p.y_ps = int(y_ps);
+  p.Ntot = N * p.P;
+  p.x_nstride = x_nstride;
+  p.y_nstride = y_nstride;
+  p.relu = relu ? 1 : 0;
+  p.Mp = pln.Mp;
+  p.x_f32 = nchw ? 1 : 0;
+  p.vec_out = (M % 8 == 0 && y_ps % 8 == 0 && y_nstride % 8 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
+  if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;  // tuning knob
+  if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(int64_t(pln.krows) * pln.Mp) ||
+      !fits_i32(p.Ntot + 256) || (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))
+    return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
+  launch_conv(p, pln, ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
+}
+
+ore_status run_maxpool_nhwc(ore_ctx* ctx, const void* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
+                            int64_t x_cs, int64_t kh, int64_t kw, const Window& win, int64_t sh, int64_t sw, void* y,
+                            int64_t y_nstride, int64_t y_cs) {
+  if (N == 0) return ORE_OK;
+  NhwcPoolParams p{};
+  p.x = static_cast<const _Float16*>(x); p.y = static_cast<_Float16*>(y);
+  p.N = int(N); p.C = int(C); p.H = int(H); p.W = int(W);
+  p.kh = int(kh); p.kw = int(kw); p.sh = int(sh); p.sw = int(sw);
+  p.pt = int(win.pt); p.pl = int(win.pl);
+  p.Ho = int(win.Ho); p.Wo = int(win.Wo);
+  p.x_cs = int(x_cs ? x_cs : C); p.y_cs = int(y_cs ? y_cs : C);
+  p.x_nstride = x_nstride; p.y_nstride = y_nstride;
+  launch_maxpool_nhwc(p, ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());
   return ORE_OK;
 }
