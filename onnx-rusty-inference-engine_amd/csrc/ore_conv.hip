@@ -24,6 +24,30 @@ namespace ore {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));  // first-class vector (no struct copies)
+typedef int int4d __attribute__((ext_vector_type(4)));
+
+#ifndef ORE_DMA_ASM
+#define ORE_DMA_ASM 0  // 1: B-tile LDS-DMA by inline asm (measured equal: 5.38 vs 5.39 ms per step)
+#endif
+
+// One 4-B-per-lane LDS-DMA (lane i -> lds_addr + 4 i) through a raw buffer descriptor (offsets past
+// num_records read 0).  Inline asm rather than __builtin_amdgcn_raw_ptr_buffer_load_lds: with the
+// builtin, hipcc guards the first LDS read of every K tile with an s_waitcnt vmcnt that also waits
+// for the NEXT tile's A loads and first DMA (it cannot tell which LDS buffer a DMA writes), i.e. an
+// L2 round trip per K tile before the MFMAs start.  The kernel drains the DMA itself (vmcnt(0)
+// before the barrier that publishes the tile).  M0 is restored.
+__device__ __forceinline__ void lds_dma4(int4d rsrc, unsigned lds_addr, int voffset) {
+  int m0save;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dword %2, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(m0save)
+      : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voffset), "s"(rsrc)
+      : "memory");
+}
 
 #ifdef ORE_EXP_BFIXED  // timing experiment: B loads without the gather index math
 #define ORE_EXP_BFIXED_HOOK ok = bn_ok; off = (xoff > 0 ? xoff : 0) + ((k >> 4) & 1) * XPS;  /* channel 0/1, clamped: in bounds */
@@ -143,6 +167,8 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
   // writes 64 consecutive columns of one B row
   const __amdgpu_buffer_rsrc_t xrsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
+  const unsigned long long xb_ = reinterpret_cast<unsigned long long>(p.x);
+  const int4d xdesc = {(int)(unsigned)xb_, (int)((xb_ >> 32) & 0xffff), (int)p.x_bytes, 0x00020000};
   const int wcol0 = bcol & ~63;
   // the gather table through the constant address space: k is wave-uniform, so the entries
   // come in by scalar loads (s_load) into SGPRs instead of LDS / vector round trips
@@ -187,9 +213,13 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
         RB[j] = m_;                                                                                  \
         ROK[j] = ok;                                                                                 \
       } else if (DMA) {                                                                              \
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                    \
-            xrsrc, (__attribute__((address_space(3))) void*)&Bs[(DBUF)][krow + j * BROWS][wcol0], 4,  \
-            ok ? off * 4 : (int)0x80000000, 0, 0, 0);                                                \
+        if (ORE_DMA_ASM)                                                                             \
+          lds_dma4(xdesc, (unsigned)(size_t)(__attribute__((address_space(3))) float*)&Bs[(DBUF)][krow + j * BROWS][wcol0], \
+                   ok ? off * 4 : (int)0x80000000);                                                  \
+        else                                                                                         \
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                  \
+              xrsrc, (__attribute__((address_space(3))) void*)&Bs[(DBUF)][krow + j * BROWS][wcol0], 4, \
+              ok ? off * 4 : (int)0x80000000, 0, 0, 0);                                              \
       } else {                                                                                       \
         RB[j] = x[(unsigned)(ok ? off : 0)];                                                         \
         ROK[j] = ok; /* the zero select happens at the LDS store, after the MFMAs */                 \
@@ -785,7 +815,7 @@ ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, i
     const int bm = CFG_BM[c], rows = (M + bm - 1) / bm * bm;
     if (rows > pln.Mp) pln.Mp = rows;
   }
-  pln.krows = conv_packed_kp(K);
+  pln.krows = conv_packed_kp(f16 ? f16_conv_k(xmode, C, kh, kw) : K);
   pln.window = 0;
   if (f16) return pln;
   const int P = Ho * Wo;

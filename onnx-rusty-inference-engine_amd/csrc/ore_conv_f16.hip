@@ -6,7 +6,11 @@
 // i.e. ONE 16-B load, where an NCHW gather needs 8 scattered 2-byte loads with 8 bounds checks.
 //
 //   conv_f16_kernel<..., F16_X_NHWC_VEC>   every conv on an f16 activation with C % 8 == 0
-//   conv_f16_kernel<..., F16_X_NCHW32>     the first conv: the f32 NCHW model input, per-element
+//   conv_f16_kernel<..., F16_X_NHWC_PAIR>  the first conv (<= 4 input channels): the f32 NCHW model
+//                                          input converted to NHWC with 4 channels per pixel
+//                                          (nchw_to_nhwc4_kernel); one 8-B load per (tap, 4 channels),
+//                                          the 16-B fragment group = two horizontally adjacent taps
+//   conv_f16_kernel<..., F16_X_NCHW32>     a conv on an f32 NCHW value with > 4 channels: per-element
 //                                          gather in the reference's (c, r, s) order, rounded to f16
 //                                          while staging
 //   conv_f16_kernel<..., F16_X_NHWC_ELEM>  f16 NHWC input with C % 8 != 0 (per-element, (r, s, c))
@@ -21,16 +25,45 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
 #include "ore_kernels.h"
+
+#ifndef ORE_H_PREFETCH2
+#define ORE_H_PREFETCH2 0  // 1: two K stages of loads in flight (measured slower; see the main loop)
+#endif
 
 namespace ore {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float floatx16h __attribute__((ext_vector_type(16)));
+
+// B-operand registers of one K stage per thread, by operand mode
+template <int XMODE, int BV>
+struct BStage;
+template <int BV>
+struct BStage<F16_X_NHWC_VEC, BV> {  // one 16-B (pixel, 8-channel) load per task
+  half8 v[BV];
+  bool ok[BV];
+};
+template <int BV>
+struct BStage<F16_X_NHWC_PAIR, BV> {  // two 8-B (pixel, 4-channel) taps per task
+  half4 v[2 * BV];
+  bool ok[2 * BV];
+};
+template <int BV>
+struct BStage<F16_X_NCHW32, BV> {  // 8 scattered f32 elements per task
+  float v[8 * BV];
+  bool ok[8 * BV];
+};
+template <int BV>
+struct BStage<F16_X_NHWC_ELEM, BV> {  // 8 scattered f16 elements per task
+  _Float16 v[8 * BV];
+  bool ok[8 * BV];
+};
 
 template <int BM, int BN, int WM, int WN, int XMODE>
 __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
@@ -43,7 +76,7 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
   constexpr int BV = BN * 4 / 256;       // B tasks (one pixel x one 8-k group) per thread
   constexpr int QS = 256 / BN;           // per-element modes: k-group stride between a thread's tasks
   constexpr int SR = TM + 8;             // epilogue staging row: one pixel's TM channels + pad (halves)
-  constexpr bool VEC = XMODE == F16_X_NHWC_VEC;
+  constexpr bool LANEG = XMODE == F16_X_NHWC_VEC || XMODE == F16_X_NHWC_PAIR;  // lane-varying k group
   static_assert(WM * WN == 4 && FM >= 1 && FN >= 1 && BN % 64 == 0 && 256 % BN == 0, "tile");
   typedef typename std::conditional<XMODE == F16_X_NCHW32, float, _Float16>::type XT;
   constexpr int MAIN_HALVES = 2 * (BM + BN) * LR, EPI_HALVES = 4 * TN * SR;
@@ -68,11 +101,12 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
 
   for (int i = tid; i < BM; i += 256) sbias[i] = (p.bias && m0 + i < p.M) ? p.bias[m0 + i] : 0.0f;
 
-  // B tasks.  VEC: lane group g = tid & 3 (fixed), pixels (tid >> 2) + 64u: four lanes read 64
-  // contiguous bytes of one pixel.  Per-element: pixel tid % BN, k groups qbase + QS*u (uniform).
-  constexpr int NPX = VEC ? BV : 1;
+  // B tasks.  VEC / PAIR: lane group g = tid & 3 (fixed), pixels (tid >> 2) + 64u: four lanes
+  // read 64 contiguous bytes of one pixel.  Per-element: pixel tid % BN, k groups qbase + QS*u
+  // (uniform).
+  constexpr int NPX = LANEG ? BV : 1;
   const int g = tid & 3;
-  const int bcol0 = VEC ? (tid >> 2) : (tid % BN);
+  const int bcol0 = LANEG ? (tid >> 2) : (tid % BN);
   const int qbase = __builtin_amdgcn_readfirstlane(tid / BN);
   int xoff[NPX], ih0[NPX], iw0[NPX];
   bool nok[NPX];
@@ -91,71 +125,91 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
   const XT* __restrict__ x = reinterpret_cast<const XT*>(p.x);
   const _Float16* __restrict__ wh = reinterpret_cast<const _Float16*>(p.wp);  // [Mp][Kp]
   typedef const __attribute__((address_space(4))) long long* ktab_cptr;
-  const ktab_cptr ktab = (ktab_cptr)p.ktab;  // per k, or per 8-k group (VEC)
+  const ktab_cptr ktab = (ktab_cptr)p.ktab;  // per k, or per 8-k group (VEC, PAIR)
 
-#define ORE_H_LOADA(RA, K0)                                                                          \
-  _Pragma("unroll") for (int v_ = 0; v_ < AV; ++v_) {                                                \
-    const int c_ = (ACH % 256 == 0 || tid + v_ * 256 < ACH) ? tid + v_ * 256 : 0;                    \
-    RA[v_] = *reinterpret_cast<const half8*>(wh + (unsigned)((m0 + (c_ >> 2)) * Kp + (K0) + (c_ & 3) * 8)); \
-  }
-#define ORE_H_STOREA(RA, BUF)                                                                        \
-  _Pragma("unroll") for (int v_ = 0; v_ < AV; ++v_) {                                                \
-    const int c_ = tid + v_ * 256;                                                                   \
-    if (ACH % 256 == 0 || c_ < ACH) *reinterpret_cast<half8*>(&As[BUF][c_ >> 2][(c_ & 3) * 8]) = RA[v_]; \
-  }
-  // VEC B: the four group entries of the stage by scalar loads, this lane's picked by g; a tap
-  // outside the image (or a group past K: r = 1 << 14) is stored as zeros
-#define ORE_H_LOADB_VEC(RB, ROK, K0)                                                                 \
-  {                                                                                                  \
-    const int kb_ = (K0) >> 3;                                                                       \
-    const long long e0_ = ktab[kb_], e1_ = ktab[kb_ + 1], e2_ = ktab[kb_ + 2], e3_ = ktab[kb_ + 3];  \
-    const long long w_ = g == 0 ? e0_ : g == 1 ? e1_ : g == 2 ? e2_ : e3_;                           \
-    const int ex_ = (int)w_, ey_ = (int)(w_ >> 32);                                                  \
-    const int r_ = ey_ >> 16, s_ = ey_ & 0xffff;                                                     \
-    _Pragma("unroll") for (int u_ = 0; u_ < BV; ++u_) {                                              \
-      const bool ok_ = nok[u_] & ((unsigned)(ih0[u_] + r_) < (unsigned)p.H) &                        \
-                       ((unsigned)(iw0[u_] + s_) < (unsigned)p.W);                                   \
-      RB[u_] = *reinterpret_cast<const half8*>(x + (unsigned)(ok_ ? xoff[u_] + ex_ : 0));            \
-      ROK[u_] = ok_;                                                                                 \
-    }                                                                                                \
-  }
-#define ORE_H_STOREB_VEC(RB, ROK, BUF)                                                               \
-  _Pragma("unroll") for (int u_ = 0; u_ < BV; ++u_) {                                                \
-    const half8 z_ = {};                                                                             \
-    *reinterpret_cast<half8*>(&Bs[BUF][bcol0 + 64 * u_][g * 8]) = ROK[u_] ? RB[u_] : z_;             \
-  }
-  // per-element B: 8 scattered loads per task through the per-k table (uniform k)
-#define ORE_H_LOADB_ELEM(RB, ROK, K0)                                                                \
-  _Pragma("unroll") for (int u_ = 0; u_ < BV; ++u_) {                                                \
-    const int kg_ = (K0) + (qbase + u_ * QS) * 8;                                                    \
-    _Pragma("unroll") for (int e_ = 0; e_ < 8; ++e_) {                                               \
-      const long long w_ = ktab[kg_ + e_];                                                           \
-      const int ex_ = (int)w_, ey_ = (int)(w_ >> 32);                                                \
-      const int r_ = ey_ >> 16, s_ = ey_ & 0xffff;                                                   \
-      const bool ok_ = nok[0] & ((unsigned)(ih0[0] + r_) < (unsigned)p.H) &                          \
-                       ((unsigned)(iw0[0] + s_) < (unsigned)p.W);                                    \
-      RB[u_ * 8 + e_] = x[(unsigned)(ok_ ? xoff[0] + ex_ : 0)];                                      \
-      ROK[u_ * 8 + e_] = ok_;                                                                        \
-    }                                                                                                \
-  }
-#define ORE_H_STOREB_ELEM(RB, ROK, BUF)                                                              \
-  _Pragma("unroll") for (int u_ = 0; u_ < BV; ++u_) {                                                \
-    half8 h_;                                                                                        \
-    _Pragma("unroll") for (int e_ = 0; e_ < 8; ++e_)                                                 \
-      h_[e_] = ROK[u_ * 8 + e_] ? (_Float16)RB[u_ * 8 + e_] : (_Float16)0.0f;                        \
-    *reinterpret_cast<half8*>(&Bs[BUF][bcol0][(qbase + u_ * QS) * 8]) = h_;                          \
-  }
-#define ORE_H_COMPUTE(BUF)                                                                           \
-  _Pragma("unroll") for (int ks = 0; ks < BK; ks += 16) {                                            \
-    half8 af[FM], bf[FN];                                                                            \
-    _Pragma("unroll") for (int i = 0; i < FM; ++i)                                                   \
-      af[i] = *reinterpret_cast<const half8*>(&As[BUF][wm0 + i * 32 + lcol][ks + 8 * lrow]);         \
-    _Pragma("unroll") for (int j = 0; j < FN; ++j)                                                   \
-      bf[j] = *reinterpret_cast<const half8*>(&Bs[BUF][wn0 + j * 32 + lcol][ks + 8 * lrow]);         \
-    _Pragma("unroll") for (int i = 0; i < FM; ++i)                                                   \
-    _Pragma("unroll") for (int j = 0; j < FN; ++j)                                                   \
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);          \
-  }
+  // one K stage into registers: A (16-B weight chunks) and B per mode; a tap outside the image
+  // (or a group past K: ktab r = 1 << 14) loads from x[0] and is zeroed at the LDS store
+  auto load_stage = [&](half8 (&ra)[AV], BStage<XMODE, BV>& rb, int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      const int c = (ACH % 256 == 0 || tid + v * 256 < ACH) ? tid + v * 256 : 0;
+#ifdef ORE_EXP_H_NOA
+      ra[v] = (half8){} + (_Float16)(k0 + c);
+#else
+      ra[v] = *reinterpret_cast<const half8*>(wh + (unsigned)((m0 + (c >> 2)) * Kp + k0 + (c & 3) * 8));
+#endif
+    }
+#ifdef ORE_EXP_H_NOB
+    if constexpr (XMODE == F16_X_NHWC_VEC) {
+#pragma unroll
+      for (int u = 0; u < BV; ++u) {
+        rb.v[u] = (half8){} + (_Float16)(k0 + u);
+        rb.ok[u] = nok[u];
+      }
+      return;
+    }
+#endif
+    if constexpr (LANEG) {
+      // the stage's four group entries by scalar loads; this lane's picked by g
+      const int kb = k0 >> 3;
+      const long long e0 = ktab[kb], e1 = ktab[kb + 1], e2 = ktab[kb + 2], e3 = ktab[kb + 3];
+      const long long w = g == 0 ? e0 : g == 1 ? e1 : g == 2 ? e2 : e3;
+      const int ex = (int)w, ey = (int)(w >> 32);
+      const int r = ey >> 16, s = ey & 0x7fff;
+#pragma unroll
+      for (int u = 0; u < BV; ++u) {
+        const bool rin = nok[u] & ((unsigned)(ih0[u] + r) < (unsigned)p.H);
+        const bool ok0 = rin & ((unsigned)(iw0[u] + s) < (unsigned)p.W);
+        if constexpr (XMODE == F16_X_NHWC_VEC) {
+          rb.v[u] = *reinterpret_cast<const half8*>(x + (unsigned)(ok0 ? xoff[u] + ex : 0));
+          rb.ok[u] = ok0;
+        } else {  // PAIR: taps s and s + 1 (the latter absent past kw: ey bit 15)
+          const bool ok1 = rin & ((ey & 0x8000) == 0) & ((unsigned)(iw0[u] + s + 1) < (unsigned)p.W);
+          rb.v[2 * u] = *reinterpret_cast<const half4*>(x + (unsigned)(ok0 ? xoff[u] + ex : 0));
+          rb.v[2 * u + 1] = *reinterpret_cast<const half4*>(x + (unsigned)(ok1 ? xoff[u] + ex + p.x_ps : 0));
+          rb.ok[2 * u] = ok0;
+          rb.ok[2 * u + 1] = ok1;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < BV; ++u) {
+        const int kg = k0 + (qbase + u * QS) * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const long long w = ktab[kg + e];
+          const int ex = (int)w, ey = (int)(w >> 32);
+          const int r = ey >> 16, s = ey & 0xffff;
+          const bool ok = nok[0] & ((unsigned)(ih0[0] + r) < (unsigned)p.H) & ((unsigned)(iw0[0] + s) < (unsigned)p.W);
+          rb.v[u * 8 + e] = x[(unsigned)(ok ? xoff[0] + ex : 0)];
+          rb.ok[u * 8 + e] = ok;
+        }
+      }
+    }
+  };
+  auto store_stage = [&](const half8 (&ra)[AV], const BStage<XMODE, BV>& rb, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      const int c = tid + v * 256;
+      if (ACH % 256 == 0 || c < ACH) *reinterpret_cast<half8*>(&As[buf][c >> 2][(c & 3) * 8]) = ra[v];
+    }
+#pragma unroll
+    for (int u = 0; u < BV; ++u) {
+      if constexpr (XMODE == F16_X_NHWC_VEC) {
+        const half8 z = {};
+        *reinterpret_cast<half8*>(&Bs[buf][bcol0 + 64 * u][g * 8]) = rb.ok[u] ? rb.v[u] : z;
+      } else if constexpr (XMODE == F16_X_NHWC_PAIR) {
+        const half4 z = {};
+        *reinterpret_cast<half4*>(&Bs[buf][bcol0 + 64 * u][g * 8]) = rb.ok[2 * u] ? rb.v[2 * u] : z;
+        *reinterpret_cast<half4*>(&Bs[buf][bcol0 + 64 * u][g * 8 + 4]) = rb.ok[2 * u + 1] ? rb.v[2 * u + 1] : z;
+      } else {
+        half8 h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = rb.ok[u * 8 + e] ? (_Float16)rb.v[u * 8 + e] : (_Float16)0.0f;
+        *reinterpret_cast<half8*>(&Bs[buf][bcol0][(qbase + u * QS) * 8]) = h;
+      }
+    }
+  };
 
   floatx16h acc[FM][FN];
 #pragma unroll
@@ -165,63 +219,74 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
-  __syncthreads();  // sbias
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ks = 0; ks < BK; ks += 16) {
+      half8 af[FM], bf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const half8*>(&As[buf][wm0 + i * 32 + lcol][ks + 8 * lrow]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = *reinterpret_cast<const half8*>(&Bs[buf][wn0 + j * 32 + lcol][ks + 8 * lrow]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#ifdef ORE_EXP_H_NOMFMA
+          acc[i][j][0] += (float)af[i][0] * (float)bf[j][1];
+#else
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+#endif
+    }
+  };
+
   const int ntk = Kp / BK;
-  if constexpr (VEC) {
-    {
-      half8 ra[AV], rb[BV];
-      bool rok[BV];
-      ORE_H_LOADA(ra, 0);
-      ORE_H_LOADB_VEC(rb, rok, 0);
-      ORE_H_STOREA(ra, 0);
-      ORE_H_STOREB_VEC(rb, rok, 0);
-    }
+  __syncthreads();  // sbias
+#if ORE_H_PREFETCH2
+  // Two stages of loads in flight: at stage t the registers of slot t & 1 are refilled with
+  // stage t + 2 while stage t + 1 (loaded one stage earlier) is published to the other LDS buffer
+  // after the MFMAs of stage t.  Unrolled by two so the register slots are static.  Opt-in: it
+  // raised the 128x128 kernel from 132 to 206 VGPRs and measured slower.
+  half8 ra0[AV], ra1[AV];
+  BStage<XMODE, BV> rb0, rb1;
+  load_stage(ra0, rb0, 0);
+  if (ntk > 1) load_stage(ra1, rb1, BK);
+  store_stage(ra0, rb0, 0);
+  __syncthreads();
+  for (int t = 0; t < ntk; t += 2) {
+    if (t + 2 < ntk) load_stage(ra0, rb0, (t + 2) * BK);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(0);
+    if (t + 1 >= ntk) break;
+    store_stage(ra1, rb1, 1);
     __syncthreads();
-    for (int t = 0; t < ntk - 1; ++t) {
-      const int buf = t & 1;
-      half8 ra[AV], rb[BV];
-      bool rok[BV];
-      ORE_H_LOADA(ra, (t + 1) * BK);
-      ORE_H_LOADB_VEC(rb, rok, (t + 1) * BK);
-      __builtin_amdgcn_sched_barrier(0);  // the next stage's loads issue ahead of this stage's MFMAs
-      ORE_H_COMPUTE(buf);
-      ORE_H_STOREA(ra, buf ^ 1);
-      ORE_H_STOREB_VEC(rb, rok, buf ^ 1);
-      __syncthreads();
-    }
-  } else {
-    {
-      half8 ra[AV];
-      XT rb[8 * BV];
-      bool rok[8 * BV];
-      ORE_H_LOADA(ra, 0);
-      ORE_H_LOADB_ELEM(rb, rok, 0);
-      ORE_H_STOREA(ra, 0);
-      ORE_H_STOREB_ELEM(rb, rok, 0);
-    }
+    if (t + 3 < ntk) load_stage(ra1, rb1, (t + 3) * BK);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(1);
+    if (t + 2 >= ntk) break;
+    store_stage(ra0, rb0, 0);
     __syncthreads();
-    for (int t = 0; t < ntk - 1; ++t) {
-      const int buf = t & 1;
-      half8 ra[AV];
-      XT rb[8 * BV];
-      bool rok[8 * BV];
-      ORE_H_LOADA(ra, (t + 1) * BK);
-      ORE_H_LOADB_ELEM(rb, rok, (t + 1) * BK);
-      __builtin_amdgcn_sched_barrier(0);
-      ORE_H_COMPUTE(buf);
-      ORE_H_STOREA(ra, buf ^ 1);
-      ORE_H_STOREB_ELEM(rb, rok, buf ^ 1);
+  }
+#else
+  // stage t + 1 is loaded into registers ahead of stage t's MFMAs and published to the other
+  // LDS buffer after them
+  half8 ra[AV];
+  BStage<XMODE, BV> rb;
+  load_stage(ra, rb, 0);
+  store_stage(ra, rb, 0);
+  __syncthreads();
+  for (int t = 0; t < ntk; ++t) {
+    const bool more = t + 1 < ntk;
+    if (more) load_stage(ra, rb, (t + 1) * BK);
+    __builtin_amdgcn_sched_barrier(0);  // the next stage's loads issue ahead of this stage's MFMAs
+    compute(t & 1);
+    if (more) {
+#ifndef ORE_EXP_H_NOSTORE  // timing experiments only (tools/build_exp.sh)
+      store_stage(ra, rb, (t + 1) & 1);
+#endif
       __syncthreads();
     }
   }
-  ORE_H_COMPUTE((ntk - 1) & 1);
-#undef ORE_H_LOADA
-#undef ORE_H_STOREA
-#undef ORE_H_LOADB_VEC
-#undef ORE_H_STOREB_VEC
-#undef ORE_H_LOADB_ELEM
-#undef ORE_H_STOREB_ELEM
-#undef ORE_H_COMPUTE
+#endif
 
   // epilogue: + bias (f32), optional Relu, one rounding to f16, NHWC store.  Each wave stages its
   // TM channels x TN pixels in its own LDS slice as [pixel][channel] (accumulator rows 8q + 4 lrow
@@ -275,49 +340,340 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
   }
 }
 
-// Wh[m][k] = f16(W[m][c][r][s]) zero padded to Mp x Kp; k = (c, r, s) (the reference's order, the
-// f32 NCHW input) or k = (r, s, c) (NHWC inputs: c fastest).
-__global__ __launch_bounds__(256) void pack_weights_f16_kernel(const float* __restrict__ w, int rsc, int M, int C,
-                                                               int KK, int Mp, int Kp, _Float16* __restrict__ wh) {
-  const int K = C * KK;
+// ------------------------------------------------------------------ LDS-DMA variant (16-B NHWC)
+// conv_f16_kernel spends most of its time moving the staged operands from VGPRs into LDS
+// (ds_write_b128: ablating those stores alone took 35-45 % off the 3x3 layers, the MFMAs 10 %).
+// Here every 16-B operand chunk goes global -> LDS by buffer_load_dwordx4 ... lds (no VGPR round
+// trip, no store instruction), into a ring of three K stages, each its own __shared__ array so
+// the compiler's wait for an LDS-DMA write only covers reads of the same stage:
+//   * stage layout: BMA rows of A (weights) then BN rows of B (pixels), 64 B (one 32-k stage) per
+//     row, no padding; a wave-instruction fills 64 consecutive 16-B slots.  Slot (row, q) holds
+//     k-chunk q ^ ((row >> 2) & 3), which makes the MFMA fragment reads (ds_read_b128, lane l:
+//     row l & 31, chunk ks/8 + (l >> 5)) bank-conflict free.
+//   * a tap outside the image (or a group past K) gets an out-of-range buffer offset: the load
+//     returns zeros, which is the reference's zero padding.
+//   * stage t + 2 is issued after the barrier that publishes stage t; each wave waits with a counted
+//     vmcnt for its own chunks of stage t only, so two stages of loads stay in flight.
+// Same GEMM, k order, MFMA chain and epilogue arithmetic as conv_f16_kernel<..., F16_X_NHWC_VEC>:
+// bit-identical results.
+typedef int int4v __attribute__((ext_vector_type(4)));
+
+// buffer descriptor {base, stride 0, num_records bytes, raw-buffer flags}: offsets >= num_records
+// (0x80000000) read as zeros
+__device__ __forceinline__ int4v buffer_desc(const void* base, int bytes) {
+  const unsigned long long b = reinterpret_cast<unsigned long long>(base);
+  return int4v{(int)(unsigned)b, (int)((b >> 32) & 0xffff), bytes, 0x00020000};
+}
+
+// One 16-B-per-lane LDS-DMA (lane i -> lds_addr + 16 i).  Inline asm rather than the builtin so
+// the compiler does not guard later LDS reads with its own conservative vmcnt(0) (it cannot tell
+// which ring stage a DMA writes); the kernel waits with counted vmcnt itself.  M0 is restored.
+__device__ __forceinline__ void lds_dma16(int4v rsrc, unsigned lds_addr, int voffset) {
+  int m0save;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(m0save)
+      : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voffset), "s"(rsrc)
+      : "memory");
+}
+
+__device__ __forceinline__ unsigned lds_addr_of(const _Float16* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) _Float16*)p;
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256, 2) void conv_f16_dma_kernel(ConvParams p) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 32, FN = TN / 32;
+  constexpr int AV = (BM * 4 + 255) / 256;  // A DMA instructions per thread per stage (rows padded to AV*64)
+  constexpr int BMA = AV * 64;              // A rows in the stage (rows >= BM load zeros)
+  constexpr int BV = BN * 4 / 256;          // B DMA instructions per thread per stage
+  constexpr int NQ = AV + BV;               // DMA instructions per wave per stage (uniform)
+  constexpr int SH = (BMA + BN) * 32;       // halves per stage
+  constexpr int SR = 40;                    // epilogue staging row (32 channels + 8 pad, halves)
+  static_assert(WM * WN == 4 && FM >= 1 && FN >= 1 && BN % 64 == 0 && 256 % BN == 0, "tile");
+  static_assert(2 * TN * SR <= SH, "epilogue staging of two waves fits one stage array");
+  __shared__ __attribute__((aligned(16))) _Float16 S0[SH];
+  __shared__ __attribute__((aligned(16))) _Float16 S1[SH];
+  __shared__ __attribute__((aligned(16))) _Float16 S2[SH];
+  __shared__ float sbias[BM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm0 = (wave / WN) * TM, wn0 = (wave % WN) * TN;
+  const int lrow = lane >> 5, lcol = lane & 31;
+
+  const int nwg = p.mtiles * p.ntiles;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
+  const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
+  const int mt = wgid % p.mtiles, nt = wgid / p.mtiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int Kp = (p.K + 31) & ~31;
+  const int P = p.P;
+
+  for (int i = tid; i < BM; i += 256) sbias[i] = (p.bias && m0 + i < p.M) ? p.bias[m0 + i] : 0.0f;
+
+  // this thread's slots: row (tid >> 2) + 64v, slot tid & 3 -> k-chunk g (same for A and B rows)
+  const int g = (tid & 3) ^ ((tid >> 4) & 3);
+  const int prow = tid >> 2;
+  int aoff[AV];
+#pragma unroll
+  for (int v = 0; v < AV; ++v) {
+    const int row = prow + 64 * v;
+    aoff[v] = row < BM ? ((m0 + row) * Kp + g * 8) * 2 : (int)0x80000000;
+  }
+  int xoff[BV], ih0[BV], iw0[BV];
+  bool nok[BV];
+#pragma unroll
+  for (int u = 0; u < BV; ++u) {
+    const int bn = n0 + prow + 64 * u;
+    nok[u] = bn < p.Ntot;
+    const int nn = nok[u] ? bn : 0;
+    const int img = nn / P;
+    const int pix = nn - img * P;
+    const int oh = pix / p.Wo, ow = pix - oh * p.Wo;
+    ih0[u] = oh * p.sh - p.pt;
+    iw0[u] = ow * p.sw - p.pl;
+    xoff[u] = img * (int)p.x_nstride + (ih0[u] * p.W + iw0[u]) * p.x_ps;
+  }
+  const int4v wrsrc = buffer_desc(p.wp, p.Mp * Kp * 2);
+  const int4v xrsrc = buffer_desc(p.x, (int)p.x_bytes);
+  typedef const __attribute__((address_space(4))) long long* ktab_cptr;
+  const ktab_cptr ktab = (ktab_cptr)p.ktab;
+
+  // issue stage `st` (k0 = st * 32) into stage array SA: every wave NQ DMA instructions
+#define ORE_HD_ISSUE(SA, K0)                                                                         \
+  {                                                                                                  \
+    const int k0_ = (K0);                                                                            \
+    _Pragma("unroll") for (int v_ = 0; v_ < AV; ++v_)                                                \
+      lds_dma16(wrsrc, lds_addr_of((SA) + (v_ * 256 + wave * 64) * 8), aoff[v_] < 0 ? aoff[v_] : aoff[v_] + k0_ * 2); \
+    const int kb_ = k0_ >> 3;                                                                        \
+    const long long e0_ = ktab[kb_], e1_ = ktab[kb_ + 1], e2_ = ktab[kb_ + 2], e3_ = ktab[kb_ + 3];  \
+    const long long w_ = g == 0 ? e0_ : g == 1 ? e1_ : g == 2 ? e2_ : e3_;                           \
+    const int ex_ = (int)w_, ey_ = (int)(w_ >> 32);                                                  \
+    const int r_ = ey_ >> 16, s_ = ey_ & 0x7fff;                                                     \
+    _Pragma("unroll") for (int u_ = 0; u_ < BV; ++u_) {                                              \
+      const bool ok_ = nok[u_] & ((unsigned)(ih0[u_] + r_) < (unsigned)p.H) &                        \
+                       ((unsigned)(iw0[u_] + s_) < (unsigned)p.W);                                   \
+      lds_dma16(xrsrc, lds_addr_of((SA) + (BMA * 4 + u_ * 256 + wave * 64) * 8),                     \
+                ok_ ? (xoff[u_] + ex_) * 2 : (int)0x80000000);                                       \
+    }                                                                                                \
+  }
+
+  floatx16h acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  const int sw = (lcol >> 2) & 3;  // fragment rows R have (R >> 2) & 3 == (lcol >> 2) & 3
+#define ORE_HD_COMPUTE(SA)                                                                           \
+  _Pragma("unroll") for (int ks = 0; ks < 32; ks += 16) {                                            \
+    const int q_ = ((ks >> 3) + lrow) ^ sw;                                                          \
+    half8 af[FM], bf[FN];                                                                            \
+    _Pragma("unroll") for (int i = 0; i < FM; ++i)                                                   \
+      af[i] = *reinterpret_cast<const half8*>((SA) + (wm0 + i * 32 + lcol) * 32 + q_ * 8);           \
+    _Pragma("unroll") for (int j = 0; j < FN; ++j)                                                   \
+      bf[j] = *reinterpret_cast<const half8*>((SA) + (BMA + wn0 + j * 32 + lcol) * 32 + q_ * 8);     \
+    _Pragma("unroll") for (int i = 0; i < FM; ++i)                                                   \
+    _Pragma("unroll") for (int j = 0; j < FN; ++j)                                                   \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);          \
+  }
+  // stage t in CUR; NX2 receives stage t + 2 (read last at stage t - 1, before this barrier)
+#define ORE_HD_STEP(CUR, NX2)                                                                        \
+  {                                                                                                  \
+    if (t + 1 < ntk)                                                                                 \
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ) : "memory"); /* stage t + 1 may stay in flight */ \
+    else                                                                                             \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                               \
+    __builtin_amdgcn_s_barrier();                                                                    \
+    if (t + 2 < ntk) ORE_HD_ISSUE(NX2, (t + 2) * 32);                                                \
+    ORE_HD_COMPUTE(CUR);                                                                             \
+    if (++t >= ntk) break;                                                                           \
+  }
+
+  const int ntk = Kp / 32;
+  ORE_HD_ISSUE(S0, 0);
+  if (ntk > 1) ORE_HD_ISSUE(S1, 32);
+  __syncthreads();  // sbias (the DMA stays in flight: the barrier's own wait is vmcnt-free here)
+  for (int t = 0;;) {
+    ORE_HD_STEP(S0, S2);
+    ORE_HD_STEP(S1, S0);
+    ORE_HD_STEP(S2, S1);
+  }
+#undef ORE_HD_STEP
+#undef ORE_HD_COMPUTE
+#undef ORE_HD_ISSUE
+
+  // epilogue: + bias (f32), optional Relu, one rounding, NHWC store.  Per 32-channel fragment
+  // row i each wave stages [TN pixels][32 channels] (80-B rows) in half of S0 / S1 (waves 0-1 /
+  // 2-3), then writes each pixel's 64-B channel run with 16-B stores (host: M % 8 == 0,
+  // y_ps % 8 == 0, aligned y) or 2-byte stores.
+  __syncthreads();  // every wave is done with the stage arrays
+  _Float16* stg = (wave < 2 ? S0 : S1) + (wave & 1) * (TN * SR);
+  _Float16* __restrict__ y = reinterpret_cast<_Float16*>(p.y);
+  const int yps = p.y_ps;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ch = 8 * q + 4 * lrow;
+        half4 h;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = acc[i][j][4 * q + e] + sbias[wm0 + i * 32 + ch + e];
+          if (p.relu) v = fmaxf(v, 0.0f);
+          h[e] = (_Float16)v;
+        }
+        *reinterpret_cast<half4*>(stg + (j * 32 + lcol) * SR + ch) = h;
+      }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int mb = m0 + wm0 + i * 32;
+    if (p.vec_out) {
+#pragma unroll
+      for (int idx = lane; idx < TN * 4; idx += 64) {
+        const int px = idx >> 2, cg = idx & 3;
+        const int n = n0 + wn0 + px, m = mb + cg * 8;
+        if (n < p.Ntot && m < p.M) {
+          const int img = n / P, pix = n - img * P;
+          *reinterpret_cast<half8*>(y + (unsigned)(img * (int)p.y_nstride + pix * yps + m)) =
+              *reinterpret_cast<const half8*>(stg + px * SR + cg * 8);
+        }
+      }
+    } else {
+      for (int idx = lane; idx < TN * 32; idx += 64) {
+        const int px = idx >> 5, ch = idx & 31;
+        const int n = n0 + wn0 + px, m = mb + ch;
+        if (n < p.Ntot && m < p.M) {
+          const int img = n / P, pix = n - img * P;
+          y[(unsigned)(img * (int)p.y_nstride + pix * yps + m)] = stg[px * SR + ch];
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// Wh[m][k] = f16(W[m][c][r][s]) zero padded to Mp x Kp, k in the order the operand mode gathers:
+//   F16_X_NCHW32: (c, r, s) (the reference's); F16_X_NHWC_*: (r, s, c), c fastest;
+//   F16_X_NHWC_PAIR: (r, s', c') with s' < kw rounded up to even and c' < 4 (zero weights for the
+//   padding tap and channels).
+__global__ __launch_bounds__(256) void pack_weights_f16_kernel(const float* __restrict__ w, int xmode, int M, int C,
+                                                               int kh, int kw, int Mp, int Kp, _Float16* __restrict__ wh) {
+  const int KK = kh * kw, K = C * KK, kwp = (kw + 1) & ~1;
   const long long total = (long long)Mp * Kp;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
     const int m = (int)(i / Kp), k = (int)(i - (long long)m * Kp);
     float v = 0.0f;
-    if (m < M && k < K) v = rsc ? w[((long long)m * C + (k % C)) * KK + k / C] : w[(long long)m * K + k];
+    if (m < M) {
+      if (xmode == F16_X_NHWC_PAIR) {
+        const int c = k & 3, t = k >> 2, r = t / kwp, sx = t - r * kwp;
+        if (r < kh && sx < kw && c < C) v = w[(((long long)m * C + c) * kh + r) * kw + sx];
+      } else if (xmode == F16_X_NHWC8) {
+        const int c = k & 7, rs = k >> 3;
+        if (rs < KK && c < C) v = w[((long long)m * C + c) * KK + rs];
+      } else if (k < K) {
+        v = xmode == F16_X_NCHW32 ? w[(long long)m * K + k] : w[((long long)m * C + (k % C)) * KK + k / C];
+      }
+    }
     wh[i] = (_Float16)v;
   }
 }
 
-void launch_pack_weights_f16(const float* w, int xmode, int M, int C, int kh, int kw, int Mp, void* wh,
-                             hipStream_t s) {
-  const int Kp = conv_packed_kp(C * kh * kw);
-  long long blocks = ((long long)Mp * Kp + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(pack_weights_f16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, w,
-                     xmode == F16_X_NCHW32 ? 0 : 1, M, C, kh * kw, Mp, Kp, static_cast<_Float16*>(wh));
+int f16_conv_k(int xmode, int C, int kh, int kw) {
+  return xmode == F16_X_NHWC_PAIR ? kh * ((kw + 1) & ~1) * 4 : xmode == F16_X_NHWC8 ? kh * kw * 8 : C * kh * kw;
 }
 
-// Gather table over an NHWC input, k = (r, s, c): entry {(r * W + s) * cs + c, (r << 16) | s} per k
-// (vec = false) or per group of 8 k (vec: c = the group's first channel); entries past K carry
-// r = 1 << 14, which no bounds check passes (read as zeros).
-__global__ __launch_bounds__(256) void ktab_nhwc_kernel(int2* __restrict__ ktab, int C, int K, int n, int step, int kw,
+void launch_pack_weights_f16(const float* w, int xmode, int M, int C, int kh, int kw, int Mp, void* wh,
+                             hipStream_t s) {
+  const int Kp = conv_packed_kp(f16_conv_k(xmode, C, kh, kw));
+  long long blocks = ((long long)Mp * Kp + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pack_weights_f16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, w, xmode, M, C, kh, kw, Mp, Kp,
+                     static_cast<_Float16*>(wh));
+}
+
+// Gather tables over an NHWC input with pixel stride cs, one entry {x offset, (r << 16) | s} per k
+// (F16_X_NHWC_ELEM, k = (r, s, c)) or per group of 8 k (F16_X_NHWC_VEC: c = the group's first
+// channel; F16_X_NHWC_PAIR: taps s (even) and s + 1 of 4 channels, bit 15 set when s + 1 is the
+// padding tap).  Entries past K carry r = 1 << 14, which no bounds check passes (read as zeros).
+__global__ __launch_bounds__(256) void ktab_nhwc_kernel(int2* __restrict__ ktab, int xmode, int C, int kh, int kw, int n,
                                                         int cs, int W) {
+  const int K = C * kh * kw, kwp = (kw + 1) & ~1;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     int2 e = make_int2(0, (1 << 14) << 16);
-    const int k = i * step;
-    if (k < K) {
-      const int rs = k / C, c = k - rs * C, r = rs / kw, s = rs - r * kw;
-      e = make_int2((r * W + s) * cs + c, (r << 16) | s);
+    if (xmode == F16_X_NHWC_PAIR) {
+      const int t = 2 * i, r = t / kwp, sx = t - r * kwp;
+      if (r < kh) e = make_int2((r * W + sx) * cs, (r << 16) | sx | (sx + 1 >= kw ? 0x8000 : 0));
+    } else {
+      const int k = xmode == F16_X_NHWC_VEC ? 8 * i : i;
+      if (k < K) {
+        const int rs = k / C, c = k - rs * C, r = rs / kw, sx = rs - r * kw;
+        e = make_int2((r * W + sx) * cs + c, (r << 16) | sx);
+      }
     }
     ktab[i] = e;
   }
 }
 
-void launch_ktab_nhwc(int2* ktab, int C, int kh, int kw, int cs, int W, bool vec, hipStream_t s) {
-  const int K = C * kh * kw, step = vec ? 8 : 1;
-  const int n = conv_packed_kp(K) / step;
-  hipLaunchKernelGGL(ktab_nhwc_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ktab, C, K, n, step, kw, cs, W);
+void launch_ktab_nhwc(int2* ktab, int xmode, int C, int kh, int kw, int cs, int W, hipStream_t s) {
+  if (xmode == F16_X_NHWC8) {  // the 16-B gather over the 8 converted channels
+    xmode = F16_X_NHWC_VEC;
+    C = 8;
+  }
+  const int n = conv_packed_kp(f16_conv_k(xmode, C, kh, kw)) / (xmode == F16_X_NHWC_ELEM ? 1 : 8);
+  hipLaunchKernelGGL(ktab_nhwc_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ktab, xmode, C, kh, kw, n, cs, W);
+}
+
+// f32 NCHW (plane stride x_ps, image stride x_nstride) -> f16 NHWC with CS channels per pixel
+// (channels >= C zero): the operand of F16_X_NHWC_PAIR (CS = 4) / F16_X_NHWC8 (CS = 8) for the
+// first conv.  One thread per pixel: coalesced plane reads, one 8-B / 16-B store.
+template <int CS>
+__global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float* __restrict__ x, _Float16* __restrict__ y,
+                                                           long long pixels, int HW, int C, long long x_nstride,
+                                                           int x_ps) {
+  typedef _Float16 hv __attribute__((ext_vector_type(CS)));
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < pixels; i += (long long)gridDim.x * 256) {
+    const long long n = i / HW;
+    const int q = (int)(i - n * HW);
+    const float* xp = x + n * x_nstride + q;
+    hv h;
+#pragma unroll
+    for (int c = 0; c < CS; ++c) h[c] = c < C ? (_Float16)xp[(long long)c * x_ps] : (_Float16)0.0f;
+    *reinterpret_cast<hv*>(y + i * CS) = h;
+  }
+}
+
+void launch_nchw_to_nhwc(const float* x, void* y, int N, int C, int HW, long long x_nstride, int x_ps, int cs,
+                         hipStream_t s) {
+  const long long pixels = (long long)N * HW;
+  if (pixels <= 0) return;
+  long long b = (pixels + 255) / 256;
+  if (b > 256 * 32) b = 256 * 32;
+  if (cs == 8)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<8>, dim3((unsigned)b), dim3(256), 0, s, x, static_cast<_Float16*>(y), pixels,
+                       HW, C, x_nstride, x_ps);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<4>, dim3((unsigned)b), dim3(256), 0, s, x, static_cast<_Float16*>(y), pixels,
+                       HW, C, x_nstride, x_ps);
+}
+
+static int env_knob_f16(const char* name, int dflt) {  // tuning knob, read per launch
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -329,7 +685,13 @@ static void launch_f16_cfg(const ConvParams& p0, int xmode, hipStream_t s) {
   switch (xmode) {
     case F16_X_NCHW32: hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, WN, F16_X_NCHW32>), grid, block, 0, s, p); break;
     case F16_X_NHWC_ELEM: hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, WN, F16_X_NHWC_ELEM>), grid, block, 0, s, p); break;
-    default: hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, WN, F16_X_NHWC_VEC>), grid, block, 0, s, p); break;
+    case F16_X_NHWC_PAIR: hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, WN, F16_X_NHWC_PAIR>), grid, block, 0, s, p); break;
+    default:
+      if (p.x_bytes > 0 && env_knob_f16("ORE_F16_DMA", 1))
+        hipLaunchKernelGGL((conv_f16_dma_kernel<BM, BN, WM, WN>), grid, block, 0, s, p);
+      else
+        hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, WN, F16_X_NHWC_VEC>), grid, block, 0, s, p);
+      break;
   }
 }
 

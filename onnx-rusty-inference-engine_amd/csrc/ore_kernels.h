@@ -92,12 +92,21 @@ enum {
   F16_X_NCHW32 = 0,     // f32 NCHW model input, per-element gather, k order (c, r, s) (the reference's)
   F16_X_NHWC_ELEM = 1,  // f16 NHWC input with C % 8 != 0: per-element gather, k order (r, s, c)
   F16_X_NHWC_VEC = 2,   // f16 NHWC input, C % 8 == 0: one 16-B load per (pixel, 8 channels), k order (r, s, c)
+  F16_X_NHWC_PAIR = 3,  // f32 NCHW input with C <= 4, converted to NHWC4 f16 (launch_nchw_to_nhwc): two
+                        // 8-B taps per 8-k group, k order (r, s', c') over kw rounded up to even x 4 channels
+  F16_X_NHWC8 = 4,      // f32 NCHW input with C <= 8, converted to NHWC8 f16 (channels >= C zero): the
+                        // 16-B gather of F16_X_NHWC_VEC over 8 channels, k order (r, s, c' < 8)
 };
+// GEMM K of an f16 conv (PAIR pads the taps and channels)
+int f16_conv_k(int xmode, int C, int kh, int kw);
+// f32 NCHW -> f16 NHWC with cs (4 or 8) channels per pixel, channels >= C zero
+void launch_nchw_to_nhwc(const float* x, void* y, int N, int C, int HW, long long x_nstride, int x_ps, int cs,
+                         hipStream_t s);
 // Wh[Mp][Kp] = f16(W[M][C][kh][kw]) in the k order of `xmode` (MatMul stays f32)
 void launch_pack_weights_f16(const float* w, int xmode, int M, int C, int kh, int kw, int Mp, void* wh, hipStream_t s);
-// gather tables of the f16 conv: per k for F16_X_NCHW32 (launch_ktab) / F16_X_NHWC_ELEM, per group of 8 k
-// for F16_X_NHWC_VEC; cs = the input's pixel stride
-void launch_ktab_nhwc(int2* ktab, int C, int kh, int kw, int cs, int W, bool vec, hipStream_t s);
+// gather tables of the f16 conv over an NHWC input (F16_X_NCHW32 uses launch_ktab): per k for
+// F16_X_NHWC_ELEM, per group of 8 k for F16_X_NHWC_VEC / _PAIR; cs = the input's pixel stride
+void launch_ktab_nhwc(int2* ktab, int xmode, int C, int kh, int kw, int cs, int W, hipStream_t s);
 void launch_maxpool_nhwc(const NhwcPoolParams& p, hipStream_t s);
 // GlobalAveragePool of NHWC f16 -> f32 y[n][c]
 void launch_gap_nhwc(const void* x, float* y, int N, int C, int HW, int cs, long long nstride, hipStream_t s);

@@ -84,6 +84,7 @@ struct Step {
   ConvPlan plan{};        // kernel choice and weight layout for S_CONV / S_MATMUL
   float* wp = nullptr;    // packed weights (layout per plan) for S_CONV / S_MATMUL
   const int2* ktab = nullptr;  // gather table (follows wp in the packed allocation; gather kernel only)
+  void* xcvt = nullptr;        // f16 F16_X_NHWC_PAIR: the f32 NCHW input converted to NHWC4 f16 (max_batch)
   int64_t axis = 1;
   double flops_per_img = 0, bytes_per_img = 0, bytes_fixed = 0;
 };
@@ -127,6 +128,16 @@ struct ore_model {
 };
 
 namespace {
+
+// operand mode of an f16 conv on the f32 model input: ORE_F16_FIRST=pair|nhwc8|nchw (tuning knob).
+// SqueezeNet conv1 (3 channels, 7x7/s2) at B=256: pair 355 us, nhwc8 498 us (K 392 vs 224), nchw
+// 459 us (per-element gather), conversion included (profiles/r01p_f16_first_conv.txt).
+int f16_first_mode() {
+  const char* e = getenv("ORE_F16_FIRST");
+  if (e && !strcmp(e, "nhwc8")) return F16_X_NHWC8;
+  if (e && !strcmp(e, "nchw")) return F16_X_NCHW32;
+  return F16_X_NHWC_PAIR;
+}
 
 // IEEE binary16 -> binary32 (exact)
 float half_bits_to_float(uint16_t h) {
@@ -690,7 +701,8 @@ ore_status plan(ore_model* m) {
     const Value& xv = m->values[st.in0];
     int2* kt = const_cast<int2*>(st.ktab);
     if (st.plan.f16 && st.plan.xmode != F16_X_NCHW32)
-      launch_ktab_nhwc(kt, int(st.C), int(st.kh), int(st.kw), int(xv.ps), int(st.W), st.plan.xmode == F16_X_NHWC_VEC,
+      launch_ktab_nhwc(kt, st.plan.xmode, int(st.C), int(st.kh), int(st.kw),
+                       st.plan.xmode == F16_X_NHWC_PAIR ? 4 : st.plan.xmode == F16_X_NHWC8 ? 8 : int(xv.ps), int(st.W),
                        m->ctx->stream);
     else
       launch_ktab(kt, int(st.C * st.kh * st.kw), int(st.kh), int(st.kw), int(xv.ps ? xv.ps : st.H * st.W), int(st.W),
@@ -761,6 +773,15 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
     case S_CONV: {
       const Ref x = ref_of(m, s.in0);
       const float* bias = s.in2 >= 0 ? m->values[s.in2].cptr : nullptr;
+      if (s.plan.f16 && (s.plan.xmode == F16_X_NHWC_PAIR || s.plan.xmode == F16_X_NHWC8)) {
+        // convert the f32 NCHW input to NHWC f16 (4 / 8 channels per pixel), then gather
+        const int cs = s.plan.xmode == F16_X_NHWC8 ? 8 : 4;
+        launch_nchw_to_nhwc(x.p, s.xcvt, int(n), int(s.C), int(s.H * s.W), x.nstride, int(x.ps ? x.ps : s.H * s.W), cs,
+                            ctx->stream);
+        ORE_HIP_CHECK(ctx, hipGetLastError());
+        return run_conv_f16(ctx, s.plan, s.xcvt, n, s.C, s.H, s.W, s.H * s.W * cs, cs, s.wp, s.ktab, s.M, s.kh, s.kw,
+                            bias, s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps);
+      }
       if (s.plan.f16)
         return run_conv_f16(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.ktab, s.M, s.kh, s.kw, bias,
                             s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps);
@@ -901,9 +922,14 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
     size_t total_packed = 0;
     for (auto& s : m->base_steps) {
       if (s.kind == S_CONV) {
-        // f16 operand mode by the input's layout: the f32 NCHW model input, or NHWC f16 (16-B
-        // channel groups when C % 8 == 0)
-        const int xmode = m->values[s.in0].es == 4 ? F16_X_NCHW32 : s.C % 8 == 0 ? F16_X_NHWC_VEC : F16_X_NHWC_ELEM;
+        // f16 operand mode by the input's layout: an f32 NCHW value (the model input: converted to
+        // NHWC4 when C <= 4), or NHWC f16 (16-B channel groups when C % 8 == 0)
+        const int first = f16_first_mode();
+        const int xmode = m->values[s.in0].es == 4 ? (s.C <= 4 && first == F16_X_NHWC_PAIR ? F16_X_NHWC_PAIR
+                                                      : s.C <= 8 && first == F16_X_NHWC8   ? F16_X_NHWC8
+                                                                                           : F16_X_NCHW32)
+                          : s.C % 8 == 0           ? F16_X_NHWC_VEC
+                                                   : F16_X_NHWC_ELEM;
         s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, m->f16, xmode);
       }
       else if (s.kind == S_MATMUL)
@@ -928,6 +954,11 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
       if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
         return fail(set_error(ctx, ORE_ERR_HIP, "weight packing failed"));
     }
+    for (auto& s : m->base_steps)  // NHWC4 / NHWC8 copies of f32 inputs for the PAIR / NHWC8 gathers
+      if (s.kind == S_CONV && s.plan.f16 && (s.plan.xmode == F16_X_NHWC_PAIR || s.plan.xmode == F16_X_NHWC8) &&
+          hipMalloc(&s.xcvt, size_t(max_batch) * size_t(s.H * s.W) * (s.plan.xmode == F16_X_NHWC8 ? 8 : 4) *
+                                 sizeof(uint16_t)) != hipSuccess)
+        return fail(set_error(ctx, ORE_ERR_OOM, "input conversion buffer allocation failed"));
   }
   if (g.outputs.empty()) return fail(set_error(ctx, ORE_ERR_INVALID, "model has no outputs"));
   m->output_value = value_id(m, g.outputs[0].name);
@@ -955,6 +986,8 @@ ore_status ore_model_destroy(ore_model* m) {
   if (m->arena) (void)hipFree(m->arena);
   if (m->consts) (void)hipFree(m->consts);
   if (m->packed) (void)hipFree(m->packed);
+  for (auto& s : m->base_steps)
+    if (s.xcvt) (void)hipFree(s.xcvt);
   delete m;
   return ORE_OK;
 }

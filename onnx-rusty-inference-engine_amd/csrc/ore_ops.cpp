@@ -227,6 +227,13 @@ ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_
   if (N == 0) return ORE_OK;
   if (!pln.f16) return set_error(ctx, ORE_ERR_INVALID, "internal: run_conv_f16 needs an f16 plan");
   const bool nchw = pln.xmode == F16_X_NCHW32;
+  if (pln.xmode == F16_X_NHWC8) {  // the converted input: 8 channels (>= C zero), the 16-B gather
+    if (C > 8 || x_ps != 8) return set_error(ctx, ORE_ERR_INVALID, "internal: the NHWC8 gather needs an NHWC8 input");
+    ConvPlan q = pln;
+    q.xmode = F16_X_NHWC_VEC;
+    return run_conv_f16(ctx, q, x, N, 8, H, W, x_nstride, x_ps, wp, ktab, M, kh, kw, bias, win, sh, sw, relu, y,
+                        y_nstride, y_ps);
+  }
   if (x_ps == 0) x_ps = nchw ? H * W : C;
   if (y_ps == 0) y_ps = M;
   if (nchw ? x_ps < H * W : x_ps < C) return set_error(ctx, ORE_ERR_INVALID, "input stride below its extent");
@@ -234,6 +241,8 @@ ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_
   if (pln.xmode == F16_X_NHWC_VEC &&
       (C % 8 || x_ps % 8 || x_nstride % 8 || (reinterpret_cast<uintptr_t>(x) & 15)))
     return set_error(ctx, ORE_ERR_INVALID, "internal: 16-B NHWC gather needs C, strides %% 8 == 0 and an aligned input");
+  if (pln.xmode == F16_X_NHWC_PAIR && (C > 4 || x_ps != 4 || x_nstride % 4 || (reinterpret_cast<uintptr_t>(x) & 7)))
+    return set_error(ctx, ORE_ERR_INVALID, "internal: the tap-pair gather needs an NHWC4 input");
   if (!ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
   ConvParams p{};
   p.x = static_cast<const float*>(x); p.wp = static_cast<const float*>(wp); p.ktab = ktab; p.bias = bias;
@@ -242,7 +251,7 @@ ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_
   p.M = int(M); p.kh = int(kh); p.kw = int(kw); p.sh = int(sh); p.sw = int(sw);
   p.pt = int(win.pt); p.pl = int(win.pl);
   p.Ho = int(win.Ho); p.Wo = int(win.Wo);
-  p.K = int(C * kh * kw);
+  p.K = f16_conv_k(pln.xmode, int(C), int(kh), int(kw));
   p.P = int(win.Ho * win.Wo);
   p.x_ps = int(x_ps);
   p.y_ps = int(y_ps);
@@ -253,6 +262,10 @@ ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_
   p.Mp = pln.Mp;
   p.x_f32 = nchw ? 1 : 0;
   p.vec_out = (M % 8 == 0 && y_ps % 8 == 0 && y_nstride % 8 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
+  if (pln.xmode == F16_X_NHWC_VEC) {  // extent of x for the LDS-DMA kernel's buffer resource
+    const int64_t extent = ((N - 1) * x_nstride + H * W * x_ps) * 2;
+    p.x_bytes = (extent > 0 && extent < (int64_t(1) << 31)) ? extent : 0;
+  }
   if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;  // tuning knob
   if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(int64_t(pln.krows) * pln.Mp) ||
       !fits_i32(p.Ntot + 256) || (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))

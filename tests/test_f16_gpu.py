@@ -81,9 +81,15 @@ def _sparse(rng, shape, nonzeros):
     (2, 5, 17, 19, 64, 3, 1, 1, 128, 3),   # 64-row tile -> 3x3 gather, 128-row tile
     (3, 8, 9, 9, 20, 1, 1, 0, 130, 3),     # 1x1 on f32 input -> 3x3 on C % 8 != 0 (per-element NHWC), M % 8 != 0
     (2, 3, 31, 29, 8, 3, 2, 1, 40, 3),     # 3x3/s2 -> 3x3 on C = 8 (K = 72: a partial last k stage)
+    (1, 4, 12, 12, 24, 5, 1, 2, 16, 3),    # 5x5 pad 2 on 4 channels (odd kw: the PAIR padding tap)
 ])
-def test_f16_conv_exact_integers(gpu_ctx, case):
+@pytest.mark.parametrize("first,dma", [("pair", "1"), ("nhwc8", "1"), ("nhwc8", "0"), ("nchw", "1")])
+def test_f16_conv_exact_integers(gpu_ctx, case, first, dma, monkeypatch):
+    """first: operand mode of the conv on the f32 input (ORE_F16_FIRST); dma: 16-B NHWC convs on the
+    LDS-DMA kernel (1) or the register-staged one (0)."""
     import ore
+    monkeypatch.setenv("ORE_F16_FIRST", first)
+    monkeypatch.setenv("ORE_F16_DMA", dma)
     N, C, H, W, M1, k1, s1, p1, M2, k2 = case
     rng = np.random.default_rng(hash(case) & 0xffff)
     x = _ints(rng, -2, 2, (N, C, H, W))
@@ -185,3 +191,23 @@ def test_f16_rejects_f32_only_ops(gpu_ctx):
         ore.Model(gpu_ctx, mb, max_batch=1, precision="f16")
     with pytest.raises(ore.OreError):
         ore.Model(gpu_ctx, mb, max_batch=1, precision="bf16")
+
+
+@pytest.mark.parametrize("cfg", ["0", "1", "2", "3"])
+def test_f16_dma_kernel_bit_identical(gpu_ctx, cfg, monkeypatch):
+    """The LDS-DMA kernel (ORE_F16_DMA=1, default) runs the same MFMA chain as the register-staged
+    one: equal outputs, every block tile (ORE_CONV_CFG)."""
+    import ore
+    from ore import squeezenet
+    mb = squeezenet.build(64)
+    x = _t(squeezenet.synthetic_input(3, 64, seed=4))
+    monkeypatch.setenv("ORE_CONV_CFG", cfg)
+    outs = []
+    for dma in ("1", "0"):
+        monkeypatch.setenv("ORE_F16_DMA", dma)
+        m = ore.Model(gpu_ctx, mb, max_batch=3, precision="f16")
+        m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+        outs.append((_np(m.run(x)), m.read_value("fire9/concat_1")))
+        m.close()
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
