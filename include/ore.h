@@ -151,18 +151,27 @@ ore_status ore_model_load(ore_ctx* ctx, const void* onnx_bytes, size_t len, int6
 ore_status ore_model_load_ex(ore_ctx* ctx, const void* onnx_bytes, size_t len, int64_t max_batch, int32_t flags,
                              ore_model** out);
 ore_status ore_model_destroy(ore_model* m);
-/* flags: bit 0 = fuse Conv->Relu, bit 1 = Concat in place, bit 2 = alias Dropout/Reshape.
- * ORE_FUSE_ALL is the default; 0 runs every node as its own kernel (op-by-op parity). */
+/* flags: bit 0 = fuse Conv->Relu, bit 1 = Concat in place, bit 2 = alias Dropout/Reshape,
+ * bit 5 = Conv->MaxPool (ORE_FUSE_CONV_POOL below).  ORE_FUSE_ALL is the default; 0 runs every
+ * node as its own kernel (op-by-op parity). */
 #define ORE_FUSE_CONV_RELU 1
 #define ORE_FUSE_CONCAT 2
 #define ORE_FUSE_ALIAS 4
-#define ORE_FUSE_ALL 7
+#define ORE_FUSE_ALL 39
 /* bit 4 (opt-in, not in ORE_FUSE_ALL): a 3x3 MaxPool whose only consumer is a 1x1 stride-1 Conv
  * runs inside that conv's operand gather (each B element = the window max of the pre-pool
  * tensor); the pooled tensor is never written.  Max is exact, so results are bit-identical.
  * Measured slower than the separate plane-staged pool on SqueezeNet (9 loads per operand
  * element lose the pool kernel's row reuse: +150 us per step at batch 256). */
 #define ORE_FUSE_POOL_CONV 16
+/* bit 5 (in ORE_FUSE_ALL): Conv (-> Relu) -> 3x3 / stride-2 MaxPool as ONE launch when the conv
+ * output has no other consumer: each block computes a 13 x 19 patch of conv outputs covering a
+ * 6 x 9 tile of pooled outputs (the overlapping window row / column is recomputed by the
+ * neighbouring tile) and stores only the pooled values; the pre-pool tensor never reaches HBM.
+ * Bit-identical (same per-output MFMA chain; max is exact).  Applied when the computed columns are
+ * <= ORE_EPOOL_MAX_WORK (environment, default 1.25) x the conv's own (SqueezeNet @224: conv1 +
+ * pool1 only, 1.16x); f32 models. */
+#define ORE_FUSE_CONV_POOL 32
 /* debug: give every value its own storage (no liveness reuse) so any value can be read back */
 #define ORE_KEEP_VALUES 8
 ore_status ore_model_set_fusion(ore_model* m, int32_t flags);

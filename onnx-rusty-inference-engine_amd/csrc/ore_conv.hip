@@ -26,6 +26,10 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));  // first-class vector (no struct copies)
 typedef int int4d __attribute__((ext_vector_type(4)));
 
+// pooled-epilogue tile (ORE_FUSE_CONV_POOL, 3x3 / stride-2 pools): 6 x 9 pooled outputs per block
+// from a 13 x 19 = 247-column conv-output patch of a 256-column N tile
+constexpr int EPOOL_PR = EPOOL_TILE_PR, EPOOL_PC = EPOOL_TILE_PC, EPOOL_RC = 2 * EPOOL_PR + 1, EPOOL_CC = 2 * EPOOL_PC + 1;
+
 #ifndef ORE_DMA_ASM
 #define ORE_DMA_ASM 0  // 1: B-tile LDS-DMA by inline asm (measured equal: 5.38 vs 5.39 ms per step)
 #endif
@@ -83,7 +87,7 @@ enum { B1X1 = 0, BGATHER = 1, BPOOL = 2 };  // BPOOL: B = 3x3 window max of the 
 // WS (warp-specialised): 512 threads; waves 0-3 only read LDS and issue MFMAs, waves 4-7 only
 // gather the next K tile into the other LDS buffer.  Both roles meet at the same barrier once
 // per K tile, so the MFMA waves' instruction stream carries no global loads or gather math.
-template <int BM, int BN, int WM, int WN, int BK, int BMODE, int DMA, int WS = 0>
+template <int BM, int BN, int WM, int WN, int BK, int BMODE, int DMA, int WS = 0, int EP = 0>
 __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_kernel(ConvParams p) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 32, FN = TN / 32;
@@ -132,12 +136,35 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
   const int bcol = tid % BN;
   const int krow = __builtin_amdgcn_readfirstlane(tid / BN);
   const int bn = n0 + bcol;
-  const bool bn_ok = bn < p.Ntot;
+  bool bn_ok = bn < p.Ntot;
   // element offsets fit in 32 bits (checked on the host): uniform base + 32-bit lane offset
   int xoff;
   int ih0 = 0, iw0 = 0;
   int pmask = 0;  // BPOOL: bit r*3+s set when window tap (r, s) is inside the pre-pool plane
-  {
+  // EP (pooled epilogue): N tile nt = (image, pooled tile row, pooled tile column); its BN columns
+  // are an ep_rc x ep_cc patch of conv outputs (row-major), the conv pixels that the tile's
+  // ep_pr x ep_pc pooled outputs read
+  // (3x3 / stride-2 pool: EPOOL_PR x EPOOL_PC pooled outputs from an EPOOL_RC x EPOOL_CC patch)
+  int ep_img = 0, ep_ph0 = 0, ep_pw0 = 0;
+  if (EP) {
+    const int tpi = p.ep_tr * p.ep_tc;
+    ep_img = nt / tpi;
+    const int t = nt - ep_img * tpi;
+    ep_ph0 = (t / p.ep_tc) * EPOOL_PR;
+    ep_pw0 = (t - (t / p.ep_tc) * p.ep_tc) * EPOOL_PC;
+    const int prc = bcol / EPOOL_CC, pcc = bcol - prc * EPOOL_CC;
+    const int oh = ep_ph0 * 2 - p.ep_pt + prc, ow = ep_pw0 * 2 - p.ep_pl + pcc;
+    bn_ok = ep_img < p.N && bcol < EPOOL_RC * EPOOL_CC && (unsigned)oh < (unsigned)p.Ho && (unsigned)ow < (unsigned)p.Wo;
+    xoff = ep_img * (int)p.x_nstride;
+    if (BMODE == B1X1) {
+      xoff += oh * p.W + ow;
+    } else {
+      ih0 = oh * p.sh - p.pt;
+      iw0 = ow * p.sw - p.pl;
+      xoff += ih0 * p.W + iw0;
+    }
+    if (!bn_ok) xoff = 0;
+  } else {
     const int nn = bn_ok ? bn : 0;
     const int img = nn / YPS;
     const int pix = nn - img * YPS;  // pix >= Ho*Wo: a pad column, computed and never read
@@ -348,6 +375,65 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
 
   // ---- epilogue: + bias, optional Relu, store to NCHW (possibly a channel slice)
   float* __restrict__ y = p.y;
+  if constexpr (EP) {
+    // pooled epilogue: per 32-row fragment i the block's [32][BN] conv outputs (bias + Relu; 0 for
+    // patch positions outside the conv plane = the pool's zero padding, max_pool_op.rs:265-276) go
+    // to LDS, then each of the tile's 6 x 9 pooled outputs per row takes the 3x3 max starting from
+    // -FLT_MAX (:337) and is stored to the pooled NCHW plane.  The pre-pool tensor never reaches HBM.
+    static_assert(WM == 1, "all waves share the tile's rows");
+    constexpr int SROW = BN + 4;
+    static_assert(32 * SROW <= MAIN_FLOATS && EPOOL_RC * EPOOL_CC <= BN, "pooled epilogue staging");
+    __syncthreads();  // every wave is done with the A/B tiles
+#ifdef ORE_EXP_EP_NOPOOL  // timing experiment: main loop only
+    {
+      float t_ = 0.0f;
+      for (int i = 0; i < FM; ++i)
+        for (int j = 0; j < FN; ++j)
+          for (int e = 0; e < 16; ++e) t_ += acc[i][j][e];
+      if (t_ == 1234.5f) y[tid] = t_;
+    }
+    return;
+#endif
+    const int ohb = ep_ph0 * 2 - p.ep_pt, owb = ep_pw0 * 2 - p.ep_pl;  // conv position of patch (0, 0)
+    bool cok[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wn0 + j * 32 + lcol;
+      const int prc = col / EPOOL_CC, pcc = col - prc * EPOOL_CC;
+      cok[j] = col < EPOOL_RC * EPOOL_CC && (unsigned)(ohb + prc) < (unsigned)p.Ho && (unsigned)(owb + pcc) < (unsigned)p.Wo;
+    }
+    const int pch = tid >> 3, sub = tid & 7;  // pooling: 8 threads per channel row
+#pragma unroll  // static acc indices (a runtime i would move the accumulators to scratch)
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int r = (e & 3) + 8 * (e >> 2) + 4 * lrow;
+          float v = acc[i][j][e] + sbias[i * 32 + r];
+          if (p.relu) v = fmaxf(v, 0.0f);
+          smem[r * SROW + wn0 + j * 32 + lcol] = cok[j] ? v : 0.0f;
+        }
+      __syncthreads();
+      const int m = m0 + i * 32 + pch;
+      const float* row = smem + pch * SROW;
+#pragma unroll
+      for (int q = sub; q < EPOOL_PR * EPOOL_PC; q += 8) {
+        const int a = q / EPOOL_PC, b = q - a * EPOOL_PC;
+        const float* w0 = row + (2 * a) * EPOOL_CC + 2 * b;
+        float mx = -FLT_MAX;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int sx = 0; sx < 3; ++sx) mx = fmaxf(mx, w0[r * EPOOL_CC + sx]);
+        const int ph = ep_ph0 + a, pw = ep_pw0 + b;
+        if (ph < p.ep_Ho && pw < p.ep_Wo && m < p.M && ep_img < p.N)
+          y[(unsigned)(ep_img * (int)p.y_nstride + m * YPS + ph * p.ep_Wo + pw)] = mx;
+      }
+      __syncthreads();
+    }
+    return;
+  }
   if (ORE_WS_VEC_EPI && p.vec_out) {
     // 16-B stores: each wave stages 32 output rows x TN pixels in its own LDS slice (column
     // halves swapped every 4 rows so the two lane halves' writes hit different banks), then
@@ -775,6 +861,39 @@ static void launch_conv_cfg(const ConvParams& p0, hipStream_t s) {
     else
       hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BGATHER, 0>), grid, block, 0, s, p);
   }
+}
+
+// Conv + MaxPool in one launch (ORE_FUSE_CONV_POOL): 1x4-wave tiles of BM x 256 (the N tile is a
+// conv-output patch, run_conv_epool picks its shape)
+template <int BM>
+static void launch_conv_epool_cfg(const ConvParams& p0, hipStream_t s) {
+  constexpr int BK = 16, BN = 256;
+  ConvParams p = p0;
+  p.mtiles = (p.M + BM - 1) / BM;
+  p.ntiles = p.N * p.ep_tr * p.ep_tc;
+  dim3 grid(p.mtiles * p.ntiles), block(256);
+  const bool dma = p.x_bytes > 0 && env_int("ORE_CONV_DMA", 1) != 0;
+  if (p.is1x1) {
+    if (dma)
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 1, 4, BK, B1X1, 1, 0, 1>), grid, block, 0, s, p);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 1, 4, BK, B1X1, 0, 0, 1>), grid, block, 0, s, p);
+  } else {
+    if (dma)
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 1, 4, BK, BGATHER, 1, 0, 1>), grid, block, 0, s, p);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 1, 4, BK, BGATHER, 0, 0, 1>), grid, block, 0, s, p);
+  }
+}
+
+void launch_conv_epool(const ConvParams& p, hipStream_t s) {
+  // rows per tile: 96 when it divides the channel count (conv1's 96), else 128, or 32 for M <= 32
+  if (p.M <= 32)
+    launch_conv_epool_cfg<32>(p, s);
+  else if (p.M % 96 == 0 || p.M < 96)
+    launch_conv_epool_cfg<96>(p, s);
+  else
+    launch_conv_epool_cfg<128>(p, s);
 }
 
 // Block tiles, chosen per layer to minimise the padded output channels (MFMA work on rows

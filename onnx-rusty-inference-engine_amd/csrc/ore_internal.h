@@ -97,6 +97,18 @@ ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_
                         int64_t x_nstride, int64_t x_ps, const void* wp, const int2* ktab, int64_t M, int64_t kh,
                         int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, void* y,
                         int64_t y_nstride, int64_t y_ps);
+// Conv (+ Relu) and the MaxPool (pkh x pkw, strides psh/psw, window pwin over the conv's Ho x Wo
+// output) in one launch: y is the pooled output (image stride y_nstride, plane stride y_ps)
+ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
+                          int64_t x_nstride, int64_t x_ps, const float* wp, const int2* ktab, int64_t M, int64_t kh,
+                          int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu,
+                          int64_t pkh, int64_t pkw, int64_t psh, int64_t psw, const Window& pwin, float* y,
+                          int64_t y_nstride, int64_t y_ps);
+// pooled-epilogue tiling of a conv output (Ho x Wo) and its pool (3x3 / stride 2 only): *tr x *tc
+// tiles of 6 x 9 pooled outputs per image; returns the work factor tiles * CONV_EPOOL_BN / (Ho * Wo)
+// (the conv columns computed, recomputed overlap and padding included), 0 for other pools
+double epool_tile(int64_t Ho, int64_t Wo, int64_t pkh, int64_t pkw, int64_t psh, int64_t psw, const Window& pwin,
+                  int* tr, int* tc);
 // 1x1 conv over the 3x3 MaxPool (window pwin, strides psh/psw) of x [C][pH][pW] (plane stride x_ps):
 // the pooled tensor is never materialised (ORE_FUSE_POOL_CONV)
 ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t pH,

@@ -35,6 +35,10 @@ struct ConvParams {
   int pool_sh, pool_sw, pool_pt, pool_pl, pool_H, pool_W;
   // window-staged kernel (filled by the launcher from the ConvPlan)
   int bch, ks, nst, wr, ww, tiles_per_img;
+  // pooled epilogue (ORE_FUSE_CONV_POOL, launch_conv_epool; 3x3 / stride-2 pool): y is the MaxPool
+  // output [..][ep_Ho][ep_Wo] (plane stride y_ps), pool pads ep_pt / ep_pl; a block's N tile is a
+  // 13 x 19 patch of conv outputs feeding a 6 x 9 tile of pooled outputs, ep_tr x ep_tc tiles per image
+  int ep_pt, ep_pl, ep_Ho, ep_Wo, ep_tr, ep_tc;
 };
 
 // Per-layer kernel choice and weight layout (see plan_conv in ore_conv.hip).
@@ -118,6 +122,10 @@ size_t conv_packed_bytes(const ConvPlan& pln);
 void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, const ConvPlan& pln, float* wp,
                  hipStream_t s);
 void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s);
+// Conv (+ Relu) with the following MaxPool in its epilogue (ConvParams ep_* set; f32)
+void launch_conv_epool(const ConvParams& p, hipStream_t s);
+constexpr int CONV_EPOOL_BN = 256;  // N tile of the pooled-epilogue kernel
+constexpr int EPOOL_TILE_PR = 6, EPOOL_TILE_PC = 9;  // pooled outputs per block (13 x 19 conv patch)
 // LDS-free, barrier-free variant (ore_conv_direct.hip): tiles 4-7 (needs p.x_bytes > 0)
 void launch_conv_direct(const ConvParams& p, int tile, hipStream_t s);
 constexpr int CONV_TILES_F32 = 12;  // 0-3 conv_gemm_kernel, 4-7 conv_direct_kernel (ORE_CONV_CFG only),

@@ -81,6 +81,10 @@ struct Step {
   bool pool = false;
   int64_t pH = 0, pW = 0, psh = 1, psw = 1;
   Window pwin;
+  // fused following MaxPool (ORE_FUSE_CONV_POOL): out is the pool's output; pool geometry below
+  bool epool = false;
+  int64_t ep_kh = 0, ep_kw = 0, ep_sh = 1, ep_sw = 1;
+  Window ep_win;
   ConvPlan plan{};        // kernel choice and weight layout for S_CONV / S_MATMUL
   float* wp = nullptr;    // packed weights (layout per plan) for S_CONV / S_MATMUL
   const int2* ktab = nullptr;  // gather table (follows wp in the packed allocation; gather kernel only)
@@ -529,6 +533,32 @@ ore_status plan(ore_model* m) {
     }
     count_uses(m, m->steps);
   }
+  // (1c) Conv (-> Relu) -> MaxPool, the conv output read by the pool only: one launch when the
+  // recomputed patch costs <= ORE_EPOOL_MAX_WORK x the conv's columns (f32)
+  if ((m->fusion & ORE_FUSE_CONV_POOL) && !m->f16) {
+    const char* e = getenv("ORE_EPOOL_MAX_WORK");  // tuning knob
+    const double max_work = e ? atof(e) : 1.25;
+    for (size_t i = 0; i < m->steps.size(); ++i) {
+      Step& pl = m->steps[i];
+      if (pl.kind != S_MAXPOOL) continue;
+      const int v = pl.in0;
+      const int pc = producer[v];
+      if (pc < 0 || m->values[v].uses != 1 || m->values[v].is_output) continue;
+      Step& cv = m->steps[pc];
+      if (cv.kind != S_CONV || cv.pool || cv.epool || cv.plan.window || cv.plan.f16) continue;
+      int a = 0, b = 0;
+      const double work = epool_tile(cv.win.Ho, cv.win.Wo, pl.kh, pl.kw, pl.sh, pl.sw, pl.win, &a, &b);
+      if (work == 0.0 || work > max_work) continue;
+      cv.epool = true;
+      cv.out = pl.out;
+      cv.ep_kh = pl.kh; cv.ep_kw = pl.kw; cv.ep_sh = pl.sh; cv.ep_sw = pl.sw; cv.ep_win = pl.win;
+      m->values[v].elided = true;
+      producer[pl.out] = pc;
+      pl.kind = S_NOP;
+      pl.in0 = -1;
+    }
+    count_uses(m, m->steps);
+  }
   // (2) Dropout / activation Reshape as aliases
   if (m->fusion & ORE_FUSE_ALIAS) {
     for (auto& s : m->steps) {
@@ -785,6 +815,10 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       if (s.plan.f16)
         return run_conv_f16(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.ktab, s.M, s.kh, s.kw, bias,
                             s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps);
+      if (s.epool)
+        return run_conv_epool(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.ktab, s.M, s.kh, s.kw, bias,
+                              s.win, s.sh, s.sw, s.relu, s.ep_kh, s.ep_kw, s.ep_sh, s.ep_sw, s.ep_win, y.p, y.nstride,
+                              y.ps);
       if (s.pool)
         return run_conv_pool(ctx, s.plan, x.p, n, s.C, s.pH, s.pW, x.nstride, x.ps, s.pwin, s.psh, s.psw, s.wp, s.M, bias,
                              s.relu, y.p, y.nstride, y.ps, x.es);
@@ -994,7 +1028,7 @@ ore_status ore_model_destroy(ore_model* m) {
 
 ore_status ore_model_set_fusion(ore_model* m, int32_t flags) {
   if (!m) return set_error(nullptr, ORE_ERR_INVALID, "null model");
-  m->fusion = flags & (ORE_FUSE_ALL | ORE_FUSE_POOL_CONV | ORE_KEEP_VALUES);
+  m->fusion = flags & (ORE_FUSE_ALL | ORE_FUSE_POOL_CONV | ORE_FUSE_CONV_POOL | ORE_KEEP_VALUES);
   return plan(m);
 }
 

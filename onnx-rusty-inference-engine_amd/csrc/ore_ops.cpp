@@ -180,6 +180,61 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
   return ORE_OK;
 }
 
+double epool_tile(int64_t Ho, int64_t Wo, int64_t pkh, int64_t pkw, int64_t psh, int64_t psw, const Window& pwin,
+                  int* tr, int* tc) {
+  // the kernel's pooled epilogue is specialised for 3x3 / stride-2 windows (every SqueezeNet pool)
+  if (pkh != 3 || pkw != 3 || psh != 2 || psw != 2 || Ho * Wo == 0 || pwin.Ho <= 0 || pwin.Wo <= 0) return 0.0;
+  *tr = int((pwin.Ho + EPOOL_TILE_PR - 1) / EPOOL_TILE_PR);
+  *tc = int((pwin.Wo + EPOOL_TILE_PC - 1) / EPOOL_TILE_PC);
+  return double(int64_t(*tr) * *tc * CONV_EPOOL_BN) / double(Ho * Wo);
+}
+
+ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
+                          int64_t x_nstride, int64_t x_ps, const float* wp, const int2* ktab, int64_t M, int64_t kh,
+                          int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu,
+                          int64_t pkh, int64_t pkw, int64_t psh, int64_t psw, const Window& pwin, float* y,
+                          int64_t y_nstride, int64_t y_ps) {
+  if (N == 0) return ORE_OK;
+  if (pln.f16 || pln.window) return set_error(ctx, ORE_ERR_INVALID, "internal: the pooled epilogue is f32 gather only");
+  if (x_ps == 0) x_ps = H * W;
+  if (y_ps == 0) y_ps = pwin.Ho * pwin.Wo;
+  int tr = 0, tc = 0;
+  if (epool_tile(win.Ho, win.Wo, pkh, pkw, psh, psw, pwin, &tr, &tc) == 0.0)
+    return set_error(ctx, ORE_ERR_INVALID, "internal: the pooled epilogue takes 3x3 / stride-2 pools");
+  ConvParams p{};
+  p.x = x; p.wp = wp; p.ktab = ktab; p.bias = bias; p.y = y;
+  p.N = int(N); p.C = int(C); p.H = int(H); p.W = int(W);
+  p.M = int(M); p.kh = int(kh); p.kw = int(kw); p.sh = int(sh); p.sw = int(sw);
+  p.pt = int(win.pt); p.pl = int(win.pl);
+  p.Ho = int(win.Ho); p.Wo = int(win.Wo);
+  p.K = int(C * kh * kw);
+  p.P = int(win.Ho * win.Wo);
+  p.x_ps = int(x_ps);
+  p.y_ps = int(y_ps);
+  p.x_nstride = x_nstride;
+  p.y_nstride = y_nstride;
+  p.relu = relu ? 1 : 0;
+  p.Mp = pln.Mp;
+  p.x_f32 = 1;
+  {
+    const int64_t extent = ((N - 1) * x_nstride + C * x_ps) * 4;
+    p.x_bytes = (extent > 0 && extent < (int64_t(1) << 31)) ? extent : 0;
+  }
+  p.is1x1 = (kh == 1 && kw == 1 && sh == 1 && sw == 1 && win.pt == 0 && win.pl == 0 && win.Ho == H && win.Wo == W &&
+             x_ps == H * W);
+  p.ep_pt = int(pwin.pt); p.ep_pl = int(pwin.pl); p.ep_Ho = int(pwin.Ho); p.ep_Wo = int(pwin.Wo);
+  p.ep_tr = tr; p.ep_tc = tc;
+  p.Ntot = N * int64_t(p.ep_tr) * p.ep_tc * CONV_EPOOL_BN;
+  if (x_ps < H * W || y_ps < pwin.Ho * pwin.Wo) return set_error(ctx, ORE_ERR_INVALID, "plane stride below plane size");
+  if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(int64_t(pln.krows) * pln.Mp) ||
+      !fits_i32(p.Ntot + 256) || N * p.ep_tr * p.ep_tc * ((M + 31) / 32) >= (int64_t(1) << 31))
+    return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
+  if (!p.is1x1 && !ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
+  launch_conv_epool(p, ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
+}
+
 ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t pH,
                          int64_t pW, int64_t x_nstride, int64_t x_ps, const Window& pwin, int64_t psh, int64_t psw,
                          const float* wp, int64_t M, const float* bias, bool relu, float* y, int64_t y_nstride,

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tag", default=os.path.basename(os.environ.get("ORE_LIB", "libore.so")))
+    ap.add_argument("--fusion", type=int, default=None, help="ore_model_set_fusion flags (default: the model's)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -26,6 +27,8 @@ def main():
     m = ore.Model(ctx, squeezenet.build(224), max_batch=a.batch, precision=a.precision)
     x = torch.from_numpy(squeezenet.synthetic_input(a.batch, 224, seed=0)).cuda()
     out = torch.empty((a.batch, m.output_elems), device="cuda")
+    if a.fusion is not None:
+        m.set_fusion(a.fusion)
     m.autotune(x, out)
     m.enable_timing(True)
     for _ in range(2):

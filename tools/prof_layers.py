@@ -63,8 +63,19 @@ def main():
             if ("ore::" in r["Kernel_Name"] or "_ZN3ore" in r["Kernel_Name"]) and "pack" not in r["Kernel_Name"] and "ktab" not in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     geo = geometry()
-    if any("nchw_to_nhwc4" in r["Kernel_Name"] for r in rows[-64:]):  # f16: the first conv's input conversion
+    if any("nchw_to_nhwc" in r["Kernel_Name"] for r in rows[-64:]):  # f16: the first conv's input conversion
         geo.insert(0, ("to_nhwc4", "cvt", 4, 3, 0, 224, 224))
+    # kernels per pass from the period of the name sequence; one fewer than the layer list = pool1
+    # fused into conv1 (ORE_FUSE_CONV_POOL)
+    names = [r["Kernel_Name"] for r in rows]
+    period = next((q for q in (len(geo), len(geo) - 1)
+                   if len(names) >= 3 * q and names[-q:] == names[-2 * q:-q] == names[-3 * q:-2 * q]), len(geo))
+    if period == len(geo) - 1:
+        k1 = next(i for i, g in enumerate(geo) if g[0] == "conv1")
+        name, kind, M, C, kk, H, Ho = geo[k1]
+        pool = geo[k1 + 1]
+        geo[k1] = ("conv1+pool1", "conv", M, C, kk, H, Ho, pool[6])
+        del geo[k1 + 1]
     per = len(geo)
     n = len(rows) // per
     if "--passes" in sys.argv:
@@ -78,15 +89,16 @@ def main():
     for k in range(per):
         ds = sorted(agg[k])
         d = ds[len(ds) // 2] / 1e3
-        name, kind, M, C, kk, H, Ho = geo[k]
+        name, kind, M, C, kk, H, Ho = geo[k][:7]
+        Hout = geo[k][7] if len(geo[k]) > 7 else Ho  # stored plane (the pooled one when fused)
         in_es = 4 if (k == 0 or kind in ("softmax", "cvt")) else es
         out_es = 4 if kind in ("gap", "softmax") else es
-        if kind == "conv" and name == "conv1" and geo[0][1] == "cvt":
+        if kind == "conv" and name.startswith("conv1") and geo[0][1] == "cvt":
             in_es, C = 2, 4  # reads the NHWC4 f16 copy
         fl = 2.0 * M * C * kk * kk * Ho * Ho * B if kind == "conv" else 0.0
-        if name == "conv1" and geo[0][1] == "cvt":
+        if name.startswith("conv1") and geo[0][1] == "cvt":
             fl = 2.0 * M * 3 * kk * kk * Ho * Ho * B
-        by = B * (in_es * C * H * H + out_es * M * Ho * Ho)
+        by = B * (in_es * C * H * H + out_es * M * Hout * Hout)
         ideal = max(fl / peak, by / HBM) * 1e6
         tot += d
         tot_ideal += ideal
