@@ -1179,14 +1179,19 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
   // every output is the same k-ordered MFMA chain)
   for (size_t k = 0; k < m->exec_steps.size() && !st; ++k) {
     Step& s = m->steps[m->exec_steps[k]];
-    if (s.kind != S_CONV || s.plan.window) {
+    if (s.kind != S_CONV || s.plan.window || s.epool) {  // the pooled epilogue has one tile shape
       st = launch_step(m, s, n);
       continue;
     }
     int best = s.plan.cfg;
     float best_ms = 1e30f;
-    const int ntiles = CONV_TILES_AUTOTUNE;
-    for (int c = 0; c < ntiles && !st; ++c) {
+    // candidates: the four LDS-staged tiles and, for f32, their warp-specialised forms (8-11: they
+    // win on the long-K, few-row 1x1 squeezes, e.g. fire7/8 113 -> 97 us); ORE_AUTOTUNE_WS=0 drops them
+    std::vector<int> cands = {0, 1, 2, 3};
+    const char* ews = getenv("ORE_AUTOTUNE_WS");
+    if (!s.plan.f16 && !(ews && !atoi(ews))) cands.insert(cands.end(), {8, 9, 10, 11});
+    for (size_t ci = 0; ci < cands.size() && !st; ++ci) {
+      const int c = cands[ci];
       s.plan.cfg = c;
       st = launch_step(m, s, n);  // warm-up
       if (st) break;

@@ -273,7 +273,8 @@ class Model:
                                         ctypes.c_void_p(out.data_ptr()), int(reps)), self.ctx.h)
 
     TILE_NAMES = ["128x128", "96x128", "64x128", "32x256",
-                  "direct 128x128", "direct 96x128", "direct 64x128", "direct 128x64"]
+                  "direct 128x128", "direct 96x128", "direct 64x128", "direct 128x64",
+                  "ws 128x128", "ws 96x128", "ws 64x128", "ws 32x256"]
 
     def tiles(self):
         """Block tile per exec step (-1 for non-conv steps); names in TILE_NAMES."""
