@@ -552,6 +552,8 @@ ore_status plan(ore_model* m) {
       cv.epool = true;
       cv.out = pl.out;
       cv.ep_kh = pl.kh; cv.ep_kw = pl.kw; cv.ep_sh = pl.sh; cv.ep_sw = pl.sw; cv.ep_win = pl.win;
+      // algorithmic bytes: the conv's input + the pooled output (the pre-pool tensor never moves)
+      cv.bytes_per_img = 4.0 * double(cv.C * cv.H * cv.W) + 4.0 * double(cv.M * pl.win.Ho * pl.win.Wo);
       m->values[v].elided = true;
       producer[pl.out] = pc;
       pl.kind = S_NOP;

@@ -12,13 +12,38 @@ from collections import OrderedDict, defaultdict
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "onnx-rusty-inference-engine_amd"))
-PER = 31
+PER = 31  # set by main() from the kernel-name period of the trace
 
 
-def layer_names():
+def layer_names(period):
+    """Layer names per launched kernel: pool1 fused into conv1 (ORE_FUSE_CONV_POOL) and the f16
+    input conversion change the count; decided from the trace's period."""
     from ore import onnx_wire, squeezenet
     m = onnx_wire.decode_model(squeezenet.build(224))
-    return [n.name for n in m.graph.node if n.op_type in ("Conv", "MaxPool", "GlobalAveragePool", "Softmax")]
+    names = [n.name for n in m.graph.node if n.op_type in ("Conv", "MaxPool", "GlobalAveragePool", "Softmax")]
+    if period == len(names) + 1:
+        names.insert(0, "to_nhwc")
+    if period in (len(names) - 1, len(names)) and "pool1" in names and period == len(names) - 1:
+        names[names.index("conv1")] = "conv1+pool1"
+        names.remove("pool1")
+    if period == len(names) - 1 and "to_nhwc" in names:  # f16 conversion + fused pool (not built)
+        names.remove("to_nhwc")
+    return names
+
+
+def period_of(d):
+    """Kernels per bench step from the repetition of the ore kernel names."""
+    f = os.path.join(d, "run_counter_collection.csv")
+    disp = OrderedDict()
+    for r in csv.DictReader(open(f)):
+        if ("ore::" in r["Kernel_Name"] or "_ZN3ore" in r["Kernel_Name"]) and "pack_" not in r["Kernel_Name"] and \
+                "ktab" not in r["Kernel_Name"]:
+            disp.setdefault(int(r["Dispatch_Id"]), r["Kernel_Name"])
+    names = list(disp.values())
+    for q in range(20, 40):
+        if len(names) >= 2 * q and names[-q:] == names[-2 * q:-q]:
+            return q
+    return 31
 
 
 def load(d):
@@ -27,7 +52,8 @@ def load(d):
         return None
     disp = OrderedDict()
     for r in csv.DictReader(open(f)):
-        if "ore::" not in r["Kernel_Name"] or "pack_" in r["Kernel_Name"] or "ktab" in r["Kernel_Name"]:
+        if ("ore::" not in r["Kernel_Name"] and "_ZN3ore" not in r["Kernel_Name"]) or "pack_" in r["Kernel_Name"] or \
+                "ktab" in r["Kernel_Name"]:
             continue
         k = int(r["Dispatch_Id"])
         e = disp.setdefault(k, {"name": r["Kernel_Name"], "dur": int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
@@ -38,9 +64,12 @@ def load(d):
 
 
 def main():
+    global PER
     base = sys.argv[1]
     json_out = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
-    names = layer_names()
+    first = sorted(d for d in glob.glob(os.path.join(base, "p*")) if os.path.isdir(d))
+    PER = period_of(first[0]) if first else 31
+    names = layer_names(PER)
     merged = [defaultdict(float) for _ in range(PER)]
     for d in sorted(glob.glob(os.path.join(base, "p*"))):
         if not os.path.isdir(d):
