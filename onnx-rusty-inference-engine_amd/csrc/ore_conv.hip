@@ -30,6 +30,10 @@ typedef int int4d __attribute__((ext_vector_type(4)));
 // from a 13 x 19 = 247-column conv-output patch of a 256-column N tile
 constexpr int EPOOL_PR = EPOOL_TILE_PR, EPOOL_PC = EPOOL_TILE_PC, EPOOL_RC = 2 * EPOOL_PR + 1, EPOOL_CC = 2 * EPOOL_PC + 1;
 
+#ifndef ORE_A_DMA
+#define ORE_A_DMA 1  // A (weight) tile by 16-B LDS-DMA too (0: registers + ds_write_b128)
+#endif
+
 #ifndef ORE_DMA_ASM
 #define ORE_DMA_ASM 0  // 1: B-tile LDS-DMA by inline asm (measured equal: 5.38 vs 5.39 ms per step)
 #endif
@@ -91,7 +95,11 @@ template <int BM, int BN, int WM, int WN, int BK, int BMODE, int DMA, int WS = 0
 __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_kernel(ConvParams p) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 32, FN = TN / 32;
-  constexpr int AS = BM + 4;                 // LDS row stride of the A tile (16-B aligned rows)
+  // ADMA: the A tile also goes global -> LDS by 16-B LDS-DMA (lane-linear, so unpadded rows; the
+  // fragment reads -- 32 consecutive floats per half-wave -- are conflict-free without padding)
+  // (measured: 96-row tiles gain 1-3 %, the 128x128 tile loses 4 % on fire4/expand3x3 -> off there)
+  constexpr bool ADMA = DMA && !WS && ORE_A_DMA && BM != 128;
+  constexpr int AS = ADMA ? BM : BM + 4;     // LDS row stride of the A tile (16-B aligned rows)
   constexpr int BROWS = 256 / BN;            // B rows loaded per pass
   constexpr int BLOADS = BK / BROWS;         // B elements per thread per tile
   constexpr int AF4 = BM * BK / 4;           // float4s in the A tile
@@ -190,6 +198,8 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
   }
   const float* __restrict__ x = p.x;
   const float* __restrict__ wp = p.wp;
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.wp), (short)0, (int)(((p.K + 31) & ~31) * p.Mp * 4), 0x00020000);
   // DMA: buffer resource over x's valid extent (bytes < 2^32, checked on the host); each wave
   // writes 64 consecutive columns of one B row
   const __amdgpu_buffer_rsrc_t xrsrc =
@@ -212,7 +222,15 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
       /* the A tile's tail float4s (AF4 % 256 != 0) reload element 0 and are not stored */           \
       const int e_ = (AF4 % 256 == 0 || tid + v_ * 256 < AF4) ? tid + v_ * 256 : 0;                  \
       const int kk = e_ / (BM / 4), mm = (e_ % (BM / 4)) * 4;                                        \
-      RA[v_] = *reinterpret_cast<const floatx4*>(wp + (unsigned)((k0_ + kk) * p.Mp + m0 + mm));      \
+      if (ADMA) {                                                                                    \
+        /* wave-uniform: a wave's 64 chunks are all inside or all past the tile */                  \
+        if (AF4 % 256 == 0 || v_ * 256 + wave * 64 < AF4)                                            \
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                  \
+              wrsrc, (__attribute__((address_space(3))) void*)(&As[(DBUF)][0][0] + (v_ * 256 + wave * 64) * 4), 16, \
+              ((k0_ + kk) * p.Mp + m0 + mm) * 4, 0, 0, 0);                                           \
+      } else {                                                                                       \
+        RA[v_] = *reinterpret_cast<const floatx4*>(wp + (unsigned)((k0_ + kk) * p.Mp + m0 + mm));    \
+      }                                                                                              \
     }                                                                                                \
     _Pragma("unroll") for (int j = 0; j < BLOADS; ++j) {                                             \
       const int k = k0_ + krow + j * BROWS;                                                          \
@@ -255,11 +273,12 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
   }
 #define ORE_STORE_TILE(RA, RB, ROK, BUF)                                                             \
   {                                                                                                  \
-    _Pragma("unroll") for (int v_ = 0; v_ < AVEC; ++v_) {                                            \
-      const int e_ = tid + v_ * 256;                                                                 \
-      const int kk = e_ / (BM / 4), mm = (e_ % (BM / 4)) * 4;                                        \
-      if (AF4 % 256 == 0 || e_ < AF4) *reinterpret_cast<floatx4*>(&As[BUF][kk][mm]) = RA[v_];        \
-    }                                                                                                \
+    if (!ADMA)                                                                                       \
+      _Pragma("unroll") for (int v_ = 0; v_ < AVEC; ++v_) {                                          \
+        const int e_ = tid + v_ * 256;                                                               \
+        const int kk = e_ / (BM / 4), mm = (e_ % (BM / 4)) * 4;                                      \
+        if (AF4 % 256 == 0 || e_ < AF4) *reinterpret_cast<floatx4*>(&As[BUF][kk][mm]) = RA[v_];      \
+      }                                                                                              \
     if (!DMA)                                                                                        \
       _Pragma("unroll") for (int j = 0; j < BLOADS; ++j)                                             \
         Bs[BUF][krow + j * BROWS][bcol] = ROK[j] ? RB[j] : 0.0f;                                     \
