@@ -1039,9 +1039,22 @@ static void launch_win_cfg(const ConvParams& p0, const ConvPlan& pln, hipStream_
   }
 }
 
+thread_local int last_conv_tile = -1;
+
 void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
+  last_conv_tile = pln.cfg;
   if (pln.f16) {
     launch_conv_f16(p, pln.cfg, pln.xmode, s);
+    return;
+  }
+  if (pln.cfg >= CONV_TILE_STREAM) {
+    if (conv_stream_eligible(p)) {
+      launch_conv_stream(p, pln.cfg, s);
+      return;
+    }
+    ConvPlan q = pln;  // not a stream geometry: the LDS-staged kernel
+    q.cfg = 0;
+    launch_conv(p, q, s);
     return;
   }
   if (pln.cfg >= 8) {  // warp-specialised variants of tiles 0-3

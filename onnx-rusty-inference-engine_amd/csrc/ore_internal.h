@@ -17,6 +17,10 @@ struct ore_ctx {
   std::string err;
   float* scratch = nullptr;  // per-op weight packing (stream-ordered reuse)
   size_t scratch_bytes = 0;
+  // a device range known to be mapped, set by the model walker around its conv launches (its arena,
+  // which has a 4 KiB lead): the streaming conv may read a few bytes before an input inside it
+  const char* mapped_lo = nullptr;
+  const char* mapped_hi = nullptr;
 };
 
 namespace ore {

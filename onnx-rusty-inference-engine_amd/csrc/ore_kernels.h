@@ -29,6 +29,9 @@ struct ConvParams {
                        // otherwise f16 NHWC with pixel stride x_ps (f16 kernels always write NHWC,
                        // pixel stride y_ps, columns dense over Ho*Wo: Ntot = N*P)
   long long x_bytes;   // bytes from x to the end of its last valid element (0: no buffer DMA path)
+  int x_guard;         // bytes before x known to be mapped (the streaming 3x3 conv reads a few of them,
+                       // zero-masked, instead of issuing negative buffer offsets)
+  int x_lead;          // filled by the streaming launcher: bytes it reads before x (<= x_guard)
   // fused MaxPool (ORE_FUSE_POOL_CONV, f32 only): x is the PRE-pool tensor [pool_H][pool_W] planes
   // and the conv (1x1) reads each B element as the 3x3 window max at stride (pool_sh, pool_sw)
   int pool;            // 1: BPOOL operand mode
@@ -128,8 +131,18 @@ constexpr int CONV_EPOOL_BN = 256;  // N tile of the pooled-epilogue kernel
 constexpr int EPOOL_TILE_PR = 6, EPOOL_TILE_PC = 9;  // pooled outputs per block (13 x 19 conv patch)
 // LDS-free, barrier-free variant (ore_conv_direct.hip): tiles 4-7 (needs p.x_bytes > 0)
 void launch_conv_direct(const ConvParams& p, int tile, hipStream_t s);
-constexpr int CONV_TILES_F32 = 12;  // 0-3 conv_gemm_kernel, 4-7 conv_direct_kernel (ORE_CONV_CFG only),
-                                    // 8-11 conv_gemm_kernel warp-specialised (512 threads)
+constexpr int CONV_TILES_F32 = 17;  // 0-3 conv_gemm_kernel, 4-7 conv_direct_kernel (ORE_CONV_CFG only),
+                                    // 8-11 conv_gemm_kernel warp-specialised (512 threads),
+                                    // 12-16 conv_stream_kernel (stride-1 geometries only)
+// LDS-free streaming kernel (ore_conv_stream.hip): 1x1 convs and stride-1 convs with Wo == W (every
+// expand3x3); tiles CONV_TILE_STREAM + 0..4 = 64x128, 32x256, 16x256, 48x128, 64x64 (channels x
+// pixels per wave); other geometries fall back to tile 0
+constexpr int CONV_TILE_STREAM = 12;
+bool conv_stream_eligible(const ConvParams& p);
+void launch_conv_stream(const ConvParams& p, int tile, hipStream_t s);
+// the tile launch_conv actually ran last on this thread (a 1x1 tile on an ineligible geometry runs
+// tile 0); ore_model_autotune skips candidates that fell back
+extern thread_local int last_conv_tile;
 constexpr int CONV_TILES_F16 = 4;
 constexpr int CONV_TILES_AUTOTUNE = 4;  // the direct tiles measured 15-80 % slower on every SqueezeNet layer
 void launch_maxpool(const PoolParams& p, hipStream_t s);

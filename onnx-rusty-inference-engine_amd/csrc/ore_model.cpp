@@ -108,7 +108,8 @@ struct ore_model {
   int output_value = -1;
   float* consts = nullptr;       // one device allocation for all f32 initializers
   float* packed = nullptr;       // packed conv / matmul weights (one allocation)
-  char* arena = nullptr;
+  char* arena = nullptr;        // arena_alloc + ARENA_LEAD
+  char* arena_alloc = nullptr;  // the hipMalloc'd block (a 4 KiB lead before the arena proper)
   size_t arena_bytes = 0;
   // timing
   bool timing = false;
@@ -680,11 +681,12 @@ ore_status plan(ore_model* m) {
     arena = std::max(arena, off + size);
   }
   if (size_t(arena) > m->arena_bytes) {
-    if (m->arena) (void)hipFree(m->arena);
-    m->arena = nullptr;
+    if (m->arena_alloc) (void)hipFree(m->arena_alloc);
+    m->arena = m->arena_alloc = nullptr;
     m->arena_bytes = 0;
-    if (arena > 0 && hipMalloc(reinterpret_cast<void**>(&m->arena), size_t(arena)) != hipSuccess)
+    if (arena > 0 && hipMalloc(reinterpret_cast<void**>(&m->arena_alloc), size_t(arena) + 4096) != hipSuccess)
       return err(m, ORE_ERR_OOM, "arena allocation of " + std::to_string(arena) + " bytes failed");
+    if (m->arena_alloc) m->arena = m->arena_alloc + 4096;
     m->arena_bytes = size_t(arena);
   }
   m->exec_steps.clear();
@@ -824,8 +826,12 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       if (s.pool)
         return run_conv_pool(ctx, s.plan, x.p, n, s.C, s.pH, s.pW, x.nstride, x.ps, s.pwin, s.psh, s.psw, s.wp, s.M, bias,
                              s.relu, y.p, y.nstride, y.ps, x.es);
-      return run_conv(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, s.wp, s.ktab, s.M, s.kh, s.kw, bias, s.win, s.sh, s.sw, s.relu,
-                      y.p, y.nstride, x.ps, y.ps, x.es);
+      ctx->mapped_lo = m->arena_alloc;  // the arena and its 4 KiB lead are mapped
+      ctx->mapped_hi = m->arena ? m->arena + m->arena_bytes : nullptr;
+      const ore_status st = run_conv(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, s.wp, s.ktab, s.M, s.kh, s.kw, bias,
+                                     s.win, s.sh, s.sw, s.relu, y.p, y.nstride, x.ps, y.ps, x.es);
+      ctx->mapped_lo = ctx->mapped_hi = nullptr;
+      return st;
     }
     case S_MATMUL: {
       const Ref x = ref_of(m, s.in0);
@@ -1019,7 +1025,7 @@ ore_status ore_model_destroy(ore_model* m) {
   if (m->side) (void)hipStreamDestroy(m->side);
   if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
   if (m->ev_join) (void)hipEventDestroy(m->ev_join);
-  if (m->arena) (void)hipFree(m->arena);
+  if (m->arena_alloc) (void)hipFree(m->arena_alloc);
   if (m->consts) (void)hipFree(m->consts);
   if (m->packed) (void)hipFree(m->packed);
   for (auto& s : m->base_steps)
@@ -1192,11 +1198,17 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
     std::vector<int> cands = {0, 1, 2, 3};
     const char* ews = getenv("ORE_AUTOTUNE_WS");
     if (!s.plan.f16 && !(ews && !atoi(ews))) cands.insert(cands.end(), {8, 9, 10, 11});
+    // the LDS-free streaming kernel (tiles 12-16) where the geometry allows it (launch_conv falls
+    // back to tile 0 elsewhere, and such candidates are skipped below)
+    if (!s.plan.f16 && s.kind == S_CONV && !s.pool)
+      for (int c = CONV_TILE_STREAM; c < CONV_TILE_STREAM + 5; ++c) cands.push_back(c);
     for (size_t ci = 0; ci < cands.size() && !st; ++ci) {
       const int c = cands[ci];
       s.plan.cfg = c;
+      last_conv_tile = -1;
       st = launch_step(m, s, n);  // warm-up
       if (st) break;
+      if (last_conv_tile != c) continue;  // fell back to another tile: not a distinct candidate
       if (hipEventRecord(e0, ctx->stream) != hipSuccess) { st = set_error(ctx, ORE_ERR_HIP, "event record"); break; }
       for (int r = 0; r < reps && !st; ++r) st = launch_step(m, s, n);
       if (st) break;

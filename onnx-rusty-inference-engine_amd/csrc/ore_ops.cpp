@@ -170,6 +170,12 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
   if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;  // tuning knob
   p.is1x1 = (kh == 1 && kw == 1 && sh == 1 && sw == 1 && win.pt == 0 && win.pl == 0 && win.Ho == H && win.Wo == W &&
              x_ps == y_ps);
+  {  // mapped bytes before x: the rest of x's 4 KiB page, or the walker's arena lead
+    const char* xc = reinterpret_cast<const char*>(x);
+    int64_t g = int64_t(reinterpret_cast<uintptr_t>(x) & 4095);
+    if (ctx->mapped_lo && xc >= ctx->mapped_lo && xc < ctx->mapped_hi) g = std::max<int64_t>(g, std::min<int64_t>(xc - ctx->mapped_lo, 1 << 20));
+    p.x_guard = int(g);
+  }
   if (x_ps < H * W || y_ps < win.Ho * win.Wo) return set_error(ctx, ORE_ERR_INVALID, "plane stride below plane size");
   if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(int64_t(pln.krows) * pln.Mp) ||
       !fits_i32(p.Ntot + 256) || (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))

@@ -116,6 +116,58 @@ def test_conv2d_direct_bit_identical(gpu_ctx, case, tile, monkeypatch):
     assert np.abs(outs[1] - ref).max() <= 1e-4 * (np.abs(ref).max() + 1.0)
 
 
+STREAM_CASES = [
+    # N, C, H, W, M, k, pad, bias: 16-B aligned output planes (Ho*Wo % 4 == 0), C*k*k % 16 == 0
+    (3, 96, 12, 12, 16, 1, 0, True),     # squeeze
+    (2, 16, 8, 8, 64, 1, 0, True),       # expand1x1, K = 16 (the ring's prologue only)
+    (2, 64, 4, 6, 200, 1, 0, False),     # M % 64 != 0: ragged channel tile
+    (5, 32, 10, 10, 40, 1, 0, True),     # 500 columns: ragged pixel tile
+    (1, 512, 6, 6, 1000, 1, 0, True),    # conv10-like
+    (2, 48, 7, 4, 48, 1, 0, True),       # fewer columns than one wave tile
+    (2, 16, 13, 13, 24, 1, 0, True),     # 169-pixel planes: not eligible, falls back to tile 0
+    (2, 16, 12, 12, 64, 3, 1, True),     # expand3x3 (STAPS): zero-padded taps, row wraps
+    (3, 32, 10, 10, 128, 3, 1, False),   # 300 columns over 3 images
+    (1, 48, 7, 8, 192, 3, 1, True),      # W = 8: 4-pixel groups straddle rows
+    (2, 64, 6, 6, 256, 3, 1, True),
+    (2, 16, 9, 12, 40, 3, 0, True),      # VALID 3x3: Wo != W -> falls back
+]
+
+
+@pytest.mark.parametrize("tile", ["12", "13", "14", "15", "16"])
+@pytest.mark.parametrize("case", STREAM_CASES)
+def test_conv_stream_bit_identical(gpu_ctx, case, tile, monkeypatch):
+    """The LDS-free streaming kernel (ore_conv_stream.hip, 16x16x4 MFMA, tiles 12-16: 1x1 and 3x3
+    'same' convs) runs the same k-ordered fmaf chain per output as the LDS-staged kernel:
+    bit-identical to tile 0, and within the conv tolerance of the oracle."""
+    import ore
+    N, C, H, W, M, k, pad, with_bias = case
+    rng = np.random.default_rng(zlib.crc32(repr(case).encode()) ^ 0x1111)
+    x = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    w = rng.standard_normal((M, C, k, k)).astype(np.float32)
+    b = rng.standard_normal((M,)).astype(np.float32) if with_bias else None
+    pads = [pad] * 4
+    # x 256 B into a 4 KiB page: the 3x3 stream kernel reads up to (W + 1) floats before x (masked),
+    # which the per-op path allows only inside x's own page
+    import torch
+    buf = torch.zeros(x.size + 1024 + 64, dtype=torch.float32, device="cuda")
+    xd = buf[1024 + 64:].view(x.shape)
+    xd.copy_(_t(x))
+    outs = []
+    for t in ("0", tile):
+        monkeypatch.setenv("ORE_CONV_CFG", t)
+        for relu in (False, True):
+            outs.append(_np(ore.convolution(gpu_ctx, xd, _t(w), _t(b) if b is not None else None,
+                                            auto_pad="NOTSET", pads=pads, strides=(1, 1), fuse_relu=relu)))
+    np.testing.assert_array_equal(outs[2], outs[0])
+    np.testing.assert_array_equal(outs[3], outs[1])
+    ref = oracle.conv2d(x, w, b, auto_pad="NOTSET", pads=pads, strides=(1, 1))
+    Ho, Wo = ref.shape[2], ref.shape[3]
+    bound = _conv_bound(x, w, pads, (1, 1), Ho, Wo) + (np.abs(b)[None, :, None, None] if b is not None else 0)
+    err = np.abs(outs[2].astype(np.float64) - ref.astype(np.float64))
+    assert np.all(err <= 2e-6 * bound + 1e-30), f"max err {err.max()}"
+    np.testing.assert_array_equal(outs[3], np.maximum(outs[2], 0))
+
+
 def test_conv_integer_exact(gpu_ctx):
     """Small-integer data: every partial sum is exact in f32, so GPU == oracle bit for bit."""
     import ore
