@@ -1048,7 +1048,7 @@ void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
     return;
   }
   if (pln.cfg >= CONV_TILE_STREAM) {
-    if (conv_stream_eligible(p)) {
+    if (conv_stream_eligible(p, pln.cfg)) {
       launch_conv_stream(p, pln.cfg, s);
       return;
     }

@@ -34,7 +34,12 @@ enum { S1X1 = 0, STAPS = 1 };
 
 template <int MF>
 __device__ __forceinline__ void cs_load_a(__amdgpu_buffer_rsrc_t r, int voff, int soff, float (&a)[MF]) {
-  if constexpr (MF == 4) {
+  if constexpr (MF == 8) {
+    const cs_floatx4 v = __builtin_bit_cast(cs_floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+    const cs_floatx4 w = __builtin_bit_cast(cs_floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16, soff, 0));
+    a[0] = v[0]; a[1] = v[1]; a[2] = v[2]; a[3] = v[3];
+    a[4] = w[0]; a[5] = w[1]; a[6] = w[2]; a[7] = w[3];
+  } else if constexpr (MF == 4) {
     const cs_floatx4 v = __builtin_bit_cast(cs_floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
     a[0] = v[0]; a[1] = v[1]; a[2] = v[2]; a[3] = v[3];
   } else if constexpr (MF == 3) {
@@ -218,7 +223,15 @@ static int stream_mode(const ConvParams& p) {
   return ((reinterpret_cast<uintptr_t>(p.x) & 3) == 0 && p.x_guard >= stream_lead(p)) ? 2 : 0;
 }
 
-bool conv_stream_eligible(const ConvParams& p) { return stream_mode(p) != 0; }
+static int stream_depth(int tile) {
+  const int t = tile - CONV_TILE_STREAM;
+  return t == 6 ? 8 : t == 8 ? 2 : 4;
+}
+
+// the geometry allows the streaming kernel and the tile's ring depth divides the K steps
+bool conv_stream_eligible(const ConvParams& p, int tile) {
+  return stream_mode(p) != 0 && (p.K / 4) % stream_depth(tile) == 0;
+}
 
 template <int MF, int NB, int D>
 static void launch_cs(const ConvParams& p0, hipStream_t s) {
@@ -234,14 +247,18 @@ static void launch_cs(const ConvParams& p0, hipStream_t s) {
     hipLaunchKernelGGL((conv_stream_kernel<MF, NB, D, STAPS>), grid, block, 0, s, p);
 }
 
-// tiles CONV_TILE_STREAM + 0..4 (ConvPlan::cfg); the caller checks conv_stream_eligible
+// tiles CONV_TILE_STREAM + 0..8 (ConvPlan::cfg); the caller checks conv_stream_eligible
 void launch_conv_stream(const ConvParams& p, int tile, hipStream_t s) {
   switch (tile - CONV_TILE_STREAM) {
     case 0: launch_cs<4, 2, 4>(p, s); break;   // 64 x 128
     case 1: launch_cs<2, 4, 4>(p, s); break;   // 32 x 256
     case 2: launch_cs<1, 4, 4>(p, s); break;   // 16 x 256
     case 3: launch_cs<3, 2, 4>(p, s); break;   // 48 x 128
-    default: launch_cs<4, 1, 4>(p, s); break;  // 64 x 64
+    case 4: launch_cs<4, 1, 4>(p, s); break;   // 64 x 64
+    case 5: launch_cs<8, 1, 4>(p, s); break;   // 128 x 64
+    case 6: launch_cs<4, 1, 8>(p, s); break;   // 64 x 64, 8 k-steps in flight
+    case 7: launch_cs<2, 2, 4>(p, s); break;   // 32 x 128
+    default: launch_cs<8, 1, 2>(p, s); break;  // 128 x 64, 2 k-steps in flight
   }
 }
 

@@ -131,14 +131,14 @@ constexpr int CONV_EPOOL_BN = 256;  // N tile of the pooled-epilogue kernel
 constexpr int EPOOL_TILE_PR = 6, EPOOL_TILE_PC = 9;  // pooled outputs per block (13 x 19 conv patch)
 // LDS-free, barrier-free variant (ore_conv_direct.hip): tiles 4-7 (needs p.x_bytes > 0)
 void launch_conv_direct(const ConvParams& p, int tile, hipStream_t s);
-constexpr int CONV_TILES_F32 = 17;  // 0-3 conv_gemm_kernel, 4-7 conv_direct_kernel (ORE_CONV_CFG only),
+constexpr int CONV_TILES_F32 = 21;  // 0-3 conv_gemm_kernel, 4-7 conv_direct_kernel (ORE_CONV_CFG only),
                                     // 8-11 conv_gemm_kernel warp-specialised (512 threads),
-                                    // 12-16 conv_stream_kernel (stride-1 geometries only)
+                                    // 12-20 conv_stream_kernel (stride-1 geometries only)
 // LDS-free streaming kernel (ore_conv_stream.hip): 1x1 convs and stride-1 convs with Wo == W (every
-// expand3x3); tiles CONV_TILE_STREAM + 0..4 = 64x128, 32x256, 16x256, 48x128, 64x64 (channels x
-// pixels per wave); other geometries fall back to tile 0
+// expand3x3); tiles CONV_TILE_STREAM + 0..8 = 64x128, 32x256, 16x256, 48x128, 64x64, 128x64, 64x64 D8,
+// 32x128, 128x64 D2 (channels x pixels per wave); other geometries fall back to tile 0
 constexpr int CONV_TILE_STREAM = 12;
-bool conv_stream_eligible(const ConvParams& p);
+bool conv_stream_eligible(const ConvParams& p, int tile);
 void launch_conv_stream(const ConvParams& p, int tile, hipStream_t s);
 // the tile launch_conv actually ran last on this thread (a 1x1 tile on an ineligible geometry runs
 // tile 0); ore_model_autotune skips candidates that fell back
@@ -150,7 +150,8 @@ void launch_relu(const float* x, float* y, long long n, hipStream_t s);
 void launch_relu_f16(const void* x, void* y, long long n, hipStream_t s);
 void launch_add_bcast(const AddParams& p, hipStream_t s);
 void launch_softmax(const float* x, float* y, long long rows, int D, hipStream_t s);
-void launch_gap(const void* x, int es, float* y, long long rows, int HW, hipStream_t s);  // es: 4 f32, 2 f16 input
+// rows of HW elements at a row stride of ps (>= HW); es: 4 f32, 2 f16 input
+void launch_gap(const void* x, int es, float* y, long long rows, int HW, int ps, hipStream_t s);
 void launch_concat(const void* a, const void* b, void* y, int es, long long outer, long long ia, long long ib,
                    hipStream_t s);
 

@@ -225,8 +225,63 @@ __global__ __launch_bounds__(256) void maxpool_planes_kernel(PoolParams p, int p
   }
 }
 
+// Chunk-staged MaxPool: one block per PB consecutive (n, c) planes of a tensor whose planes are
+// evenly spaced (x_nstride == C * x_ps, y_nstride == C * y_ps: one contiguous run of PB * x_ps
+// elements, padded planes included).  The run goes to LDS by 16-B loads issued back to back (one
+// plane of 27 x 27 is only 182 float4s: staging plane by plane leaves most lanes idle and one load
+// round trip per plane), then all PB * Ho * Wo windows are evaluated from LDS.
+template <typename T, int KH, int KW>
+__global__ __launch_bounds__(256) void maxpool_chunk_kernel(PoolParams p, int pb, long long planes) {
+  extern __shared__ __attribute__((aligned(16))) char tile_raw[];
+  T* tile = reinterpret_cast<T*>(tile_raw);  // [pb][x_ps]
+  const long long q0 = (long long)blockIdx.x * pb;
+  const int nq = (int)min((long long)pb, planes - q0);
+  const int tid = threadIdx.x;
+  const T* __restrict__ src = reinterpret_cast<const T*>(p.x) + q0 * p.x_ps;
+  const int cnt = (nq - 1) * p.x_ps + p.H * p.W;  // elements to stage (the last plane's padding skipped)
+  constexpr int EV = 16 / (int)sizeof(T);
+  const int nv = cnt / EV;  // host: x 16-B aligned, x_ps % EV == 0
+  const uint4* __restrict__ xv = reinterpret_cast<const uint4*>(src);
+  uint4* tv = reinterpret_cast<uint4*>(tile);
+  int i = tid;
+  for (; i + 7 * 256 < nv; i += 8 * 256) {
+    uint4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = xv[i + u * 256];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) tv[i + u * 256] = v[u];
+  }
+  for (; i < nv; i += 256) tv[i] = xv[i];
+  for (int e = nv * EV + tid; e < cnt; e += 256) tile[e] = src[e];
+  __syncthreads();
+  const int P = p.Ho * p.Wo;
+  const int total = nq * P;
+  const int kh = KH ? KH : p.kh, kw = KW ? KW : p.kw;
+  T* __restrict__ y = reinterpret_cast<T*>(p.y) + q0 * p.y_ps;
+  for (int o = tid; o < total; o += 256) {
+    const int q = o / P, r = o - q * P;
+    const int oh = r / p.Wo, ow = r - oh * p.Wo;
+    const int ih0 = oh * p.sh - p.pt, iw0 = ow * p.sw - p.pl;
+    const T* tq = tile + q * p.x_ps;
+    float m = -FLT_MAX;
+#pragma unroll
+    for (int rr = 0; rr < kh; ++rr) {
+      const int ih = ih0 + rr;
+      const bool rok = (unsigned)ih < (unsigned)p.H;
+#pragma unroll
+      for (int s2 = 0; s2 < kw; ++s2) {
+        const int iw = iw0 + s2;
+        const float v = (rok && (unsigned)iw < (unsigned)p.W) ? (float)tq[ih * p.W + iw] : 0.0f;
+        m = fmaxf(m, v);
+      }
+    }
+    y[q * p.y_ps + r] = (T)m;
+  }
+}
+
 // tuning knobs, read per launch so tests can switch them: ORE_POOL_VARIANT 0 auto, 1 band
-// LDS-staged, 2 direct, 3 column strip, 4 plane-staged; ORE_POOL_LDS_KB (planes per block of
+// LDS-staged, 2 direct, 3 column strip, 4 plane-staged, 5 chunk-staged (ORE_POOL_CHUNK_KB of LDS
+// per block); ORE_POOL_LDS_KB (planes per block of
 // variant 4 = budget / plane bytes); ORE_POOL_RB (output rows per thread of variant 3)
 static int env_knob(const char* name, int dflt) {
   const char* e = getenv(name);
@@ -246,13 +301,37 @@ static void launch_maxpool_t(const PoolParams& p, hipStream_t s) {
     // >= 2048 elements up to 48 KB (f32 pool1 485 -> 367 us, pool3 318 -> 227 us; f16 pool1 617 ->
     // 204, pool3 380 -> 186); 27x27 planes: the direct kernel for f32 (150 us vs strip 171), the
     // column strip for f16 (120 us vs direct 169)
+    // Evenly spaced planes (every SqueezeNet pool in the fused graph): the chunk-staged kernel with
+    // 12 KB of LDS per block (pool3 205 -> 196 us, pool5 162 -> 99 us; 24 / 48 KB measured slower)
     const bool s332 = p.kh == 3 && p.kw == 3 && p.sh == 2;
-    if ((long long)p.H * p.W >= 2048 && plane_bytes <= 48 * 1024)
+    constexpr int EV = 16 / (int)sizeof(T);
+    if (p.x_nstride == (long long)p.C * p.x_ps && p.y_nstride == (long long)p.C * p.y_ps && p.x_ps % EV == 0 &&
+        (reinterpret_cast<uintptr_t>(p.x) & 15) == 0 && (long long)p.x_ps * (long long)sizeof(T) <= 12 * 1024)
+      v = 5;
+    else if ((long long)p.H * p.W >= 2048 && plane_bytes <= 48 * 1024)
       v = 4;
     else if (s332 && (plane_bytes > 48 * 1024 || sizeof(T) == 2))
       v = 3;
     else
       v = 2;
+  }
+  if (v == 5) {  // chunk-staged (falls through when the planes are not evenly spaced)
+    constexpr int EV = 16 / (int)sizeof(T);
+    const long long lds_budget = (long long)env_knob("ORE_POOL_CHUNK_KB", 12) * 1024;
+    const long long pbytes = (long long)p.x_ps * (long long)sizeof(T);
+    int pb = (int)(lds_budget / pbytes);
+    if (pb > 64) pb = 64;
+    if (p.x_nstride == (long long)p.C * p.x_ps && p.y_nstride == (long long)p.C * p.y_ps && p.x_ps % EV == 0 &&
+        (reinterpret_cast<uintptr_t>(p.x) & 15) == 0 && pb >= 1) {
+      const long long nblk = (planes + pb - 1) / pb;
+      const size_t lds = (size_t)((pb - 1) * pbytes + plane_bytes);
+      if (p.kh == 3 && p.kw == 3)
+        hipLaunchKernelGGL((maxpool_chunk_kernel<T, 3, 3>), dim3((unsigned)nblk), dim3(256), lds, s, p, pb, planes);
+      else
+        hipLaunchKernelGGL((maxpool_chunk_kernel<T, 0, 0>), dim3((unsigned)nblk), dim3(256), lds, s, p, pb, planes);
+      return;
+    }
+    v = 2;
   }
   if (v == 1 && sizeof(T) == 4 && POOL_LDS_FLOATS / p.W >= p.kh) {
     const int rows_fit = POOL_LDS_FLOATS / p.W;
@@ -431,49 +510,74 @@ void launch_softmax(const float* x, float* y, long long rows, int D, hipStream_t
 // ------------------------------------------------------------------------------------------
 template <typename T>  // input element type (f32 sums either way)
 __global__ __launch_bounds__(256) void gap_kernel(const T* __restrict__ x, float* __restrict__ y,
-                                                  long long rows, int HW) {
-  extern __shared__ float tile[];  // 64 * HW floats
+                                                  long long rows, int HW, int ps) {
+  extern __shared__ float tile[];  // 64 * ps floats (rows of ps elements, the first HW summed)
   const long long r0 = (long long)blockIdx.x * 64;
   const long long nr = rows - r0 < 64 ? rows - r0 : 64;
-  const long long base = r0 * HW;
-  const long long cnt = nr * HW;
+  const long long base = r0 * ps;
+  const long long cnt = (nr - 1) * ps + HW;
   for (long long i = threadIdx.x; i < cnt; i += 256) tile[i] = (float)x[base + i];
   __syncthreads();
   if (threadIdx.x < nr) {
-    const float* tr = tile + (long long)threadIdx.x * HW;
+    const float* tr = tile + (long long)threadIdx.x * ps;
     float s = 0.0f;
     for (int i = 0; i < HW; ++i) s = s + tr[i];
     y[r0 + threadIdx.x] = s / (float)HW;
   }
 }
 
+// f32 rows with 16-B aligned starts (ps % 4 == 0): one row per lane, read by float4 in order, summed
+// sequentially (the same order as gap_kernel); no LDS, 256 rows per block.  Opt-in (ORE_GAP_VEC=1):
+// measured 152 us vs the LDS-staged kernel's 60 us on SqueezeNet's pool10 at B = 256 (64 lanes
+// touching 64 different lines per load)
+__global__ __launch_bounds__(256) void gap_vec_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                      long long rows, int HW, int ps) {
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= rows) return;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const float* tr = x + r * ps;
+  float s = 0.0f;
+  int i = 0;
+  for (; i + 4 <= HW; i += 4) {
+    const f4 v = *reinterpret_cast<const f4*>(tr + i);
+    s = s + v[0];
+    s = s + v[1];
+    s = s + v[2];
+    s = s + v[3];
+  }
+  for (; i < HW; ++i) s = s + tr[i];
+  y[r] = s / (float)HW;
+}
+
 template <typename T>
 __global__ __launch_bounds__(64) void gap_big_kernel(const T* __restrict__ x, float* __restrict__ y,
-                                                     long long rows, int HW) {
+                                                     long long rows, int HW, int ps) {
   const long long r = (long long)blockIdx.x * 64 + threadIdx.x;
   if (r >= rows) return;
-  const T* tr = x + r * HW;
+  const T* tr = x + r * ps;
   float s = 0.0f;
   for (int i = 0; i < HW; ++i) s = s + (float)tr[i];
   y[r] = s / (float)HW;
 }
 
 template <typename T>
-static void launch_gap_t(const T* x, float* y, long long rows, int HW, hipStream_t s) {
+static void launch_gap_t(const T* x, float* y, long long rows, int HW, int ps, hipStream_t s) {
   if (rows <= 0) return;
-  const unsigned blocks = (unsigned)((rows + 63) / 64);
-  const size_t lds = (size_t)64 * HW * sizeof(float);
-  if (lds <= 64 * 1024)
-    hipLaunchKernelGGL(gap_kernel<T>, dim3(blocks), dim3(256), lds, s, x, y, rows, HW);
+  const size_t lds = (size_t)64 * ps * sizeof(float);
+  if (sizeof(T) == 4 && ps % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && env_knob("ORE_GAP_VEC", 0))
+    hipLaunchKernelGGL(gap_vec_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const float*>(x), y, rows, HW, ps);
+  else if (lds <= 64 * 1024)
+    hipLaunchKernelGGL(gap_kernel<T>, dim3((unsigned)((rows + 63) / 64)), dim3(256), lds, s, x, y, rows, HW, ps);
   else
-    hipLaunchKernelGGL(gap_big_kernel<T>, dim3(blocks), dim3(64), 0, s, x, y, rows, HW);
+    hipLaunchKernelGGL(gap_big_kernel<T>, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, x, y, rows, HW, ps);
 }
 
-void launch_gap(const void* x, int es, float* y, long long rows, int HW, hipStream_t s) {
+void launch_gap(const void* x, int es, float* y, long long rows, int HW, int ps, hipStream_t s) {
   if (es == 2)
-    launch_gap_t(static_cast<const _Float16*>(x), y, rows, HW, s);
+    launch_gap_t(static_cast<const _Float16*>(x), y, rows, HW, ps, s);
   else
-    launch_gap_t(static_cast<const float*>(x), y, rows, HW, s);
+    launch_gap_t(static_cast<const float*>(x), y, rows, HW, ps, s);
 }
 
 // ------------------------------------------------------------------------------------------

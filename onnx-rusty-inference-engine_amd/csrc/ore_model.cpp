@@ -604,10 +604,17 @@ ore_status plan(ore_model* m) {
     std::vector<char> dense(m->values.size(), 0);
     for (const Step& st : m->steps) {
       if (st.kind == S_NOP) continue;
-      const bool ok = st.kind == S_CONV || st.kind == S_MAXPOOL;
+      // GlobalAveragePool reads f32 planes at any stride (launch_step)
+      const bool ok = st.kind == S_CONV || st.kind == S_MAXPOOL || (st.kind == S_GAP && !m->values[st.in0].nhwc);
       for (int id : {st.in0, st.in2, st.out})
         if (id >= 0 && !m->values[id].is_const && !ok) dense[root(id)] = 1;
       if (st.in1 >= 0 && !m->values[st.in1].is_const) dense[root(st.in1)] = 1;
+    }
+    // a contiguous view (Dropout / Reshape alias) keeps its root's planes only as a 4-D
+    // intermediate; as a graph output or a reshaped 2-D value it needs the dense layout
+    for (size_t id = 0; id < m->values.size(); ++id) {
+      const Value& v = m->values[id];
+      if (v.alias_of >= 0 && !v.slice && (v.is_output || v.ndim != 4)) dense[root(int(id))] = 1;
     }
     for (size_t id = 0; id < m->values.size(); ++id) {
       Value& v = m->values[id];
@@ -617,7 +624,10 @@ ore_status plan(ore_model* m) {
         continue;
       }
       const int64_t P = v.dims[2] * v.dims[3];
-      const int64_t Pp = (P + 31) / 32 * 32;
+      // 128-B aligned planes when that costs <= 5 %, else 16-B aligned ones (13 x 13 -> 172: the
+      // streaming conv's 16-B operand loads and stores need 4-float planes)
+      int64_t Pp = (P + 31) / 32 * 32;
+      if (Pp - P > P / 20) Pp = (P + 3) / 4 * 4;
       const bool pad = (m->fusion & ORE_FUSE_CONCAT) && !dense[id] && !v.is_input && !v.is_output && Pp - P <= P / 20;
       v.ps = pad ? Pp : P;
     }
@@ -626,7 +636,8 @@ ore_status plan(ore_model* m) {
         const Value& r = m->values[root(int(&v - &m->values[0]))];
         v.ps = r.ps;
         if (v.nhwc != r.nhwc) return err(m, ORE_ERR_INVALID, "internal: view of a different layout (" + v.name + ")");
-        if (!v.slice && r.ps != (r.nhwc ? r.dims[1] : r.dims[2] * r.dims[3]))
+        if (!v.slice && r.ps != (r.nhwc ? r.dims[1] : r.dims[2] * r.dims[3]) &&
+            (v.is_output || v.dims[2] * v.dims[3] != r.dims[2] * r.dims[3]))
           return err(m, ORE_ERR_INVALID, "internal: dense alias of a padded value (" + v.name + ")");
       }
   }
@@ -847,6 +858,16 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
                          y.ps, x.es);
     }
     default: break;
+  }
+  if (s.kind == S_GAP && m->values[s.in0].es == 4) {  // f32 NCHW rows, possibly padded planes
+    const Value& X = m->values[s.in0];
+    const Ref x = ref_of(m, s.in0);
+    const int64_t HW = X.dims[2] * X.dims[3], ps = x.ps ? x.ps : HW;
+    if (x.nstride != X.dims[1] * ps || y.nstride != X.dims[1])
+      return err(m, ORE_ERR_INVALID, "internal: GlobalAveragePool on a strided view");
+    launch_gap(x.p, 4, y.p, n * X.dims[1], int(HW), int(ps), ctx->stream);
+    ORE_HIP_CHECK(ctx, hipGetLastError());
+    return ORE_OK;
   }
   if (m->values[s.in0].es == 2) return launch_step_f16(m, s, n);
   // contiguous ops through the public entry points
@@ -1198,10 +1219,10 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
     std::vector<int> cands = {0, 1, 2, 3};
     const char* ews = getenv("ORE_AUTOTUNE_WS");
     if (!s.plan.f16 && !(ews && !atoi(ews))) cands.insert(cands.end(), {8, 9, 10, 11});
-    // the LDS-free streaming kernel (tiles 12-16) where the geometry allows it (launch_conv falls
+    // the LDS-free streaming kernel (tiles 12-20) where the geometry allows it (launch_conv falls
     // back to tile 0 elsewhere, and such candidates are skipped below)
     if (!s.plan.f16 && s.kind == S_CONV && !s.pool)
-      for (int c = CONV_TILE_STREAM; c < CONV_TILE_STREAM + 5; ++c) cands.push_back(c);
+      for (int c = CONV_TILE_STREAM; c < CONV_TILES_F32; ++c) cands.push_back(c);
     for (size_t ci = 0; ci < cands.size() && !st; ++ci) {
       const int c = cands[ci];
       s.plan.cfg = c;

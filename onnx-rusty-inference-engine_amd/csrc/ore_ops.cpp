@@ -604,7 +604,7 @@ ore_status ore_gap_f32(ore_ctx* ctx, const ore_tensor* x, ore_tensor* y) {
     return set_error(ctx, ORE_ERR_INVALID, "GlobalAveragePool expects contiguous [N,C,H,W] -> [N,C,1,1]");
   const int64_t HW = x->dims[2] * x->dims[3];
   if (HW <= 0 || HW >= (int64_t(1) << 31)) return set_error(ctx, ORE_ERR_INVALID, "GAP spatial size");
-  launch_gap(x->data, 4, y->data, x->dims[0] * x->dims[1], int(HW), ctx->stream);
+  launch_gap(x->data, 4, y->data, x->dims[0] * x->dims[1], int(HW), int(HW), ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());
   return ORE_OK;
 }

@@ -229,10 +229,10 @@ POOL_CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4"])
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "5"])
 @pytest.mark.parametrize("case", POOL_CASES)
 def test_maxpool(gpu_ctx, case, variant, monkeypatch):
-    """Every MaxPool kernel (ORE_POOL_VARIANT: auto, band-LDS, direct, column strip, plane-LDS;
+    """Every MaxPool kernel (ORE_POOL_VARIANT: auto, band-LDS, direct, column strip, plane-LDS, chunk-LDS;
     a variant that does not apply to a shape falls through to the direct kernel)."""
     import ore
     monkeypatch.setenv("ORE_POOL_VARIANT", variant)
