@@ -95,9 +95,11 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(ConvParams p) {
       for (int q = 0; q < 4; ++q) {
         const int oh = (pix + q) / p.W, ow = (pix + q) - oh * p.W;  // oh >= Ho: a pad column
         unsigned cm = 0, m = 0;
-        for (int s = 0; s < p.kw; ++s) cm |= ((unsigned)(ow - p.pl + s) < (unsigned)p.W ? 1u : 0u) << s;
-        for (int r = 0; r < p.kh; ++r)
-          if (oh < p.Ho && (unsigned)(oh - p.pt + r) < (unsigned)p.H) m |= cm << (r * p.kw);
+#pragma unroll
+        for (int s = 0; s < 3; ++s) cm |= ((unsigned)(ow - p.pl + s) < (unsigned)p.W ? 1u : 0u) << s;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+          if (oh < p.Ho && (unsigned)(oh - p.pt + r) < (unsigned)p.H) m |= cm << (r * 3);
         tmask[g][q] = m;
       }
     }
@@ -138,8 +140,9 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(ConvParams p) {
       _Pragma("unroll") for (int g = 0; g < NB; ++g) rb[SLOT][g] = __builtin_bit_cast(          \
           cs_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, xoff[g], s_ * xstep, 0));         \
     } else {                                                                                      \
-      const int r_ = (tt * 11) >> 5; /* tt / 3 for tt < 9 */                                      \
-      const int to_ = cx + tap0 + 4 * (r_ * p.W + (tt - 3 * r_));                                 \
+      /* tt / 3 for tt < 9, 24-bit multiplies (v_mul_u32_u24, full rate; v_mul_lo_u32 is 1/4) */  \
+      const int r_ = (int)(__umul24((unsigned)tt, 11u) >> 5);                                     \
+      const int to_ = cx + tap0 + 4 * ((int)__umul24((unsigned)r_, (unsigned)(p.W - 3)) + tt);    \
       _Pragma("unroll") for (int g = 0; g < NB; ++g) rb[SLOT][g] = __builtin_bit_cast(          \
           cs_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, xoff[g] + to_, 0, 0));            \
       rt[SLOT] = tt;                                                                              \
@@ -219,7 +222,7 @@ static int stream_mode(const ConvParams& p) {
     const uintptr_t xa = reinterpret_cast<uintptr_t>(p.x);
     return ((xa & 15) == 0 && p.x_ps % 4 == 0 && p.x_nstride % 4 == 0) ? 1 : 0;
   }
-  if (p.kh != 3 || p.kw != 3 || p.sh != 1 || p.sw != 1 || p.Wo != p.W || p.pt > 1 || p.pl > 1) return 0;
+  if (p.kh != 3 || p.kw != 3 || p.sh != 1 || p.sw != 1 || p.Wo != p.W || p.W < 3 || p.pt > 1 || p.pl > 1) return 0;
   return ((reinterpret_cast<uintptr_t>(p.x) & 3) == 0 && p.x_guard >= stream_lead(p)) ? 2 : 0;
 }
 
