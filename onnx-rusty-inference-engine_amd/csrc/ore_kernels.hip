@@ -465,6 +465,7 @@ void launch_add_bcast(const AddParams& p, hipStream_t s) {
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void softmax_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                       int D) {
+  extern __shared__ float ebuf[];  // D exponentials (the 8 summing lanes read them from LDS)
   __shared__ float red[4];
   __shared__ float part[8];
   const long long row = blockIdx.x;
@@ -480,8 +481,43 @@ __global__ __launch_bounds__(256) void softmax_kernel(const float* __restrict__ 
   __syncthreads();
   m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 
+  for (int i = tid; i < D; i += 256) ebuf[i] = expf(xr[i] - m);
+  __syncthreads();
+  const int nfull = D / 8;
+  if (tid < 8) {
+    float s = 0.0f;
+#pragma unroll 8
+    for (int c = 0; c < nfull; ++c) s = s + ebuf[c * 8 + tid];
+    part[tid] = s;
+  }
+  __syncthreads();
+  float sum = 0.0f;
+  sum = sum + (part[0] + part[4]);
+  sum = sum + (part[1] + part[5]);
+  sum = sum + (part[2] + part[6]);
+  sum = sum + (part[3] + part[7]);
+  for (int i = nfull * 8; i < D; ++i) sum = sum + ebuf[i];
+  for (int i = tid; i < D; i += 256) yr[i] = ebuf[i] / sum;
+}
+
+// rows whose exponentials do not fit the LDS budget: the same order, e staged in y
+__global__ __launch_bounds__(256) void softmax_big_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                          int D) {
+  __shared__ float red[4];
+  __shared__ float part[8];
+  const long long row = blockIdx.x;
+  const float* xr = x + row * D;
+  float* yr = y + row * D;
+  const int tid = threadIdx.x;
+  float m = -INFINITY;
+  for (int i = tid; i < D; i += 256) m = fmaxf(xr[i], m);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   for (int i = tid; i < D; i += 256) yr[i] = expf(xr[i] - m);
-  __syncthreads();  // block-scope visibility of yr for the 8 summing lanes (same CU, L1 write-through of own stores)
+  __syncthreads();  // block-scope visibility of yr for the 8 summing lanes
   const int nfull = D / 8;
   if (tid < 8) {
     float s = 0.0f;
@@ -501,7 +537,10 @@ __global__ __launch_bounds__(256) void softmax_kernel(const float* __restrict__ 
 
 void launch_softmax(const float* x, float* y, long long rows, int D, hipStream_t s) {
   if (rows <= 0) return;
-  hipLaunchKernelGGL(softmax_kernel, dim3((unsigned)rows), dim3(256), 0, s, x, y, D);
+  if ((size_t)D * 4 <= 48 * 1024)
+    hipLaunchKernelGGL(softmax_kernel, dim3((unsigned)rows), dim3(256), (size_t)D * 4, s, x, y, D);
+  else
+    hipLaunchKernelGGL(softmax_big_kernel, dim3((unsigned)rows), dim3(256), 0, s, x, y, D);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -511,15 +550,39 @@ void launch_softmax(const float* x, float* y, long long rows, int D, hipStream_t
 template <typename T>  // input element type (f32 sums either way)
 __global__ __launch_bounds__(256) void gap_kernel(const T* __restrict__ x, float* __restrict__ y,
                                                   long long rows, int HW, int ps) {
-  extern __shared__ float tile[];  // 64 * ps floats (rows of ps elements, the first HW summed)
+  // 64 rows of HW elements at an odd LDS row stride (HW | 1: the 64 summing lanes read 64 distinct
+  // banks; a 172-float stride would put 4 lanes on each bank), each wave copying 16 rows with
+  // coalesced loads along the row
+  extern __shared__ float tile[];  // 64 * (HW | 1) floats
+  const int ls = HW | 1;
   const long long r0 = (long long)blockIdx.x * 64;
-  const long long nr = rows - r0 < 64 ? rows - r0 : 64;
-  const long long base = r0 * ps;
-  const long long cnt = (nr - 1) * ps + HW;
-  for (long long i = threadIdx.x; i < cnt; i += 256) tile[i] = (float)x[base + i];
+  const int nr = (int)(rows - r0 < 64 ? rows - r0 : 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (HW <= 256) {  // every load of the wave's 16 rows in flight before the first LDS store
+    float v[16][4];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int r = wave + 4 * j;
+      const T* __restrict__ src = x + (r0 + (r < nr ? r : 0)) * ps;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[j][u] = (lane + 64 * u < HW) ? (float)src[lane + 64 * u] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int r = wave + 4 * j;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (r < nr && lane + 64 * u < HW) tile[r * ls + lane + 64 * u] = v[j][u];
+    }
+  } else {
+    for (int r = wave; r < nr; r += 4) {
+      const T* __restrict__ src = x + (r0 + r) * ps;
+      for (int c = lane; c < HW; c += 64) tile[r * ls + c] = (float)src[c];
+    }
+  }
   __syncthreads();
   if (threadIdx.x < nr) {
-    const float* tr = tile + (long long)threadIdx.x * ps;
+    const float* tr = tile + threadIdx.x * ls;
     float s = 0.0f;
     for (int i = 0; i < HW; ++i) s = s + tr[i];
     y[r0 + threadIdx.x] = s / (float)HW;
@@ -563,7 +626,7 @@ __global__ __launch_bounds__(64) void gap_big_kernel(const T* __restrict__ x, fl
 template <typename T>
 static void launch_gap_t(const T* x, float* y, long long rows, int HW, int ps, hipStream_t s) {
   if (rows <= 0) return;
-  const size_t lds = (size_t)64 * ps * sizeof(float);
+  const size_t lds = (size_t)64 * (HW | 1) * sizeof(float);
   if (sizeof(T) == 4 && ps % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && env_knob("ORE_GAP_VEC", 0))
     hipLaunchKernelGGL(gap_vec_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
                        reinterpret_cast<const float*>(x), y, rows, HW, ps);

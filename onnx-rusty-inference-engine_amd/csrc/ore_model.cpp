@@ -628,7 +628,9 @@ ore_status plan(ore_model* m) {
       // streaming conv's 16-B operand loads and stores need 4-float planes)
       int64_t Pp = (P + 31) / 32 * 32;
       if (Pp - P > P / 20) Pp = (P + 3) / 4 * 4;
-      const bool pad = (m->fusion & ORE_FUSE_CONCAT) && !dense[id] && !v.is_input && !v.is_output && Pp - P <= P / 20;
+      static const bool pad_planes = getenv("ORE_PAD_PLANES") ? atoi(getenv("ORE_PAD_PLANES")) != 0 : true;  // experiment knob
+      const bool pad = pad_planes && (m->fusion & ORE_FUSE_CONCAT) && !dense[id] && !v.is_input && !v.is_output &&
+                       Pp - P <= P / 20;
       v.ps = pad ? Pp : P;
     }
     for (auto& v : m->values)  // views inherit the plane stride of their root
