@@ -4,23 +4,27 @@ average duration, next to bench.py's own HIP-event figure (roofline.per_launch_a
 usage: python tools/prof_summary.py <run_kernel_stats.csv> [bench_json] > profiles/rNN_prof_summary.txt
 
 With run_kernel_trace.csv beside the stats file, the classes are also computed over the timed
-steps only (the last `steps` x 31 dispatches of the run: autotune candidates and warm-up runs
+steps only (the last `steps` x per-step dispatches of the run: autotune candidates and warm-up runs
 excluded), which is what bench.py's per_launch_avg_us measures."""
 import csv
 import json
 import os
 import sys
 
-CLASSES = [("conv (f32 MFMA)", "conv_gemm_kernel"), ("conv (f16 MFMA)", "conv_f16_kernel"),
+CLASSES = [("conv (f32 MFMA)", ("conv_gemm_kernel", "conv_stream_kernel")), ("conv (f16 MFMA)", "conv_f16_kernel"),
            ("conv (window)", "conv_win_kernel"), ("maxpool", "maxpool"), ("gap", "gap_kernel"),
            ("softmax", "softmax_kernel"), ("pack/ktab (load time)", "pack_"), ("ktab", "ktab_kernel")]
+
+
+def hit(key, name):
+    return any(k in name for k in key) if isinstance(key, tuple) else key in name
 
 
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     print(f"{'class':24s} {'launches':>9s} {'total ms':>10s} {'avg us':>9s}")
     for label, key in CLASSES:
-        sel = [r for r in rows if key in r["Name"]]
+        sel = [r for r in rows if hit(key, r["Name"])]
         if not sel:
             continue
         calls = sum(int(r["Calls"]) for r in sel)
@@ -31,10 +35,14 @@ def main():
     if os.path.exists(trace) and bench:
         disp = [r for r in csv.DictReader(open(trace)) if "ore::" in r["Kernel_Name"]]
         disp.sort(key=lambda r: int(r["Dispatch_Id"]))
-        last = disp[-31 * int(bench["steps"]):]
-        print(f"\ntimed steps only (last {len(last)} dispatches = {bench['steps']} steps x 31):")
+        # dispatches per step: the distance between the last two softmax launches (every step ends
+        # with the softmax)
+        sm = [i for i, r in enumerate(disp) if "softmax" in r["Kernel_Name"]]
+        per = sm[-1] - sm[-2] if len(sm) >= 2 else 31
+        last = disp[-per * int(bench["steps"]):]
+        print(f"\ntimed steps only (last {len(last)} dispatches = {bench['steps']} steps x {per}):")
         for label, key in CLASSES:
-            sel = [r for r in last if key in r["Kernel_Name"]]
+            sel = [r for r in last if hit(key, r["Kernel_Name"])]
             if sel:
                 tot = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in sel)
                 print(f"{label:24s} {len(sel):9d} {tot / 1e6:10.3f} {tot / len(sel) / 1e3:9.2f}")
