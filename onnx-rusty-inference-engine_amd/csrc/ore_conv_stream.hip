@@ -236,7 +236,8 @@ static int stream_mode(const ConvParams& p) {
     return ((xa & 15) == 0 && p.x_ps % 4 == 0 && p.x_nstride % 4 == 0) ? 1 : 0;
   }
   if (p.kh != 3 || p.kw != 3 || p.sh != 1 || p.sw != 1 || p.Wo != p.W || p.W < 3 || p.pt > 1 || p.pl > 1) return 0;
-  return ((reinterpret_cast<uintptr_t>(p.x) & 3) == 0 && p.x_guard >= stream_lead(p)) ? 2 : 0;
+  return ((reinterpret_cast<uintptr_t>(p.x) & 3) == 0 && p.x_guard >= stream_lead(p) &&
+          p.x_bytes + stream_lead(p) < (1LL << 31)) ? 2 : 0;
 }
 
 static int stream_depth(int tile) {
@@ -263,7 +264,8 @@ static void launch_cs(const ConvParams& p0, hipStream_t s) {
     hipLaunchKernelGGL((conv_stream_kernel<MF, NB, D, STAPS>), grid, block, 0, s, p);
 }
 
-// tiles CONV_TILE_STREAM + 0..8 (ConvPlan::cfg); the caller checks conv_stream_eligible
+// tiles CONV_TILE_STREAM + 0..8 (ConvPlan::cfg); 16 x 512 tiles (NB = 8) measured no faster
+// on the 54 x 54 squeezes (tools/bench_1x1.py, profiles/r01y_bench_1x1.txt); the caller checks conv_stream_eligible
 void launch_conv_stream(const ConvParams& p, int tile, hipStream_t s) {
   switch (tile - CONV_TILE_STREAM) {
     case 0: launch_cs<4, 2, 4>(p, s); break;   // 64 x 128

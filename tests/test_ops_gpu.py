@@ -123,6 +123,7 @@ STREAM_CASES = [
     (2, 64, 4, 6, 200, 1, 0, False),     # M % 64 != 0: ragged channel tile
     (5, 32, 10, 10, 40, 1, 0, True),     # 500 columns: ragged pixel tile
     (1, 512, 6, 6, 1000, 1, 0, True),    # conv10-like
+    (3, 32, 16, 16, 16, 1, 0, True),     # 768 columns over 3 images
     (2, 48, 7, 4, 48, 1, 0, True),       # fewer columns than one wave tile
     (2, 16, 13, 13, 24, 1, 0, True),     # 169-pixel planes: not eligible, falls back to tile 0
     (2, 16, 12, 12, 64, 3, 1, True),     # expand3x3 (STAPS): zero-padded taps, row wraps
@@ -133,7 +134,7 @@ STREAM_CASES = [
 ]
 
 
-@pytest.mark.parametrize("tile", ["12", "13", "14", "15", "16"])
+@pytest.mark.parametrize("tile", [str(t) for t in range(12, 21)])
 @pytest.mark.parametrize("case", STREAM_CASES)
 def test_conv_stream_bit_identical(gpu_ctx, case, tile, monkeypatch):
     """The LDS-free streaming kernel (ore_conv_stream.hip, 16x16x4 MFMA, tiles 12-16: 1x1 and 3x3

@@ -20,7 +20,7 @@ SHAPES = [("f2.sq", 96, 54, 16), ("f3.sq", 128, 54, 16), ("f4.sq", 128, 54, 32),
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--tiles", default="0,3,12,13,14,15,16")
+    ap.add_argument("--tiles", default="3,12,13,14,15,16,19")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--only", default="")
