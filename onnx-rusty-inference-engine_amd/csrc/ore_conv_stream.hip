@@ -73,17 +73,17 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(ConvParams p) {
 
   // this lane's 4-pixel column group per 64-pixel block g (clamped into range: the last tile's
   // surplus lanes re-read valid columns and are masked at the store)
-  const long long ntot = p.Ntot;
+  const int ntot = (int)p.Ntot;  // < 2^31 (host)
   int xoff[NB], yoff[NB];
   bool cok[NB];
   unsigned tmask[MODE == STAPS ? NB : 1][4];  // STAPS: bit t = tap t of pixel q reads inside the image
 #pragma unroll
   for (int g = 0; g < NB; ++g) {
-    long long col = (long long)ct * (64 * NB) + 64 * g + 4 * lj;
+    int col = ct * (64 * NB) + 64 * g + 4 * lj;
     cok[g] = col < ntot;
     if (!cok[g]) col = ntot - 4;
-    const int img = (int)(col / YPS);
-    const int pix = (int)col - img * YPS;
+    const int img = col / YPS;
+    const int pix = col - img * YPS;
     yoff[g] = img * (int)p.y_nstride + pix;  // elements
     if constexpr (MODE == S1X1) {
       xoff[g] = (img * (int)p.x_nstride + lk * p.x_ps + pix) * 4;  // bytes; + 16 s x_ps per k-step
@@ -91,9 +91,12 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(ConvParams p) {
       // input element of tap (r, s) = pix + (r - pt) W + (s - pl) (stride 1, Wo == W); the tap part
       // is added per k-step
       xoff[g] = (img * (int)p.x_nstride + pix) * 4;
+      const int oh0 = pix / p.W, ow0 = pix - oh0 * p.W;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int oh = (pix + q) / p.W, ow = (pix + q) - oh * p.W;  // oh >= Ho: a pad column
+        // pixel pix + q (W >= 3: at most one row wrap); oh >= Ho: a pad column
+        const bool wrap = ow0 + q >= p.W;
+        const int oh = oh0 + (wrap ? 1 : 0), ow = ow0 + q - (wrap ? p.W : 0);
         unsigned cm = 0, m = 0;
 #pragma unroll
         for (int s = 0; s < 3; ++s) cm |= ((unsigned)(ow - p.pl + s) < (unsigned)p.W ? 1u : 0u) << s;
