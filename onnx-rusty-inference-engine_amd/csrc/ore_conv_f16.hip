@@ -65,7 +65,13 @@ struct BStage<F16_X_NHWC_ELEM, BV> {  // 8 scattered f16 elements per task
   bool ok[8 * BV];
 };
 
-template <int BM, int BN, int WM, int WN, int XMODE>
+// EP (ORE_FUSE_CONV_POOL on an f16 model): the block's BN = 256 columns are a 13 x 19 patch of conv
+// outputs (ConvParams ep_*; as conv_gemm_kernel's pooled epilogue) and only the 6 x 9 tile of
+// 3x3 / stride-2 pooled outputs is stored (NHWC f16).  The conv values are rounded to f16 first, as
+// the separate conv stores them, so the pooled result is the separate pool's bit for bit.
+constexpr int H_EP_PR = EPOOL_TILE_PR, H_EP_PC = EPOOL_TILE_PC, H_EP_RC = 2 * H_EP_PR + 1, H_EP_CC = 2 * H_EP_PC + 1;
+
+template <int BM, int BN, int WM, int WN, int XMODE, int EP = 0>
 __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
   constexpr int BK = 32;                 // k per stage: two 32x32x16 k-steps, four 8-k groups
   constexpr int LR = 40;                 // LDS row: 32 halves + 8 pad = 80 B
@@ -79,7 +85,9 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
   constexpr bool LANEG = XMODE == F16_X_NHWC_VEC || XMODE == F16_X_NHWC_PAIR;  // lane-varying k group
   static_assert(WM * WN == 4 && FM >= 1 && FN >= 1 && BN % 64 == 0 && 256 % BN == 0, "tile");
   typedef typename std::conditional<XMODE == F16_X_NCHW32, float, _Float16>::type XT;
-  constexpr int MAIN_HALVES = 2 * (BM + BN) * LR, EPI_HALVES = 4 * TN * SR;
+  constexpr int SRE = BM + 8;            // EP staging row: one conv position's BM channels + pad (halves)
+  constexpr int MAIN_HALVES = 2 * (BM + BN) * LR, EPI_HALVES = EP ? BN * SRE : 4 * TN * SR;
+  static_assert(!EP || (WM == 1 && BN == 256 && H_EP_RC * H_EP_CC <= BN), "pooled epilogue tile");
   __shared__ __attribute__((aligned(16))) _Float16 smem[MAIN_HALVES > EPI_HALVES ? MAIN_HALVES : EPI_HALVES];
   __shared__ float sbias[BM];
   _Float16(*As)[BM][LR] = reinterpret_cast<_Float16(*)[BM][LR]>(smem);
@@ -110,14 +118,35 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
   const int qbase = __builtin_amdgcn_readfirstlane(tid / BN);
   int xoff[NPX], ih0[NPX], iw0[NPX];
   bool nok[NPX];
+  // EP: N tile nt = (image, pooled tile row, pooled tile column)
+  int ep_img = 0, ep_ph0 = 0, ep_pw0 = 0;
+  if constexpr (EP) {
+    const int tpi = p.ep_tr * p.ep_tc;
+    ep_img = nt / tpi;
+    const int t = nt - ep_img * tpi;
+    ep_ph0 = (t / p.ep_tc) * H_EP_PR;
+    ep_pw0 = (t - (t / p.ep_tc) * p.ep_tc) * H_EP_PC;
+  }
 #pragma unroll
   for (int u = 0; u < NPX; ++u) {
-    const int bn = n0 + bcol0 + 64 * u;
-    nok[u] = bn < p.Ntot;
-    const int nn = nok[u] ? bn : 0;
-    const int img = nn / P;
-    const int pix = nn - img * P;
-    const int oh = pix / p.Wo, ow = pix - oh * p.Wo;
+    int img, oh, ow;
+    if constexpr (EP) {
+      const int bcol = bcol0 + 64 * u;
+      const int prc = bcol / H_EP_CC, pcc = bcol - prc * H_EP_CC;
+      img = ep_img;
+      oh = ep_ph0 * 2 - p.ep_pt + prc;
+      ow = ep_pw0 * 2 - p.ep_pl + pcc;
+      nok[u] = img < p.N && bcol < H_EP_RC * H_EP_CC && (unsigned)oh < (unsigned)p.Ho && (unsigned)ow < (unsigned)p.Wo;
+      if (!nok[u]) img = oh = ow = 0;
+    } else {
+      const int bn = n0 + bcol0 + 64 * u;
+      nok[u] = bn < p.Ntot;
+      const int nn = nok[u] ? bn : 0;
+      img = nn / P;
+      const int pix = nn - img * P;
+      oh = pix / p.Wo;
+      ow = pix - oh * p.Wo;
+    }
     ih0[u] = oh * p.sh - p.pt;
     iw0[u] = ow * p.sw - p.pl;
     xoff[u] = img * (int)p.x_nstride + (ih0[u] * p.W + iw0[u]) * (XMODE == F16_X_NCHW32 ? 1 : p.x_ps);
@@ -288,6 +317,67 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
   }
 #endif
 
+  if constexpr (EP) {
+    // pooled epilogue: every conv position of the patch goes to LDS as [position][channel] f16
+    // (bias, Relu, one rounding; 0 outside the conv plane = the pool's zero padding,
+    // max_pool_op.rs:265-276), then each (pooled output, 8-channel group) takes the 3x3 max from
+    // -FLT_MAX (:337) and leaves by one 16-B NHWC store
+    __syncthreads();  // every wave is done with the operand tiles
+    const int ohb = ep_ph0 * 2 - p.ep_pt, owb = ep_pw0 * 2 - p.ep_pl;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wn0 + j * 32 + lcol;
+      const int prc = col / H_EP_CC, pcc = col - prc * H_EP_CC;
+      const bool cok = col < H_EP_RC * H_EP_CC && (unsigned)(ohb + prc) < (unsigned)p.Ho &&
+                       (unsigned)(owb + pcc) < (unsigned)p.Wo;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ch = i * 32 + 8 * q + 4 * lrow;
+          half4 h;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = acc[i][j][4 * q + e] + sbias[ch + e];
+            if (p.relu) v = fmaxf(v, 0.0f);
+            h[e] = cok ? (_Float16)v : (_Float16)0.0f;
+          }
+          *reinterpret_cast<half4*>(smem + col * SRE + ch) = h;
+        }
+    }
+    __syncthreads();
+    _Float16* __restrict__ y = reinterpret_cast<_Float16*>(p.y);
+    constexpr int CGN = BM / 8;  // 8-channel groups
+    for (int task = tid; task < H_EP_PR * H_EP_PC * CGN; task += 256) {
+      const int pp = task / CGN, cg = task - pp * CGN;
+      const int a = pp / H_EP_PC, b = pp - a * H_EP_PC;
+      float mx[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) mx[e] = -FLT_MAX;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const half8 v = *reinterpret_cast<const half8*>(smem + ((2 * a + r) * H_EP_CC + 2 * b + s) * SRE + cg * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], (float)v[e]);
+        }
+      const int ph = ep_ph0 + a, pw = ep_pw0 + b, m = m0 + cg * 8;
+      if (ph >= p.ep_Ho || pw >= p.ep_Wo || ep_img >= p.N || m >= p.M) continue;
+      _Float16* dst = y + (unsigned)(ep_img * (int)p.y_nstride + (ph * p.ep_Wo + pw) * p.y_ps + m);
+      if (p.vec_out) {
+        half8 h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = (_Float16)mx[e];
+        *reinterpret_cast<half8*>(dst) = h;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (m + e < p.M) dst[e] = (_Float16)mx[e];
+      }
+    }
+    return;
+  }
   // epilogue: + bias (f32), optional Relu, one rounding to f16, NHWC store.  Each wave stages its
   // TM channels x TN pixels in its own LDS slice as [pixel][channel] (accumulator rows 8q + 4 lrow
   // + 0..3 are four consecutive channels: one 8-B write), then stores every pixel's channel run
@@ -693,6 +783,32 @@ static void launch_f16_cfg(const ConvParams& p0, int xmode, hipStream_t s) {
         hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, WN, F16_X_NHWC_VEC>), grid, block, 0, s, p);
       break;
   }
+}
+
+// pooled epilogue (EP): BM x 256 tiles of 1 x 4 waves, the N tile a 13 x 19 conv patch
+template <int BM>
+static void launch_f16_epool_cfg(const ConvParams& p0, int xmode, hipStream_t s) {
+  ConvParams p = p0;
+  p.mtiles = (p.M + BM - 1) / BM;
+  p.ntiles = p.N * p.ep_tr * p.ep_tc;
+  dim3 grid((unsigned)(p.mtiles * p.ntiles)), block(256);
+  switch (xmode) {
+    case F16_X_NCHW32: hipLaunchKernelGGL((conv_f16_kernel<BM, 256, 1, 4, F16_X_NCHW32, 1>), grid, block, 0, s, p); break;
+    case F16_X_NHWC_ELEM: hipLaunchKernelGGL((conv_f16_kernel<BM, 256, 1, 4, F16_X_NHWC_ELEM, 1>), grid, block, 0, s, p); break;
+    case F16_X_NHWC_PAIR: hipLaunchKernelGGL((conv_f16_kernel<BM, 256, 1, 4, F16_X_NHWC_PAIR, 1>), grid, block, 0, s, p); break;
+    default: hipLaunchKernelGGL((conv_f16_kernel<BM, 256, 1, 4, F16_X_NHWC_VEC, 1>), grid, block, 0, s, p); break;
+  }
+}
+
+void launch_conv_f16_epool(const ConvParams& p, int xmode, hipStream_t s) {
+  // rows per tile as launch_conv_epool: 96 when it divides the channel count (conv1's 96), else 128,
+  // or 32 for M <= 32
+  if (p.M <= 32)
+    launch_f16_epool_cfg<32>(p, xmode, s);
+  else if (p.M % 96 == 0 || p.M < 96)
+    launch_f16_epool_cfg<96>(p, xmode, s);
+  else
+    launch_f16_epool_cfg<128>(p, xmode, s);
 }
 
 void launch_conv_f16(const ConvParams& p, int cfg, int xmode, hipStream_t s) {

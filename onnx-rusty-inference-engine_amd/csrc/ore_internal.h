@@ -95,12 +95,18 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
                     const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, float* y,
                     int64_t y_nstride, int64_t x_ps = 0, int64_t y_ps = 0,  // plane strides, 0 = dense
                     int x_es = 4);  // input element bytes (2: f16; only with an f16 plan, whose output is f16)
+// the MaxPool fused into an f16 conv's epilogue (ORE_FUSE_CONV_POOL; 3x3 / stride 2)
+struct F16Epool {
+  int64_t kh, kw, sh, sw;
+  Window win;  // the pool's window over the conv output
+};
 // f16 plan (f16 models): y is NHWC f16 with pixel stride y_ps; x is the f32 NCHW model input
 // (F16_X_NCHW32, plane stride x_ps) or NHWC f16 with pixel stride x_ps.  ktab per plan.xmode.
+// ep: the following MaxPool in the epilogue (y is then the pooled NHWC output)
 ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_t N, int64_t C, int64_t H, int64_t W,
                         int64_t x_nstride, int64_t x_ps, const void* wp, const int2* ktab, int64_t M, int64_t kh,
                         int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, void* y,
-                        int64_t y_nstride, int64_t y_ps);
+                        int64_t y_nstride, int64_t y_ps, const F16Epool* ep = nullptr);
 // Conv (+ Relu) and the MaxPool (pkh x pkw, strides psh/psw, window pwin over the conv's Ho x Wo
 // output) in one launch: y is the pooled output (image stride y_nstride, plane stride y_ps)
 ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,

@@ -120,6 +120,9 @@ void launch_gap_nhwc(const void* x, float* y, int N, int C, int HW, int cs, long
 // Concat along channels of two dense NHWC f16 values (pixels = N*H*W)
 void launch_concat_nhwc(const void* a, const void* b, void* y, long long pixels, int Ca, int Cb, hipStream_t s);
 void launch_conv_f16(const ConvParams& p, int cfg, int xmode, hipStream_t s);
+// f16 Conv (+ Relu) with the following 3x3 / stride-2 MaxPool in its epilogue (ConvParams ep_*,
+// NHWC f16 pooled output)
+void launch_conv_f16_epool(const ConvParams& p, int xmode, hipStream_t s);
 size_t conv_packed_bytes(const ConvPlan& pln);
 // packs ONNX weights [M][C][kh][kw] (or MatMul [K][M]) in the layout the plan's kernel reads
 void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, const ConvPlan& pln, float* wp,

@@ -535,8 +535,8 @@ ore_status plan(ore_model* m) {
     count_uses(m, m->steps);
   }
   // (1c) Conv (-> Relu) -> MaxPool, the conv output read by the pool only: one launch when the
-  // recomputed patch costs <= ORE_EPOOL_MAX_WORK x the conv's columns (f32)
-  if ((m->fusion & ORE_FUSE_CONV_POOL) && !m->f16) {
+  // recomputed patch costs <= ORE_EPOOL_MAX_WORK x the conv's columns (f32 and f16 models)
+  if (m->fusion & ORE_FUSE_CONV_POOL) {
     const char* e = getenv("ORE_EPOOL_MAX_WORK");  // tuning knob
     const double max_work = e ? atof(e) : 1.25;
     for (size_t i = 0; i < m->steps.size(); ++i) {
@@ -546,7 +546,8 @@ ore_status plan(ore_model* m) {
       const int pc = producer[v];
       if (pc < 0 || m->values[v].uses != 1 || m->values[v].is_output) continue;
       Step& cv = m->steps[pc];
-      if (cv.kind != S_CONV || cv.pool || cv.epool || cv.plan.window || cv.plan.f16) continue;
+      if (cv.kind != S_CONV || cv.pool || cv.epool || cv.plan.window) continue;
+      if (cv.plan.f16 != (m->values[pl.out].es == 2 ? 1 : 0)) continue;  // f16 conv -> f16 pool only
       int a = 0, b = 0;
       const double work = epool_tile(cv.win.Ho, cv.win.Wo, pl.kh, pl.kw, pl.sh, pl.sw, pl.win, &a, &b);
       if (work == 0.0 || work > max_work) continue;
@@ -554,7 +555,8 @@ ore_status plan(ore_model* m) {
       cv.out = pl.out;
       cv.ep_kh = pl.kh; cv.ep_kw = pl.kw; cv.ep_sh = pl.sh; cv.ep_sw = pl.sw; cv.ep_win = pl.win;
       // algorithmic bytes: the conv's input + the pooled output (the pre-pool tensor never moves)
-      cv.bytes_per_img = 4.0 * double(cv.C * cv.H * cv.W) + 4.0 * double(cv.M * pl.win.Ho * pl.win.Wo);
+      cv.bytes_per_img = double(m->values[cv.in0].es) * double(cv.C * cv.H * cv.W) +
+                         double(m->values[pl.out].es) * double(cv.M * pl.win.Ho * pl.win.Wo);
       m->values[v].elided = true;
       producer[pl.out] = pc;
       pl.kind = S_NOP;
@@ -820,6 +822,7 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
     case S_CONV: {
       const Ref x = ref_of(m, s.in0);
       const float* bias = s.in2 >= 0 ? m->values[s.in2].cptr : nullptr;
+      const F16Epool ep{s.ep_kh, s.ep_kw, s.ep_sh, s.ep_sw, s.ep_win};
       if (s.plan.f16 && (s.plan.xmode == F16_X_NHWC_PAIR || s.plan.xmode == F16_X_NHWC8)) {
         // convert the f32 NCHW input to NHWC f16 (4 / 8 channels per pixel), then gather
         const int cs = s.plan.xmode == F16_X_NHWC8 ? 8 : 4;
@@ -827,11 +830,11 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
                             ctx->stream);
         ORE_HIP_CHECK(ctx, hipGetLastError());
         return run_conv_f16(ctx, s.plan, s.xcvt, n, s.C, s.H, s.W, s.H * s.W * cs, cs, s.wp, s.ktab, s.M, s.kh, s.kw,
-                            bias, s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps);
+                            bias, s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps, s.epool ? &ep : nullptr);
       }
       if (s.plan.f16)
         return run_conv_f16(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.ktab, s.M, s.kh, s.kw, bias,
-                            s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps);
+                            s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps, s.epool ? &ep : nullptr);
       if (s.epool)
         return run_conv_epool(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.ktab, s.M, s.kh, s.kw, bias,
                               s.win, s.sh, s.sw, s.relu, s.ep_kh, s.ep_kw, s.ep_sh, s.ep_sw, s.ep_win, y.p, y.nstride,

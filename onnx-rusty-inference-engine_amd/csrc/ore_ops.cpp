@@ -284,7 +284,7 @@ ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int6
 ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_t N, int64_t C, int64_t H, int64_t W,
                         int64_t x_nstride, int64_t x_ps, const void* wp, const int2* ktab, int64_t M, int64_t kh,
                         int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, void* y,
-                        int64_t y_nstride, int64_t y_ps) {
+                        int64_t y_nstride, int64_t y_ps, const F16Epool* ep) {
   if (N == 0) return ORE_OK;
   if (!pln.f16) return set_error(ctx, ORE_ERR_INVALID, "internal: run_conv_f16 needs an f16 plan");
   const bool nchw = pln.xmode == F16_X_NCHW32;
@@ -293,7 +293,7 @@ ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_
     ConvPlan q = pln;
     q.xmode = F16_X_NHWC_VEC;
     return run_conv_f16(ctx, q, x, N, 8, H, W, x_nstride, x_ps, wp, ktab, M, kh, kw, bias, win, sh, sw, relu, y,
-                        y_nstride, y_ps);
+                        y_nstride, y_ps, ep);
   }
   if (x_ps == 0) x_ps = nchw ? H * W : C;
   if (y_ps == 0) y_ps = M;
@@ -328,10 +328,21 @@ ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_
     p.x_bytes = (extent > 0 && extent < (int64_t(1) << 31)) ? extent : 0;
   }
   if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;  // tuning knob
+  if (ep) {  // pooled epilogue: y is the pool's NHWC output [pwin.Ho][pwin.Wo]
+    int tr = 0, tc = 0;
+    if (epool_tile(win.Ho, win.Wo, ep->kh, ep->kw, ep->sh, ep->sw, ep->win, &tr, &tc) == 0.0)
+      return set_error(ctx, ORE_ERR_INVALID, "internal: the pooled epilogue takes 3x3 / stride-2 pools");
+    p.ep_pt = int(ep->win.pt); p.ep_pl = int(ep->win.pl); p.ep_Ho = int(ep->win.Ho); p.ep_Wo = int(ep->win.Wo);
+    p.ep_tr = tr; p.ep_tc = tc;
+    p.Ntot = N * int64_t(tr) * tc * CONV_EPOOL_BN;
+  }
   if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(int64_t(pln.krows) * pln.Mp) ||
       !fits_i32(p.Ntot + 256) || (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))
     return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
-  launch_conv(p, pln, ctx->stream);
+  if (ep)
+    launch_conv_f16_epool(p, pln.xmode, ctx->stream);
+  else
+    launch_conv(p, pln, ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());
   return ORE_OK;
 }

@@ -294,9 +294,11 @@ def _conv_pool_model(x_shape, w, b, conv_pads, conv_strides, relu, pool_k, pool_
     (4, 30, 24, 5, 1, 2, True, 3, 2, [1, 0, 0, 1]),     # asymmetric pool pads, 32-row tile
     (6, 20, 16, 3, 2, 1, True, 2, 2, [0, 0, 0, 0]),     # 2x2 pool: not fused (the epilogue takes 3x3/s2)
 ])
-def test_conv_pool_fusion_bit_identical(gpu_ctx, case):
+@pytest.mark.parametrize("precision", ["f32", "f16"])
+def test_conv_pool_fusion_bit_identical(gpu_ctx, case, precision):
     """ORE_FUSE_CONV_POOL: the pooled epilogue equals the separate conv + pool kernels bit for bit
-    (forced with ORE_EPOOL_MAX_WORK so the small planes qualify)."""
+    (forced with ORE_EPOOL_MAX_WORK so the small planes qualify).  f16 models: the conv values are
+    rounded to f16 before the max, as the separate conv stores them (NHWC f16)."""
     import os
     import ore
     C, H, M, k, cs, cp, relu, pk, ps, ppads = case
@@ -309,7 +311,7 @@ def test_conv_pool_fusion_bit_identical(gpu_ctx, case):
     os.environ["ORE_EPOOL_MAX_WORK"] = "100"
     try:
         for fusion in (ore.FUSE_ALL | ore.KEEP_VALUES, (ore.FUSE_ALL & ~ore.FUSE_CONV_POOL) | ore.KEEP_VALUES):
-            m = ore.Model(gpu_ctx, mb, max_batch=3)
+            m = ore.Model(gpu_ctx, mb, max_batch=3, precision=precision)
             m.set_fusion(fusion)
             _np(m.run(_t(x)))
             vals.append(m.read_value("p"))
@@ -323,20 +325,22 @@ def test_conv_pool_fusion_bit_identical(gpu_ctx, case):
     import oracle
     c = oracle.conv2d(x, w, b, pads=[cp] * 4, strides=(cs, cs))
     ref = oracle.maxpool2d(oracle.relu(c) if relu else c, (pk, pk), (ps, ps), auto_pad="NOTSET", pads=ppads)
-    np.testing.assert_allclose(vals[0], ref, rtol=1e-5, atol=1e-5)
+    tol = 1e-5 if precision == "f32" else 2e-2 * (np.abs(ref).max() + 1.0)  # f16 storage: ~3 significant digits
+    np.testing.assert_allclose(vals[0], ref, rtol=tol if precision == "f16" else 1e-5, atol=tol)
 
 
 @pytest.mark.parametrize("hw", [64, 224])
-def test_squeezenet_conv_pool_fusion(gpu_ctx, hw):
+@pytest.mark.parametrize("precision", ["f32", "f16"])
+def test_squeezenet_conv_pool_fusion(gpu_ctx, hw, precision):
     """SqueezeNet with conv1 + pool1 fused (the only pair under the default work bound at 224):
-    probabilities bit-identical to the unfused pool."""
+    probabilities bit-identical to the unfused pool, in the f32 and the f16 model."""
     import ore
     from ore import squeezenet
     mb = squeezenet.build(hw)
     x = _t(squeezenet.synthetic_input(3, hw, seed=17))
     outs = []
     for fusion in (ore.FUSE_ALL, ore.FUSE_ALL & ~ore.FUSE_CONV_POOL):
-        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        m = ore.Model(gpu_ctx, mb, max_batch=3, precision=precision)
         m.set_fusion(fusion)
         outs.append(_np(m.run(x)))
         m.close()
