@@ -152,12 +152,13 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* onnx_bytes, size_t len, i
                              ore_model** out);
 ore_status ore_model_destroy(ore_model* m);
 /* flags: bit 0 = fuse Conv->Relu, bit 1 = Concat in place, bit 2 = alias Dropout/Reshape,
- * bit 5 = Conv->MaxPool (ORE_FUSE_CONV_POOL below).  ORE_FUSE_ALL is the default; 0 runs every
- * node as its own kernel (op-by-op parity). */
+ * bit 5 = Conv->MaxPool (ORE_FUSE_CONV_POOL below), bit 6 = fire module + next squeeze
+ * (ORE_FUSE_FIRE below).  ORE_FUSE_ALL is the default; 0 runs every node as its own kernel
+ * (op-by-op parity). */
 #define ORE_FUSE_CONV_RELU 1
 #define ORE_FUSE_CONCAT 2
 #define ORE_FUSE_ALIAS 4
-#define ORE_FUSE_ALL 39
+#define ORE_FUSE_ALL 103
 /* bit 4 (opt-in, not in ORE_FUSE_ALL): a 3x3 MaxPool whose only consumer is a 1x1 stride-1 Conv
  * runs inside that conv's operand gather (each B element = the window max of the pre-pool
  * tensor); the pooled tensor is never written.  Max is exact, so results are bit-identical.
@@ -172,6 +173,14 @@ ore_status ore_model_destroy(ore_model* m);
  * <= ORE_EPOOL_MAX_WORK (environment, default 1.25) x the conv's own (SqueezeNet @224: conv1 +
  * pool1 only, 1.16x); f32 models. */
 #define ORE_FUSE_CONV_POOL 32
+/* bit 6: a fire module (Concat of a 1x1 and a 3x3 'same' Conv + Relu of one value, 64-multiple
+ * channel counts) and the 1x1 Conv + Relu (<= 64 channels) that is the Concat's only reader -- the
+ * next fire's squeeze -- as ONE launch: the expand outputs and the Concat never reach HBM.
+ * Bit-identical (every output keeps its k-ordered MFMA chain; the squeeze still sums the concat
+ * channels in ascending order).  f32 models; applied when max_batch * H * W >= ORE_FIRE_MIN_COLS
+ * (environment, default 65536: one 64-pixel wave per SIMD), below which the fused launch has too
+ * few waves (batch 1 keeps the separate kernels). */
+#define ORE_FUSE_FIRE 64
 /* debug: give every value its own storage (no liveness reuse) so any value can be read back */
 #define ORE_KEEP_VALUES 8
 ore_status ore_model_set_fusion(ore_model* m, int32_t flags);

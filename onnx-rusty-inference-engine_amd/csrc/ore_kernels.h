@@ -86,6 +86,29 @@ struct AddParams {
   long long bs[4];  // b strides in elements, 0 on broadcast axes
 };
 
+// A fire module fused with the next squeeze (ore_fire.hip, ORE_FUSE_FIRE): S' = Relu(Ws [e1; e3] + bs)
+// with e1 = Relu(W1 S + b1) (1x1), e3 = Relu(W3 * S + b3) (3x3, pad 1), e1 / e3 never stored.
+struct FireParams {
+  const float* x;   // S [N][C][H][W], plane stride x_ps, image stride x_nstride
+  const float* w1;  // W1 packed by launch_fire_pack: [roundup(C, 32)][E1]
+  const float* b1;
+  const float* w3;  // W3 packed by launch_fire_pack: [roundup(9C, 32)][E3], k = (c, r, s)
+  const float* b3;
+  const float* ws;  // the squeeze's standard K-major packing [roundup(E1 + E3, 32)][Msp] (launch_pack)
+  const float* bs;
+  float* y;         // S' [N][Ms][H][W], plane stride y_ps (= columns per image), image stride y_nstride
+  int N, C, H, W, E1, E3, Ms, Msp;
+  int x_ps, y_ps;
+  long long x_nstride, y_nstride, Ntot;  // Ntot = N * y_ps
+  long long x_bytes;                     // x's valid extent in bytes
+  int x_guard, x_lead;                   // mapped bytes before x; bytes the 3x3 taps read before it
+  int ntiles;                            // filled by the launcher
+};
+bool fire_eligible(const FireParams& p);
+void launch_fire(const FireParams& p, hipStream_t s);
+// W [M][K] -> the fire kernel's row-permuted K-major packing (M % 64 == 0)
+void launch_fire_pack(const float* w, int M, int K, float* wf, hipStream_t s);
+
 int conv_tile_config(int M);
 int conv_packed_mp(int M);  // padded M of the packed weights
 int conv_packed_kp(int K);  // padded K of the packed weights

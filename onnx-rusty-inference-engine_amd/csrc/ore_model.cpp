@@ -27,7 +27,7 @@ using namespace ore;
 
 namespace {
 
-enum StepKind { S_CONV, S_MAXPOOL, S_RELU, S_ADD, S_SOFTMAX, S_MATMUL, S_GAP, S_CONCAT, S_COPY, S_NOP };
+enum StepKind { S_CONV, S_MAXPOOL, S_RELU, S_ADD, S_SOFTMAX, S_MATMUL, S_GAP, S_CONCAT, S_COPY, S_NOP, S_FIRE };
 
 struct Value {
   std::string name;
@@ -85,6 +85,13 @@ struct Step {
   bool epool = false;
   int64_t ep_kh = 0, ep_kw = 0, ep_sh = 1, ep_sw = 1;
   Window ep_win;
+  // S_FIRE (ORE_FUSE_FIRE): this squeeze conv also computes the fire module feeding it; in0 is the
+  // fire's input S (C = its channels for the expands, fire_K = the squeeze's K = E1 + E3)
+  int64_t fire_C = 0, fire_E1 = 0, fire_E3 = 0;
+  const float* fire_w1 = nullptr;  // launch_fire_pack layouts of the expand weights
+  const float* fire_w3 = nullptr;
+  const float* fire_b1 = nullptr;
+  const float* fire_b3 = nullptr;
   ConvPlan plan{};        // kernel choice and weight layout for S_CONV / S_MATMUL
   float* wp = nullptr;    // packed weights (layout per plan) for S_CONV / S_MATMUL
   const int2* ktab = nullptr;  // gather table (follows wp in the packed allocation; gather kernel only)
@@ -108,6 +115,7 @@ struct ore_model {
   int output_value = -1;
   float* consts = nullptr;       // one device allocation for all f32 initializers
   float* packed = nullptr;       // packed conv / matmul weights (one allocation)
+  std::map<int, float*> fire_packs;  // base step index -> its weights in launch_fire_pack layout
   char* arena = nullptr;        // arena_alloc + ARENA_LEAD
   char* arena_alloc = nullptr;  // the hipMalloc'd block (a 4 KiB lead before the arena proper)
   size_t arena_bytes = 0;
@@ -478,7 +486,16 @@ void count_uses(ore_model* m, const std::vector<Step>& steps) {
       if (id >= 0) m->values[id].uses++;
 }
 
-bool strided_writer(const Step& s) { return s.kind == S_CONV || s.kind == S_MAXPOOL; }
+// plane stride of a padded activation: 128-B aligned planes when that costs <= 5 %, else 16-B
+// aligned ones when that does (13 x 13 -> 172: the streaming conv's 16-B operand loads and stores
+// need 4-float planes), else dense
+int64_t padded_plane(int64_t P) {
+  int64_t Pp = (P + 31) / 32 * 32;
+  if (Pp - P > P / 20) Pp = (P + 3) / 4 * 4;
+  return Pp - P <= P / 20 ? Pp : P;
+}
+
+bool strided_writer(const Step& s) { return s.kind == S_CONV || s.kind == S_FIRE || s.kind == S_MAXPOOL; }
 
 ore_status plan(ore_model* m) {
   m->steps = m->base_steps;
@@ -564,6 +581,67 @@ ore_status plan(ore_model* m) {
     }
     count_uses(m, m->steps);
   }
+  // (1d) fire module + the next squeeze in one launch (ORE_FUSE_FIRE, f32): Concat(e1, e3) whose
+  // inputs are a 1x1 and a 3x3 'same' Conv (+ Relu) of one value S, read only by a 1x1 Conv (+ Relu)
+  // with at most 64 output channels
+  if ((m->fusion & ORE_FUSE_FIRE) && !m->f16 && (m->fusion & ORE_FUSE_CONV_RELU)) {
+    const char* e = getenv("ORE_FIRE_MIN_COLS");  // tuning knob (tests set 0)
+    const int64_t min_cols = e ? atoll(e) : 65536;
+    for (size_t i = 0; i < m->steps.size(); ++i) {
+      Step& cc = m->steps[i];
+      if (cc.kind != S_CONCAT || cc.axis != 1 || cc.in0 < 0 || cc.in1 < 0 || cc.in0 == cc.in1) continue;
+      const int pa = producer[cc.in0], pb = producer[cc.in1];
+      if (pa < 0 || pb < 0) continue;
+      int qi = -1;
+      for (size_t j = i + 1; j < m->steps.size(); ++j)
+        if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == cc.out || m->steps[j].in1 == cc.out)) { qi = int(j); break; }
+      if (qi < 0) continue;
+      Step &e1 = m->steps[pa], &e3 = m->steps[pb], &q = m->steps[qi];
+      auto is1x1 = [](const Step& s) {
+        return s.kind == S_CONV && s.relu && !s.pool && !s.epool && !s.plan.window && !s.plan.f16 && s.kh == 1 &&
+               s.kw == 1 && s.sh == 1 && s.sw == 1 && s.win.pt == 0 && s.win.pl == 0 && s.win.Ho == s.H && s.win.Wo == s.W;
+      };
+      const bool e3ok = e3.kind == S_CONV && e3.relu && !e3.pool && !e3.epool && !e3.plan.window && !e3.plan.f16 &&
+                        e3.kh == 3 && e3.kw == 3 && e3.sh == 1 && e3.sw == 1 && e3.win.pt == 1 && e3.win.pl == 1 &&
+                        e3.win.Ho == e3.H && e3.win.Wo == e3.W;
+      if (!is1x1(e1) || !e3ok || !is1x1(q) || q.in0 != cc.out || e1.in0 != e3.in0 || e1.H != e3.H || e1.W != e3.W) continue;
+      if (e1.M % 64 || e3.M % 64 || q.M > 64 || e1.C % 16 || q.C != e1.M + e3.M) continue;
+      if (m->max_batch * e1.H * e1.W < min_cols) continue;
+      if (padded_plane(e1.H * e1.W) % 4 || (m->fusion & ORE_FUSE_CONCAT) == 0) continue;  // 16-B planes (layout below)
+      const Value &va = m->values[cc.in0], &vb = m->values[cc.in1], &vc = m->values[cc.out], &vs = m->values[e1.in0];
+      if (va.uses != 1 || vb.uses != 1 || vc.uses != 1 || va.is_output || vb.is_output || vc.is_output || vs.es != 4) continue;
+      // the expand weights in the fire kernel's row-permuted packing (made once per model)
+      bool packed_ok = true;
+      for (int idx : {pa, pb}) {
+        if (m->fire_packs.count(idx)) continue;
+        const Step& e = m->steps[idx];
+        const int64_t K = e.C * e.kh * e.kw, Kp = (K + 31) / 32 * 32;
+        float* buf = nullptr;
+        if (hipMalloc(reinterpret_cast<void**>(&buf), size_t(Kp * e.M) * 4) != hipSuccess) { packed_ok = false; break; }
+        launch_fire_pack(m->values[e.in1].cptr, int(e.M), int(K), buf, m->ctx->stream);
+        m->fire_packs[idx] = buf;
+      }
+      if (!packed_ok || hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
+        return err(m, ORE_ERR_HIP, "fire weight packing failed");
+      q.kind = S_FIRE;
+      q.in0 = e1.in0;
+      q.fire_C = e1.C;
+      q.fire_E1 = e1.M;
+      q.fire_E3 = e3.M;
+      q.fire_w1 = m->fire_packs[pa];
+      q.fire_w3 = m->fire_packs[pb];
+      q.fire_b1 = e1.in2 >= 0 ? m->values[e1.in2].cptr : nullptr;
+      q.fire_b3 = e3.in2 >= 0 ? m->values[e3.in2].cptr : nullptr;
+      if (!q.fire_b1 || !q.fire_b3 || q.in2 < 0) return err(m, ORE_ERR_UNSUPPORTED, "fused fire needs conv biases");
+      q.flops_per_img += e1.flops_per_img + e3.flops_per_img;
+      q.bytes_per_img = 4.0 * double(e1.C * e1.H * e1.W) + 4.0 * double(q.M * q.H * q.W);
+      q.name = e1.name.substr(0, e1.name.find('/')) + "+" + q.name;
+      m->values[cc.in0].elided = m->values[cc.in1].elided = m->values[cc.out].elided = true;
+      e1.kind = e3.kind = cc.kind = S_NOP;
+      e1.in0 = e3.in0 = cc.in0 = cc.in1 = -1;
+    }
+    count_uses(m, m->steps);
+  }
   // (2) Dropout / activation Reshape as aliases
   if (m->fusion & ORE_FUSE_ALIAS) {
     for (auto& s : m->steps) {
@@ -607,7 +685,8 @@ ore_status plan(ore_model* m) {
     for (const Step& st : m->steps) {
       if (st.kind == S_NOP) continue;
       // GlobalAveragePool reads f32 planes at any stride (launch_step)
-      const bool ok = st.kind == S_CONV || st.kind == S_MAXPOOL || (st.kind == S_GAP && !m->values[st.in0].nhwc);
+      const bool ok = st.kind == S_CONV || st.kind == S_FIRE || st.kind == S_MAXPOOL ||
+                      (st.kind == S_GAP && !m->values[st.in0].nhwc);
       for (int id : {st.in0, st.in2, st.out})
         if (id >= 0 && !m->values[id].is_const && !ok) dense[root(id)] = 1;
       if (st.in1 >= 0 && !m->values[st.in1].is_const) dense[root(st.in1)] = 1;
@@ -626,14 +705,9 @@ ore_status plan(ore_model* m) {
         continue;
       }
       const int64_t P = v.dims[2] * v.dims[3];
-      // 128-B aligned planes when that costs <= 5 %, else 16-B aligned ones (13 x 13 -> 172: the
-      // streaming conv's 16-B operand loads and stores need 4-float planes)
-      int64_t Pp = (P + 31) / 32 * 32;
-      if (Pp - P > P / 20) Pp = (P + 3) / 4 * 4;
       static const bool pad_planes = getenv("ORE_PAD_PLANES") ? atoi(getenv("ORE_PAD_PLANES")) != 0 : true;  // experiment knob
-      const bool pad = pad_planes && (m->fusion & ORE_FUSE_CONCAT) && !dense[id] && !v.is_input && !v.is_output &&
-                       Pp - P <= P / 20;
-      v.ps = pad ? Pp : P;
+      const bool pad = pad_planes && (m->fusion & ORE_FUSE_CONCAT) && !dense[id] && !v.is_input && !v.is_output;
+      v.ps = pad ? padded_plane(P) : P;
     }
     for (auto& v : m->values)  // views inherit the plane stride of their root
       if (v.alias_of >= 0 && v.ndim == 4) {
@@ -849,6 +923,16 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       ctx->mapped_lo = ctx->mapped_hi = nullptr;
       return st;
     }
+    case S_FIRE: {
+      const Ref x = ref_of(m, s.in0);
+      ctx->mapped_lo = m->arena_alloc;  // the arena and its 4 KiB lead are mapped
+      ctx->mapped_hi = m->arena ? m->arena + m->arena_bytes : nullptr;
+      const ore_status st = run_fire(ctx, x.p, n, s.fire_C, s.H, s.W, x.nstride, x.ps ? x.ps : s.H * s.W, s.fire_w1,
+                                     s.fire_b1, s.fire_E1, s.fire_w3, s.fire_b3, s.fire_E3, s.wp, s.plan.Mp,
+                                     m->values[s.in2].cptr, s.M, y.p, y.nstride, y.ps ? y.ps : s.H * s.W);
+      ctx->mapped_lo = ctx->mapped_hi = nullptr;
+      return st;
+    }
     case S_MATMUL: {
       const Ref x = ref_of(m, s.in0);
       return run_conv(ctx, s.plan, x.p, n, s.C, 1, 1, x.nstride, s.wp, s.ktab, s.M, 1, 1, nullptr, s.win, 1, 1, false, y.p,
@@ -1054,6 +1138,7 @@ ore_status ore_model_destroy(ore_model* m) {
   if (m->arena_alloc) (void)hipFree(m->arena_alloc);
   if (m->consts) (void)hipFree(m->consts);
   if (m->packed) (void)hipFree(m->packed);
+  for (auto& kv : m->fire_packs) (void)hipFree(kv.second);
   for (auto& s : m->base_steps)
     if (s.xcvt) (void)hipFree(s.xcvt);
   delete m;
@@ -1062,7 +1147,7 @@ ore_status ore_model_destroy(ore_model* m) {
 
 ore_status ore_model_set_fusion(ore_model* m, int32_t flags) {
   if (!m) return set_error(nullptr, ORE_ERR_INVALID, "null model");
-  m->fusion = flags & (ORE_FUSE_ALL | ORE_FUSE_POOL_CONV | ORE_FUSE_CONV_POOL | ORE_KEEP_VALUES);
+  m->fusion = flags & (ORE_FUSE_ALL | ORE_FUSE_POOL_CONV | ORE_FUSE_CONV_POOL | ORE_FUSE_FIRE | ORE_KEEP_VALUES);
   return plan(m);
 }
 
@@ -1259,6 +1344,7 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
 int32_t ore_model_step_tile(ore_model* m, int32_t i) {
   if (!m || i < 0 || size_t(i) >= m->exec_steps.size()) return -1;
   const Step& s = m->steps[m->exec_steps[i]];
+  if (s.kind == S_FIRE) return CONV_TILES_F32;  // "fire": the fused fire kernel (ore.Model.TILE_NAMES)
   return (s.kind == S_CONV || s.kind == S_MATMUL) ? s.plan.cfg : -1;
 }
 
@@ -1313,7 +1399,8 @@ int32_t ore_model_step_count(ore_model* m) { return m ? int32_t(m->exec_steps.si
 ore_status ore_model_step_info(ore_model* m, int32_t i, const char** op, const char** name, double* flops, double* bytes) {
   if (!m || i < 0 || size_t(i) >= m->exec_steps.size()) return set_error(nullptr, ORE_ERR_INVALID, "bad step index");
   const Step& s = m->steps[m->exec_steps[i]];
-  static const char* kinds[] = {"Conv", "MaxPool", "Relu", "Add", "Softmax", "MatMul", "GlobalAveragePool", "Concat", "Copy", "Nop"};
+  static const char* kinds[] = {"Conv", "MaxPool", "Relu", "Add", "Softmax", "MatMul", "GlobalAveragePool", "Concat", "Copy",
+                                "Nop", "Conv"};  // S_FIRE: three convs (expand 1x1 / 3x3 + squeeze) in one launch
   if (op) *op = kinds[s.kind];
   if (name) *name = s.name.c_str();
   const double n = double(m->last_n);

@@ -186,6 +186,37 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
   return ORE_OK;
 }
 
+ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
+                    int64_t x_ps, const float* w1, const float* b1, int64_t E1, const float* w3, const float* b3,
+                    int64_t E3, const float* ws, int64_t Msp, const float* bs, int64_t Ms, float* y, int64_t y_nstride,
+                    int64_t y_ps) {
+  if (N == 0) return ORE_OK;
+  FireParams p{};
+  p.x = x; p.w1 = w1; p.b1 = b1; p.w3 = w3; p.b3 = b3; p.ws = ws; p.bs = bs; p.y = y;
+  p.N = int(N); p.C = int(C); p.H = int(H); p.W = int(W);
+  p.E1 = int(E1); p.E3 = int(E3); p.Ms = int(Ms); p.Msp = int(Msp);
+  p.x_ps = int(x_ps); p.y_ps = int(y_ps);
+  p.x_nstride = x_nstride; p.y_nstride = y_nstride;
+  p.Ntot = N * y_ps;
+  const int64_t extent = ((N - 1) * x_nstride + C * x_ps) * 4;
+  p.x_bytes = (extent > 0 && extent < (int64_t(1) << 31)) ? extent : 0;
+  {  // mapped bytes before x (as run_conv): the rest of x's page or the walker's arena lead
+    const char* xc = reinterpret_cast<const char*>(x);
+    int64_t g = int64_t(reinterpret_cast<uintptr_t>(x) & 4095);
+    if (ctx->mapped_lo && xc >= ctx->mapped_lo && xc < ctx->mapped_hi)
+      g = std::max<int64_t>(g, std::min<int64_t>(xc - ctx->mapped_lo, 1 << 20));
+    p.x_guard = int(g);
+  }
+  p.x_lead = int(((W + 1) * 4 + 15) & ~int64_t(15));
+  if (x_ps < H * W || y_ps < H * W || !fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) ||
+      !fits_i32(p.Ntot + 256))
+    return set_error(ctx, ORE_ERR_INVALID, "fire geometry exceeds 32-bit indexing");
+  if (!fire_eligible(p)) return set_error(ctx, ORE_ERR_INVALID, "internal: fused fire module on an unsupported layout");
+  launch_fire(p, ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
+}
+
 double epool_tile(int64_t Ho, int64_t Wo, int64_t pkh, int64_t pkw, int64_t psh, int64_t psw, const Window& pwin,
                   int* tr, int* tc) {
   // the kernel's pooled epilogue is specialised for 3x3 / stride-2 windows (every SqueezeNet pool)

@@ -345,3 +345,81 @@ def test_squeezenet_conv_pool_fusion(gpu_ctx, hw, precision):
         outs.append(_np(m.run(x)))
         m.close()
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def _fire_model(C, H, W, S1, E1, E3, S2):
+    """squeeze (C -> S1) -> expand 1x1 (E1) / 3x3 pad 1 (E3) -> Concat -> squeeze (S2) -> GAP, all Relu."""
+    from ore import onnx_wire as wr
+    rng = np.random.default_rng(C * 7 + H + W + S1 + E1 + E3 + S2)
+    shapes = {"wq": (S1, C, 1, 1), "w1": (E1, S1, 1, 1), "w3": (E3, S1, 3, 3), "wn": (S2, E1 + E3, 1, 1)}
+    inits, vinfo = [], [wr.encode_value_info("x", (1, C, H, W))]
+    for n, shp in shapes.items():
+        fan = shp[1] * shp[2] * shp[3]
+        w = (rng.standard_normal(shp) * np.sqrt(2.0 / fan)).astype(np.float32)
+        b = rng.uniform(-0.1, 0.1, shp[0]).astype(np.float32)
+        inits += [wr.encode_tensor(n, w), wr.encode_tensor("b" + n, b)]
+        vinfo += [wr.encode_value_info(n, w.shape), wr.encode_value_info("b" + n, b.shape)]
+    conv = lambda i, w, o, pads: wr.encode_node("Conv", [i, w, "b" + w], [o], attrs=[
+        wr.encode_attr_ints("pads", pads), wr.encode_attr_ints("strides", [1, 1])])
+    nodes = [conv("x", "wq", "q", [0] * 4), wr.encode_node("Relu", ["q"], ["qr"]),
+             conv("qr", "w1", "e1", [0] * 4), wr.encode_node("Relu", ["e1"], ["e1r"]),
+             conv("qr", "w3", "e3", [1] * 4), wr.encode_node("Relu", ["e3"], ["e3r"]),
+             wr.encode_node("Concat", ["e1r", "e3r"], ["cat"], attrs=[wr.encode_attr_int("axis", 1)]),
+             conv("cat", "wn", "n", [0] * 4), wr.encode_node("Relu", ["n"], ["nr"]),
+             wr.encode_node("GlobalAveragePool", ["nr"], ["y"])]
+    return wr.encode_model("fire", nodes, inits, vinfo, [wr.encode_value_info("y", (1, S2, 1, 1))])
+
+
+@pytest.mark.parametrize("case", [
+    # C, H, W, S1, E1, E3, S2: the fused fire kernel's shapes (16-B planes: H*W % 4 == 0 after padding)
+    (16, 12, 12, 16, 64, 64, 16),     # fire2 -> squeeze3 shape family
+    (32, 9, 8, 32, 128, 128, 48),     # fire5 -> squeeze6 (MFS = 3), W = 8: row wraps inside a pixel group
+    (24, 8, 7, 48, 192, 192, 64),     # fire7 -> squeeze8 (MFS = 4), W = 7
+    (16, 13, 13, 16, 64, 128, 32),    # unequal expands, fire9-like 13 x 13 planes
+])
+def test_fire_fusion_bit_identical(gpu_ctx, case, monkeypatch):
+    """ORE_FUSE_FIRE: expand 1x1 + expand 3x3 + Concat + the next squeeze in one launch equals the
+    separate kernels bit for bit (forced with ORE_FIRE_MIN_COLS=0 at these small sizes), and the
+    oracle within the conv tolerance."""
+    import ore
+    import oracle
+    monkeypatch.setenv("ORE_FIRE_MIN_COLS", "0")
+    C, H, W, S1, E1, E3, S2 = case
+    mb = _fire_model(*case)
+    x = np.random.default_rng(sum(case)).standard_normal((5, C, H, W)).astype(np.float32)
+    vals = []
+    for fusion in (ore.FUSE_ALL | ore.KEEP_VALUES, (ore.FUSE_ALL & ~ore.FUSE_FIRE) | ore.KEEP_VALUES):
+        m = ore.Model(gpu_ctx, mb, max_batch=5)
+        m.set_fusion(fusion)
+        y = _np(m.run(_t(x)))
+        vals.append((y, m.read_value("nr")))
+        if fusion & ore.FUSE_FIRE:
+            assert "fire" in [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+            with pytest.raises(ore.OreError):
+                m.read_value("cat")  # never materialised
+        m.close()
+    np.testing.assert_array_equal(vals[0][1], vals[1][1])
+    np.testing.assert_array_equal(vals[0][0], vals[1][0])
+    ref = oracle.Model(mb).run(x, S2)
+    np.testing.assert_allclose(vals[0][0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("hw", [64, 224])
+def test_squeezenet_fire_fusion(gpu_ctx, hw, monkeypatch):
+    """SqueezeNet with the five fire + squeeze pairs fused (ORE_FIRE_MIN_COLS=0 so batch 3 fuses):
+    probabilities bit-identical to the separate kernels."""
+    import ore
+    from ore import squeezenet
+    monkeypatch.setenv("ORE_FIRE_MIN_COLS", "0")
+    mb = squeezenet.build(hw)
+    x = _t(squeezenet.synthetic_input(3, hw, seed=19))
+    outs = []
+    for fusion in (ore.FUSE_ALL, ore.FUSE_ALL & ~ore.FUSE_FIRE):
+        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion(fusion)
+        outs.append(_np(m.run(x)))
+        if fusion & ore.FUSE_FIRE:
+            # @64 the 7 x 7 planes of fire5-8 cannot take 16-B padding: fire2 and fire3 only
+            assert sum(1 for t in m.tiles() if t >= 0 and ore.Model.TILE_NAMES[t] == "fire") == (5 if hw == 224 else 2)
+        m.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
