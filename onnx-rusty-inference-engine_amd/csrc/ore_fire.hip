@@ -47,8 +47,11 @@ void launch_fire_pack(const float* w, int M, int K, float* wf, hipStream_t s) {
 }
 
 // MFS: 16-row fragments of the squeeze output (Ms <= 16 MFS), D: K-loop ring depth
+#ifndef ORE_FIRE_MINB
+#define ORE_FIRE_MINB 2  // __launch_bounds__ minimum blocks per CU (experiment knob)
+#endif
 template <int MFS, int D>
-__global__ __launch_bounds__(256, 2) void fire_kernel(FireParams p) {
+__global__ __launch_bounds__(256, ORE_FIRE_MINB) void fire_kernel(FireParams p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nwg = gridDim.x, bid = blockIdx.x;
@@ -231,11 +234,15 @@ bool fire_eligible(const FireParams& p) {
          p.x_guard >= p.x_lead && p.x_bytes + p.x_lead < (1LL << 31) && p.Msp % 4 == 0;
 }
 
+#ifndef ORE_FIRE_D
+#define ORE_FIRE_D 4  // K-loop ring depth (experiment knob)
+#endif
+
 template <int MFS>
 static void launch_fire_cfg(const FireParams& p0, hipStream_t s) {
   FireParams p = p0;
   p.ntiles = (int)((p.Ntot + 63) / 64);
-  hipLaunchKernelGGL((fire_kernel<MFS, 4>), dim3((unsigned)((p.ntiles + 3) / 4)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL((fire_kernel<MFS, ORE_FIRE_D>), dim3((unsigned)((p.ntiles + 3) / 4)), dim3(256), 0, s, p);
 }
 
 void launch_fire(const FireParams& p, hipStream_t s) {
