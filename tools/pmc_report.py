@@ -68,8 +68,15 @@ def main():
     base = sys.argv[1]
     json_out = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
     first = sorted(d for d in glob.glob(os.path.join(base, "p*")) if os.path.isdir(d))
-    PER = period_of(first[0]) if first else 31
-    names = layer_names(PER)
+    steps = None
+    if os.path.exists(os.path.join(base, "steps.json")):  # bench.py --dump-steps: the plan's own names
+        import json
+        steps = json.load(open(os.path.join(base, "steps.json")))
+        PER = len(steps)
+        names = [s["name"] for s in steps]
+    else:
+        PER = period_of(first[0]) if first else 31
+        names = layer_names(PER)
     merged = [defaultdict(float) for _ in range(PER)]
     for d in sorted(glob.glob(os.path.join(base, "p*"))):
         if not os.path.isdir(d):
@@ -105,11 +112,16 @@ def main():
               f"{(busy / 8 / (dur * 1e3)) if busy else 0:5.2f} {r.get('vgpr', '')}/{r.get('agpr', '')}")
     if json_out:
         import json
-        conv = [r for r in merged if "conv" in str(r.get("name", ""))]
+        if steps:
+            conv = [r for r, st in zip(merged, steps) if st["op"] == "Conv"]
+        else:
+            conv = [r for r in merged if "conv" in str(r.get("name", "")) or "fire_kernel" in str(r.get("name", ""))]
         fetch = sum(2 * r.get("FETCH_SIZE", 0) * 1024 for r in conv)  # KB -> B, x2 gfx950 correction
         write = sum(r.get("WRITE_SIZE", 0) * 1024 for r in conv)
         out = {"kernel_class": "conv", "launches": len(conv), "hbm_bytes_per_launch": (fetch + write) / max(len(conv), 1),
                "fetch_bytes_per_launch": fetch / max(len(conv), 1), "write_bytes_per_launch": write / max(len(conv), 1),
+               "algorithmic_bytes_per_launch": (sum(st["bytes"] for st in steps if st["op"] == "Conv") / max(len(conv), 1)
+                                                if steps else None),
                "source": base, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, FETCH_SIZE x2 (gfx950)"}
         with open(json_out, "w") as f:
             json.dump(out, f, indent=1)
