@@ -1,0 +1,305 @@
+// Conv (stride 2, no padding) + Relu + MaxPool 3x3 / stride 2 / no padding in one launch: SqueezeNet's
+// conv1 -> relu_conv1 -> pool1 (convolution_op.rs:94-517, relu_op.rs:31-33, max_pool_op.rs:157-360).
+//
+// Why a second pooled-conv kernel.  conv_gemm_kernel's pooled epilogue (ore_conv.hip) gives each block
+// a 13 x 19 conv-output patch for a 6 x 9 pooled tile: the patch borders are recomputed by the
+// neighbouring tiles (247 conv outputs per 216 needed) and the LDS-staged main loop runs ~100 TF/s.
+// Here a block owns (image, 16 MF output channels) and WALKS the conv output plane row-major, 64 quads
+// of 4 consecutive output columns per step (4 waves x 16 lanes), so no conv output is computed twice
+// (only the 3 columns that pad a 109-wide row to 28 quads); the pooled rows live in an LDS ring.
+//
+// Main loop (as conv_stream_kernel, ore_conv_stream.hip): LDS-free implicit GEMM on
+// v_mfma_f32_16x16x4_f32, k = (c, r, s) in the reference's order, lane (lk, lj) supplies k = 4 t + lk
+// for the quad of lane lj.  With stride 2 the quad's four inputs of a tap are elements 0, 2, 4, 6 of an
+// 8-float run: one 16-B + one 12-B load, element q feeding the q-th of four MFMAs.  The tap offset
+// c x_ps + r W + s advances by 4 k per step (carries, no table).  Taps k >= K read past the buffer
+// (0), against zero weights.  The operand ring runs ACROSS the block's steps: the next step's first
+// k-steps are in flight while the epilogue of this one pools.
+//
+// Pooled epilogue without recomputation: after bias + Relu every conv output is >= +0, so its f32 bit
+// pattern orders like the value and the 3x3 max is an LDS ds_max_u32 into the pooled cell (exact, any
+// order; the ring starts at +0 = max(-FLT_MAX, values >= 0), the reference's start value,
+// max_pool_op.rs:337).  A quad (4 columns 4qx..4qx+3 of conv row oy) contributes
+//   max(v0, v1, v2) -> pooled column 2qx, max(v2, v3) -> 2qx + 1, v0 -> 2qx - 1,
+// to pooled row oy / 2 and, for an even oy, also oy / 2 - 1.  After each step the block barrier
+// publishes the maxima and the pooled rows whose three conv rows are done are stored and their ring
+// slot cleared.  Every pooled output is the max of the same nine values as in the unfused graph, and
+// each conv output is the same k-ordered MFMA chain + bias as conv_gemm_kernel's: bit-identical.
+#include <hip/hip_runtime.h>
+
+#include "ore_kernels.h"
+
+namespace ore {
+
+typedef float cp_floatx4 __attribute__((ext_vector_type(4)));
+typedef float cp_floatx3 __attribute__((ext_vector_type(3)));
+
+// pooled rows held in LDS (nring slots, pooled row py in slot py % nring): enough that the rows live
+// during a step never share a slot AND a slot cleared after a step is not touched by the next one (no
+// barrier separates the two).  Two consecutive steps of S quads span G2 = (qrow + 2 S - 2) / qrow conv
+// rows at most; nring = (G2 + 4) / 2 covers both, checked by simulation over widths 6..229 and heights
+// 5..229 for S = 64 and 128 (4 / 7 slots for a 28-quad row).
+static int cp_nring(int qrow, int S) { return ((qrow + 2 * S - 2) / qrow + 4) / 2; }
+
+template <int MF>
+__device__ __forceinline__ void cp_load_a(__amdgpu_buffer_rsrc_t r, int voff, int soff, float (&a)[MF]) {
+  if constexpr (MF == 6) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const cp_floatx4 v = __builtin_bit_cast(cp_floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+    const f2 w = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, voff + 16, soff, 0));
+    a[0] = v[0]; a[1] = v[1]; a[2] = v[2]; a[3] = v[3]; a[4] = w[0]; a[5] = w[1];
+  } else if constexpr (MF == 4) {
+    const cp_floatx4 v = __builtin_bit_cast(cp_floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+    a[0] = v[0]; a[1] = v[1]; a[2] = v[2]; a[3] = v[3];
+  } else if constexpr (MF == 3) {
+    const cp_floatx3 v = __builtin_bit_cast(cp_floatx3, __builtin_amdgcn_raw_buffer_load_b96(r, voff, soff, 0));
+    a[0] = v[0]; a[1] = v[1]; a[2] = v[2];
+  } else {
+    static_assert(MF == 2, "MF");
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 v = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+    a[0] = v[0]; a[1] = v[1];
+  }
+}
+
+// MF: 16-channel fragments per block (every wave computes all 16 MF channels of its 16 quads);
+// D: k-steps in flight; NW: waves per block.  qrow = quads per conv row, nsteps = 16 NW-quad steps per
+// image.
+template <int MF, int D, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvParams p, int qrow, int nsteps, int nring) {
+  extern __shared__ unsigned cp_lds[];  // [nring][16 MF][Wp] pooled maxima (f32 bits)
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lk = lane >> 4, lj = lane & 15;
+  // XCD-aware bijective remap: the m tiles of one image (same input rows) share an XCD's L2
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
+  const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
+  const int img = wgid / p.mtiles, mt = wgid - img * p.mtiles;
+  const int m0 = mt * (16 * MF);
+  const int Wp = p.ep_Wo, Hp = p.ep_Ho;
+  constexpr int CH = 16 * MF;
+  const int slot = CH * Wp;
+
+  for (int i = tid; i < nring * slot; i += 64 * NW) cp_lds[i] = 0u;
+
+  const int nq = p.Ho * qrow;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
+  const int kp = (p.K + 31) & ~31;
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0, kp * p.Mp * 4, 0x00020000);
+  const int aoff = (lk * p.Mp + m0 + MF * lj) * 4;  // bytes; + 16 t Mp per k-step
+  const int astep = 16 * p.Mp;
+  const int nks = (p.K + 3) >> 2;
+  const int ximg = img * (int)p.x_nstride;
+
+  // bias of this lane's channels m0 + MF (4 lk + e) + f
+  float bias[MF][4];
+#pragma unroll
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + MF * (4 * lk + e) + f;
+      bias[f][e] = (p.bias && m < p.M) ? p.bias[m] : 0.0f;
+    }
+
+  // loader: step ls (wave-uniform), k-step lt, this lane's quad base and tap (c, r, s) of k = 4 lt + lk
+  int ls = 0, lt = 0;
+  int lc = 0, lr = 0, lsx = lk, loff = lk;
+  auto quad_base = [&](int st) -> int {
+    int qd = st * (16 * NW) + wave * 16 + lj;
+    if (qd >= nq) qd = nq - 1;  // surplus lanes of the last step re-read a valid quad (not pooled)
+    const int oy = qd / qrow, qx = qd - oy * qrow;
+    return ximg + 2 * oy * p.W + 8 * qx;  // input (2 oy, 2 (4 qx))
+  };
+  int lbase = quad_base(0);
+
+  cp_floatx4 acc[MF][4];
+#pragma unroll
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[f][q] = cp_floatx4{0.f, 0.f, 0.f, 0.f};
+  float ra[D][MF];
+  cp_floatx4 rb0[D];
+  cp_floatx3 rb1[D];
+
+#ifndef ORE_EXP_CP_ONELOAD
+#define CP_LOAD_B1(SLOT) \
+  rb1[SLOT] = __builtin_bit_cast(cp_floatx3, __builtin_amdgcn_raw_buffer_load_b96(xr, o_ + 16, 0, 0));
+#else  // timing experiment only (tools/build_exp.sh): one 16-B operand load per k-step
+#define CP_LOAD_B1(SLOT) rb1[SLOT] = cp_floatx3{rb0[SLOT][1], rb0[SLOT][2], rb0[SLOT][3]};
+#endif
+#define CP_LOAD(SLOT)                                                                                  \
+  {                                                                                                    \
+    cp_load_a<MF>(wr, aoff, lt * astep, ra[SLOT]);                                                     \
+    const int o_ = lc < p.C ? (lbase + loff) * 4 : 0x7ff00000; /* k >= K: past the buffer -> 0 */      \
+    rb0[SLOT] = __builtin_bit_cast(cp_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, o_, 0, 0));   \
+    CP_LOAD_B1(SLOT)                                                                                   \
+    lsx += 4; loff += 4;                                                                               \
+    if (lsx >= p.kw) {                                                                                 \
+      lsx -= p.kw; loff += p.W - p.kw; ++lr;                                                           \
+      if (lr >= p.kh) { lr = 0; loff += p.x_ps - p.kh * p.W; ++lc; }                                   \
+    }                                                                                                  \
+    if (++lt == nks) {                                                                                 \
+      lt = 0; lc = 0; lr = 0; lsx = lk; loff = lk;                                                     \
+      if (++ls < nsteps) lbase = quad_base(ls);                                                        \
+    }                                                                                                  \
+  }
+#define CP_MFMA(SLOT)                                                                                  \
+  __builtin_amdgcn_s_setprio(1);                                                                       \
+  _Pragma("unroll") for (int f = 0; f < MF; ++f) {                                                     \
+    acc[f][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb0[SLOT][0], acc[f][0], 0, 0, 0);   \
+    acc[f][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb0[SLOT][2], acc[f][1], 0, 0, 0);   \
+    acc[f][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb1[SLOT][0], acc[f][2], 0, 0, 0);   \
+    acc[f][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb1[SLOT][2], acc[f][3], 0, 0, 0);   \
+  }                                                                                                    \
+  __builtin_amdgcn_s_setprio(0);
+
+  __syncthreads();  // the ring is zero before the first ds_max
+  const int total = nsteps * nks;
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (d < total) CP_LOAD(d);
+  int ct = 0, cs = 0, py_next = 0;  // consumer k-step / step, first pooled row not yet stored
+  for (int g0 = 0; g0 < total; g0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (g0 + d < total) {
+        CP_MFMA(d);
+        __builtin_amdgcn_sched_barrier(0);
+        if (g0 + d + D < total) CP_LOAD(d);
+        __builtin_amdgcn_sched_barrier(0);
+        if (++ct == nks) {
+          ct = 0;
+          // ---- epilogue of step cs: bias + Relu, 3x3 maxima into the LDS ring ----
+          int qd = cs * (16 * NW) + wave * 16 + lj;
+          const bool qv = qd < nq;
+          if (!qv) qd = nq - 1;
+          const int oy = qd / qrow, qx = qd - oy * qrow;
+          const int pya = oy >> 1;                                 // top (even oy) / middle (odd oy) row
+          const int pyb = ((oy & 1) == 0 && oy >= 2) ? pya - 1 : -1;  // bottom row (even oy)
+          const int px0 = 2 * qx;
+          const bool oka = qv && pya < Hp, okb = qv && pyb >= 0 && pyb < Hp;
+          const int sa = (pya % nring) * slot, sb = (pyb < 0 ? 0 : pyb % nring) * slot;
+#pragma unroll
+          for (int f = 0; f < MF; ++f)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int cl = MF * (4 * lk + e) + f;
+              float v[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const float t = acc[f][q][e] + bias[f][e];
+                v[q] = t > 0.0f ? t : 0.0f;  // Relu, canonical +0
+              }
+              const unsigned c0 = __float_as_uint(fmaxf(fmaxf(v[0], v[1]), v[2]));
+              const unsigned c1 = __float_as_uint(fmaxf(v[2], v[3]));
+              const unsigned c2 = __float_as_uint(v[0]);
+#ifdef ORE_EXP_CP_NOEPI  // timing experiment only: no pooled maxima
+              if (c0 == 0x7f7f7f7fu && c1 == c2) p.y[cl] = 0.0f;
+              continue;
+#endif
+              if (oka) {
+                unsigned* row = cp_lds + sa + cl * Wp;
+                if (px0 < Wp) atomicMax(row + px0, c0);
+                if (px0 + 1 < Wp) atomicMax(row + px0 + 1, c1);
+                if (qx > 0 && px0 - 1 < Wp) atomicMax(row + px0 - 1, c2);
+              }
+              if (okb) {
+                unsigned* row = cp_lds + sb + cl * Wp;
+                if (px0 < Wp) atomicMax(row + px0, c0);
+                if (px0 + 1 < Wp) atomicMax(row + px0 + 1, c1);
+                if (qx > 0 && px0 - 1 < Wp) atomicMax(row + px0 - 1, c2);
+              }
+            }
+#pragma unroll
+          for (int f = 0; f < MF; ++f)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[f][q] = cp_floatx4{0.f, 0.f, 0.f, 0.f};
+          __syncthreads();
+          // ---- store the pooled rows whose conv rows 2py .. 2py + 2 are all done ----
+          const int qend = (cs + 1) * (16 * NW) < nq ? (cs + 1) * (16 * NW) : nq;
+          const int rows_done = qend / qrow;
+          int py_end = qend == nq ? Hp : (rows_done >= 3 ? ((rows_done - 3) >> 1) + 1 : 0);
+          if (py_end > Hp) py_end = Hp;
+          for (int py = py_next; py < py_end; ++py) {
+            unsigned* src = cp_lds + (py % nring) * slot;
+            float* dst = p.y + (long long)img * p.y_nstride + (long long)m0 * p.y_ps + py * Wp;
+            for (int i = tid; i < slot; i += 64 * NW) {
+              const int cl = i / Wp, px = i - cl * Wp;
+              if (m0 + cl < p.M) dst[cl * p.y_ps + px] = __uint_as_float(src[i]);
+              src[i] = 0u;
+            }
+          }
+          if (py_end > py_next) py_next = py_end;
+          ++cs;
+        }
+      }
+    }
+  }
+#undef CP_LOAD
+#undef CP_MFMA
+}
+
+// variants (ConvParams::ep_variant): 2 = 48 channels x 64 quads per block (4 waves), 3 = 96 channels
+// x 128 quads (8 waves: twice the MFMAs per operand load, one block per CU)
+static void cp_shape(int variant, int M, int* mf, int* nw) {
+  *mf = variant == 3 ? 6 : (M > 32 ? 3 : 2);
+  *nw = variant == 3 ? 8 : 4;
+}
+static size_t cp_lds_bytes(const ConvParams& p, int variant) {
+  int mf, nw;
+  cp_shape(variant, p.M, &mf, &nw);
+  return size_t(cp_nring((p.Wo + 3) / 4, 16 * nw)) * 16 * mf * p.ep_Wo * 4;
+}
+
+bool conv_pool_stream_eligible(const ConvParams& p, int variant) {
+  if (variant != 2 && variant != 3) return false;
+  if (!p.relu || p.sh != 2 || p.sw != 2 || p.pt != 0 || p.pl != 0 || p.kw < 4 || p.kh < 1 || p.x_bytes <= 0)
+    return false;
+  if (p.ep_pt != 0 || p.ep_pl != 0 || p.ep_Ho < 1 || p.ep_Wo < 1) return false;
+  // every pooled window inside the conv plane (no pool padding), every tap inside the input
+  if (2 * (p.ep_Ho - 1) + 2 > p.Ho - 1 || 2 * (p.ep_Wo - 1) + 2 > p.Wo - 1) return false;
+  if (2 * (p.Ho - 1) + p.kh > p.H || 2 * (p.Wo - 1) + p.kw > p.W) return false;
+  if ((reinterpret_cast<uintptr_t>(p.x) & 3) != 0) return false;
+  if (variant == 3 && p.M < 64) return false;  // mostly idle rows
+  return cp_lds_bytes(p, variant) <= (variant == 3 ? 152 : 64) * 1024;
+}
+
+template <int MF, int D, int NW>
+static void launch_cp(const ConvParams& p0, size_t lds, hipStream_t s) {
+  ConvParams p = p0;
+  p.mtiles = (p.M + 16 * MF - 1) / (16 * MF);
+  const int qrow = (p.Wo + 3) / 4;
+  const int nsteps = (p.Ho * qrow + 16 * NW - 1) / (16 * NW);
+  const int nring = cp_nring(qrow, 16 * NW);
+  if (lds > 64 * 1024) {  // above the default dynamic-LDS limit (once per process and instantiation)
+    static bool raised = false;
+    if (!raised) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pool_stream_kernel<MF, D, NW>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      raised = true;
+    }
+  }
+  hipLaunchKernelGGL((conv_pool_stream_kernel<MF, D, NW>), dim3((unsigned)(p.N * p.mtiles)), dim3(64 * NW), lds, s,
+                     p, qrow, nsteps, nring);
+}
+
+#ifndef ORE_CP_D
+#define ORE_CP_D 4  // k-steps in flight (build knob)
+#endif
+void launch_conv_pool_stream(const ConvParams& p, int variant, hipStream_t s) {
+  int mf, nw;
+  cp_shape(variant, p.M, &mf, &nw);
+  const size_t lds = cp_lds_bytes(p, variant);
+  if (variant == 3)
+    launch_cp<6, ORE_CP_D, 8>(p, lds, s);
+  else if (mf == 3)
+    launch_cp<3, ORE_CP_D, 4>(p, lds, s);
+  else
+    launch_cp<2, ORE_CP_D, 4>(p, lds, s);
+}
+
+}  // namespace ore

@@ -42,6 +42,7 @@ struct ConvParams {
   // output [..][ep_Ho][ep_Wo] (plane stride y_ps), pool pads ep_pt / ep_pl; a block's N tile is a
   // 13 x 19 patch of conv outputs feeding a 6 x 9 tile of pooled outputs, ep_tr x ep_tc tiles per image
   int ep_pt, ep_pl, ep_Ho, ep_Wo, ep_tr, ep_tc;
+  int ep_variant;      // pooled-conv kernel (launch_conv_epool): 0 auto, 1 patch, 2 / 3 row walk
 };
 
 // Per-layer kernel choice and weight layout (see plan_conv in ore_conv.hip).
@@ -54,6 +55,7 @@ struct ConvPlan {
   int wr, ww, wq;      // window rows, columns, loads per lane per row
   int Mp, krows;       // packed weights are krows x Mp floats
   size_t lds;          // dynamic LDS bytes of the window kernel
+  int epv = 0;         // pooled-epilogue steps: ConvParams::ep_variant (ore_model_autotune)
 };
 
 struct PoolParams {
@@ -153,6 +155,15 @@ void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, 
 void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s);
 // Conv (+ Relu) with the following MaxPool in its epilogue (ConvParams ep_* set; f32)
 void launch_conv_epool(const ConvParams& p, hipStream_t s);
+// Stride-2 Conv + Relu + 3x3 / stride-2 MaxPool walking the conv plane row-major with the pooled rows
+// in an LDS ring (ore_conv_pool.hip; conv1 + pool1): launch_conv_epool takes it when eligible
+// (ORE_CONV_POOL_STREAM=0 keeps conv_gemm_kernel's patch epilogue)
+// variants (ConvParams::ep_variant): 1 = the patch kernel, 2 = walk 48 channels x 64 quads per block,
+// 3 = walk 96 channels x 128 quads; 0 = the best eligible of 3, 2, 1.  ORE_CONV_POOL_STREAM=0/1/2
+// forces 1/2/3 (tests).  launch_conv_epool leaves last_conv_tile = EPOOL_TILE_BASE + variant run.
+constexpr int EPOOL_TILE_BASE = 21;
+bool conv_pool_stream_eligible(const ConvParams& p, int variant);
+void launch_conv_pool_stream(const ConvParams& p, int variant, hipStream_t s);
 constexpr int CONV_EPOOL_BN = 256;  // N tile of the pooled-epilogue kernel
 constexpr int EPOOL_TILE_PR = 6, EPOOL_TILE_PC = 9;  // pooled outputs per block (13 x 19 conv patch)
 // LDS-free, barrier-free variant (ore_conv_direct.hip): tiles 4-7 (needs p.x_bytes > 0)

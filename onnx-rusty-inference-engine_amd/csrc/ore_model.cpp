@@ -1298,7 +1298,30 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
   // every output is the same k-ordered MFMA chain)
   for (size_t k = 0; k < m->exec_steps.size() && !st; ++k) {
     Step& s = m->steps[m->exec_steps[k]];
-    if (s.kind != S_CONV || s.plan.window || s.epool) {  // the pooled epilogue has one tile shape
+    if (s.kind == S_CONV && s.epool && !s.plan.f16) {  // f32 pooled conv: patch vs row-walk kernels
+      int best = 0;
+      float best_ms = 1e30f;
+      for (int v = 1; v <= 3 && !st; ++v) {
+        s.plan.epv = v;
+        last_conv_tile = -1;
+        st = launch_step(m, s, n);  // warm-up
+        if (st || last_conv_tile != EPOOL_TILE_BASE + v) continue;  // not eligible here
+        if (hipEventRecord(e0, ctx->stream) != hipSuccess) { st = set_error(ctx, ORE_ERR_HIP, "event record"); break; }
+        for (int r = 0; r < reps && !st; ++r) st = launch_step(m, s, n);
+        float ms = 0.f;
+        if (st || hipEventRecord(e1, ctx->stream) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+            hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
+          if (!st) st = set_error(ctx, ORE_ERR_HIP, "autotune timing failed");
+          break;
+        }
+        if (ms < best_ms) { best_ms = ms; best = v; }
+      }
+      s.plan.epv = best;
+      m->base_steps[m->exec_steps[k]].plan.epv = best;
+      if (!st) st = launch_step(m, s, n);
+      continue;
+    }
+    if (s.kind != S_CONV || s.plan.window || s.epool) {  // f16 pooled epilogue: one tile shape
       st = launch_step(m, s, n);
       continue;
     }
@@ -1345,6 +1368,7 @@ int32_t ore_model_step_tile(ore_model* m, int32_t i) {
   if (!m || i < 0 || size_t(i) >= m->exec_steps.size()) return -1;
   const Step& s = m->steps[m->exec_steps[i]];
   if (s.kind == S_FIRE) return CONV_TILES_F32;  // "fire": the fused fire kernel (ore.Model.TILE_NAMES)
+  if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.plan.epv > 0) return EPOOL_TILE_BASE + s.plan.epv;
   return (s.kind == S_CONV || s.kind == S_MATMUL) ? s.plan.cfg : -1;
 }
 

@@ -276,7 +276,8 @@ class Model:
                   "direct 128x128", "direct 96x128", "direct 64x128", "direct 128x64",
                   "ws 128x128", "ws 96x128", "ws 64x128", "ws 32x256",
                   "stream 64x128", "stream 32x256", "stream 16x256", "stream 48x128", "stream 64x64",
-                  "stream 128x64", "stream 64x64 d8", "stream 32x128", "stream 128x64 d2", "fire"]
+                  "stream 128x64", "stream 64x64 d8", "stream 32x128", "stream 128x64 d2", "fire",
+                  "epool patch", "epool walk48", "epool walk96"]
 
     def tiles(self):
         """Block tile per exec step (-1 for non-conv steps); names in TILE_NAMES."""

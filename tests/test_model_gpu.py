@@ -329,6 +329,45 @@ def test_conv_pool_fusion_bit_identical(gpu_ctx, case, precision):
     np.testing.assert_allclose(vals[0], ref, rtol=tol if precision == "f16" else 1e-5, atol=tol)
 
 
+@pytest.mark.parametrize("case", [
+    # C, H, M, k: stride-2 'valid' conv + Relu + 3x3 / stride-2 pool (the row-walking kernel's family)
+    (3, 45, 96, 7),    # conv1 shape family: Ho 20, 5 quads per row, two 48-channel tiles
+    (3, 64, 96, 7),    # Ho 29: a 64-quad step spans a row boundary mid-row
+    (3, 31, 40, 5),    # M = 40: one 48-channel tile, channels 40..47 masked
+    (2, 50, 100, 4),   # kw = 4 (one tap carry per k-step), M = 100: a 4-channel last tile
+    (4, 23, 20, 7),    # M = 20: 32-channel tiles (MF = 2), Ho 9 -> a single step per image
+    (3, 113, 64, 7),   # Ho 54 (even), 14 quads per row, pooled 26 x 26
+])
+def test_conv_pool_walk_bit_identical(gpu_ctx, case, monkeypatch):
+    """The row-walking conv + pool kernels (ore_conv_pool.hip, LDS-ring pooled epilogue with ds_max on
+    the f32 bits; ORE_CONV_POOL_STREAM=1: 48 channels x 64 quads per block, =2: 96 x 128) equal the
+    patch-epilogue kernel (=0) and the separate conv + Relu + MaxPool kernels bit for bit, and the
+    oracle within the conv tolerance."""
+    import ore
+    C, H, M, k = case
+    rng = np.random.default_rng(sum(case))
+    w = (rng.standard_normal((M, C, k, k)) * 0.3).astype(np.float32)
+    b = rng.uniform(-0.5, 0.5, M).astype(np.float32)
+    x = rng.standard_normal((3, C, H, H)).astype(np.float32)
+    mb = _conv_pool_model((1, C, H, H), w, b, [0] * 4, [2, 2], True, [3, 3], [2, 2], [0, 0, 0, 0])
+    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "100")
+    vals = []
+    for walk, fusion in (("1", ore.FUSE_ALL), ("0", ore.FUSE_ALL), ("2", ore.FUSE_ALL),
+                         ("1", ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
+        monkeypatch.setenv("ORE_CONV_POOL_STREAM", walk)
+        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion(fusion | ore.KEEP_VALUES)
+        _np(m.run(_t(x)))
+        vals.append(m.read_value("p"))
+        m.close()
+    for v in vals[1:]:
+        np.testing.assert_array_equal(vals[0], v)
+    import oracle
+    ref = oracle.maxpool2d(oracle.relu(oracle.conv2d(x, w, b, pads=[0] * 4, strides=(2, 2))), (3, 3), (2, 2),
+                           auto_pad="NOTSET", pads=[0, 0, 0, 0])
+    np.testing.assert_allclose(vals[0], ref, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("hw", [64, 224])
 @pytest.mark.parametrize("precision", ["f32", "f16"])
 def test_squeezenet_conv_pool_fusion(gpu_ctx, hw, precision):
