@@ -181,6 +181,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
           const int pya = oy >> 1;                                 // top (even oy) / middle (odd oy) row
           const int pyb = ((oy & 1) == 0 && oy >= 2) ? pya - 1 : -1;  // bottom row (even oy)
           const int px0 = 2 * qx;
+          // right: lane lj + 1 holds quad qd + 1 of this conv row (its column 4qx + 4 is folded into c1);
+          // left: column 4qx still has to reach pooled column 2qx - 1 itself (no left lane folded it)
+          const bool right = lj < 15 && qx < qrow - 1;
+          const bool left = qx > 0 && lj == 0;
           const bool oka = qv && pya < Hp, okb = qv && pyb >= 0 && pyb < Hp;
           const int sa = (pya % nring) * slot, sb = (pyb < 0 ? 0 : pyb % nring) * slot;
 #pragma unroll
@@ -195,8 +199,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
                 v[q] = t > 0.0f ? t : 0.0f;  // Relu, canonical +0
               }
               const unsigned c0 = __float_as_uint(fmaxf(fmaxf(v[0], v[1]), v[2]));
-              const unsigned c1 = __float_as_uint(fmaxf(v[2], v[3]));
               const unsigned c2 = __float_as_uint(v[0]);
+              // pooled column 2qx + 1 also takes the right neighbour quad's first column: lane lj + 1
+              // (DPP row_shl:1 within the 16-lane row) when that quad continues this conv row
+              const unsigned nb = (unsigned)__builtin_amdgcn_update_dpp((int)c2, (int)c2, 0x101, 0xf, 0xf, false);
+              const unsigned c1 = __float_as_uint(fmaxf(v[2], v[3])) > nb || !right ? __float_as_uint(fmaxf(v[2], v[3]))
+                                                                                  : nb;
 #ifdef ORE_EXP_CP_NOEPI  // timing experiment only: no pooled maxima
               if (c0 == 0x7f7f7f7fu && c1 == c2) p.y[cl] = 0.0f;
               continue;
@@ -205,13 +213,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
                 unsigned* row = cp_lds + sa + cl * Wp;
                 if (px0 < Wp) atomicMax(row + px0, c0);
                 if (px0 + 1 < Wp) atomicMax(row + px0 + 1, c1);
-                if (qx > 0 && px0 - 1 < Wp) atomicMax(row + px0 - 1, c2);
+                if (left && px0 - 1 < Wp) atomicMax(row + px0 - 1, c2);
               }
               if (okb) {
                 unsigned* row = cp_lds + sb + cl * Wp;
                 if (px0 < Wp) atomicMax(row + px0, c0);
                 if (px0 + 1 < Wp) atomicMax(row + px0 + 1, c1);
-                if (qx > 0 && px0 - 1 < Wp) atomicMax(row + px0 - 1, c2);
+                if (left && px0 - 1 < Wp) atomicMax(row + px0 - 1, c2);
               }
             }
 #pragma unroll
@@ -227,11 +235,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
           for (int py = py_next; py < py_end; ++py) {
             unsigned* src = cp_lds + (py % nring) * slot;
             float* dst = p.y + (long long)img * p.y_nstride + (long long)m0 * p.y_ps + py * Wp;
-            for (int i = tid; i < slot; i += 64 * NW) {
-              const int cl = i / Wp, px = i - cl * Wp;
-              if (m0 + cl < p.M) dst[cl * p.y_ps + px] = __uint_as_float(src[i]);
-              src[i] = 0u;
-            }
+            // lane -> pooled column, wave -> channel (a 216-B run per channel row; no division)
+            for (int px = lane; px < Wp; px += 64)
+              for (int cl = wave; cl < CH; cl += NW) {
+                if (m0 + cl < p.M) dst[cl * p.y_ps + px] = __uint_as_float(src[cl * Wp + px]);
+                src[cl * Wp + px] = 0u;
+              }
           }
           if (py_end > py_next) py_next = py_end;
           ++cs;
