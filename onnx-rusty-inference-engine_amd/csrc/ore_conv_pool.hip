@@ -226,7 +226,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
           for (int f = 0; f < MF; ++f)
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[f][q] = cp_floatx4{0.f, 0.f, 0.f, 0.f};
+#ifndef ORE_EXP_CP_LGKMBAR
           __syncthreads();
+#else  // experiment: publish the LDS maxima only (the next step's operand loads stay in flight)
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
           // ---- store the pooled rows whose conv rows 2py .. 2py + 2 are all done ----
           const int qend = (cs + 1) * (16 * NW) < nq ? (cs + 1) * (16 * NW) : nq;
           const int rows_done = qend / qrow;
