@@ -220,7 +220,8 @@ def main():
             achieved = conv["flops"] / (conv["ms"] * 1e-3) / 1e12
             peak = PEAK_F16_MFMA_TFLOPS if f16 else PEAK_F32_MFMA_TFLOPS
             kname = ("conv_f16_kernel (implicit-GEMM MFMA 32x32x16 f16, f32 accumulate" if f16 else
-                     "Conv class: conv_stream_kernel (LDS-free implicit GEMM, MFMA 16x16x4 f32) + conv_gemm_kernel "
+                     "Conv class: conv_stream_kernel (LDS-free implicit GEMM, MFMA 16x16x4 f32), fire_kernel (fire "
+                     "module + next squeeze), conv_pool_stream_kernel (conv1 + pool1 row walk) and conv_gemm_kernel "
                      "(LDS-staged, MFMA 32x32x2 f32) per the autotuned tile") + f", {conv['launches']} launches/step)"
             # HBM bytes per conv launch from the PMC passes of tools/pmc.sh (FETCH_SIZE x2 +
             # WRITE_SIZE, separate --pmc runs; counters cannot be read inside this timed run)

@@ -231,7 +231,10 @@ def test_autotune_keeps_results(gpu_ctx, precision):
     tiles1 = m.tiles()
     assert len(tiles1) == len(tiles0) and sum(t >= 0 for t in tiles1) == 26
     m.set_fusion(0)  # the choice survives re-planning
-    assert [t for t in m.tiles() if t >= 0] == [t for t in tiles1 if t >= 0]
+    a, b = [t for t in tiles1 if t >= 0], [t for t in m.tiles() if t >= 0]
+    if a[0] >= ore.Model.TILE_NAMES.index("epool patch"):  # conv1 + pool1 fused: its kernel choice (patch vs
+        a, b = a[1:], b[1:]                                # row walk) has no unfused counterpart
+    assert a == b
     np.testing.assert_array_equal(_np(m.run(x)), before)
     m.close()
 
