@@ -62,10 +62,18 @@ __device__ __forceinline__ void cp_load_a(__amdgpu_buffer_rsrc_t r, int voff, in
   }
 }
 
+// operand modes: CP_S2 = stride-2 'valid' conv (kw >= 4; conv1), CP_1X1 = 1x1 stride 1, CP_T3 = 3x3
+// stride 1 'same' (pads <= 1; taps outside the image zeroed per element from a per-pixel tap mask, as
+// conv_stream_kernel's STAPS mode) -- the last two are SqueezeNet's expand convs ahead of pool3 / pool5
+enum { CP_S2 = 0, CP_1X1 = 1, CP_T3 = 2 };
+#ifndef ORE_CP_D
+#define ORE_CP_D 4  // k-steps in flight (build knob)
+#endif
+
 // MF: 16-channel fragments per block (every wave computes all 16 MF channels of its 16 quads);
 // D: k-steps in flight; NW: waves per block.  qrow = quads per conv row, nsteps = 16 NW-quad steps per
 // image.
-template <int MF, int D, int NW>
+template <int MF, int D, int NW, int MODE>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvParams p, int qrow, int nsteps, int nring) {
   extern __shared__ unsigned cp_lds[];  // [nring][16 MF][Wp] pooled maxima (f32 bits)
   const int tid = threadIdx.x;
@@ -85,8 +93,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
   for (int i = tid; i < nring * slot; i += 64 * NW) cp_lds[i] = 0u;
 
   const int nq = p.Ho * qrow;
+  // CP_T3: the resource starts x_lead bytes before x so that no tap offset is negative (a negative
+  // offset would zero the whole 16-B access, valid elements included); those bytes are masked taps
+  const int xlead = MODE == CP_T3 ? p.x_lead : 0;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
+      const_cast<char*>(reinterpret_cast<const char*>(p.x) - xlead), (short)0, (int)p.x_bytes + xlead, 0x00020000);
   const int kp = (p.K + 31) & ~31;
   const __amdgpu_buffer_rsrc_t wr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0, kp * p.Mp * 4, 0x00020000);
@@ -107,12 +118,30 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
 
   // loader: step ls (wave-uniform), k-step lt, this lane's quad base and tap (c, r, s) of k = 4 lt + lk
   int ls = 0, lt = 0;
-  int lc = 0, lr = 0, lsx = lk, loff = lk;
+  // CP_S2: tap (lc, lr, lsx), offset loff; CP_1X1: channel lc, offset loff = lc x_ps; CP_T3: tap
+  // tt = 3 r + s of channel lc, channel offset loff = lc x_ps
+  int lc = MODE == CP_1X1 ? lk : 0, lr = 0, lsx = lk, loff = MODE == CP_S2 ? lk : MODE == CP_1X1 ? lk * p.x_ps : 0;
+  int tt = lk;
+  unsigned tmask[4] = {0u, 0u, 0u, 0u};  // CP_T3: bit 3 r + s = tap (r, s) of pixel q inside the image
   auto quad_base = [&](int st) -> int {
     int qd = st * (16 * NW) + wave * 16 + lj;
     if (qd >= nq) qd = nq - 1;  // surplus lanes of the last step re-read a valid quad (not pooled)
     const int oy = qd / qrow, qx = qd - oy * qrow;
-    return ximg + 2 * oy * p.W + 8 * qx;  // input (2 oy, 2 (4 qx))
+    if constexpr (MODE == CP_S2) return ximg + 2 * oy * p.W + 8 * qx;  // input (2 oy, 2 (4 qx))
+    if constexpr (MODE == CP_1X1) return ximg + oy * p.W + 4 * qx;
+    // CP_T3: element of tap (0, 0) relative to the resource start
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ow = 4 * qx + q;
+      unsigned cm = 0, m = 0;
+#pragma unroll
+      for (int c3 = 0; c3 < 3; ++c3) cm |= ((unsigned)(ow - p.pl + c3) < (unsigned)p.W ? 1u : 0u) << c3;
+#pragma unroll
+      for (int r3 = 0; r3 < 3; ++r3)
+        if ((unsigned)(oy - p.pt + r3) < (unsigned)p.H) m |= cm << (3 * r3);
+      tmask[q] = m;
+    }
+    return (xlead >> 2) + ximg + (oy - p.pt) * p.W + 4 * qx - p.pl;
   };
   int lbase = quad_base(0);
 
@@ -123,7 +152,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
     for (int q = 0; q < 4; ++q) acc[f][q] = cp_floatx4{0.f, 0.f, 0.f, 0.f};
   float ra[D][MF];
   cp_floatx4 rb0[D];
-  cp_floatx3 rb1[D];
+  cp_floatx3 rb1[MODE == CP_S2 ? D : 1];
+  int rt[MODE == CP_T3 ? D : 1];  // CP_T3: the tap of each ring slot's k (for its zero mask)
 
 #ifndef ORE_EXP_CP_ONELOAD
 #define CP_LOAD_B1(SLOT) \
@@ -134,26 +164,57 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
 #define CP_LOAD(SLOT)                                                                                  \
   {                                                                                                    \
     cp_load_a<MF>(wr, aoff, lt * astep, ra[SLOT]);                                                     \
-    const int o_ = lc < p.C ? (lbase + loff) * 4 : 0x7ff00000; /* k >= K: past the buffer -> 0 */      \
-    rb0[SLOT] = __builtin_bit_cast(cp_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, o_, 0, 0));   \
-    CP_LOAD_B1(SLOT)                                                                                   \
-    lsx += 4; loff += 4;                                                                               \
-    if (lsx >= p.kw) {                                                                                 \
-      lsx -= p.kw; loff += p.W - p.kw; ++lr;                                                           \
-      if (lr >= p.kh) { lr = 0; loff += p.x_ps - p.kh * p.W; ++lc; }                                   \
+    if constexpr (MODE == CP_S2) {                                                                     \
+      const int o_ = lc < p.C ? (lbase + loff) * 4 : 0x7ff00000; /* k >= K: past the buffer -> 0 */    \
+      rb0[SLOT] = __builtin_bit_cast(cp_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, o_, 0, 0)); \
+      CP_LOAD_B1(SLOT)                                                                                 \
+      lsx += 4; loff += 4;                                                                             \
+      if (lsx >= p.kw) {                                                                               \
+        lsx -= p.kw; loff += p.W - p.kw; ++lr;                                                         \
+        if (lr >= p.kh) { lr = 0; loff += p.x_ps - p.kh * p.W; ++lc; }                                 \
+      }                                                                                                \
+    } else if constexpr (MODE == CP_1X1) {                                                             \
+      const int o_ = lc < p.C ? (lbase + loff) * 4 : 0x7ff00000;                                       \
+      rb0[SLOT] = __builtin_bit_cast(cp_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, o_, 0, 0)); \
+      lc += 4; loff += 4 * p.x_ps;                                                                     \
+    } else {                                                                                           \
+      /* tt / 3 for tt < 9 by a 24-bit multiply (as conv_stream_kernel) */                             \
+      const int r_ = (int)(__umul24((unsigned)tt, 11u) >> 5);                                          \
+      const int o_ = lc < p.C ? (lbase + loff + (int)__umul24((unsigned)r_, (unsigned)(p.W - 3)) + tt) * 4 \
+                              : 0x7ff00000;                                                            \
+      rb0[SLOT] = __builtin_bit_cast(cp_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, o_, 0, 0)); \
+      rt[SLOT] = tt;                                                                                   \
+      tt += 4;                                                                                         \
+      if (tt >= 9) { tt -= 9; loff += p.x_ps; ++lc; }                                                  \
     }                                                                                                  \
     if (++lt == nks) {                                                                                 \
-      lt = 0; lc = 0; lr = 0; lsx = lk; loff = lk;                                                     \
+      lt = 0; lr = 0; lsx = lk; tt = lk;                                                               \
+      lc = MODE == CP_1X1 ? lk : 0;                                                                    \
+      loff = MODE == CP_S2 ? lk : MODE == CP_1X1 ? lk * p.x_ps : 0;                                    \
       if (++ls < nsteps) lbase = quad_base(ls);                                                        \
     }                                                                                                  \
   }
 #define CP_MFMA(SLOT)                                                                                  \
+  if constexpr (MODE == CP_T3) { /* zero the taps outside the image (the reference's zero padding) */  \
+    const int4 v_ = __builtin_bit_cast(int4, rb0[SLOT]);                                               \
+    int4 w_;                                                                                           \
+    w_.x = v_.x & __builtin_amdgcn_sbfe((int)tmask[0], rt[SLOT], 1);                                   \
+    w_.y = v_.y & __builtin_amdgcn_sbfe((int)tmask[1], rt[SLOT], 1);                                   \
+    w_.z = v_.z & __builtin_amdgcn_sbfe((int)tmask[2], rt[SLOT], 1);                                   \
+    w_.w = v_.w & __builtin_amdgcn_sbfe((int)tmask[3], rt[SLOT], 1);                                   \
+    rb0[SLOT] = __builtin_bit_cast(cp_floatx4, w_);                                                    \
+  }                                                                                                    \
   __builtin_amdgcn_s_setprio(1);                                                                       \
   _Pragma("unroll") for (int f = 0; f < MF; ++f) {                                                     \
-    acc[f][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb0[SLOT][0], acc[f][0], 0, 0, 0);   \
-    acc[f][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb0[SLOT][2], acc[f][1], 0, 0, 0);   \
-    acc[f][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb1[SLOT][0], acc[f][2], 0, 0, 0);   \
-    acc[f][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb1[SLOT][2], acc[f][3], 0, 0, 0);   \
+    if constexpr (MODE == CP_S2) {                                                                     \
+      acc[f][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb0[SLOT][0], acc[f][0], 0, 0, 0); \
+      acc[f][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb0[SLOT][2], acc[f][1], 0, 0, 0); \
+      acc[f][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb1[SLOT][0], acc[f][2], 0, 0, 0); \
+      acc[f][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb1[SLOT][2], acc[f][3], 0, 0, 0); \
+    } else {                                                                                           \
+      _Pragma("unroll") for (int q = 0; q < 4; ++q)                                                    \
+        acc[f][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb0[SLOT][q], acc[f][q], 0, 0, 0); \
+    }                                                                                                  \
   }                                                                                                    \
   __builtin_amdgcn_s_setprio(0);
 
@@ -196,7 +257,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
 #pragma unroll
               for (int q = 0; q < 4; ++q) {
                 const float t = acc[f][q][e] + bias[f][e];
-                v[q] = t > 0.0f ? t : 0.0f;  // Relu, canonical +0
+                // Relu, canonical +0; columns >= Wo (the quad padding) count as the pool's zero padding
+                v[q] = (t > 0.0f && px0 * 2 + q < p.Wo) ? t : 0.0f;
               }
               const unsigned c0 = __float_as_uint(fmaxf(fmaxf(v[0], v[1]), v[2]));
               const unsigned c2 = __float_as_uint(v[0]);
@@ -257,9 +319,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
 }
 
 // variants (ConvParams::ep_variant): 2 = 48 channels x 64 quads per block (4 waves), 3 = 96 channels
-// x 128 quads (8 waves: twice the MFMAs per operand load, one block per CU)
+// x 128 quads (8 waves: twice the MFMAs per operand load, one block per CU), 4 = 64 channels x 64
+// quads (4 waves)
 static void cp_shape(int variant, int M, int* mf, int* nw) {
-  *mf = variant == 3 ? 6 : (M > 32 ? 3 : 2);
+  *mf = variant == 3 ? 6 : variant == 4 ? 4 : (M > 32 ? 3 : 2);
   *nw = variant == 3 ? 8 : 4;
 }
 static size_t cp_lds_bytes(const ConvParams& p, int variant) {
@@ -267,52 +330,74 @@ static size_t cp_lds_bytes(const ConvParams& p, int variant) {
   cp_shape(variant, p.M, &mf, &nw);
   return size_t(cp_nring((p.Wo + 3) / 4, 16 * nw)) * 16 * mf * p.ep_Wo * 4;
 }
+static int cp_lead(const ConvParams& p) { return ((p.pt * p.W + p.pl) * 4 + 15) & ~15; }
 
-bool conv_pool_stream_eligible(const ConvParams& p, int variant) {
-  if (variant != 2 && variant != 3) return false;
-  if (!p.relu || p.sh != 2 || p.sw != 2 || p.pt != 0 || p.pl != 0 || p.kw < 4 || p.kh < 1 || p.x_bytes <= 0)
-    return false;
-  if (p.ep_pt != 0 || p.ep_pl != 0 || p.ep_Ho < 1 || p.ep_Wo < 1) return false;
-  // every pooled window inside the conv plane (no pool padding), every tap inside the input
-  if (2 * (p.ep_Ho - 1) + 2 > p.Ho - 1 || 2 * (p.ep_Wo - 1) + 2 > p.Wo - 1) return false;
-  if (2 * (p.Ho - 1) + p.kh > p.H || 2 * (p.Wo - 1) + p.kw > p.W) return false;
-  if ((reinterpret_cast<uintptr_t>(p.x) & 3) != 0) return false;
-  if (variant == 3 && p.M < 64) return false;  // mostly idle rows
-  return cp_lds_bytes(p, variant) <= (variant == 3 ? 152 : 64) * 1024;
+// -1: not eligible, else the operand mode
+static int cp_mode(const ConvParams& p) {
+  if (!p.relu || p.x_bytes <= 0 || (reinterpret_cast<uintptr_t>(p.x) & 3) != 0) return -1;
+  // pooled windows start inside the conv plane; a window may reach one row / column past it (the
+  // pool's bottom / right zero padding: neutral after the Relu)
+  if (p.ep_pt != 0 || p.ep_pl != 0 || p.ep_Ho < 1 || p.ep_Wo < 1) return -1;
+  if (2 * (p.ep_Ho - 1) + 2 > p.Ho || 2 * (p.ep_Wo - 1) + 2 > p.Wo) return -1;
+  if (p.sh == 2 && p.sw == 2 && p.pt == 0 && p.pl == 0 && p.kw >= 4 && p.kh >= 1 && 2 * (p.Ho - 1) + p.kh <= p.H &&
+      2 * (p.Wo - 1) + p.kw <= p.W)
+    return CP_S2;
+  if (p.kh == 1 && p.kw == 1 && p.sh == 1 && p.sw == 1 && p.pt == 0 && p.pl == 0 && p.Ho == p.H && p.Wo == p.W)
+    return CP_1X1;
+  if (p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.pt <= 1 && p.pl <= 1 && p.Wo == p.W && p.Ho == p.H &&
+      p.W >= 3 && p.x_guard >= cp_lead(p) && p.x_bytes + cp_lead(p) < (1LL << 31))
+    return CP_T3;
+  return -1;
 }
 
-template <int MF, int D, int NW>
+bool conv_pool_stream_eligible(const ConvParams& p, int variant) {
+  if (variant < 2 || variant > 4 || cp_mode(p) < 0) return false;
+  if (variant == 3 && p.M < 64) return false;  // mostly idle rows
+  if (variant == 4 && p.M < 48) return false;
+  return cp_lds_bytes(p, variant) <= size_t(variant == 3 ? 152 : 78) * 1024;
+}
+
+template <int MF, int D, int NW, int MODE>
 static void launch_cp(const ConvParams& p0, size_t lds, hipStream_t s) {
   ConvParams p = p0;
   p.mtiles = (p.M + 16 * MF - 1) / (16 * MF);
+  p.x_lead = MODE == CP_T3 ? cp_lead(p) : 0;
   const int qrow = (p.Wo + 3) / 4;
   const int nsteps = (p.Ho * qrow + 16 * NW - 1) / (16 * NW);
   const int nring = cp_nring(qrow, 16 * NW);
   if (lds > 64 * 1024) {  // above the default dynamic-LDS limit (once per process and instantiation)
     static bool raised = false;
     if (!raised) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pool_stream_kernel<MF, D, NW>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pool_stream_kernel<MF, D, NW, MODE>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       raised = true;
     }
   }
-  hipLaunchKernelGGL((conv_pool_stream_kernel<MF, D, NW>), dim3((unsigned)(p.N * p.mtiles)), dim3(64 * NW), lds, s,
-                     p, qrow, nsteps, nring);
+  hipLaunchKernelGGL((conv_pool_stream_kernel<MF, D, NW, MODE>), dim3((unsigned)(p.N * p.mtiles)), dim3(64 * NW), lds,
+                     s, p, qrow, nsteps, nring);
 }
 
-#ifndef ORE_CP_D
-#define ORE_CP_D 4  // k-steps in flight (build knob)
-#endif
+template <int MF, int NW>
+static void launch_cp_mode(const ConvParams& p, size_t lds, hipStream_t s) {
+  switch (cp_mode(p)) {
+    case CP_S2: launch_cp<MF, ORE_CP_D, NW, CP_S2>(p, lds, s); break;
+    case CP_1X1: launch_cp<MF, ORE_CP_D, NW, CP_1X1>(p, lds, s); break;
+    default: launch_cp<MF, ORE_CP_D, NW, CP_T3>(p, lds, s); break;
+  }
+}
+
 void launch_conv_pool_stream(const ConvParams& p, int variant, hipStream_t s) {
   int mf, nw;
   cp_shape(variant, p.M, &mf, &nw);
   const size_t lds = cp_lds_bytes(p, variant);
   if (variant == 3)
-    launch_cp<6, ORE_CP_D, 8>(p, lds, s);
+    launch_cp_mode<6, 8>(p, lds, s);
+  else if (variant == 4)
+    launch_cp_mode<4, 4>(p, lds, s);
   else if (mf == 3)
-    launch_cp<3, ORE_CP_D, 4>(p, lds, s);
+    launch_cp_mode<3, 4>(p, lds, s);
   else
-    launch_cp<2, ORE_CP_D, 4>(p, lds, s);
+    launch_cp_mode<2, 4>(p, lds, s);
 }
 
 }  // namespace ore

@@ -371,6 +371,45 @@ def test_conv_pool_walk_bit_identical(gpu_ctx, case, monkeypatch):
     np.testing.assert_allclose(vals[0], ref, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("case", [
+    # C, H, M, k, conv pad, pool pads: stride-1 convs + Relu + 3x3 / stride-2 pool (operand modes 1x1 / 3x3)
+    (32, 54, 128, 1, 0, [0, 0, 1, 1]),   # fire4 expand1x1 -> pool3 (ceil-mode bottom / right pad)
+    (32, 54, 128, 3, 1, [0, 0, 1, 1]),   # fire4 expand3x3 -> pool3
+    (64, 27, 256, 3, 1, [0, 0, 0, 0]),   # fire8 expand3x3 -> pool5
+    (64, 27, 256, 1, 0, [0, 0, 0, 0]),   # fire8 expand1x1 -> pool5
+    (5, 21, 40, 3, 1, [0, 0, 1, 1]),     # odd width (quad padding inside a window), masked channel tail
+    (6, 18, 20, 1, 0, [0, 0, 0, 0]),     # 32-channel tiles
+    (7, 9, 64, 3, 1, [0, 0, 1, 1]),      # 3 quads per row: a step spans many rows
+])
+def test_conv_pool_walk_stride1_bit_identical(gpu_ctx, case, monkeypatch):
+    """The row-walking conv + pool kernel's stride-1 operand modes (1x1; 3x3 'same' with per-element
+    tap masks) for every block shape equal the patch-epilogue kernel and the separate kernels bit for
+    bit, ceil-mode pool pads included."""
+    import ore
+    C, H, M, k, cp, ppads = case
+    rng = np.random.default_rng(C * H + M + k)
+    w = (rng.standard_normal((M, C, k, k)) * 0.3).astype(np.float32)
+    b = rng.uniform(-0.5, 0.5, M).astype(np.float32)
+    x = rng.standard_normal((3, C, H, H)).astype(np.float32)
+    mb = _conv_pool_model((1, C, H, H), w, b, [cp] * 4, [1, 1], True, [3, 3], [2, 2], ppads)
+    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "100")
+    vals = []
+    for walk, fusion in (("0", ore.FUSE_ALL), ("1", ore.FUSE_ALL), ("2", ore.FUSE_ALL), ("3", ore.FUSE_ALL),
+                         ("0", ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
+        monkeypatch.setenv("ORE_CONV_POOL_STREAM", walk)
+        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion(fusion | ore.KEEP_VALUES)
+        _np(m.run(_t(x)))
+        vals.append(m.read_value("p"))
+        m.close()
+    for v in vals[1:]:
+        np.testing.assert_array_equal(vals[0], v)
+    import oracle
+    ref = oracle.maxpool2d(oracle.relu(oracle.conv2d(x, w, b, pads=[cp] * 4, strides=(1, 1))), (3, 3), (2, 2),
+                           auto_pad="NOTSET", pads=ppads)
+    np.testing.assert_allclose(vals[0], ref, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("hw", [64, 224])
 @pytest.mark.parametrize("precision", ["f32", "f16"])
 def test_squeezenet_conv_pool_fusion(gpu_ctx, hw, precision):
