@@ -181,6 +181,14 @@ ore_status ore_model_destroy(ore_model* m);
  * (environment, default 65536: one 64-pixel wave per SIMD), below which the fused launch has too
  * few waves (batch 1 keeps the separate kernels). */
 #define ORE_FUSE_FIRE 64
+/* bit 7 (opt-in, not in ORE_FUSE_ALL): Concat(e1, e3) -> 3x3 / stride-2 MaxPool with e1 / e3 Convs
+ * (+ Relu) read only by the Concat (SqueezeNet's fire4 -> pool3, fire8 -> pool5): each conv's pooled
+ * epilogue (the row-walking kernel, ore_conv_pool.hip) writes its channel slice of the pool output,
+ * so neither the expand outputs nor the Concat reach HBM.  Bit-identical (the pool is per channel;
+ * every pooled value is the max of the same nine values).  f32 models.  Measured slower at batch
+ * 256 (fire8: 694 vs 625 us per step for the expands + pool5): the walker's expand3x3 reaches 93 of
+ * the streaming kernel's 124 TF/s. */
+#define ORE_FUSE_CONCAT_POOL 128
 /* debug: give every value its own storage (no liveness reuse) so any value can be read back */
 #define ORE_KEEP_VALUES 8
 ore_status ore_model_set_fusion(ore_model* m, int32_t flags);

@@ -153,7 +153,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
   float ra[D][MF];
   cp_floatx4 rb0[D];
   cp_floatx3 rb1[MODE == CP_S2 ? D : 1];
-  int rt[MODE == CP_T3 ? D : 1];  // CP_T3: the tap of each ring slot's k (for its zero mask)
+  // CP_T3: each ring slot's zero mask, bit q = pixel q's tap inside the image (taken at load time:
+  // the loader runs D k-steps ahead and moves to the next step's quad -- and masks -- first)
+  int rt[MODE == CP_T3 ? D : 1];
 
 #ifndef ORE_EXP_CP_ONELOAD
 #define CP_LOAD_B1(SLOT) \
@@ -183,7 +185,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
       const int o_ = lc < p.C ? (lbase + loff + (int)__umul24((unsigned)r_, (unsigned)(p.W - 3)) + tt) * 4 \
                               : 0x7ff00000;                                                            \
       rb0[SLOT] = __builtin_bit_cast(cp_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, o_, 0, 0)); \
-      rt[SLOT] = tt;                                                                                   \
+      rt[SLOT] = (int)(((tmask[0] >> tt) & 1u) | (((tmask[1] >> tt) & 1u) << 1) |                      \
+                       (((tmask[2] >> tt) & 1u) << 2) | (((tmask[3] >> tt) & 1u) << 3));                \
       tt += 4;                                                                                         \
       if (tt >= 9) { tt -= 9; loff += p.x_ps; ++lc; }                                                  \
     }                                                                                                  \
@@ -198,10 +201,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
   if constexpr (MODE == CP_T3) { /* zero the taps outside the image (the reference's zero padding) */  \
     const int4 v_ = __builtin_bit_cast(int4, rb0[SLOT]);                                               \
     int4 w_;                                                                                           \
-    w_.x = v_.x & __builtin_amdgcn_sbfe((int)tmask[0], rt[SLOT], 1);                                   \
-    w_.y = v_.y & __builtin_amdgcn_sbfe((int)tmask[1], rt[SLOT], 1);                                   \
-    w_.z = v_.z & __builtin_amdgcn_sbfe((int)tmask[2], rt[SLOT], 1);                                   \
-    w_.w = v_.w & __builtin_amdgcn_sbfe((int)tmask[3], rt[SLOT], 1);                                   \
+    w_.x = v_.x & __builtin_amdgcn_sbfe(rt[SLOT], 0, 1);                                               \
+    w_.y = v_.y & __builtin_amdgcn_sbfe(rt[SLOT], 1, 1);                                               \
+    w_.z = v_.z & __builtin_amdgcn_sbfe(rt[SLOT], 2, 1);                                               \
+    w_.w = v_.w & __builtin_amdgcn_sbfe(rt[SLOT], 3, 1);                                               \
     rb0[SLOT] = __builtin_bit_cast(cp_floatx4, w_);                                                    \
   }                                                                                                    \
   __builtin_amdgcn_s_setprio(1);                                                                       \

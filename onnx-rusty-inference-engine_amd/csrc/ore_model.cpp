@@ -83,6 +83,7 @@ struct Step {
   Window pwin;
   // fused following MaxPool (ORE_FUSE_CONV_POOL): out is the pool's output; pool geometry below
   bool epool = false;
+  mutable int ran_tile = -1;  // pooled conv: the kernel variant its last launch took (EPOOL_TILE_BASE + v)
   int64_t ep_kh = 0, ep_kw = 0, ep_sh = 1, ep_sw = 1;
   Window ep_win;
   // S_FIRE (ORE_FUSE_FIRE): this squeeze conv also computes the fire module feeding it; in0 is the
@@ -108,6 +109,7 @@ struct ore_model {
   int32_t fusion = ORE_FUSE_ALL;
   bool f16 = false;              // ORE_LOAD_F16: f16 conv/pool activations, f32 accumulation
   std::vector<Value> values;
+  size_t n_base_values = 0;      // values of the graph; plan() appends views after them (pooled slices)
   std::map<std::string, int> by_name;
   std::vector<Step> base_steps;  // unfused, one per node
   std::vector<Step> steps;       // after fusion
@@ -499,6 +501,8 @@ bool strided_writer(const Step& s) { return s.kind == S_CONV || s.kind == S_FIRE
 
 ore_status plan(ore_model* m) {
   m->steps = m->base_steps;
+  if (!m->n_base_values) m->n_base_values = m->values.size();
+  m->values.resize(m->n_base_values);  // drop the previous plan's views
   for (auto& v : m->values) {
     v.alias_of = -1; v.alias_ch = 0; v.slice = false; v.ps = 0; v.elided = false; v.arena_off = -1;
     v.nhwc = !v.is_const && v.es == 2 && v.ndim == 4;
@@ -578,6 +582,66 @@ ore_status plan(ore_model* m) {
       producer[pl.out] = pc;
       pl.kind = S_NOP;
       pl.in0 = -1;
+    }
+    count_uses(m, m->steps);
+  }
+  // (1e) Concat(e1, e3) -> 3x3 / stride-2 MaxPool, e1 / e3 Convs (+ Relu) read only by the Concat
+  // (f32; SqueezeNet's fire4 -> pool3 and fire8 -> pool5): each conv's pooled epilogue writes its
+  // channel slice of the pool output (a view appended to the values), so neither the two conv
+  // outputs nor the concat reach HBM.  The MaxPool of a Concat is the Concat of the per-slice
+  // MaxPools (the pool is per channel), so every pooled value is the same max of the same nine
+  // values.  No patch-work bound: the row-walking kernels (ore_conv_pool.hip) compute no conv output
+  // twice, and ore_model_autotune keeps the patch kernel only where it is faster.  Opt-in
+  // (ORE_FUSE_CONCAT_POOL): measured slower than the streaming expands + the chunk-staged pool.
+  if ((m->fusion & ORE_FUSE_CONCAT_POOL) && (m->fusion & ORE_FUSE_CONV_POOL) && (m->fusion & ORE_FUSE_CONCAT) &&
+      !m->f16) {
+    for (size_t i = 0; i < m->steps.size(); ++i) {
+      Step& pl = m->steps[i];
+      if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2) continue;
+      const int cv = pl.in0;
+      const int ci = producer[cv];
+      if (ci < 0 || m->values[cv].uses != 1 || m->values[cv].is_output || m->values[pl.out].is_output) continue;
+      Step& cc = m->steps[ci];
+      if (cc.kind != S_CONCAT || cc.axis != 1 || cc.in0 < 0 || cc.in1 < 0 || cc.in0 == cc.in1) continue;
+      const int pa = producer[cc.in0], pb = producer[cc.in1];
+      if (pa < 0 || pb < 0 || pa == pb) continue;
+      auto ok = [&](const Step& st, int v) {
+        return st.kind == S_CONV && st.relu && !st.pool && !st.epool && !st.plan.window && !st.plan.f16 &&
+               m->values[v].uses == 1 && !m->values[v].is_output && m->values[v].ndim == 4;
+      };
+      if (!ok(m->steps[pa], cc.in0) || !ok(m->steps[pb], cc.in1)) continue;
+      int t1 = 0, t2 = 0;
+      const Step& sa = m->steps[pa];
+      if (epool_tile(sa.win.Ho, sa.win.Wo, pl.kh, pl.kw, pl.sh, pl.sw, pl.win, &t1, &t2) == 0.0) continue;
+      const int pout = pl.out;
+      const int64_t Hp = m->values[pout].dims[2], Wp = m->values[pout].dims[3];
+      const int pes = m->values[pout].es;
+      const std::string pname = m->values[pout].name;
+      int64_t ch0 = 0;
+      for (int half = 0; half < 2; ++half) {
+        const int si = half ? pb : pa, src = half ? cc.in1 : cc.in0;
+        Value v;
+        v.name = pname + (half ? "#slice1" : "#slice0");
+        v.ndim = 4;
+        v.dims[0] = 1; v.dims[1] = m->values[src].dims[1]; v.dims[2] = Hp; v.dims[3] = Wp;
+        v.es = pes;
+        v.alias_of = pout; v.alias_ch = ch0; v.slice = true;
+        ch0 += v.dims[1];
+        m->values.push_back(v);
+        producer.push_back(si);
+        const int vid = int(m->values.size()) - 1;
+        Step& st = m->steps[si];
+        m->values[src].elided = true;
+        st.epool = true;
+        st.out = vid;
+        st.ep_kh = pl.kh; st.ep_kw = pl.kw; st.ep_sh = pl.sh; st.ep_sw = pl.sw; st.ep_win = pl.win;
+        st.bytes_per_img = double(m->values[st.in0].es) * double(st.C * st.H * st.W) +
+                           double(pes) * double(st.M * Hp * Wp);
+      }
+      m->values[cv].elided = true;
+      producer[pout] = pa;
+      cc.kind = S_NOP; cc.in0 = cc.in1 = -1;
+      pl.kind = S_NOP; pl.in0 = -1;
     }
     count_uses(m, m->steps);
   }
@@ -909,10 +973,16 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       if (s.plan.f16)
         return run_conv_f16(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.ktab, s.M, s.kh, s.kw, bias,
                             s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps, s.epool ? &ep : nullptr);
-      if (s.epool)
-        return run_conv_epool(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.ktab, s.M, s.kh, s.kw, bias,
-                              s.win, s.sh, s.sw, s.relu, s.ep_kh, s.ep_kw, s.ep_sh, s.ep_sw, s.ep_win, y.p, y.nstride,
-                              y.ps);
+      if (s.epool) {
+        ctx->mapped_lo = m->arena_alloc;  // the arena and its 4 KiB lead are mapped
+        ctx->mapped_hi = m->arena ? m->arena + m->arena_bytes : nullptr;
+        const ore_status r = run_conv_epool(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.ktab, s.M, s.kh,
+                                            s.kw, bias, s.win, s.sh, s.sw, s.relu, s.ep_kh, s.ep_kw, s.ep_sh, s.ep_sw,
+                                            s.ep_win, y.p, y.nstride, y.ps);
+        ctx->mapped_lo = ctx->mapped_hi = nullptr;
+        s.ran_tile = last_conv_tile;
+        return r;
+      }
       if (s.pool)
         return run_conv_pool(ctx, s.plan, x.p, n, s.C, s.pH, s.pW, x.nstride, x.ps, s.pwin, s.psh, s.psw, s.wp, s.M, bias,
                              s.relu, y.p, y.nstride, y.ps, x.es);
@@ -1147,7 +1217,8 @@ ore_status ore_model_destroy(ore_model* m) {
 
 ore_status ore_model_set_fusion(ore_model* m, int32_t flags) {
   if (!m) return set_error(nullptr, ORE_ERR_INVALID, "null model");
-  m->fusion = flags & (ORE_FUSE_ALL | ORE_FUSE_POOL_CONV | ORE_FUSE_CONV_POOL | ORE_FUSE_FIRE | ORE_KEEP_VALUES);
+  m->fusion = flags & (ORE_FUSE_ALL | ORE_FUSE_POOL_CONV | ORE_FUSE_CONV_POOL | ORE_FUSE_FIRE | ORE_FUSE_CONCAT_POOL |
+                       ORE_KEEP_VALUES);
   return plan(m);
 }
 
@@ -1369,6 +1440,7 @@ int32_t ore_model_step_tile(ore_model* m, int32_t i) {
   const Step& s = m->steps[m->exec_steps[i]];
   if (s.kind == S_FIRE) return CONV_TILES_F32;  // "fire": the fused fire kernel (ore.Model.TILE_NAMES)
   if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.plan.epv > 0) return EPOOL_TILE_BASE + s.plan.epv;
+  if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.ran_tile >= 0) return s.ran_tile;
   return (s.kind == S_CONV || s.kind == S_MATMUL) ? s.plan.cfg : -1;
 }
 

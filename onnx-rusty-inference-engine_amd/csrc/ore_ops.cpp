@@ -262,6 +262,13 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
   p.ep_pt = int(pwin.pt); p.ep_pl = int(pwin.pl); p.ep_Ho = int(pwin.Ho); p.ep_Wo = int(pwin.Wo);
   p.ep_tr = tr; p.ep_tc = tc;
   p.ep_variant = pln.epv;
+  {  // mapped bytes before x (as run_conv): the row-walking 3x3 kernel reads a few of them, masked
+    const char* xc = reinterpret_cast<const char*>(x);
+    int64_t g = int64_t(reinterpret_cast<uintptr_t>(x) & 4095);
+    if (ctx->mapped_lo && xc >= ctx->mapped_lo && xc < ctx->mapped_hi)
+      g = std::max<int64_t>(g, std::min<int64_t>(xc - ctx->mapped_lo, 1 << 20));
+    p.x_guard = int(g);
+  }
   p.Ntot = N * int64_t(p.ep_tr) * p.ep_tc * CONV_EPOOL_BN;
   if (x_ps < H * W || y_ps < pwin.Ho * pwin.Wo) return set_error(ctx, ORE_ERR_INVALID, "plane stride below plane size");
   if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(int64_t(pln.krows) * pln.Mp) ||

@@ -232,9 +232,10 @@ def test_autotune_keeps_results(gpu_ctx, precision):
     assert len(tiles1) == len(tiles0) and sum(t >= 0 for t in tiles1) == 26
     m.set_fusion(0)  # the choice survives re-planning
     a, b = [t for t in tiles1 if t >= 0], [t for t in m.tiles() if t >= 0]
-    if a[0] >= ore.Model.TILE_NAMES.index("epool patch"):  # conv1 + pool1 fused: its kernel choice (patch vs
-        a, b = a[1:], b[1:]                                # row walk) has no unfused counterpart
-    assert a == b
+    # convs with a pooled epilogue (conv1 + pool1, fire4 / fire8 expands + pool3 / pool5): their kernel
+    # choice (patch vs row walk) has no unfused counterpart
+    ep = ore.Model.TILE_NAMES.index("epool patch")
+    assert len(a) == len(b) and [x for x, y in zip(a, b) if x < ep] == [y for x, y in zip(a, b) if x < ep]
     np.testing.assert_array_equal(_np(m.run(x)), before)
     m.close()
 
@@ -272,10 +273,13 @@ def test_model_errors(gpu_ctx):
         ore.Model(gpu_ctx, b"\xff\xff\xff", 1)
 
 
-def _conv_pool_model(x_shape, w, b, conv_pads, conv_strides, relu, pool_k, pool_s, pool_pads):
+def _conv_pool_model(x_shape, w, b, conv_pads, conv_strides, relu, pool_k, pool_s, pool_pads, pre_relu=False):
+    """x [-> Relu] -> Conv [-> Relu] -> MaxPool -> GAP.  pre_relu puts the conv input in the walker's
+    arena (mapped bytes before it, as for every inner layer of a real graph)."""
     from ore import onnx_wire as wr
-    nodes = [wr.encode_node("Conv", ["x", "w", "b"], ["c"], attrs=[wr.encode_attr_ints("pads", conv_pads),
-                                                                   wr.encode_attr_ints("strides", conv_strides)])]
+    nodes = [wr.encode_node("Relu", ["x"], ["xr"])] if pre_relu else []
+    nodes.append(wr.encode_node("Conv", ["xr" if pre_relu else "x", "w", "b"], ["c"], attrs=[
+        wr.encode_attr_ints("pads", conv_pads), wr.encode_attr_ints("strides", conv_strides)]))
     cur = "c"
     if relu:
         nodes.append(wr.encode_node("Relu", ["c"], ["r"]))
@@ -391,9 +395,10 @@ def test_conv_pool_walk_stride1_bit_identical(gpu_ctx, case, monkeypatch):
     w = (rng.standard_normal((M, C, k, k)) * 0.3).astype(np.float32)
     b = rng.uniform(-0.5, 0.5, M).astype(np.float32)
     x = rng.standard_normal((3, C, H, H)).astype(np.float32)
-    mb = _conv_pool_model((1, C, H, H), w, b, [cp] * 4, [1, 1], True, [3, 3], [2, 2], ppads)
+    mb = _conv_pool_model((1, C, H, H), w, b, [cp] * 4, [1, 1], True, [3, 3], [2, 2], ppads, pre_relu=True)
     monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "100")
     vals = []
+    names = ore.Model.TILE_NAMES
     for walk, fusion in (("0", ore.FUSE_ALL), ("1", ore.FUSE_ALL), ("2", ore.FUSE_ALL), ("3", ore.FUSE_ALL),
                          ("0", ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
         monkeypatch.setenv("ORE_CONV_POOL_STREAM", walk)
@@ -401,13 +406,44 @@ def test_conv_pool_walk_stride1_bit_identical(gpu_ctx, case, monkeypatch):
         m.set_fusion(fusion | ore.KEEP_VALUES)
         _np(m.run(_t(x)))
         vals.append(m.read_value("p"))
+        if fusion & ore.FUSE_CONV_POOL and walk in ("1", "3") and M >= 48:  # the forced walker really ran
+            ran = [names[t] for t in m.tiles() if t >= names.index("epool patch")]
+            assert ran == [["epool walk48", "epool walk96", "epool walk64"][int(walk) - 1]], ran
         m.close()
     for v in vals[1:]:
         np.testing.assert_array_equal(vals[0], v)
     import oracle
-    ref = oracle.maxpool2d(oracle.relu(oracle.conv2d(x, w, b, pads=[cp] * 4, strides=(1, 1))), (3, 3), (2, 2),
-                           auto_pad="NOTSET", pads=ppads)
+    ref = oracle.maxpool2d(oracle.relu(oracle.conv2d(oracle.relu(x), w, b, pads=[cp] * 4, strides=(1, 1))), (3, 3),
+                           (2, 2), auto_pad="NOTSET", pads=ppads)
     np.testing.assert_allclose(vals[0], ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("hw", [64, 224])
+def test_squeezenet_concat_pool_fusion(gpu_ctx, hw):
+    """Opt-in ORE_FUSE_CONCAT_POOL (fire4 -> pool3, fire8 -> pool5 pooled in the expand convs'
+    epilogues, the expand outputs and their concat never stored): every value the fused graph
+    materialises -- pool3 / pool5 included -- and the probabilities equal the unfused run's bit
+    for bit; the row-walking kernel runs for the pooled expands."""
+    import ore
+    from ore import onnx_wire, squeezenet
+    mb = squeezenet.build(hw)
+    model = onnx_wire.decode_model(mb)
+    xt = _t(squeezenet.synthetic_input(3, hw, seed=41))
+    ref = ore.Model(gpu_ctx, mb, max_batch=3)
+    ref.set_fusion(ore.KEEP_VALUES)
+    y0 = _np(ref.run(xt))
+    fused = ore.Model(gpu_ctx, mb, max_batch=3)
+    fused.set_fusion(ore.FUSE_ALL | ore.FUSE_CONCAT_POOL | ore.KEEP_VALUES)
+    y1 = _np(fused.run(xt))
+    np.testing.assert_array_equal(y0, y1)
+    for v in ("pool3", "pool5"):
+        name = [n.output[0] for n in model.graph.node if n.name == v][0]
+        np.testing.assert_array_equal(fused.read_value(name), ref.read_value(name), err_msg=v)
+    names = ore.Model.TILE_NAMES
+    walk = [names[t] for t in fused.tiles() if t >= names.index("epool walk48")]
+    assert len(walk) >= 4, walk  # fire4 / fire8 expand1x1 + expand3x3 (+ conv1 @224)
+    ref.close()
+    fused.close()
 
 
 @pytest.mark.parametrize("hw", [64, 224])
