@@ -74,7 +74,7 @@ enum { CP_S2 = 0, CP_1X1 = 1, CP_T3 = 2 };
 // D: k-steps in flight; NW: waves per block.  qrow = quads per conv row, nsteps = 16 NW-quad steps per
 // image.
 template <int MF, int D, int NW, int MODE>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvParams p, int qrow, int nsteps, int nring) {
+__global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvParams p, int qrow, int nbands, int nring) {
   extern __shared__ unsigned cp_lds[];  // [nring][16 MF][Wp] pooled maxima (f32 bits)
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -84,7 +84,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
   const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
-  const int img = wgid / p.mtiles, mt = wgid - img * p.mtiles;
+  // block = (image, band of pooled rows, m tile); the m tiles of one band are adjacent
+  const int ib = wgid / p.mtiles, mt = wgid - ib * p.mtiles;
+  const int img = ib / nbands, band = ib - img * nbands;
   const int m0 = mt * (16 * MF);
   const int Wp = p.ep_Wo, Hp = p.ep_Ho;
   constexpr int CH = 16 * MF;
@@ -92,7 +94,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
 
   for (int i = tid; i < nring * slot; i += 64 * NW) cp_lds[i] = 0u;
 
-  const int nq = p.Ho * qrow;
+  // band: pooled rows [py0, py1) from conv rows 2 py0 .. 2 py1 (the band's last pooled row reads
+  // row 2 py1, which the next band recomputes as its first: one conv row per band boundary)
+  const int pb = (Hp + nbands - 1) / nbands;
+  const int py0 = band * pb, py1 = py0 + pb < Hp ? py0 + pb : Hp;
+  const int q0 = 2 * py0 * qrow;
+  const int nq = (2 * py1 + 1 < p.Ho ? 2 * py1 + 1 : p.Ho) * qrow;  // quads [q0, nq) of this band
+  const int nsteps = py0 < py1 ? (nq - q0 + 16 * NW - 1) / (16 * NW) : 0;
   // CP_T3: the resource starts x_lead bytes before x so that no tap offset is negative (a negative
   // offset would zero the whole 16-B access, valid elements included); those bytes are masked taps
   const int xlead = MODE == CP_T3 ? p.x_lead : 0;
@@ -124,7 +132,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
   int tt = lk;
   unsigned tmask[4] = {0u, 0u, 0u, 0u};  // CP_T3: bit 3 r + s = tap (r, s) of pixel q inside the image
   auto quad_base = [&](int st) -> int {
-    int qd = st * (16 * NW) + wave * 16 + lj;
+    int qd = q0 + st * (16 * NW) + wave * 16 + lj;
     if (qd >= nq) qd = nq - 1;  // surplus lanes of the last step re-read a valid quad (not pooled)
     const int oy = qd / qrow, qx = qd - oy * qrow;
     if constexpr (MODE == CP_S2) return ximg + 2 * oy * p.W + 8 * qx;  // input (2 oy, 2 (4 qx))
@@ -226,7 +234,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
 #pragma unroll
   for (int d = 0; d < D; ++d)
     if (d < total) CP_LOAD(d);
-  int ct = 0, cs = 0, py_next = 0;  // consumer k-step / step, first pooled row not yet stored
+  int ct = 0, cs = 0, py_next = py0;  // consumer k-step / step, first pooled row not yet stored
   for (int g0 = 0; g0 < total; g0 += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -238,7 +246,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
         if (++ct == nks) {
           ct = 0;
           // ---- epilogue of step cs: bias + Relu, 3x3 maxima into the LDS ring ----
-          int qd = cs * (16 * NW) + wave * 16 + lj;
+          int qd = q0 + cs * (16 * NW) + wave * 16 + lj;
           const bool qv = qd < nq;
           if (!qv) qd = nq - 1;
           const int oy = qd / qrow, qx = qd - oy * qrow;
@@ -249,7 +257,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
           // left: column 4qx still has to reach pooled column 2qx - 1 itself (no left lane folded it)
           const bool right = lj < 15 && qx < qrow - 1;
           const bool left = qx > 0 && lj == 0;
-          const bool oka = qv && pya < Hp, okb = qv && pyb >= 0 && pyb < Hp;
+          const bool oka = qv && pya >= py0 && pya < py1, okb = qv && pyb >= py0 && pyb < py1;
           const int sa = (pya % nring) * slot, sb = (pyb < 0 ? 0 : pyb % nring) * slot;
 #pragma unroll
           for (int f = 0; f < MF; ++f)
@@ -297,10 +305,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
           asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #endif
           // ---- store the pooled rows whose conv rows 2py .. 2py + 2 are all done ----
-          const int qend = (cs + 1) * (16 * NW) < nq ? (cs + 1) * (16 * NW) : nq;
+          const int qend = q0 + (cs + 1) * (16 * NW) < nq ? q0 + (cs + 1) * (16 * NW) : nq;
           const int rows_done = qend / qrow;
-          int py_end = qend == nq ? Hp : (rows_done >= 3 ? ((rows_done - 3) >> 1) + 1 : 0);
-          if (py_end > Hp) py_end = Hp;
+          int py_end = qend == nq ? py1 : (rows_done >= 3 ? ((rows_done - 3) >> 1) + 1 : 0);
+          if (py_end > py1) py_end = py1;
           for (int py = py_next; py < py_end; ++py) {
             unsigned* src = cp_lds + (py % nring) * slot;
             float* dst = p.y + (long long)img * p.y_nstride + (long long)m0 * p.y_ps + py * Wp;
@@ -324,10 +332,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
 // variants (ConvParams::ep_variant): 2 = 48 channels x 64 quads per block (4 waves), 3 = 96 channels
 // x 128 quads (8 waves: twice the MFMAs per operand load, one block per CU), 4 = 64 channels x 64
 // quads (4 waves)
+// x 128 quads (8 waves), 5 = variant 4 over 3 bands of pooled rows per image (3x the blocks: three
+// 4-wave blocks per CU instead of two where the grid is N x 2 m tiles)
 static void cp_shape(int variant, int M, int* mf, int* nw) {
-  *mf = variant == 3 ? 6 : variant == 4 ? 4 : (M > 32 ? 3 : 2);
+  *mf = variant == 3 ? 6 : (variant == 4 || variant == 5) ? 4 : (M > 32 ? 3 : 2);
   *nw = variant == 3 ? 8 : 4;
 }
+static int cp_bands(int variant) { return variant == 5 ? 3 : 1; }
 static size_t cp_lds_bytes(const ConvParams& p, int variant) {
   int mf, nw;
   cp_shape(variant, p.M, &mf, &nw);
@@ -354,19 +365,19 @@ static int cp_mode(const ConvParams& p) {
 }
 
 bool conv_pool_stream_eligible(const ConvParams& p, int variant) {
-  if (variant < 2 || variant > 4 || cp_mode(p) < 0) return false;
+  if (variant < 2 || variant > 5 || cp_mode(p) < 0) return false;
   if (variant == 3 && p.M < 64) return false;  // mostly idle rows
-  if (variant == 4 && p.M < 48) return false;
+  if ((variant == 4 || variant == 5) && p.M < 48) return false;
+  if (variant == 5 && p.ep_Ho < 6) return false;
   return cp_lds_bytes(p, variant) <= size_t(variant == 3 ? 152 : 78) * 1024;
 }
 
 template <int MF, int D, int NW, int MODE>
-static void launch_cp(const ConvParams& p0, size_t lds, hipStream_t s) {
+static void launch_cp(const ConvParams& p0, size_t lds, int nbands, hipStream_t s) {
   ConvParams p = p0;
   p.mtiles = (p.M + 16 * MF - 1) / (16 * MF);
   p.x_lead = MODE == CP_T3 ? cp_lead(p) : 0;
   const int qrow = (p.Wo + 3) / 4;
-  const int nsteps = (p.Ho * qrow + 16 * NW - 1) / (16 * NW);
   const int nring = cp_nring(qrow, 16 * NW);
   if (lds > 64 * 1024) {  // above the default dynamic-LDS limit (once per process and instantiation)
     static bool raised = false;
@@ -376,16 +387,16 @@ static void launch_cp(const ConvParams& p0, size_t lds, hipStream_t s) {
       raised = true;
     }
   }
-  hipLaunchKernelGGL((conv_pool_stream_kernel<MF, D, NW, MODE>), dim3((unsigned)(p.N * p.mtiles)), dim3(64 * NW), lds,
-                     s, p, qrow, nsteps, nring);
+  hipLaunchKernelGGL((conv_pool_stream_kernel<MF, D, NW, MODE>), dim3((unsigned)(p.N * nbands * p.mtiles)),
+                     dim3(64 * NW), lds, s, p, qrow, nbands, nring);
 }
 
 template <int MF, int NW>
-static void launch_cp_mode(const ConvParams& p, size_t lds, hipStream_t s) {
+static void launch_cp_mode(const ConvParams& p, size_t lds, int nbands, hipStream_t s) {
   switch (cp_mode(p)) {
-    case CP_S2: launch_cp<MF, ORE_CP_D, NW, CP_S2>(p, lds, s); break;
-    case CP_1X1: launch_cp<MF, ORE_CP_D, NW, CP_1X1>(p, lds, s); break;
-    default: launch_cp<MF, ORE_CP_D, NW, CP_T3>(p, lds, s); break;
+    case CP_S2: launch_cp<MF, ORE_CP_D, NW, CP_S2>(p, lds, nbands, s); break;
+    case CP_1X1: launch_cp<MF, ORE_CP_D, NW, CP_1X1>(p, lds, nbands, s); break;
+    default: launch_cp<MF, ORE_CP_D, NW, CP_T3>(p, lds, nbands, s); break;
   }
 }
 
@@ -393,14 +404,15 @@ void launch_conv_pool_stream(const ConvParams& p, int variant, hipStream_t s) {
   int mf, nw;
   cp_shape(variant, p.M, &mf, &nw);
   const size_t lds = cp_lds_bytes(p, variant);
+  const int nb = cp_bands(variant);
   if (variant == 3)
-    launch_cp_mode<6, 8>(p, lds, s);
-  else if (variant == 4)
-    launch_cp_mode<4, 4>(p, lds, s);
+    launch_cp_mode<6, 8>(p, lds, nb, s);
+  else if (variant == 4 || variant == 5)
+    launch_cp_mode<4, 4>(p, lds, nb, s);
   else if (mf == 3)
-    launch_cp_mode<3, 4>(p, lds, s);
+    launch_cp_mode<3, 4>(p, lds, nb, s);
   else
-    launch_cp_mode<2, 4>(p, lds, s);
+    launch_cp_mode<2, 4>(p, lds, nb, s);
 }
 
 }  // namespace ore

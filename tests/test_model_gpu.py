@@ -400,15 +400,15 @@ def test_conv_pool_walk_stride1_bit_identical(gpu_ctx, case, monkeypatch):
     vals = []
     names = ore.Model.TILE_NAMES
     for walk, fusion in (("0", ore.FUSE_ALL), ("1", ore.FUSE_ALL), ("2", ore.FUSE_ALL), ("3", ore.FUSE_ALL),
-                         ("0", ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
+                         ("4", ore.FUSE_ALL), ("0", ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
         monkeypatch.setenv("ORE_CONV_POOL_STREAM", walk)
         m = ore.Model(gpu_ctx, mb, max_batch=3)
         m.set_fusion(fusion | ore.KEEP_VALUES)
         _np(m.run(_t(x)))
         vals.append(m.read_value("p"))
-        if fusion & ore.FUSE_CONV_POOL and walk in ("1", "3") and M >= 48:  # the forced walker really ran
-            ran = [names[t] for t in m.tiles() if t >= names.index("epool patch")]
-            assert ran == [["epool walk48", "epool walk96", "epool walk64"][int(walk) - 1]], ran
+        if fusion & ore.FUSE_CONV_POOL and walk in ("1", "3", "4") and M >= 48 and (walk != "4" or H >= 12):
+            ran = [names[t] for t in m.tiles() if t >= names.index("epool patch")]  # the forced walker ran
+            assert ran == [names[names.index("epool patch") + int(walk)]], ran
         m.close()
     for v in vals[1:]:
         np.testing.assert_array_equal(vals[0], v)
