@@ -100,6 +100,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
   const int py0 = band * pb, py1 = py0 + pb < Hp ? py0 + pb : Hp;
   const int q0 = 2 * py0 * qrow;
   const int nq = (2 * py1 + 1 < p.Ho ? 2 * py1 + 1 : p.Ho) * qrow;  // quads [q0, nq) of this band
+  const bool colpad = 2 * (Wp - 1) + 2 >= p.Wo;  // a pooled window reaches a quad-padding column
   const int nsteps = py0 < py1 ? (nq - q0 + 16 * NW - 1) / (16 * NW) : 0;
   // CP_T3: the resource starts x_lead bytes before x so that no tap offset is negative (a negative
   // offset would zero the whole 16-B access, valid elements included); those bytes are masked taps
@@ -268,8 +269,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
 #pragma unroll
               for (int q = 0; q < 4; ++q) {
                 const float t = acc[f][q][e] + bias[f][e];
-                // Relu, canonical +0; columns >= Wo (the quad padding) count as the pool's zero padding
-                v[q] = (t > 0.0f && px0 * 2 + q < p.Wo) ? t : 0.0f;
+                v[q] = t > 0.0f ? t : 0.0f;  // Relu, canonical +0
+              }
+              if (colpad) {  // columns >= Wo (the quad padding) read by a window: the pool's zero padding
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  if (px0 * 2 + q >= p.Wo) v[q] = 0.0f;
               }
               const unsigned c0 = __float_as_uint(fmaxf(fmaxf(v[0], v[1]), v[2]));
               const unsigned c2 = __float_as_uint(v[0]);
