@@ -171,7 +171,10 @@ ore_status ore_model_destroy(ore_model* m);
  * neighbouring tile) and stores only the pooled values; the pre-pool tensor never reaches HBM.
  * Bit-identical (same per-output MFMA chain; max is exact).  Applied when the computed columns are
  * <= ORE_EPOOL_MAX_WORK (environment, default 1.25) x the conv's own (SqueezeNet @224: conv1 +
- * pool1 only, 1.16x); f32 models. */
+ * pool1 only, 1.16x).  f32 models: ore_model_autotune also times the row-walking kernels
+ * (ore_conv_pool.hip: a block walks the conv plane row-major and max-reduces into an LDS ring of
+ * pooled rows, nothing recomputed) and keeps the fastest -- conv1 + pool1: 96 channels x 128
+ * quads per block, 1016 -> ~900 us at batch 256. */
 #define ORE_FUSE_CONV_POOL 32
 /* bit 6: a fire module (Concat of a 1x1 and a 3x3 'same' Conv + Relu of one value, 64-multiple
  * channel counts) and the 1x1 Conv + Relu (<= 64 channels) that is the Concat's only reader -- the
