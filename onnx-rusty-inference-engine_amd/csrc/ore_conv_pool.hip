@@ -27,6 +27,9 @@
 // each conv output is the same k-ordered MFMA chain + bias as conv_gemm_kernel's: bit-identical.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "ore_kernels.h"
 
 namespace ore {
@@ -40,6 +43,49 @@ typedef float cp_floatx3 __attribute__((ext_vector_type(3)));
 // rows at most; nring = (G2 + 4) / 2 covers both, checked by simulation over widths 6..229 and heights
 // 5..229 for S = 64 and 128 (4 / 7 slots for a 28-quad row).
 static int cp_nring(int qrow, int S) { return ((qrow + 2 * S - 2) / qrow + 4) / 2; }
+
+// Exact ring size for a geometry by simulating the walk (the kernel's step / flush rules): the
+// smallest nring such that no two live pooled rows share a slot and, unless a second barrier
+// separates the clears from the next step's maxima (dbar), no slot cleared after a step is
+// touched by the next one.  Used for the double-barrier variant, whose point is a smaller ring.
+static int cp_nring_exact(int qrow, int Ho, int Hp, int S, int nbands, bool dbar) {
+  int need = 2;
+  const int pbn = (Hp + nbands - 1) / nbands;
+  for (int band = 0; band < nbands; ++band) {
+    const int py0 = band * pbn, py1 = py0 + pbn < Hp ? py0 + pbn : Hp;
+    if (py0 >= py1) continue;
+    const int q0 = 2 * py0 * qrow, nq = (2 * py1 + 1 < Ho ? 2 * py1 + 1 : Ho) * qrow;
+    for (int nr = need; nr < 256; ++nr) {
+      std::vector<int> owner(nr, -1);
+      std::vector<char> cleared(nr, 0);
+      int py_next = py0;
+      bool ok = true;
+      for (int qs = q0; qs < nq && ok; qs += S) {
+        const int qe = qs + S < nq ? qs + S : nq;
+        for (int qd = qs; qd < qe && ok; ++qd) {
+          const int oy = qd / qrow, pa = oy >> 1, pbr = ((oy & 1) == 0 && oy >= 2) ? pa - 1 : -1;
+          for (int py : {pa, pbr}) {
+            if (py < py0 || py >= py1) continue;
+            const int sl = py % nr;
+            if ((owner[sl] >= 0 && owner[sl] != py) || (!dbar && cleared[sl])) { ok = false; break; }
+            owner[sl] = py;
+          }
+        }
+        const int rd = qe / qrow;
+        int pe = qe == nq ? py1 : (rd >= 3 ? ((rd - 3) >> 1) + 1 : 0);
+        if (pe > py1) pe = py1;
+        std::fill(cleared.begin(), cleared.end(), 0);
+        for (int py = py_next; py < pe; ++py) {
+          cleared[py % nr] = 1;
+          if (owner[py % nr] == py) owner[py % nr] = -1;
+        }
+        if (pe > py_next) py_next = pe;
+      }
+      if (ok) { need = nr; break; }
+    }
+  }
+  return need;
+}
 
 template <int MF>
 __device__ __forceinline__ void cp_load_a(__amdgpu_buffer_rsrc_t r, int voff, int soff, float (&a)[MF]) {
@@ -73,7 +119,7 @@ enum { CP_S2 = 0, CP_1X1 = 1, CP_T3 = 2 };
 // MF: 16-channel fragments per block (every wave computes all 16 MF channels of its 16 quads);
 // D: k-steps in flight; NW: waves per block.  qrow = quads per conv row, nsteps = 16 NW-quad steps per
 // image.
-template <int MF, int D, int NW, int MODE>
+template <int MF, int D, int NW, int MODE, bool DB>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvParams p, int qrow, int nbands, int nring) {
   extern __shared__ unsigned cp_lds[];  // [nring][16 MF][Wp] pooled maxima (f32 bits)
   const int tid = threadIdx.x;
@@ -325,6 +371,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
               }
           }
           if (py_end > py_next) py_next = py_end;
+          if constexpr (DB) __syncthreads();  // the clears land before the next step's maxima
           ++cs;
         }
       }
@@ -336,18 +383,30 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
 
 // variants (ConvParams::ep_variant): 2 = 48 channels x 64 quads per block (4 waves), 3 = 96 channels
 // x 128 quads (8 waves: twice the MFMAs per operand load, one block per CU), 4 = 64 channels x 64
-// quads (4 waves)
-// x 128 quads (8 waves), 5 = variant 4 over 3 bands of pooled rows per image (3x the blocks: three
-// 4-wave blocks per CU instead of two where the grid is N x 2 m tiles)
+// quads (4 waves), 5 = variant 4 over 3 bands of pooled rows per image (3x the blocks), 6 = 96
+// channels x 64 quads over 2 bands with a second barrier per step (the smaller ring lets two blocks
+// share a CU, so one block's MFMAs run under the other's epilogue)
 static void cp_shape(int variant, int M, int* mf, int* nw) {
-  *mf = variant == 3 ? 6 : (variant == 4 || variant == 5) ? 4 : (M > 32 ? 3 : 2);
+  *mf = (variant == 3 || variant == 6) ? 6 : (variant == 4 || variant == 5) ? 4 : (M > 32 ? 3 : 2);
   *nw = variant == 3 ? 8 : 4;
 }
-static int cp_bands(int variant) { return variant == 5 ? 3 : 1; }
+static int cp_bands(int variant) { return variant == 5 ? 3 : variant == 6 ? 2 : 1; }
+static int cp_ring(const ConvParams& p, int variant) {
+  int mf, nw;
+  cp_shape(variant, p.M, &mf, &nw);
+  const int qrow = (p.Wo + 3) / 4;
+  if (variant != 6) return cp_nring(qrow, 16 * nw);
+  static thread_local int key[4] = {-1, -1, -1, -1}, val = 0;  // one geometry cached per thread
+  if (key[0] != qrow || key[1] != p.Ho || key[2] != p.ep_Ho || key[3] != 16 * nw) {
+    key[0] = qrow; key[1] = p.Ho; key[2] = p.ep_Ho; key[3] = 16 * nw;
+    val = cp_nring_exact(qrow, p.Ho, p.ep_Ho, 16 * nw, cp_bands(variant), true);
+  }
+  return val;
+}
 static size_t cp_lds_bytes(const ConvParams& p, int variant) {
   int mf, nw;
   cp_shape(variant, p.M, &mf, &nw);
-  return size_t(cp_nring((p.Wo + 3) / 4, 16 * nw)) * 16 * mf * p.ep_Wo * 4;
+  return size_t(cp_ring(p, variant)) * 16 * mf * p.ep_Wo * 4;
 }
 static int cp_lead(const ConvParams& p) { return ((p.pt * p.W + p.pl) * 4 + 15) & ~15; }
 
@@ -370,38 +429,37 @@ static int cp_mode(const ConvParams& p) {
 }
 
 bool conv_pool_stream_eligible(const ConvParams& p, int variant) {
-  if (variant < 2 || variant > 5 || cp_mode(p) < 0) return false;
-  if (variant == 3 && p.M < 64) return false;  // mostly idle rows
+  if (variant < 2 || variant > 6 || cp_mode(p) < 0) return false;
+  if ((variant == 3 || variant == 6) && p.M < 64) return false;  // mostly idle rows
   if ((variant == 4 || variant == 5) && p.M < 48) return false;
   if (variant == 5 && p.ep_Ho < 6) return false;
   return cp_lds_bytes(p, variant) <= size_t(variant == 3 ? 152 : 78) * 1024;
 }
 
-template <int MF, int D, int NW, int MODE>
-static void launch_cp(const ConvParams& p0, size_t lds, int nbands, hipStream_t s) {
+template <int MF, int D, int NW, int MODE, bool DB>
+static void launch_cp(const ConvParams& p0, size_t lds, int nbands, int nring, hipStream_t s) {
   ConvParams p = p0;
   p.mtiles = (p.M + 16 * MF - 1) / (16 * MF);
   p.x_lead = MODE == CP_T3 ? cp_lead(p) : 0;
   const int qrow = (p.Wo + 3) / 4;
-  const int nring = cp_nring(qrow, 16 * NW);
   if (lds > 64 * 1024) {  // above the default dynamic-LDS limit (once per process and instantiation)
     static bool raised = false;
     if (!raised) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pool_stream_kernel<MF, D, NW, MODE>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pool_stream_kernel<MF, D, NW, MODE, DB>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       raised = true;
     }
   }
-  hipLaunchKernelGGL((conv_pool_stream_kernel<MF, D, NW, MODE>), dim3((unsigned)(p.N * nbands * p.mtiles)),
+  hipLaunchKernelGGL((conv_pool_stream_kernel<MF, D, NW, MODE, DB>), dim3((unsigned)(p.N * nbands * p.mtiles)),
                      dim3(64 * NW), lds, s, p, qrow, nbands, nring);
 }
 
-template <int MF, int NW>
-static void launch_cp_mode(const ConvParams& p, size_t lds, int nbands, hipStream_t s) {
+template <int MF, int NW, bool DB = false>
+static void launch_cp_mode(const ConvParams& p, size_t lds, int nbands, int nring, hipStream_t s) {
   switch (cp_mode(p)) {
-    case CP_S2: launch_cp<MF, ORE_CP_D, NW, CP_S2>(p, lds, nbands, s); break;
-    case CP_1X1: launch_cp<MF, ORE_CP_D, NW, CP_1X1>(p, lds, nbands, s); break;
-    default: launch_cp<MF, ORE_CP_D, NW, CP_T3>(p, lds, nbands, s); break;
+    case CP_S2: launch_cp<MF, ORE_CP_D, NW, CP_S2, DB>(p, lds, nbands, nring, s); break;
+    case CP_1X1: launch_cp<MF, ORE_CP_D, NW, CP_1X1, DB>(p, lds, nbands, nring, s); break;
+    default: launch_cp<MF, ORE_CP_D, NW, CP_T3, DB>(p, lds, nbands, nring, s); break;
   }
 }
 
@@ -409,15 +467,17 @@ void launch_conv_pool_stream(const ConvParams& p, int variant, hipStream_t s) {
   int mf, nw;
   cp_shape(variant, p.M, &mf, &nw);
   const size_t lds = cp_lds_bytes(p, variant);
-  const int nb = cp_bands(variant);
-  if (variant == 3)
-    launch_cp_mode<6, 8>(p, lds, nb, s);
+  const int nb = cp_bands(variant), nr = cp_ring(p, variant);
+  if (variant == 6)
+    launch_cp_mode<6, 4, true>(p, lds, nb, nr, s);
+  else if (variant == 3)
+    launch_cp_mode<6, 8>(p, lds, nb, nr, s);
   else if (variant == 4 || variant == 5)
-    launch_cp_mode<4, 4>(p, lds, nb, s);
+    launch_cp_mode<4, 4>(p, lds, nb, nr, s);
   else if (mf == 3)
-    launch_cp_mode<3, 4>(p, lds, nb, s);
+    launch_cp_mode<3, 4>(p, lds, nb, nr, s);
   else
-    launch_cp_mode<2, 4>(p, lds, nb, s);
+    launch_cp_mode<2, 4>(p, lds, nb, nr, s);
 }
 
 }  // namespace ore

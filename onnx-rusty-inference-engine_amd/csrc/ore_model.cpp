@@ -1372,7 +1372,7 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
     if (s.kind == S_CONV && s.epool && !s.plan.f16) {  // f32 pooled conv: patch vs row-walk kernels
       int best = 0;
       float best_ms = 1e30f;
-      for (int v = 1; v <= 5 && !st; ++v) {
+      for (int v = 1; v <= 6 && !st; ++v) {
         s.plan.epv = v;
         last_conv_tile = -1;
         st = launch_step(m, s, n);  // warm-up

@@ -278,7 +278,7 @@ class Model:
                   "stream 64x128", "stream 32x256", "stream 16x256", "stream 48x128", "stream 64x64",
                   "stream 128x64", "stream 64x64 d8", "stream 32x128", "stream 128x64 d2", "fire",
                   "epool patch", "epool walk48", "epool walk96", "epool walk64",
-                  "epool walk64 b3"]
+                  "epool walk64 b3", "epool walk96 b2"]
 
     def tiles(self):
         """Block tile per exec step (-1 for non-conv steps); names in TILE_NAMES."""

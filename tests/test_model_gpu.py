@@ -359,7 +359,7 @@ def test_conv_pool_walk_bit_identical(gpu_ctx, case, monkeypatch):
     mb = _conv_pool_model((1, C, H, H), w, b, [0] * 4, [2, 2], True, [3, 3], [2, 2], [0, 0, 0, 0])
     monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "100")
     vals = []
-    for walk, fusion in (("1", ore.FUSE_ALL), ("0", ore.FUSE_ALL), ("2", ore.FUSE_ALL),
+    for walk, fusion in (("1", ore.FUSE_ALL), ("0", ore.FUSE_ALL), ("2", ore.FUSE_ALL), ("5", ore.FUSE_ALL),
                          ("1", ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
         monkeypatch.setenv("ORE_CONV_POOL_STREAM", walk)
         m = ore.Model(gpu_ctx, mb, max_batch=3)
@@ -400,7 +400,7 @@ def test_conv_pool_walk_stride1_bit_identical(gpu_ctx, case, monkeypatch):
     vals = []
     names = ore.Model.TILE_NAMES
     for walk, fusion in (("0", ore.FUSE_ALL), ("1", ore.FUSE_ALL), ("2", ore.FUSE_ALL), ("3", ore.FUSE_ALL),
-                         ("4", ore.FUSE_ALL), ("0", ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
+                         ("4", ore.FUSE_ALL), ("5", ore.FUSE_ALL), ("0", ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
         monkeypatch.setenv("ORE_CONV_POOL_STREAM", walk)
         m = ore.Model(gpu_ctx, mb, max_batch=3)
         m.set_fusion(fusion | ore.KEEP_VALUES)
