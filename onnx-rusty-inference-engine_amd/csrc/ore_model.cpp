@@ -1372,7 +1372,9 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
     if (s.kind == S_CONV && s.epool && !s.plan.f16) {  // f32 pooled conv: patch vs row-walk kernels
       int best = 0;
       float best_ms = 1e30f;
-      for (int v = 1; v <= 6 && !st; ++v) {
+      // variant 6 (two 4-wave blocks per CU) wins this isolated timing on conv1 but loses inside the
+      // graph (963 vs 913 us, profiles/r01zg_conv1_walk96_b2.txt): forced only (ORE_CONV_POOL_STREAM=5)
+      for (int v = 1; v <= 5 && !st; ++v) {
         s.plan.epv = v;
         last_conv_tile = -1;
         st = launch_step(m, s, n);  // warm-up
