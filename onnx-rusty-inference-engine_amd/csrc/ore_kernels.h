@@ -160,7 +160,8 @@ void launch_conv_epool(const ConvParams& p, hipStream_t s);
 // (ORE_CONV_POOL_STREAM=0 keeps conv_gemm_kernel's patch epilogue)
 // variants (ConvParams::ep_variant): 1 = the patch kernel, 2 = walk 48 channels x 64 quads per block,
 // 3 = walk 96 channels x 128 quads, 4 = walk 64 x 64, 5 = 4 over 3 bands of pooled rows, 6 = walk
-// 96 x 64 over 2 bands (two blocks per CU); 0 = the first eligible of 3, 4, 2, 1.
+// 96 x 64 over 2 bands (two blocks per CU); 0 = the first eligible of 3, 4, 2, 1 at batch >= 128,
+// else 1.
 // ORE_CONV_POOL_STREAM=0..5 forces 1..6 (tests).  launch_conv_epool leaves last_conv_tile = EPOOL_TILE_BASE + variant run.
 constexpr int EPOOL_TILE_BASE = 21;
 bool conv_pool_stream_eligible(const ConvParams& p, int variant);

@@ -419,7 +419,7 @@ def test_conv_pool_walk_stride1_bit_identical(gpu_ctx, case, monkeypatch):
 
 
 @pytest.mark.parametrize("hw", [64, 224])
-def test_squeezenet_concat_pool_fusion(gpu_ctx, hw):
+def test_squeezenet_concat_pool_fusion(gpu_ctx, hw, monkeypatch):
     """Opt-in ORE_FUSE_CONCAT_POOL (fire4 -> pool3, fire8 -> pool5 pooled in the expand convs'
     epilogues, the expand outputs and their concat never stored): every value the fused graph
     materialises -- pool3 / pool5 included -- and the probabilities equal the unfused run's bit
@@ -432,6 +432,7 @@ def test_squeezenet_concat_pool_fusion(gpu_ctx, hw):
     ref = ore.Model(gpu_ctx, mb, max_batch=3)
     ref.set_fusion(ore.KEEP_VALUES)
     y0 = _np(ref.run(xt))
+    monkeypatch.setenv("ORE_CONV_POOL_STREAM", "3")  # the 64-channel walker (auto takes it from batch 128)
     fused = ore.Model(gpu_ctx, mb, max_batch=3)
     fused.set_fusion(ore.FUSE_ALL | ore.FUSE_CONCAT_POOL | ore.KEEP_VALUES)
     y1 = _np(fused.run(xt))
