@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--no-b1", action="store_true", help="skip the batch-1 latency probe")
     ap.add_argument("--no-autotune", action="store_true", help="keep the heuristic per-layer conv tiles")
     ap.add_argument("--dump-steps", default="", help="write the plan's kernel steps (op, name, flops, bytes) as JSON")
+    ap.add_argument("--fusion", type=int, default=None, help="ore_model_set_fusion flags (experiments; default: the model's)")
     ap.add_argument("--precision", choices=["f32", "f16"], default="f32",
                     help="f16: the fp16 variant (SURVEY.md §8(f)3, config 5); the headline metric is f32")
     return ap.parse_args()
@@ -145,6 +146,8 @@ def main():
     gathered = torch.empty((world * B, model.output_elems), dtype=torch.float32, device=f"cuda:{local}") \
         if world > 1 else out
 
+    if args.fusion is not None:
+        model.set_fusion(args.fusion)
     if not args.no_autotune:  # per-layer conv tile search, outside the timed region
         model.autotune(x, out)
     if args.dump_steps and rank == 0:  # kernel-step names for tools/pmc_report.py
