@@ -153,12 +153,13 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* onnx_bytes, size_t len, i
 ore_status ore_model_destroy(ore_model* m);
 /* flags: bit 0 = fuse Conv->Relu, bit 1 = Concat in place, bit 2 = alias Dropout/Reshape,
  * bit 5 = Conv->MaxPool (ORE_FUSE_CONV_POOL below), bit 6 = fire module + next squeeze
- * (ORE_FUSE_FIRE below).  ORE_FUSE_ALL is the default; 0 runs every node as its own kernel
+ * (ORE_FUSE_FIRE below), bit 7 = Concat->MaxPool in the producers (ORE_FUSE_CONCAT_POOL below).
+ * ORE_FUSE_ALL is the default; 0 runs every node as its own kernel
  * (op-by-op parity). */
 #define ORE_FUSE_CONV_RELU 1
 #define ORE_FUSE_CONCAT 2
 #define ORE_FUSE_ALIAS 4
-#define ORE_FUSE_ALL 103
+#define ORE_FUSE_ALL 231
 /* bit 4 (opt-in, not in ORE_FUSE_ALL): a 3x3 MaxPool whose only consumer is a 1x1 stride-1 Conv
  * runs inside that conv's operand gather (each B element = the window max of the pre-pool
  * tensor); the pooled tensor is never written.  Max is exact, so results are bit-identical.
@@ -184,13 +185,14 @@ ore_status ore_model_destroy(ore_model* m);
  * (environment, default 65536: one 64-pixel wave per SIMD), below which the fused launch has too
  * few waves (batch 1 keeps the separate kernels). */
 #define ORE_FUSE_FIRE 64
-/* bit 7 (opt-in, not in ORE_FUSE_ALL): Concat(e1, e3) -> 3x3 / stride-2 MaxPool with e1 / e3 Convs
+/* bit 7 (in ORE_FUSE_ALL): Concat(e1, e3) -> 3x3 / stride-2 MaxPool with e1 / e3 Convs
  * (+ Relu) read only by the Concat (SqueezeNet's fire4 -> pool3, fire8 -> pool5): each conv's pooled
  * epilogue (the row-walking kernel, ore_conv_pool.hip) writes its channel slice of the pool output,
  * so neither the expand outputs nor the Concat reach HBM.  Bit-identical (the pool is per channel;
- * every pooled value is the max of the same nine values).  f32 models.  Measured slower at batch
- * 256 (fire8: 694 vs 625 us per step for the expands + pool5): the walker's expand3x3 reaches 93 of
- * the streaming kernel's 124 TF/s. */
+ * every pooled value is the max of the same nine values).  f32 models, conv planes of at least
+ * ORE_CONCAT_POOL_MIN_HW (environment, default 1024) pixels: at batch 256 fire4 -> pool3 (54 x 54)
+ * saves 40 us per step, fire8 -> pool5 (27 x 27) would cost 21 us (the walker's expand3x3 runs at
+ * 88-92 % of the streaming kernel's rate). */
 #define ORE_FUSE_CONCAT_POOL 128
 /* debug: give every value its own storage (no liveness reuse) so any value can be read back */
 #define ORE_KEEP_VALUES 8

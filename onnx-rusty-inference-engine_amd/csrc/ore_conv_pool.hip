@@ -139,6 +139,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
   const int slot = CH * Wp;
 
   for (int i = tid; i < nring * slot; i += 64 * NW) cp_lds[i] = 0u;
+  // CP_T3: per k = 4 t + lk of a step, {c x_ps + r W + s (-1 past K), tap 3 r + s} behind the ring
+  int2* tap_tab = reinterpret_cast<int2*>(cp_lds + nring * slot);
+  if constexpr (MODE == CP_T3) {
+    for (int k = tid; k < 4 * ((p.K + 3) >> 2); k += 64 * NW) {
+      const int c = k / 9, t9 = k - 9 * c;
+      tap_tab[k] = int2{c < p.C ? c * p.x_ps + (t9 / 3) * p.W + t9 % 3 : -1, t9};
+    }
+  }
 
   // band: pooled rows [py0, py1) from conv rows 2 py0 .. 2 py1 (the band's last pooled row reads
   // row 2 py1, which the next band recomputes as its first: one conv row per band boundary)
@@ -177,7 +185,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
   // tt = 3 r + s of channel lc, channel offset loff = lc x_ps
   int lc = MODE == CP_1X1 ? lk : 0, lr = 0, lsx = lk, loff = MODE == CP_S2 ? lk : MODE == CP_1X1 ? lk * p.x_ps : 0;
   int tt = lk;
-  unsigned tmask[4] = {0u, 0u, 0u, 0u};  // CP_T3: bit 3 r + s = tap (r, s) of pixel q inside the image
+  // CP_T3: bit 3 r + s = tap (r, s) of pixel q inside the image; the loader's copy (tmask, written
+  // when it moves to the next step's quad, D k-steps ahead) and the consumer's (tmc, taken over at
+  // the step's epilogue)
+  unsigned tmask[4] = {0u, 0u, 0u, 0u}, tmc[4] = {0u, 0u, 0u, 0u};
   auto quad_base = [&](int st) -> int {
     int qd = q0 + st * (16 * NW) + wave * 16 + lj;
     if (qd >= nq) qd = nq - 1;  // surplus lanes of the last step re-read a valid quad (not pooled)
@@ -199,6 +210,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
     return (xlead >> 2) + ximg + (oy - p.pt) * p.W + 4 * qx - p.pl;
   };
   int lbase = quad_base(0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) tmc[q] = tmask[q];
 
   cp_floatx4 acc[MF][4];
 #pragma unroll
@@ -208,9 +221,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
   float ra[D][MF];
   cp_floatx4 rb0[D];
   cp_floatx3 rb1[MODE == CP_S2 ? D : 1];
-  // CP_T3: each ring slot's zero mask, bit q = pixel q's tap inside the image (taken at load time:
-  // the loader runs D k-steps ahead and moves to the next step's quad -- and masks -- first)
-  int rt[MODE == CP_T3 ? D : 1];
+  int rt[MODE == CP_T3 ? D : 1];  // CP_T3: the tap of each ring slot's k (for its zero mask)
 
 #ifndef ORE_EXP_CP_ONELOAD
 #define CP_LOAD_B1(SLOT) \
@@ -235,15 +246,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
       rb0[SLOT] = __builtin_bit_cast(cp_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, o_, 0, 0)); \
       lc += 4; loff += 4 * p.x_ps;                                                                     \
     } else {                                                                                           \
-      /* tt / 3 for tt < 9 by a 24-bit multiply (as conv_stream_kernel) */                             \
-      const int r_ = (int)(__umul24((unsigned)tt, 11u) >> 5);                                          \
-      const int o_ = lc < p.C ? (lbase + loff + (int)__umul24((unsigned)r_, (unsigned)(p.W - 3)) + tt) * 4 \
-                              : 0x7ff00000;                                                            \
+      /* the k-step's (tap offset, tap) from the block's LDS table: the same every step */            \
+      const int2 e_ = tap_tab[4 * lt + lk];                                                            \
+      const int o_ = e_.x >= 0 ? (lbase + e_.x) * 4 : 0x7ff00000;                                      \
       rb0[SLOT] = __builtin_bit_cast(cp_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, o_, 0, 0)); \
-      rt[SLOT] = (int)(((tmask[0] >> tt) & 1u) | (((tmask[1] >> tt) & 1u) << 1) |                      \
-                       (((tmask[2] >> tt) & 1u) << 2) | (((tmask[3] >> tt) & 1u) << 3));                \
-      tt += 4;                                                                                         \
-      if (tt >= 9) { tt -= 9; loff += p.x_ps; ++lc; }                                                  \
+      rt[SLOT] = e_.y;                                                                                 \
     }                                                                                                  \
     if (++lt == nks) {                                                                                 \
       lt = 0; lr = 0; lsx = lk; tt = lk;                                                               \
@@ -256,10 +263,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
   if constexpr (MODE == CP_T3) { /* zero the taps outside the image (the reference's zero padding) */  \
     const int4 v_ = __builtin_bit_cast(int4, rb0[SLOT]);                                               \
     int4 w_;                                                                                           \
-    w_.x = v_.x & __builtin_amdgcn_sbfe(rt[SLOT], 0, 1);                                               \
-    w_.y = v_.y & __builtin_amdgcn_sbfe(rt[SLOT], 1, 1);                                               \
-    w_.z = v_.z & __builtin_amdgcn_sbfe(rt[SLOT], 2, 1);                                               \
-    w_.w = v_.w & __builtin_amdgcn_sbfe(rt[SLOT], 3, 1);                                               \
+    w_.x = v_.x & __builtin_amdgcn_sbfe((int)tmc[0], rt[SLOT], 1);                                     \
+    w_.y = v_.y & __builtin_amdgcn_sbfe((int)tmc[1], rt[SLOT], 1);                                     \
+    w_.z = v_.z & __builtin_amdgcn_sbfe((int)tmc[2], rt[SLOT], 1);                                     \
+    w_.w = v_.w & __builtin_amdgcn_sbfe((int)tmc[3], rt[SLOT], 1);                                     \
     rb0[SLOT] = __builtin_bit_cast(cp_floatx4, w_);                                                    \
   }                                                                                                    \
   __builtin_amdgcn_s_setprio(1);                                                                       \
@@ -282,16 +289,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
   for (int d = 0; d < D; ++d)
     if (d < total) CP_LOAD(d);
   int ct = 0, cs = 0, py_next = py0;  // consumer k-step / step, first pooled row not yet stored
-  for (int g0 = 0; g0 < total; g0 += D) {
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      if (g0 + d < total) {
-        CP_MFMA(d);
-        __builtin_amdgcn_sched_barrier(0);
-        if (g0 + d + D < total) CP_LOAD(d);
-        __builtin_amdgcn_sched_barrier(0);
-        if (++ct == nks) {
-          ct = 0;
+  // epilogue of step cs (once per step): bias + Relu, 3x3 maxima into the LDS ring, barrier, stores
+  auto cp_epilogue = [&]() {
           // ---- epilogue of step cs: bias + Relu, 3x3 maxima into the LDS ring ----
           int qd = q0 + cs * (16 * NW) + wave * 16 + lj;
           const bool qv = qd < nq;
@@ -372,10 +371,41 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
           }
           if (py_end > py_next) py_next = py_end;
           if constexpr (DB) __syncthreads();  // the clears land before the next step's maxima
-          ++cs;
+#pragma unroll
+    for (int q_ = 0; q_ < 4; ++q_) tmc[q_] = tmask[q_];
+    ++cs;
+  };
+  if constexpr (MODE != CP_S2) {
+    // stride-1 modes (host: nks % D == 0): the ring-slot pattern repeats every step, so the epilogue
+    // follows the step's k-steps once in the code (conv1's 37 k-steps keep the rolling form below)
+    for (int g0 = 0; g0 < total; g0 += nks) {
+      for (int s0 = 0; s0 < nks; s0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          CP_MFMA(d);
+          __builtin_amdgcn_sched_barrier(0);
+          if (g0 + s0 + d + D < total) CP_LOAD(d);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      cp_epilogue();
+    }
+  } else {
+  for (int g0 = 0; g0 < total; g0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (g0 + d < total) {
+        CP_MFMA(d);
+        __builtin_amdgcn_sched_barrier(0);
+        if (g0 + d + D < total) CP_LOAD(d);
+        __builtin_amdgcn_sched_barrier(0);
+        if (++ct == nks) {
+          ct = 0;
+          cp_epilogue();
         }
       }
     }
+  }
   }
 #undef CP_LOAD
 #undef CP_MFMA
@@ -403,10 +433,12 @@ static int cp_ring(const ConvParams& p, int variant) {
   }
   return val;
 }
+static int cp_mode(const ConvParams& p);
 static size_t cp_lds_bytes(const ConvParams& p, int variant) {
   int mf, nw;
   cp_shape(variant, p.M, &mf, &nw);
-  return size_t(cp_ring(p, variant)) * 16 * mf * p.ep_Wo * 4;
+  const size_t tab = cp_mode(p) == CP_T3 ? size_t(4 * ((p.K + 3) / 4)) * 8 : 0;  // the T3 tap table
+  return size_t(cp_ring(p, variant)) * 16 * mf * p.ep_Wo * 4 + tab;
 }
 static int cp_lead(const ConvParams& p) { return ((p.pt * p.W + p.pl) * 4 + 15) & ~15; }
 
@@ -420,17 +452,18 @@ static int cp_mode(const ConvParams& p) {
   if (p.sh == 2 && p.sw == 2 && p.pt == 0 && p.pl == 0 && p.kw >= 4 && p.kh >= 1 && 2 * (p.Ho - 1) + p.kh <= p.H &&
       2 * (p.Wo - 1) + p.kw <= p.W)
     return CP_S2;
-  if (p.kh == 1 && p.kw == 1 && p.sh == 1 && p.sw == 1 && p.pt == 0 && p.pl == 0 && p.Ho == p.H && p.Wo == p.W)
+  if (p.kh == 1 && p.kw == 1 && p.sh == 1 && p.sw == 1 && p.pt == 0 && p.pl == 0 && p.Ho == p.H && p.Wo == p.W &&
+      p.C % (4 * ORE_CP_D) == 0)
     return CP_1X1;
   if (p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.pt <= 1 && p.pl <= 1 && p.Wo == p.W && p.Ho == p.H &&
-      p.W >= 3 && p.x_guard >= cp_lead(p) && p.x_bytes + cp_lead(p) < (1LL << 31))
+      p.W >= 3 && p.x_guard >= cp_lead(p) && p.x_bytes + cp_lead(p) < (1LL << 31) && (9 * p.C) % (4 * ORE_CP_D) == 0)
     return CP_T3;
   return -1;
 }
 
 bool conv_pool_stream_eligible(const ConvParams& p, int variant) {
   if (variant < 2 || variant > 6 || cp_mode(p) < 0) return false;
-  if ((variant == 3 || variant == 6) && p.M < 64) return false;  // mostly idle rows
+  if ((variant == 3 || variant == 6) && (p.M < 64 || cp_mode(p) != CP_S2)) return false;  // idle rows / spills
   if ((variant == 4 || variant == 5) && p.M < 48) return false;
   if (variant == 5 && p.ep_Ho < 6) return false;
   return cp_lds_bytes(p, variant) <= size_t(variant == 3 ? 152 : 78) * 1024;
@@ -456,10 +489,14 @@ static void launch_cp(const ConvParams& p0, size_t lds, int nbands, int nring, h
 
 template <int MF, int NW, bool DB = false>
 static void launch_cp_mode(const ConvParams& p, size_t lds, int nbands, int nring, hipStream_t s) {
-  switch (cp_mode(p)) {
-    case CP_S2: launch_cp<MF, ORE_CP_D, NW, CP_S2, DB>(p, lds, nbands, nring, s); break;
-    case CP_1X1: launch_cp<MF, ORE_CP_D, NW, CP_1X1, DB>(p, lds, nbands, nring, s); break;
-    default: launch_cp<MF, ORE_CP_D, NW, CP_T3, DB>(p, lds, nbands, nring, s); break;
+  if constexpr (MF == 6) {  // the 96-channel tiles: conv1 only (the stride-1 modes would spill)
+    launch_cp<MF, ORE_CP_D, NW, CP_S2, DB>(p, lds, nbands, nring, s);
+  } else {
+    switch (cp_mode(p)) {
+      case CP_S2: launch_cp<MF, ORE_CP_D, NW, CP_S2, DB>(p, lds, nbands, nring, s); break;
+      case CP_1X1: launch_cp<MF, ORE_CP_D, NW, CP_1X1, DB>(p, lds, nbands, nring, s); break;
+      default: launch_cp<MF, ORE_CP_D, NW, CP_T3, DB>(p, lds, nbands, nring, s); break;
+    }
   }
 }
 

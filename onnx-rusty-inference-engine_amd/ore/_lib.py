@@ -16,7 +16,7 @@ ORE_OK = 0
 STATUS_NAMES = {0: "ORE_OK", 1: "ORE_ERR_INVALID", 2: "ORE_ERR_UNSUPPORTED", 3: "ORE_ERR_HIP",
                 4: "ORE_ERR_OOM", 5: "ORE_ERR_PARSE"}
 
-FUSE_CONV_RELU, FUSE_CONCAT, FUSE_ALIAS, FUSE_ALL, KEEP_VALUES, FUSE_POOL_CONV, FUSE_CONV_POOL = 1, 2, 4, 103, 8, 16, 32
+FUSE_CONV_RELU, FUSE_CONCAT, FUSE_ALIAS, FUSE_ALL, KEEP_VALUES, FUSE_POOL_CONV, FUSE_CONV_POOL = 1, 2, 4, 231, 8, 16, 32
 FUSE_FIRE = 64
 FUSE_CONCAT_POOL = 128
 LOAD_F16 = 1  # ore_model_load_ex flag: the fp16 variant
