@@ -233,7 +233,9 @@ def main():
             if os.path.exists(tfile):
                 with open(tfile) as f:
                     tj = json.load(f)
-                traffic, tsrc = round(tj["hbm_bytes_per_launch"]), f"profiles/pmc_traffic_{args.precision}.json"
+                traffic = round(tj["hbm_bytes_per_launch"])
+                tsrc = (f"profiles/pmc_traffic_{args.precision}.json: PMC FETCH_SIZE/WRITE_SIZE passes of an earlier "
+                        f"rocprofv3 run ({tj.get('source', 'tools/pmc.sh')}), not measured in this run")
             result["roofline"] = {
                 "bound": "mfma", "kernel": kname,
                 "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",

@@ -141,6 +141,11 @@ ore_status ore_reshape(const ore_tensor* x, const int64_t* shape, int32_t n_shap
  * Unsupported ops/attributes fail here (the reference panics when it reaches them). */
 ore_status ore_model_load(ore_ctx* ctx, const void* onnx_bytes, size_t len, int64_t max_batch,
                           ore_model** out);
+/* Host-only wire-format check of an ONNX ModelProto, the reference's
+ * `ModelProto::parse_from_bytes` (main.rs:30) before any inference: ORE_OK, or ORE_ERR_PARSE for
+ * malformed protobuf (truncated payloads, a field sent with the wrong wire type, ...) with the
+ * reason in ore_last_error(NULL).  Touches no device; ore_model_load runs the same parser. */
+ore_status ore_model_parse(const void* onnx_bytes, size_t len);
 /* Load flags.  ORE_LOAD_F16: the fp16 variant (no reference
  * counterpart -- the reference is f32 only): Conv weights and the activations of Conv / MaxPool /
  * Relu / Concat / Dropout are f16, Conv accumulates in f32 on the f16 matrix cores (bias and Relu

@@ -27,6 +27,8 @@
 // each conv output is the same k-ordered MFMA chain + bias as conv_gemm_kernel's: bit-identical.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <algorithm>
 #include <vector>
 
@@ -475,12 +477,17 @@ static void launch_cp(const ConvParams& p0, size_t lds, int nbands, int nring, h
   p.mtiles = (p.M + 16 * MF - 1) / (16 * MF);
   p.x_lead = MODE == CP_T3 ? cp_lead(p) : 0;
   const int qrow = (p.Wo + 3) / 4;
-  if (lds > 64 * 1024) {  // above the default dynamic-LDS limit (once per process and instantiation)
-    static bool raised = false;
-    if (!raised) {
+  if (lds > 64 * 1024) {
+    // above the default dynamic-LDS limit: raise it once per DEVICE and instantiation (the
+    // attribute binds to the current device; one ore_ctx per device may call from its own thread)
+    static std::atomic<unsigned long long> raised{0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (!(raised.load(std::memory_order_acquire) & bit)) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pool_stream_kernel<MF, D, NW, MODE, DB>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      raised = true;
+      raised.fetch_or(bit, std::memory_order_acq_rel);
     }
   }
   hipLaunchKernelGGL((conv_pool_stream_kernel<MF, D, NW, MODE, DB>), dim3((unsigned)(p.N * nbands * p.mtiles)),

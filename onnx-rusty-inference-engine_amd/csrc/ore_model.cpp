@@ -591,8 +591,10 @@ ore_status plan(ore_model* m) {
   // outputs nor the concat reach HBM.  The MaxPool of a Concat is the Concat of the per-slice
   // MaxPools (the pool is per channel), so every pooled value is the same max of the same nine
   // values.  No patch-work bound: the row-walking kernels (ore_conv_pool.hip) compute no conv output
-  // twice, and ore_model_autotune keeps the patch kernel only where it is faster.  Opt-in
-  // (ORE_FUSE_CONCAT_POOL): measured slower than the streaming expands + the chunk-staged pool.
+  // twice, and ore_model_autotune keeps the patch kernel only where it is faster.  On by default
+  // (ORE_FUSE_CONCAT_POOL is in ORE_FUSE_ALL) for pooled planes of >= 1024 pixels, i.e. fire4 ->
+  // pool3 (-40 us per B=256 step); fire8 -> pool5 (27^2 planes) stays unfused, measured slower
+  // (DESIGN.md section 9).
   if ((m->fusion & ORE_FUSE_CONCAT_POOL) && (m->fusion & ORE_FUSE_CONV_POOL) && (m->fusion & ORE_FUSE_CONCAT) &&
       !m->f16) {
     for (size_t i = 0; i < m->steps.size(); ++i) {
@@ -1072,6 +1074,14 @@ ore_status ore_model_load(ore_ctx* ctx, const void* bytes, size_t len, int64_t m
   return ore_model_load_ex(ctx, bytes, len, max_batch, 0, out);
 }
 
+ore_status ore_model_parse(const void* bytes, size_t len) {
+  if (!bytes) return set_error(nullptr, ORE_ERR_INVALID, "null argument");
+  Graph g;
+  std::string perr;
+  if (!parse_model(static_cast<const uint8_t*>(bytes), len, &g, &perr)) return set_error(nullptr, ORE_ERR_PARSE, "%s", perr.c_str());
+  return ORE_OK;
+}
+
 ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_t max_batch, int32_t flags,
                              ore_model** out) {
   if (!ctx || !bytes || !out || max_batch <= 0) return set_error(ctx, ORE_ERR_INVALID, "invalid argument");
@@ -1319,6 +1329,23 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
     const Value& rv = m->values[rid];
     if (!rv.is_const && rv.first < 0 && !rv.is_input)
       return set_error(ctx, ORE_ERR_INVALID, "value '%s' not materialised", name);
+    // Without ORE_KEEP_VALUES the arena reuses slots by liveness: a value whose bytes a later value
+    // (first write after this one's last read) overlaps was overwritten during the run -> refuse
+    // rather than return stale data.
+    if (!(m->fusion & ORE_KEEP_VALUES) && rv.arena_off >= 0) {
+      auto extent = [&](const Value& x) {
+        return ((x.image_stride() * m->max_batch * x.es) + 255) / 256 * 256;
+      };
+      const int64_t lo = rv.arena_off, hi = rv.arena_off + extent(rv);
+      for (size_t j = 0; j < m->values.size(); ++j) {
+        const Value& o = m->values[j];
+        if (int(j) == rid || o.arena_off < 0 || o.alias_of >= 0 || o.is_const || o.is_input || o.elided) continue;
+        if (o.first > rv.last && o.arena_off < hi && lo < o.arena_off + extent(o))
+          return set_error(ctx, ORE_ERR_INVALID,
+                           "value '%s' was overwritten by a later value in the arena (load with ORE_KEEP_VALUES "
+                           "to read intermediate values)", name);
+      }
+    }
   }
   ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
   ORE_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));

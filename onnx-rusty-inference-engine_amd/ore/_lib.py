@@ -28,7 +28,7 @@ EXPORTED = [
     "ore_sync", "ore_last_error", "ore_malloc", "ore_free", "ore_upload", "ore_download",
     "ore_conv_out_shape", "ore_pool_out_shape", "ore_conv2d_f32", "ore_maxpool2d_f32", "ore_relu_f32",
     "ore_add_f32", "ore_softmax_f32", "ore_matmul_f32", "ore_gap_f32", "ore_concat_f32", "ore_dropout_f32",
-    "ore_reshape", "ore_model_load", "ore_model_load_ex", "ore_model_destroy", "ore_model_set_fusion", "ore_model_input_dims",
+    "ore_reshape", "ore_model_parse", "ore_model_load", "ore_model_load_ex", "ore_model_destroy", "ore_model_set_fusion", "ore_model_input_dims",
     "ore_model_output_elems", "ore_model_run", "ore_model_read_value", "ore_model_autotune",
     "ore_model_step_tile", "ore_model_set_streams",
     "ore_model_graph_capture", "ore_model_graph_launch", "ore_model_enable_timing",
@@ -96,6 +96,7 @@ def load():
         "ore_concat_f32": (i32, [vp, T, T, i64, T]),
         "ore_dropout_f32": (i32, [vp, T, T]),
         "ore_reshape": (i32, [T, I64P, i32, T]),
+        "ore_model_parse": (i32, [ctypes.c_char_p, ctypes.c_size_t]),
         "ore_model_load": (i32, [vp, ctypes.c_char_p, ctypes.c_size_t, i64, ctypes.POINTER(vp)]),
         "ore_model_load_ex": (i32, [vp, ctypes.c_char_p, ctypes.c_size_t, i64, i32, ctypes.POINTER(vp)]),
         "ore_model_destroy": (i32, [vp]),

@@ -239,13 +239,28 @@ class Model:
     def set_fusion(self, flags: int):
         check(load().ore_model_set_fusion(self.h, int(flags)), self.ctx.h)
 
-    def run_into(self, x, out):
-        """Asynchronous on the context stream; x [n, C, H, W], out [n, output_elems] (CUDA)."""
+    def _check_io(self, x, out):
+        """The walker reads x and writes out through raw device pointers: both must be contiguous
+        float32 tensors on this context's device, x [n, C, H, W] with n <= max_batch and out holding
+        n * output_elems floats (the same contract _desc() enforces for the per-op entries)."""
+        torch = _torch()
+        for name, t in (("x", x), ("out", out)):
+            if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype != torch.float32:
+                raise OreError(1, f"{name}: expected a float32 CUDA tensor")
+            if t.device.index != self.ctx.device:
+                raise OreError(1, f"{name}: on cuda:{t.device.index}, the context is on cuda:{self.ctx.device}")
+            if not t.is_contiguous():
+                raise OreError(1, f"{name}: expected a contiguous tensor")
         n = x.shape[0]
         if tuple(x.shape[1:]) != self.input_dims:
             raise OreError(1, f"input dims {tuple(x.shape[1:])} != model {self.input_dims}")
-        if not (x.is_contiguous() and out.is_contiguous()) or out.numel() < n * self.output_elems:
-            raise OreError(1, "bad input/output buffers")
+        if out.numel() < n * self.output_elems:
+            raise OreError(1, f"out holds {out.numel()} floats, {n} images need {n * self.output_elems}")
+        return n
+
+    def run_into(self, x, out):
+        """Asynchronous on the context stream; x [n, C, H, W], out [n, output_elems] (CUDA)."""
+        n = self._check_io(x, out)
         check(load().ore_model_run(self.h, ctypes.c_void_p(x.data_ptr()), int(n), ctypes.c_void_p(out.data_ptr())),
               self.ctx.h)
         return out
@@ -267,8 +282,7 @@ class Model:
 
     def autotune(self, x, out, reps: int = 3):
         """Per-layer block-tile search on a real run (ore_model_autotune); synchronous."""
-        if tuple(x.shape[1:]) != self.input_dims or not (x.is_contiguous() and out.is_contiguous()):
-            raise OreError(1, "bad input/output buffers")
+        self._check_io(x, out)
         check(load().ore_model_autotune(self.h, ctypes.c_void_p(x.data_ptr()), int(x.shape[0]),
                                         ctypes.c_void_p(out.data_ptr()), int(reps)), self.ctx.h)
 
@@ -292,10 +306,7 @@ class Model:
     def capture(self, x, out):
         """Capture run_into(x, out) as a HIP graph on the context stream (ore_model_graph_capture);
         replay() re-runs it on whatever x / out hold then."""
-        n = x.shape[0]
-        if tuple(x.shape[1:]) != self.input_dims or not (x.is_contiguous() and out.is_contiguous()) \
-                or out.numel() < n * self.output_elems:
-            raise OreError(1, "bad input/output buffers")
+        n = self._check_io(x, out)
         self._graph_bufs = (x, out)  # the graph holds these pointers
         check(load().ore_model_graph_capture(self.h, ctypes.c_void_p(x.data_ptr()), int(n),
                                              ctypes.c_void_p(out.data_ptr())), self.ctx.h)

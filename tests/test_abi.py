@@ -116,3 +116,101 @@ def test_ctx_create_reports_missing_gpu():
     st = ore.load().ore_ctx_create(0, ctypes.byref(h))
     assert st == 3  # ORE_ERR_HIP, no crash
     assert np.isscalar(st)
+
+
+# --------------------------------------------------------------- wire-format hardening (host only)
+def _parse(buf: bytes) -> int:
+    return ore.load().ore_model_parse(buf, len(buf))
+
+
+def test_parse_accepts_models():
+    from ore import squeezenet
+    mnist = open(os.path.join(HERE, "golden", "mnist-8.onnx"), "rb").read()
+    assert _parse(mnist) == 0
+    assert _parse(squeezenet.build(64)) == 0
+
+
+def _mini_model(node_fields=None, attr=None, tensor_fields=None):
+    """A one-Relu model whose node / attribute / initializer payloads the caller can replace."""
+    from ore import onnx_wire as w
+    node = node_fields if node_fields is not None else w.encode_node("Relu", ["x"], ["y"], attrs=[attr] if attr else [])
+    init = tensor_fields if tensor_fields is not None else w.encode_tensor("b", np.zeros(3, np.float32))
+    return w.encode_model("g", [node], [init], [w.encode_value_info("x", [1, 3])], [w.encode_value_info("y", [1, 3])])
+
+
+def test_parse_rejects_wire_type_mismatch():
+    """a string / bytes / packed field sent as a varint (or a float attribute that is not
+    a 4-byte fixed32) is malformed input -> ORE_ERR_PARSE, never a read through a stale pointer."""
+    from ore import onnx_wire as w
+    PARSE = 5  # ORE_ERR_PARSE
+    assert _parse(_mini_model()) == 0
+    # NodeProto.input (1) as a varint
+    assert _parse(_mini_model(node_fields=w._vi(1, 5) + w._ld(2, b"y") + w._ld(4, b"Relu"))) == PARSE
+    # NodeProto.op_type (4) as a fixed32
+    assert _parse(_mini_model(node_fields=w._ld(1, b"x") + w._ld(2, b"y") + w._key(4, 5) + b"Relu")) == PARSE
+    # AttributeProto.s (4) as a varint, AttributeProto.name (1) as a varint
+    assert _parse(_mini_model(attr=w._ld(1, b"a") + w._vi(20, 3) + w._vi(4, 7))) == PARSE
+    assert _parse(_mini_model(attr=w._vi(1, 9) + w._vi(20, 2) + w._vi(3, 1))) == PARSE
+    # AttributeProto.f (2): a varint, and an 8-byte fixed64
+    assert _parse(_mini_model(attr=w._ld(1, b"a") + w._vi(20, 1) + w._vi(2, 1))) == PARSE
+    assert _parse(_mini_model(attr=w._ld(1, b"a") + w._vi(20, 1) + w._key(2, 1) + b"\0" * 8)) == PARSE
+    # TensorProto.name (8) / float_data (4) / raw_data (9) as varints; float_data not a multiple of 4
+    good = w._vi(1, 3) + w._vi(2, 1)
+    assert _parse(_mini_model(tensor_fields=good + w._ld(9, b"\0" * 12) + w._vi(8, 1))) == PARSE
+    assert _parse(_mini_model(tensor_fields=good + w._vi(4, 1) + w._ld(8, b"b"))) == PARSE
+    assert _parse(_mini_model(tensor_fields=good + w._vi(9, 1) + w._ld(8, b"b"))) == PARSE
+    assert _parse(_mini_model(tensor_fields=good + w._ld(4, b"\0" * 10) + w._ld(8, b"b"))) == PARSE
+    # TensorProto.data_type (2) as length-delimited
+    assert _parse(_mini_model(tensor_fields=w._vi(1, 3) + w._ld(2, b"\1") + w._ld(8, b"b"))) == PARSE
+    # ModelProto.graph (7) as a varint; truncated buffer
+    assert _parse(w._vi(1, 3) + w._vi(7, 1)) == PARSE
+    mnist = open(os.path.join(HERE, "golden", "mnist-8.onnx"), "rb").read()
+    assert _parse(mnist[: len(mnist) // 2]) == PARSE
+    assert b"malformed" in ore.load().ore_last_error(None)
+
+
+def test_parse_fuzz_mutated_mnist():
+    """Random byte mutations of mnist-8.onnx (the reference's own model): the parser returns OK or
+    ORE_ERR_PARSE and never crashes.  Run in a child process so a crash fails this test cleanly."""
+    import subprocess
+    import sys
+    code = f"""
+import sys, random
+sys.path[:0] = {[os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "onnx-rusty-inference-engine_amd")]!r}
+import ore
+L = ore.load()
+buf = bytearray(open({os.path.join(HERE, "golden", "mnist-8.onnx")!r}, "rb").read())
+rng = random.Random(1234)
+seen = set()
+for it in range(3000):
+    b = bytearray(buf)
+    for _ in range(rng.randint(1, 4)):
+        i = rng.randrange(min(len(b), 4096)) if rng.random() < 0.8 else rng.randrange(len(b))
+        b[i] = rng.randrange(256)
+    if rng.random() < 0.2:
+        b = b[: rng.randrange(len(b))]
+    st = L.ore_model_parse(bytes(b), len(b))
+    assert st in (0, 5), st
+    seen.add(st)
+print(sorted(seen))
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "5" in r.stdout  # some mutations were rejected
+
+
+def test_model_io_checks_host():
+    """run_into / autotune / capture hand raw pointers to the walker, so they reject what
+    _desc() rejects for the per-op entries (checked here on CPU tensors, before any device call)."""
+    import torch
+    m = object.__new__(ore.Model)
+    m.ctx = type("C", (), {"device": 0})()
+    m.input_dims = (3, 8, 8)
+    m.output_elems = 10
+    x = torch.zeros((2, 3, 8, 8))
+    out = torch.zeros((2, 10))
+    for fn in (m.run_into, m.autotune, m.capture):
+        with pytest.raises(ore.OreError, match="float32 CUDA"):
+            fn(x, out)
+        with pytest.raises(ore.OreError, match="float32 CUDA"):
+            fn(x.double(), out)

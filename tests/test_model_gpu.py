@@ -423,7 +423,8 @@ def test_conv_pool_walk_stride1_bit_identical(gpu_ctx, case, monkeypatch):
 
 @pytest.mark.parametrize("hw", [64, 224])
 def test_squeezenet_concat_pool_fusion(gpu_ctx, hw, monkeypatch):
-    """Opt-in ORE_FUSE_CONCAT_POOL (fire4 -> pool3, fire8 -> pool5 pooled in the expand convs'
+    """ORE_FUSE_CONCAT_POOL (in FUSE_ALL; by default fire4 -> pool3 only, here forced onto fire8 ->
+    pool5 too with ORE_CONCAT_POOL_MIN_HW=0: the pools computed in the expand convs'
     epilogues, the expand outputs and their concat never stored): every value the fused graph
     materialises -- pool3 / pool5 included -- and the probabilities equal the unfused run's bit
     for bit; the row-walking kernel runs for the pooled expands."""
@@ -545,3 +546,97 @@ def test_squeezenet_fire_fusion(gpu_ctx, hw, monkeypatch):
             assert sum(1 for t in m.tiles() if t >= 0 and ore.Model.TILE_NAMES[t] == "fire") == (5 if hw == 224 else 2)
         m.close()
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def test_model_io_checks_gpu(gpu_ctx):
+    """an f16 / f64 output or input, or a non-contiguous one, is refused before the
+    walker sees the pointer (an f16 out would otherwise take 2x its size in f32 stores)."""
+    import torch
+    import ore
+    m = ore.Model(gpu_ctx, _mnist_bytes(), max_batch=4)
+    x = torch.zeros((2, 1, 28, 28), device="cuda")
+    out = torch.zeros((2, 10), device="cuda")
+    m.run_into(x, out)
+    for fn in (m.run_into, m.autotune, m.capture):
+        with pytest.raises(ore.OreError, match="float32 CUDA"):
+            fn(x, out.half())
+        with pytest.raises(ore.OreError, match="float32 CUDA"):
+            fn(x.double(), out)
+        with pytest.raises(ore.OreError, match="contiguous"):
+            fn(torch.zeros((2, 1, 28, 56), device="cuda")[..., ::2], out)
+        with pytest.raises(ore.OreError, match="holds"):
+            fn(x, torch.zeros((1, 10), device="cuda"))
+    m.close()
+
+
+def test_read_value_refuses_overwritten(gpu_ctx):
+    """without ORE_KEEP_VALUES the arena reuses slots, so an early intermediate whose
+    bytes a later value overwrote is refused (not returned stale); the graph output and, with
+    KEEP_VALUES, every value stay readable."""
+    import ore
+    from ore import squeezenet
+    mb = squeezenet.build(64)
+    x = _t(squeezenet.synthetic_input(2, 64, seed=3))
+    m = ore.Model(gpu_ctx, mb, max_batch=2)
+    m.set_fusion(0)  # op by op: every node's output is a value of its own
+    y = _np(m.run(x))
+    from ore import onnx_wire
+    g = onnx_wire.decode_model(mb).graph
+    names = [n.output[0] for n in g.node]
+    refused = 0
+    for nm in names[:10]:
+        try:
+            m.read_value(nm)
+        except ore.OreError as e:
+            assert "overwritten" in str(e)
+            refused += 1
+    assert refused > 0  # op-by-op SqueezeNet reuses the early slots
+    keep = ore.Model(gpu_ctx, mb, max_batch=2)
+    keep.set_fusion(ore.KEEP_VALUES)
+    np.testing.assert_array_equal(_np(keep.run(x)), y)
+    for nm in names[:10]:
+        keep.read_value(nm)
+    m.close()
+    keep.close()
+
+
+def test_two_contexts_large_lds_variant(monkeypatch):
+    """the 152 KiB row-walking conv1 + pool1 variant raises its dynamic-LDS limit per
+    device (not once per process); two contexts driven from two host threads both run the
+    batch-128 conv1 + pool1 step and agree bit for bit."""
+    import threading
+    import torch
+    import ore
+    C, H, M, k = 3, 45, 96, 7
+    rng = np.random.default_rng(5)
+    w = (rng.standard_normal((M, C, k, k)) * 0.3).astype(np.float32)
+    b = rng.uniform(-0.5, 0.5, M).astype(np.float32)
+    mb = _conv_pool_model((1, C, H, H), w, b, [0] * 4, [2, 2], True, [3, 3], [2, 2], [0, 0, 0, 0])
+    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "100")
+    monkeypatch.setenv("ORE_CONV_POOL_STREAM", "2")  # variant 3: 96 channels x 128 quads, 152 KiB of LDS
+    x = torch.from_numpy(rng.standard_normal((128, C, H, H)).astype(np.float32)).cuda()
+    res, errs = [None, None], []
+
+    def work(i):
+        try:
+            torch.cuda.set_device(0)
+            ctx = ore.Context(0, use_torch_stream=False)
+            m = ore.Model(ctx, mb, max_batch=128)
+            m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+            out = torch.empty((128, m.output_elems), device="cuda")
+            m.run_into(x, out)
+            ctx.sync()
+            res[i] = m.read_value("p")
+            assert "epool walk96" in [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+            m.close()
+            ctx.close()
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    np.testing.assert_array_equal(res[0], res[1])
