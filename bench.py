@@ -45,8 +45,10 @@ def parse():
     ap.add_argument("--no-autotune", action="store_true", help="keep the heuristic per-layer conv tiles")
     ap.add_argument("--dump-steps", default="", help="write the plan's kernel steps (op, name, flops, bytes) as JSON")
     ap.add_argument("--fusion", type=int, default=None, help="ore_model_set_fusion flags (experiments; default: the model's)")
-    ap.add_argument("--precision", choices=["f32", "f16"], default="f32",
-                    help="f16: the fp16 variant (SURVEY.md §8(f)3, config 5); the headline metric is f32")
+    ap.add_argument("--precision", choices=["f32", "f32x3", "f16"], default="f32",
+                    help="f32: convs on the f32-input MFMA; f32x3: the same f32 model with its convs on the BF16 "
+                         "matrix cores by an exact 3-way bf16 split (ORE_LOAD_X3); f16: the fp16 variant "
+                         "(SURVEY.md §8(f)3, config 5)")
     return ap.parse_args()
 
 
@@ -139,6 +141,7 @@ def main():
     ctx = ore.Context(local)
     model = ore.Model(ctx, model_bytes, max_batch=B, precision=args.precision)
     f16 = args.precision == "f16"
+    x3 = args.precision == "f32x3"
     g = torch.Generator(device=f"cuda:{local}")
     g.manual_seed(1000 + rank)
     x = (torch.rand((B, 3, args.hw, args.hw), generator=g, device=f"cuda:{local}") * 100.0 - 50.0).contiguous()
@@ -199,10 +202,10 @@ def main():
         result = {
             "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "higher_is_better": True,
-            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": args.precision,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f16" if f16 else "f32",
             "data": "synthetic (seeded U(-50,50) 3x224x224 images; seeded He-normal SqueezeNet-1.0 weights)",
             "config": {"workload": f"SqueezeNet-1.0 (66 nodes, 818.9 MMAC/img) "
-                                   f"{'fp16 (config 5: f16 activations/weights, f32 accumulate)' if f16 else 'fp32'} "
+                                   f"{'fp16 (config 5: f16 activations/weights, f32 accumulate)' if f16 else 'fp32 (convs: exact 3-way bf16 split, 6 part products, f32 accumulate)' if x3 else 'fp32'} "
                                    f"inference, batch {B} per GPU, 3x{args.hw}x{args.hw}",
                        "model": "squeezenet1.0-8 topology, synthetic weights", "global_batch": world * B,
                        "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}",
@@ -221,8 +224,11 @@ def main():
                 c["launches"] += 1
             conv = classes.get("Conv", {"ms": 1e-9, "flops": 0.0, "bytes": 0.0, "launches": 1})
             achieved = conv["flops"] / (conv["ms"] * 1e-3) / 1e12
-            peak = PEAK_F16_MFMA_TFLOPS if f16 else PEAK_F32_MFMA_TFLOPS
+            # x3: every f32 MAC is six bf16 part products on the 2.5 PF/s BF16 matrix cores
+            peak = PEAK_F16_MFMA_TFLOPS if f16 else PEAK_F16_MFMA_TFLOPS / 6.0 if x3 else PEAK_F32_MFMA_TFLOPS
             kname = ("conv_f16_kernel (implicit-GEMM MFMA 32x32x16 f16, f32 accumulate" if f16 else
+                     "conv_x3_kernel (f32 implicit GEMM on MFMA 16x16x32 bf16: both operands split exactly into "
+                     "3 bf16 parts, 6 part products per f32 MAC; peak = 2500 / 6 TFLOP/s of f32 work" if x3 else
                      "Conv class: conv_stream_kernel (LDS-free implicit GEMM, MFMA 16x16x4 f32), fire_kernel (fire "
                      "module + next squeeze), conv_pool_stream_kernel (conv1 + pool1 row walk) and conv_gemm_kernel "
                      "(LDS-staged, MFMA 32x32x2 f32) per the autotuned tile") + f", {conv['launches']} launches/step)"

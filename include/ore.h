@@ -153,6 +153,16 @@ ore_status ore_model_parse(const void* onnx_bytes, size_t len);
  * stay f32 (Add / MatMul / Softmax on an f16 value is rejected).  The model input and
  * graph.output[0] stay f32 (an f16 graph output is rejected). */
 #define ORE_LOAD_F16 1
+/* ORE_LOAD_X3: the f32 model on the BF16 matrix cores.  gfx950's f32-input MFMA runs at 1/16 of
+ * the BF16 rate; every f32 weight and activation operand of a Conv / MatMul is split exactly into
+ * three bf16 parts (hi + mid + lo) and the six part products whose orders sum to <= 2 are
+ * accumulated in f32 (v_mfma_f32_16x16x32_bf16).  The dropped products are below 2^-24 of each
+ * a*b, so every output is the f32 dot product to within f32 accumulation rounding (tested against a
+ * float64 reference next to the f32-MFMA kernels' own error, tests/test_x3_gpu.py), at 0.375 of the
+ * f32-MFMA cost.  Storage, every other op and the model input / output stay f32; results are
+ * tile-independent but not bit-identical to the f32-MFMA kernels (a different summation order).
+ * The fire / pooled-conv fusions are f32-MFMA kernels and are not applied to an x3 model. */
+#define ORE_LOAD_X3 2
 ore_status ore_model_load_ex(ore_ctx* ctx, const void* onnx_bytes, size_t len, int64_t max_batch, int32_t flags,
                              ore_model** out);
 ore_status ore_model_destroy(ore_model* m);

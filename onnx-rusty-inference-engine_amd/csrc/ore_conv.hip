@@ -18,6 +18,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "ore_kernels.h"
 
 namespace ore {
@@ -947,9 +949,31 @@ static const int CFG_BN[4] = {128, 128, 128, 256};
 
 
 ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
-                   bool is1x1, bool f16, int xmode) {
+                   bool is1x1, bool f16, int xmode, bool x3) {
   (void)H; (void)W; (void)pt;
   ConvPlan pln{};
+  if (x3 && !f16) {  // ore_conv_x3.hip: packed rows cover every x3 tile (64 / 96 / 128 rows)
+    pln.x3 = 1;
+    pln.cfg = X3_TILE_BASE + x3_tile_config(M);
+    pln.Mp = std::max((M + 127) / 128 * 128, (M + 95) / 96 * 96);
+    pln.krows = conv_packed_kp(C * kh * kw);
+    // stride-1 geometry whose window fits: the window-staged kernel (each input element split once
+    // per block instead of once per tap); ORE_X3_WINDOW=0 keeps the gather kernel (experiments)
+    if (x3w_geometry(C, kh, kw, sh, sw) && env_int("ORE_X3_WINDOW", 1) != 0) {
+      const int t = (Ho * Wo < 256 ? 6 : 4) + (M <= 64 ? 1 : 0);
+      if (x3w_plan_lds(Ho, Wo, kh, kw, C, t) <= 80 * 1024) {
+        pln.x3 = 2;
+        pln.cfg = X3_TILE_BASE + t;
+        pln.bch = x3w_groups(C);
+        pln.nst = (C + 8 * pln.bch - 1) / (8 * pln.bch);
+        pln.ks = (kh * kw * pln.bch + 3) / 4;
+        pln.krows = pln.nst * pln.ks * 32;
+      }
+    }
+    const int forced = env_int("ORE_X3_TILE", -1);  // tuning knob (within the plan's kernel family)
+    if (forced >= 0 && forced < 4) pln.cfg = X3_TILE_BASE + forced + (pln.x3 == 2 ? 4 : 0);
+    return pln;
+  }
   pln.f16 = f16 ? 1 : 0;
   pln.xmode = f16 ? xmode : 0;
   pln.cfg = conv_tile_config(M);
@@ -1016,11 +1040,19 @@ ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, i
 }
 
 size_t conv_packed_bytes(const ConvPlan& pln) {
-  return (size_t)pln.krows * pln.Mp * (pln.f16 ? sizeof(_Float16) : sizeof(float));
+  return (size_t)pln.krows * pln.Mp * (pln.x3 ? 3 * 2 : pln.f16 ? sizeof(_Float16) : sizeof(float));
 }
 
 void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, const ConvPlan& pln, float* wp,
                  hipStream_t s) {
+  if (pln.x3 == 2) {
+    launch_pack_x3w(w, M, C, kh, kw, pln.Mp, pln.bch, pln.ks, pln.nst, wp, s);
+    return;
+  }
+  if (pln.x3) {
+    launch_pack_x3(w, kmajor_src, M, C * kh * kw, pln.Mp, wp, s);
+    return;
+  }
   if (pln.f16) {
     (void)kmajor_src;  // f16 plans are convs only (MatMul stays f32)
     launch_pack_weights_f16(w, pln.xmode, M, C, kh, kw, pln.Mp, wp, s);
@@ -1056,6 +1088,21 @@ thread_local int last_conv_tile = -1;
 
 void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
   last_conv_tile = pln.cfg;
+  if (pln.x3) {  // the caller (run_conv) checked conv_x3_eligible
+    int t = pln.cfg - X3_TILE_BASE;
+    if (pln.x3 == 2) {
+      ConvParams q = p;
+      q.bch = pln.bch; q.nst = pln.nst; q.ks = pln.ks;
+      if (t < 4 || !conv_x3w_eligible(q, t)) t = conv_x3w_eligible(q, 6) ? 6 : 7;  // a window tile that fits
+      last_conv_tile = X3_TILE_BASE + t;
+      launch_conv_x3(q, t, s);
+      return;
+    }
+    if (t >= 4) t = 0;
+    last_conv_tile = X3_TILE_BASE + t;
+    launch_conv_x3(p, t, s);
+    return;
+  }
   if (pln.f16) {
     launch_conv_f16(p, pln.cfg, pln.xmode, s);
     return;

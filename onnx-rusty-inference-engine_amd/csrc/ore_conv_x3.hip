@@ -1,0 +1,632 @@
+// Conv (convolution_op.rs:94-517) and MatMul (mul_op.rs:23) in f32 on the BF16 matrix cores:
+// the "x3" path (ORE_LOAD_X3, include/ore.h).
+//
+// gfx950 has no reduced-precision f32 MFMA (no xf32); its f32-input MFMA runs at 1/16 of the BF16
+// rate (MI355X_MICROARCH.md 'Matrix cores').  An f32 value splits EXACTLY into three bf16 values,
+//   x = hi + mid + lo,  hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid)
+// (round-to-nearest at each step: |mid| <= 2^-8 |x|, |lo| <= 2^-16 |x|, and lo is exact because
+// x - hi - mid has at most 8 significant bits left), and every bf16 x bf16 product is exact in f32.
+// So  a.b = sum over the nine part products;  the six kept here are every product whose parts'
+// orders sum to <= 2 (hh, hm, mh, mm, hl, lh).  The three dropped ones (ml, lm, ll) are below
+// 2^-24 |a.b| each -- under the f32 rounding of the product itself -- so every output is the
+// f32 dot product to within the accumulation rounding, at 6/16 = 0.375 of the f32-MFMA cost:
+// 2.5 PF/s / 6 = 417 TFLOP/s of f32 work against the 157.3 TFLOP/s f32-MFMA peak.  Accumulation is
+// in f32 inside v_mfma_f32_16x16x32_bf16.  Every tile runs the same per-output sequence (K in
+// chunks of 32, the six products in a fixed order), so results do not depend on the tile.
+//
+// Implicit GEMM Y[m][n] = sum_k W[m][k] X[k][n] (+ bias, Relu): m = output channel, n = (image,
+// output pixel), k = (cin, r, s), the reference's order (convolution_op.rs:422-480).
+//   * A (weights): split and packed ONCE at load (launch_pack_x3): per 32-k chunk and part, rows of
+//     64 B (32 bf16), 16-B k-groups XOR-swizzled by row so that the fragment reads are
+//     bank-conflict free; one chunk of the block's rows is a contiguous run -> LDS by 16-B LDS-DMA.
+//   * B (im2col of x, never materialised): each thread gathers 8 consecutive k of one pixel
+//     (dword buffer loads, coalesced across the wave's 64 consecutive pixels; the gather table
+//     and tap masks of conv_gemm_kernel), splits them in registers and writes the three parts
+//     to LDS as 16-B k-groups.  Split work is done once per (pixel, k) per block and shared by
+//     the block's BM output channels.
+//   * Fragments (cdna_hip_programming.md §3): lane l holds A[row l&15][k 8(l>>4)..+7] and
+//     B[k 8(l>>4)..+7][col l&15].  The B rows of a 64-pixel group are permuted so that MFMA g's
+//     column c is pixel 4c + g: each lane's four accumulators of a group are four consecutive
+//     output pixels -> 16-B epilogue stores.
+//   * Block 256 threads = 2x2 waves of 16FM x 16FN; LDS = one chunk (A + B, three parts each),
+//     two blocks per CU (one block's MFMAs run while the other splits / waits at its barrier).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <type_traits>
+
+#include "ore_kernels.h"
+
+namespace ore {
+
+typedef __bf16 x3_bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 x3_bf2 __attribute__((ext_vector_type(2)));
+typedef float x3_f2 __attribute__((ext_vector_type(2)));
+typedef float x3_f4 __attribute__((ext_vector_type(4)));
+typedef unsigned x3_u4 __attribute__((ext_vector_type(4)));
+
+// two floats -> packed bf16 pair (round to nearest even; v_cvt_pk_bf16_f32), a in the low half
+__device__ __forceinline__ unsigned x3_pk(float a, float b) {
+  const x3_f2 v = {a, b};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, x3_bf2));
+}
+
+// exact three-way split of (a, b): a = hi.lo16 + mid.lo16 + lo.lo16 (as f32), b likewise in the high halves
+__device__ __forceinline__ void x3_split(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
+  h = x3_pk(a, b);
+  const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
+  m = x3_pk(ra, rb);
+  const float sa = ra - __uint_as_float(m << 16), sb = rb - __uint_as_float(m & 0xffff0000u);
+  l = x3_pk(sa, sb);
+}
+
+// swizzled position of k-group kg (0..3) in LDS / packed row `row` (64-B rows): the fragment read
+// of lanes {0-3,12-15,20-27} (one ds_read_b128 bank group) then hits 16 distinct 16-B slots
+__host__ __device__ __forceinline__ int x3_slot(int row, int kg) { return kg ^ ((0 - (row >> 2)) & 3); }
+
+// ------------------------------------------------------------------ weight packing
+// w: ONNX [M][K] (kmajor_src 0) or MatMul B [K][M] (1) -> wx[kc][part][Mp][32] bf16 (k-group slots
+// swizzled by row), zero padded to Kp = roundup(K, 32) and Mp rows
+__global__ __launch_bounds__(256) void pack_x3_kernel(const float* __restrict__ w, unsigned* __restrict__ wx, int M,
+                                                      int K, int Mp, int Kp, int kmajor_src) {
+  // one thread per (kc, m, slot, pair): 4 pairs per 16-B slot
+  const long long total = (long long)(Kp / 32) * Mp * 16;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int pr = (int)(i & 3), slot = (int)((i >> 2) & 3);
+    const long long rm = i >> 4;
+    const int m = (int)(rm % Mp), kc = (int)(rm / Mp);
+    const int k = kc * 32 + 8 * x3_slot(m, slot) + 2 * pr;
+    float v[2];
+    for (int e = 0; e < 2; ++e) {
+      const int kk = k + e;
+      v[e] = (kk < K && m < M) ? (kmajor_src ? w[(long long)kk * M + m] : w[(long long)m * K + kk]) : 0.0f;
+    }
+    unsigned h, md, l;
+    x3_split(v[0], v[1], h, md, l);
+    const unsigned parts[3] = {h, md, l};
+    for (int q = 0; q < 3; ++q)  // dword index: ((kc*3 + q)*Mp + m)*16 + slot*4 + pr
+      wx[(((long long)kc * 3 + q) * Mp + m) * 16 + slot * 4 + pr] = parts[q];
+  }
+}
+
+// ------------------------------------------------------------------ the conv
+enum { X3_1X1 = 0, X3_G32 = 1, X3_G64 = 2 };  // operand gather: 1x1 rows; taps <= 32; taps <= 64
+
+template <int FM, int FN, int MODE>
+__global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvParams p) {
+  constexpr int BM = 32 * FM, BN = 32 * FN;  // 2 x 2 waves of 16FM x 16FN
+  constexpr int SA = BM * 64, SB = BN * 64;   // bytes of one part of the A / B chunk image
+  constexpr int NIT = BN * 4 / 256;           // (pixel, k-group) items per thread per chunk
+  constexpr int KGS = 256 / BN;               // k-group step between a thread's items
+  static_assert(FN % 4 == 0 && BN % 64 == 0 && NIT >= 1 && SA % 1024 == 0, "tile");
+  __shared__ __attribute__((aligned(16))) char lds[3 * SA + 3 * SB];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware bijective remap: consecutive tile ids (the M tiles of one N tile first) on one XCD
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
+  const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
+  const int mt = wgid % p.mtiles, nt = wgid / p.mtiles;
+  const int m0 = mt * BM;
+  const int n0 = nt * BN;  // Ntot < 2^31 (host)
+  const int K = p.K, XPS = p.x_ps, YPS = p.y_ps;
+  const int nch = (K + 31) >> 5;
+
+  // ---- gather role: pixel gn of the tile, k-groups kgb + j KGS (j < NIT); kgb is wave-uniform
+  const int gn = tid % BN;
+  const int kgb = __builtin_amdgcn_readfirstlane(tid / BN);
+  const int ntot = (int)p.Ntot;
+  int col = n0 + gn;
+  if (col >= ntot) col = ntot - 1;  // tail columns gather a valid pixel; never stored
+  const int img = col / YPS, pix = col - img * YPS;
+  int xoff;                         // element offset of the pixel's (tap 0) input
+  unsigned tm0 = 0, tm1 = 0;        // gather: bit t = tap t = r kw + s inside the image
+  if constexpr (MODE == X3_1X1) {
+    xoff = img * (int)p.x_nstride + pix;
+  } else {
+    const int oh = pix / p.Wo, ow = pix - oh * p.Wo;  // pix >= Ho Wo: a pad column (rows past Ho)
+    const int ih0 = oh * p.sh - p.pt, iw0 = ow * p.sw - p.pl;
+    xoff = img * (int)p.x_nstride + ih0 * p.W + iw0;
+    for (int r = 0; r < p.kh; ++r) {
+      const bool rok = oh < p.Ho && (unsigned)(ih0 + r) < (unsigned)p.H;
+      for (int s = 0; s < p.kw; ++s) {
+        const int t = r * p.kw + s;
+        const bool ok = rok && (unsigned)(iw0 + s) < (unsigned)p.W;
+        if (t < 32) tm0 |= (ok ? 1u : 0u) << t;
+        else tm1 |= (ok ? 1u : 0u) << (t - 32);
+      }
+    }
+  }
+  const int grow = (gn & ~63) + 16 * (gn & 3) + ((gn >> 2) & 15);  // LDS row of this pixel (MFMA g = gn & 3)
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.wp), (short)0, (int)((long long)nch * 3 * p.Mp * 64), 0x00020000);
+  typedef const __attribute__((address_space(4))) long long* ktab_cptr;
+  const ktab_cptr ktab = (ktab_cptr)p.ktab;
+
+  float rv[NIT][8];
+  // gather chunk c's (pixel, k) values into rv: taps outside the image and k >= K read 0.  Every
+  // load is issued (k >= K at an out-of-range offset), so a gather is always NIT * 8 vector-memory
+  // operations -- the main loop's vmcnt accounting relies on it.
+  auto gather = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) {
+      const int kg0 = c * 32 + 8 * (kgb + j * KGS);  // wave-uniform
+      if constexpr (MODE == X3_1X1) {
+        const int vo = kg0 < K ? xoff * 4 : (int)0x80000000;  // a whole k-group past K: out of range
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = kg0 + e;
+          float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, k * XPS * 4, 0));
+          if (K % 8 != 0 && k >= K) v = 0.0f;  // uniform
+          rv[j][e] = v;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = kg0 + e;
+          const long long w_ = ktab[k];  // Kp entries; k >= K: an entry with r = 2^14
+          const int ex = (int)w_, ey = (int)(w_ >> 32);
+          const int t = (ey >> 16) * p.kw + (ey & 0xffff);
+          const unsigned tm = (MODE == X3_G32 || t < 32) ? tm0 : tm1;
+          const int bit = k < K ? __builtin_amdgcn_sbfe((int)tm, t & 31, 1) : 0;  // 0 / -1
+          const int raw = (int)__builtin_amdgcn_raw_buffer_load_b32(xr, (xoff + ex) * 4, 0, 0);
+          rv[j][e] = __builtin_bit_cast(float, raw & bit);
+        }
+      }
+    }
+  };
+  // split rv and write the three parts of each k-group to LDS
+  auto store_b = [&]() {
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) {
+      x3_u4 h, m, l;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        unsigned hh, mm, ll;
+        x3_split(rv[j][2 * e], rv[j][2 * e + 1], hh, mm, ll);
+        h[e] = hh; m[e] = mm; l[e] = ll;
+      }
+      const int off = 3 * SA + grow * 64 + x3_slot(grow, kgb + j * KGS) * 16;
+      *reinterpret_cast<x3_u4*>(lds + off) = h;
+      *reinterpret_cast<x3_u4*>(lds + off + SB) = m;
+      *reinterpret_cast<x3_u4*>(lds + off + 2 * SB) = l;
+    }
+  };
+  // the A chunk (three parts x BM rows x 64 B, contiguous per part in wx) by 16-B LDS-DMA
+  auto dma_a = [&](int c) {
+    constexpr int PIECES = 3 * SA / 1024;  // 1 KiB per wave-instruction; SA / 1024 pieces per part
+#pragma unroll
+    for (int u = 0; u < (PIECES + 3) / 4; ++u) {
+      const int piece = u * 4 + wave;
+      if (PIECES % 4 == 0 || piece < PIECES) {  // wave-uniform
+        const int q = piece / (SA / 1024), o = (piece - q * (SA / 1024)) * 1024 + lane * 16;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            wr, (__attribute__((address_space(3))) void*)(lds + piece * 1024), 16, (q * p.Mp + m0) * 64 + o,
+            c * 3 * p.Mp * 64, 0, 0);
+      }
+    }
+  };
+
+  x3_f4 acc[FM][FN];
+#pragma unroll
+  for (int f = 0; f < FM; ++f)
+#pragma unroll
+    for (int g = 0; g < FN; ++g) acc[f][g] = x3_f4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets: row (lane & 15) of a 16-row group, k-group lane >> 4 at its swizzled slot
+  const int fslot = x3_slot(lane & 15, lane >> 4) * 16;
+  const int arow = (wm * 16 * FM + (lane & 15)) * 64 + fslot;
+  const int brow = 3 * SA + (wn * 16 * FN + (lane & 15)) * 64 + fslot;
+
+  dma_a(0);
+  gather(0);
+  __builtin_amdgcn_sched_barrier(0);
+  store_b();
+  if (nch > 1) gather(1);
+  __builtin_amdgcn_sched_barrier(0);
+  for (int c = 0; c < nch; ++c) {
+    // chunk c's A (DMA) and B (ds_write) have landed: the DMA is older than the gather of chunk c + 1
+    if (c + 1 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIT * 8) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    x3_bf8 af[3][FM], bf[3][FN];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+#pragma unroll
+      for (int f = 0; f < FM; ++f) af[q][f] = *reinterpret_cast<const x3_bf8*>(lds + q * SA + arow + f * 1024);
+#pragma unroll
+      for (int g = 0; g < FN; ++g) bf[q][g] = *reinterpret_cast<const x3_bf8*>(lds + q * SB + brow + g * 1024);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave holds its fragments: the LDS chunk is free
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 < nch) {
+      dma_a(c + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      store_b();  // chunk c + 1 (gathered during chunk c - 1 / the prologue)
+      if (c + 2 < nch) gather(c + 2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the six part products, smallest first, in the same order for every tile
+#pragma unroll
+    for (int f = 0; f < FM; ++f)
+#pragma unroll
+      for (int g = 0; g < FN; ++g) {
+        x3_f4 a = acc[f][g];
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2][f], bf[0][g], a, 0, 0, 0);  // lo . hi
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][f], bf[2][g], a, 0, 0, 0);  // hi . lo
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][f], bf[1][g], a, 0, 0, 0);  // mid . mid
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][f], bf[0][g], a, 0, 0, 0);  // mid . hi
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][f], bf[1][g], a, 0, 0, 0);  // hi . mid
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][f], bf[0][g], a, 0, 0, 0);  // hi . hi
+        acc[f][g] = a;
+      }
+  }
+
+  // ---- epilogue: fragment f's register e = channel m0 + 16(wm FM + f) + 4(lane >> 4) + e; MFMA g of
+  // group G = pixel n0 + 16 wn FN + 64 G + 4 (lane & 15) + g
+  float* __restrict__ y = p.y;
+#pragma unroll
+  for (int G = 0; G < FN / 4; ++G) {
+    const int n = n0 + wn * 16 * FN + 64 * G + 4 * (lane & 15);
+    if (n >= ntot) continue;
+    const int oi = n / YPS, op = n - oi * YPS;
+    float* yb = y + (unsigned)(oi * (int)p.y_nstride + op);
+#pragma unroll
+    for (int f = 0; f < FM; ++f)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + 16 * (wm * FM + f) + 4 * (lane >> 4) + e;
+        if (m >= p.M) continue;
+        const float b = p.bias ? p.bias[m] : 0.0f;
+        x3_f4 v = {acc[f][4 * G][e] + b, acc[f][4 * G + 1][e] + b, acc[f][4 * G + 2][e] + b, acc[f][4 * G + 3][e] + b};
+        if (p.relu) {
+          v[0] = fmaxf(v[0], 0.0f); v[1] = fmaxf(v[1], 0.0f); v[2] = fmaxf(v[2], 0.0f); v[3] = fmaxf(v[3], 0.0f);
+        }
+        if (p.vec_out) {
+          *reinterpret_cast<x3_f4*>(yb + (unsigned)(m * YPS)) = v;
+        } else {  // 4 pixels that may straddle an image boundary (y_ps % 4 != 0)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int ng = n + g;
+            if (ng >= ntot) break;
+            const int gi = ng / YPS, gp = ng - gi * YPS;
+            y[(unsigned)(gi * (int)p.y_nstride + m * YPS + gp)] = v[g];
+          }
+        }
+      }
+  }
+}
+
+
+// ------------------------------------------------------------------ the window-staged conv (stride 1)
+// For stride-1 convs (every SqueezeNet expand3x3; MNIST's 5x5): a block owns BM output channels x
+// BN consecutive output pixels of ONE image.  The input rows those pixels touch (plus the kernel's
+// halo) are staged ONCE per chunk of 8G channels into LDS, already split: [part][window pixel]
+// [G groups of 8 channels] bf16, so each input element is loaded and split once per block instead
+// of once per tap (the gather kernel's im2col).  B fragments are then read straight from the
+// window at a per-tap offset: k = (chunk, tap, channel group, channel), i.e. 8 consecutive
+// channels of one tap per fragment k-group (ORE_LOAD_X3 does not keep the reference's (c, r, s)
+// summation order; it is f32-accurate either way, tests/test_x3_gpu.py).  A (weights, packed per
+// k-step by launch_pack_x3w) goes global -> registers with one k-step of prefetch: no LDS and no
+// barrier in the main loop (the two waves sharing an A row range hit the CU's L1).
+template <int FM, int FN, int G, int SACC>
+__global__ __launch_bounds__(256, 2) void conv_x3w_kernel(ConvParams p) {
+  constexpr int BM = 32 * FM, BN = 32 * FN;
+  constexpr int RB = G * 16;  // bytes per window pixel per part
+  extern __shared__ __attribute__((aligned(16))) char wlds[];
+  const int PB = p.wr * p.ww * RB;  // bytes of one part of the window
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
+  const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
+  const int mt = wgid % p.mtiles, nt = wgid / p.mtiles;
+  const int img = nt / p.tiles_per_img, tile = nt - img * p.tiles_per_img;
+  const int m0 = mt * BM;
+  const int P = p.P, Wo = p.Wo, ww = p.ww;
+  const int p0 = tile * BN;
+  const int oh_first = p0 / Wo;
+  const int pend = (p0 + BN < P ? p0 + BN : P) - 1;
+  const int nwp = ((pend / Wo) - oh_first + p.kh) * ww;  // window pixels this tile uses (<= p.wr * ww)
+  const int ih_first = oh_first - p.pt;
+  const int ntaps = p.kh * p.kw;
+
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
+  const int nsteps = p.ks;  // k-steps (32 k) per chunk
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.wp), (short)0, (int)((long long)p.nst * nsteps * 3 * p.Mp * 64), 0x00020000);
+
+  // B fragment bases: MFMA g's column c is pixel p0 + 16 (wn FN + g) + c (clamped into the plane)
+  int wbase[FN];
+#pragma unroll
+  for (int g = 0; g < FN; ++g) {
+    int pp = p0 + 16 * (wn * FN + g) + (lane & 15);
+    if (pp > P - 1) pp = P - 1;
+    const int oh = pp / Wo, ow = pp - oh * Wo;
+    wbase[g] = (oh - oh_first) * ww + ow;
+  }
+  // A fragment source: row m0 + 16 (wm FM + f) + (lane & 15), k-group lane >> 4 (unswizzled packing)
+  const int aoff = (m0 + 16 * wm * FM + (lane & 15)) * 64 + (lane >> 4) * 16;
+  const int astep = 3 * p.Mp * 64;  // bytes per k-step of packed weights
+
+  x3_f4 acc[FM][FN];
+#pragma unroll
+  for (int f = 0; f < FM; ++f)
+#pragma unroll
+    for (int g = 0; g < FN; ++g) acc[f][g] = x3_f4{0.f, 0.f, 0.f, 0.f};
+
+  x3_bf8 af[2][3][FM];  // A fragments of two k-steps (static indices only: the loop below is unrolled by 2)
+  auto load_a = [&](auto bufc, int gs) {
+    constexpr int buf = decltype(bufc)::value;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+        af[buf][q][f] = __builtin_bit_cast(
+            x3_bf8, __builtin_amdgcn_raw_buffer_load_b128(wr, aoff + (q * p.Mp + 16 * f) * 64, gs * astep, 0));
+  };
+  // stage channels [8G ch, 8G (ch + 1)) of the window, split (every element once)
+  auto stage = [&](int ch) {
+    if (ch > 0) __syncthreads();  // every wave is done with the previous chunk's window
+    const int c0 = ch * 8 * G;
+    for (int i = tid; i < nwp * G; i += 256) {
+      const int g = i / nwp, wpix = i - g * nwp;
+      const int wrow = wpix / ww, wc = wpix - wrow * ww;
+      const int ih = ih_first + wrow, iw = wc - p.pl;
+      const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && c0 + 8 * g < p.C;
+      const int vo = ok ? (img * (int)p.x_nstride + (c0 + 8 * g) * p.x_ps + ih * p.W + iw) * 4 : (int)0x80000000;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, j * p.x_ps * 4, 0));
+      x3_u4 h, m, l;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        unsigned hh, mm, ll;
+        x3_split(v[2 * e], v[2 * e + 1], hh, mm, ll);
+        h[e] = hh; m[e] = mm; l[e] = ll;
+      }
+      const int slot = G == 4 ? x3_slot(wpix, g) : g;
+      char* dst = wlds + wpix * RB + slot * 16;
+      *reinterpret_cast<x3_u4*>(dst) = h;
+      *reinterpret_cast<x3_u4*>(dst + PB) = m;
+      *reinterpret_cast<x3_u4*>(dst + 2 * PB) = l;
+    }
+    __syncthreads();
+  };
+  const int nk = p.nst * nsteps;
+  const unsigned kwinv = (65536u + p.kw - 1) / p.kw;  // t / kw = (t * kwinv) >> 16 for t < 64
+  // one k-step gs = (chunk gs / nsteps, step gs % nsteps) with the A fragments in af[buf]; the
+  // next k-step's A is loaded into af[buf ^ 1] first.  k-group lane >> 4 of step s is (tap,
+  // channel group) gidx / G, gidx % G with gidx = 4 s + (lane >> 4).
+  auto step = [&](int gs, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    const int ch = gs / nsteps, s = gs - ch * nsteps;
+    if (s == 0) stage(ch);  // uniform
+    if (gs + 1 < nk) load_a(std::integral_constant<int, buf ^ 1>{}, gs + 1);
+    const int gidx = s * 4 + (lane >> 4);
+    int t = gidx / G;
+    const int gg = gidx - t * G;
+    if (t >= ntaps) t = 0;  // padding groups: zero weights, any finite data
+    const int tr = (int)(((unsigned)t * kwinv) >> 16);
+    const int toff = tr * ww + (t - tr * p.kw);
+    x3_bf8 bfr[3][FN];
+#pragma unroll
+    for (int g = 0; g < FN; ++g) {
+      const int row = wbase[g] + toff;
+      const int off = row * RB + (G == 4 ? x3_slot(row, gg) : gg) * 16;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) bfr[q][g] = *reinterpret_cast<const x3_bf8*>(wlds + q * PB + off);
+    }
+#pragma unroll
+    for (int f = 0; f < FM; ++f)
+#pragma unroll
+      for (int g = 0; g < FN; ++g) {
+        // SACC: the k-step's six products start from 0 and the step sum is added to the running
+        // total with one f32 add (block summation: the products are never aligned to the total)
+        x3_f4 a = SACC ? x3_f4{0.f, 0.f, 0.f, 0.f} : acc[f][g];
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][2][f], bfr[0][g], a, 0, 0, 0);  // lo . hi
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][0][f], bfr[2][g], a, 0, 0, 0);  // hi . lo
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][1][f], bfr[1][g], a, 0, 0, 0);  // mid . mid
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][1][f], bfr[0][g], a, 0, 0, 0);  // mid . hi
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][0][f], bfr[1][g], a, 0, 0, 0);  // hi . mid
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][0][f], bfr[0][g], a, 0, 0, 0);  // hi . hi
+        acc[f][g] = SACC ? acc[f][g] + a : a;
+      }
+  };
+  load_a(std::integral_constant<int, 0>{}, 0);
+  for (int gs = 0; gs < nk; gs += 2) {
+    step(gs, std::integral_constant<int, 0>{});
+    if (gs + 1 < nk) step(gs + 1, std::integral_constant<int, 1>{});
+  }
+
+  // ---- epilogue: register e of fragment f = channel m0 + 16 (wm FM + f) + 4 (lane >> 4) + e, MFMA g's
+  // column = pixel p0 + 16 (wn FN + g) + (lane & 15)
+  float* __restrict__ y = p.y + (unsigned)(img * (int)p.y_nstride);
+#pragma unroll
+  for (int g = 0; g < FN; ++g) {
+    const int pp = p0 + 16 * (wn * FN + g) + (lane & 15);
+    if (pp >= P) continue;
+#pragma unroll
+    for (int f = 0; f < FM; ++f)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + 16 * (wm * FM + f) + 4 * (lane >> 4) + e;
+        if (m >= p.M) continue;
+        float v = acc[f][g][e] + (p.bias ? p.bias[m] : 0.0f);
+        if (p.relu) v = fmaxf(v, 0.0f);
+        y[(unsigned)(m * p.y_ps + pp)] = v;
+      }
+  }
+}
+
+// window packing: k-step gs = (chunk, step) of 32 k = 4 groups (lane >> 4) of 8 channels; group gidx
+// = step * 4 + (lane >> 4) is tap gidx / G, channel group gidx % G of the chunk -> wq[gs][part][Mp][4][8]
+__global__ __launch_bounds__(256) void pack_x3w_kernel(const float* __restrict__ w, unsigned* __restrict__ wq, int M,
+                                                       int C, int kh, int kw, int Mp, int G, int nsteps, int nchunks) {
+  const long long total = (long long)nchunks * nsteps * Mp * 16;  // (gs, m, group, pair)
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int pr = (int)(i & 3), grp = (int)((i >> 2) & 3);
+    const long long rm = i >> 4;
+    const int m = (int)(rm % Mp), gs = (int)(rm / Mp);
+    const int ch = gs / nsteps, st = gs - ch * nsteps;
+    const int gidx = st * 4 + grp, t = gidx / G, cg = gidx - t * G;
+    float v[2];
+    for (int e = 0; e < 2; ++e) {
+      const int c = ch * 8 * G + cg * 8 + 2 * pr + e;
+      v[e] = (m < M && t < kh * kw && c < C) ? w[(((long long)m * C + c) * kh + t / kw) * kw + t % kw] : 0.0f;
+    }
+    unsigned h, md, l;
+    x3_split(v[0], v[1], h, md, l);
+    const unsigned parts[3] = {h, md, l};
+    for (int q = 0; q < 3; ++q) wq[(((long long)gs * 3 + q) * Mp + m) * 16 + grp * 4 + pr] = parts[q];
+  }
+}
+
+// ------------------------------------------------------------------ host side
+// tiles (ConvPlan::cfg - X3_TILE_BASE): 0-3 the gather kernel, 4-7 the window kernel; rows x pixels per block
+static const int X3_BM[X3_TILES] = {128, 64, 96, 64, 128, 64, 128, 64};
+static const int X3_BN[X3_TILES] = {128, 256, 128, 128, 128, 128, 64, 64};
+
+int x3_tile_rows(int tile) { return X3_BM[tile]; }
+
+int x3_tile_config(int M) {
+  if (M % 96 == 0 && M % 128 != 0) return 2;
+  if (M <= 64) return 1;
+  return 0;
+}
+
+bool conv_x3_eligible(const ConvParams& p) { return p.x_bytes > 0 && (p.is1x1 || (long long)p.kh * p.kw <= 64); }
+
+// window geometry: stride 1, C % 8 == 0, at most 5 x 5 taps
+bool x3w_geometry(int C, int kh, int kw, int sh, int sw) {
+  return sh == 1 && sw == 1 && C % 8 == 0 && kh <= 5 && kw <= 5 && kh * kw > 1;
+}
+
+int x3w_groups(int C) { return C % 32 == 0 ? 4 : 2; }
+
+// window rows (span of output rows + halo) of the worst tile, and its LDS bytes
+static size_t x3w_lds(const ConvParams& p, int BN, int G, int* wrows) {
+  const int P = p.Ho * p.Wo;
+  int span = 1;
+  for (int p0 = 0; p0 < P; p0 += BN) {
+    const int pe = (p0 + BN < P ? p0 + BN : P) - 1;
+    span = std::max(span, pe / p.Wo - p0 / p.Wo + 1);
+  }
+  *wrows = span + p.kh - 1;
+  return (size_t)3 * *wrows * (p.Wo + p.kw - 1) * G * 16;
+}
+
+bool conv_x3w_eligible(const ConvParams& p, int tile) {
+  if (tile < 4 || p.x_bytes <= 0 || !x3w_geometry(p.C, p.kh, p.kw, p.sh, p.sw)) return false;
+  int wrows = 0;
+  return x3w_lds(p, X3_BN[tile], p.bch, &wrows) <= 80 * 1024;
+}
+
+void launch_pack_x3(const float* w, bool kmajor_src, int M, int K, int Mp, void* wx, hipStream_t s) {
+  const int Kp = (K + 31) / 32 * 32;
+  const long long total = (long long)(Kp / 32) * Mp * 16;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pack_x3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, w, reinterpret_cast<unsigned*>(wx), M, K,
+                     Mp, Kp, kmajor_src ? 1 : 0);
+}
+
+void launch_pack_x3w(const float* w, int M, int C, int kh, int kw, int Mp, int G, int nsteps, int nchunks, void* wq,
+                     hipStream_t s) {
+  const long long total = (long long)nchunks * nsteps * Mp * 16;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pack_x3w_kernel, dim3((unsigned)blocks), dim3(256), 0, s, w, reinterpret_cast<unsigned*>(wq), M, C,
+                     kh, kw, Mp, G, nsteps, nchunks);
+}
+
+template <int FM, int FN>
+static void launch_x3(const ConvParams& p0, hipStream_t s) {
+  ConvParams p = p0;
+  p.mtiles = (p.M + 32 * FM - 1) / (32 * FM);
+  p.ntiles = (int)((p.Ntot + 32 * FN - 1) / (32 * FN));
+  const dim3 grid((unsigned)(p.mtiles * p.ntiles)), block(256);
+  if (p.is1x1)
+    hipLaunchKernelGGL((conv_x3_kernel<FM, FN, X3_1X1>), grid, block, 0, s, p);
+  else if (p.kh * p.kw <= 32)
+    hipLaunchKernelGGL((conv_x3_kernel<FM, FN, X3_G32>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_x3_kernel<FM, FN, X3_G64>), grid, block, 0, s, p);
+}
+
+template <int FM, int FN>
+static void launch_x3w(const ConvParams& p0, hipStream_t s) {
+  ConvParams p = p0;
+  int wrows = 0;
+  const size_t lds = x3w_lds(p, 32 * FN, p.bch, &wrows);
+  p.wr = wrows;
+  p.ww = p.Wo + p.kw - 1;
+  p.P = p.Ho * p.Wo;
+  p.tiles_per_img = (p.P + 32 * FN - 1) / (32 * FN);
+  p.mtiles = (p.M + 32 * FM - 1) / (32 * FM);
+  p.ntiles = p.N * p.tiles_per_img;
+  const dim3 grid((unsigned)(p.mtiles * p.ntiles)), block(256);
+  if (lds > 64 * 1024) {  // above the default dynamic-LDS limit: raise it once per device and instantiation
+    static std::atomic<unsigned long long> raised{0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (!(raised.load(std::memory_order_acquire) & bit)) {
+      const void* fns[4] = {reinterpret_cast<const void*>(&conv_x3w_kernel<FM, FN, 4, 0>),
+                            reinterpret_cast<const void*>(&conv_x3w_kernel<FM, FN, 2, 0>),
+                            reinterpret_cast<const void*>(&conv_x3w_kernel<FM, FN, 4, 1>),
+                            reinterpret_cast<const void*>(&conv_x3w_kernel<FM, FN, 2, 1>)};
+      for (const void* fn : fns) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      raised.fetch_or(bit, std::memory_order_acq_rel);
+    }
+  }
+  // block summation on by default (ORE_X3_SACC=0: one running accumulator, an experiment knob): 3x
+  // lower error than one accumulator on the SqueezeNet shapes (profiles/r02_x3_accuracy.json)
+  const bool sacc = getenv("ORE_X3_SACC") ? atoi(getenv("ORE_X3_SACC")) != 0 : true;
+  if (sacc) {
+    if (p.bch == 4)
+      hipLaunchKernelGGL((conv_x3w_kernel<FM, FN, 4, 1>), grid, block, lds, s, p);
+    else
+      hipLaunchKernelGGL((conv_x3w_kernel<FM, FN, 2, 1>), grid, block, lds, s, p);
+  } else if (p.bch == 4) {
+    hipLaunchKernelGGL((conv_x3w_kernel<FM, FN, 4, 0>), grid, block, lds, s, p);
+  } else {
+    hipLaunchKernelGGL((conv_x3w_kernel<FM, FN, 2, 0>), grid, block, lds, s, p);
+  }
+}
+
+size_t x3w_plan_lds(int Ho, int Wo, int kh, int kw, int C, int tile) {
+  ConvParams p{};
+  p.Ho = Ho; p.Wo = Wo; p.kh = kh; p.kw = kw;
+  int wrows = 0;
+  return x3w_lds(p, X3_BN[tile], x3w_groups(C), &wrows);
+}
+
+void launch_conv_x3(const ConvParams& p, int tile, hipStream_t s) {
+  switch (tile) {
+    case 1: launch_x3<2, 8>(p, s); break;   // 64 x 256
+    case 2: launch_x3<3, 4>(p, s); break;   // 96 x 128
+    case 3: launch_x3<2, 4>(p, s); break;   // 64 x 128
+    case 4: launch_x3w<4, 4>(p, s); break;  // window 128 x 128
+    case 5: launch_x3w<2, 4>(p, s); break;  // window 64 x 128
+    case 6: launch_x3w<4, 2>(p, s); break;  // window 128 x 64
+    case 7: launch_x3w<2, 2>(p, s); break;  // window 64 x 64
+    default: launch_x3<4, 4>(p, s); break;  // 128 x 128
+  }
+}
+
+}  // namespace ore

@@ -56,6 +56,7 @@ struct ConvPlan {
   int Mp, krows;       // packed weights are krows x Mp floats
   size_t lds;          // dynamic LDS bytes of the window kernel
   int epv = 0;         // pooled-epilogue steps: ConvParams::ep_variant (ore_model_autotune)
+  int x3 = 0;          // 1: conv_x3_kernel (f32 on the BF16 matrix cores, ore_conv_x3.hip); cfg = X3_TILE_BASE + tile
 };
 
 struct PoolParams {
@@ -118,7 +119,7 @@ int conv_packed_kp(int K);  // padded K of the packed weights
 void launch_pack_weights(const float* w, bool kmajor_src, int M, int K, int Mp, float* wp, hipStream_t s);
 void launch_ktab(int2* ktab, int K, int kh, int kw, int x_ps, int W, hipStream_t s);
 ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
-                   bool is1x1, bool f16 = false, int xmode = 0);
+                   bool is1x1, bool f16 = false, int xmode = 0, bool x3 = false);
 // f16 conv operand modes (ConvPlan::xmode), chosen by the input's layout:
 enum {
   F16_X_NCHW32 = 0,     // f32 NCHW model input, per-element gather, k order (c, r, s) (the reference's)
@@ -184,6 +185,27 @@ void launch_conv_stream(const ConvParams& p, int tile, hipStream_t s);
 extern thread_local int last_conv_tile;
 constexpr int CONV_TILES_F16 = 4;
 constexpr int CONV_TILES_AUTOTUNE = 4;  // the direct tiles measured 15-80 % slower on every SqueezeNet layer
+// f32 conv on the BF16 matrix cores by an exact three-way bf16 split of both operands (six part
+// products, f32 accumulation; ore_conv_x3.hip).  Tiles X3_TILE_BASE + 0..3 = 128x128, 64x256,
+// 96x128, 64x128 (channels x pixels per block); results do not depend on the tile.  Weights
+// packed by launch_pack_x3: [Kp / 32][3][Mp][32] bf16 (6 bytes per packed f32 weight).
+// Window-staged variant (stride-1 convs with C % 8 == 0, ConvPlan::x3 == 2): tiles X3_TILE_BASE + 4..7 =
+// 128x128, 64x128, 128x64, 64x64; weights packed by launch_pack_x3w per k-step of (tap, 8-channel
+// group) pairs: [nchunks * nsteps][3][Mp][32] bf16 (ConvPlan bch = groups G per chunk, nst = chunks,
+// ks = k-steps per chunk; the same fields go to ConvParams).
+constexpr int X3_TILE_BASE = 28;
+constexpr int X3_TILES = 8;
+int x3_tile_config(int M);  // 0..3 (gather tiles)
+int x3_tile_rows(int tile);
+bool conv_x3_eligible(const ConvParams& p);
+bool conv_x3w_eligible(const ConvParams& p, int tile);
+bool x3w_geometry(int C, int kh, int kw, int sh, int sw);
+int x3w_groups(int C);
+size_t x3w_plan_lds(int Ho, int Wo, int kh, int kw, int C, int tile);  // dynamic LDS of window tile `tile`
+void launch_pack_x3(const float* w, bool kmajor_src, int M, int K, int Mp, void* wx, hipStream_t s);
+void launch_pack_x3w(const float* w, int M, int C, int kh, int kw, int Mp, int G, int nsteps, int nchunks, void* wq,
+                     hipStream_t s);
+void launch_conv_x3(const ConvParams& p, int tile, hipStream_t s);
 void launch_maxpool(const PoolParams& p, hipStream_t s);
 void launch_relu(const float* x, float* y, long long n, hipStream_t s);
 void launch_relu_f16(const void* x, void* y, long long n, hipStream_t s);

@@ -108,6 +108,7 @@ struct ore_model {
   int64_t max_batch = 0;
   int32_t fusion = ORE_FUSE_ALL;
   bool f16 = false;              // ORE_LOAD_F16: f16 conv/pool activations, f32 accumulation
+  bool x3 = false;               // ORE_LOAD_X3: f32 convs / MatMuls on the BF16 matrix cores (ore_conv_x3.hip)
   std::vector<Value> values;
   size_t n_base_values = 0;      // values of the graph; plan() appends views after them (pooled slices)
   std::map<std::string, int> by_name;
@@ -532,7 +533,7 @@ ore_status plan(ore_model* m) {
     count_uses(m, m->steps);
   }
   // (1b) 3x3 MaxPool -> its only consumer, a plain 1x1 Conv: the pool runs in the conv's gather
-  if ((m->fusion & ORE_FUSE_POOL_CONV) && !m->f16) {
+  if ((m->fusion & ORE_FUSE_POOL_CONV) && !m->f16 && !m->x3) {
     for (size_t i = 0; i < m->steps.size(); ++i) {
       Step& pl = m->steps[i];
       if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3) continue;
@@ -567,7 +568,7 @@ ore_status plan(ore_model* m) {
       const int pc = producer[v];
       if (pc < 0 || m->values[v].uses != 1 || m->values[v].is_output) continue;
       Step& cv = m->steps[pc];
-      if (cv.kind != S_CONV || cv.pool || cv.epool || cv.plan.window) continue;
+      if (cv.kind != S_CONV || cv.pool || cv.epool || cv.plan.window || cv.plan.x3) continue;
       if (cv.plan.f16 != (m->values[pl.out].es == 2 ? 1 : 0)) continue;  // f16 conv -> f16 pool only
       int a = 0, b = 0;
       const double work = epool_tile(cv.win.Ho, cv.win.Wo, pl.kh, pl.kw, pl.sh, pl.sw, pl.win, &a, &b);
@@ -596,7 +597,7 @@ ore_status plan(ore_model* m) {
   // pool3 (-40 us per B=256 step); fire8 -> pool5 (27^2 planes) stays unfused, measured slower
   // (DESIGN.md section 9).
   if ((m->fusion & ORE_FUSE_CONCAT_POOL) && (m->fusion & ORE_FUSE_CONV_POOL) && (m->fusion & ORE_FUSE_CONCAT) &&
-      !m->f16) {
+      !m->f16 && !m->x3) {
     for (size_t i = 0; i < m->steps.size(); ++i) {
       Step& pl = m->steps[i];
       if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2) continue;
@@ -655,7 +656,7 @@ ore_status plan(ore_model* m) {
   // (1d) fire module + the next squeeze in one launch (ORE_FUSE_FIRE, f32): Concat(e1, e3) whose
   // inputs are a 1x1 and a 3x3 'same' Conv (+ Relu) of one value S, read only by a 1x1 Conv (+ Relu)
   // with at most 64 output channels
-  if ((m->fusion & ORE_FUSE_FIRE) && !m->f16 && (m->fusion & ORE_FUSE_CONV_RELU)) {
+  if ((m->fusion & ORE_FUSE_FIRE) && !m->f16 && !m->x3 && (m->fusion & ORE_FUSE_CONV_RELU)) {
     const char* e = getenv("ORE_FIRE_MIN_COLS");  // tuning knob (tests set 0)
     const int64_t min_cols = e ? atoll(e) : 65536;
     for (size_t i = 0; i < m->steps.size(); ++i) {
@@ -1085,7 +1086,9 @@ ore_status ore_model_parse(const void* bytes, size_t len) {
 ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_t max_batch, int32_t flags,
                              ore_model** out) {
   if (!ctx || !bytes || !out || max_batch <= 0) return set_error(ctx, ORE_ERR_INVALID, "invalid argument");
-  if (flags & ~ORE_LOAD_F16) return set_error(ctx, ORE_ERR_INVALID, "unknown load flags 0x%x", unsigned(flags));
+  if (flags & ~(ORE_LOAD_F16 | ORE_LOAD_X3)) return set_error(ctx, ORE_ERR_INVALID, "unknown load flags 0x%x", unsigned(flags));
+  if ((flags & ORE_LOAD_F16) && (flags & ORE_LOAD_X3))
+    return set_error(ctx, ORE_ERR_INVALID, "ORE_LOAD_F16 and ORE_LOAD_X3 are exclusive");
   ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
   Graph g;
   std::string perr;
@@ -1094,6 +1097,7 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
   m->ctx = ctx;
   m->max_batch = max_batch;
   m->f16 = (flags & ORE_LOAD_F16) != 0;
+  m->x3 = (flags & ORE_LOAD_X3) != 0;
   auto fail = [&](ore_status st) {
     ore_model_destroy(m);
     return st;
@@ -1167,10 +1171,10 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
                                                                                            : F16_X_NCHW32)
                           : s.C % 8 == 0           ? F16_X_NHWC_VEC
                                                    : F16_X_NHWC_ELEM;
-        s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, m->f16, xmode);
+        s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, m->f16, xmode, m->x3);
       }
       else if (s.kind == S_MATMUL)
-        s.plan = conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win);
+        s.plan = conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win, false, 0, m->x3);
       else
         continue;
       total_packed += (packed_bytes(s.plan) + 255) / 256 * 256;
@@ -1436,10 +1440,13 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
     // win on the long-K, few-row 1x1 squeezes, e.g. fire7/8 113 -> 97 us); ORE_AUTOTUNE_WS=0 drops them
     std::vector<int> cands = {0, 1, 2, 3};
     const char* ews = getenv("ORE_AUTOTUNE_WS");
-    if (!s.plan.f16 && !(ews && !atoi(ews))) cands.insert(cands.end(), {8, 9, 10, 11});
+    if (s.plan.x3) {  // the x3 tiles of the plan's kernel family only (its packed layout)
+      cands.clear();
+      for (int c = 0; c < 4; ++c) cands.push_back(X3_TILE_BASE + c + (s.plan.x3 == 2 ? 4 : 0));
+    } else if (!s.plan.f16 && !(ews && !atoi(ews))) cands.insert(cands.end(), {8, 9, 10, 11});
     // the LDS-free streaming kernel (tiles 12-20) where the geometry allows it (launch_conv falls
     // back to tile 0 elsewhere, and such candidates are skipped below)
-    if (!s.plan.f16 && s.kind == S_CONV && !s.pool)
+    if (!s.plan.f16 && !s.plan.x3 && s.kind == S_CONV && !s.pool)
       for (int c = CONV_TILE_STREAM; c < CONV_TILES_F32; ++c) cands.push_back(c);
     for (size_t ci = 0; ci < cands.size() && !st; ++ci) {
       const int c = cands[ci];

@@ -1,5 +1,6 @@
 // C ABI: context, memory, reference geometry and the per-op entry points that replace the
 // functions behind `node_inference` (model_inference.rs:137-161).
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -98,9 +99,9 @@ static bool contiguous(const ore_tensor* t) {
 static bool fits_i32(int64_t v) { return v >= 0 && v < (int64_t(1) << 31); }
 
 ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
-                   const Window& win, bool f16, int xmode) {
+                   const Window& win, bool f16, int xmode, bool x3) {
   return plan_conv(int(M), int(C), int(H), int(W), int(kh), int(kw), int(sh), int(sw), int(win.pt), int(win.pl),
-                   int(win.Ho), int(win.Wo), kh == 1 && kw == 1, f16, xmode);
+                   int(win.Ho), int(win.Wo), kh == 1 && kw == 1, f16, xmode, x3);
 }
 
 size_t packed_bytes(const ConvPlan& pln) {
@@ -181,6 +182,26 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
       !fits_i32(p.Ntot + 256) || (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))
     return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
   if (!pln.window && !p.is1x1 && !ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
+  if (pln.x3) {
+    // the x3 kernel addresses x through a buffer resource (32-bit byte offsets): a batch whose input
+    // extent does not fit runs in image chunks that do
+    if (!p.is1x1 && p.kh * p.kw > 64) return set_error(ctx, ORE_ERR_UNSUPPORTED, "x3 conv: more than 64 taps");
+    int64_t nb = N;
+    while (nb > 1 && ((nb - 1) * x_nstride + C * x_ps) * 4 >= (int64_t(1) << 31)) nb = (nb + 1) / 2;
+    if ((C * x_ps) * 4 >= (int64_t(1) << 31)) return set_error(ctx, ORE_ERR_UNSUPPORTED, "x3 conv: one image exceeds 2 GiB");
+    for (int64_t i0 = 0; i0 < N; i0 += nb) {
+      const int64_t nc = std::min(nb, N - i0);
+      ConvParams q = p;
+      q.x = x + i0 * x_nstride;
+      q.y = y + i0 * y_nstride;
+      q.N = int(nc);
+      q.Ntot = nc * y_ps;
+      q.x_bytes = ((nc - 1) * x_nstride + C * x_ps) * 4;
+      launch_conv(q, pln, ctx->stream);
+      ORE_HIP_CHECK(ctx, hipGetLastError());
+    }
+    return ORE_OK;
+  }
   launch_conv(p, pln, ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());
   return ORE_OK;

@@ -20,6 +20,7 @@ FUSE_CONV_RELU, FUSE_CONCAT, FUSE_ALIAS, FUSE_ALL, KEEP_VALUES, FUSE_POOL_CONV, 
 FUSE_FIRE = 64
 FUSE_CONCAT_POOL = 128
 LOAD_F16 = 1  # ore_model_load_ex flag: the fp16 variant
+LOAD_X3 = 2   # ore_model_load_ex flag: f32 convs on the BF16 matrix cores (exact 3-way bf16 split)
 PAD = {"NOTSET": 0, "NOT_SET": 0, "SAME_UPPER": 1, "SAME_LOWER": 2, "VALID": 3}
 
 # every symbol include/ore.h declares (checked by tests/test_abi.py on CPU)

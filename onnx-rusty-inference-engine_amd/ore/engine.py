@@ -16,7 +16,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import LOAD_F16, ConvAttrs, OreError, PoolAttrs, Tensor, check, load
+from ._lib import LOAD_F16, LOAD_X3, ConvAttrs, OreError, PoolAttrs, Tensor, check, load
 
 __all__ = ["Context", "Model", "OreError", "convolution", "max_pool", "relu", "add", "softmax", "mul",
            "global_average_pool", "concatenation", "drop_out", "reshape", "inference", "conv_out_shape",
@@ -218,13 +218,15 @@ class Model:
     """ore_model: the device-resident walker over one ONNX graph."""
 
     def __init__(self, ctx: Context, onnx_bytes: bytes, max_batch: int, precision: str = "f32"):
-        """precision "f16": the fp16 variant (ORE_LOAD_F16, include/ore.h); input/output stay f32."""
-        if precision not in ("f32", "f16"):
-            raise OreError(1, f"precision must be 'f32' or 'f16', not {precision!r}")
+        """precision "f32": convs on the f32-input MFMA; "f32x3": the same f32 model with its convs /
+        MatMuls on the BF16 matrix cores through an exact three-way bf16 split (ORE_LOAD_X3,
+        include/ore.h); "f16": the fp16 variant (ORE_LOAD_F16).  Input / output stay f32."""
+        if precision not in ("f32", "f32x3", "f16"):
+            raise OreError(1, f"precision must be 'f32', 'f32x3' or 'f16', not {precision!r}")
         self.ctx = ctx
         self.precision = precision
         h = ctypes.c_void_p()
-        flags = LOAD_F16 if precision == "f16" else 0
+        flags = {"f32": 0, "f32x3": LOAD_X3, "f16": LOAD_F16}[precision]
         check(load().ore_model_load_ex(ctx.h, onnx_bytes, len(onnx_bytes), int(max_batch), flags, ctypes.byref(h)),
               ctx.h)
         self.h = h
@@ -292,7 +294,9 @@ class Model:
                   "stream 64x128", "stream 32x256", "stream 16x256", "stream 48x128", "stream 64x64",
                   "stream 128x64", "stream 64x64 d8", "stream 32x128", "stream 128x64 d2", "fire",
                   "epool patch", "epool walk48", "epool walk96", "epool walk64",
-                  "epool walk64 b3", "epool walk96 b2"]
+                  "epool walk64 b3", "epool walk96 b2",
+                  "x3 128x128", "x3 64x256", "x3 96x128", "x3 64x128",
+                  "x3w 128x128", "x3w 64x128", "x3w 128x64", "x3w 64x64"]
 
     def tiles(self):
         """Block tile per exec step (-1 for non-conv steps); names in TILE_NAMES."""
