@@ -320,7 +320,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvParams p) {
 // k-step by launch_pack_x3w) goes global -> registers with one k-step of prefetch: no LDS and no
 // barrier in the main loop (the two waves sharing an A row range hit the CU's L1).
 template <int FM, int FN, int G, int SACC>
-__global__ __launch_bounds__(256, 2) void conv_x3w_kernel(ConvParams p) {
+__global__ __launch_bounds__(256, FM * FN <= 8 ? 3 : 2) void conv_x3w_kernel(ConvParams p) {
   constexpr int BM = 32 * FM, BN = 32 * FN;
   constexpr int RB = G * 16;  // bytes per window pixel per part
   extern __shared__ __attribute__((aligned(16))) char wlds[];
@@ -362,11 +362,16 @@ __global__ __launch_bounds__(256, 2) void conv_x3w_kernel(ConvParams p) {
   const int aoff = (m0 + 16 * wm * FM + (lane & 15)) * 64 + (lane >> 4) * 16;
   const int astep = 3 * p.Mp * 64;  // bytes per k-step of packed weights
 
-  x3_f4 acc[FM][FN];
+  // running sums as scalar floats: the SACC block sums are added with scalar v_add_f32 (a v4f32 add
+  // lowers to packed v_pk_add_f32, dearer than two scalar adds beside MFMAs: MI355X_MICROARCH.md
+  // 'price of one filler beside MFMAs')
+  float acc[FM][FN][4];
 #pragma unroll
   for (int f = 0; f < FM; ++f)
 #pragma unroll
-    for (int g = 0; g < FN; ++g) acc[f][g] = x3_f4{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < FN; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[f][g][e] = 0.0f;
 
   x3_bf8 af[2][3][FM];  // A fragments of two k-steps (static indices only: the loop below is unrolled by 2)
   auto load_a = [&](auto bufc, int gs) {
@@ -375,35 +380,43 @@ __global__ __launch_bounds__(256, 2) void conv_x3w_kernel(ConvParams p) {
     for (int q = 0; q < 3; ++q)
 #pragma unroll
       for (int f = 0; f < FM; ++f)
-        af[buf][q][f] = __builtin_bit_cast(
-            x3_bf8, __builtin_amdgcn_raw_buffer_load_b128(wr, aoff + (q * p.Mp + 16 * f) * 64, gs * astep, 0));
+        af[buf][q][f] = __builtin_bit_cast(  // per-lane part in voffset, the uniform rest in soffset
+            x3_bf8, __builtin_amdgcn_raw_buffer_load_b128(wr, aoff, gs * astep + (q * p.Mp + 16 * f) * 64, 0));
   };
-  // stage channels [8G ch, 8G (ch + 1)) of the window, split (every element once)
+  // stage channels [8G ch, 8G (ch + 1)) of the window, split (every element once).  A thread owns
+  // whole window pixels: the 8G loads of a pixel are issued back to back (one latency per pixel,
+  // not per channel group), coalesced across the wave's consecutive pixels.
   auto stage = [&](int ch) {
     if (ch > 0) __syncthreads();  // every wave is done with the previous chunk's window
     const int c0 = ch * 8 * G;
-    for (int i = tid; i < nwp * G; i += 256) {
-      const int g = i / nwp, wpix = i - g * nwp;
+    for (int wpix = tid; wpix < nwp; wpix += 256) {
       const int wrow = wpix / ww, wc = wpix - wrow * ww;
       const int ih = ih_first + wrow, iw = wc - p.pl;
-      const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && c0 + 8 * g < p.C;
-      const int vo = ok ? (img * (int)p.x_nstride + (c0 + 8 * g) * p.x_ps + ih * p.W + iw) * 4 : (int)0x80000000;
-      float v[8];
+      const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      const int vb = (img * (int)p.x_nstride + c0 * p.x_ps + ih * p.W + iw) * 4;
+      float v[G][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, j * p.x_ps * 4, 0));
-      x3_u4 h, m, l;
+      for (int g = 0; g < G; ++g) {
+        const int vo = ok && c0 + 8 * g < p.C ? vb : (int)0x80000000;  // out of range: reads 0
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        unsigned hh, mm, ll;
-        x3_split(v[2 * e], v[2 * e + 1], hh, mm, ll);
-        h[e] = hh; m[e] = mm; l[e] = ll;
+        for (int j = 0; j < 8; ++j)
+          v[g][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, (8 * g + j) * p.x_ps * 4, 0));
       }
-      const int slot = G == 4 ? x3_slot(wpix, g) : g;
-      char* dst = wlds + wpix * RB + slot * 16;
-      *reinterpret_cast<x3_u4*>(dst) = h;
-      *reinterpret_cast<x3_u4*>(dst + PB) = m;
-      *reinterpret_cast<x3_u4*>(dst + 2 * PB) = l;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        x3_u4 h, m, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          unsigned hh, mm, ll;
+          x3_split(v[g][2 * e], v[g][2 * e + 1], hh, mm, ll);
+          h[e] = hh; m[e] = mm; l[e] = ll;
+        }
+        const int slot = G == 4 ? x3_slot(wpix, g) : g;
+        char* dst = wlds + wpix * RB + slot * 16;
+        *reinterpret_cast<x3_u4*>(dst) = h;
+        *reinterpret_cast<x3_u4*>(dst + PB) = m;
+        *reinterpret_cast<x3_u4*>(dst + 2 * PB) = l;
+      }
     }
     __syncthreads();
   };
@@ -422,7 +435,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3w_kernel(ConvParams p) {
     const int gg = gidx - t * G;
     if (t >= ntaps) t = 0;  // padding groups: zero weights, any finite data
     const int tr = (int)(((unsigned)t * kwinv) >> 16);
-    const int toff = tr * ww + (t - tr * p.kw);
+    const int toff = (int)__umul24((unsigned)tr, (unsigned)ww) + (t - (int)__umul24((unsigned)tr, (unsigned)p.kw));
     x3_bf8 bfr[3][FN];
 #pragma unroll
     for (int g = 0; g < FN; ++g) {
@@ -431,20 +444,27 @@ __global__ __launch_bounds__(256, 2) void conv_x3w_kernel(ConvParams p) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) bfr[q][g] = *reinterpret_cast<const x3_bf8*>(wlds + q * PB + off);
     }
+    // B column group outer: the first MFMAs wait only for the first group's three fragment reads
 #pragma unroll
-    for (int f = 0; f < FM; ++f)
+    for (int g = 0; g < FN; ++g)
 #pragma unroll
-      for (int g = 0; g < FN; ++g) {
+      for (int f = 0; f < FM; ++f) {
         // SACC: the k-step's six products start from 0 and the step sum is added to the running
         // total with one f32 add (block summation: the products are never aligned to the total)
-        x3_f4 a = SACC ? x3_f4{0.f, 0.f, 0.f, 0.f} : acc[f][g];
+        x3_f4 a = SACC ? x3_f4{0.f, 0.f, 0.f, 0.f} : x3_f4{acc[f][g][0], acc[f][g][1], acc[f][g][2], acc[f][g][3]};
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][2][f], bfr[0][g], a, 0, 0, 0);  // lo . hi
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][0][f], bfr[2][g], a, 0, 0, 0);  // hi . lo
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][1][f], bfr[1][g], a, 0, 0, 0);  // mid . mid
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][1][f], bfr[0][g], a, 0, 0, 0);  // mid . hi
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][0][f], bfr[1][g], a, 0, 0, 0);  // hi . mid
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][0][f], bfr[0][g], a, 0, 0, 0);  // hi . hi
-        acc[f][g] = SACC ? acc[f][g] + a : a;
+        if constexpr (SACC) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[f][g][e] += a[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[f][g][e] = a[e];
+        }
       }
   };
   load_a(std::integral_constant<int, 0>{}, 0);

@@ -96,6 +96,12 @@ struct Step {
   ConvPlan plan{};        // kernel choice and weight layout for S_CONV / S_MATMUL
   float* wp = nullptr;    // packed weights (layout per plan) for S_CONV / S_MATMUL
   const int2* ktab = nullptr;  // gather table (follows wp in the packed allocation; gather kernel only)
+  // ORE_LOAD_X3: the x3 plan of this conv (ore_conv_x3.hip), packed next to the f32-MFMA one; plan()
+  // switches an unfused conv to it (x3_wanted), a conv taken by an f32-MFMA fusion keeps `plan`
+  bool has_x3 = false;
+  ConvPlan plan_x3{};
+  float* wp_x3 = nullptr;
+  const int2* ktab_x3 = nullptr;
   void* xcvt = nullptr;        // f16 F16_X_NHWC_PAIR: the f32 NCHW input converted to NHWC4 f16 (max_batch)
   int64_t axis = 1;
   double flops_per_img = 0, bytes_per_img = 0, bytes_fixed = 0;
@@ -109,6 +115,7 @@ struct ore_model {
   int32_t fusion = ORE_FUSE_ALL;
   bool f16 = false;              // ORE_LOAD_F16: f16 conv/pool activations, f32 accumulation
   bool x3 = false;               // ORE_LOAD_X3: f32 convs / MatMuls on the BF16 matrix cores (ore_conv_x3.hip)
+  bool x3_all = false;           // ORE_X3_ALL=1 (tests, experiments): every conv on x3, no f32-MFMA fusions
   std::vector<Value> values;
   size_t n_base_values = 0;      // values of the graph; plan() appends views after them (pooled slices)
   std::map<std::string, int> by_name;
@@ -500,6 +507,21 @@ int64_t padded_plane(int64_t P) {
 
 bool strided_writer(const Step& s) { return s.kind == S_CONV || s.kind == S_FIRE || s.kind == S_MAXPOOL; }
 
+// ORE_LOAD_X3: convs whose x3 kernel beats the f32-MFMA one at SqueezeNet's shapes (batch 256,
+// profiles/r02*_layers*.txt): stride-1 k x k convs on the window-staged kernel (every expand3x3),
+// and 1x1 convs / MatMuls with M >= 256 and K >= 256 (conv10: MFMA-bound).  The other 1x1 convs
+// are HBM-bound, where the f32-MFMA streaming kernels are faster, and the stride-2 7x7 conv1 stays on
+// the f32-MFMA row-walking kernel with pool1 fused.  ORE_X3_ALL=1: every conv.
+bool x3_wanted(const ore_model* m, const Step& s) {
+  if (m->x3_all) return true;
+  if (s.kind == S_MATMUL) return s.M >= 256 && s.C >= 256;
+  if (s.kind != S_CONV) return false;
+  const bool k1 = s.kh == 1 && s.kw == 1 && s.sh == 1 && s.sw == 1;
+  if (k1) return s.M >= 256 && s.C >= 256;
+  return x3w_geometry(int(s.C), int(s.kh), int(s.kw), int(s.sh), int(s.sw)) &&
+         x3w_plan_lds(int(s.win.Ho), int(s.win.Wo), int(s.kh), int(s.kw), int(s.C), 6) <= 80 * 1024;
+}
+
 ore_status plan(ore_model* m) {
   m->steps = m->base_steps;
   if (!m->n_base_values) m->n_base_values = m->values.size();
@@ -533,7 +555,7 @@ ore_status plan(ore_model* m) {
     count_uses(m, m->steps);
   }
   // (1b) 3x3 MaxPool -> its only consumer, a plain 1x1 Conv: the pool runs in the conv's gather
-  if ((m->fusion & ORE_FUSE_POOL_CONV) && !m->f16 && !m->x3) {
+  if ((m->fusion & ORE_FUSE_POOL_CONV) && !m->f16 && !m->x3_all) {
     for (size_t i = 0; i < m->steps.size(); ++i) {
       Step& pl = m->steps[i];
       if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3) continue;
@@ -568,7 +590,7 @@ ore_status plan(ore_model* m) {
       const int pc = producer[v];
       if (pc < 0 || m->values[v].uses != 1 || m->values[v].is_output) continue;
       Step& cv = m->steps[pc];
-      if (cv.kind != S_CONV || cv.pool || cv.epool || cv.plan.window || cv.plan.x3) continue;
+      if (cv.kind != S_CONV || cv.pool || cv.epool || cv.plan.window || m->x3_all) continue;
       if (cv.plan.f16 != (m->values[pl.out].es == 2 ? 1 : 0)) continue;  // f16 conv -> f16 pool only
       int a = 0, b = 0;
       const double work = epool_tile(cv.win.Ho, cv.win.Wo, pl.kh, pl.kw, pl.sh, pl.sw, pl.win, &a, &b);
@@ -597,7 +619,7 @@ ore_status plan(ore_model* m) {
   // pool3 (-40 us per B=256 step); fire8 -> pool5 (27^2 planes) stays unfused, measured slower
   // (DESIGN.md section 9).
   if ((m->fusion & ORE_FUSE_CONCAT_POOL) && (m->fusion & ORE_FUSE_CONV_POOL) && (m->fusion & ORE_FUSE_CONCAT) &&
-      !m->f16 && !m->x3) {
+      !m->f16 && !m->x3_all) {
     for (size_t i = 0; i < m->steps.size(); ++i) {
       Step& pl = m->steps[i];
       if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2) continue;
@@ -656,9 +678,14 @@ ore_status plan(ore_model* m) {
   // (1d) fire module + the next squeeze in one launch (ORE_FUSE_FIRE, f32): Concat(e1, e3) whose
   // inputs are a 1x1 and a 3x3 'same' Conv (+ Relu) of one value S, read only by a 1x1 Conv (+ Relu)
   // with at most 64 output channels
-  if ((m->fusion & ORE_FUSE_FIRE) && !m->f16 && !m->x3 && (m->fusion & ORE_FUSE_CONV_RELU)) {
+  if ((m->fusion & ORE_FUSE_FIRE) && !m->f16 && !m->x3_all && (m->fusion & ORE_FUSE_CONV_RELU)) {
     const char* e = getenv("ORE_FIRE_MIN_COLS");  // tuning knob (tests set 0)
     const int64_t min_cols = e ? atoll(e) : 65536;
+    // x3 models: the f32-MFMA fire kernel only where it beats the x3 expand3x3 + separate 1x1s
+    // (planes of >= ORE_X3_FIRE_MIN_HW pixels, default 1024: SqueezeNet's 54 x 54 fire2 / fire3;
+    // at 27 x 27 the x3 expand3x3 wins)
+    const char* ex = getenv("ORE_X3_FIRE_MIN_HW");
+    const int64_t x3_fire_min_hw = ex ? atoll(ex) : 1024;
     for (size_t i = 0; i < m->steps.size(); ++i) {
       Step& cc = m->steps[i];
       if (cc.kind != S_CONCAT || cc.axis != 1 || cc.in0 < 0 || cc.in1 < 0 || cc.in0 == cc.in1) continue;
@@ -679,6 +706,7 @@ ore_status plan(ore_model* m) {
       if (!is1x1(e1) || !e3ok || !is1x1(q) || q.in0 != cc.out || e1.in0 != e3.in0 || e1.H != e3.H || e1.W != e3.W) continue;
       if (e1.M % 64 || e3.M % 64 || q.M > 64 || e1.C % 16 || q.C != e1.M + e3.M) continue;
       if (m->max_batch * e1.H * e1.W < min_cols) continue;
+      if (m->x3 && e3.has_x3 && e1.H * e1.W < x3_fire_min_hw) continue;
       if (padded_plane(e1.H * e1.W) % 4 || (m->fusion & ORE_FUSE_CONCAT) == 0) continue;  // 16-B planes (layout below)
       const Value &va = m->values[cc.in0], &vb = m->values[cc.in1], &vc = m->values[cc.out], &vs = m->values[e1.in0];
       if (va.uses != 1 || vb.uses != 1 || vc.uses != 1 || va.is_output || vb.is_output || vc.is_output || vs.es != 4) continue;
@@ -714,6 +742,14 @@ ore_status plan(ore_model* m) {
     }
     count_uses(m, m->steps);
   }
+  // (1f) ORE_LOAD_X3: every conv / matmul not taken by an f32-MFMA fusion above runs its x3 plan
+  if (m->x3)
+    for (auto& st : m->steps)
+      if ((st.kind == S_CONV || st.kind == S_MATMUL) && st.has_x3 && !st.pool && !st.epool) {
+        st.plan = st.plan_x3;
+        st.wp = st.wp_x3;
+        st.ktab = st.ktab_x3;
+      }
   // (2) Dropout / activation Reshape as aliases
   if (m->fusion & ORE_FUSE_ALIAS) {
     for (auto& s : m->steps) {
@@ -1098,6 +1134,7 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
   m->max_batch = max_batch;
   m->f16 = (flags & ORE_LOAD_F16) != 0;
   m->x3 = (flags & ORE_LOAD_X3) != 0;
+  m->x3_all = m->x3 && getenv("ORE_X3_ALL") && atoi(getenv("ORE_X3_ALL")) != 0;
   auto fail = [&](ore_status st) {
     ore_model_destroy(m);
     return st;
@@ -1171,13 +1208,19 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
                                                                                            : F16_X_NCHW32)
                           : s.C % 8 == 0           ? F16_X_NHWC_VEC
                                                    : F16_X_NHWC_ELEM;
-        s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, m->f16, xmode, m->x3);
+        s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, m->f16, xmode);
       }
       else if (s.kind == S_MATMUL)
-        s.plan = conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win, false, 0, m->x3);
+        s.plan = conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win);
       else
         continue;
       total_packed += (packed_bytes(s.plan) + 255) / 256 * 256;
+      if (m->x3 && x3_wanted(m, s)) {
+        s.has_x3 = true;
+        s.plan_x3 = s.kind == S_CONV ? conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, false, 0, true)
+                                     : conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win, false, 0, true);
+        total_packed += (packed_bytes(s.plan_x3) + 255) / 256 * 256;
+      }
     }
     if (total_packed) {
       if (hipMalloc(reinterpret_cast<void**>(&m->packed), total_packed) != hipSuccess)
@@ -1191,6 +1234,14 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
                     ctx->stream);
         s.ktab = s.plan.window ? nullptr : reinterpret_cast<int2*>(base + conv_packed_bytes(s.plan));
         poff += (packed_bytes(s.plan) + 255) / 256 * 256;
+        if (s.has_x3) {
+          char* bx = reinterpret_cast<char*>(m->packed) + poff;
+          s.wp_x3 = reinterpret_cast<float*>(bx);
+          launch_pack(m->values[s.in1].cptr, s.w_kmajor, int(s.M), int(s.C), int(s.kh), int(s.kw), s.plan_x3, s.wp_x3,
+                      ctx->stream);
+          s.ktab_x3 = reinterpret_cast<int2*>(bx + conv_packed_bytes(s.plan_x3));
+          poff += (packed_bytes(s.plan_x3) + 255) / 256 * 256;
+        }
       }
       if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
         return fail(set_error(ctx, ORE_ERR_HIP, "weight packing failed"));
@@ -1467,7 +1518,9 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
       if (ms < best_ms) { best_ms = ms; best = c; }
     }
     s.plan.cfg = best;
-    m->base_steps[m->exec_steps[k]].plan.cfg = best;  // steps are a per-plan copy of base_steps
+    // steps are a per-plan copy of base_steps
+    if (s.plan.x3) m->base_steps[m->exec_steps[k]].plan_x3.cfg = best;
+    else m->base_steps[m->exec_steps[k]].plan.cfg = best;
     if (!st) st = launch_step(m, s, n);                // leave the real output for the next step
   }
   (void)hipEventDestroy(e0);

@@ -31,6 +31,16 @@ def _np(t):
     return t.cpu().numpy()
 
 
+@pytest.fixture(autouse=True)
+def x3_all(monkeypatch, request):
+    """Kernel-level tests put every conv on x3 (ORE_X3_ALL=1); tests marked `hybrid` keep the
+    default ORE_LOAD_X3 policy (x3 where it wins, the f32-MFMA fusions elsewhere)."""
+    if "hybrid" not in request.keywords:
+        monkeypatch.setenv("ORE_X3_ALL", "1")
+    else:
+        monkeypatch.delenv("ORE_X3_ALL", raising=False)
+
+
 def conv_f64(x, w, b, pads, strides):
     """Direct convolution in float64 (zero padding, pads t, l, b, r) and sum |w x| per output."""
     x = x.astype(np.float64)
@@ -206,39 +216,81 @@ def test_x3_mnist_golden(gpu_ctx):
     m.close()
 
 
-@pytest.fixture(scope="module")
-def x3_224(gpu_ctx):
+@pytest.mark.hybrid
+def test_x3_hybrid_mnist_golden(gpu_ctx):
+    """MNIST-8 with the default x3 policy: conv 2 (5x5, 8 channels) on the window kernel, the rest
+    on the f32-MFMA kernels; still within 1e-6 max|y| of mnist_output_0.pb."""
     import ore
-    from ore import squeezenet
-    m = ore.Model(gpu_ctx, squeezenet.build(224), max_batch=256, precision="f32x3")
-    yield m
+    from ore import onnx_wire
+    with open(os.path.join(GOLD, "mnist-8.onnx"), "rb") as f:
+        m = ore.Model(gpu_ctx, f.read(), max_batch=4, precision="f32x3")
+    x = onnx_wire.load_tensor(os.path.join(GOLD, "mnist_data_0.pb")).to_numpy()
+    g = onnx_wire.load_tensor(os.path.join(GOLD, "mnist_output_0.pb")).to_numpy()
+    y = _np(m.run(_t(x)))
+    assert np.abs(y - g).max() <= 1e-6 * np.abs(g).max()
+    names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+    assert sum(n.startswith("x3w") for n in names) == 1, names
     m.close()
 
 
-def test_x3_squeezenet_synth_vs_oracle(x3_224):
+def _x3_model(gpu_ctx, hybrid, max_batch):
+    import ore
+    from ore import squeezenet
+    if hybrid:
+        os.environ.pop("ORE_X3_ALL", None)
+    else:
+        os.environ["ORE_X3_ALL"] = "1"
+    try:
+        return ore.Model(gpu_ctx, squeezenet.build(224), max_batch=max_batch, precision="f32x3")
+    finally:
+        os.environ.pop("ORE_X3_ALL", None)
+
+
+@pytest.mark.parametrize("hybrid", [True, False])
+def test_x3_squeezenet_synth_vs_oracle_and_f64(gpu_ctx, hybrid):
+    """Synthetic SqueezeNet @224: <= 1e-5 max-abs of the oracle (the bar), same argmax, and no
+    farther from the float64 result than the oracle itself is (block summation makes the x3 convs
+    more accurate than an f32 fma chain)."""
     from golden.make_golden import squeezenet_inputs
     ref = np.load(os.path.join(GOLD, "squeezenet_synth_oracle.npz"))["output"]
-    y = _np(x3_224.run(_t(squeezenet_inputs())))
+    f64 = np.load(os.path.join(GOLD, "squeezenet_synth_f64.npz"))["output"]
+    m = _x3_model(gpu_ctx, hybrid, 2)
+    y = _np(m.run(_t(squeezenet_inputs())))
+    m.close()
     assert np.abs(y - ref).max() <= 1e-5
     assert np.array_equal(y.argmax(1), ref.argmax(1))
+    assert np.abs(y - f64).max() <= np.abs(ref - f64).max() * 1.5
 
 
-def test_x3_squeezenet_batch256_properties(x3_224):
+@pytest.mark.parametrize("hybrid", [True, False])
+def test_x3_squeezenet_batch256_properties(gpu_ctx, hybrid):
     """B = 256: rows sum to 1, each image equals itself run alone bit for bit, and the autotuned
     tiles change no bit."""
+    import torch
     from ore import squeezenet
+    m = _x3_model(gpu_ctx, hybrid, 256)
     x = squeezenet.synthetic_input(256, 224, seed=123)
     xt = _t(x)
-    y = _np(x3_224.run(xt))
+    y = _np(m.run(xt))
     assert y.shape == (256, 1000) and np.isfinite(y).all()
     assert np.abs(y.sum(1) - 1.0).max() <= 1e-5
     for i in (0, 77, 255):
-        yi = _np(x3_224.run(xt[i:i + 1].contiguous()))
+        yi = _np(m.run(xt[i:i + 1].contiguous()))
         assert np.array_equal(yi[0], y[i]), i
-    import torch
     out = torch.empty((256, 1000), device="cuda")
-    x3_224.autotune(xt, out)
-    assert np.array_equal(_np(x3_224.run(xt)), y)
+    m.autotune(xt, out)
+    assert np.array_equal(_np(m.run(xt)), y)
+    names = [ore_tile_name(t) for t in m.tiles() if t >= 0]
+    m.close()
+    if hybrid:  # conv1 + pool1 on the f32-MFMA walker, the expand3x3s and conv10 on x3
+        assert names[0].startswith("epool") and sum(n.startswith("x3") for n in names) >= 6, names
+    else:
+        assert all(n.startswith("x3") for n in names), names
+
+
+def ore_tile_name(t):
+    import ore
+    return ore.Model.TILE_NAMES[t]
 
 
 def test_x3_node_level_parity(gpu_ctx):
