@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-b1", action="store_true", help="skip the batch-1 latency probe")
     ap.add_argument("--no-autotune", action="store_true", help="keep the heuristic per-layer conv tiles")
     ap.add_argument("--dump-steps", default="", help="write the plan's kernel steps (op, name, flops, bytes) as JSON")
+    ap.add_argument("--no-winograd", action="store_true",
+                    help="f32: 3x3 stride-1 convs on the direct kernels only (ORE_LOAD_NO_WINOGRAD)")
     ap.add_argument("--fusion", type=int, default=None, help="ore_model_set_fusion flags (experiments; default: the model's)")
     ap.add_argument("--precision", choices=["f32", "f32x3", "f16"], default="f32",
                     help="f32: convs on the f32-input MFMA; f32x3: the same f32 model with its convs on the BF16 "
@@ -82,7 +84,7 @@ def cpu_baseline(model_bytes, hw, threads):
                       f"{float(np.median(done)):.2f} s"}
 
 
-def b1_latency(model_bytes, hw, local, precision, iters=200):
+def b1_latency(model_bytes, hw, local, precision, winograd=True, iters=200):
     """Batch-1 latency (SURVEY.md §8(d) B = 1 config): one image per synchronous call, issued
     as plain launches, as one HIP-graph replay, and as a graph with the fire modules' expand
     branches on two streams (ore_model_set_streams).  Milliseconds per image."""
@@ -94,7 +96,7 @@ def b1_latency(model_bytes, hw, local, precision, iters=200):
     x = (torch.rand((1, 3, hw, hw), device=f"cuda:{local}") * 100.0 - 50.0).contiguous()
     res = {}
     for label, streams, graph in (("plain_ms", 1, False), ("graph_ms", 1, True), ("graph_2streams_ms", 2, True)):
-        m = ore.Model(ctx, model_bytes, max_batch=1, precision=precision)
+        m = ore.Model(ctx, model_bytes, max_batch=1, precision=precision, winograd=winograd)
         m.set_streams(streams)
         out = torch.empty((1, m.output_elems), device=f"cuda:{local}")
         torch.cuda.synchronize()
@@ -139,7 +141,7 @@ def main():
     B = args.global_batch // world if strong else args.batch
     model_bytes = squeezenet.build(args.hw)
     ctx = ore.Context(local)
-    model = ore.Model(ctx, model_bytes, max_batch=B, precision=args.precision)
+    model = ore.Model(ctx, model_bytes, max_batch=B, precision=args.precision, winograd=not args.no_winograd)
     f16 = args.precision == "f16"
     x3 = args.precision == "f32x3"
     g = torch.Generator(device=f"cuda:{local}")
@@ -273,7 +275,8 @@ def main():
             if f16:
                 result["top1_agrees_with_cpu"] = bool((out[:2].cpu().numpy().argmax(1) == ref.argmax(1)).all())
             if not args.no_b1:
-                result["b1_latency_ms"] = b1_latency(model_bytes, args.hw, local, args.precision)
+                result["b1_latency_ms"] = b1_latency(model_bytes, args.hw, local, args.precision,
+                                                     winograd=not args.no_winograd)
             if not args.no_cpu_baseline:
                 threads = args.cpu_threads or min(16, os.cpu_count() or 1)
                 result["cpu_baseline"] = cpu_baseline(model_bytes, args.hw, threads)

@@ -93,6 +93,15 @@ ore_status ore_ctx_set_stream(ore_ctx* ctx, void* hip_stream);
 void* ore_ctx_get_stream(ore_ctx* ctx);
 ore_status ore_sync(ore_ctx* ctx);
 const char* ore_last_error(ore_ctx* ctx);
+/* Conv algorithm of the per-op entry ore_conv2d_f32 on this context (extension; the reference has
+ * one algorithm, im2col + per-channel dots, convolution_op.rs:224-517).  ORE_CONV_ALGO_DIRECT (the
+ * default): the implicit GEMM in the reference's k order.  ORE_CONV_ALGO_WINOGRAD: 3x3 / stride-1 /
+ * pad-1 convs with C % 8 == 0 by Winograd F(2x2, 3x3) in f32 (2.25x fewer MFMAs; its error against a
+ * float64 reference is at or below the direct f32 conv's, but results are not bit-identical to it);
+ * other geometries stay direct.  Models choose per ORE_LOAD_NO_WINOGRAD instead. */
+#define ORE_CONV_ALGO_DIRECT 0
+#define ORE_CONV_ALGO_WINOGRAD 1
+ore_status ore_ctx_set_conv_algo(ore_ctx* ctx, int32_t algo);
 
 ore_status ore_malloc(ore_ctx* ctx, size_t bytes, void** dptr);
 ore_status ore_free(ore_ctx* ctx, void* dptr);
@@ -163,6 +172,11 @@ ore_status ore_model_parse(const void* onnx_bytes, size_t len);
  * tile-independent but not bit-identical to the f32-MFMA kernels (a different summation order).
  * The fire / pooled-conv fusions are f32-MFMA kernels and are not applied to an x3 model. */
 #define ORE_LOAD_X3 2
+/* ORE_LOAD_NO_WINOGRAD: an f32 model runs its 3x3 / stride-1 / pad-1 convs (SqueezeNet's
+ * expand3x3) on the direct kernels only.  By default (f32 models, not x3) every such conv that no
+ * direct-kernel fusion takes runs Winograd F(2x2, 3x3) in f32 (ore_conv_wino.hip; see
+ * ORE_CONV_ALGO_WINOGRAD above).  The choice is made at load time, never by timing. */
+#define ORE_LOAD_NO_WINOGRAD 4
 ore_status ore_model_load_ex(ore_ctx* ctx, const void* onnx_bytes, size_t len, int64_t max_batch, int32_t flags,
                              ore_model** out);
 ore_status ore_model_destroy(ore_model* m);

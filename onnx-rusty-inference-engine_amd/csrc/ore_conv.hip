@@ -949,9 +949,18 @@ static const int CFG_BN[4] = {128, 128, 128, 256};
 
 
 ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
-                   bool is1x1, bool f16, int xmode, bool x3) {
-  (void)H; (void)W; (void)pt;
+                   bool is1x1, bool f16, int xmode, bool x3, bool wino) {
+  (void)pt;
   ConvPlan pln{};
+  if (wino && !x3 && !f16 && conv_wino_geometry(C, kh, kw, sh, sw, pt, pl, H, W, Ho, Wo)) {
+    pln.wino = 1;
+    pln.cfg = WINO_TILE_BASE + 0;
+    const int forced = env_int("ORE_WINO_TILE", -1);  // tuning knob
+    if (forced >= 0 && forced < WINO_TILES_N) pln.cfg = WINO_TILE_BASE + forced;
+    pln.Mp = wino_packed_mp(M);
+    pln.krows = 16 * C;  // U is 16 positions x C rows of Mp floats
+    return pln;
+  }
   if (x3 && !f16) {  // ore_conv_x3.hip: packed rows cover every x3 tile (64 / 96 / 128 rows)
     pln.x3 = 1;
     pln.cfg = X3_TILE_BASE + x3_tile_config(M);
@@ -1045,6 +1054,10 @@ size_t conv_packed_bytes(const ConvPlan& pln) {
 
 void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, const ConvPlan& pln, float* wp,
                  hipStream_t s) {
+  if (pln.wino) {
+    launch_pack_wino(w, M, C, pln.Mp, wp, s);
+    return;
+  }
   if (pln.x3 == 2) {
     launch_pack_x3w(w, M, C, kh, kw, pln.Mp, pln.bch, pln.ks, pln.nst, wp, s);
     return;
@@ -1088,6 +1101,13 @@ thread_local int last_conv_tile = -1;
 
 void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
   last_conv_tile = pln.cfg;
+  if (pln.wino) {  // the caller (run_conv) keeps x_bytes within the buffer range
+    int t = pln.cfg - WINO_TILE_BASE;
+    if (!conv_wino_eligible(p, t)) t = 2;
+    last_conv_tile = WINO_TILE_BASE + t;
+    launch_conv_wino(p, t, s);
+    return;
+  }
   if (pln.x3) {  // the caller (run_conv) checked conv_x3_eligible
     int t = pln.cfg - X3_TILE_BASE;
     if (pln.x3 == 2) {

@@ -1,0 +1,474 @@
+// 3x3 / stride-1 / pad-1 Conv (convolution_op.rs:94-517 at SqueezeNet's expand3x3 geometry) by
+// Winograd F(2x2, 3x3) in f32 on the f32-input MFMA (v_mfma_f32_32x32x2_f32; 16x16x4 variants).
+//
+// Every 2x2 block ("tile") of output pixels of one channel m is
+//   Y = A^T [ sum_c (G g_mc G^T) .* (B^T d_c B) ] A
+// with d_c the 4x4 input window of channel c (rows 2ty-1 .. 2ty+2, columns 2tx-1 .. 2tx+2, zero
+// outside the image: the reference's zero padding) and g_mc the 3x3 kernel.  The 16 element-wise
+// products over c are 16 independent GEMMs ("positions" xi = 4 i + j):
+//   M_xi[m][t] = sum_c U_xi[m][c] V_xi[c][t],   U = G g G^T (packed once), V = B^T d B (per k-step)
+// so the MFMA work is 16 C M per tile against 36 C M for the direct conv (2.25x fewer MFMAs).  All
+// arithmetic is f32; each position sums C products (the direct conv sums 9C), and the measured error
+// against a float64 reference is at or below the direct f32 conv's (DESIGN.md section 3.3,
+// tests/test_wino_gpu.py).  The results are NOT bit-identical to the direct kernels; they do not
+// depend on the tile (every position is one c-ordered chain, the transforms a fixed add order).
+//
+// Operands go straight from global memory (L1/L2) into the MFMA registers, as in the streaming conv
+// (no LDS, no barrier; each wave runs independently):
+//   * B: in the 32x32x2 kernel lane l of MFMA xi supplies V_xi[c = 2 s + (l >> 5)][tile l & 31]: it
+//     loads the 4x4 window of its tile for that channel (four 16-B row loads, 4-B aligned; rows
+//     outside the image get an out-of-range buffer offset and read as 0; the image's first tile
+//     column loads from column 0 and shifts right in registers, so no offset is negative), zeroes the
+//     columns outside the image and transforms it in registers (32 adds): one window feeds 16 MFMAs.
+//   * A: U is packed [c][xi / 4][m][xi % 4]: a lane's 16 positions of its channel row are four 16-B
+//     loads, each wave-instruction two contiguous 512-B runs.
+//   * the K loop is unrolled, with the weights DA and the windows DB k-steps ahead in register rings.
+// Wave tile: 32 channels x 32 tiles (128 output pixels, 16 x 16 accumulators of 16 floats in the
+// AccVGPRs); 4 waves per block share a tile group when M >= 128 (their windows hit the CU's L1).
+// Epilogue: each lane holds all 16 positions of 16 (channel, tile) pairs -> A^T M A (24 adds) + bias
+// (+ Relu) -> 4 pixels each, no cross-lane traffic.
+// The 16x16x4 kernel (16 MF channels x 16 NT tiles per wave) is the same scheme at other tile shapes.
+#include <hip/hip_runtime.h>
+
+#include "ore_kernels.h"
+
+namespace ore {
+
+typedef float wg_floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16_t __attribute__((ext_vector_type(16)));
+
+// U[((c * 4 + xi / 4) * Mp + m) * 4 + xi % 4] = (G g_mc G^T)[xi / 4][xi % 4] (f64, rounded once): for a
+// fixed (channel, position quad) the channels' 16-B quads are contiguous, so the A loads of a wave
+// (one quad per lane, consecutive channels in consecutive lanes) are 512-B runs;
+// G = [[1, 0, 0], [1/2, 1/2, 1/2], [1/2, -1/2, 1/2], [0, 0, 1]]; rows m >= M are zero
+__global__ __launch_bounds__(256) void wino_pack_kernel(const float* __restrict__ w, float* __restrict__ u, int M,
+                                                        int C, int Mp) {
+  const long long total = (long long)C * Mp * 16;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long r = i >> 2;  // (c * 4 + q) * Mp + m
+    const int m = (int)(r % Mp);
+    const long long cq = r / Mp;
+    const int c = (int)(cq >> 2);
+    const int xi = (int)(((cq & 3) << 2) | (i & 3));
+    float v = 0.0f;
+    if (m < M) {
+      const double G[4][3] = {{1.0, 0.0, 0.0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0.0, 0.0, 1.0}};
+      const float* g = w + ((long long)m * C + c) * 9;
+      const int a = xi >> 2, b = xi & 3;
+      double s = 0.0;
+      for (int p = 0; p < 3; ++p)
+        for (int q = 0; q < 3; ++q) s += G[a][p] * (double)g[p * 3 + q] * G[b][q];
+      v = (float)s;
+    }
+    u[i] = v;
+  }
+}
+
+int wino_packed_mp(int M) { return (M + 63) / 64 * 64; }
+
+void launch_pack_wino(const float* w, int M, int C, int Mp, float* u, hipStream_t s) {
+  long long blocks = ((long long)C * Mp * 16 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(wino_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, w, u, M, C, Mp);
+}
+
+// V = B^T d B of a 4x4 window (rows i, columns j), B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]];
+// v[4 i + j]
+__device__ __forceinline__ void wg_input_transform(const float (&d)[4][4], float (&v)[16]) {
+  float t[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    t[0][j] = d[0][j] - d[2][j];
+    t[1][j] = d[1][j] + d[2][j];
+    t[2][j] = d[2][j] - d[1][j];
+    t[3][j] = d[1][j] - d[3][j];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[4 * i + 0] = t[i][0] - t[i][2];
+    v[4 * i + 1] = t[i][1] + t[i][2];
+    v[4 * i + 2] = t[i][2] - t[i][1];
+    v[4 * i + 3] = t[i][1] - t[i][3];
+  }
+}
+
+// Y = A^T M A, A^T = [[1,1,1,0],[0,1,-1,-1]]: y[2 i + j] (i = row, j = column of the 2x2 tile)
+__device__ __forceinline__ void wg_output_transform(const float (&mx)[16], float (&y)[4]) {
+  float t0[4], t1[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    t0[j] = mx[j] + mx[4 + j] + mx[8 + j];
+    t1[j] = mx[4 + j] - mx[8 + j] - mx[12 + j];
+  }
+  y[0] = t0[0] + t0[1] + t0[2];
+  y[1] = t0[1] - t0[2] - t0[3];
+  y[2] = t1[0] + t1[1] + t1[2];
+  y[3] = t1[1] - t1[2] - t1[3];
+}
+
+constexpr int WG_OOB = 0x7FFFFF00;  // a buffer offset past any resource (x_bytes < 2^31 - 2^21)
+
+// the tile and window geometry of one lane: tile t (flattened over images), its window's row byte
+// offsets for input channel `csub` (out-of-range rows -> WG_OOB), the column shift of the image's
+// first tile column, the column-validity masks of the loaded elements and the output position
+struct WgTile {
+  int roff[4];
+  int ybase;         // output element offset of the tile's top-left pixel (channel 0)
+  unsigned cmask;    // bit k: loaded element k lies inside the row
+  bool sh1, tok, c1ok, r1ok;
+};
+
+__device__ __forceinline__ WgTile wg_tile(const ConvParams& p, int t, int csub, int T, int TW, int TPI) {
+  WgTile w;
+  w.tok = t < T;
+  if (!w.tok) t = T - 1;
+  const int img = t / TPI;
+  const int rem = t - img * TPI;
+  const int ty = rem / TW, tx = rem - ty * TW;
+  const int iy0 = 2 * ty - 1;
+  w.sh1 = tx == 0;
+  const int cs = w.sh1 ? 0 : 2 * tx - 1;  // first loaded column
+  unsigned cm = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) cm |= (cs + k < p.W ? 1u : 0u) << k;
+  w.cmask = cm;
+  const int base = (img * (int)p.x_nstride + csub * p.x_ps + cs) * 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) w.roff[r] = (unsigned)(iy0 + r) < (unsigned)p.H ? base + (iy0 + r) * p.W * 4 : WG_OOB;
+  w.ybase = img * (int)p.y_nstride + (2 * ty) * p.W + 2 * tx;
+  w.c1ok = 2 * tx + 1 < p.W;
+  w.r1ok = 2 * ty + 1 < p.H;
+  return w;
+}
+
+// the 4 loaded rows of a window -> V = B^T d B (column masks, first-column shift)
+__device__ __forceinline__ void wg_window(const wg_floatx4 (&rows)[4], const WgTile& w, float (&v)[16]) {
+  float d[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int4 q = __builtin_bit_cast(int4, rows[r]);
+    const int e0 = q.x, e1 = q.y & __builtin_amdgcn_sbfe((int)w.cmask, 1, 1);
+    const int e2 = q.z & __builtin_amdgcn_sbfe((int)w.cmask, 2, 1);
+    const int e3 = q.w & __builtin_amdgcn_sbfe((int)w.cmask, 3, 1);
+    d[r][0] = w.sh1 ? 0.0f : __builtin_bit_cast(float, e0);
+    d[r][1] = __builtin_bit_cast(float, w.sh1 ? e0 : e1);
+    d[r][2] = __builtin_bit_cast(float, w.sh1 ? e1 : e2);
+    d[r][3] = __builtin_bit_cast(float, w.sh1 ? e2 : e3);
+  }
+  wg_input_transform(d, v);
+}
+
+// the 16 position sums of one (channel m, tile) -> bias b (+ Relu) -> the tile's (up to) 4 pixels
+__device__ __forceinline__ void wg_store(const ConvParams& p, const WgTile& w, int m, float b, const float (&mx)[16]) {
+  float o[4];
+  wg_output_transform(mx, o);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    o[q] += b;
+    if (p.relu) o[q] = fmaxf(o[q], 0.0f);
+  }
+  if (!w.tok) return;
+#ifdef ORE_EXP_WG_NOSTORE  // timing experiment only: stores skipped (kept live by a never-true test)
+  if (o[0] != 1.2345e-30f) return;
+#endif
+  float* yp = p.y + (unsigned)(w.ybase + m * p.y_ps);
+  yp[0] = o[0];
+  if (w.c1ok) yp[1] = o[1];
+  if (w.r1ok) {
+    yp[p.W] = o[2];
+    if (w.c1ok) yp[p.W + 1] = o[3];
+  }
+}
+
+// The K loop of both kernels over WG_LOAD_A(slot, step), WG_LOAD_B(slot, step), WG_MFMA(a slot, b slot)
+#define WG_KLOOP(NKS_RT)                                                                               \
+  if constexpr (NKS > 0) {                                                                             \
+    /* step s: its MFMAs (operands A slot s % DA, windows transformed during step s - 1) interleaved  \
+       with the refill loads and the transform of step s + 1's windows, so the loads' and VALU's     \
+       issue cycles hide behind the MFMA pipe (one wave per SIMD: nothing else would cover them) */   \
+    _Pragma("unroll") for (int s_ = 0; s_ < (DB < NKS ? DB : NKS); ++s_) { WG_LOAD_B(s_, s_) }          \
+    _Pragma("unroll") for (int s_ = 0; s_ < (DA < NKS ? DA : NKS); ++s_) { WG_LOAD_A(s_, s_) }          \
+    WG_WINDOWS(0, vc_)                                                                                 \
+    _Pragma("unroll") for (int s_ = 0; s_ < NKS; ++s_) {                                              \
+      __builtin_amdgcn_sched_barrier(0);                                                               \
+      WG_MFMAS(s_ % DA, vc_);                                                                          \
+      if (s_ + 1 < NKS) { WG_WINDOWS((s_ + 1) % DB, vn_) }                                             \
+      if (s_ + DA < NKS) { WG_LOAD_A(s_ % DA, s_ + DA) }                                               \
+      if (s_ + DB < NKS) { WG_LOAD_B(s_ % DB, s_ + DB) }                                               \
+      _Pragma("unroll") for (int i_ = 0; i_ < WG_NMFMA; ++i_) {                                        \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); /* one MFMA */                              \
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0); /* one VMEM read */                         \
+        __builtin_amdgcn_sched_group_barrier(0x002, WG_VALU_PER_MFMA, 0);                              \
+      }                                                                                                \
+      __builtin_amdgcn_sched_barrier(0);                                                               \
+      WG_COPYV(vc_, vn_)                                                                               \
+    }                                                                                                  \
+  } else { /* rolled: 2-deep rings (host: the k-step count is even) */                                \
+    const int nks_ = (NKS_RT);                                                                         \
+    _Pragma("unroll") for (int d_ = 0; d_ < 2; ++d_) { WG_LOAD_A(d_, d_) WG_LOAD_B(d_, d_) }           \
+    for (int s0_ = 0; s0_ < nks_ - 2; s0_ += 2) {                                                      \
+      _Pragma("unroll") for (int d_ = 0; d_ < 2; ++d_) {                                               \
+        WG_MFMA(d_, d_);                                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                                             \
+        WG_LOAD_A(d_, s0_ + 2 + d_)                                                                    \
+        WG_LOAD_B(d_, s0_ + 2 + d_)                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                             \
+      }                                                                                                \
+    }                                                                                                  \
+    _Pragma("unroll") for (int d_ = 0; d_ < 2; ++d_) { WG_MFMA(d_, d_); }                              \
+  }
+
+__device__ __forceinline__ int wg_block_wave(int* gw) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // XCD-aware bijective block remap, as in the other conv kernels
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
+  const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
+  *gw = wgid * 4 + wave;
+  return wave;
+}
+
+// 32x32x2 kernel: 32 channels x 32 tiles per wave.  NKS > 0: the K loop has exactly NKS k-steps (2
+// channels each) and is unrolled completely, the A operands (weights, L2-resident) DA k-steps ahead
+// and the B windows (activations, first touch from HBM / the Infinity Cache) DB k-steps ahead, and
+// the compiler's wait-count pass waits for each step's own loads (in a rolled loop it drains every
+// load at the loop head, exposing a full memory latency per ring turn); NKS = 0: any C, a rolled
+// loop with 2-deep rings.
+template <int DA, int DB, int NKS>
+__global__ __launch_bounds__(256, 1) void conv_wino32_kernel(ConvParams p) {
+  const int lane = threadIdx.x & 63;
+  int gw;
+  wg_block_wave(&gw);
+  const int mt = gw % p.mtiles, tg = gw / p.mtiles;
+  if (tg >= p.ntiles) return;  // wave-uniform; no barrier in this kernel
+  const int m0 = mt * 32;
+  const int lr = lane >> 5, lc = lane & 31;
+  const int TW = (p.W + 1) >> 1, TPI = TW * ((p.H + 1) >> 1);
+  const WgTile w = wg_tile(p, tg * 32 + lc, lr, p.N * TPI, TW, TPI);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0,
+                                                                      (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0,
+                                                                      p.C * p.Mp * 16 * 4, 0x00020000);
+  const int aoff = (lr * 4 * p.Mp + m0 + lc) * 16;  // bytes: U[c = lr][quad 0][m0 + lc]; + Mp 16 per quad
+  const int aq = p.Mp * 16, astep = 2 * 4 * p.Mp * 16, xstep = 8 * p.x_ps;
+  // the wave's 32 biases by scalar loads before the K loop (a vector load in the epilogue would wait
+  // on the stores issued before it; SGPRs keep the VGPRs for the ring)
+  float bs[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) bs[j] = p.bias ? p.bias[min(m0 + j, p.M - 1)] : 0.0f;
+
+  floatx16_t acc[16];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[xi][e] = 0.0f;
+  wg_floatx4 ra[DA][4], rb[DB][4];
+#ifndef ORE_EXP_WG_NOA
+#define WG_LOAD_A(SLOT, S_)                                                                            \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) ra[SLOT][i] = __builtin_bit_cast(                    \
+        wg_floatx4, __builtin_amdgcn_raw_buffer_load_b128(ur, aoff + aq * i, (S_) * astep, 0));
+#else  // timing experiment only (tools/build_exp.sh): no A loads
+#define WG_LOAD_A(SLOT, S_)                                                                            \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) ra[SLOT][i] = wg_floatx4{(float)(S_), 1.f, 2.f, 3.f};
+#endif
+#if !defined(ORE_EXP_WG_NOB) && !defined(ORE_EXP_WG_ALIGNB)
+#define WG_LOAD_B(SLOT, S_)                                                                            \
+    _Pragma("unroll") for (int r = 0; r < 4; ++r) rb[SLOT][r] = __builtin_bit_cast(                    \
+        wg_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, w.roff[r], (S_) * xstep, 0));
+#elif defined(ORE_EXP_WG_ALIGNB)  // timing experiment only: the B rows loaded from 16-B aligned offsets
+#define WG_LOAD_B(SLOT, S_)                                                                            \
+    _Pragma("unroll") for (int r = 0; r < 4; ++r) rb[SLOT][r] = __builtin_bit_cast(                    \
+        wg_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, w.roff[r] & ~15, (S_) * xstep, 0));
+#else  // timing experiment only: no B loads
+#define WG_LOAD_B(SLOT, S_)                                                                            \
+    _Pragma("unroll") for (int r = 0; r < 4; ++r) rb[SLOT][r] = wg_floatx4{(float)(S_), (float)lane, 2.f, 3.f};
+#endif
+#define WG_MFMA(SA, SB)                                                                                \
+  {                                                                                                    \
+    float v_[16];                                                                                      \
+    wg_window(rb[SB], w, v_);                                                                          \
+    WG_MFMAS(SA, v_)                                                                                   \
+  }
+#define WG_MFMAS(SA, V)                                                                                \
+    _Pragma("unroll") for (int xi = 0; xi < 16; ++xi)                                                  \
+        acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[SA][xi >> 2][xi & 3], V[xi], acc[xi], 0, 0, 0);
+#define WG_WINDOWS(SB, V) wg_window(rb[SB], w, V);
+#define WG_COPYV(D_, S_) _Pragma("unroll") for (int i = 0; i < 16; ++i) D_[i] = S_[i];
+#define WG_NMFMA 16
+#define WG_VALU_PER_MFMA 4
+  float vc_[16], vn_[16];
+  WG_KLOOP(p.C >> 1)
+#undef WG_MFMAS
+#undef WG_WINDOWS
+#undef WG_COPYV
+#undef WG_NMFMA
+#undef WG_VALU_PER_MFMA
+#undef WG_LOAD_A
+#undef WG_LOAD_B
+#undef WG_MFMA
+  // accumulator element e of a lane is row (e & 3) + 8 (e >> 2) + 4 lr (channel), column lc (tile)
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int m = m0 + (e & 3) + 8 * (e >> 2) + 4 * lr;
+    if (m >= p.M) continue;
+    float mx[16];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) mx[xi] = acc[xi][e];
+    const int r = (e & 3) + 8 * (e >> 2);
+    wg_store(p, w, m, lr ? bs[r + 4] : bs[r], mx);
+  }
+}
+
+// 16x16x4 kernel: MF 16-channel fragments x NT 16-tile groups per wave (row slot j of fragment f is
+// channel m0 + MF j + f); k-steps of 4 channels; DA, DB, NKS as in conv_wino32_kernel
+template <int MF, int NT, int DA, int DB, int NKS>
+__global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
+  const int lane = threadIdx.x & 63;
+  int gw;
+  wg_block_wave(&gw);
+  const int mt = gw % p.mtiles, tg = gw / p.mtiles;
+  if (tg >= p.ntiles) return;
+  const int m0 = mt * (16 * MF);
+  const int lk = lane >> 4, lj = lane & 15;
+  const int TW = (p.W + 1) >> 1, TPI = TW * ((p.H + 1) >> 1);
+  WgTile w[NT];
+#pragma unroll
+  for (int g = 0; g < NT; ++g) w[g] = wg_tile(p, (tg * NT + g) * 16 + lj, lk, p.N * TPI, TW, TPI);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0,
+                                                                      (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0,
+                                                                      p.C * p.Mp * 16 * 4, 0x00020000);
+  const int aoff = (lk * 4 * p.Mp + m0 + MF * lj) * 16;  // U[c = lk][quad 0][MF consecutive channels]
+  const int aq = p.Mp * 16, astep = 4 * 4 * p.Mp * 16, xstep = 16 * p.x_ps;
+  float bias[MF][4];
+#pragma unroll
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + MF * (4 * lk + e) + f;
+      bias[f][e] = p.bias && m < p.M ? p.bias[m] : 0.0f;
+    }
+
+  wg_floatx4 acc[16][MF][NT];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+    for (int f = 0; f < MF; ++f)
+#pragma unroll
+      for (int g = 0; g < NT; ++g) acc[xi][f][g] = wg_floatx4{0.f, 0.f, 0.f, 0.f};
+  wg_floatx4 ra[DA][MF][4], rb[DB][NT][4];
+#define WG_LOAD_A(SLOT, S)                                                                             \
+  {                                                                                                    \
+    const int st_ = (S);                                                                               \
+    _Pragma("unroll") for (int f = 0; f < MF; ++f)                                                     \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) ra[SLOT][f][i] = __builtin_bit_cast(                 \
+        wg_floatx4, __builtin_amdgcn_raw_buffer_load_b128(ur, aoff + 16 * f + aq * i, st_ * astep, 0)); \
+  }
+#define WG_LOAD_B(SLOT, S)                                                                             \
+  {                                                                                                    \
+    const int st_ = (S);                                                                               \
+    _Pragma("unroll") for (int g = 0; g < NT; ++g)                                                     \
+    _Pragma("unroll") for (int r = 0; r < 4; ++r) rb[SLOT][g][r] = __builtin_bit_cast(                 \
+        wg_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, w[g].roff[r], st_ * xstep, 0));          \
+  }
+#define WG_MFMA(SA, SB)                                                                                \
+  {                                                                                                    \
+    float v_[NT][16];                                                                                  \
+    WG_WINDOWS(SB, v_)                                                                                 \
+    WG_MFMAS(SA, v_)                                                                                   \
+  }
+#define WG_MFMAS(SA, V)                                                                                \
+    _Pragma("unroll") for (int xi = 0; xi < 16; ++xi)                                                  \
+    _Pragma("unroll") for (int f = 0; f < MF; ++f)                                                     \
+    _Pragma("unroll") for (int g = 0; g < NT; ++g)                                                     \
+        acc[xi][f][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SA][f][xi >> 2][xi & 3], V[g][xi], acc[xi][f][g], 0, 0, 0);
+#define WG_WINDOWS(SB, V) _Pragma("unroll") for (int g = 0; g < NT; ++g) wg_window(rb[SB][g], w[g], V[g]);
+#define WG_COPYV(D_, S_) \
+    _Pragma("unroll") for (int g = 0; g < NT; ++g) _Pragma("unroll") for (int i = 0; i < 16; ++i) D_[g][i] = S_[g][i];
+#define WG_NMFMA (16 * MF * NT)
+#define WG_VALU_PER_MFMA 2
+  float vc_[NT][16], vn_[NT][16];
+  WG_KLOOP(p.C >> 2)
+#undef WG_MFMAS
+#undef WG_WINDOWS
+#undef WG_COPYV
+#undef WG_NMFMA
+#undef WG_VALU_PER_MFMA
+#undef WG_LOAD_A
+#undef WG_LOAD_B
+#undef WG_MFMA
+  // lane (lk, lj) of fragment f holds rows 4 lk + e = channel m0 + MF (4 lk + e) + f of tile lj
+#pragma unroll
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + MF * (4 * lk + e) + f;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int g = 0; g < NT; ++g) {
+        float mx[16];
+#pragma unroll
+        for (int xi = 0; xi < 16; ++xi) mx[xi] = acc[xi][f][g][e];
+        wg_store(p, w[g], m, bias[f][e], mx);
+      }
+    }
+}
+
+// Winograd tiles (ConvPlan cfg = WINO_TILE_BASE + t): shape (32: 32x32x2, 16: 16x16x4), channels and
+// 2x2 tiles per wave, A / B ring depths of the unrolled K loop
+struct WinoTile { int shape, ch, tiles, da, db; };
+static const WinoTile WINO_TILES[WINO_TILES_N] = {{32, 32, 32, 2, 8}, {32, 32, 32, 2, 4}, {16, 32, 16, 2, 8},
+                                                  {16, 16, 32, 2, 4}};
+
+bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo) {
+  return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && Ho == H && Wo == W && C % 16 == 0 && C > 0;
+}
+
+bool conv_wino_eligible(const ConvParams& p, int tile) {
+  if (tile < 0 || tile >= WINO_TILES_N) return false;
+  const WinoTile& wt = WINO_TILES[tile];
+  const int nks = p.C / (wt.shape == 32 ? 2 : 4);
+  return conv_wino_geometry(p.C, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.H, p.W, p.Ho, p.Wo) && nks % 2 == 0 &&
+         p.x_bytes > 0 && p.x_bytes < (1LL << 31) - (1LL << 21) && (reinterpret_cast<uintptr_t>(p.x) & 3) == 0 &&
+         p.Mp % 64 == 0 && (long long)p.C * p.Mp * 64 < (1LL << 31) &&
+         (long long)p.N * ((p.H + 1) / 2) * ((p.W + 1) / 2) < (1LL << 30);
+}
+
+static void wg_grid(ConvParams& p, int ch, int tiles, dim3* grid) {
+  const long long T = (long long)p.N * ((p.H + 1) / 2) * ((p.W + 1) / 2);
+  p.mtiles = (p.M + ch - 1) / ch;
+  p.ntiles = (int)((T + tiles - 1) / tiles);
+  const long long waves = (long long)p.mtiles * p.ntiles;
+  *grid = dim3((unsigned)((waves + 3) / 4));
+}
+
+void launch_conv_wino(const ConvParams& p0, int tile, hipStream_t s) {
+  ConvParams p = p0;
+  const WinoTile& wt = WINO_TILES[tile < 0 || tile >= WINO_TILES_N ? 0 : tile];
+  dim3 grid;
+  wg_grid(p, wt.ch, wt.tiles, &grid);
+  // C = 16, 32, 48, 64 (SqueezeNet's expand3x3 inputs): K loop fully unrolled
+  const int cq = p.C % 16 == 0 && p.C <= 64 ? p.C / 16 : 0;
+#define WG_L32(DA_, DB_, CQ) hipLaunchKernelGGL((conv_wino32_kernel<DA_, DB_, 8 * CQ>), grid, dim3(256), 0, s, p)
+#define WG_L16(MF_, NT_, DA_, DB_, CQ) \
+  hipLaunchKernelGGL((conv_wino16_kernel<MF_, NT_, DA_, DB_, 4 * CQ>), grid, dim3(256), 0, s, p)
+#define WG_BY_C(L, ...)                         \
+  switch (cq) {                                 \
+    case 1: L(__VA_ARGS__, 1); break;           \
+    case 2: L(__VA_ARGS__, 2); break;           \
+    case 3: L(__VA_ARGS__, 3); break;           \
+    case 4: L(__VA_ARGS__, 4); break;           \
+    default: L(__VA_ARGS__, 0); break;          \
+  }
+  switch (tile) {
+    case 0: WG_BY_C(WG_L32, 2, 8); break;
+    case 1: WG_BY_C(WG_L32, 2, 4); break;
+    case 2: WG_BY_C(WG_L16, 2, 1, 2, 8); break;
+    default: WG_BY_C(WG_L16, 1, 2, 2, 4); break;
+  }
+#undef WG_BY_C
+#undef WG_L16
+#undef WG_L32
+}
+
+}  // namespace ore

@@ -21,6 +21,7 @@ struct ore_ctx {
   // which has a 4 KiB lead): the streaming conv may read a few bytes before an input inside it
   const char* mapped_lo = nullptr;
   const char* mapped_hi = nullptr;
+  int conv_algo = 0;  // ore_ctx_set_conv_algo (per-op ore_conv2d_f32 only)
 };
 
 namespace ore {
@@ -87,7 +88,7 @@ ore_status resolve_window(ore_ctx* ctx, int auto_pad, const int64_t* pads, int n
 // ---------------------------------------------------------------- launches over resolved geometry
 // Kernel plan of a conv (or MatMul as a 1x1 conv) over resolved geometry.
 ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
-                   const Window& win, bool f16 = false, int xmode = 0, bool x3 = false);
+                   const Window& win, bool f16 = false, int xmode = 0, bool x3 = false, bool wino = false);
 // wp: weights packed by launch_pack for plan `pln`
 // ktab: gather table (launch_ktab) for non-1x1 geometry on the gather kernel
 ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,

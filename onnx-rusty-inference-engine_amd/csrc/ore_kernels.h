@@ -57,6 +57,7 @@ struct ConvPlan {
   size_t lds;          // dynamic LDS bytes of the window kernel
   int epv = 0;         // pooled-epilogue steps: ConvParams::ep_variant (ore_model_autotune)
   int x3 = 0;          // 1: conv_x3_kernel (f32 on the BF16 matrix cores, ore_conv_x3.hip); cfg = X3_TILE_BASE + tile
+  int wino = 0;        // 1: conv_wino_kernel (Winograd F(2x2, 3x3), ore_conv_wino.hip); cfg = WINO_TILE_BASE + tile
 };
 
 struct PoolParams {
@@ -119,7 +120,7 @@ int conv_packed_kp(int K);  // padded K of the packed weights
 void launch_pack_weights(const float* w, bool kmajor_src, int M, int K, int Mp, float* wp, hipStream_t s);
 void launch_ktab(int2* ktab, int K, int kh, int kw, int x_ps, int W, hipStream_t s);
 ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
-                   bool is1x1, bool f16 = false, int xmode = 0, bool x3 = false);
+                   bool is1x1, bool f16 = false, int xmode = 0, bool x3 = false, bool wino = false);
 // f16 conv operand modes (ConvPlan::xmode), chosen by the input's layout:
 enum {
   F16_X_NCHW32 = 0,     // f32 NCHW model input, per-element gather, k order (c, r, s) (the reference's)
@@ -206,6 +207,17 @@ void launch_pack_x3(const float* w, bool kmajor_src, int M, int K, int Mp, void*
 void launch_pack_x3w(const float* w, int M, int C, int kh, int kw, int Mp, int G, int nsteps, int nchunks, void* wq,
                      hipStream_t s);
 void launch_conv_x3(const ConvParams& p, int tile, hipStream_t s);
+// 3x3 / stride-1 / pad-1 f32 conv by Winograd F(2x2, 3x3) on the f32 MFMA (ore_conv_wino.hip).  Tiles
+// WINO_TILE_BASE + 0..3 = 32 ch x 32 tiles (32x32x2 MFMA, ring 4 / 2), 32 x 16, 16 x 32 (16x16x4);
+// results do not depend on the tile (not bit-identical to the direct kernels).  Weights packed by
+// launch_pack_wino: U = G g G^T as [C][4][Mp][4] f32 (channel, position quad, m, position) (Mp = wino_packed_mp(M)).
+constexpr int WINO_TILE_BASE = X3_TILE_BASE + X3_TILES;
+constexpr int WINO_TILES_N = 4;
+bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo);
+bool conv_wino_eligible(const ConvParams& p, int tile);
+int wino_packed_mp(int M);
+void launch_pack_wino(const float* w, int M, int C, int Mp, float* u, hipStream_t s);
+void launch_conv_wino(const ConvParams& p, int tile, hipStream_t s);
 void launch_maxpool(const PoolParams& p, hipStream_t s);
 void launch_relu(const float* x, float* y, long long n, hipStream_t s);
 void launch_relu_f16(const void* x, void* y, long long n, hipStream_t s);

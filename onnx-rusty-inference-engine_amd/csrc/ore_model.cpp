@@ -102,6 +102,12 @@ struct Step {
   ConvPlan plan_x3{};
   float* wp_x3 = nullptr;
   const int2* ktab_x3 = nullptr;
+  // f32 models (not x3, not ORE_LOAD_NO_WINOGRAD): the Winograd F(2x2, 3x3) plan of a 3x3 / stride-1 /
+  // pad-1 conv (ore_conv_wino.hip), packed next to the direct one; plan() switches a conv that no
+  // direct-kernel fusion takes to it
+  bool has_wino = false;
+  ConvPlan plan_wino{};
+  float* wp_wino = nullptr;
   void* xcvt = nullptr;        // f16 F16_X_NHWC_PAIR: the f32 NCHW input converted to NHWC4 f16 (max_batch)
   int64_t axis = 1;
   double flops_per_img = 0, bytes_per_img = 0, bytes_fixed = 0;
@@ -116,6 +122,7 @@ struct ore_model {
   bool f16 = false;              // ORE_LOAD_F16: f16 conv/pool activations, f32 accumulation
   bool x3 = false;               // ORE_LOAD_X3: f32 convs / MatMuls on the BF16 matrix cores (ore_conv_x3.hip)
   bool x3_all = false;           // ORE_X3_ALL=1 (tests, experiments): every conv on x3, no f32-MFMA fusions
+  bool wino = false;             // f32 model without ORE_LOAD_NO_WINOGRAD: Winograd plans for 3x3 s1 p1 convs
   std::vector<Value> values;
   size_t n_base_values = 0;      // values of the graph; plan() appends views after them (pooled slices)
   std::map<std::string, int> by_name;
@@ -750,6 +757,15 @@ ore_status plan(ore_model* m) {
         st.wp = st.wp_x3;
         st.ktab = st.ktab_x3;
       }
+  // (1g) f32 models: every 3x3 / stride-1 / pad-1 conv not taken by a direct-kernel fusion above runs
+  // Winograd F(2x2, 3x3) (a load-time rule: the algorithm never depends on timing)
+  if (m->wino)
+    for (auto& st : m->steps)
+      if (st.kind == S_CONV && st.has_wino && !st.pool && !st.epool) {
+        st.plan = st.plan_wino;
+        st.wp = st.wp_wino;
+        st.ktab = nullptr;
+      }
   // (2) Dropout / activation Reshape as aliases
   if (m->fusion & ORE_FUSE_ALIAS) {
     for (auto& s : m->steps) {
@@ -1122,7 +1138,7 @@ ore_status ore_model_parse(const void* bytes, size_t len) {
 ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_t max_batch, int32_t flags,
                              ore_model** out) {
   if (!ctx || !bytes || !out || max_batch <= 0) return set_error(ctx, ORE_ERR_INVALID, "invalid argument");
-  if (flags & ~(ORE_LOAD_F16 | ORE_LOAD_X3)) return set_error(ctx, ORE_ERR_INVALID, "unknown load flags 0x%x", unsigned(flags));
+  if (flags & ~(ORE_LOAD_F16 | ORE_LOAD_X3 | ORE_LOAD_NO_WINOGRAD)) return set_error(ctx, ORE_ERR_INVALID, "unknown load flags 0x%x", unsigned(flags));
   if ((flags & ORE_LOAD_F16) && (flags & ORE_LOAD_X3))
     return set_error(ctx, ORE_ERR_INVALID, "ORE_LOAD_F16 and ORE_LOAD_X3 are exclusive");
   ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
@@ -1135,6 +1151,9 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
   m->f16 = (flags & ORE_LOAD_F16) != 0;
   m->x3 = (flags & ORE_LOAD_X3) != 0;
   m->x3_all = m->x3 && getenv("ORE_X3_ALL") && atoi(getenv("ORE_X3_ALL")) != 0;
+  // ORE_NO_WINOGRAD=1 (tests of the direct-kernel fusions, experiments) acts as ORE_LOAD_NO_WINOGRAD
+  m->wino = !m->f16 && !m->x3 && (flags & ORE_LOAD_NO_WINOGRAD) == 0 &&
+            !(getenv("ORE_NO_WINOGRAD") && atoi(getenv("ORE_NO_WINOGRAD")) != 0);
   auto fail = [&](ore_status st) {
     ore_model_destroy(m);
     return st;
@@ -1221,6 +1240,11 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
                                      : conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win, false, 0, true);
         total_packed += (packed_bytes(s.plan_x3) + 255) / 256 * 256;
       }
+      if (m->wino && s.kind == S_CONV) {
+        s.plan_wino = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, false, 0, false, true);
+        s.has_wino = s.plan_wino.wino != 0;
+        if (s.has_wino) total_packed += (conv_packed_bytes(s.plan_wino) + 255) / 256 * 256;
+      }
     }
     if (total_packed) {
       if (hipMalloc(reinterpret_cast<void**>(&m->packed), total_packed) != hipSuccess)
@@ -1241,6 +1265,12 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
                       ctx->stream);
           s.ktab_x3 = reinterpret_cast<int2*>(bx + conv_packed_bytes(s.plan_x3));
           poff += (packed_bytes(s.plan_x3) + 255) / 256 * 256;
+        }
+        if (s.has_wino) {
+          s.wp_wino = reinterpret_cast<float*>(reinterpret_cast<char*>(m->packed) + poff);
+          launch_pack(m->values[s.in1].cptr, false, int(s.M), int(s.C), int(s.kh), int(s.kw), s.plan_wino, s.wp_wino,
+                      ctx->stream);
+          poff += (conv_packed_bytes(s.plan_wino) + 255) / 256 * 256;
         }
       }
       if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
@@ -1494,10 +1524,13 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
     if (s.plan.x3) {  // the x3 tiles of the plan's kernel family only (its packed layout)
       cands.clear();
       for (int c = 0; c < 4; ++c) cands.push_back(X3_TILE_BASE + c + (s.plan.x3 == 2 ? 4 : 0));
+    } else if (s.plan.wino) {  // the Winograd tiles (its packed layout)
+      cands.clear();
+      for (int c = 0; c < WINO_TILES_N; ++c) cands.push_back(WINO_TILE_BASE + c);
     } else if (!s.plan.f16 && !(ews && !atoi(ews))) cands.insert(cands.end(), {8, 9, 10, 11});
     // the LDS-free streaming kernel (tiles 12-20) where the geometry allows it (launch_conv falls
     // back to tile 0 elsewhere, and such candidates are skipped below)
-    if (!s.plan.f16 && !s.plan.x3 && s.kind == S_CONV && !s.pool)
+    if (!s.plan.f16 && !s.plan.x3 && !s.plan.wino && s.kind == S_CONV && !s.pool)
       for (int c = CONV_TILE_STREAM; c < CONV_TILES_F32; ++c) cands.push_back(c);
     for (size_t ci = 0; ci < cands.size() && !st; ++ci) {
       const int c = cands[ci];
@@ -1520,6 +1553,7 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
     s.plan.cfg = best;
     // steps are a per-plan copy of base_steps
     if (s.plan.x3) m->base_steps[m->exec_steps[k]].plan_x3.cfg = best;
+    else if (s.plan.wino) m->base_steps[m->exec_steps[k]].plan_wino.cfg = best;
     else m->base_steps[m->exec_steps[k]].plan.cfg = best;
     if (!st) st = launch_step(m, s, n);                // leave the real output for the next step
   }

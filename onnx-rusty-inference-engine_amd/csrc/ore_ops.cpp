@@ -99,9 +99,9 @@ static bool contiguous(const ore_tensor* t) {
 static bool fits_i32(int64_t v) { return v >= 0 && v < (int64_t(1) << 31); }
 
 ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
-                   const Window& win, bool f16, int xmode, bool x3) {
+                   const Window& win, bool f16, int xmode, bool x3, bool wino) {
   return plan_conv(int(M), int(C), int(H), int(W), int(kh), int(kw), int(sh), int(sw), int(win.pt), int(win.pl),
-                   int(win.Ho), int(win.Wo), kh == 1 && kw == 1, f16, xmode, x3);
+                   int(win.Ho), int(win.Wo), kh == 1 && kw == 1, f16, xmode, x3, wino);
 }
 
 size_t packed_bytes(const ConvPlan& pln) {
@@ -181,14 +181,15 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
   if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(int64_t(pln.krows) * pln.Mp) ||
       !fits_i32(p.Ntot + 256) || (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))
     return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
-  if (!pln.window && !p.is1x1 && !ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
-  if (pln.x3) {
-    // the x3 kernel addresses x through a buffer resource (32-bit byte offsets): a batch whose input
-    // extent does not fit runs in image chunks that do
-    if (!p.is1x1 && p.kh * p.kw > 64) return set_error(ctx, ORE_ERR_UNSUPPORTED, "x3 conv: more than 64 taps");
+  if (!pln.window && !pln.wino && !p.is1x1 && !ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
+  if (pln.x3 || pln.wino) {
+    // the x3 / Winograd kernels address x through a buffer resource (32-bit byte offsets): a batch
+    // whose input extent does not fit runs in image chunks that do
+    if (pln.x3 && !p.is1x1 && p.kh * p.kw > 64) return set_error(ctx, ORE_ERR_UNSUPPORTED, "x3 conv: more than 64 taps");
+    const int64_t lim = pln.wino ? (int64_t(1) << 31) - (int64_t(1) << 21) : int64_t(1) << 31;
     int64_t nb = N;
-    while (nb > 1 && ((nb - 1) * x_nstride + C * x_ps) * 4 >= (int64_t(1) << 31)) nb = (nb + 1) / 2;
-    if ((C * x_ps) * 4 >= (int64_t(1) << 31)) return set_error(ctx, ORE_ERR_UNSUPPORTED, "x3 conv: one image exceeds 2 GiB");
+    while (nb > 1 && ((nb - 1) * x_nstride + C * x_ps) * 4 >= lim) nb = (nb + 1) / 2;
+    if ((C * x_ps) * 4 >= lim) return set_error(ctx, ORE_ERR_UNSUPPORTED, "x3 / Winograd conv: one image exceeds 2 GiB");
     for (int64_t i0 = 0; i0 < N; i0 += nb) {
       const int64_t nc = std::min(nb, N - i0);
       ConvParams q = p;
@@ -486,6 +487,14 @@ ore_status ore_ctx_destroy(ore_ctx* ctx) {
   return ORE_OK;
 }
 
+ore_status ore_ctx_set_conv_algo(ore_ctx* ctx, int32_t algo) {
+  if (!ctx) return set_error(nullptr, ORE_ERR_INVALID, "null context");
+  if (algo != ORE_CONV_ALGO_DIRECT && algo != ORE_CONV_ALGO_WINOGRAD)
+    return set_error(ctx, ORE_ERR_INVALID, "unknown conv algorithm %d", int(algo));
+  ctx->conv_algo = algo;
+  return ORE_OK;
+}
+
 ore_status ore_ctx_set_stream(ore_ctx* ctx, void* s) {
   if (!ctx) return set_error(nullptr, ORE_ERR_INVALID, "null ctx");
   ctx->stream = reinterpret_cast<hipStream_t>(s);
@@ -582,7 +591,7 @@ ore_status ore_conv2d_f32(ore_ctx* ctx, const ore_tensor* x, const ore_tensor* w
   if (x->dims[0] == 0) return ORE_OK;
   const int2* kt = nullptr;
   const ConvPlan pln = conv_plan(w->dims[0], w->dims[1], x->dims[2], x->dims[3], w->dims[2], w->dims[3], a->strides[0],
-                                 a->strides[1], win);
+                                 a->strides[1], win, false, 0, false, ctx->conv_algo == ORE_CONV_ALGO_WINOGRAD);
   float* wp = pack_to_scratch(ctx, pln, w->data, false, w->dims[0], w->dims[1], w->dims[2], w->dims[3], x->dims[2],
                               x->dims[3], &kt);
   if (!wp) return ORE_ERR_OOM;

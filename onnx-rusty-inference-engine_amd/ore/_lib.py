@@ -21,12 +21,14 @@ FUSE_FIRE = 64
 FUSE_CONCAT_POOL = 128
 LOAD_F16 = 1  # ore_model_load_ex flag: the fp16 variant
 LOAD_X3 = 2   # ore_model_load_ex flag: f32 convs on the BF16 matrix cores (exact 3-way bf16 split)
+LOAD_NO_WINOGRAD = 4  # ore_model_load_ex flag: 3x3 stride-1 convs on the direct kernels only
+CONV_ALGO_DIRECT, CONV_ALGO_WINOGRAD = 0, 1  # ore_ctx_set_conv_algo (per-op ore_conv2d_f32)
 PAD = {"NOTSET": 0, "NOT_SET": 0, "SAME_UPPER": 1, "SAME_LOWER": 2, "VALID": 3}
 
 # every symbol include/ore.h declares (checked by tests/test_abi.py on CPU)
 EXPORTED = [
     "ore_abi_version", "ore_ctx_create", "ore_ctx_destroy", "ore_ctx_set_stream", "ore_ctx_get_stream",
-    "ore_sync", "ore_last_error", "ore_malloc", "ore_free", "ore_upload", "ore_download",
+    "ore_ctx_set_conv_algo", "ore_sync", "ore_last_error", "ore_malloc", "ore_free", "ore_upload", "ore_download",
     "ore_conv_out_shape", "ore_pool_out_shape", "ore_conv2d_f32", "ore_maxpool2d_f32", "ore_relu_f32",
     "ore_add_f32", "ore_softmax_f32", "ore_matmul_f32", "ore_gap_f32", "ore_concat_f32", "ore_dropout_f32",
     "ore_reshape", "ore_model_parse", "ore_model_load", "ore_model_load_ex", "ore_model_destroy", "ore_model_set_fusion", "ore_model_input_dims",
@@ -79,6 +81,7 @@ def load():
         "ore_ctx_destroy": (i32, [vp]),
         "ore_ctx_set_stream": (i32, [vp, vp]),
         "ore_ctx_get_stream": (vp, [vp]),
+        "ore_ctx_set_conv_algo": (i32, [vp, i32]),
         "ore_sync": (i32, [vp]),
         "ore_last_error": (cs, [vp]),
         "ore_malloc": (i32, [vp, ctypes.c_size_t, ctypes.POINTER(vp)]),

@@ -16,7 +16,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import LOAD_F16, LOAD_X3, ConvAttrs, OreError, PoolAttrs, Tensor, check, load
+from ._lib import LOAD_F16, LOAD_NO_WINOGRAD, LOAD_X3, ConvAttrs, OreError, PoolAttrs, Tensor, check, load
 
 __all__ = ["Context", "Model", "OreError", "convolution", "max_pool", "relu", "add", "softmax", "mul",
            "global_average_pool", "concatenation", "drop_out", "reshape", "inference", "conv_out_shape",
@@ -43,6 +43,11 @@ class Context:
 
     def set_stream(self, stream_ptr: Optional[int]):
         check(load().ore_ctx_set_stream(self.h, ctypes.c_void_p(stream_ptr or None)), self.h)
+
+    def set_conv_algo(self, algo: int):
+        """ore_ctx_set_conv_algo: the per-op convolution()'s algorithm (CONV_ALGO_DIRECT, the
+        reference's k order; CONV_ALGO_WINOGRAD, F(2x2, 3x3) on eligible 3x3 stride-1 convs)."""
+        check(load().ore_ctx_set_conv_algo(self.h, int(algo)), self.h)
 
     @property
     def stream(self) -> int:
@@ -217,16 +222,21 @@ def reshape(x, shape: Sequence[int]):
 class Model:
     """ore_model: the device-resident walker over one ONNX graph."""
 
-    def __init__(self, ctx: Context, onnx_bytes: bytes, max_batch: int, precision: str = "f32"):
+    def __init__(self, ctx: Context, onnx_bytes: bytes, max_batch: int, precision: str = "f32",
+                 winograd: bool = True):
         """precision "f32": convs on the f32-input MFMA; "f32x3": the same f32 model with its convs /
         MatMuls on the BF16 matrix cores through an exact three-way bf16 split (ORE_LOAD_X3,
-        include/ore.h); "f16": the fp16 variant (ORE_LOAD_F16).  Input / output stay f32."""
+        include/ore.h); "f16": the fp16 variant (ORE_LOAD_F16).  Input / output stay f32.
+        winograd (f32 only): 3x3 stride-1 pad-1 convs that no direct-kernel fusion takes run
+        Winograd F(2x2, 3x3) in f32; False = ORE_LOAD_NO_WINOGRAD (direct kernels only)."""
         if precision not in ("f32", "f32x3", "f16"):
             raise OreError(1, f"precision must be 'f32', 'f32x3' or 'f16', not {precision!r}")
         self.ctx = ctx
         self.precision = precision
         h = ctypes.c_void_p()
         flags = {"f32": 0, "f32x3": LOAD_X3, "f16": LOAD_F16}[precision]
+        if not winograd:
+            flags |= LOAD_NO_WINOGRAD
         check(load().ore_model_load_ex(ctx.h, onnx_bytes, len(onnx_bytes), int(max_batch), flags, ctypes.byref(h)),
               ctx.h)
         self.h = h
@@ -296,7 +306,8 @@ class Model:
                   "epool patch", "epool walk48", "epool walk96", "epool walk64",
                   "epool walk64 b3", "epool walk96 b2",
                   "x3 128x128", "x3 64x256", "x3 96x128", "x3 64x128",
-                  "x3w 128x128", "x3w 64x128", "x3w 128x64", "x3w 64x64"]
+                  "x3w 128x128", "x3w 64x128", "x3w 128x64", "x3w 64x64",
+                  "wino 32x32 d4", "wino 32x32 d2", "wino16 32x16", "wino16 16x32"]
 
     def tiles(self):
         """Block tile per exec step (-1 for non-conv steps); names in TILE_NAMES."""

@@ -27,6 +27,14 @@ def _np(t):
     return t.cpu().numpy()
 
 
+@pytest.fixture(autouse=True)
+def direct_kernels(monkeypatch):
+    """These tests pin the direct kernels and their fusions (bit-identical to the unfused graph);
+    the Winograd 3x3 path, on by default for f32 models, has its own parity tests
+    (tests/test_wino_gpu.py)."""
+    monkeypatch.setenv("ORE_NO_WINOGRAD", "1")
+
+
 def _mnist_bytes():
     with open(os.path.join(GOLD, "mnist-8.onnx"), "rb") as f:
         return f.read()
@@ -36,7 +44,7 @@ def _mnist_bytes():
 def squeeze224(gpu_ctx):
     import ore
     from ore import squeezenet
-    m = ore.Model(gpu_ctx, squeezenet.build(224), max_batch=256)
+    m = ore.Model(gpu_ctx, squeezenet.build(224), max_batch=256, winograd=False)
     yield m
     m.close()
 

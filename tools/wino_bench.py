@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Winograd F(2x2, 3x3) vs the direct kernels on SqueezeNet's expand3x3 geometries at batch 256:
+single Conv + Relu graphs through the walker, each tile timed (HIP events), direct = the autotuned
+direct kernel.  usage: python tools/wino_bench.py [--batch 256] [--reps 20]"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "onnx-rusty-inference-engine_amd"))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+from bench_ops import conv_graph  # noqa: E402
+
+E3 = [("f2.e3", 16, 54, 64), ("f4.e3", 32, 54, 128), ("f5.e3", 32, 27, 128), ("f6.e3", 48, 27, 192),
+      ("f8.e3", 64, 27, 256), ("f9.e3", 64, 13, 256)]
+
+
+def timed(ctx, mb, x, reps, winograd, tune=True):
+    import ore
+    import torch
+    m = ore.Model(ctx, mb, max_batch=x.shape[0], winograd=winograd)
+    out = torch.empty((x.shape[0], m.output_elems), device="cuda")
+    if tune:
+        m.autotune(x, out)
+    for _ in range(3):
+        m.run_into(x, out)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        m.run_into(x, out)
+    e1.record()
+    torch.cuda.synchronize()
+    tile = ore.Model.TILE_NAMES[m.tiles()[0]]
+    m.close()
+    return e0.elapsed_time(e1) / reps * 1000.0, tile
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--tiles", default="0,1,2,3")
+    ap.add_argument("--no-direct", action="store_true")
+    ap.add_argument("--only", default="", help="comma-separated layer names")
+    a = ap.parse_args()
+    import torch
+    import ore
+    ctx = ore.Context(0)
+    B = a.batch
+    tag = os.path.basename(os.environ.get("ORE_LIB", "libore.so"))
+    for name, cin, h, cout in E3:
+        if a.only and name not in a.only.split(","):
+            continue
+        x = torch.randn((B, cin, h, h), device="cuda")
+        mb = conv_graph(cin, h, cout, 3, 1, 1)
+        fl = 2.0 * B * cout * h * h * cin * 9
+        line = f"{tag} {name:6s}"
+        if not a.no_direct:
+            us_d, tile_d = timed(ctx, mb, x, a.reps, False)
+            line += f" direct {us_d:8.1f} us {fl / us_d / 1e6:6.1f} TF/s ({tile_d})"
+        for t in [int(v) for v in a.tiles.split(",")]:
+            os.environ["ORE_WINO_TILE"] = str(t)
+            us, tile = timed(ctx, mb, x, a.reps, True, tune=False)
+            line += f" | {tile} {us:7.1f} us {fl / us / 1e6:6.1f}"
+        os.environ.pop("ORE_WINO_TILE", None)
+        print(line, flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
