@@ -30,12 +30,16 @@
 // The 16x16x4 kernel (16 MF channels x 16 NT tiles per wave) is the same scheme at other tile shapes.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
+
 #include "ore_kernels.h"
 
 namespace ore {
 
 typedef float wg_floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16_t __attribute__((ext_vector_type(16)));
+typedef int int4d_t __attribute__((ext_vector_type(4)));
 
 // U[((c * 4 + xi / 4) * Mp + m) * 4 + xi % 4] = (G g_mc G^T)[xi / 4][xi % 4] (f64, rounded once): for a
 // fixed (channel, position quad) the channels' 16-B quads are contiguous, so the A loads of a wave
@@ -289,9 +293,14 @@ __global__ __launch_bounds__(256, 1) void conv_wino32_kernel(ConvParams p) {
     wg_window(rb[SB], w, v_);                                                                          \
     WG_MFMAS(SA, v_)                                                                                   \
   }
+#ifndef ORE_EXP_WG_NOMFMA
 #define WG_MFMAS(SA, V)                                                                                \
     _Pragma("unroll") for (int xi = 0; xi < 16; ++xi)                                                  \
         acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[SA][xi >> 2][xi & 3], V[xi], acc[xi], 0, 0, 0);
+#else  // timing experiment only: operands consumed by one VALU op each instead of the MFMAs
+#define WG_MFMAS(SA, V)                                                                                \
+    _Pragma("unroll") for (int xi = 0; xi < 16; ++xi) acc[xi][xi] += ra[SA][xi >> 2][xi & 3] * V[xi];
+#endif
 #define WG_WINDOWS(SB, V) wg_window(rb[SB], w, V);
 #define WG_COPYV(D_, S_) _Pragma("unroll") for (int i = 0; i < 16; ++i) D_[i] = S_[i];
 #define WG_NMFMA 16
@@ -414,11 +423,203 @@ __global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// LDS-staged Winograd kernel (tile 4).  The register-streaming kernels above move 16 window floats and
+// 16 U floats per (channel, tile) and lane through the vector-memory path, which caps them near 15 B
+// per clock per CU of VGPR-bound loads (profiles/r02b_pmc_wino32_vs_gemm_f8e3.txt: TD 79 % busy at
+// 41 % MFMA).  Here
+//   * U of the block's 32 output channels (C x 16 x 32 floats, 32-128 KB) is loaded into LDS once
+//     and stays there: blocks are persistent over a range of tile groups of one 32-channel tile;
+//   * each wave stages, per k-step, the input rows its tile group reads (2 channels x (2R + 2) rows,
+//     zero-padded by one column each side) into its own LDS ring by LDS-DMA: each input element
+//     crosses the memory path once per wave instead of ~4 times, and rows / columns outside the
+//     image arrive as zeros (out-of-range buffer offsets), so the windows need no masks;
+//   * windows (16 x ds_read_b32) and U (4 x ds_read_b128) come from LDS, one k-step ahead of the MFMAs.
+// A tile group is R whole tile rows of one image (R = floor(32 / TW)); lane l & 31 is tile
+// (l & 31) / TW, (l & 31) % TW of the group (lanes past the group idle), l >> 5 the channel.
+struct WlGeom {
+  int TW, TH, R, Wp;  // tiles per row / column, tile rows per group, padded staging row width
+  int gpi, G;         // groups per image, groups in the batch
+  int bpm;            // blocks in the grid (split evenly over the 32-channel tiles)
+  int ubytes, ringb;  // LDS bytes of U and of one wave's ring
+};
+
+__device__ __forceinline__ void wl_dma(int4d_t rsrc, unsigned lds_addr, int voffset, int soffset) {
+  int m0save;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dword %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(m0save)
+      : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voffset), "s"(rsrc), "s"(soffset)
+      : "memory");
+}
+
+#define WL_VMCNT(n) (((n) & 15) | (((n) >> 4) << 14) | (7 << 4) | (15 << 8))
+
+// NKS: k-steps (C / 2), NI: 64-float DMA pieces per staged channel, DR: ring slots (k-steps ahead,
+// at most 4: the counted waits below assume at most 2 later steps in flight)
+template <int NKS, int NI, int DR>
+__global__ __launch_bounds__(256, 1) void conv_winol_kernel(ConvParams p, WlGeom g) {
+  extern __shared__ __attribute__((aligned(16))) float wl_lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // block b -> (32-channel tile mt, its bi-th of bpm(mt) group ranges): the m-tiles split the grid
+  // evenly (g.bpm = blocks in the grid)
+  const int b = blockIdx.x;
+  const int mt = (int)(((long long)b * p.mtiles) / g.bpm);
+  const int b0 = (int)(((long long)mt * g.bpm + p.mtiles - 1) / p.mtiles);
+  const int b1 = (int)(((long long)(mt + 1) * g.bpm + p.mtiles - 1) / p.mtiles);
+  const int bi = b - b0, nbm = b1 - b0;
+  const int m0 = mt * 32;
+  constexpr int C = 2 * NKS;
+  // ---- U of channels m0 .. m0 + 31 into LDS: [c][q][32][4] floats (from the global [c][q][Mp][4])
+  {
+    const wg_floatx4* __restrict__ ug = reinterpret_cast<const wg_floatx4*>(p.wp);
+    wg_floatx4* ul = reinterpret_cast<wg_floatx4*>(wl_lds);
+    for (int i = tid; i < C * 4 * 32; i += 256) {
+      const int m = i & 31, cq = i >> 5;
+      ul[i] = ug[(long long)cq * p.Mp + m0 + m];
+    }
+  }
+  __syncthreads();  // the only barrier: from here each wave runs on its own
+  const int g0 = (int)((long long)bi * g.G / nbm), g1 = (int)((long long)(bi + 1) * g.G / nbm);
+  const int ringf = (g.ubytes + wave * g.ringb) / 4;  // this wave's ring (float index)
+  const unsigned ring = (unsigned)(size_t)(__attribute__((address_space(3))) float*)wl_lds + ringf * 4;  // LDS address
+  constexpr int CHUNK = NI * 64 + 1;  // floats per staged channel (+1: the two channels on other banks)
+  const int lr = lane >> 5, lc = lane & 31;
+  const unsigned long long xb = reinterpret_cast<unsigned long long>(p.x);
+  const int4d_t xdesc = {(int)(unsigned)xb, (int)((xb >> 32) & 0xffff), (int)p.x_bytes, 0x00020000};
+  const int cstep = p.x_ps * 4;  // bytes between input channel planes
+  const wg_floatx4* ul = reinterpret_cast<const wg_floatx4*>(wl_lds);
+
+  for (int gi = g0 + wave; gi < g1; gi += 4) {
+    const int img = gi / g.gpi, ty0 = (gi - img * g.gpi) * g.R;
+    // opaque per group: the per-step DMA offsets below are computed at their use, not hoisted out of
+    // the group loop into ~100 live SGPRs
+    int cst = cstep;
+    unsigned rg = ring;
+    asm volatile("" : "+s"(cst), "+s"(rg));
+    // this lane's DMA sources: staged element e = i 64 + lane of a channel = padded row e / Wp,
+    // column e % Wp (column 0 and W + 1 .. Wp - 1 are padding) -> input row 2 ty0 - 1 + row
+    int voff[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int e = i * 64 + lane;
+      const int rr = e / g.Wp, cc = e - rr * g.Wp;
+      const int row = 2 * ty0 - 1 + rr, col = cc - 1;
+      voff[i] = (rr < 2 * g.R + 2 && (unsigned)row < (unsigned)p.H && (unsigned)col < (unsigned)p.W)
+                    ? (int)((img * p.x_nstride + (long long)row * p.W + col) * 4)
+                    : WG_OOB;
+    }
+    // this lane's tile and its window's base in a staged channel (floats)
+    const int tyl = lc / g.TW, tx = lc - tyl * g.TW;
+    const bool tok = lc < g.R * g.TW && ty0 + tyl < g.TH;
+    const int wbase = (2 * tyl) * g.Wp + 2 * tx + lr * CHUNK;
+    const float* rowp[4];  // the window's rows in ring slot 0 (other slots: + a constant offset)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rowp[r] = wl_lds + ringf + wbase + r * g.Wp;
+    WgTile w;
+    w.tok = tok;
+    w.ybase = img * (int)p.y_nstride + (2 * (ty0 + tyl)) * p.W + 2 * tx;
+    w.c1ok = 2 * tx + 1 < p.W;
+    w.r1ok = 2 * (ty0 + tyl) + 1 < p.H;
+
+#define WL_STAGE(SLOT, S)                                                                              \
+    _Pragma("unroll") for (int ch = 0; ch < 2; ++ch)                                                   \
+    _Pragma("unroll") for (int i = 0; i < NI; ++i)                                                     \
+      wl_dma(xdesc, rg + (((SLOT) * 2 + ch) * CHUNK + i * 64) * 4, voff[i], (2 * (S) + ch) * cst);
+#define WL_READ(SLOT, S, RA, V)                                                                        \
+    {                                                                                                  \
+      float d_[4][4];                                                                                  \
+      _Pragma("unroll") for (int r = 0; r < 4; ++r)                                                    \
+      _Pragma("unroll") for (int j = 0; j < 4; ++j) d_[r][j] = rowp[r][(SLOT) * 2 * CHUNK + j];        \
+      _Pragma("unroll") for (int q = 0; q < 4; ++q) RA[q] = ul[((2 * (S) + lr) * 4 + q) * 32 + lc];    \
+      wg_input_transform(d_, V);                                                                       \
+    }
+    floatx16_t acc[16];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[xi][e] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < DR && s < NKS; ++s) { WL_STAGE(s, s) }
+    wg_floatx4 ra[2][4];
+    float v[2][16];
+    __builtin_amdgcn_s_waitcnt(WL_VMCNT(2 * NI * ((DR < NKS ? DR : NKS) - 1)));
+    WL_READ(0, 0, ra[0], v[0])
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      const int cur = s & 1, nxt = cur ^ 1;
+      __builtin_amdgcn_sched_barrier(0);  // keep each step's LDS reads in their step (register pressure)
+      if (s + 1 < NKS) {
+        // step s + 1's staged rows have landed (the DMAs of the `later` steps after it may still be in
+        // flight; every older VMEM operation, epilogue stores included, has completed)
+        const int later = (DR - 2 < NKS - 2 - s ? DR - 2 : NKS - 2 - s);
+        if (later >= 2) __builtin_amdgcn_s_waitcnt(WL_VMCNT(2 * 2 * NI));
+        else if (later == 1) __builtin_amdgcn_s_waitcnt(WL_VMCNT(2 * NI));
+        else __builtin_amdgcn_s_waitcnt(WL_VMCNT(0));
+        WL_READ((s + 1) % DR, s + 1, ra[nxt], v[nxt])
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi)
+        acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[cur][xi >> 2][xi & 3], v[cur][xi], acc[xi], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (s + DR < NKS) {
+        // slot s % DR was read (step s's window, before the previous MFMAs): refill it for step s + DR
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this lane's reads of the slot are done
+        WL_STAGE(s % DR, s + DR)
+      }
+    }
+#undef WL_STAGE
+#undef WL_READ
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int rw = (e & 3) + 8 * (e >> 2);
+      const int m = m0 + rw + 4 * lr;
+      // the two lane halves' biases by scalar loads (lgkmcnt: no wait on the stores issued before)
+      const float b0 = p.bias ? p.bias[min(m0 + rw, p.M - 1)] : 0.0f;
+      const float b1 = p.bias ? p.bias[min(m0 + rw + 4, p.M - 1)] : 0.0f;
+      if (m < p.M) {
+        float mx[16];
+#pragma unroll
+        for (int xi = 0; xi < 16; ++xi) mx[xi] = acc[xi][e];
+        wg_store(p, w, m, lr ? b1 : b0, mx);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one accumulator row at a time (register pressure)
+    }
+  }
+}
+
 // Winograd tiles (ConvPlan cfg = WINO_TILE_BASE + t): shape (32: 32x32x2, 16: 16x16x4), channels and
 // 2x2 tiles per wave, A / B ring depths of the unrolled K loop
 struct WinoTile { int shape, ch, tiles, da, db; };
 static const WinoTile WINO_TILES[WINO_TILES_N] = {{32, 32, 32, 2, 8}, {32, 32, 32, 2, 4}, {16, 32, 16, 2, 8},
-                                                  {16, 16, 32, 2, 4}};
+                                                  {16, 16, 32, 2, 4}, {0, 32, 32, 0, 4}};  // 4: conv_winol_kernel
+constexpr int WL_DR = 4;
+
+// the LDS kernel's geometry; false when the layer does not fit it
+static bool wl_geom(const ConvParams& p, WlGeom* g, int* ni, size_t* lds) {
+  if (p.C % 16 != 0 || p.C > 64 || p.C <= 0) return false;
+  g->TW = (p.W + 1) / 2;
+  g->TH = (p.H + 1) / 2;
+  if (g->TW > 32) return false;
+  g->R = std::min(32 / g->TW, g->TH);
+  g->Wp = 2 * g->TW + 2;
+  const int floats = (2 * g->R + 2) * g->Wp;
+  if (floats > 256) return false;
+  *ni = floats > 192 ? 4 : 3;
+  g->gpi = (g->TH + g->R - 1) / g->R;
+  g->G = p.N * g->gpi;
+  g->ubytes = p.C * 4 * 32 * 16;
+  g->ringb = (WL_DR * 2 * ((*ni) * 64 + 1) * 4 + 15) / 16 * 16;
+  *lds = (size_t)g->ubytes + 4 * (size_t)g->ringb;
+  return *lds <= 160 * 1024;
+}
 
 bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo) {
   return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && Ho == H && Wo == W && C % 16 == 0 && C > 0;
@@ -426,6 +627,13 @@ bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, i
 
 bool conv_wino_eligible(const ConvParams& p, int tile) {
   if (tile < 0 || tile >= WINO_TILES_N) return false;
+  if (tile == 4) {
+    WlGeom g;
+    int ni;
+    size_t lds;
+    return conv_wino_geometry(p.C, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.H, p.W, p.Ho, p.Wo) && wl_geom(p, &g, &ni, &lds) &&
+           p.x_bytes > 0 && p.x_bytes < (1LL << 31) - (1LL << 21) && p.Mp % 64 == 0;
+  }
   const WinoTile& wt = WINO_TILES[tile];
   const int nks = p.C / (wt.shape == 32 ? 2 : 4);
   return conv_wino_geometry(p.C, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.H, p.W, p.Ho, p.Wo) && nks % 2 == 0 &&
@@ -442,7 +650,57 @@ static void wg_grid(ConvParams& p, int ch, int tiles, dim3* grid) {
   *grid = dim3((unsigned)((waves + 3) / 4));
 }
 
+template <int NKS, int NI>
+static void launch_wl(const ConvParams& p, const WlGeom& g, size_t lds, dim3 grid, hipStream_t s) {
+  if (lds > 64 * 1024) {  // above the default dynamic-LDS limit: raise it once per device and instantiation
+    static std::atomic<unsigned long long> raised{0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (!(raised.load(std::memory_order_acquire) & bit)) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_winol_kernel<NKS, NI, WL_DR>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      raised.fetch_or(bit, std::memory_order_acq_rel);
+    }
+  }
+  hipLaunchKernelGGL((conv_winol_kernel<NKS, NI, WL_DR>), grid, dim3(256), lds, s, p, g);
+}
+
+static void launch_winol(const ConvParams& p0, hipStream_t s) {
+  ConvParams p = p0;
+  WlGeom g;
+  int ni = 3;
+  size_t lds = 0;
+  if (!wl_geom(p, &g, &ni, &lds)) return;  // the caller checked conv_wino_eligible
+  p.mtiles = (p.M + 31) / 32;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    ncu = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) ? prop.multiProcessorCount
+                                                                                                   : 256;
+  }
+  const int bpc = lds <= 80 * 1024 ? 2 : 1;  // blocks per CU the LDS allows
+  // one round of blocks over the chip, at least 4 groups (one per wave) per block and one block per m-tile
+  g.bpm = std::max(p.mtiles, std::min(ncu * bpc, p.mtiles * ((g.G + 3) / 4)));
+  const dim3 grid((unsigned)g.bpm);
+  switch (p.C / 16 * 10 + ni) {
+    case 13: launch_wl<8, 3>(p, g, lds, grid, s); break;
+    case 14: launch_wl<8, 4>(p, g, lds, grid, s); break;
+    case 23: launch_wl<16, 3>(p, g, lds, grid, s); break;
+    case 24: launch_wl<16, 4>(p, g, lds, grid, s); break;
+    case 33: launch_wl<24, 3>(p, g, lds, grid, s); break;
+    case 34: launch_wl<24, 4>(p, g, lds, grid, s); break;
+    case 43: launch_wl<32, 3>(p, g, lds, grid, s); break;
+    default: launch_wl<32, 4>(p, g, lds, grid, s); break;
+  }
+}
+
 void launch_conv_wino(const ConvParams& p0, int tile, hipStream_t s) {
+  if (tile == 4) {
+    launch_winol(p0, s);
+    return;
+  }
   ConvParams p = p0;
   const WinoTile& wt = WINO_TILES[tile < 0 || tile >= WINO_TILES_N ? 0 : tile];
   dim3 grid;

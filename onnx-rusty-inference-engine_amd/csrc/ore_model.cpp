@@ -1524,9 +1524,10 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
     if (s.plan.x3) {  // the x3 tiles of the plan's kernel family only (its packed layout)
       cands.clear();
       for (int c = 0; c < 4; ++c) cands.push_back(X3_TILE_BASE + c + (s.plan.x3 == 2 ? 4 : 0));
-    } else if (s.plan.wino) {  // the Winograd tiles (its packed layout)
+    } else if (s.plan.wino) {  // the Winograd tiles (its packed layout); tile 4 (LDS-staged) measured
+      // slower on every SqueezeNet expand3x3 (profiles/r02c_wino_tiles.txt): forced only (ORE_WINO_TILE=4)
       cands.clear();
-      for (int c = 0; c < WINO_TILES_N; ++c) cands.push_back(WINO_TILE_BASE + c);
+      for (int c = 0; c < 4; ++c) cands.push_back(WINO_TILE_BASE + c);
     } else if (!s.plan.f16 && !(ews && !atoi(ews))) cands.insert(cands.end(), {8, 9, 10, 11});
     // the LDS-free streaming kernel (tiles 12-20) where the geometry allows it (launch_conv falls
     // back to tile 0 elsewhere, and such candidates are skipped below)

@@ -114,7 +114,8 @@ def test_wino_exact_on_small_integers(gpu_ctx):
 
 @pytest.mark.parametrize("ci", [0, 3, 4, 5, 9])
 def test_wino_tiles_bit_identical(gpu_ctx, ci, monkeypatch):
-    """Every Winograd tile (ORE_WINO_TILE=0..3) computes each output the same way: identical bits;
+    """Every Winograd tile (ORE_WINO_TILE=0..4; 4 = the LDS-staged kernel) computes each output the
+    same way: identical bits;
     the model reports the tile it ran."""
     import ore
     N, C, H, W, M = CASES[ci]
@@ -125,7 +126,7 @@ def test_wino_tiles_bit_identical(gpu_ctx, ci, monkeypatch):
     mb = _conv_model((1, C, H, W), w, b, [1] * 4, [1, 1])
     base = ore.Model.TILE_NAMES.index("wino 32x32 d4")
     outs = []
-    for t in range(4):
+    for t in range(5):
         monkeypatch.setenv("ORE_WINO_TILE", str(t))
         m = ore.Model(gpu_ctx, mb, max_batch=N)
         outs.append(_np(m.run(_t(x))))

@@ -41,7 +41,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--tiles", default="0,1,2,3")
+    ap.add_argument("--tiles", default="0,2,4")
     ap.add_argument("--no-direct", action="store_true")
     ap.add_argument("--only", default="", help="comma-separated layer names")
     a = ap.parse_args()
