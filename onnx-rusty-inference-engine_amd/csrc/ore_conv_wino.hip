@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <type_traits>
 
 #include "ore_kernels.h"
 
@@ -122,7 +123,8 @@ struct WgTile {
   bool sh1, tok, c1ok, r1ok;
 };
 
-__device__ __forceinline__ WgTile wg_tile(const ConvParams& p, int t, int csub, int T, int TW, int TPI) {
+template <class P>
+__device__ __forceinline__ WgTile wg_tile(const P& p, int t, int csub, int T, int TW, int TPI) {
   WgTile w;
   w.tok = t < T;
   if (!w.tok) t = T - 1;
@@ -421,6 +423,293 @@ __global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
         wg_store(p, w[g], m, bias[f][e], mx);
       }
     }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// The fused fire module (ore_fire.hip's fire_kernel: expand1x1 + expand3x3 + Concat + the next
+// squeeze in one launch) with the expand3x3 by Winograd F(2x2, 3x3): FireParams::wino.  A wave owns
+// 16 2x2 tiles (64 output pixels, the direct kernel's column tile); MFMA column slot lj of MFMA q is
+// pixel q (row-major in the tile) of tile lj, for e1, e3 and the squeeze alike.
+//   * e1: 64-channel chunks, the direct kernel's 1x1 K loop and row-permuted weights (launch_fire_pack)
+//     with the B operand of tile lj's 4 pixels loaded as two 8-B row pairs;
+//   * e3: 32-channel chunks on conv_wino16_kernel's scheme (MF = 2); U packed [c][q][E3][4] with the
+//     rows of each 32-channel chunk permuted (launch_fire_pack_wino) so that accumulator row 4 lk + e of
+//     fragment f is channel c0 + 16 f + 4 e + lk: after the output transform, lane group lk holds
+//     concat channel c0 + 4 t + lk at t = 4 f + e, the operand the squeeze takes at its k-step t;
+//   * squeeze: unchanged (ascending concat channels, one fmaf chain).
+// Bit-identical to the unfused graph with Winograd expand3x3 (every e3 output is the same c-ordered
+// position sums and the same transform; the row permutation only moves outputs between lanes).
+__global__ __launch_bounds__(256) void fire_wino_pack_kernel(const float* __restrict__ w, float* __restrict__ u,
+                                                             int M, int C) {
+  const long long total = (long long)C * M * 16;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long r = i >> 2;  // (c * 4 + q) * M + m'
+    const int mq = (int)(r % M);
+    const long long cq = r / M;
+    const int c = (int)(cq >> 2);
+    const int xi = (int)(((cq & 3) << 2) | (i & 3));
+    const int c0 = mq & ~31, j = mq & 31, lj = j >> 1, f = j & 1;
+    const int m = c0 + 16 * f + 4 * (lj & 3) + (lj >> 2);
+    const double G[4][3] = {{1.0, 0.0, 0.0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0.0, 0.0, 1.0}};
+    const float* g = w + ((long long)m * C + c) * 9;
+    const int a = xi >> 2, b = xi & 3;
+    double sacc = 0.0;
+    for (int pp = 0; pp < 3; ++pp)
+      for (int q = 0; q < 3; ++q) sacc += G[a][pp] * (double)g[pp * 3 + q] * G[b][q];
+    u[i] = (float)sacc;
+  }
+}
+
+void launch_fire_pack_wino(const float* w, int M, int C, float* u, hipStream_t s) {
+  long long blocks = ((long long)C * M * 16 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(fire_wino_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, w, u, M, C);
+}
+
+// MFS: 16-row fragments of the squeeze output; NKS: e3 k-steps (C / 4); DA / DB: e3 ring depths
+template <int MFS, int NKS, int DA, int DB>
+__global__ __launch_bounds__(256, 1) void fire_wino_kernel(FireParams p) {
+  const int lane = threadIdx.x & 63;
+  int gw;
+  wg_block_wave(&gw);
+  if (gw >= p.ntiles) return;  // wave-uniform; no barrier in this kernel
+  const int lk = lane >> 4, lj = lane & 15;
+  const int TW = (p.W + 1) >> 1, TPI = TW * ((p.H + 1) >> 1);
+  const int T = p.N * TPI;
+  const WgTile w = wg_tile(p, gw * 16 + lj, lk, T, TW, TPI);  // e3 window rows (channel lk of a k-step)
+  // e1 / squeeze pixels of tile lj: element offsets of its top-left pixel (input plane / output)
+  int t_ = gw * 16 + lj;
+  if (t_ >= T) t_ = T - 1;
+  const int img = t_ / TPI, rem = t_ - img * TPI, ty = rem / TW, tx = rem - ty * TW;
+  const int xpix = img * (int)p.x_nstride + (2 * ty) * p.W + 2 * tx;  // channel 0
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0,
+                                                                      (int)p.x_bytes, 0x00020000);
+  const int C = p.C;
+  const __amdgpu_buffer_rsrc_t w1r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.w1), (short)0, ((C + 31) & ~31) * p.E1 * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.w3), (short)0,
+                                                                      C * p.E3 * 16 * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.ws), (short)0, (((p.E1 + p.E3) + 31) & ~31) * p.Msp * 4, 0x00020000);
+
+  wg_floatx4 accs[MFS][4];  // squeeze: row 4 lk + e of fragment fs, pixel q of tile lj
+#pragma unroll
+  for (int fs = 0; fs < MFS; ++fs)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) accs[fs][q] = wg_floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // squeeze k-steps over T_ chunk values val[t][q] = concat channel cat0 + 4 t + lk at pixel q
+  auto squeeze = [&](auto nt_tag, const float (*val)[4], int cat0) __attribute__((always_inline)) {
+    constexpr int NTT = decltype(nt_tag)::value;
+    const int saoff = ((cat0 + lk) * p.Msp + MFS * lj) * 4;
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) {
+      float as[MFS];
+      const int so = saoff + t * 16 * p.Msp;
+      if constexpr (MFS == 4) {
+        const wg_floatx4 v = __builtin_bit_cast(wg_floatx4, __builtin_amdgcn_raw_buffer_load_b128(wsr, so, 0, 0));
+        as[0] = v[0]; as[1] = v[1]; as[2] = v[2]; as[3] = v[3];
+      } else if constexpr (MFS == 3) {
+        typedef float f3 __attribute__((ext_vector_type(3)));
+        const f3 v = __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(wsr, so, 0, 0));
+        as[0] = v[0]; as[1] = v[1]; as[2] = v[2];
+      } else if constexpr (MFS == 2) {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const f2 v = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(wsr, so, 0, 0));
+        as[0] = v[0]; as[1] = v[1];
+      } else {
+        as[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wsr, so, 0, 0));
+      }
+#pragma unroll
+      for (int fs = 0; fs < MFS; ++fs)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          accs[fs][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(as[fs], val[t][q], accs[fs][q], 0, 0, 0);
+    }
+  };
+
+  // ---- e1: 64-channel chunks (the direct fire kernel's K loop over C, 4 channels per k-step)
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  for (int c0 = 0; c0 < p.E1; c0 += 64) {
+    const int aoff = (lk * p.E1 + c0 + 4 * lj) * 4, astep = 16 * p.E1;
+    const int xo = (xpix + lk * p.x_ps) * 4, xstep = 16 * p.x_ps, xrow = p.W * 4;
+    wg_floatx4 acc[4][4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[f][q] = wg_floatx4{0.f, 0.f, 0.f, 0.f};
+    constexpr int D1 = 4;
+    wg_floatx4 ra[D1];
+    f2v rb0[D1], rb1[D1];
+#define FW_LOAD1(SLOT, S)                                                                              \
+    {                                                                                                  \
+      const int s_ = (S);                                                                              \
+      ra[SLOT] = __builtin_bit_cast(wg_floatx4, __builtin_amdgcn_raw_buffer_load_b128(w1r, aoff, s_ * astep, 0)); \
+      rb0[SLOT] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(xr, xo, s_ * xstep, 0));  \
+      rb1[SLOT] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(xr, xo + xrow, s_ * xstep, 0)); \
+    }
+#define FW_MFMA1(SLOT)                                                                                 \
+    {                                                                                                  \
+      const float bq_[4] = {rb0[SLOT][0], rb0[SLOT][1], rb1[SLOT][0], rb1[SLOT][1]};                   \
+      __builtin_amdgcn_s_setprio(1);                                                                   \
+      _Pragma("unroll") for (int f = 0; f < 4; ++f)                                                    \
+      _Pragma("unroll") for (int q = 0; q < 4; ++q)                                                    \
+        acc[f][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], bq_[q], acc[f][q], 0, 0, 0);     \
+      __builtin_amdgcn_s_setprio(0);                                                                   \
+    }
+    constexpr int nks1 = NKS;  // C / 4 k-steps (host: NKS % D1 == 0)
+#pragma unroll
+    for (int d = 0; d < D1; ++d) FW_LOAD1(d, d);
+#pragma unroll
+    for (int s0 = 0; s0 < nks1 - D1; s0 += D1) {
+#pragma unroll
+      for (int d = 0; d < D1; ++d) {
+        FW_MFMA1(d);
+        __builtin_amdgcn_sched_barrier(0);
+        FW_LOAD1(d, s0 + D1 + d);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D1; ++d) FW_MFMA1(d);
+#undef FW_LOAD1
+#undef FW_MFMA1
+    // bias + Relu: accumulator row 4 lk + e of fragment f is channel c0 + 16 f + 4 e + lk (t = 4 f + e)
+    float val[16][4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float b = p.b1[c0 + 16 * f + 4 * e + lk];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) val[4 * f + e][q] = fmaxf(acc[f][q][e] + b, 0.0f);
+      }
+    squeeze(std::integral_constant<int, 16>{}, val, c0);
+  }
+
+  // ---- e3: 32-channel Winograd chunks
+  for (int c0 = 0; c0 < p.E3; c0 += 32) {
+    const int aoff = (lk * 4 * p.E3 + c0 + 2 * lj) * 16;  // U[c = lk][quad 0][c0 + 2 lj]
+    const int aq = p.E3 * 16, astep = 4 * 4 * p.E3 * 16, xstep = 16 * p.x_ps;
+    wg_floatx4 acc[16][2][1];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+      for (int f = 0; f < 2; ++f) acc[xi][f][0] = wg_floatx4{0.f, 0.f, 0.f, 0.f};
+    wg_floatx4 ra[DA][2][4], rb[DB][1][4];
+    constexpr int MF = 2, NT = 1;
+    const WgTile* wp_ = &w;
+#define WG_LOAD_A(SLOT, S)                                                                             \
+  {                                                                                                    \
+    const int st_ = (S);                                                                               \
+    _Pragma("unroll") for (int f = 0; f < MF; ++f)                                                     \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) ra[SLOT][f][i] = __builtin_bit_cast(                 \
+        wg_floatx4, __builtin_amdgcn_raw_buffer_load_b128(ur, aoff + 16 * f + aq * i, st_ * astep, 0)); \
+  }
+#define WG_LOAD_B(SLOT, S)                                                                             \
+  {                                                                                                    \
+    const int st_ = (S);                                                                               \
+    _Pragma("unroll") for (int r = 0; r < 4; ++r) rb[SLOT][0][r] = __builtin_bit_cast(                 \
+        wg_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, wp_->roff[r], st_ * xstep, 0));          \
+  }
+#define WG_MFMA(SA, SB)                                                                                \
+  {                                                                                                    \
+    float v_[NT][16];                                                                                  \
+    WG_WINDOWS(SB, v_)                                                                                 \
+    WG_MFMAS(SA, v_)                                                                                   \
+  }
+#define WG_MFMAS(SA, V)                                                                                \
+    _Pragma("unroll") for (int xi = 0; xi < 16; ++xi)                                                  \
+    _Pragma("unroll") for (int f = 0; f < MF; ++f)                                                     \
+        acc[xi][f][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SA][f][xi >> 2][xi & 3], V[0][xi], acc[xi][f][0], 0, 0, 0);
+#define WG_WINDOWS(SB, V) wg_window(rb[SB][0], *wp_, V[0]);
+#define WG_COPYV(D_, S_) _Pragma("unroll") for (int i = 0; i < 16; ++i) D_[0][i] = S_[0][i];
+#define WG_NMFMA (16 * MF * NT)
+#define WG_VALU_PER_MFMA 2
+    float vc_[NT][16], vn_[NT][16];
+    WG_KLOOP(NKS)
+#undef WG_MFMAS
+#undef WG_WINDOWS
+#undef WG_COPYV
+#undef WG_NMFMA
+#undef WG_VALU_PER_MFMA
+#undef WG_LOAD_A
+#undef WG_LOAD_B
+#undef WG_MFMA
+    // output transform + bias + Relu: row 4 lk + e of fragment f = channel c0 + 16 f + 4 e + lk (t = 4 f + e)
+    float val[8][4];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float mx[16], o[4];
+#pragma unroll
+        for (int xi = 0; xi < 16; ++xi) mx[xi] = acc[xi][f][0][e];
+        wg_output_transform(mx, o);
+        const float b = p.b3[c0 + 16 * f + 4 * e + lk];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) val[4 * f + e][q] = fmaxf(o[q] + b, 0.0f);
+      }
+    squeeze(std::integral_constant<int, 8>{}, val, p.E1 + c0);
+  }
+
+  // S' = Relu(squeeze + bs): squeeze channel MFS (4 lk + e) + fs at pixel q of tile lj
+  if (!w.tok) return;
+  float* __restrict__ y = p.y;
+  const int ybase = img * (int)p.y_nstride + (2 * ty) * p.W + 2 * tx;
+#pragma unroll
+  for (int fs = 0; fs < MFS; ++fs)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = MFS * (4 * lk + e) + fs;
+      if (m >= p.Ms) continue;
+      const float b = p.bs[m];
+      float o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = fmaxf(accs[fs][q][e] + b, 0.0f);
+      float* yp = y + (unsigned)(ybase + m * p.y_ps);
+      yp[0] = o[0];
+      if (w.c1ok) yp[1] = o[1];
+      if (w.r1ok) {
+        yp[p.W] = o[2];
+        if (w.c1ok) yp[p.W + 1] = o[3];
+      }
+    }
+}
+
+bool fire_wino_eligible(const FireParams& p) {
+  const uintptr_t xa = reinterpret_cast<uintptr_t>(p.x);
+  return p.E1 % 64 == 0 && p.E3 % 32 == 0 && p.E1 > 0 && p.E3 > 0 && p.Ms >= 1 && p.Ms <= 64 && p.C % 16 == 0 &&
+         p.C <= 64 && p.C > 0 && (xa & 3) == 0 && p.x_bytes > 0 && p.x_bytes < (1LL << 31) - (1LL << 21) &&
+         (long long)p.C * p.E3 * 64 < (1LL << 31) && p.Msp % 4 == 0 &&
+         (long long)p.N * ((p.H + 1) / 2) * ((p.W + 1) / 2) < (1LL << 30);
+}
+
+template <int MFS, int NKS>
+static void launch_fw(const FireParams& p0, hipStream_t s) {
+  FireParams p = p0;
+  const long long T = (long long)p.N * ((p.H + 1) / 2) * ((p.W + 1) / 2);
+  p.ntiles = (int)((T + 15) / 16);
+  hipLaunchKernelGGL((fire_wino_kernel<MFS, NKS, 2, 4>), dim3((unsigned)((p.ntiles + 3) / 4)), dim3(256), 0, s, p);
+}
+
+template <int MFS>
+static void launch_fw_c(const FireParams& p, hipStream_t s) {
+  switch (p.C / 16) {
+    case 1: launch_fw<MFS, 4>(p, s); break;
+    case 2: launch_fw<MFS, 8>(p, s); break;
+    case 3: launch_fw<MFS, 12>(p, s); break;
+    default: launch_fw<MFS, 16>(p, s); break;
+  }
+}
+
+void launch_fire_wino(const FireParams& p, hipStream_t s) {
+  switch ((p.Ms + 15) / 16) {
+    case 1: launch_fw_c<1>(p, s); break;
+    case 2: launch_fw_c<2>(p, s); break;
+    case 3: launch_fw_c<3>(p, s); break;
+    default: launch_fw_c<4>(p, s); break;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------------

@@ -121,7 +121,7 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
 ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
                     int64_t x_ps, const float* w1, const float* b1, int64_t E1, const float* w3, const float* b3,
                     int64_t E3, const float* ws, int64_t Msp, const float* bs, int64_t Ms, float* y, int64_t y_nstride,
-                    int64_t y_ps);
+                    int64_t y_ps, bool wino = false);
 // pooled-epilogue tiling of a conv output (Ho x Wo) and its pool (3x3 / stride 2 only): *tr x *tc
 // tiles of 6 x 9 pooled outputs per image; returns the work factor tiles * CONV_EPOOL_BN / (Ho * Wo)
 // (the conv columns computed, recomputed overlap and padding included), 0 for other pools

@@ -107,9 +107,15 @@ struct FireParams {
   long long x_bytes;                     // x's valid extent in bytes
   int x_guard, x_lead;                   // mapped bytes before x; bytes the 3x3 taps read before it
   int ntiles;                            // filled by the launcher
+  int wino;                              // 1: e3 by Winograd (launch_fire_wino; w3 from launch_fire_pack_wino)
 };
 bool fire_eligible(const FireParams& p);
 void launch_fire(const FireParams& p, hipStream_t s);
+// the fire module with its expand3x3 by Winograd F(2x2, 3x3) (ore_conv_wino.hip): w3 packed by
+// launch_fire_pack_wino ([C][4][E3][4] f32, rows of each 32-channel chunk permuted); C <= 64, E3 % 32 == 0
+bool fire_wino_eligible(const FireParams& p);
+void launch_fire_wino(const FireParams& p, hipStream_t s);
+void launch_fire_pack_wino(const float* w, int M, int C, float* u, hipStream_t s);
 // W [M][K] -> the fire kernel's row-permuted K-major packing (M % 64 == 0)
 void launch_fire_pack(const float* w, int M, int K, float* wf, hipStream_t s);
 

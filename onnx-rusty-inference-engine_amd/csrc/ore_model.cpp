@@ -93,6 +93,7 @@ struct Step {
   const float* fire_w3 = nullptr;
   const float* fire_b1 = nullptr;
   const float* fire_b3 = nullptr;
+  bool fire_wino = false;          // the e3 by Winograd (fire_wino_kernel; fire_w3 in launch_fire_pack_wino layout)
   ConvPlan plan{};        // kernel choice and weight layout for S_CONV / S_MATMUL
   float* wp = nullptr;    // packed weights (layout per plan) for S_CONV / S_MATMUL
   const int2* ktab = nullptr;  // gather table (follows wp in the packed allocation; gather kernel only)
@@ -717,16 +718,28 @@ ore_status plan(ore_model* m) {
       if (padded_plane(e1.H * e1.W) % 4 || (m->fusion & ORE_FUSE_CONCAT) == 0) continue;  // 16-B planes (layout below)
       const Value &va = m->values[cc.in0], &vb = m->values[cc.in1], &vc = m->values[cc.out], &vs = m->values[e1.in0];
       if (va.uses != 1 || vb.uses != 1 || vc.uses != 1 || va.is_output || vb.is_output || vc.is_output || vs.es != 4) continue;
-      // the expand weights in the fire kernel's row-permuted packing (made once per model)
+      // Winograd e3 (f32 models with Winograd on; the fire_wino_kernel's limits): bit-identical to the
+      // unfused graph, whose expand3x3 runs Winograd too
+      // Off by default: measured slower than the direct fire kernel on every SqueezeNet module
+      // (fire_wino_kernel runs one wave per SIMD and is vector-memory bound on the e3 operands,
+      // DESIGN.md section 3.3); ORE_FIRE_WINO=1 turns it on (tests, experiments)
+      const char* efw = getenv("ORE_FIRE_WINO");
+      const bool fw = efw && atoi(efw) != 0 && m->wino && e3.has_wino && e1.C <= 64 && e3.M % 32 == 0;
+      // the expand weights in the fire kernel's row-permuted packing (made once per model; key -1 - idx:
+      // the Winograd e3 packing)
       bool packed_ok = true;
       for (int idx : {pa, pb}) {
-        if (m->fire_packs.count(idx)) continue;
+        const bool wpack = fw && idx == pb;
+        const int key = wpack ? -1 - idx : idx;
+        if (m->fire_packs.count(key)) continue;
         const Step& e = m->steps[idx];
         const int64_t K = e.C * e.kh * e.kw, Kp = (K + 31) / 32 * 32;
+        const size_t bytes = wpack ? size_t(e.C * e.M * 16) * 4 : size_t(Kp * e.M) * 4;
         float* buf = nullptr;
-        if (hipMalloc(reinterpret_cast<void**>(&buf), size_t(Kp * e.M) * 4) != hipSuccess) { packed_ok = false; break; }
-        launch_fire_pack(m->values[e.in1].cptr, int(e.M), int(K), buf, m->ctx->stream);
-        m->fire_packs[idx] = buf;
+        if (hipMalloc(reinterpret_cast<void**>(&buf), bytes) != hipSuccess) { packed_ok = false; break; }
+        if (wpack) launch_fire_pack_wino(m->values[e.in1].cptr, int(e.M), int(e.C), buf, m->ctx->stream);
+        else launch_fire_pack(m->values[e.in1].cptr, int(e.M), int(K), buf, m->ctx->stream);
+        m->fire_packs[key] = buf;
       }
       if (!packed_ok || hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
         return err(m, ORE_ERR_HIP, "fire weight packing failed");
@@ -736,7 +749,8 @@ ore_status plan(ore_model* m) {
       q.fire_E1 = e1.M;
       q.fire_E3 = e3.M;
       q.fire_w1 = m->fire_packs[pa];
-      q.fire_w3 = m->fire_packs[pb];
+      q.fire_w3 = m->fire_packs[fw ? -1 - pb : pb];
+      q.fire_wino = fw;
       q.fire_b1 = e1.in2 >= 0 ? m->values[e1.in2].cptr : nullptr;
       q.fire_b3 = e3.in2 >= 0 ? m->values[e3.in2].cptr : nullptr;
       if (!q.fire_b1 || !q.fire_b3 || q.in2 < 0) return err(m, ORE_ERR_UNSUPPORTED, "fused fire needs conv biases");
@@ -1059,7 +1073,8 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       ctx->mapped_hi = m->arena ? m->arena + m->arena_bytes : nullptr;
       const ore_status st = run_fire(ctx, x.p, n, s.fire_C, s.H, s.W, x.nstride, x.ps ? x.ps : s.H * s.W, s.fire_w1,
                                      s.fire_b1, s.fire_E1, s.fire_w3, s.fire_b3, s.fire_E3, s.wp, s.plan.Mp,
-                                     m->values[s.in2].cptr, s.M, y.p, y.nstride, y.ps ? y.ps : s.H * s.W);
+                                     m->values[s.in2].cptr, s.M, y.p, y.nstride, y.ps ? y.ps : s.H * s.W,
+                                     s.fire_wino);
       ctx->mapped_lo = ctx->mapped_hi = nullptr;
       return st;
     }
@@ -1567,7 +1582,8 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
 int32_t ore_model_step_tile(ore_model* m, int32_t i) {
   if (!m || i < 0 || size_t(i) >= m->exec_steps.size()) return -1;
   const Step& s = m->steps[m->exec_steps[i]];
-  if (s.kind == S_FIRE) return CONV_TILES_F32;  // "fire": the fused fire kernel (ore.Model.TILE_NAMES)
+  if (s.kind == S_FIRE)  // "fire" / "fire wino": the fused fire kernels (ore.Model.TILE_NAMES)
+    return s.fire_wino ? WINO_TILE_BASE + WINO_TILES_N : CONV_TILES_F32;
   if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.plan.epv > 0) return EPOOL_TILE_BASE + s.plan.epv;
   if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.ran_tile >= 0) return s.ran_tile;
   return (s.kind == S_CONV || s.kind == S_MATMUL) ? s.plan.cfg : -1;

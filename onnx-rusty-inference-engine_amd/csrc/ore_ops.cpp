@@ -211,9 +211,10 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
 ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
                     int64_t x_ps, const float* w1, const float* b1, int64_t E1, const float* w3, const float* b3,
                     int64_t E3, const float* ws, int64_t Msp, const float* bs, int64_t Ms, float* y, int64_t y_nstride,
-                    int64_t y_ps) {
+                    int64_t y_ps, bool wino) {
   if (N == 0) return ORE_OK;
   FireParams p{};
+  p.wino = wino ? 1 : 0;
   p.x = x; p.w1 = w1; p.b1 = b1; p.w3 = w3; p.b3 = b3; p.ws = ws; p.bs = bs; p.y = y;
   p.N = int(N); p.C = int(C); p.H = int(H); p.W = int(W);
   p.E1 = int(E1); p.E3 = int(E3); p.Ms = int(Ms); p.Msp = int(Msp);
@@ -233,6 +234,12 @@ ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t 
   if (x_ps < H * W || y_ps < H * W || !fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) ||
       !fits_i32(p.Ntot + 256))
     return set_error(ctx, ORE_ERR_INVALID, "fire geometry exceeds 32-bit indexing");
+  if (p.wino) {
+    if (!fire_wino_eligible(p)) return set_error(ctx, ORE_ERR_INVALID, "internal: Winograd fire module on an unsupported layout");
+    launch_fire_wino(p, ctx->stream);
+    ORE_HIP_CHECK(ctx, hipGetLastError());
+    return ORE_OK;
+  }
   if (!fire_eligible(p)) return set_error(ctx, ORE_ERR_INVALID, "internal: fused fire module on an unsupported layout");
   launch_fire(p, ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());

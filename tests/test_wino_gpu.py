@@ -40,6 +40,7 @@ def _np(t):
 def default_algo(monkeypatch):
     monkeypatch.delenv("ORE_NO_WINOGRAD", raising=False)
     monkeypatch.delenv("ORE_WINO_TILE", raising=False)
+    monkeypatch.delenv("ORE_FIRE_WINO", raising=False)
 
 
 # N, C, H, W, M: the SqueezeNet expand3x3 families and ragged edges (odd planes, 1-pixel planes,
@@ -217,3 +218,61 @@ def test_set_conv_algo_rejects_unknown(gpu_ctx):
     import ore
     with pytest.raises(ore.OreError):
         gpu_ctx.set_conv_algo(7)
+
+
+@pytest.mark.parametrize("case", [
+    # C, H, W, S1, E1, E3, S2 (as tests/test_model_gpu.py::test_fire_fusion_bit_identical)
+    (16, 12, 12, 16, 64, 64, 16),     # fire2 -> squeeze3 family
+    (32, 9, 8, 32, 128, 128, 48),     # fire5 -> squeeze6 (MFS = 3), W = 8
+    (24, 8, 7, 48, 192, 192, 64),     # fire7 -> squeeze8 (MFS = 4), odd W: right-edge tiles half outside
+    (16, 13, 13, 16, 64, 128, 32),    # unequal expands, 13 x 13 planes (odd H and W)
+])
+def test_fire_wino_fusion_bit_identical(gpu_ctx, case, monkeypatch):
+    """The fused fire module with its expand3x3 by Winograd ("fire wino", opt-in ORE_FIRE_WINO=1) equals
+    the separate kernels (Winograd expand3x3) bit for bit, and the oracle within the conv tolerance."""
+    import ore
+    import oracle
+    from test_model_gpu import _fire_model
+    monkeypatch.setenv("ORE_FIRE_MIN_COLS", "0")
+    monkeypatch.setenv("ORE_FIRE_WINO", "1")
+    C, H, W, S1, E1, E3, S2 = case
+    mb = _fire_model(*case)
+    x = np.random.default_rng(sum(case)).standard_normal((5, C, H, W)).astype(np.float32)
+    vals = []
+    for fusion in (ore.FUSE_ALL | ore.KEEP_VALUES, (ore.FUSE_ALL & ~ore.FUSE_FIRE) | ore.KEEP_VALUES):
+        m = ore.Model(gpu_ctx, mb, max_batch=5)
+        m.set_fusion(fusion)
+        y = _np(m.run(_t(x)))
+        vals.append((y, m.read_value("nr")))
+        names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+        if fusion & ore.FUSE_FIRE:
+            assert "fire wino" in names, names
+        else:
+            assert any(n.startswith("wino") for n in names), names
+        m.close()
+    np.testing.assert_array_equal(vals[0][1], vals[1][1])
+    np.testing.assert_array_equal(vals[0][0], vals[1][0])
+    ref = oracle.Model(mb).run(x, S2)
+    np.testing.assert_allclose(vals[0][0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("hw", [64, 224])
+def test_squeezenet_fire_wino_fusion(gpu_ctx, hw, monkeypatch):
+    """SqueezeNet with the fire + squeeze pairs fused on the Winograd fire kernel: probabilities
+    bit-identical to the separate (Winograd) kernels."""
+    import ore
+    from ore import squeezenet
+    monkeypatch.setenv("ORE_FIRE_MIN_COLS", "0")
+    monkeypatch.setenv("ORE_FIRE_WINO", "1")
+    mb = squeezenet.build(hw)
+    x = _t(squeezenet.synthetic_input(3, hw, seed=19))
+    outs = []
+    for fusion in (ore.FUSE_ALL, ore.FUSE_ALL & ~ore.FUSE_FIRE):
+        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion(fusion)
+        outs.append(_np(m.run(x)))
+        if fusion & ore.FUSE_FIRE:
+            n = sum(1 for t in m.tiles() if t >= 0 and ore.Model.TILE_NAMES[t] == "fire wino")
+            assert n == (5 if hw == 224 else 2), n
+        m.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
