@@ -41,6 +41,7 @@ namespace ore {
 typedef float wg_floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16_t __attribute__((ext_vector_type(16)));
 typedef int int4d_t __attribute__((ext_vector_type(4)));
+typedef float wg_f2 __attribute__((ext_vector_type(2)));
 
 // U[((c * 4 + xi / 4) * Mp + m) * 4 + xi % 4] = (G g_mc G^T)[xi / 4][xi % 4] (f64, rounded once): for a
 // fixed (channel, position quad) the channels' 16-B quads are contiguous, so the A loads of a wave
@@ -177,12 +178,19 @@ __device__ __forceinline__ void wg_store(const ConvParams& p, const WgTile& w, i
 #ifdef ORE_EXP_WG_NOSTORE  // timing experiment only: stores skipped (kept live by a never-true test)
   if (o[0] != 1.2345e-30f) return;
 #endif
-  float* yp = p.y + (unsigned)(w.ybase + m * p.y_ps);
-  yp[0] = o[0];
-  if (w.c1ok) yp[1] = o[1];
-  if (w.r1ok) {
-    yp[p.W] = o[2];
-    if (w.c1ok) yp[p.W + 1] = o[3];
+  // a tile row's two pixels as one 8-B store (4-B aligned on odd planes; buffer stores take that),
+  // so a wave-instruction writes whole lines: two 4-B stores per row wrote every line twice
+  // (PMC WRITE_SIZE 1.5x the output, profiles/r02e_pmc_layers.txt)
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, 0x7FFFFFF0, 0x00020000);
+  const int yo = (w.ybase + m * p.y_ps) * 4;
+  typedef int wg_i2 __attribute__((ext_vector_type(2)));
+  if (w.c1ok) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(wg_i2, (wg_f2){o[0], o[1]}), yr, yo, 0, 0);
+    if (w.r1ok)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(wg_i2, (wg_f2){o[2], o[3]}), yr, yo + p.W * 4, 0, 0);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, o[0]), yr, yo, 0, 0);
+    if (w.r1ok) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, o[2]), yr, yo + p.W * 4, 0, 0);
   }
 }
 
