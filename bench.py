@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-b1", action="store_true", help="skip the batch-1 latency probe")
     ap.add_argument("--no-autotune", action="store_true", help="keep the heuristic per-layer conv tiles")
     ap.add_argument("--dump-steps", default="", help="write the plan's kernel steps (op, name, flops, bytes) as JSON")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="2: independent neighbouring steps on a side stream (ore_model_set_streams; experiments)")
     ap.add_argument("--no-winograd", action="store_true",
                     help="f32: 3x3 stride-1 convs on the direct kernels only (ORE_LOAD_NO_WINOGRAD)")
     ap.add_argument("--fusion", type=int, default=None, help="ore_model_set_fusion flags (experiments; default: the model's)")
@@ -153,6 +155,8 @@ def main():
 
     if args.fusion is not None:
         model.set_fusion(args.fusion)
+    if args.streams != 1:
+        model.set_streams(args.streams)
     if not args.no_autotune:  # per-layer conv tile search, outside the timed region
         model.autotune(x, out)
     if args.dump_steps and rank == 0:  # kernel-step names for tools/pmc_report.py

@@ -11,7 +11,7 @@ while read -r GROUP; do
   [ -z "$GROUP" ] && continue
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $GROUP --kernel-trace --output-format csv -d "$OUT/p$i" -o run -- \
-    python3 "$ROOT/tools/wino_one.py" "$@" > "$OUT/p$i.log" 2>&1
+    python3 "$ROOT/tools/${WPMC_SCRIPT:-wino_one.py}" "$@" > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "pass $i [$GROUP] rc=$rc"
   case $rc in 0) ;; *) exit $rc;; esac

@@ -6,13 +6,13 @@ for tag in sys.argv[1:]:
         # per dispatch sum counter values for conv kernels
         disp = collections.defaultdict(dict)
         for r in rows:
-            if "conv" not in r["Kernel_Name"]: continue
+            if "conv" not in r["Kernel_Name"] or "pack" in r["Kernel_Name"] or "ktab" in r["Kernel_Name"]: continue
             d = r["Dispatch_Id"]; disp[d][r["Counter_Name"]] = disp[d].get(r["Counter_Name"], 0) + float(r["Counter_Value"])
         ds = sorted(disp, key=int)[-3:]
         for d in ds:
             for k, v in disp[d].items(): vals[k].append(v)
     kt = list(csv.DictReader(open(glob.glob(f"gpurun_out/wpmc_{tag}/p1/run_kernel_trace.csv")[0])))
-    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000 for r in kt if "conv" in r["Kernel_Name"]]
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000 for r in kt if "conv" in r["Kernel_Name"] and "pack" not in r["Kernel_Name"]]
     print(tag, "kernel", [r["Kernel_Name"][:60] for r in kt if "conv" in r["Kernel_Name"]][-1], "us", [round(x,1) for x in durs[-3:]])
     v = {k: sum(x) / len(x) for k, x in vals.items()}
     for k in sorted(v): print(f"  {k:28s} {v[k]:.4g}")
