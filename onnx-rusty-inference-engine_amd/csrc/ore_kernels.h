@@ -119,6 +119,30 @@ void launch_fire_pack_wino(const float* w, int M, int C, float* u, hipStream_t s
 // W [M][K] -> the fire kernel's row-permuted K-major packing (M % 64 == 0)
 void launch_fire_pack(const float* w, int M, int K, float* wf, hipStream_t s);
 
+// f16 models: the fused fire module (ore_fire_f16.hip) on NHWC f16 values (pixel strides in
+// elements, image strides in elements); weights packed by launch_fire_pack_f16
+struct FireF16Params {
+  const void* x;   // S: f16 NHWC, C channels, pixel stride x_cs
+  const void* w1;  // expand1x1: launch_fire_pack_f16(w, E1, C, 1)
+  const float* b1;
+  const void* w3;  // expand3x3: launch_fire_pack_f16(w, E3, C, 9), k = (r, s, c)
+  const float* b3;
+  const void* ws;  // next squeeze: launch_fire_pack_f16(w, Ms, E1 + E3, 1)
+  const float* bs;
+  void* y;         // S': f16 NHWC, Ms channels, pixel stride y_cs
+  int N, C, H, W, E1, E3, Ms, Msp;
+  int x_cs, y_cs;
+  long long x_nstride, y_nstride;
+  int tiles_per_img;  // filled by the launcher
+};
+constexpr int FIRE_F16_LDS_MAX = 80 * 1024;  // the input halo of one workgroup (two per CU)
+int fire_f16_lds_bytes(int C, int H, int W);
+bool fire_f16_eligible(const FireF16Params& p);
+void launch_fire_f16(const FireF16Params& p, hipStream_t s);
+// W [M][C][kk] f32 (kk = 1 or 9) -> [C kk / 16][roundup(M, 32)][16] f16 with permuted rows
+size_t fire_pack_f16_bytes(int M, int C, int kk);
+void launch_fire_pack_f16(const float* w, int M, int C, int kk, void* out, hipStream_t s);
+
 int conv_tile_config(int M);
 int conv_packed_mp(int M);  // padded M of the packed weights
 int conv_packed_kp(int K);  // padded K of the packed weights

@@ -94,6 +94,8 @@ struct Step {
   const float* fire_b1 = nullptr;
   const float* fire_b3 = nullptr;
   bool fire_wino = false;          // the e3 by Winograd (fire_wino_kernel; fire_w3 in launch_fire_pack_wino layout)
+  bool fire_f16 = false;           // f16 model: fire_f16_kernel, fire_w1 / fire_w3 / fire_ws16 in launch_fire_pack_f16 layout
+  const void* fire_ws16 = nullptr;
   ConvPlan plan{};        // kernel choice and weight layout for S_CONV / S_MATMUL
   float* wp = nullptr;    // packed weights (layout per plan) for S_CONV / S_MATMUL
   const int2* ktab = nullptr;  // gather table (follows wp in the packed allocation; gather kernel only)
@@ -763,6 +765,69 @@ ore_status plan(ore_model* m) {
     }
     count_uses(m, m->steps);
   }
+  // (1e) f16 models: the same fire module + next squeeze pattern in one fire_f16_kernel launch
+  // (ore_fire_f16.hip): expand1x1 / expand3x3 (+ Relu) on 16-B NHWC gathers, C % 16 == 0 and <= 64,
+  // expands in 32-channel chunks, the squeeze <= 64 channels; bit-identical to the three
+  // conv_f16_kernel launches
+  if ((m->fusion & ORE_FUSE_FIRE) && m->f16 && (m->fusion & ORE_FUSE_CONV_RELU)) {
+    for (size_t i = 0; i < m->steps.size(); ++i) {
+      Step& cc = m->steps[i];
+      if (cc.kind != S_CONCAT || cc.axis != 1 || cc.in0 < 0 || cc.in1 < 0 || cc.in0 == cc.in1) continue;
+      const int pa = producer[cc.in0], pb = producer[cc.in1];
+      if (pa < 0 || pb < 0) continue;
+      int qi = -1;
+      for (size_t j = i + 1; j < m->steps.size(); ++j)
+        if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == cc.out || m->steps[j].in1 == cc.out)) { qi = int(j); break; }
+      if (qi < 0) continue;
+      Step &e1 = m->steps[pa], &e3 = m->steps[pb], &q = m->steps[qi];
+      auto vec16 = [](const Step& s) {
+        return s.kind == S_CONV && s.relu && !s.pool && !s.epool && s.plan.f16 && s.plan.xmode == F16_X_NHWC_VEC &&
+               s.sh == 1 && s.sw == 1 && s.win.Ho == s.H && s.win.Wo == s.W;
+      };
+      auto is1x1 = [&](const Step& s) { return vec16(s) && s.kh == 1 && s.kw == 1 && s.win.pt == 0 && s.win.pl == 0; };
+      const bool e3ok = vec16(e3) && e3.kh == 3 && e3.kw == 3 && e3.win.pt == 1 && e3.win.pl == 1;
+      if (!is1x1(e1) || !e3ok || !is1x1(q) || q.in0 != cc.out || e1.in0 != e3.in0 || e1.H != e3.H || e1.W != e3.W) continue;
+      if (e1.C % 16 || e1.C > 64 || e1.M % 32 || e3.M % 32 || q.M % 8 || q.M > 64 || q.C != e1.M + e3.M) continue;
+      if (fire_f16_lds_bytes(int(e1.C), int(e1.H), int(e1.W)) > FIRE_F16_LDS_MAX || q.in2 < 0 || e1.in2 < 0 || e3.in2 < 0) continue;
+      const Value &va = m->values[cc.in0], &vb = m->values[cc.in1], &vc = m->values[cc.out], &vs = m->values[e1.in0];
+      if (va.uses != 1 || vb.uses != 1 || vc.uses != 1 || va.is_output || vb.is_output || vc.is_output || vs.es != 2) continue;
+      // the three weight packings (made once per model; keys 2000000 + expand index, 3000000 + squeeze index)
+      bool packed_ok = true;
+      for (int idx : {pa, pb, qi}) {
+        const int key = (idx == qi ? 3000000 : 2000000) + idx;
+        if (m->fire_packs.count(key)) continue;
+        const Step& e = m->steps[idx];
+        const int kk = int(e.kh * e.kw);
+        float* buf = nullptr;
+        if (hipMalloc(reinterpret_cast<void**>(&buf), fire_pack_f16_bytes(int(e.M), int(e.C), kk)) != hipSuccess) {
+          packed_ok = false;
+          break;
+        }
+        launch_fire_pack_f16(m->values[e.in1].cptr, int(e.M), int(e.C), kk, buf, m->ctx->stream);
+        m->fire_packs[key] = buf;
+      }
+      if (!packed_ok || hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
+        return err(m, ORE_ERR_HIP, "f16 fire weight packing failed");
+      q.kind = S_FIRE;
+      q.fire_f16 = true;
+      q.in0 = e1.in0;
+      q.fire_C = e1.C;
+      q.fire_E1 = e1.M;
+      q.fire_E3 = e3.M;
+      q.fire_w1 = m->fire_packs[2000000 + pa];
+      q.fire_w3 = m->fire_packs[2000000 + pb];
+      q.fire_ws16 = m->fire_packs[3000000 + qi];
+      q.fire_b1 = m->values[e1.in2].cptr;
+      q.fire_b3 = m->values[e3.in2].cptr;
+      q.flops_per_img += e1.flops_per_img + e3.flops_per_img;
+      q.bytes_per_img = 2.0 * double(e1.C * e1.H * e1.W) + 2.0 * double(q.M * q.H * q.W);
+      q.name = e1.name.substr(0, e1.name.find('/')) + "+" + q.name;
+      m->values[cc.in0].elided = m->values[cc.in1].elided = m->values[cc.out].elided = true;
+      e1.kind = e3.kind = cc.kind = S_NOP;
+      e1.in0 = e3.in0 = cc.in0 = cc.in1 = -1;
+    }
+    count_uses(m, m->steps);
+  }
   // (1f) ORE_LOAD_X3: every conv / matmul not taken by an f32-MFMA fusion above runs its x3 plan
   if (m->x3)
     for (auto& st : m->steps)
@@ -1069,6 +1134,10 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
     }
     case S_FIRE: {
       const Ref x = ref_of(m, s.in0);
+      if (s.fire_f16)
+        return run_fire_f16(ctx, x.p, n, s.fire_C, s.H, s.W, x.nstride, x.ps ? x.ps : s.fire_C, s.fire_w1, s.fire_b1,
+                            s.fire_E1, s.fire_w3, s.fire_b3, s.fire_E3, s.fire_ws16, m->values[s.in2].cptr, s.M, y.p,
+                            y.nstride, y.ps ? y.ps : s.M);
       ctx->mapped_lo = m->arena_alloc;  // the arena and its 4 KiB lead are mapped
       ctx->mapped_hi = m->arena ? m->arena + m->arena_bytes : nullptr;
       const ore_status st = run_fire(ctx, x.p, n, s.fire_C, s.H, s.W, x.nstride, x.ps ? x.ps : s.H * s.W, s.fire_w1,
@@ -1582,8 +1651,8 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
 int32_t ore_model_step_tile(ore_model* m, int32_t i) {
   if (!m || i < 0 || size_t(i) >= m->exec_steps.size()) return -1;
   const Step& s = m->steps[m->exec_steps[i]];
-  if (s.kind == S_FIRE)  // "fire" / "fire wino": the fused fire kernels (ore.Model.TILE_NAMES)
-    return s.fire_wino ? WINO_TILE_BASE + WINO_TILES_N : CONV_TILES_F32;
+  if (s.kind == S_FIRE)  // "fire" / "fire wino" / "fire f16": the fused fire kernels (ore.Model.TILE_NAMES)
+    return s.fire_f16 ? WINO_TILE_BASE + WINO_TILES_N + 1 : s.fire_wino ? WINO_TILE_BASE + WINO_TILES_N : CONV_TILES_F32;
   if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.plan.epv > 0) return EPOOL_TILE_BASE + s.plan.epv;
   if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.ran_tile >= 0) return s.ran_tile;
   return (s.kind == S_CONV || s.kind == S_MATMUL) ? s.plan.cfg : -1;

@@ -246,6 +246,25 @@ ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t 
   return ORE_OK;
 }
 
+ore_status run_fire_f16(ore_ctx* ctx, const void* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
+                        int64_t x_cs, const void* w1, const float* b1, int64_t E1, const void* w3, const float* b3,
+                        int64_t E3, const void* ws, const float* bs, int64_t Ms, void* y, int64_t y_nstride,
+                        int64_t y_cs) {
+  if (N == 0) return ORE_OK;
+  if (!fits_i32(N) || !fits_i32(H * W) || !fits_i32(x_cs) || !fits_i32(y_cs))
+    return set_error(ctx, ORE_ERR_INVALID, "fire geometry exceeds 32-bit indexing");
+  FireF16Params p{};
+  p.x = x; p.w1 = w1; p.b1 = b1; p.w3 = w3; p.b3 = b3; p.ws = ws; p.bs = bs; p.y = y;
+  p.N = int(N); p.C = int(C); p.H = int(H); p.W = int(W);
+  p.E1 = int(E1); p.E3 = int(E3); p.Ms = int(Ms); p.Msp = int((Ms + 31) / 32 * 32);
+  p.x_cs = int(x_cs); p.y_cs = int(y_cs);
+  p.x_nstride = x_nstride; p.y_nstride = y_nstride;
+  if (!fire_f16_eligible(p)) return set_error(ctx, ORE_ERR_INVALID, "internal: f16 fire module on an unsupported layout");
+  launch_fire_f16(p, ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  return ORE_OK;
+}
+
 double epool_tile(int64_t Ho, int64_t Wo, int64_t pkh, int64_t pkw, int64_t psh, int64_t psw, const Window& pwin,
                   int* tr, int* tc) {
   // the kernel's pooled epilogue is specialised for 3x3 / stride-2 windows (every SqueezeNet pool)

@@ -211,3 +211,108 @@ def test_f16_dma_kernel_bit_identical(gpu_ctx, cfg, monkeypatch):
         m.close()
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+def _fire_model_f16(C, H, W, S1, E1, E3, S2, ints=False, seed=0):
+    """squeeze (C -> S1) -> expand 1x1 (E1) / 3x3 pad 1 (E3) -> Concat -> squeeze (S2) -> GAP, all
+    Relu; ints: sparse {-1, 0, 1} weights and small integer biases (every value exact in f16).
+    Returns (model bytes, {name: (w, b)})."""
+    from ore import onnx_wire as wr
+    rng = np.random.default_rng(seed + C * 7 + H + W + S1 + E1 + E3 + S2)
+    shapes = {"wq": (S1, C, 1, 1), "w1": (E1, S1, 1, 1), "w3": (E3, S1, 3, 3), "wn": (S2, E1 + E3, 1, 1)}
+    params, inits, vinfo = {}, [], [wr.encode_value_info("x", (1, C, H, W))]
+    for n, shp in shapes.items():
+        if ints:
+            w, b = _sparse(rng, shp, 8), _ints(rng, -4, 4, (shp[0],))
+        else:
+            fan = shp[1] * shp[2] * shp[3]
+            w = (rng.standard_normal(shp) * np.sqrt(2.0 / fan)).astype(np.float32)
+            b = rng.uniform(-0.1, 0.1, shp[0]).astype(np.float32)
+        params[n] = (w, b)
+        inits += [wr.encode_tensor(n, w), wr.encode_tensor("b" + n, b)]
+        vinfo += [wr.encode_value_info(n, w.shape), wr.encode_value_info("b" + n, b.shape)]
+    conv = lambda i, w, o, pads: wr.encode_node("Conv", [i, w, "b" + w], [o], attrs=[
+        wr.encode_attr_ints("pads", pads), wr.encode_attr_ints("strides", [1, 1])])
+    nodes = [conv("x", "wq", "q", [0] * 4), wr.encode_node("Relu", ["q"], ["qr"]),
+             conv("qr", "w1", "e1", [0] * 4), wr.encode_node("Relu", ["e1"], ["e1r"]),
+             conv("qr", "w3", "e3", [1] * 4), wr.encode_node("Relu", ["e3"], ["e3r"]),
+             wr.encode_node("Concat", ["e1r", "e3r"], ["cat"], attrs=[wr.encode_attr_int("axis", 1)]),
+             conv("cat", "wn", "n", [0] * 4), wr.encode_node("Relu", ["n"], ["nr"]),
+             wr.encode_node("GlobalAveragePool", ["nr"], ["y"])]
+    return wr.encode_model("fire", nodes, inits, vinfo, [wr.encode_value_info("y", (1, S2, 1, 1))]), params
+
+
+FIRE_F16_CASES = [
+    # C, H, W, S1, E1, E3, S2 -> fire_f16_kernel<S1 / 16, ceil(S2 / 32)>
+    (16, 12, 12, 16, 64, 64, 16),     # fire2 -> squeeze3 family, one tile per image
+    (32, 9, 8, 32, 128, 128, 48),     # fire5 -> squeeze6 (48 of 64 squeeze rows), W = 8
+    (24, 8, 7, 48, 192, 192, 64),     # fire7 -> squeeze8, W = 7
+    (16, 13, 13, 64, 64, 128, 32),    # C = 64, unequal expands, 13 x 13
+    (8, 54, 54, 16, 64, 64, 32),      # SqueezeNet fire3 plane: 12 tiles per image, tile edges mid-row
+    (16, 27, 27, 48, 192, 192, 48),   # fire6 plane: 3 tiles, the last partial
+]
+
+
+@pytest.mark.parametrize("case", FIRE_F16_CASES)
+def test_f16_fire_fusion_bit_identical(gpu_ctx, case):
+    """f16 models: expand 1x1 + expand 3x3 + Concat + the next squeeze in one fire_f16_kernel launch
+    equals the three separate conv_f16_kernel launches bit for bit; the concat is never stored."""
+    import ore
+    C, H, W = case[:3]
+    mb, _ = _fire_model_f16(*case)
+    x = np.random.default_rng(sum(case)).standard_normal((3, C, H, W)).astype(np.float32)
+    vals = []
+    for fusion in (ore.FUSE_ALL | ore.KEEP_VALUES, (ore.FUSE_ALL & ~ore.FUSE_FIRE) | ore.KEEP_VALUES):
+        m = ore.Model(gpu_ctx, mb, max_batch=3, precision="f16")
+        m.set_fusion(fusion)
+        y = _np(m.run(_t(x)))
+        vals.append((y, m.read_value("nr")))
+        names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+        assert ("fire f16" in names) == bool(fusion & ore.FUSE_FIRE)
+        if fusion & ore.FUSE_FIRE:
+            with pytest.raises(ore.OreError):
+                m.read_value("cat")  # never materialised
+        m.close()
+    np.testing.assert_array_equal(vals[0][1], vals[1][1])
+    np.testing.assert_array_equal(vals[0][0], vals[1][0])
+    assert np.abs(vals[0][1]).max() > 0  # not a dead (all-Relu-zero) module
+
+
+@pytest.mark.parametrize("case", [FIRE_F16_CASES[1], FIRE_F16_CASES[4]])
+def test_f16_fire_fusion_exact_integers(gpu_ctx, case):
+    """Small-integer weights / biases / input: every product and sum of the fused module is exact in
+    f16 / f32, so the fused f16 kernel equals the f32 oracle bit for bit (checks the permuted
+    packings, the halo staging and the tap offsets independently of the unfused kernels)."""
+    import ore
+    C, H, W, S1, E1, E3, S2 = case
+    mb, prm = _fire_model_f16(*case, ints=True, seed=3)
+    x = _ints(np.random.default_rng(11), -2, 2, (2, C, H, W))
+    m = ore.Model(gpu_ctx, mb, max_batch=2, precision="f16")
+    m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+    _np(m.run(_t(x)))
+    assert "fire f16" in [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+    q = oracle.relu(oracle.conv2d(x, *prm["wq"], pads=[0] * 4, strides=(1, 1)))
+    e1 = oracle.relu(oracle.conv2d(q, *prm["w1"], pads=[0] * 4, strides=(1, 1)))
+    e3 = oracle.relu(oracle.conv2d(q, *prm["w3"], pads=[1] * 4, strides=(1, 1)))
+    n = oracle.relu(oracle.conv2d(np.concatenate([e1, e3], 1), *prm["wn"], pads=[0] * 4, strides=(1, 1)))
+    assert np.abs(n).max() < 2048 and np.abs(n).max() > 0
+    np.testing.assert_array_equal(m.read_value("nr"), n)
+    m.close()
+
+
+def test_f16_squeezenet_fire_fusion(gpu_ctx):
+    """SqueezeNet-1.0 @224, f16: the five fire + squeeze pairs run fire_f16_kernel (fire4 / fire8 feed
+    a MaxPool, fire9 conv10) and the probabilities equal the unfused graph's bit for bit."""
+    import ore
+    from ore import squeezenet
+    mb = squeezenet.build(224)
+    x = _t(squeezenet.synthetic_input(3, 224, seed=21))
+    outs = []
+    for fusion in (ore.FUSE_ALL, ore.FUSE_ALL & ~ore.FUSE_FIRE):
+        m = ore.Model(gpu_ctx, mb, max_batch=3, precision="f16")
+        m.set_fusion(fusion)
+        outs.append(_np(m.run(x)))
+        n = sum(1 for t in m.tiles() if t >= 0 and ore.Model.TILE_NAMES[t] == "fire f16")
+        assert n == (5 if fusion & ore.FUSE_FIRE else 0)
+        m.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
