@@ -24,7 +24,13 @@
 // Same operands, same k order, same MFMA instruction and the same f32 epilogue arithmetic as the
 // three separate conv_f16_kernel launches: bit-identical results (tests/test_f16_gpu.py).  Skipped
 // zero k-steps (the separate kernels pad K to 32) add exact zeros to a never-negative-zero sum.
+#include <float.h>
 #include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
 
 #include "ore_kernels.h"
 
@@ -47,34 +53,134 @@ __host__ __device__ inline int ff_halo_rows(int H, int W) {
 __device__ __forceinline__ fh8 ld_g(const _Float16* p) { return *reinterpret_cast<const fh8*>(p); }
 __device__ __forceinline__ fh8 ld_s(const _Float16* p) { return *reinterpret_cast<const fh8*>(p); }
 
+// Stage input rows hr0 .. hr0 + nrows - 1 (columns -1 .. W, zeros outside the image) of image x into
+// the LDS halo, pixel stride PS halves, 16-B chunks
+template <int NKC, int PS>
+__device__ __forceinline__ void ff_stage_halo(_Float16* halo, const _Float16* __restrict__ x, int x_cs, int H, int W,
+                                              int hr0, int nrows) {
+  const int W2 = W + 2, nck = nrows * W2 * (2 * NKC);
+  for (int i = threadIdx.x; i < nck; i += 256) {
+    const int px = i / (2 * NKC), ck = i - px * (2 * NKC);
+    const int rr = px / W2, cc = px - rr * W2;
+    const int ih = hr0 + rr, iw = cc - 1;
+    fh8 v = {};
+    if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) v = ld_g(x + (ih * W + iw) * x_cs + ck * 8);
+    *reinterpret_cast<fh8*>(halo + px * PS + ck * 8) = v;
+  }
+}
+
+template <int F>
+__device__ __forceinline__ void ff_zero(ff16 (&acc)[F]) {
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[f][e] = 0.0f;
+}
+
+// One 32-channel chunk (rows c0 .. c0 + 31 of the permuted packing) of expand1x1 over F pixel
+// fragments: NKC k-steps on the centre tap (hb[f] + ctr)
+template <int NKC, int F>
+__device__ __forceinline__ void ff_e1_chunk(ff16 (&acc)[F], const _Float16* __restrict__ w1, int E1, int c0, int arow,
+                                            const _Float16* halo, const int (&hb)[F], int ctr) {
+  fh8 a[NKC];
+#pragma unroll
+  for (int s = 0; s < NKC; ++s) a[s] = ld_g(w1 + (s * E1 + c0) * 16 + arow);
+  ff_zero(acc);
+#pragma unroll
+  for (int s = 0; s < NKC; ++s) {
+    fh8 b[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) b[f] = ld_s(halo + hb[f] + ctr + 16 * s);
+#pragma unroll
+    for (int f = 0; f < F; ++f) acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[s], b[f], acc[f], 0, 0, 0);
+  }
+}
+
+// One 32-channel chunk of expand3x3: 9 taps x NKC k-steps, k order (r, s, c).  B fragments one step
+// ahead, A PD steps ahead; the scheduling barrier keeps every step's loads in it (unpinned, the
+// scheduler hoists all F x 9 NKC LDS reads and spills).
+template <int NKC, int F, int PS>
+__device__ __forceinline__ void ff_e3_chunk(ff16 (&acc)[F], const _Float16* __restrict__ w3, int E3, int c0, int arow,
+                                            const _Float16* halo, const int (&hb)[F], int W2) {
+  constexpr int NS3 = 9 * NKC, PD = 6;
+  fh8 a[PD];
+#pragma unroll
+  for (int s = 0; s < PD; ++s)
+    if (s < NS3) a[s] = ld_g(w3 + (s * E3 + c0) * 16 + arow);
+  ff_zero(acc);
+  auto boff = [&](int s) __attribute__((always_inline)) {
+    const int tap = s / NKC, cs = s - tap * NKC;
+    return ((tap / 3) * W2 + tap % 3) * PS + 16 * cs;
+  };
+  fh8 bn[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) bn[f] = ld_s(halo + hb[f] + boff(0));
+#pragma unroll
+  for (int s = 0; s < NS3; ++s) {
+    const fh8 cur = a[s % PD];
+    fh8 b[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) b[f] = bn[f];
+    if (s + PD < NS3) a[s % PD] = ld_g(w3 + ((s + PD) * E3 + c0) * 16 + arow);
+    if (s + 1 < NS3) {
+#pragma unroll
+      for (int f = 0; f < F; ++f) bn[f] = ld_s(halo + hb[f] + boff(s + 1));
+    }
+#pragma unroll
+    for (int f = 0; f < F; ++f) acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur, b[f], acc[f], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// this lane's 16 bias values of a chunk: channel c0 + 16 (e >> 3) + 8 h + (e & 7) for element e
+__device__ __forceinline__ void ff_bias16(float (&bv)[16], const float* __restrict__ bias, int c0, int h) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const float4 u0 = *reinterpret_cast<const float4*>(bias + c0 + 16 * t + 8 * h);
+    const float4 u1 = *reinterpret_cast<const float4*>(bias + c0 + 16 * t + 8 * h + 4);
+    bv[8 * t + 0] = u0.x; bv[8 * t + 1] = u0.y; bv[8 * t + 2] = u0.z; bv[8 * t + 3] = u0.w;
+    bv[8 * t + 4] = u1.x; bv[8 * t + 5] = u1.y; bv[8 * t + 6] = u1.z; bv[8 * t + 7] = u1.w;
+  }
+}
+
+// squeeze epilogue of F pixel fragments: bias + Relu + one rounding; element 8g + e of lane half h
+// = channel 32 i + 16 g + 8 h + e, one 16-B store per (fragment, g) at y + yo[f] + 32 i + 16 g
+template <int MSF, int F>
+__device__ __forceinline__ void ff_store_squeeze(const ff16 (&sacc)[MSF][F], const FireF16Params& p, _Float16* y,
+                                                 const int (&yo)[F], const bool (&pok)[F], int h) {
+#pragma unroll
+  for (int i = 0; i < MSF; ++i)
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int ch = 32 * i + 16 * g + 8 * h;
+      if (ch >= p.Ms) continue;
+      const float4 u0 = *reinterpret_cast<const float4*>(p.bs + ch);
+      const float4 u1 = *reinterpret_cast<const float4*>(p.bs + ch + 4);
+      const float bv[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        if (!pok[f]) continue;
+        fh8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (_Float16)fmaxf(sacc[i][f][8 * g + e] + bv[e], 0.0f);
+        *reinterpret_cast<fh8*>(y + yo[f] + 32 * i + 16 * g) = o;
+      }
+    }
+}
+
 template <int NKC, int MSF>
 __global__ __launch_bounds__(256, 2) void fire_f16_kernel(FireF16Params p) {
   extern __shared__ __attribute__((aligned(16))) _Float16 halo[];
   constexpr int C = 16 * NKC, PS = C + 8;  // input channels; LDS pixel stride (halves)
-  constexpr int NS3 = 9 * NKC;             // expand3x3 k-steps
-  constexpr int PD = 6;                    // expand3x3 A-operand loads in flight
-  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, h = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = threadIdx.x & 63, lr = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = p.H, W = p.W, HW = H * W, W2 = W + 2;
   const int img = blockIdx.x / p.tiles_per_img;
   const int q0 = (blockIdx.x - img * p.tiles_per_img) * FF_PIX;
   const int qlast = min(q0 + FF_PIX - 1, HW - 1);
-  const int hr0 = q0 / W - 1;                        // image row of halo row 0
-  const int nrows = qlast / W - q0 / W + 3;
-  const _Float16* __restrict__ x = static_cast<const _Float16*>(p.x) + (long long)img * p.x_nstride;
-
-  // stage the halo: nrows x (W + 2) pixels x C channels, 16-B chunks
-  {
-    const int nck = nrows * W2 * (2 * NKC);
-    for (int i = tid; i < nck; i += 256) {
-      const int px = i / (2 * NKC), ck = i - px * (2 * NKC);
-      const int rr = px / W2, cc = px - rr * W2;
-      const int ih = hr0 + rr, iw = cc - 1;
-      fh8 v = {};
-      if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) v = ld_g(x + (ih * W + iw) * p.x_cs + ck * 8);
-      *reinterpret_cast<fh8*>(halo + px * PS + ck * 8) = v;
-    }
-  }
+  const int hr0 = q0 / W - 1;  // image row of halo row 0
+  ff_stage_halo<NKC, PS>(halo, static_cast<const _Float16*>(p.x) + (long long)img * p.x_nstride, p.x_cs, H, W, hr0,
+                         qlast / W - q0 / W + 3);
   __syncthreads();
   if (q0 + 64 * wave >= HW) return;  // no pixel of this wave (after the only barrier)
 
@@ -91,19 +197,12 @@ __global__ __launch_bounds__(256, 2) void fire_f16_kernel(FireF16Params p) {
     yo[f] = qq * p.y_cs + 8 * h;
   }
   const int ctr = (W2 + 1) * PS;  // tap (1, 1)
-  const _Float16* __restrict__ w1 = static_cast<const _Float16*>(p.w1);
-  const _Float16* __restrict__ w3 = static_cast<const _Float16*>(p.w3);
   const _Float16* __restrict__ ws = static_cast<const _Float16*>(p.ws);
-  const int E1 = p.E1, E3 = p.E3, Msp = p.Msp;
   const int arow = lr * 16 + 8 * h;  // this lane's 8 halves inside a [row][16] fragment block
 
   ff16 sacc[MSF][2];
 #pragma unroll
-  for (int i = 0; i < MSF; ++i)
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) sacc[i][f][e] = 0.0f;
+  for (int i = 0; i < MSF; ++i) ff_zero(sacc[i]);
 
   // bias + Relu + one rounding of a finished 32-channel chunk (c0 inside its conv, cat0 inside the
   // concat), then the squeeze's two k-steps over it
@@ -112,15 +211,9 @@ __global__ __launch_bounds__(256, 2) void fire_f16_kernel(FireF16Params p) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < MSF; ++i) aq[t][i] = ld_g(ws + ((cat0 / 16 + t) * Msp + 32 * i) * 16 + arow);
+      for (int i = 0; i < MSF; ++i) aq[t][i] = ld_g(ws + ((cat0 / 16 + t) * p.Msp + 32 * i) * 16 + arow);
     float bv[16];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const float4 u0 = *reinterpret_cast<const float4*>(bias + c0 + 16 * t + 8 * h);
-      const float4 u1 = *reinterpret_cast<const float4*>(bias + c0 + 16 * t + 8 * h + 4);
-      bv[8 * t + 0] = u0.x; bv[8 * t + 1] = u0.y; bv[8 * t + 2] = u0.z; bv[8 * t + 3] = u0.w;
-      bv[8 * t + 4] = u1.x; bv[8 * t + 5] = u1.y; bv[8 * t + 6] = u1.z; bv[8 * t + 7] = u1.w;
-    }
+    ff_bias16(bv, bias, c0, h);
     fh8 bq[2][2];
 #pragma unroll
     for (int f = 0; f < 2; ++f)
@@ -134,78 +227,135 @@ __global__ __launch_bounds__(256, 2) void fire_f16_kernel(FireF16Params p) {
         for (int f = 0; f < 2; ++f) sacc[i][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aq[t][i], bq[t][f], sacc[i][f], 0, 0, 0);
   };
 
-  // expand1x1 chunks: NKC k-steps on the centre tap
-  for (int c0 = 0; c0 < E1; c0 += 32) {
-    fh8 a[NKC];
-#pragma unroll
-    for (int s = 0; s < NKC; ++s) a[s] = ld_g(w1 + (s * E1 + c0) * 16 + arow);
+  for (int c0 = 0; c0 < p.E1; c0 += 32) {  // expand1x1 chunks
     ff16 acc[2];
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[f][e] = 0.0f;
-#pragma unroll
-    for (int s = 0; s < NKC; ++s) {
-      const fh8 b0 = ld_s(halo + hb[0] + ctr + 16 * s), b1 = ld_s(halo + hb[1] + ctr + 16 * s);
-      acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[s], b0, acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[s], b1, acc[1], 0, 0, 0);
-    }
+    ff_e1_chunk<NKC, 2>(acc, static_cast<const _Float16*>(p.w1), p.E1, c0, arow, halo, hb, ctr);
     feed(acc, p.b1, c0, c0);
   }
-  // expand3x3 chunks: 9 taps x NKC k-steps, k order (r, s, c)
-  for (int c0 = 0; c0 < E3; c0 += 32) {
-    fh8 a[PD];
-#pragma unroll
-    for (int s = 0; s < PD; ++s)
-      if (s < NS3) a[s] = ld_g(w3 + (s * E3 + c0) * 16 + arow);
+  for (int c0 = 0; c0 < p.E3; c0 += 32) {  // expand3x3 chunks
     ff16 acc[2];
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[f][e] = 0.0f;
-    // B fragments one step ahead, A PD steps ahead; the barrier keeps every step's loads in it
-    // (unpinned, the scheduler hoists all 2 x NS3 LDS reads and spills)
-    auto boff = [&](int s) __attribute__((always_inline)) {
-      const int tap = s / NKC, cs = s - tap * NKC;
-      return ((tap / 3) * W2 + tap % 3) * PS + 16 * cs;
-    };
-    fh8 bn0 = ld_s(halo + hb[0] + boff(0)), bn1 = ld_s(halo + hb[1] + boff(0));
-#pragma unroll
-    for (int s = 0; s < NS3; ++s) {
-      const fh8 cur = a[s % PD], b0 = bn0, b1 = bn1;
-      if (s + PD < NS3) a[s % PD] = ld_g(w3 + ((s + PD) * E3 + c0) * 16 + arow);
-      if (s + 1 < NS3) {
-        bn0 = ld_s(halo + hb[0] + boff(s + 1));
-        bn1 = ld_s(halo + hb[1] + boff(s + 1));
-      }
-      acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur, b0, acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur, b1, acc[1], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    feed(acc, p.b3, c0, E1 + c0);
+    ff_e3_chunk<NKC, 2, PS>(acc, static_cast<const _Float16*>(p.w3), p.E3, c0, arow, halo, hb, W2);
+    feed(acc, p.b3, c0, p.E1 + c0);
   }
+  ff_store_squeeze<MSF, 2>(sacc, p, static_cast<_Float16*>(p.y) + (long long)img * p.y_nstride, yo, pok, h);
+}
 
-  // squeeze epilogue: bias + Relu + one rounding; element 8g + e of lane half h = channel
-  // 32 i + 16 g + 8 h + e, one 16-B store per (fragment, g)
-  _Float16* __restrict__ y = static_cast<_Float16*>(p.y) + (long long)img * p.y_nstride;
+// The pooled variant: Concat(e1, e3) -> 3x3 / stride-2 MaxPool -> squeeze.  One workgroup = a band
+// of PR pooled rows of one image; it computes the conv rows that band's windows read (2 PR + 1,
+// one row shared with the next band) as up to 4 waves x F fragments of 32 conv pixels.  Per 32-channel
+// chunk every wave writes its conv values (bias, Relu, f16 -- what the separate conv stores) to an
+// LDS conv tile [pixel][32 channels] (80-B rows); after a barrier each wave with pooled pixels takes
+// one fragment of them (lane = pooled pixel), forms its 3x3 max in f32 from -FLT_MAX with the
+// window's outside taps read as 0 (maxpool_nhwc_kernel's arithmetic: the separate pool's result bit
+// for bit) and feeds it to the squeeze's two k-steps of the chunk; a second barrier frees the tile.
+template <int NKC, int MSF, int F>
+__global__ __launch_bounds__(256, 2) void fire_pool_f16_kernel(FireF16Params p) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+  constexpr int C = 16 * NKC, PS = C + 8, TS = 40;  // halo / conv tile pixel strides (halves)
+  const int lane = threadIdx.x & 63, lr = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H = p.H, W = p.W, W2 = W + 2, Wp = p.Wp;
+  const int nbands = (p.Hp + p.PR - 1) / p.PR;
+  const int img = blockIdx.x / nbands, band = blockIdx.x - img * nbands;
+  const int pr0 = band * p.PR, npr = min(p.PR, p.Hp - pr0);
+  const int cr0 = max(0, 2 * pr0 - p.ppt), cr1 = min(H - 1, 2 * (pr0 + npr - 1) - p.ppt + 2);
+  const int ncp = (cr1 - cr0 + 1) * W;  // conv pixels of the band
+  const int crmax = min(H, 2 * p.PR + 1);
+  _Float16* halo = smem;
+  _Float16* tile = smem + ((crmax + 2) * W2 * PS + 7) / 8 * 8;
+  ff_stage_halo<NKC, PS>(halo, static_cast<const _Float16*>(p.x) + (long long)img * p.x_nstride, p.x_cs, H, W, cr0 - 1,
+                         cr1 - cr0 + 3);
+
+  // conv pixels of this wave: fragments F wave .. F wave + F - 1 (a wave with none of the band's
+  // pixels skips the expand MFMAs: a short last band costs its live waves only); halo offset of
+  // tap (0, 0) and conv-tile offset
+  const bool clive = wave * F * 32 < ncp;
+  int hb[F], tj[F];
+  bool cok[F];
 #pragma unroll
-  for (int i = 0; i < MSF; ++i)
+  for (int f = 0; f < F; ++f) {
+    const int j = (wave * F + f) * 32 + lr;
+    cok[f] = j < ncp;
+    const int jj = cok[f] ? j : 0;
+    const int rr = jj / W, cc = jj - rr * W;
+    hb[f] = (rr * W2 + cc) * PS + 8 * h;
+    tj[f] = jj * TS + 8 * h;
+  }
+  // the pooled pixel of this lane (waves with 32 w < P pooled pixels take part in the squeeze)
+  const int P = npr * Wp;
+  const bool wact = wave * 32 < P;
+  const int k = wave * 32 + lr;
+  bool pok[1] = {k < P};
+  const int kk = pok[0] ? k : 0;
+  const int pa = pr0 + kk / Wp, pb = kk - (kk / Wp) * Wp;
+  const int ih0 = 2 * pa - p.ppt, iw0 = 2 * pb - p.ppl;
+  int yo[1] = {(pa * Wp + pb) * p.y_cs + 8 * h};
+  const int ctr = (W2 + 1) * PS;
+  const _Float16* __restrict__ ws = static_cast<const _Float16*>(p.ws);
+  const int arow = lr * 16 + 8 * h;
+  ff16 sacc[MSF][1];
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      const int ch = 32 * i + 16 * g + 8 * h;
-      if (ch >= p.Ms) continue;
-      const float4 u0 = *reinterpret_cast<const float4*>(p.bs + ch);
-      const float4 u1 = *reinterpret_cast<const float4*>(p.bs + ch + 4);
-      const float bv[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+  for (int i = 0; i < MSF; ++i) ff_zero(sacc[i]);
+  __syncthreads();  // halo
+
+  auto pool_feed = [&](const ff16 (&acc)[F], const float* __restrict__ bias, int c0, int cat0) __attribute__((always_inline)) {
+    float bv[16];
+    ff_bias16(bv, bias, c0, h);
 #pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        if (!pok[f]) continue;
+    for (int f = 0; f < F; ++f) {
+      if (!cok[f]) continue;
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
         fh8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (_Float16)fmaxf(sacc[i][f][8 * g + e] + bv[e], 0.0f);
-        *reinterpret_cast<fh8*>(y + yo[f] + 32 * i + 16 * g) = o;
+        for (int e = 0; e < 8; ++e) o[e] = (_Float16)fmaxf(acc[f][8 * g + e] + bv[8 * g + e], 0.0f);
+        *reinterpret_cast<fh8*>(tile + tj[f] + 16 * g) = o;
       }
     }
+    __syncthreads();  // conv tile of the chunk complete
+    if (wact) {
+      fh8 aq[2][MSF];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < MSF; ++i) aq[t][i] = ld_g(ws + ((cat0 / 16 + t) * p.Msp + 32 * i) * 16 + arow);
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        float m[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = -FLT_MAX;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int s = 0; s < 3; ++s) {
+            const int ih = ih0 + r, iw = iw0 + s;
+            fh8 v = {};
+            if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+              v = ld_s(tile + ((ih - cr0) * W + iw) * TS + 16 * g + 8 * h);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], (float)v[e]);
+          }
+        fh8 bq;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bq[e] = (_Float16)m[e];
+#pragma unroll
+        for (int i = 0; i < MSF; ++i) sacc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aq[g][i], bq, sacc[i][0], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // the tile is free for the next chunk
+  };
+
+  for (int c0 = 0; c0 < p.E1; c0 += 32) {
+    ff16 acc[F];
+    if (clive) ff_e1_chunk<NKC, F>(acc, static_cast<const _Float16*>(p.w1), p.E1, c0, arow, halo, hb, ctr);
+    pool_feed(acc, p.b1, c0, c0);
+  }
+  for (int c0 = 0; c0 < p.E3; c0 += 32) {
+    ff16 acc[F];
+    if (clive) ff_e3_chunk<NKC, F, PS>(acc, static_cast<const _Float16*>(p.w3), p.E3, c0, arow, halo, hb, W2);
+    pool_feed(acc, p.b3, c0, p.E1 + c0);
+  }
+  if (wact) ff_store_squeeze<MSF, 1>(sacc, p, static_cast<_Float16*>(p.y) + (long long)img * p.y_nstride, yo, pok, h);
 }
 
 // W [M][C][kh][kw] f32 (kh = kw = 1 or 3) -> [K / 16][Mp][16] f16, k = (r, s, c), rows of every
@@ -230,18 +380,75 @@ __global__ __launch_bounds__(256) void fire_pack_f16_kernel(const float* __restr
 
 int fire_f16_lds_bytes(int C, int H, int W) { return ff_halo_rows(H, W) * (W + 2) * (C + 8) * 2; }
 
+static int fire_pool_lds_bytes(int C, int H, int W, int PR) {
+  const int crmax = std::min(H, 2 * PR + 1);
+  return ((crmax + 2) * (W + 2) * (C + 8) + 7) / 8 * 8 * 2 + crmax * W * 40 * 2;
+}
+
+bool fire_pool_f16_plan(FireF16Params* p) {
+  // per F (conv fragments per wave): the largest band whose conv rows fit 128 F pixels, whose pooled
+  // pixels fit the 4 waves' squeeze fragments and whose halo + conv tile fit the LDS budget; the
+  // shape computing the fewest 32-pixel conv fragments (+ 4 per band: staging, barriers) wins
+  // (ORE_FIRE_POOL_SHAPE=F,PR forces one: experiments)
+  long long best = -1;
+  for (int F = 2; F <= 4; ++F) {
+    int PR = 0;
+    for (int r = 1; r <= p->Hp; ++r) {
+      if ((2 * r + 1) * p->W > 128 * F || r * p->Wp > 128 || fire_pool_lds_bytes(p->C, p->H, p->W, r) > FIRE_F16_LDS_MAX) break;
+      PR = r;
+    }
+    if (PR == 0) continue;
+    long long cost = 0;
+    for (int pr0 = 0; pr0 < p->Hp; pr0 += PR) {
+      const int npr = std::min(PR, p->Hp - pr0);
+      const int cr0 = std::max(0, 2 * pr0 - p->ppt), cr1 = std::min(p->H - 1, 2 * (pr0 + npr - 1) - p->ppt + 2);
+      cost += ((cr1 - cr0 + 1) * p->W + 32 * F - 1) / (32 * F) * F + 4;  // live waves x F fragments
+    }
+    if (best < 0 || cost < best) {
+      best = cost;
+      p->F = F;
+      p->PR = PR;
+    }
+  }
+  if (const char* e = getenv("ORE_FIRE_POOL_SHAPE")) {
+    int f = 0, r = 0;
+    if (sscanf(e, "%d,%d", &f, &r) == 2 && f >= 2 && f <= 4 && r >= 1 && (2 * r + 1) * p->W <= 128 * f &&
+        r * p->Wp <= 128 && fire_pool_lds_bytes(p->C, p->H, p->W, r) <= FIRE_F16_LDS_MAX) {
+      p->F = f;
+      p->PR = r;
+    }
+  }
+  return best > 0;
+}
+
 bool fire_f16_eligible(const FireF16Params& p) {
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-  return p.C % 16 == 0 && p.C >= 16 && p.C <= 64 && p.E1 % 32 == 0 && p.E3 % 32 == 0 && p.E1 > 0 && p.E3 > 0 &&
-         p.Ms % 8 == 0 && p.Ms > 0 && p.Ms <= 64 && p.Msp == (p.Ms + 31) / 32 * 32 && p.x_cs % 8 == 0 &&
-         p.y_cs % 8 == 0 && p.x_cs >= p.C && p.y_cs >= p.Ms && p.x_nstride % 8 == 0 && p.y_nstride % 8 == 0 &&
-         al16(p.x) && al16(p.y) && al16(p.w1) && al16(p.w3) && al16(p.ws) && al16(p.b1) && al16(p.b3) && al16(p.bs) &&
-         p.H > 0 && p.W > 0 && p.N > 0 && fire_f16_lds_bytes(p.C, p.H, p.W) <= FIRE_F16_LDS_MAX &&
-         (long long)p.H * p.W * p.x_cs < (1LL << 30) && (long long)p.H * p.W * p.y_cs < (1LL << 30);
+  const bool common = p.C % 16 == 0 && p.C >= 16 && p.C <= 64 && p.E1 % 32 == 0 && p.E3 % 32 == 0 && p.E1 > 0 &&
+                      p.E3 > 0 && p.Ms % 8 == 0 && p.Ms > 0 && p.Ms <= 64 && p.Msp == (p.Ms + 31) / 32 * 32 &&
+                      p.x_cs % 8 == 0 && p.y_cs % 8 == 0 && p.x_cs >= p.C && p.y_cs >= p.Ms && p.x_nstride % 8 == 0 &&
+                      p.y_nstride % 8 == 0 && al16(p.x) && al16(p.y) && al16(p.w1) && al16(p.w3) && al16(p.ws) &&
+                      al16(p.b1) && al16(p.b3) && al16(p.bs) && p.H > 0 && p.W > 0 && p.N > 0 &&
+                      (long long)p.H * p.W * p.x_cs < (1LL << 30) && (long long)p.H * p.W * p.y_cs < (1LL << 30);
+  if (!common) return false;
+  if (!p.pool) return fire_f16_lds_bytes(p.C, p.H, p.W) <= FIRE_F16_LDS_MAX;
+  // pooled: 3x3 / stride 2, every window inside the padded plane and touching the image
+  return p.F >= 2 && p.F <= 4 && p.PR >= 1 && p.Hp > 0 && p.Wp > 0 && p.ppt >= 0 && p.ppl >= 0 && p.ppt <= 2 &&
+         p.ppl <= 2 && 2 * (p.Hp - 1) - p.ppt < p.H && 2 * (p.Wp - 1) - p.ppl < p.W && p.PR * p.Wp <= 128 &&
+         (2 * p.PR + 1) * p.W <= 128 * p.F && fire_pool_lds_bytes(p.C, p.H, p.W, p.PR) <= FIRE_F16_LDS_MAX;
 }
 
 template <int NKC, int MSF>
 static void launch_ff(FireF16Params p, hipStream_t s) {
+  if (p.pool) {
+    const unsigned lds = (unsigned)fire_pool_lds_bytes(p.C, p.H, p.W, p.PR);
+    const dim3 grid((unsigned)(p.N * ((p.Hp + p.PR - 1) / p.PR)));
+    switch (p.F) {
+      case 2: hipLaunchKernelGGL((fire_pool_f16_kernel<NKC, MSF, 2>), grid, dim3(256), lds, s, p); break;
+      case 3: hipLaunchKernelGGL((fire_pool_f16_kernel<NKC, MSF, 3>), grid, dim3(256), lds, s, p); break;
+      default: hipLaunchKernelGGL((fire_pool_f16_kernel<NKC, MSF, 4>), grid, dim3(256), lds, s, p); break;
+    }
+    return;
+  }
   p.tiles_per_img = (p.H * p.W + FF_PIX - 1) / FF_PIX;
   const unsigned lds = (unsigned)fire_f16_lds_bytes(p.C, p.H, p.W);
   hipLaunchKernelGGL((fire_f16_kernel<NKC, MSF>), dim3((unsigned)(p.N * p.tiles_per_img)), dim3(256), lds, s, p);

@@ -123,11 +123,12 @@ ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t 
                     int64_t E3, const float* ws, int64_t Msp, const float* bs, int64_t Ms, float* y, int64_t y_nstride,
                     int64_t y_ps, bool wino = false);
 // the f16 fused fire module (ore_fire_f16.hip): x = S, y = S' NHWC f16 (pixel strides x_cs / y_cs,
-// image strides in elements); w1 / w3 / ws in launch_fire_pack_f16 layout
+// image strides in elements); w1 / w3 / ws in launch_fire_pack_f16 layout; pool: a 3x3 / stride-2
+// MaxPool (window over the H x W conv plane) between the Concat and the squeeze, y on its plane
 ore_status run_fire_f16(ore_ctx* ctx, const void* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
                         int64_t x_cs, const void* w1, const float* b1, int64_t E1, const void* w3, const float* b3,
                         int64_t E3, const void* ws, const float* bs, int64_t Ms, void* y, int64_t y_nstride,
-                        int64_t y_cs);
+                        int64_t y_cs, const Window* pool = nullptr);
 // pooled-epilogue tiling of a conv output (Ho x Wo) and its pool (3x3 / stride 2 only): *tr x *tc
 // tiles of 6 x 9 pooled outputs per image; returns the work factor tiles * CONV_EPOOL_BN / (Ho * Wo)
 // (the conv columns computed, recomputed overlap and padding included), 0 for other pools

@@ -134,9 +134,16 @@ struct FireF16Params {
   int x_cs, y_cs;
   long long x_nstride, y_nstride;
   int tiles_per_img;  // filled by the launcher
+  // pool = 1: a 3x3 / stride-2 MaxPool (pads ppt / ppl, output Hp x Wp) sits between the Concat and
+  // the squeeze (SqueezeNet fire4 -> pool3 -> fire5, fire8 -> pool5 -> fire9); y is then the squeeze
+  // output on the pooled plane.  PR pooled rows per workgroup, F conv fragments per wave
+  // (fire_pool_f16_plan)
+  int pool, Hp, Wp, ppt, ppl, PR, F;
 };
 constexpr int FIRE_F16_LDS_MAX = 80 * 1024;  // the input halo of one workgroup (two per CU)
 int fire_f16_lds_bytes(int C, int H, int W);
+// pooled variant: picks p->F / p->PR (false: no band shape fits the LDS budget)
+bool fire_pool_f16_plan(FireF16Params* p);
 bool fire_f16_eligible(const FireF16Params& p);
 void launch_fire_f16(const FireF16Params& p, hipStream_t s);
 // W [M][C][kk] f32 (kk = 1 or 9) -> [C kk / 16][roundup(M, 32)][16] f16 with permuted rows

@@ -96,6 +96,9 @@ struct Step {
   bool fire_wino = false;          // the e3 by Winograd (fire_wino_kernel; fire_w3 in launch_fire_pack_wino layout)
   bool fire_f16 = false;           // f16 model: fire_f16_kernel, fire_w1 / fire_w3 / fire_ws16 in launch_fire_pack_f16 layout
   const void* fire_ws16 = nullptr;
+  bool fire_pool = false;          // f16: a 3x3 / stride-2 MaxPool between the Concat and this squeeze
+  int64_t fire_H = 0, fire_W = 0;  //   (fire_pool_f16_kernel): the expands' plane and the pool window
+  Window fire_pwin;
   ConvPlan plan{};        // kernel choice and weight layout for S_CONV / S_MATMUL
   float* wp = nullptr;    // packed weights (layout per plan) for S_CONV / S_MATMUL
   const int2* ktab = nullptr;  // gather table (follows wp in the packed allocation; gather kernel only)
@@ -768,17 +771,36 @@ ore_status plan(ore_model* m) {
   // (1e) f16 models: the same fire module + next squeeze pattern in one fire_f16_kernel launch
   // (ore_fire_f16.hip): expand1x1 / expand3x3 (+ Relu) on 16-B NHWC gathers, C % 16 == 0 and <= 64,
   // expands in 32-channel chunks, the squeeze <= 64 channels; bit-identical to the three
-  // conv_f16_kernel launches
+  // conv_f16_kernel launches.  With a 3x3 / stride-2 MaxPool between the Concat and the squeeze
+  // (SqueezeNet fire4 -> pool3 -> fire5, fire8 -> pool5 -> fire9) the pooled kernel takes all four
+  // steps (bit-identical to the three convs + maxpool_nhwc_kernel)
   if ((m->fusion & ORE_FUSE_FIRE) && m->f16 && (m->fusion & ORE_FUSE_CONV_RELU)) {
+    // the pooled form (fire_pool_f16_kernel) also needs ORE_FUSE_CONV_POOL; ORE_FIRE_POOL=0 turns it off
+    const char* efp = getenv("ORE_FIRE_POOL");
+    const bool fire_pool = (m->fusion & ORE_FUSE_CONV_POOL) && !(efp && atoi(efp) == 0);
     for (size_t i = 0; i < m->steps.size(); ++i) {
       Step& cc = m->steps[i];
       if (cc.kind != S_CONCAT || cc.axis != 1 || cc.in0 < 0 || cc.in1 < 0 || cc.in0 == cc.in1) continue;
       const int pa = producer[cc.in0], pb = producer[cc.in1];
       if (pa < 0 || pb < 0) continue;
-      int qi = -1;
-      for (size_t j = i + 1; j < m->steps.size(); ++j)
-        if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == cc.out || m->steps[j].in1 == cc.out)) { qi = int(j); break; }
+      auto consumer = [&](int v, size_t from) {
+        for (size_t j = from; j < m->steps.size(); ++j)
+          if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == v || m->steps[j].in1 == v)) return int(j);
+        return -1;
+      };
+      int qi = consumer(cc.out, i + 1), pi = -1;
       if (qi < 0) continue;
+      // pooled form: Concat -> 3x3 / stride-2 MaxPool (read once) -> squeeze
+      if (m->steps[qi].kind == S_MAXPOOL) {
+        const Step& pl = m->steps[qi];
+        if (!fire_pool || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2 || pl.in0 != cc.out) continue;
+        const Value& pv = m->values[pl.out];
+        if (pv.uses != 1 || pv.is_output) continue;
+        pi = qi;
+        qi = consumer(pl.out, size_t(pi) + 1);
+        if (qi < 0) continue;
+      }
+      const int qin = pi >= 0 ? m->steps[pi].out : cc.out;
       Step &e1 = m->steps[pa], &e3 = m->steps[pb], &q = m->steps[qi];
       auto vec16 = [](const Step& s) {
         return s.kind == S_CONV && s.relu && !s.pool && !s.epool && s.plan.f16 && s.plan.xmode == F16_X_NHWC_VEC &&
@@ -786,9 +808,19 @@ ore_status plan(ore_model* m) {
       };
       auto is1x1 = [&](const Step& s) { return vec16(s) && s.kh == 1 && s.kw == 1 && s.win.pt == 0 && s.win.pl == 0; };
       const bool e3ok = vec16(e3) && e3.kh == 3 && e3.kw == 3 && e3.win.pt == 1 && e3.win.pl == 1;
-      if (!is1x1(e1) || !e3ok || !is1x1(q) || q.in0 != cc.out || e1.in0 != e3.in0 || e1.H != e3.H || e1.W != e3.W) continue;
+      if (!is1x1(e1) || !e3ok || !is1x1(q) || q.in0 != qin || e1.in0 != e3.in0 || e1.H != e3.H || e1.W != e3.W) continue;
       if (e1.C % 16 || e1.C > 64 || e1.M % 32 || e3.M % 32 || q.M % 8 || q.M > 64 || q.C != e1.M + e3.M) continue;
-      if (fire_f16_lds_bytes(int(e1.C), int(e1.H), int(e1.W)) > FIRE_F16_LDS_MAX || q.in2 < 0 || e1.in2 < 0 || e3.in2 < 0) continue;
+      if (q.in2 < 0 || e1.in2 < 0 || e3.in2 < 0) continue;
+      if (pi < 0 && fire_f16_lds_bytes(int(e1.C), int(e1.H), int(e1.W)) > FIRE_F16_LDS_MAX) continue;
+      if (pi >= 0) {  // a band shape must fit (fire_pool_f16_plan) and every window touch the image
+        const Step& pl = m->steps[pi];
+        FireF16Params fp{};
+        fp.C = int(e1.C); fp.H = int(e1.H); fp.W = int(e1.W);
+        fp.Hp = int(pl.win.Ho); fp.Wp = int(pl.win.Wo); fp.ppt = int(pl.win.pt); fp.ppl = int(pl.win.pl);
+        if (pl.H != e1.H || pl.W != e1.W || !fire_pool_f16_plan(&fp) || pl.win.pt > 2 || pl.win.pl > 2 ||
+            2 * (fp.Hp - 1) - fp.ppt >= fp.H || 2 * (fp.Wp - 1) - fp.ppl >= fp.W)
+          continue;
+      }
       const Value &va = m->values[cc.in0], &vb = m->values[cc.in1], &vc = m->values[cc.out], &vs = m->values[e1.in0];
       if (va.uses != 1 || vb.uses != 1 || vc.uses != 1 || va.is_output || vb.is_output || vc.is_output || vs.es != 2) continue;
       // the three weight packings (made once per model; keys 2000000 + expand index, 3000000 + squeeze index)
@@ -810,6 +842,16 @@ ore_status plan(ore_model* m) {
         return err(m, ORE_ERR_HIP, "f16 fire weight packing failed");
       q.kind = S_FIRE;
       q.fire_f16 = true;
+      q.fire_pool = pi >= 0;
+      q.fire_H = e1.H;
+      q.fire_W = e1.W;
+      if (pi >= 0) {
+        Step& pl = m->steps[pi];
+        q.fire_pwin = pl.win;
+        m->values[pl.out].elided = true;
+        pl.kind = S_NOP;
+        pl.in0 = -1;
+      }
       q.in0 = e1.in0;
       q.fire_C = e1.C;
       q.fire_E1 = e1.M;
@@ -821,7 +863,7 @@ ore_status plan(ore_model* m) {
       q.fire_b3 = m->values[e3.in2].cptr;
       q.flops_per_img += e1.flops_per_img + e3.flops_per_img;
       q.bytes_per_img = 2.0 * double(e1.C * e1.H * e1.W) + 2.0 * double(q.M * q.H * q.W);
-      q.name = e1.name.substr(0, e1.name.find('/')) + "+" + q.name;
+      q.name = e1.name.substr(0, e1.name.find('/')) + (pi >= 0 ? "+pool+" : "+") + q.name;
       m->values[cc.in0].elided = m->values[cc.in1].elided = m->values[cc.out].elided = true;
       e1.kind = e3.kind = cc.kind = S_NOP;
       e1.in0 = e3.in0 = cc.in0 = cc.in1 = -1;
@@ -1135,9 +1177,10 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
     case S_FIRE: {
       const Ref x = ref_of(m, s.in0);
       if (s.fire_f16)
-        return run_fire_f16(ctx, x.p, n, s.fire_C, s.H, s.W, x.nstride, x.ps ? x.ps : s.fire_C, s.fire_w1, s.fire_b1,
-                            s.fire_E1, s.fire_w3, s.fire_b3, s.fire_E3, s.fire_ws16, m->values[s.in2].cptr, s.M, y.p,
-                            y.nstride, y.ps ? y.ps : s.M);
+        return run_fire_f16(ctx, x.p, n, s.fire_C, s.fire_pool ? s.fire_H : s.H, s.fire_pool ? s.fire_W : s.W,
+                            x.nstride, x.ps ? x.ps : s.fire_C, s.fire_w1, s.fire_b1, s.fire_E1, s.fire_w3, s.fire_b3,
+                            s.fire_E3, s.fire_ws16, m->values[s.in2].cptr, s.M, y.p, y.nstride, y.ps ? y.ps : s.M,
+                            s.fire_pool ? &s.fire_pwin : nullptr);
       ctx->mapped_lo = m->arena_alloc;  // the arena and its 4 KiB lead are mapped
       ctx->mapped_hi = m->arena ? m->arena + m->arena_bytes : nullptr;
       const ore_status st = run_fire(ctx, x.p, n, s.fire_C, s.H, s.W, x.nstride, x.ps ? x.ps : s.H * s.W, s.fire_w1,

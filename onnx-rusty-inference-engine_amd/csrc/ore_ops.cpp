@@ -249,7 +249,7 @@ ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t 
 ore_status run_fire_f16(ore_ctx* ctx, const void* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
                         int64_t x_cs, const void* w1, const float* b1, int64_t E1, const void* w3, const float* b3,
                         int64_t E3, const void* ws, const float* bs, int64_t Ms, void* y, int64_t y_nstride,
-                        int64_t y_cs) {
+                        int64_t y_cs, const Window* pool) {
   if (N == 0) return ORE_OK;
   if (!fits_i32(N) || !fits_i32(H * W) || !fits_i32(x_cs) || !fits_i32(y_cs))
     return set_error(ctx, ORE_ERR_INVALID, "fire geometry exceeds 32-bit indexing");
@@ -259,6 +259,11 @@ ore_status run_fire_f16(ore_ctx* ctx, const void* x, int64_t N, int64_t C, int64
   p.E1 = int(E1); p.E3 = int(E3); p.Ms = int(Ms); p.Msp = int((Ms + 31) / 32 * 32);
   p.x_cs = int(x_cs); p.y_cs = int(y_cs);
   p.x_nstride = x_nstride; p.y_nstride = y_nstride;
+  if (pool) {
+    p.pool = 1;
+    p.Hp = int(pool->Ho); p.Wp = int(pool->Wo); p.ppt = int(pool->pt); p.ppl = int(pool->pl);
+    if (!fire_pool_f16_plan(&p)) return set_error(ctx, ORE_ERR_INVALID, "internal: no band shape for the pooled f16 fire module");
+  }
   if (!fire_f16_eligible(p)) return set_error(ctx, ORE_ERR_INVALID, "internal: f16 fire module on an unsupported layout");
   launch_fire_f16(p, ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());

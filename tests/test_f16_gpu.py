@@ -213,10 +213,10 @@ def test_f16_dma_kernel_bit_identical(gpu_ctx, cfg, monkeypatch):
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
 
 
-def _fire_model_f16(C, H, W, S1, E1, E3, S2, ints=False, seed=0):
-    """squeeze (C -> S1) -> expand 1x1 (E1) / 3x3 pad 1 (E3) -> Concat -> squeeze (S2) -> GAP, all
-    Relu; ints: sparse {-1, 0, 1} weights and small integer biases (every value exact in f16).
-    Returns (model bytes, {name: (w, b)})."""
+def _fire_model_f16(C, H, W, S1, E1, E3, S2, ints=False, seed=0, pool=None):
+    """squeeze (C -> S1) -> expand 1x1 (E1) / 3x3 pad 1 (E3) -> Concat [-> 3x3 / stride-2 MaxPool with
+    pads `pool`] -> squeeze (S2) -> GAP, all Relu; ints: sparse {-1, 0, 1} weights and small integer
+    biases (every value exact in f16).  Returns (model bytes, {name: (w, b)})."""
     from ore import onnx_wire as wr
     rng = np.random.default_rng(seed + C * 7 + H + W + S1 + E1 + E3 + S2)
     shapes = {"wq": (S1, C, 1, 1), "w1": (E1, S1, 1, 1), "w3": (E3, S1, 3, 3), "wn": (S2, E1 + E3, 1, 1)}
@@ -236,9 +236,13 @@ def _fire_model_f16(C, H, W, S1, E1, E3, S2, ints=False, seed=0):
     nodes = [conv("x", "wq", "q", [0] * 4), wr.encode_node("Relu", ["q"], ["qr"]),
              conv("qr", "w1", "e1", [0] * 4), wr.encode_node("Relu", ["e1"], ["e1r"]),
              conv("qr", "w3", "e3", [1] * 4), wr.encode_node("Relu", ["e3"], ["e3r"]),
-             wr.encode_node("Concat", ["e1r", "e3r"], ["cat"], attrs=[wr.encode_attr_int("axis", 1)]),
-             conv("cat", "wn", "n", [0] * 4), wr.encode_node("Relu", ["n"], ["nr"]),
-             wr.encode_node("GlobalAveragePool", ["nr"], ["y"])]
+             wr.encode_node("Concat", ["e1r", "e3r"], ["cat"], attrs=[wr.encode_attr_int("axis", 1)])]
+    if pool is not None:
+        nodes.append(wr.encode_node("MaxPool", ["cat"], ["pc"], attrs=[
+            wr.encode_attr_ints("kernel_shape", [3, 3]), wr.encode_attr_ints("strides", [2, 2]),
+            wr.encode_attr_string("auto_pad", "NOTSET"), wr.encode_attr_ints("pads", pool)]))
+    nodes += [conv("pc" if pool is not None else "cat", "wn", "n", [0] * 4), wr.encode_node("Relu", ["n"], ["nr"]),
+              wr.encode_node("GlobalAveragePool", ["nr"], ["y"])]
     return wr.encode_model("fire", nodes, inits, vinfo, [wr.encode_value_info("y", (1, S2, 1, 1))]), params
 
 
@@ -301,8 +305,9 @@ def test_f16_fire_fusion_exact_integers(gpu_ctx, case):
 
 
 def test_f16_squeezenet_fire_fusion(gpu_ctx):
-    """SqueezeNet-1.0 @224, f16: the five fire + squeeze pairs run fire_f16_kernel (fire4 / fire8 feed
-    a MaxPool, fire9 conv10) and the probabilities equal the unfused graph's bit for bit."""
+    """SqueezeNet-1.0 @224, f16: the five fire + squeeze pairs run fire_f16_kernel, fire4 / fire8 with
+    their MaxPool and the next squeeze fire_pool_f16_kernel (fire9 feeds conv10: unfused), and the
+    probabilities equal the unfused graph's bit for bit."""
     import ore
     from ore import squeezenet
     mb = squeezenet.build(224)
@@ -313,6 +318,64 @@ def test_f16_squeezenet_fire_fusion(gpu_ctx):
         m.set_fusion(fusion)
         outs.append(_np(m.run(x)))
         n = sum(1 for t in m.tiles() if t >= 0 and ore.Model.TILE_NAMES[t] == "fire f16")
-        assert n == (5 if fusion & ore.FUSE_FIRE else 0)
+        assert n == (7 if fusion & ore.FUSE_FIRE else 0)  # + fire4 -> pool3 -> fire5, fire8 -> pool5 -> fire9
         m.close()
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+FIRE_POOL_F16_CASES = [
+    # C, H, W, S1, E1, E3, S2, pool pads
+    (16, 54, 54, 32, 128, 128, 32, [0, 0, 1, 1]),   # SqueezeNet fire4 -> pool3 -> fire5
+    (32, 27, 27, 64, 256, 256, 64, [0, 0, 1, 1]),   # fire8 -> pool5 -> fire9
+    (8, 13, 15, 16, 64, 96, 48, [1, 1, 1, 1]),      # padded on all sides, unequal expands, 48 squeeze rows
+    (8, 9, 8, 48, 32, 64, 16, [0, 0, 0, 0]),        # floor-mode pool, C = 48
+    (8, 38, 33, 32, 64, 64, 24, [0, 0, 1, 1]),      # 4 bands of 5 pooled rows, the last 4
+]
+
+
+@pytest.mark.parametrize("case", FIRE_POOL_F16_CASES)
+def test_f16_fire_pool_fusion_bit_identical(gpu_ctx, case):
+    """f16: expand 1x1 + expand 3x3 + Concat + MaxPool + the next squeeze in one fire_pool_f16_kernel
+    launch equals the separate kernels bit for bit; neither the concat nor the pooled map is stored."""
+    import ore
+    C, H, W = case[:3]
+    mb, _ = _fire_model_f16(*case[:7], pool=case[7])
+    x = np.random.default_rng(sum(case[:7])).standard_normal((3, C, H, W)).astype(np.float32)
+    vals = []
+    for fusion in (ore.FUSE_ALL | ore.KEEP_VALUES, (ore.FUSE_ALL & ~ore.FUSE_FIRE) | ore.KEEP_VALUES):
+        m = ore.Model(gpu_ctx, mb, max_batch=3, precision="f16")
+        m.set_fusion(fusion)
+        y = _np(m.run(_t(x)))
+        vals.append((y, m.read_value("nr")))
+        names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+        assert ("fire f16" in names) == bool(fusion & ore.FUSE_FIRE)
+        if fusion & ore.FUSE_FIRE:
+            for v in ("cat", "pc"):
+                with pytest.raises(ore.OreError):
+                    m.read_value(v)  # never materialised
+        m.close()
+    np.testing.assert_array_equal(vals[0][1], vals[1][1])
+    np.testing.assert_array_equal(vals[0][0], vals[1][0])
+    assert np.abs(vals[0][1]).max() > 0
+
+
+@pytest.mark.parametrize("case", [FIRE_POOL_F16_CASES[0], FIRE_POOL_F16_CASES[2]])
+def test_f16_fire_pool_fusion_exact_integers(gpu_ctx, case):
+    """Small-integer data: the pooled fused kernel equals the f32 oracle (conv, Relu, Concat, the
+    reference's MaxPool, conv) bit for bit."""
+    import ore
+    C, H, W, S1, E1, E3, S2, pads = case
+    mb, prm = _fire_model_f16(*case[:7], ints=True, seed=5, pool=pads)
+    x = _ints(np.random.default_rng(13), -2, 2, (2, C, H, W))
+    m = ore.Model(gpu_ctx, mb, max_batch=2, precision="f16")
+    m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+    _np(m.run(_t(x)))
+    assert "fire f16" in [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+    q = oracle.relu(oracle.conv2d(x, *prm["wq"], pads=[0] * 4, strides=(1, 1)))
+    e1 = oracle.relu(oracle.conv2d(q, *prm["w1"], pads=[0] * 4, strides=(1, 1)))
+    e3 = oracle.relu(oracle.conv2d(q, *prm["w3"], pads=[1] * 4, strides=(1, 1)))
+    pc = oracle.maxpool2d(np.concatenate([e1, e3], 1), (3, 3), (2, 2), auto_pad="NOTSET", pads=pads)
+    n = oracle.relu(oracle.conv2d(pc, *prm["wn"], pads=[0] * 4, strides=(1, 1)))
+    assert np.abs(n).max() < 2048 and np.abs(n).max() > 0
+    np.testing.assert_array_equal(m.read_value("nr"), n)
+    m.close()
