@@ -1142,6 +1142,14 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       const Ref x = ref_of(m, s.in0);
       const float* bias = s.in2 >= 0 ? m->values[s.in2].cptr : nullptr;
       const F16Epool ep{s.ep_kh, s.ep_kw, s.ep_sh, s.ep_sw, s.ep_win};
+      if (s.plan.f16 && s.plan.xmode == F16_X_NHWC_PAIR && s.epool) {  // one launch from the f32 input
+        bool ran = false;
+        const ore_status st = run_conv_pair_pool_f16(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.M, s.kh,
+                                                     s.kw, bias, s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps, ep, &ran);
+        if (ran) s.ran_tile = WINO_TILE_BASE + WINO_TILES_N + 2;  // "first conv pool f16" (ore.Model.TILE_NAMES)
+        if (st != ORE_OK || ran) return st;
+        s.ran_tile = -1;
+      }
       if (s.plan.f16 && (s.plan.xmode == F16_X_NHWC_PAIR || s.plan.xmode == F16_X_NHWC8)) {
         // convert the f32 NCHW input to NHWC f16 (4 / 8 channels per pixel), then gather
         const int cs = s.plan.xmode == F16_X_NHWC8 ? 8 : 4;
@@ -1697,7 +1705,7 @@ int32_t ore_model_step_tile(ore_model* m, int32_t i) {
   if (s.kind == S_FIRE)  // "fire" / "fire wino" / "fire f16": the fused fire kernels (ore.Model.TILE_NAMES)
     return s.fire_f16 ? WINO_TILE_BASE + WINO_TILES_N + 1 : s.fire_wino ? WINO_TILE_BASE + WINO_TILES_N : CONV_TILES_F32;
   if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.plan.epv > 0) return EPOOL_TILE_BASE + s.plan.epv;
-  if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.ran_tile >= 0) return s.ran_tile;
+  if (s.kind == S_CONV && s.epool && s.ran_tile >= 0) return s.ran_tile;
   return (s.kind == S_CONV || s.kind == S_MATMUL) ? s.plan.cfg : -1;
 }
 

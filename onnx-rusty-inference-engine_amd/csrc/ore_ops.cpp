@@ -373,6 +373,46 @@ ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int6
   return ORE_OK;
 }
 
+ore_status run_conv_pair_pool_f16(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H,
+                                  int64_t W, int64_t x_nstride, int64_t x_ps, const void* wp, int64_t M, int64_t kh,
+                                  int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu,
+                                  void* y, int64_t y_nstride, int64_t y_ps, const F16Epool& ep, bool* ran) {
+  *ran = false;
+  if (getenv("ORE_DEBUG_C1")) fprintf(stderr, "c1pool: xmode %d ep %lldx%lld\n", pln.xmode, (long long)ep.kh, (long long)ep.kw);
+  if (const char* e = getenv("ORE_F16_C1POOL"))
+    if (atoi(e) == 0) return ORE_OK;
+  if (N == 0 || !pln.f16 || pln.xmode != F16_X_NHWC_PAIR) return ORE_OK;
+  if (x_ps == 0) x_ps = H * W;
+  if (y_ps == 0) y_ps = M;
+  int tr = 0, tc = 0;
+  if (epool_tile(win.Ho, win.Wo, ep.kh, ep.kw, ep.sh, ep.sw, ep.win, &tr, &tc) == 0.0) return ORE_OK;
+  if (!fits_i32(N * int64_t(tr) * tc) || !fits_i32(C * x_ps) || !fits_i32(y_ps * ep.win.Ho * ep.win.Wo) || x_ps < H * W)
+    return ORE_OK;
+  ConvParams p{};
+  p.x = x; p.wp = static_cast<const float*>(wp); p.bias = bias; p.y = static_cast<float*>(y);
+  p.N = int(N); p.C = int(C); p.H = int(H); p.W = int(W);
+  p.M = int(M); p.kh = int(kh); p.kw = int(kw); p.sh = int(sh); p.sw = int(sw);
+  p.pt = int(win.pt); p.pl = int(win.pl); p.Ho = int(win.Ho); p.Wo = int(win.Wo);
+  p.K = f16_conv_k(pln.xmode, int(C), int(kh), int(kw));
+  p.x_ps = int(x_ps); p.y_ps = int(y_ps);
+  p.x_nstride = x_nstride; p.y_nstride = y_nstride;
+  p.relu = relu ? 1 : 0;
+  p.Mp = pln.Mp;
+  p.ep_pt = int(ep.win.pt); p.ep_pl = int(ep.win.pl); p.ep_Ho = int(ep.win.Ho); p.ep_Wo = int(ep.win.Wo);
+  p.ep_tr = tr; p.ep_tc = tc;
+  if (!conv_pair_pool_f16_eligible(p)) {
+    if (getenv("ORE_DEBUG_C1"))
+      fprintf(stderr, "c1pool ineligible: C %d H %d W %d M %d k %dx%d s %d,%d p %d,%d K %d Mp %d x_ps %d y_ps %d yns %lld y %p wp %p tr %d tc %d\n",
+              p.C, p.H, p.W, p.M, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.K, p.Mp, p.x_ps, p.y_ps, p.y_nstride,
+              static_cast<void*>(p.y), static_cast<const void*>(p.wp), p.ep_tr, p.ep_tc);
+    return ORE_OK;
+  }
+  launch_conv_pair_pool_f16(p, ctx->stream);
+  ORE_HIP_CHECK(ctx, hipGetLastError());
+  *ran = true;
+  return ORE_OK;
+}
+
 ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_t N, int64_t C, int64_t H, int64_t W,
                         int64_t x_nstride, int64_t x_ps, const void* wp, const int2* ktab, int64_t M, int64_t kh,
                         int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, void* y,

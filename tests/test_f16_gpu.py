@@ -379,3 +379,78 @@ def test_f16_fire_pool_fusion_exact_integers(gpu_ctx, case):
     assert np.abs(n).max() < 2048 and np.abs(n).max() > 0
     np.testing.assert_array_equal(m.read_value("nr"), n)
     m.close()
+
+
+C1POOL_CASES = [
+    # N, C, H, W, M, k, stride, pad, pool pads
+    (2, 3, 67, 71, 96, 7, 2, 0, [0, 0, 0, 0]),   # SqueezeNet conv1 + pool1 geometry, partial tiles
+    (3, 1, 40, 33, 64, 7, 2, 0, [0, 0, 1, 1]),   # one channel, ceil-mode pool
+    (2, 4, 29, 30, 40, 3, 2, 2, [1, 1, 1, 1]),   # 3x3 (PAIR padding tap), M % 32 != 0, padded pool
+    (1, 3, 47, 45, 128, 3, 2, 2, [0, 0, 1, 1]),  # 4 channel fragments (3x3: the weights fit LDS)
+]
+
+
+@pytest.mark.parametrize("case", C1POOL_CASES)
+def test_f16_first_conv_pool_fused_bit_identical(gpu_ctx, case, monkeypatch):
+    """f16 first conv (f32 NCHW input, <= 4 channels) + Relu + 3x3/s2 MaxPool: the one-launch kernel
+    (conv_pair_pool_f16_kernel, reads the f32 input itself) equals the two-launch path (NHWC4
+    conversion + conv_f16_kernel with the pooled epilogue) bit for bit."""
+    import ore
+    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "8")  # pooled epilogue at these small planes too
+    N, C, H, W, M, k, st, pd, pp = case
+    rng = np.random.default_rng(sum(case[:8]))
+    x = (rng.standard_normal((N, C, H, W)) * 20).astype(np.float32)
+    w1 = (rng.standard_normal((M, C, k, k)) * np.sqrt(2.0 / (C * k * k))).astype(np.float32)
+    b1 = rng.uniform(-0.1, 0.1, M).astype(np.float32)
+    w2 = (rng.standard_normal((16, M, 1, 1)) * np.sqrt(2.0 / M)).astype(np.float32)
+    mb = _chain_model((1, C, H, W), [(w1, b1, [pd] * 4, [st, st], True), (w2, None, [0] * 4, [1, 1], False)], pool=pp)
+    vals = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("ORE_F16_C1POOL", on)
+        m = ore.Model(gpu_ctx, mb, max_batch=N, precision="f16")
+        m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+        y = _np(m.run(_t(x)))
+        vals.append((y, m.read_value("p0"), m.read_value("c1")))
+        assert ("first conv pool f16" in [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]) == (on == "1")
+        m.close()
+    for a, b in zip(vals[0], vals[1]):
+        np.testing.assert_array_equal(a, b)
+    assert np.abs(vals[0][1]).max() > 0
+
+
+def test_f16_first_conv_pool_exact_integers(gpu_ctx, monkeypatch):
+    """Small integers: the one-launch first conv + pool equals the f32 oracle bit for bit."""
+    import ore
+    monkeypatch.setenv("ORE_F16_C1POOL", "1")
+    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "8")
+    rng = np.random.default_rng(8)
+    x = _ints(rng, -3, 3, (2, 3, 51, 49))
+    w1, b1 = _sparse(rng, (96, 3, 7, 7), 16), _ints(rng, -8, 8, (96,))
+    w2 = _sparse(rng, (8, 96, 1, 1), 8)
+    mb = _chain_model((1, 3, 51, 49), [(w1, b1, [0] * 4, [2, 2], True), (w2, None, [0] * 4, [1, 1], False)],
+                      pool=[0, 0, 1, 1])
+    m = ore.Model(gpu_ctx, mb, max_batch=2, precision="f16")
+    m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+    _np(m.run(_t(x)))
+    assert ore.Model.TILE_NAMES[m.tiles()[0]] == "first conv pool f16"
+    r0 = oracle.relu(oracle.conv2d(x, w1, b1, pads=[0] * 4, strides=(2, 2)))
+    p0 = oracle.maxpool2d(r0, (3, 3), (2, 2), auto_pad="NOTSET", pads=[0, 0, 1, 1])
+    np.testing.assert_array_equal(m.read_value("p0"), p0)
+    m.close()
+
+
+def test_f16_squeezenet_first_conv_pool_fused(gpu_ctx, monkeypatch):
+    """SqueezeNet-1.0 @224 f16: probabilities with the one-launch conv1 + pool1 equal the two-launch
+    path's bit for bit."""
+    import ore
+    from ore import squeezenet
+    mb = squeezenet.build(224)
+    x = _t(squeezenet.synthetic_input(3, 224, seed=23))
+    outs = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("ORE_F16_C1POOL", on)
+        m = ore.Model(gpu_ctx, mb, max_batch=3, precision="f16")
+        outs.append(_np(m.run(x)))
+        assert (ore.Model.TILE_NAMES[m.tiles()[0]] == "first conv pool f16") == (on == "1")
+        m.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
