@@ -54,18 +54,33 @@ __device__ __forceinline__ fh8 ld_g(const _Float16* p) { return *reinterpret_cas
 __device__ __forceinline__ fh8 ld_s(const _Float16* p) { return *reinterpret_cast<const fh8*>(p); }
 
 // Stage input rows hr0 .. hr0 + nrows - 1 (columns -1 .. W, zeros outside the image) of image x into
-// the LDS halo, pixel stride PS halves, 16-B chunks
+// the LDS halo, pixel stride PS halves, 16-B chunks.  Raw buffer loads, 8 per thread in flight: an
+// offset past the image's records reads zeros, so there is no branch around a load (behind one the
+// compiler waits for each load before the next).
 template <int NKC, int PS>
 __device__ __forceinline__ void ff_stage_halo(_Float16* halo, const _Float16* __restrict__ x, int x_cs, int H, int W,
                                               int hr0, int nrows) {
+  constexpr int B = 8;
   const int W2 = W + 2, nck = nrows * W2 * (2 * NKC);
-  for (int i = threadIdx.x; i < nck; i += 256) {
-    const int px = i / (2 * NKC), ck = i - px * (2 * NKC);
-    const int rr = px / W2, cc = px - rr * W2;
-    const int ih = hr0 + rr, iw = cc - 1;
-    fh8 v = {};
-    if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) v = ld_g(x + (ih * W + iw) * x_cs + ck * 8);
-    *reinterpret_cast<fh8*>(halo + px * PS + ck * 8) = v;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(x), (short)0, H * W * x_cs * 2, 0x00020000);
+  for (int i0 = 0; i0 < nck; i0 += 256 * B) {
+    fh8 v[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int i = i0 + 256 * u + (int)threadIdx.x;
+      const int px = i / (2 * NKC), ck = i - px * (2 * NKC);
+      const int rr = px / W2, cc = px - rr * W2;
+      const int ih = hr0 + rr, iw = cc - 1;
+      const bool in = i < nck && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      v[u] = __builtin_bit_cast(fh8, __builtin_amdgcn_raw_buffer_load_b128(
+                                         rs, in ? ((ih * W + iw) * x_cs + ck * 8) * 2 : (int)0x80000000, 0, 0));
+    }
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int i = i0 + 256 * u + (int)threadIdx.x;
+      if (i < nck) *reinterpret_cast<fh8*>(halo + (i / (2 * NKC)) * PS + (i - (i / (2 * NKC)) * (2 * NKC)) * 8) = v[u];
+    }
   }
 }
 
