@@ -909,12 +909,20 @@ static void launch_conv_epool_cfg(const ConvParams& p0, hipStream_t s) {
 
 void launch_conv_epool(const ConvParams& p, hipStream_t s) {
   int v = p.ep_variant;
-  if (const char* e = getenv("ORE_CONV_POOL_STREAM")) v = atoi(e) + 1;  // 0..3 -> patch / walk48 / walk96 / walk64
+  if (const char* e = getenv("ORE_CONV_POOL_STREAM")) v = atoi(e) + 1;  // 0..3 -> patch / walk48 / walk96 / walk64, 6 -> window
   // auto: a walker block owns a whole image (x its m tile), so below ~one block per CU (batch < 128
   // for conv1) the patch kernel's many small tiles fill the chip better
   if (v == 0 && p.N >= 128)
     v = conv_pool_stream_eligible(p, 3) ? 3 : conv_pool_stream_eligible(p, 4) ? 4 : conv_pool_stream_eligible(p, 2) ? 2 : 1;
   if (v == 0) v = 1;
+  if (v == EPOOL_WIN_VARIANT) {
+    if (p.wc1 && conv_win_pool_f32_eligible(p)) {
+      launch_conv_win_pool_f32(p, p.wc1, s);
+      last_conv_tile = EPOOL_WIN_TILE;
+      return;
+    }
+    v = 1;
+  }
   if (v >= 2 && conv_pool_stream_eligible(p, v)) {
     launch_conv_pool_stream(p, v, s);
     last_conv_tile = EPOOL_TILE_BASE + v;

@@ -43,6 +43,7 @@ struct ConvParams {
   // 13 x 19 patch of conv outputs feeding a 6 x 9 tile of pooled outputs, ep_tr x ep_tc tiles per image
   int ep_pt, ep_pl, ep_Ho, ep_Wo, ep_tr, ep_tc;
   int ep_variant;      // pooled-conv kernel (launch_conv_epool): 0 auto, 1 patch, 2 / 3 row walk
+  const float* wc1;    // variant 7: weights in launch_pack_c1_f32 layout (null: variant 7 unavailable)
 };
 
 // Per-layer kernel choice and weight layout (see plan_conv in ore_conv.hip).
@@ -208,6 +209,15 @@ void launch_conv_epool(const ConvParams& p, hipStream_t s);
 // else 1.
 // ORE_CONV_POOL_STREAM=0..5 forces 1..6 (tests).  launch_conv_epool leaves last_conv_tile = EPOOL_TILE_BASE + variant run.
 constexpr int EPOOL_TILE_BASE = 21;
+// variant 7 (ore_conv1_f32.hip): the first conv (7x7 / stride 2, C in {1, 3, 4}, 64 < M <= 128) with
+// its input window in LDS, weights packed by launch_pack_c1_f32 (ConvPlan::wc1); reported as tile
+// EPOOL_WIN_TILE (after the Winograd / fused-f16 tile ids: ore.Model.TILE_NAMES "epool window f32")
+constexpr int EPOOL_WIN_VARIANT = 7, EPOOL_WIN_TILE = 44;
+inline int epool_tile_id(int variant) { return variant == EPOOL_WIN_VARIANT ? EPOOL_WIN_TILE : EPOOL_TILE_BASE + variant; }
+bool conv_win_pool_f32_eligible(const ConvParams& p);
+void launch_conv_win_pool_f32(const ConvParams& p, const float* wc, hipStream_t s);
+size_t c1_f32_pack_bytes(int M, int K);
+void launch_pack_c1_f32(const float* w, int M, int K, float* out, hipStream_t s);
 bool conv_pool_stream_eligible(const ConvParams& p, int variant);
 void launch_conv_pool_stream(const ConvParams& p, int variant, hipStream_t s);
 constexpr int CONV_EPOOL_BN = 256;  // N tile of the pooled-epilogue kernel

@@ -115,6 +115,7 @@ struct Step {
   ConvPlan plan_wino{};
   float* wp_wino = nullptr;
   void* xcvt = nullptr;        // f16 F16_X_NHWC_PAIR: the f32 NCHW input converted to NHWC4 f16 (max_batch)
+  const float* wc1 = nullptr;  // f32 pooled first conv: weights for pooled-conv variant 7 (launch_pack_c1_f32)
   int64_t axis = 1;
   double flops_per_img = 0, bytes_per_img = 0, bytes_fixed = 0;
 };
@@ -610,6 +611,22 @@ ore_status plan(ore_model* m) {
       if (work == 0.0 || work > max_work) continue;
       cv.epool = true;
       cv.out = pl.out;
+      // f32: pack the weights for the window kernel (pooled-conv variant 7) when its geometry fits
+      if (!cv.plan.f16 && cv.kh == 7 && cv.kw == 7 && cv.sh == 2 && cv.sw == 2 && cv.in1 >= 0 &&
+          (cv.C == 1 || cv.C == 3 || cv.C == 4) && cv.M > 32 && cv.M <= 128) {
+        const int key = 4000000 + pc;
+        if (!m->fire_packs.count(key)) {
+          float* buf = nullptr;
+          const int K = int(cv.C * cv.kh * cv.kw);
+          if (hipMalloc(reinterpret_cast<void**>(&buf), c1_f32_pack_bytes(int(cv.M), K)) != hipSuccess)
+            return err(m, ORE_ERR_OOM, "conv weight packing allocation failed");
+          launch_pack_c1_f32(m->values[cv.in1].cptr, int(cv.M), K, buf, m->ctx->stream);
+          if (hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
+            return err(m, ORE_ERR_HIP, "conv weight packing failed");
+          m->fire_packs[key] = buf;
+        }
+        cv.wc1 = m->fire_packs[key];
+      }
       cv.ep_kh = pl.kh; cv.ep_kw = pl.kw; cv.ep_sh = pl.sh; cv.ep_sw = pl.sw; cv.ep_win = pl.win;
       // algorithmic bytes: the conv's input + the pooled output (the pre-pool tensor never moves)
       cv.bytes_per_img = double(m->values[cv.in0].es) * double(cv.C * cv.H * cv.W) +
@@ -1167,7 +1184,7 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
         ctx->mapped_hi = m->arena ? m->arena + m->arena_bytes : nullptr;
         const ore_status r = run_conv_epool(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.ktab, s.M, s.kh,
                                             s.kw, bias, s.win, s.sh, s.sw, s.relu, s.ep_kh, s.ep_kw, s.ep_sh, s.ep_sw,
-                                            s.ep_win, y.p, y.nstride, y.ps);
+                                            s.ep_win, y.p, y.nstride, y.ps, s.wc1);
         ctx->mapped_lo = ctx->mapped_hi = nullptr;
         s.ran_tile = last_conv_tile;
         return r;
@@ -1626,11 +1643,12 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
       float best_ms = 1e30f;
       // variant 6 (two 4-wave blocks per CU) wins this isolated timing on conv1 but loses inside the
       // graph (963 vs 913 us, profiles/r01zg_conv1_walk96_b2.txt): forced only (ORE_CONV_POOL_STREAM=5)
-      for (int v = 1; v <= 5 && !st; ++v) {
+      for (int v : {1, 2, 3, 4, 5, EPOOL_WIN_VARIANT}) {
+        if (st) break;
         s.plan.epv = v;
         last_conv_tile = -1;
         st = launch_step(m, s, n);  // warm-up
-        if (st || last_conv_tile != EPOOL_TILE_BASE + v) continue;  // not eligible here
+        if (st || last_conv_tile != epool_tile_id(v)) continue;  // not eligible here
         if (hipEventRecord(e0, ctx->stream) != hipSuccess) { st = set_error(ctx, ORE_ERR_HIP, "event record"); break; }
         for (int r = 0; r < reps && !st; ++r) st = launch_step(m, s, n);
         float ms = 0.f;
@@ -1704,7 +1722,7 @@ int32_t ore_model_step_tile(ore_model* m, int32_t i) {
   const Step& s = m->steps[m->exec_steps[i]];
   if (s.kind == S_FIRE)  // "fire" / "fire wino" / "fire f16": the fused fire kernels (ore.Model.TILE_NAMES)
     return s.fire_f16 ? WINO_TILE_BASE + WINO_TILES_N + 1 : s.fire_wino ? WINO_TILE_BASE + WINO_TILES_N : CONV_TILES_F32;
-  if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.plan.epv > 0) return EPOOL_TILE_BASE + s.plan.epv;
+  if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.plan.epv > 0) return epool_tile_id(s.plan.epv);
   if (s.kind == S_CONV && s.epool && s.ran_tile >= 0) return s.ran_tile;
   return (s.kind == S_CONV || s.kind == S_MATMUL) ? s.plan.cfg : -1;
 }

@@ -283,7 +283,7 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
                           int64_t x_nstride, int64_t x_ps, const float* wp, const int2* ktab, int64_t M, int64_t kh,
                           int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu,
                           int64_t pkh, int64_t pkw, int64_t psh, int64_t psw, const Window& pwin, float* y,
-                          int64_t y_nstride, int64_t y_ps) {
+                          int64_t y_nstride, int64_t y_ps, const float* wc1) {
   if (N == 0) return ORE_OK;
   if (pln.f16 || pln.window) return set_error(ctx, ORE_ERR_INVALID, "internal: the pooled epilogue is f32 gather only");
   if (x_ps == 0) x_ps = H * W;
@@ -315,6 +315,7 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
   p.ep_pt = int(pwin.pt); p.ep_pl = int(pwin.pl); p.ep_Ho = int(pwin.Ho); p.ep_Wo = int(pwin.Wo);
   p.ep_tr = tr; p.ep_tc = tc;
   p.ep_variant = pln.epv;
+  p.wc1 = wc1;
   {  // mapped bytes before x (as run_conv): the row-walking 3x3 kernel reads a few of them, masked
     const char* xc = reinterpret_cast<const char*>(x);
     int64_t g = int64_t(reinterpret_cast<uintptr_t>(x) & 4095);

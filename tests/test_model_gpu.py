@@ -353,10 +353,13 @@ def test_conv_pool_fusion_bit_identical(gpu_ctx, case, precision):
     (2, 50, 100, 4),   # kw = 4 (one tap carry per k-step), M = 100: a 4-channel last tile
     (4, 23, 20, 7),    # M = 20: 32-channel tiles (MF = 2), Ho 9 -> a single step per image
     (3, 113, 64, 7),   # Ho 54 (even), 14 quads per row, pooled 26 x 26
+    (1, 40, 128, 7),   # one input channel, 4 channel fragments (window kernel)
+    (4, 37, 72, 7),    # four input channels, M = 72: a partial third fragment (window kernel)
 ])
 def test_conv_pool_walk_bit_identical(gpu_ctx, case, monkeypatch):
     """The row-walking conv + pool kernels (ore_conv_pool.hip, LDS-ring pooled epilogue with ds_max on
-    the f32 bits; ORE_CONV_POOL_STREAM=1: 48 channels x 64 quads per block, =2: 96 x 128) equal the
+    the f32 bits; ORE_CONV_POOL_STREAM=1: 48 channels x 64 quads per block, =2: 96 x 128) and the
+    window kernel (=6, ore_conv1_f32.hip: 7x7 / stride 2, C in {1, 3, 4}, 32 < M <= 128) equal the
     patch-epilogue kernel (=0) and the separate conv + Relu + MaxPool kernels bit for bit, and the
     oracle within the conv tolerance."""
     import ore
@@ -368,13 +371,16 @@ def test_conv_pool_walk_bit_identical(gpu_ctx, case, monkeypatch):
     mb = _conv_pool_model((1, C, H, H), w, b, [0] * 4, [2, 2], True, [3, 3], [2, 2], [0, 0, 0, 0])
     monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "100")
     vals = []
+    names = ore.Model.TILE_NAMES
     for walk, fusion in (("1", ore.FUSE_ALL), ("0", ore.FUSE_ALL), ("2", ore.FUSE_ALL), ("5", ore.FUSE_ALL),
-                         ("1", ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
+                         ("6", ore.FUSE_ALL), ("1", ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
         monkeypatch.setenv("ORE_CONV_POOL_STREAM", walk)
         m = ore.Model(gpu_ctx, mb, max_batch=3)
         m.set_fusion(fusion | ore.KEEP_VALUES)
         _np(m.run(_t(x)))
         vals.append(m.read_value("p"))
+        if walk == "6" and k == 7 and C in (1, 3, 4) and 32 < M <= 128:  # the window kernel (variant 7) ran
+            assert [names[t] for t in m.tiles() if t >= 0] == ["epool window f32"]
         m.close()
     for v in vals[1:]:
         np.testing.assert_array_equal(vals[0], v)
