@@ -232,12 +232,15 @@ def main():
             achieved = conv["flops"] / (conv["ms"] * 1e-3) / 1e12
             # x3: every f32 MAC is six bf16 part products on the 2.5 PF/s BF16 matrix cores
             peak = PEAK_F16_MFMA_TFLOPS if f16 else PEAK_F16_MFMA_TFLOPS / 6.0 if x3 else PEAK_F32_MFMA_TFLOPS
-            kname = ("conv_f16_kernel (implicit-GEMM MFMA 32x32x16 f16, f32 accumulate" if f16 else
+            kname = ("Conv class: conv_pair_pool_f16_kernel (conv1 + pool1 straight from the f32 input), "
+                     "fire_f16_kernel / fire_pool_f16_kernel (fire module [+ MaxPool] + next squeeze) and "
+                     "conv_f16_kernel (implicit GEMM), all MFMA 32x32x16 f16 with f32 accumulate" if f16 else
                      "conv_x3_kernel (f32 implicit GEMM on MFMA 16x16x32 bf16: both operands split exactly into "
                      "3 bf16 parts, 6 part products per f32 MAC; peak = 2500 / 6 TFLOP/s of f32 work" if x3 else
                      "Conv class: conv_stream_kernel (LDS-free implicit GEMM, MFMA 16x16x4 f32), fire_kernel (fire "
-                     "module + next squeeze), conv_pool_stream_kernel (conv1 + pool1 row walk) and conv_gemm_kernel "
-                     "(LDS-staged, MFMA 32x32x2 f32) per the autotuned tile") + f", {conv['launches']} launches/step)"
+                     "module + next squeeze), conv_pool_stream_kernel / conv_win_pool_f32_kernel (conv1 + pool1), "
+                     "conv_wino32/16_kernel (Winograd F(2x2,3x3) expand3x3, FLOPs counted as direct) and "
+                     "conv_gemm_kernel (LDS-staged, MFMA 32x32x2 f32) per the autotuned tile") + f", {conv['launches']} launches/step)"
             # HBM bytes per conv launch from the PMC passes of tools/pmc.sh (FETCH_SIZE x2 +
             # WRITE_SIZE, separate --pmc runs; counters cannot be read inside this timed run)
             traffic, tsrc = None, None

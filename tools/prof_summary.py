@@ -12,7 +12,9 @@ import os
 import sys
 
 CLASSES = [("conv (f32 MFMA)", ("conv_gemm_kernel", "conv_stream_kernel", "fire_kernel", "conv_pool_stream_kernel",
-                                "conv_wino32_kernel", "conv_wino16_kernel", "conv_winol_kernel", "fire_wino_kernel")), ("conv (f16 MFMA)", "conv_f16_kernel"),
+                                "conv_wino32_kernel", "conv_wino16_kernel", "conv_winol_kernel", "fire_wino_kernel",
+                                "conv_win_pool_f32_kernel")),
+           ("conv (f16 MFMA)", ("conv_f16_kernel", "fire_f16_kernel", "fire_pool_f16_kernel", "conv_pair_pool_f16_kernel")),
            ("conv (window)", "conv_win_kernel"), ("maxpool", "maxpool"), ("gap", "gap_kernel"),
            ("softmax", "softmax_kernel"), ("pack/ktab (load time)", "pack_"), ("ktab", "ktab_kernel")]
 
