@@ -14,8 +14,9 @@ import sys
 CLASSES = [("conv (f32 MFMA)", ("conv_gemm_kernel", "conv_stream_kernel", "fire_kernel", "conv_pool_stream_kernel",
                                 "conv_wino32_kernel", "conv_wino16_kernel", "conv_winol_kernel", "fire_wino_kernel",
                                 "conv_win_pool_f32_kernel")),
-           ("conv (f16 MFMA)", ("conv_f16_kernel", "fire_f16_kernel", "fire_pool_f16_kernel", "conv_pair_pool_f16_kernel")),
-           ("conv (window)", "conv_win_kernel"), ("maxpool", "maxpool"), ("gap", "gap_kernel"),
+           ("conv (f16 MFMA)", ("conv_f16_kernel", "conv_f16_dma_kernel", "conv_f16_epool", "fire_f16_kernel",
+                                "fire_pool_f16_kernel", "conv_pair_pool_f16_kernel")),
+           ("conv (window)", "conv_win_kernel"), ("maxpool", "maxpool"), ("gap", ("gap_kernel", "gap_nhwc_kernel")),
            ("softmax", "softmax_kernel"), ("pack/ktab (load time)", "pack_"), ("ktab", "ktab_kernel")]
 
 
@@ -36,7 +37,7 @@ def main():
     trace = os.path.join(os.path.dirname(sys.argv[1]), "run_kernel_trace.csv")
     bench = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1]) if len(sys.argv) > 2 else None
     if os.path.exists(trace) and bench:
-        disp = [r for r in csv.DictReader(open(trace)) if "ore::" in r["Kernel_Name"]]
+        disp = [r for r in csv.DictReader(open(trace)) if "ore::" in r["Kernel_Name"] or "_ZN3ore" in r["Kernel_Name"]]
         disp.sort(key=lambda r: int(r["Dispatch_Id"]))
         # dispatches per step: the distance between the last two softmax launches (every step ends
         # with the softmax)
