@@ -111,35 +111,44 @@ __device__ __forceinline__ void ff_e1_chunk(ff16 (&acc)[F], const _Float16* __re
   }
 }
 
-// One 32-channel chunk of expand3x3: 9 taps x NKC k-steps, k order (r, s, c).  B fragments one step
+// One 32-channel chunk of expand3x3: 9 taps x NKC k-steps, k order (r, s, c).  B fragments BD steps
 // ahead, A PD steps ahead; the scheduling barrier keeps every step's loads in it (unpinned, the
-// scheduler hoists all F x 9 NKC LDS reads and spills).
+// scheduler hoists all F x 9 NKC LDS reads and spills).  One step of B prefetch left the LDS latency
+// exposed behind an lgkmcnt(0) per step (2 MFMAs cover ~64 clocks).
+#ifndef ORE_FF_BD
+#define ORE_FF_BD 2
+#endif
+#ifndef ORE_FF_PD
+#define ORE_FF_PD 8
+#endif
 template <int NKC, int F, int PS>
 __device__ __forceinline__ void ff_e3_chunk(ff16 (&acc)[F], const _Float16* __restrict__ w3, int E3, int c0, int arow,
                                             const _Float16* halo, const int (&hb)[F], int W2) {
-  constexpr int NS3 = 9 * NKC, PD = 6;
+  constexpr int NS3 = 9 * NKC, PD = ORE_FF_PD < NS3 ? ORE_FF_PD : NS3, BD = ORE_FF_BD;
   fh8 a[PD];
 #pragma unroll
-  for (int s = 0; s < PD; ++s)
-    if (s < NS3) a[s] = ld_g(w3 + (s * E3 + c0) * 16 + arow);
+  for (int s = 0; s < PD; ++s) a[s] = ld_g(w3 + (s * E3 + c0) * 16 + arow);
   ff_zero(acc);
   auto boff = [&](int s) __attribute__((always_inline)) {
     const int tap = s / NKC, cs = s - tap * NKC;
     return ((tap / 3) * W2 + tap % 3) * PS + 16 * cs;
   };
-  fh8 bn[F];
+  fh8 bn[BD][F];
 #pragma unroll
-  for (int f = 0; f < F; ++f) bn[f] = ld_s(halo + hb[f] + boff(0));
+  for (int d = 0; d < BD; ++d)
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+      if (d < NS3) bn[d][f] = ld_s(halo + hb[f] + boff(d));
 #pragma unroll
   for (int s = 0; s < NS3; ++s) {
     const fh8 cur = a[s % PD];
     fh8 b[F];
 #pragma unroll
-    for (int f = 0; f < F; ++f) b[f] = bn[f];
+    for (int f = 0; f < F; ++f) b[f] = bn[s % BD][f];
     if (s + PD < NS3) a[s % PD] = ld_g(w3 + ((s + PD) * E3 + c0) * 16 + arow);
-    if (s + 1 < NS3) {
+    if (s + BD < NS3) {
 #pragma unroll
-      for (int f = 0; f < F; ++f) bn[f] = ld_s(halo + hb[f] + boff(s + 1));
+      for (int f = 0; f < F; ++f) bn[s % BD][f] = ld_s(halo + hb[f] + boff(s + BD));
     }
 #pragma unroll
     for (int f = 0; f < F; ++f) acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur, b[f], acc[f], 0, 0, 0);
