@@ -258,8 +258,18 @@ static bool c3_launch(const ConvParams& p, const float* wc, hipStream_t s) {
     int v = 0;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
   }
-  const unsigned grid = (unsigned)std::min<long long>(tiles, 2LL * ncu);
-  hipLaunchKernelGGL((conv_win_pool_f32_kernel<MF, C, 7, 7, 2>), dim3(grid), dim3(256), G::LDS + MF * 32 * 4, s, p, wc);
+  // persistent: as many workgroups as fit on the chip at once (registers and LDS; 3 per CU for
+  // conv1's 96 channels), each taking every grid-th tile
+  const unsigned lds = G::LDS + MF * 32 * 4;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_win_pool_f32_kernel<MF, C, 7, 7, 2>, 256, lds) !=
+          hipSuccess || per_cu < 1)
+    per_cu = 2;
+#ifdef ORE_C3_WPC
+  per_cu = ORE_C3_WPC;  // experiment knob
+#endif
+  const unsigned grid = (unsigned)std::min<long long>(tiles, (long long)per_cu * ncu);
+  hipLaunchKernelGGL((conv_win_pool_f32_kernel<MF, C, 7, 7, 2>), dim3(grid), dim3(256), lds, s, p, wc);
   return true;
 }
 

@@ -166,6 +166,33 @@ __global__ __launch_bounds__(256, ORE_FIRE_MINB) void fire_kernel(FireParams p) 
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    // the squeeze's A operand (16 k-steps of this chunk) in 4 groups of 4 k-steps, one group ahead;
+    // group 0 is issued before the ring drain.  (Loaded at their use, the compiler put a vmcnt(0)
+    // behind every pair: 8 exposed L2 round trips per chunk, ~20 % of the module's time.)
+    const int saoff = ((cat0 + lk) * p.Msp + MFS * lj) * 4;
+    float asq[2][4][MFS];
+    auto sload = [&](float (&dst)[4][MFS], int g) __attribute__((always_inline)) {
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int so = saoff + (4 * g + tt) * 16 * p.Msp;
+        if constexpr (MFS == 4) {
+          const fi_floatx4 v = __builtin_bit_cast(fi_floatx4, __builtin_amdgcn_raw_buffer_load_b128(wsr, so, 0, 0));
+          dst[tt][0] = v[0]; dst[tt][1] = v[1]; dst[tt][2] = v[2]; dst[tt][3] = v[3];
+        } else if constexpr (MFS == 3) {
+          typedef float f3 __attribute__((ext_vector_type(3)));
+          const f3 v = __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(wsr, so, 0, 0));
+          dst[tt][0] = v[0]; dst[tt][1] = v[1]; dst[tt][2] = v[2];
+        } else if constexpr (MFS == 2) {
+          typedef float f2 __attribute__((ext_vector_type(2)));
+          const f2 v = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(wsr, so, 0, 0));
+          dst[tt][0] = v[0]; dst[tt][1] = v[1];
+        } else {
+          dst[tt][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wsr, so, 0, 0));
+        }
+      }
+    };
+    sload(asq[0], 0);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int d = 0; d < D; ++d) FI_MFMA(d);
 #undef FI_LOAD
@@ -182,30 +209,20 @@ __global__ __launch_bounds__(256, ORE_FIRE_MINB) void fire_kernel(FireParams p) 
       }
     // squeeze over these 64 concat channels: k-step t = 4 f + e takes concat channel cat0 + 4 t + lk
     // from lane group lk (the value acc[f][q][e]); A = Ws packed K-major (row cat0 + 4 t + lk)
-    const int saoff = ((cat0 + lk) * p.Msp + MFS * lj) * 4;
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      float as[MFS];
-      const int so = saoff + t * 16 * p.Msp;
-      if constexpr (MFS == 4) {
-        const fi_floatx4 v = __builtin_bit_cast(fi_floatx4, __builtin_amdgcn_raw_buffer_load_b128(wsr, so, 0, 0));
-        as[0] = v[0]; as[1] = v[1]; as[2] = v[2]; as[3] = v[3];
-      } else if constexpr (MFS == 3) {
-        typedef float f3 __attribute__((ext_vector_type(3)));
-        const f3 v = __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(wsr, so, 0, 0));
-        as[0] = v[0]; as[1] = v[1]; as[2] = v[2];
-      } else if constexpr (MFS == 2) {
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        const f2 v = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(wsr, so, 0, 0));
-        as[0] = v[0]; as[1] = v[1];
-      } else {
-        as[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wsr, so, 0, 0));
+    for (int g = 0; g < 4; ++g) {
+      if (g + 1 < 4) sload(asq[(g + 1) & 1], g + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int t = 4 * g + tt;
+#pragma unroll
+        for (int fs = 0; fs < MFS; ++fs)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            accs[fs][q] =
+                __builtin_amdgcn_mfma_f32_16x16x4f32(asq[g & 1][tt][fs], acc[t >> 2][q][t & 3], accs[fs][q], 0, 0, 0);
       }
-#pragma unroll
-      for (int fs = 0; fs < MFS; ++fs)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          accs[fs][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(as[fs], acc[t >> 2][q][t & 3], accs[fs][q], 0, 0, 0);
     }
   };
   for (int c0 = 0; c0 < p.E1; c0 += 64) chunk(std::integral_constant<int, 0>{}, c0, c0);
