@@ -46,19 +46,19 @@ struct C1Geom {
   int w_halves, halo_halves, lds_bytes;
 };
 
-__host__ __device__ inline C1Geom c1_geom(int MF, int kh, int kwp, int sh, int sw) {
+__host__ __device__ inline C1Geom c1_geom(int MF, int kh, int kwp, int sh, int sw, bool sq = false) {
   C1Geom g;
   g.KS = kh * kwp * 4 / 16;
   g.hr = (C1_RC - 1) * sh + kh;
   g.hc = (C1_CC - 1) * sw + kwp;
   g.w_halves = g.KS * MF * 32 * 16;
   g.halo_halves = (g.hr * g.hc * 4 + 7) / 8 * 8;
-  g.lds_bytes = (g.w_halves + g.halo_halves + C1_NPX * C1_TS) * 2 + MF * 32 * 4;
+  g.lds_bytes = (g.w_halves + g.halo_halves + C1_NPX * C1_TS) * 2 + MF * 32 * 4 + (sq ? 64 * C1_TS * 2 + 32 * 4 : 0);
   return g;
 }
 
-template <int MF, int KH, int KW, int S>
-__global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p) {
+template <int MF, int KH, int KW, int S, int SQ>
+__global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p, C1Squeeze sq) {
   constexpr int KWP = (KW + 1) & ~1, KS = KH * KWP * 4 / 16;
   constexpr int HR = (C1_RC - 1) * S + KH, HC = (C1_CC - 1) * S + KWP;  // input window of a tile
   constexpr int NQ = (HR * HC + 255) / 256;                              // window pixels per thread
@@ -69,6 +69,10 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
   _Float16* halo = smem + W_HALVES;         // [HR][HC][4]
   _Float16* ct = halo + HALO_HALVES;        // [C1_NPX][C1_TS]
   float* sbias = reinterpret_cast<float*>(ct + C1_NPX * C1_TS);  // [MF * 32]
+  // SQ: the pooled values of one fragment [64 pixels][40] (all four waves pool, waves 0 and 1 run the
+  // squeeze's MFMAs with its weights from L2) and the squeeze bias
+  _Float16* pt = reinterpret_cast<_Float16*>(sbias + MF * 32);
+  float* qbias = reinterpret_cast<float*>(pt + (SQ ? 64 * C1_TS : 0));
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Kp = (p.K + 31) & ~31;
@@ -86,6 +90,10 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
   }
 
   for (int q = tid; q < MF * 32; q += 256) sbias[q] = (p.bias && q < p.M) ? p.bias[q] : 0.0f;
+  if constexpr (SQ) {
+    for (int q = tid; q < 32; q += 256) qbias[q] = q < sq.M ? sq.bias[q] : 0.0f;
+  }
+  const _Float16* __restrict__ wq = static_cast<const _Float16*>(sq.w);
 
   // this lane's two patch pixels (fragments 2 wave, 2 wave + 1)
   int bofs[2], tpx[2];
@@ -194,7 +202,15 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
       }
     }
 
-    // per 32-channel fragment: conv tile, 3x3 max, 16-B NHWC stores
+    // SQ: waves 0 and 1 own the tile's pooled pixels 32 w + lane (54 of 64 used) as the squeeze's B
+    // columns; the squeeze accumulates over the channel fragments in order (k = channel)
+    c1f16 sacc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) sacc[e] = 0.0f;
+    const int kq = 32 * (wave & 1) + lr, kqc = kq < C1_PR * C1_PC ? kq : 0;
+    const int qa = kqc / C1_PC, qb = kqc - qa * C1_PC;
+
+    // per 32-channel fragment: conv tile, 3x3 max, 16-B NHWC stores (SQ: the squeeze's k-steps)
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
       float bv[16];
@@ -224,10 +240,40 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
       }
       __syncthreads();
       if (i == 0) store_window();  // every wave is past its k-loop: the window is free
+      if constexpr (SQ) {
+        {  // every thread: one (pooled pixel, 8 channels) of the 64 x 32 block (pixels >= 54: pixel 0)
+          const int k = tid >> 2, cg = tid & 3, kc = k < C1_PR * C1_PC ? k : 0;
+          const int a = kc / C1_PC, b = kc - a * C1_PC;
+          float mx[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) mx[e] = -FLT_MAX;
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+              const c1h8 v = *reinterpret_cast<const c1h8*>(ct + ((2 * a + r) * C1_CC + 2 * b + s) * C1_TS + cg * 8);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], (float)v[e]);
+            }
+          c1h8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (_Float16)mx[e];
+          *reinterpret_cast<c1h8*>(pt + k * C1_TS + cg * 8) = o;
+        }
+        __syncthreads();
+        if (wave < 2) {
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const c1h8 bq = *reinterpret_cast<const c1h8*>(pt + (32 * wave + lr) * C1_TS + 16 * t + 8 * h);
+            const c1h8 aq = *reinterpret_cast<const c1h8*>(wq + ((2 * i + t) * 32 + lr) * 16 + 8 * h);
+            sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(aq, bq, sacc, 0, 0, 0);
+          }
+        }
+      }
 #ifdef ORE_EXP_C1_NOPOOL
       if (tid < 0) {
 #else
-      if (tid < ctile_tasks) {
+      if (!SQ && tid < ctile_tasks) {
 #endif
         const int pp = tid >> 2, cg = tid & 3;
         const int a = pp / C1_PC, b = pp - a * C1_PC;
@@ -252,17 +298,33 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
       }
       if (i + 1 < MF) __syncthreads();  // the conv tile is rewritten by the next fragment
     }
+    if constexpr (SQ) {
+      // squeeze output: bias + Relu + one rounding; element 8 g + e of lane half h = channel 16 g + 8 h + e
+      const int ph = ph0 + qa, pw = pw0 + qb;
+      if (wave < 2 && kq < C1_PR * C1_PC && ph < p.ep_Ho && pw < p.ep_Wo) {
+        _Float16* yq = static_cast<_Float16*>(sq.y) + (long long)img * sq.y_nstride + (ph * p.ep_Wo + pw) * sq.y_cs;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const int ch = 16 * g + 8 * h;
+          if (ch >= sq.M) continue;
+          c1h8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (_Float16)fmaxf(sacc[8 * g + e] + qbias[ch + e], 0.0f);
+          *reinterpret_cast<c1h8*>(yq + ch) = o;
+        }
+      }
+    }
   }
 }
 
-template <int MF>
-static bool c1_dispatch(const ConvParams& p, unsigned grid, unsigned lds, hipStream_t s) {
+template <int MF, int SQ>
+static bool c1_dispatch(const ConvParams& p, const C1Squeeze& sq, unsigned grid, unsigned lds, hipStream_t s) {
   if (p.kh == 7 && p.kw == 7 && p.sh == 2) {
-    hipLaunchKernelGGL((conv_pair_pool_f16_kernel<MF, 7, 7, 2>), dim3(grid), dim3(256), lds, s, p);
+    hipLaunchKernelGGL((conv_pair_pool_f16_kernel<MF, 7, 7, 2, SQ>), dim3(grid), dim3(256), lds, s, p, sq);
     return true;
   }
-  if (p.kh == 3 && p.kw == 3 && p.sh == 2) {
-    hipLaunchKernelGGL((conv_pair_pool_f16_kernel<MF, 3, 3, 2>), dim3(grid), dim3(256), lds, s, p);
+  if (!SQ && p.kh == 3 && p.kw == 3 && p.sh == 2) {
+    hipLaunchKernelGGL((conv_pair_pool_f16_kernel<MF, 3, 3, 2, 0>), dim3(grid), dim3(256), lds, s, p, sq);
     return true;
   }
   return false;
@@ -270,20 +332,26 @@ static bool c1_dispatch(const ConvParams& p, unsigned grid, unsigned lds, hipStr
 
 }  // namespace
 
-bool conv_pair_pool_f16_eligible(const ConvParams& p) {
+bool conv_pair_pool_f16_eligible(const ConvParams& p, const C1Squeeze* sq) {
   if (!((p.kh == 7 && p.kw == 7) || (p.kh == 3 && p.kw == 3))) return false;
   const int MF = (p.M + 31) / 32, kwp = (p.kw + 1) & ~1;
   if (MF < 1 || MF > 4 || p.M % 8 || p.C < 1 || p.C > 4 || p.sh != 2 || p.sw != 2 || p.pl % 2) return false;
   if (p.y_ps % 8 || p.y_nstride % 8 || (reinterpret_cast<uintptr_t>(p.y) & 15) || (reinterpret_cast<uintptr_t>(p.wp) & 15))
     return false;
   if (p.K != p.kh * kwp * 4 || p.Mp < MF * 32 - 31) return false;
-  const C1Geom g = c1_geom(MF, p.kh, kwp, p.sh, p.sw);
+  if (sq) {  // the fused squeeze: 7x7 only, whole 32-channel fragments in, <= 32 channels out
+    auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    if (p.kh != 7 || (MF != 2 && MF != 3) || p.M != 32 * MF || sq->M < 8 || sq->M > 32 || sq->M % 8 || sq->y_cs % 8 ||
+        sq->y_cs < sq->M || sq->y_nstride % 8 || !al16(sq->y) || !al16(sq->w) || !sq->bias)
+      return false;
+  }
+  const C1Geom g = c1_geom(MF, p.kh, kwp, p.sh, p.sw, sq != nullptr);
   return g.lds_bytes <= 80 * 1024 && (long long)p.H * p.W < (1LL << 30) && p.ep_tr > 0 && p.ep_tc > 0;
 }
 
-void launch_conv_pair_pool_f16(const ConvParams& p, hipStream_t s) {
+void launch_conv_pair_pool_f16(const ConvParams& p, const C1Squeeze* sq, hipStream_t s) {
   const int MF = (p.M + 31) / 32, kwp = (p.kw + 1) & ~1;
-  const C1Geom g = c1_geom(MF, p.kh, kwp, p.sh, p.sw);
+  const C1Geom g = c1_geom(MF, p.kh, kwp, p.sh, p.sw, sq != nullptr);
   long long tiles = (long long)p.N * p.ep_tr * p.ep_tc;
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
@@ -291,11 +359,17 @@ void launch_conv_pair_pool_f16(const ConvParams& p, hipStream_t s) {
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
   }
   const unsigned grid = (unsigned)std::min<long long>(tiles, 2LL * ncu);  // persistent: weights staged once
+  const C1Squeeze none{};
+  if (sq) {
+    if (MF == 2) c1_dispatch<2, 1>(p, *sq, grid, g.lds_bytes, s);
+    else c1_dispatch<3, 1>(p, *sq, grid, g.lds_bytes, s);
+    return;
+  }
   switch (MF) {
-    case 1: c1_dispatch<1>(p, grid, g.lds_bytes, s); break;
-    case 2: c1_dispatch<2>(p, grid, g.lds_bytes, s); break;
-    case 3: c1_dispatch<3>(p, grid, g.lds_bytes, s); break;
-    default: c1_dispatch<4>(p, grid, g.lds_bytes, s); break;
+    case 1: c1_dispatch<1, 0>(p, none, grid, g.lds_bytes, s); break;
+    case 2: c1_dispatch<2, 0>(p, none, grid, g.lds_bytes, s); break;
+    case 3: c1_dispatch<3, 0>(p, none, grid, g.lds_bytes, s); break;
+    default: c1_dispatch<4, 0>(p, none, grid, g.lds_bytes, s); break;
   }
 }
 

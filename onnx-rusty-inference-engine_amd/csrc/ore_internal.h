@@ -107,7 +107,8 @@ struct F16Epool {
 ore_status run_conv_pair_pool_f16(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H,
                                   int64_t W, int64_t x_nstride, int64_t x_ps, const void* wp, int64_t M, int64_t kh,
                                   int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu,
-                                  void* y, int64_t y_nstride, int64_t y_ps, const F16Epool& ep, bool* ran);
+                                  void* y, int64_t y_nstride, int64_t y_ps, const F16Epool& ep, bool* ran,
+                                  const C1Squeeze* sq = nullptr);
 // f16 plan (f16 models): y is NHWC f16 with pixel stride y_ps; x is the f32 NCHW model input
 // (F16_X_NCHW32, plane stride x_ps) or NHWC f16 with pixel stride x_ps.  ktab per plan.xmode.
 // ep: the following MaxPool in the epilogue (y is then the pooled NHWC output)

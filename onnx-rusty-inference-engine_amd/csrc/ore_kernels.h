@@ -150,8 +150,18 @@ void launch_fire_f16(const FireF16Params& p, hipStream_t s);
 // f16 models: the first conv (f32 NCHW input, <= 4 channels, F16_X_NHWC_PAIR packing in p.wp) with
 // its 3x3 / stride-2 MaxPool in one persistent launch (ore_conv1_f16.hip); p as for
 // launch_conv_f16_epool but p.x is the f32 model input itself (no NHWC4 conversion)
-bool conv_pair_pool_f16_eligible(const ConvParams& p);
-void launch_conv_pair_pool_f16(const ConvParams& p, hipStream_t s);
+// sq: the pooled map's only consumer, a 1x1 conv + Relu (<= 32 channels, weights by
+// launch_fire_pack_f16(w, M, C, 1)), fused in (the pooled map is never stored; y = its output)
+struct C1Squeeze {
+  const void* w;
+  const float* bias;
+  int M;
+  void* y;                // f16 NHWC on the pooled plane, pixel stride y_cs
+  long long y_nstride;
+  int y_cs;
+};
+bool conv_pair_pool_f16_eligible(const ConvParams& p, const C1Squeeze* sq = nullptr);
+void launch_conv_pair_pool_f16(const ConvParams& p, const C1Squeeze* sq, hipStream_t s);
 // W [M][C][kk] f32 (kk = 1 or 9) -> [C kk / 16][roundup(M, 32)][16] f16 with permuted rows
 size_t fire_pack_f16_bytes(int M, int C, int kk);
 void launch_fire_pack_f16(const float* w, int M, int C, int kk, void* out, hipStream_t s);

@@ -116,6 +116,12 @@ struct Step {
   float* wp_wino = nullptr;
   void* xcvt = nullptr;        // f16 F16_X_NHWC_PAIR: the f32 NCHW input converted to NHWC4 f16 (max_batch)
   const float* wc1 = nullptr;  // f32 pooled first conv: weights for pooled-conv variant 7 (launch_pack_c1_f32)
+  // f16 pooled first conv with the next 1x1 conv (+ Relu) fused in (conv_pair_pool_f16_kernel SQ):
+  // out is that conv's output; the squeeze weights in launch_fire_pack_f16 layout
+  bool c1sq = false;
+  const void* sq_w = nullptr;
+  const float* sq_b = nullptr;
+  int64_t sq_M = 0;
   int64_t axis = 1;
   double flops_per_img = 0, bytes_per_img = 0, bytes_fixed = 0;
 };
@@ -887,6 +893,55 @@ ore_status plan(ore_model* m) {
     }
     count_uses(m, m->steps);
   }
+  // (1h) f16 models: the first conv + pool (F16_X_NHWC_PAIR, pooled epilogue) whose pooled map is read
+  // only by a 1x1 conv (+ Relu) with <= 32 channels takes that conv into its launch
+  // (conv_pair_pool_f16_kernel SQ: SqueezeNet's conv1 + pool1 + fire2/squeeze1x1); the pooled map is
+  // never stored.  Bit-identical to the separate squeeze (same k-ordered chain over the same f16
+  // pooled values).  ORE_F16_C1POOL=0 (the two-launch first conv) turns it off.
+  if (m->f16 && (m->fusion & ORE_FUSE_CONV_POOL) && (m->fusion & ORE_FUSE_CONV_RELU)) {
+    const char* ec = getenv("ORE_F16_C1POOL");
+    const bool on = !(ec && atoi(ec) == 0);
+    for (size_t i = 0; on && i < m->steps.size(); ++i) {
+      Step& cv = m->steps[i];
+      if (cv.kind != S_CONV || !cv.plan.f16 || cv.plan.xmode != F16_X_NHWC_PAIR || !cv.epool || cv.c1sq) continue;
+      if (cv.kh != 7 || cv.kw != 7 || cv.sh != 2 || cv.sw != 2 || cv.win.pl % 2 || cv.C > 4 ||
+          (cv.M != 64 && cv.M != 96))
+        continue;
+      const Value& pv = m->values[cv.out];
+      if (pv.uses != 1 || pv.is_output) continue;
+      int qi = -1;
+      for (size_t j = i + 1; j < m->steps.size(); ++j)
+        if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == cv.out || m->steps[j].in1 == cv.out)) { qi = int(j); break; }
+      if (qi < 0) continue;
+      Step& q = m->steps[qi];
+      if (q.kind != S_CONV || !q.relu || q.pool || q.epool || !q.plan.f16 || q.plan.xmode != F16_X_NHWC_VEC ||
+          q.kh != 1 || q.kw != 1 || q.sh != 1 || q.sw != 1 || q.win.pt || q.win.pl || q.in0 != cv.out ||
+          q.C != cv.M || q.M > 32 || q.M % 8 || q.in2 < 0)
+        continue;
+      const int key = 5000000 + qi;
+      if (!m->fire_packs.count(key)) {
+        float* buf = nullptr;
+        if (hipMalloc(reinterpret_cast<void**>(&buf), fire_pack_f16_bytes(int(q.M), int(q.C), 1)) != hipSuccess)
+          return err(m, ORE_ERR_OOM, "squeeze weight packing allocation failed");
+        launch_fire_pack_f16(m->values[q.in1].cptr, int(q.M), int(q.C), 1, buf, m->ctx->stream);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
+          return err(m, ORE_ERR_HIP, "squeeze weight packing failed");
+        m->fire_packs[key] = buf;
+      }
+      cv.c1sq = true;
+      cv.sq_w = m->fire_packs[key];
+      cv.sq_b = m->values[q.in2].cptr;
+      cv.sq_M = q.M;
+      m->values[cv.out].elided = true;
+      cv.out = q.out;
+      cv.flops_per_img += q.flops_per_img;
+      cv.bytes_per_img = double(m->values[cv.in0].es) * double(cv.C * cv.H * cv.W) + 2.0 * double(q.M * q.H * q.W);
+      cv.name = cv.name + "+" + q.name;
+      q.kind = S_NOP;
+      q.in0 = -1;
+    }
+    count_uses(m, m->steps);
+  }
   // (1f) ORE_LOAD_X3: every conv / matmul not taken by an f32-MFMA fusion above runs its x3 plan
   if (m->x3)
     for (auto& st : m->steps)
@@ -1161,11 +1216,14 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       const F16Epool ep{s.ep_kh, s.ep_kw, s.ep_sh, s.ep_sw, s.ep_win};
       if (s.plan.f16 && s.plan.xmode == F16_X_NHWC_PAIR && s.epool) {  // one launch from the f32 input
         bool ran = false;
+        const C1Squeeze sq{s.sq_w, s.sq_b, int(s.sq_M), y.p, y.nstride, int(y.ps ? y.ps : s.sq_M)};
         const ore_status st = run_conv_pair_pool_f16(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.M, s.kh,
-                                                     s.kw, bias, s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps, ep, &ran);
+                                                     s.kw, bias, s.win, s.sh, s.sw, s.relu, s.c1sq ? nullptr : y.p,
+                                                     y.nstride, s.c1sq ? s.M : y.ps, ep, &ran, s.c1sq ? &sq : nullptr);
         if (ran) s.ran_tile = WINO_TILE_BASE + WINO_TILES_N + 2;  // "first conv pool f16" (ore.Model.TILE_NAMES)
         if (st != ORE_OK || ran) return st;
         s.ran_tile = -1;
+        if (s.c1sq) return err(m, ORE_ERR_INVALID, "internal: the fused first conv + squeeze declined its launch");
       }
       if (s.plan.f16 && (s.plan.xmode == F16_X_NHWC_PAIR || s.plan.xmode == F16_X_NHWC8)) {
         // convert the f32 NCHW input to NHWC f16 (4 / 8 channels per pixel), then gather

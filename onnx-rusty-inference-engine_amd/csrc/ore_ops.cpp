@@ -377,11 +377,12 @@ ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int6
 ore_status run_conv_pair_pool_f16(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H,
                                   int64_t W, int64_t x_nstride, int64_t x_ps, const void* wp, int64_t M, int64_t kh,
                                   int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu,
-                                  void* y, int64_t y_nstride, int64_t y_ps, const F16Epool& ep, bool* ran) {
+                                  void* y, int64_t y_nstride, int64_t y_ps, const F16Epool& ep, bool* ran,
+                                  const C1Squeeze* sq) {
   *ran = false;
   if (getenv("ORE_DEBUG_C1")) fprintf(stderr, "c1pool: xmode %d ep %lldx%lld\n", pln.xmode, (long long)ep.kh, (long long)ep.kw);
   if (const char* e = getenv("ORE_F16_C1POOL"))
-    if (atoi(e) == 0) return ORE_OK;
+    if (atoi(e) == 0 && !sq) return ORE_OK;
   if (N == 0 || !pln.f16 || pln.xmode != F16_X_NHWC_PAIR) return ORE_OK;
   if (x_ps == 0) x_ps = H * W;
   if (y_ps == 0) y_ps = M;
@@ -401,14 +402,14 @@ ore_status run_conv_pair_pool_f16(ore_ctx* ctx, const ConvPlan& pln, const float
   p.Mp = pln.Mp;
   p.ep_pt = int(ep.win.pt); p.ep_pl = int(ep.win.pl); p.ep_Ho = int(ep.win.Ho); p.ep_Wo = int(ep.win.Wo);
   p.ep_tr = tr; p.ep_tc = tc;
-  if (!conv_pair_pool_f16_eligible(p)) {
+  if (!conv_pair_pool_f16_eligible(p, sq)) {
     if (getenv("ORE_DEBUG_C1"))
       fprintf(stderr, "c1pool ineligible: C %d H %d W %d M %d k %dx%d s %d,%d p %d,%d K %d Mp %d x_ps %d y_ps %d yns %lld y %p wp %p tr %d tc %d\n",
               p.C, p.H, p.W, p.M, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.K, p.Mp, p.x_ps, p.y_ps, p.y_nstride,
               static_cast<void*>(p.y), static_cast<const void*>(p.wp), p.ep_tr, p.ep_tc);
     return ORE_OK;
   }
-  launch_conv_pair_pool_f16(p, ctx->stream);
+  launch_conv_pair_pool_f16(p, sq, ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());
   *ran = true;
   return ORE_OK;

@@ -454,3 +454,42 @@ def test_f16_squeezenet_first_conv_pool_fused(gpu_ctx, monkeypatch):
         assert (ore.Model.TILE_NAMES[m.tiles()[0]] == "first conv pool f16") == (on == "1")
         m.close()
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("case", [
+    # N, H, W, M, pool pads, squeeze channels
+    (2, 67, 71, 96, [0, 0, 0, 0], 16),   # SqueezeNet conv1 + pool1 + fire2/squeeze1x1 family
+    (3, 40, 33, 64, [0, 0, 1, 1], 32),   # two channel fragments in, 32 out, ceil-mode pool
+    (2, 45, 52, 96, [1, 1, 1, 1], 24),   # padded pool, 24 squeeze channels (a partial store group)
+])
+def test_f16_first_conv_pool_squeeze_fused(gpu_ctx, case, monkeypatch):
+    """The first conv + Relu + MaxPool + the next 1x1 conv + Relu in one launch (the pooled map never
+    stored) equals the two-launch first conv + the separate squeeze bit for bit."""
+    import ore
+    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "8")
+    N, H, W, M, pp, Q = case
+    rng = np.random.default_rng(sum(case[:4]) + Q)
+    x = (rng.standard_normal((N, 3, H, W)) * 20).astype(np.float32)
+    w1 = (rng.standard_normal((M, 3, 7, 7)) * np.sqrt(2.0 / 147)).astype(np.float32)
+    b1 = rng.uniform(-0.1, 0.1, M).astype(np.float32)
+    w2 = (rng.standard_normal((Q, M, 1, 1)) * np.sqrt(2.0 / M)).astype(np.float32)
+    b2 = rng.uniform(-0.1, 0.1, Q).astype(np.float32)
+    mb = _chain_model((1, 3, H, W), [(w1, b1, [0] * 4, [2, 2], True), (w2, b2, [0] * 4, [1, 1], True)], pool=pp)
+    vals = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("ORE_F16_C1POOL", on)
+        m = ore.Model(gpu_ctx, mb, max_batch=N, precision="f16")
+        m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+        y = _np(m.run(_t(x)))
+        vals.append((y, m.read_value("r1")))
+        names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+        if on == "1":
+            assert names == ["first conv pool f16"], names  # one conv launch: the squeeze is inside
+            with pytest.raises(ore.OreError):
+                m.read_value("p0")  # the pooled map is never stored
+        else:
+            assert len(names) == 2, names
+        m.close()
+    np.testing.assert_array_equal(vals[0][1], vals[1][1])
+    np.testing.assert_array_equal(vals[0][0], vals[1][0])
+    assert np.abs(vals[0][1]).max() > 0
