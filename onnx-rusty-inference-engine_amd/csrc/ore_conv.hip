@@ -910,6 +910,15 @@ static void launch_conv_epool_cfg(const ConvParams& p0, hipStream_t s) {
 void launch_conv_epool(const ConvParams& p, hipStream_t s) {
   int v = p.ep_variant;
   if (const char* e = getenv("ORE_CONV_POOL_STREAM")) v = atoi(e) + 1;  // 0..3 -> patch / walk48 / walk96 / walk64, 6 -> window
+  if (p.sq1) {  // the fused squeeze exists in the window kernel only
+    if (p.wc1 && conv_win_pool_f32_eligible(p, p.sq1)) {
+      launch_conv_win_pool_f32(p, p.wc1, p.sq1, s);
+      last_conv_tile = EPOOL_WIN_TILE;
+    } else {
+      last_conv_tile = -2;  // declined: the walker reports an error
+    }
+    return;
+  }
   // auto: a walker block owns a whole image (x its m tile), so below ~one block per CU (batch < 128
   // for conv1) the patch kernel's many small tiles fill the chip better
   if (v == 0 && p.N >= 128)
@@ -917,7 +926,7 @@ void launch_conv_epool(const ConvParams& p, hipStream_t s) {
   if (v == 0) v = 1;
   if (v == EPOOL_WIN_VARIANT) {
     if (p.wc1 && conv_win_pool_f32_eligible(p)) {
-      launch_conv_win_pool_f32(p, p.wc1, s);
+      launch_conv_win_pool_f32(p, p.wc1, nullptr, s);
       last_conv_tile = EPOOL_WIN_TILE;
       return;
     }

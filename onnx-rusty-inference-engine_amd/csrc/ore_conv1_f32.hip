@@ -53,18 +53,35 @@ struct C3Geo {
   }
 };
 
-template <int MF, int C, int KH, int KW, int S>
-__global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p, const float* __restrict__ wc) {
+template <int MF, int C, int KH, int KW, int S, int SQ>
+__global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p, const float* __restrict__ wc,
+                                                                   C1SqueezeF32 sq) {
   using G = C3Geo<C, KH, KW, S>;
   extern __shared__ __attribute__((aligned(16))) float c3s[];
   float* win = c3s;                          // [C][HR][HC]
   float* ct = c3s + (G::WIN + 3) / 4 * 4;    // [C3_NPX][C3_TS]
   float* sbias = ct + C3_NPX * C3_TS;        // [MF * 32]
+  // SQ: one fragment's pooled values [64 pixels][C3_TS] (the squeeze's B operand) and its bias
+  float* pt = sbias + MF * 32;
+  float* qbias = pt + (SQ ? 64 * C3_TS : 0);
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Mp32 = MF * 32;
   for (int q = tid; q < Mp32; q += 256) sbias[q] = (p.bias && q < p.M) ? p.bias[q] : 0.0f;
+  if constexpr (SQ) {
+    for (int q = tid; q < 16; q += 256) qbias[q] = q < sq.M ? sq.bias[q] : 0.0f;
+  }
 
+  // SQ: the squeeze's A values of this lane for every fragment, once per workgroup (the weights do
+  // not change across tiles; loaded at their use each would expose an L2 round trip)
+  float aqv[SQ ? MF : 1][8];
+  if constexpr (SQ) {
+    const int lj = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) aqv[i][t] = sq.w[(lj < sq.M ? lj : 0) * p.M + 32 * i + 4 * t + lk];
+  }
   // the lane's two patch pixels: window base (bytes) per step kind (plain scalars, not an array: an
   // array indexed by the unrolled step's kind stayed in scratch), conv-tile offset
   int bk0[2], bk1[2], bk2[2], bk3[2], tpx[2];
@@ -178,6 +195,11 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
       __builtin_amdgcn_sched_barrier(0);
     }
 
+    // SQ: the squeeze (<= 16 channels, v_mfma_f32_16x16x4_f32) over the tile's 54 pooled pixels, 16 per
+    // wave: lane (lk, lj) accumulates rows 4 lk + 0..3 of pixel 16 wave + lj, k = channel ascending
+    c3f4 sacc = {0.0f, 0.0f, 0.0f, 0.0f};
+    const int sk = 16 * wave + (lane & 15), slk = lane >> 4;
+
     // per 32-channel fragment: conv tile (bias, Relu, 0 outside the conv plane), 3x3 max, NCHW stores
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
@@ -204,10 +226,37 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
       if (i == 0) store_window();  // every wave is past its K loop: the window is free
       // (pooled output, 4 channels) per task, 432 tasks (a one-round 8-channel variant with all 18
       // reads in flight measured slower: 923 vs 891 us)
+      if constexpr (SQ) {
+        // every thread: two (pooled pixel, 4 channels) of the 64 x 32 block (pixels >= 54: pixel 0)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int t = tid + 256 * u, k = t >> 3, cg = t & 7, kc = k < C3_PR * C3_PC ? k : 0;
+          const int aa = kc / C3_PC, bb = kc - aa * C3_PC;
+          c3f4 mx = {-FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX};
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+              const c3f4 v = *reinterpret_cast<const c3f4*>(ct + ((2 * aa + r) * C3_CC + 2 * bb + s) * C3_TS + 4 * cg);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) mx[e] = fmaxf(mx[e], v[e]);
+            }
+          *reinterpret_cast<c3f4*>(pt + k * C3_TS + 4 * cg) = mx;
+        }
+        __syncthreads();
+        // 8 k-steps of 4 channels: B = pooled (pixel sk, channel 4 t + lk), A = W[lj][32 i + 4 t + lk]
+        const int lj = lane & 15;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const float bq = pt[sk * C3_TS + 4 * t + slk];
+          const float aq = lj < sq.M ? aqv[i][t] : 0.0f;
+          sacc = __builtin_amdgcn_mfma_f32_16x16x4f32(aq, bq, sacc, 0, 0, 0);
+        }
+      }
 #ifdef ORE_EXP_C3_NOPOOL  // timing experiments only (tools/build_exp.sh)
       for (int t = tid; t < 0; t += 256) {
 #else
-      for (int t = tid; t < C3_PR * C3_PC * 8; t += 256) {
+      for (int t = tid; !SQ && t < C3_PR * C3_PC * 8; t += 256) {
 #endif
         const int cg = t / (C3_PR * C3_PC), pp = t - cg * (C3_PR * C3_PC);
         const int aa = pp / C3_PC, bb = pp - aa * C3_PC;
@@ -232,6 +281,17 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
       }
       if (i + 1 < MF) __syncthreads();  // the conv tile is rewritten by the next fragment
     }
+    if constexpr (SQ) {  // squeeze output: bias + Relu, NCHW (rows 4 lk + e of pixel sk)
+      const int aa = sk / C3_PC, bb = sk - aa * C3_PC, ph = ph0 + aa, pw = pw0 + bb;
+      if (sk < C3_PR * C3_PC && ph < p.ep_Ho && pw < p.ep_Wo) {
+        float* yq = sq.y + (long long)img * sq.y_nstride + ph * p.ep_Wo + pw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = 4 * slk + e;
+          if (m < sq.M) yq[(long long)m * sq.y_ps] = fmaxf(sacc[e] + qbias[m], 0.0f);
+        }
+      }
+    }
   }
 }
 
@@ -249,8 +309,8 @@ __global__ __launch_bounds__(256) void pack_c1_f32_kernel(const float* __restric
   }
 }
 
-template <int MF, int C>
-static bool c3_launch(const ConvParams& p, const float* wc, hipStream_t s) {
+template <int MF, int C, int SQ>
+static bool c3_launch(const ConvParams& p, const float* wc, const C1SqueezeF32& sq, hipStream_t s) {
   using G = C3Geo<C, 7, 7, 2>;
   const long long tiles = (long long)p.N * p.ep_tr * p.ep_tc;
   int dev = 0, ncu = 256;
@@ -260,16 +320,16 @@ static bool c3_launch(const ConvParams& p, const float* wc, hipStream_t s) {
   }
   // persistent: as many workgroups as fit on the chip at once (registers and LDS; 3 per CU for
   // conv1's 96 channels), each taking every grid-th tile
-  const unsigned lds = G::LDS + MF * 32 * 4;
+  const unsigned lds = G::LDS + MF * 32 * 4 + (SQ ? 64 * C3_TS * 4 + 16 * 4 : 0);
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_win_pool_f32_kernel<MF, C, 7, 7, 2>, 256, lds) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_win_pool_f32_kernel<MF, C, 7, 7, 2, SQ>, 256, lds) !=
           hipSuccess || per_cu < 1)
     per_cu = 2;
 #ifdef ORE_C3_WPC
   per_cu = ORE_C3_WPC;  // experiment knob
 #endif
   const unsigned grid = (unsigned)std::min<long long>(tiles, (long long)per_cu * ncu);
-  hipLaunchKernelGGL((conv_win_pool_f32_kernel<MF, C, 7, 7, 2>), dim3(grid), dim3(256), lds, s, p, wc);
+  hipLaunchKernelGGL((conv_win_pool_f32_kernel<MF, C, 7, 7, 2, SQ>), dim3(grid), dim3(256), lds, s, p, wc, sq);
   return true;
 }
 
@@ -285,25 +345,33 @@ void launch_pack_c1_f32(const float* w, int M, int K, float* out, hipStream_t s)
   hipLaunchKernelGGL(pack_c1_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, w, M, K, Mp32, out);
 }
 
-bool conv_win_pool_f32_eligible(const ConvParams& p) {
+bool conv_win_pool_f32_eligible(const ConvParams& p, const C1SqueezeF32* sq) {
   const int MF = (p.M + 31) / 32;
+  if (sq && (sq->M < 1 || sq->M > 16 || !sq->w || !sq->bias || !sq->y || sq->y_ps < p.ep_Ho * p.ep_Wo || MF != 3 ||
+             p.C != 3))
+    return false;
   return p.kh == 7 && p.kw == 7 && p.sh == 2 && p.sw == 2 && (p.C == 1 || p.C == 3 || p.C == 4) && MF >= 2 &&
          MF <= 4 && p.ep_tr > 0 && p.ep_tc > 0 && p.x_ps >= p.H * p.W && (long long)p.C * p.x_ps * 4 < (1LL << 31) &&
          p.H < 4096 && p.W < 4096;
 }
 
-void launch_conv_win_pool_f32(const ConvParams& p, const float* wc, hipStream_t s) {
+void launch_conv_win_pool_f32(const ConvParams& p, const float* wc, const C1SqueezeF32* sq, hipStream_t s) {
   const int MF = (p.M + 31) / 32;
+  const C1SqueezeF32 none{};
+  if (sq) {  // the fused squeeze: conv1's geometry (96 channels, 3 inputs)
+    c3_launch<3, 3, 1>(p, wc, *sq, s);
+    return;
+  }
   switch (MF * 8 + p.C) {
-    case 2 * 8 + 1: c3_launch<2, 1>(p, wc, s); break;
-    case 2 * 8 + 3: c3_launch<2, 3>(p, wc, s); break;
-    case 2 * 8 + 4: c3_launch<2, 4>(p, wc, s); break;
-    case 3 * 8 + 1: c3_launch<3, 1>(p, wc, s); break;
-    case 3 * 8 + 3: c3_launch<3, 3>(p, wc, s); break;
-    case 3 * 8 + 4: c3_launch<3, 4>(p, wc, s); break;
-    case 4 * 8 + 1: c3_launch<4, 1>(p, wc, s); break;
-    case 4 * 8 + 3: c3_launch<4, 3>(p, wc, s); break;
-    default: c3_launch<4, 4>(p, wc, s); break;
+    case 2 * 8 + 1: c3_launch<2, 1, 0>(p, wc, none, s); break;
+    case 2 * 8 + 3: c3_launch<2, 3, 0>(p, wc, none, s); break;
+    case 2 * 8 + 4: c3_launch<2, 4, 0>(p, wc, none, s); break;
+    case 3 * 8 + 1: c3_launch<3, 1, 0>(p, wc, none, s); break;
+    case 3 * 8 + 3: c3_launch<3, 3, 0>(p, wc, none, s); break;
+    case 3 * 8 + 4: c3_launch<3, 4, 0>(p, wc, none, s); break;
+    case 4 * 8 + 1: c3_launch<4, 1, 0>(p, wc, none, s); break;
+    case 4 * 8 + 3: c3_launch<4, 3, 0>(p, wc, none, s); break;
+    default: c3_launch<4, 4, 0>(p, wc, none, s); break;
   }
 }
 

@@ -122,7 +122,8 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
                           int64_t x_nstride, int64_t x_ps, const float* wp, const int2* ktab, int64_t M, int64_t kh,
                           int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu,
                           int64_t pkh, int64_t pkw, int64_t psh, int64_t psw, const Window& pwin, float* y,
-                          int64_t y_nstride, int64_t y_ps, const float* wc1 = nullptr);
+                          int64_t y_nstride, int64_t y_ps, const float* wc1 = nullptr,
+                          const C1SqueezeF32* sq1 = nullptr);
 // a fire module fused with the next squeeze (ORE_FUSE_FIRE, ore_fire.hip): x = S [C][H][W] (plane
 // stride x_ps), w1 / w3 in launch_fire_pack layout, ws the squeeze's launch_pack layout (row stride
 // Msp); y = S' [Ms][H][W] (plane stride y_ps, the column count per image)

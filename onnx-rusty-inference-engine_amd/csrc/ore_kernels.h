@@ -44,6 +44,7 @@ struct ConvParams {
   int ep_pt, ep_pl, ep_Ho, ep_Wo, ep_tr, ep_tc;
   int ep_variant;      // pooled-conv kernel (launch_conv_epool): 0 auto, 1 patch, 2 / 3 row walk
   const float* wc1;    // variant 7: weights in launch_pack_c1_f32 layout (null: variant 7 unavailable)
+  const struct C1SqueezeF32* sq1;  // variant 7 with the next 1x1 conv fused in (forces variant 7)
 };
 
 // Per-layer kernel choice and weight layout (see plan_conv in ore_conv.hip).
@@ -224,8 +225,18 @@ constexpr int EPOOL_TILE_BASE = 21;
 // EPOOL_WIN_TILE (after the Winograd / fused-f16 tile ids: ore.Model.TILE_NAMES "epool window f32")
 constexpr int EPOOL_WIN_VARIANT = 7, EPOOL_WIN_TILE = 44;
 inline int epool_tile_id(int variant) { return variant == EPOOL_WIN_VARIANT ? EPOOL_WIN_TILE : EPOOL_TILE_BASE + variant; }
-bool conv_win_pool_f32_eligible(const ConvParams& p);
-void launch_conv_win_pool_f32(const ConvParams& p, const float* wc, hipStream_t s);
+// sq: the pooled map's only consumer, a 1x1 conv + Relu with <= 16 channels (ONNX weights [M][K]),
+// fused in (conv1's geometry only); the pooled map is never stored, y = the squeeze's NCHW output
+struct C1SqueezeF32 {
+  const float* w;
+  const float* bias;
+  int M;
+  float* y;
+  long long y_nstride;
+  int y_ps;
+};
+bool conv_win_pool_f32_eligible(const ConvParams& p, const C1SqueezeF32* sq = nullptr);
+void launch_conv_win_pool_f32(const ConvParams& p, const float* wc, const C1SqueezeF32* sq, hipStream_t s);
 size_t c1_f32_pack_bytes(int M, int K);
 void launch_pack_c1_f32(const float* w, int M, int K, float* out, hipStream_t s);
 bool conv_pool_stream_eligible(const ConvParams& p, int variant);

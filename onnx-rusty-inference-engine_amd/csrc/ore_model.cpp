@@ -942,6 +942,42 @@ ore_status plan(ore_model* m) {
     }
     count_uses(m, m->steps);
   }
+  // (1i) f32 models: the first conv + pool on the window kernel (pooled-conv variant 7) takes the next
+  // 1x1 conv (+ Relu, <= 16 channels) when it is the pooled map's only reader (SqueezeNet's conv1 +
+  // pool1 + fire2/squeeze1x1; the pooled map is never stored).  Bit-identical to the separate squeeze
+  // (the same k-ordered fma chain over the same pooled values).  ORE_C1_SQUEEZE=0 turns it off.
+  if (!m->f16 && !m->x3_all && (m->fusion & ORE_FUSE_CONV_POOL) && (m->fusion & ORE_FUSE_CONV_RELU)) {
+    const char* ec = getenv("ORE_C1_SQUEEZE");
+    const bool on = !(ec && atoi(ec) == 0);
+    for (size_t i = 0; on && i < m->steps.size(); ++i) {
+      Step& cv = m->steps[i];
+      if (cv.kind != S_CONV || cv.plan.f16 || !cv.epool || !cv.wc1 || cv.c1sq || cv.C != 3 || cv.M != 96) continue;
+      const Value& pv = m->values[cv.out];
+      if (pv.uses != 1 || pv.is_output) continue;
+      int qi = -1;
+      for (size_t j = i + 1; j < m->steps.size(); ++j)
+        if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == cv.out || m->steps[j].in1 == cv.out)) { qi = int(j); break; }
+      if (qi < 0) continue;
+      Step& q = m->steps[qi];
+      if (q.kind != S_CONV || !q.relu || q.pool || q.epool || q.plan.f16 || q.plan.x3 || q.kh != 1 || q.kw != 1 ||
+          q.sh != 1 || q.sw != 1 || q.win.pt || q.win.pl || q.in0 != cv.out || q.C != cv.M || q.M > 16 || q.in2 < 0 ||
+          q.in1 < 0 || !m->values[q.in1].cptr)
+        continue;
+      cv.c1sq = true;
+      cv.sq_w = m->values[q.in1].cptr;  // ONNX [M][C][1][1] = [M][K]
+      cv.sq_b = m->values[q.in2].cptr;
+      cv.sq_M = q.M;
+      cv.plan.epv = EPOOL_WIN_VARIANT;
+      m->values[cv.out].elided = true;
+      cv.out = q.out;
+      cv.flops_per_img += q.flops_per_img;
+      cv.bytes_per_img = 4.0 * double(cv.C * cv.H * cv.W) + 4.0 * double(q.M * q.H * q.W);
+      cv.name = cv.name + "+" + q.name;
+      q.kind = S_NOP;
+      q.in0 = -1;
+    }
+    count_uses(m, m->steps);
+  }
   // (1f) ORE_LOAD_X3: every conv / matmul not taken by an f32-MFMA fusion above runs its x3 plan
   if (m->x3)
     for (auto& st : m->steps)
@@ -1240,9 +1276,13 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       if (s.epool) {
         ctx->mapped_lo = m->arena_alloc;  // the arena and its 4 KiB lead are mapped
         ctx->mapped_hi = m->arena ? m->arena + m->arena_bytes : nullptr;
+        const int64_t pplane = s.ep_win.Ho * s.ep_win.Wo;
+        const C1SqueezeF32 sq1{static_cast<const float*>(s.sq_w), s.sq_b, int(s.sq_M), y.p, y.nstride,
+                               int(y.ps ? y.ps : pplane)};
         const ore_status r = run_conv_epool(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.ktab, s.M, s.kh,
                                             s.kw, bias, s.win, s.sh, s.sw, s.relu, s.ep_kh, s.ep_kw, s.ep_sh, s.ep_sw,
-                                            s.ep_win, y.p, y.nstride, y.ps, s.wc1);
+                                            s.ep_win, s.c1sq ? nullptr : y.p, y.nstride, s.c1sq ? pplane : y.ps, s.wc1,
+                                            s.c1sq ? &sq1 : nullptr);
         ctx->mapped_lo = ctx->mapped_hi = nullptr;
         s.ran_tile = last_conv_tile;
         return r;
@@ -1696,6 +1736,12 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
   // every output is the same k-ordered MFMA chain)
   for (size_t k = 0; k < m->exec_steps.size() && !st; ++k) {
     Step& s = m->steps[m->exec_steps[k]];
+    if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.c1sq) {  // the fused squeeze: the window kernel only
+      s.plan.epv = EPOOL_WIN_VARIANT;
+      m->base_steps[m->exec_steps[k]].plan.epv = EPOOL_WIN_VARIANT;
+      st = launch_step(m, s, n);
+      continue;
+    }
     if (s.kind == S_CONV && s.epool && !s.plan.f16) {  // f32 pooled conv: patch vs row-walk kernels
       int best = 0;
       float best_ms = 1e30f;

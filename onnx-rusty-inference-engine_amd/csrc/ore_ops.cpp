@@ -283,7 +283,7 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
                           int64_t x_nstride, int64_t x_ps, const float* wp, const int2* ktab, int64_t M, int64_t kh,
                           int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu,
                           int64_t pkh, int64_t pkw, int64_t psh, int64_t psw, const Window& pwin, float* y,
-                          int64_t y_nstride, int64_t y_ps, const float* wc1) {
+                          int64_t y_nstride, int64_t y_ps, const float* wc1, const C1SqueezeF32* sq1) {
   if (N == 0) return ORE_OK;
   if (pln.f16 || pln.window) return set_error(ctx, ORE_ERR_INVALID, "internal: the pooled epilogue is f32 gather only");
   if (x_ps == 0) x_ps = H * W;
@@ -316,6 +316,7 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
   p.ep_tr = tr; p.ep_tc = tc;
   p.ep_variant = pln.epv;
   p.wc1 = wc1;
+  p.sq1 = sq1;
   {  // mapped bytes before x (as run_conv): the row-walking 3x3 kernel reads a few of them, masked
     const char* xc = reinterpret_cast<const char*>(x);
     int64_t g = int64_t(reinterpret_cast<uintptr_t>(x) & 4095);
@@ -331,6 +332,8 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
   if (!p.is1x1 && !ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
   launch_conv_epool(p, ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());
+  if (sq1 && last_conv_tile != EPOOL_WIN_TILE)
+    return set_error(ctx, ORE_ERR_INVALID, "internal: the fused first conv + squeeze declined its launch");
   return ORE_OK;
 }
 

@@ -238,11 +238,11 @@ def test_autotune_keeps_results(gpu_ctx, precision):
     np.testing.assert_array_equal(_np(out), before)  # the autotune pass leaves a real result
     np.testing.assert_array_equal(_np(m.run(x)), before)
     tiles1 = m.tiles()
-    # f32 at batch 8: 26 conv launches (the fire fusion waits for >= 65536 columns); f16: 11 (conv1 +
-    # pool1 + fire2's squeeze, 5 fused fire modules, 2 fire + pool + squeeze, fire9's expands, conv10)
-    assert len(tiles1) == len(tiles0) and sum(t >= 0 for t in tiles1) == (26 if precision == "f32" else 11)
-    # the choice survives re-planning (f16: the same fused plan; f32: the unfused one)
-    m.set_fusion(0 if precision == "f32" else ore.FUSE_ALL)
+    # f32 at batch 8: 25 conv launches (conv1 + pool1 + fire2's squeeze in one; the fire fusion waits
+    # for >= 65536 columns); f16: 11 (conv1 + pool1 + fire2's squeeze, 5 fused fire modules, 2 fire +
+    # pool + squeeze, fire9's expands, conv10)
+    assert len(tiles1) == len(tiles0) and sum(t >= 0 for t in tiles1) == (25 if precision == "f32" else 11)
+    m.set_fusion(ore.FUSE_ALL)  # the choice survives re-planning
     a, b = [t for t in tiles1 if t >= 0], [t for t in m.tiles() if t >= 0]
     # convs with a pooled epilogue (conv1 + pool1, fire4 / fire8 expands + pool3 / pool5): their kernel
     # choice (patch vs row walk) has no unfused counterpart
@@ -657,3 +657,77 @@ def test_two_contexts_large_lds_variant(monkeypatch):
         t.join()
     assert not errs, errs
     np.testing.assert_array_equal(res[0], res[1])
+
+
+def _conv_pool_squeeze_model(H, W, M, Q, pool_pads):
+    """x (3 channels) -> Conv 7x7 / 2 + Relu -> MaxPool 3x3 / 2 -> Conv 1x1 (Q) + Relu -> GAP."""
+    from ore import onnx_wire as wr
+    rng = np.random.default_rng(H * 31 + W + M + Q)
+    w1 = (rng.standard_normal((M, 3, 7, 7)) * np.sqrt(2.0 / 147)).astype(np.float32)
+    b1 = rng.uniform(-0.1, 0.1, M).astype(np.float32)
+    w2 = (rng.standard_normal((Q, M, 1, 1)) * np.sqrt(2.0 / M)).astype(np.float32)
+    b2 = rng.uniform(-0.1, 0.1, Q).astype(np.float32)
+    nodes = [wr.encode_node("Conv", ["x", "w1", "b1"], ["c"], attrs=[wr.encode_attr_ints("strides", [2, 2]),
+                                                                      wr.encode_attr_ints("pads", [0] * 4)]),
+             wr.encode_node("Relu", ["c"], ["r"]),
+             wr.encode_node("MaxPool", ["r"], ["p"], attrs=[
+                 wr.encode_attr_ints("kernel_shape", [3, 3]), wr.encode_attr_ints("strides", [2, 2]),
+                 wr.encode_attr_string("auto_pad", "NOTSET"), wr.encode_attr_ints("pads", pool_pads)]),
+             wr.encode_node("Conv", ["p", "w2", "b2"], ["q"], attrs=[wr.encode_attr_ints("strides", [1, 1]),
+                                                                     wr.encode_attr_ints("pads", [0] * 4)]),
+             wr.encode_node("Relu", ["q"], ["qr"]),
+             wr.encode_node("GlobalAveragePool", ["qr"], ["y"])]
+    inits = [wr.encode_tensor(n, a) for n, a in (("w1", w1), ("b1", b1), ("w2", w2), ("b2", b2))]
+    vinfo = [wr.encode_value_info("x", (1, 3, H, W))] + [wr.encode_value_info(n, a.shape) for n, a in
+                                                          (("w1", w1), ("b1", b1), ("w2", w2), ("b2", b2))]
+    return wr.encode_model("cps", nodes, inits, vinfo, [wr.encode_value_info("y", (1, Q, 1, 1))])
+
+
+@pytest.mark.parametrize("case", [(67, 71, 16, [0, 0, 0, 0]), (40, 45, 12, [0, 0, 1, 1])])
+def test_conv_pool_squeeze_fused_bit_identical(gpu_ctx, case, monkeypatch):
+    """f32: conv1 + Relu + pool1 + the next 1x1 conv + Relu in one window-kernel launch (pooled-conv
+    variant 7 with the squeeze inside, the pooled map never stored) equals the separate launches
+    (ORE_C1_SQUEEZE=0) bit for bit, and the oracle within the conv tolerance."""
+    import ore
+    import oracle
+    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "8")
+    H, W, Q, pads = case
+    mb = _conv_pool_squeeze_model(H, W, 96, Q, pads)
+    x = (np.random.default_rng(H + W).standard_normal((3, 3, H, W)) * 20).astype(np.float32)
+    vals = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("ORE_C1_SQUEEZE", on)
+        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+        y = _np(m.run(_t(x)))
+        vals.append((y, m.read_value("qr")))
+        names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+        if on == "1":
+            assert names == ["epool window f32"], names
+            with pytest.raises(ore.OreError):
+                m.read_value("p")  # never stored
+        else:
+            assert len(names) == 2, names
+        m.close()
+    np.testing.assert_array_equal(vals[0][1], vals[1][1])
+    np.testing.assert_array_equal(vals[0][0], vals[1][0])
+    ref = oracle.Model(mb).run(x, Q)
+    np.testing.assert_allclose(vals[0][0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_squeezenet_conv1_squeeze_fused(gpu_ctx, monkeypatch):
+    """SqueezeNet-1.0 @224 f32: conv1 + pool1 + fire2/squeeze1x1 in one launch; probabilities equal the
+    plan without that fusion bit for bit."""
+    import ore
+    from ore import squeezenet
+    mb = squeezenet.build(224)
+    x = _t(squeezenet.synthetic_input(3, 224, seed=29))
+    outs = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("ORE_C1_SQUEEZE", on)
+        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        outs.append(_np(m.run(x)))
+        first = ore.Model.TILE_NAMES[m.tiles()[0]]
+        assert (first == "epool window f32") == (on == "1"), first
+        m.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
