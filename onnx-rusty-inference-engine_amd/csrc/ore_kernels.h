@@ -121,6 +121,22 @@ void launch_fire_pack_wino(const float* w, int M, int C, float* u, hipStream_t s
 // W [M][K] -> the fire kernel's row-permuted K-major packing (M % 64 == 0)
 void launch_fire_pack(const float* w, int M, int K, float* wf, hipStream_t s);
 
+// MaxPool 3x3 / stride 2 + its only reader, a 1x1 conv (+ Relu), f32 NCHW (ore_pool_conv.hip;
+// SqueezeNet pool5 + fire9/squeeze1x1): x [C][H][W] (plane stride x_ps), wp the conv's K-major
+// packing [Kp][Mp], y [M][Hp][Wp] (plane stride y_ps); C % 32 == 0, M <= 64, Wp <= 16
+struct PoolConvParams {
+  const float* x;
+  const float* wp;
+  const float* bias;
+  float* y;
+  int N, C, H, W, Hp, Wp, pt, pl, M, Mp, Kp;
+  int x_ps, y_ps;
+  long long x_nstride, y_nstride;
+  int relu;
+};
+bool pool_conv1x1_f32_eligible(const PoolConvParams& p);
+void launch_pool_conv1x1_f32(const PoolConvParams& p, hipStream_t s);
+
 // f16 models: the fused fire module (ore_fire_f16.hip) on NHWC f16 values (pixel strides in
 // elements, image strides in elements); weights packed by launch_fire_pack_f16
 struct FireF16Params {

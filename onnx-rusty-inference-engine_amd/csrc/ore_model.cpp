@@ -978,6 +978,38 @@ ore_status plan(ore_model* m) {
     }
     count_uses(m, m->steps);
   }
+  // (1j) f32: a 3x3 / stride-2 MaxPool left standing (SqueezeNet pool5) whose only reader is a 1x1
+  // Conv (+ Relu) with <= 64 channels runs inside that conv (pool_conv1x1_f32_kernel, the pooled map
+  // never stored; the (1b) step form, run_conv_pool).  Bit-identical to maxpool_kernel + the conv.
+  // ORE_POOL_SQUEEZE=0 turns it off.
+  if (!m->f16 && !m->x3_all && (m->fusion & ORE_FUSE_CONV_POOL)) {
+    const char* ep = getenv("ORE_POOL_SQUEEZE");
+    const bool on = !(ep && atoi(ep) == 0);
+    for (size_t i = 0; on && i < m->steps.size(); ++i) {
+      Step& pl = m->steps[i];
+      if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2) continue;
+      const int v = pl.out;
+      if (m->values[v].uses != 1 || m->values[v].is_output || m->values[pl.in0].es != 4 || m->values[pl.in0].nhwc) continue;
+      int ci = -1;
+      for (size_t j = i + 1; j < m->steps.size(); ++j)
+        if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == v || m->steps[j].in1 == v)) { ci = int(j); break; }
+      if (ci < 0) continue;
+      Step& cv = m->steps[ci];
+      if (cv.kind != S_CONV || cv.pool || cv.epool || cv.in0 != v || cv.kh != 1 || cv.kw != 1 || cv.sh != 1 ||
+          cv.sw != 1 || cv.win.pt || cv.win.pl || cv.plan.window || cv.plan.f16 || cv.plan.x3 || cv.plan.wino ||
+          cv.M > 64 || cv.C % 32 || pl.win.Wo > 16 || pl.win.pt > 2 || pl.win.pl > 2)
+        continue;
+      cv.pool = true;
+      cv.in0 = pl.in0;
+      cv.pH = pl.H; cv.pW = pl.W; cv.psh = pl.sh; cv.psw = pl.sw; cv.pwin = pl.win;
+      cv.bytes_per_img = 4.0 * double(pl.C * pl.H * pl.W) + 4.0 * double(cv.M * cv.H * cv.W);
+      cv.name = pl.name + "+" + cv.name;
+      m->values[v].elided = true;
+      pl.kind = S_NOP;
+      pl.in0 = -1;
+    }
+    count_uses(m, m->steps);
+  }
   // (1f) ORE_LOAD_X3: every conv / matmul not taken by an f32-MFMA fusion above runs its x3 plan
   if (m->x3)
     for (auto& st : m->steps)

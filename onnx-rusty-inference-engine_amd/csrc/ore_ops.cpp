@@ -346,6 +346,22 @@ ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int6
   const int64_t P = pwin.Ho * pwin.Wo;
   if (y_ps == 0) y_ps = P;
   if (pln.f16 || x_es != 4) return set_error(ctx, ORE_ERR_INVALID, "internal: the pooled 1x1 conv is f32 only");
+  {  // 3x3 / stride-2 pools: pool_conv1x1_f32_kernel (LDS-staged rows, MFMA squeeze), else the gather
+    PoolConvParams q{};
+    q.x = x; q.wp = wp; q.bias = bias; q.y = y;
+    q.N = int(N); q.C = int(C); q.H = int(pH); q.W = int(pW); q.Hp = int(pwin.Ho); q.Wp = int(pwin.Wo);
+    q.pt = int(pwin.pt); q.pl = int(pwin.pl); q.M = int(M); q.Mp = pln.Mp; q.Kp = pln.krows;
+    q.x_ps = int(x_ps); q.y_ps = int(y_ps); q.x_nstride = x_nstride; q.y_nstride = y_nstride;
+    q.relu = relu ? 1 : 0;
+    const char* e = getenv("ORE_POOL_CONV_GATHER");  // experiments: the conv-gather kernel instead
+    if (psh == 2 && psw == 2 && pwin.Ho > 0 && !(e && atoi(e) != 0) && fits_i32(x_nstride * N + 256) &&
+        fits_i32(y_nstride * N + 256) && pool_conv1x1_f32_eligible(q) && !pln.window && !pln.x3 && !pln.wino) {
+      // the 3x3 window is implied by the (1b) / (1j) plan (kernel_shape 3x3)
+      launch_pool_conv1x1_f32(q, ctx->stream);
+      ORE_HIP_CHECK(ctx, hipGetLastError());
+      return ORE_OK;
+    }
+  }
   ConvParams p{};
   p.x = x; p.wp = wp; p.ktab = nullptr; p.bias = bias; p.y = y;
   p.N = int(N); p.C = int(C); p.H = int(pwin.Ho); p.W = int(pwin.Wo);

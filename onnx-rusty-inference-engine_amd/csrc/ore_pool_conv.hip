@@ -1,0 +1,146 @@
+// MaxPool 3x3 / stride 2 + the 1x1 Conv (+ Relu) that is its only reader, f32 NCHW, in one launch:
+// SqueezeNet's pool5 -> fire9/squeeze1x1 (reference max_pool_op.rs:157-360, convolution_op.rs:94-517;
+// the walker used to run maxpool_kernel (382 MB in, 95 MB out at B = 256) and then the squeeze
+// (95 MB in again)).  The pooled map never reaches HBM.
+//
+// One workgroup = two pooled rows of one image (Wp <= 16 columns each: one 16-pixel fragment per
+// row) x all M <= 64 output channels (four waves x 16 channels, v_mfma_f32_16x16x4_f32).  Per chunk
+// of 32 input channels:
+//   * the 5 input rows the two pooled rows read (columns of the whole row) go global -> registers
+//     -> LDS, raw buffer loads with outside-the-image offsets reading 0 (maxpool_kernel's zero
+//     padding); the next chunk's loads are in flight while this one pools and multiplies;
+//   * every thread takes (pooled pixel, channel) maxima from -FLT_MAX over the nine window values
+//     (maxpool_kernel's arithmetic) into an LDS block [32 channels][32 pixels];
+//   * each wave runs the chunk's 8 k-steps (k = channel, ascending over the chunks: the standalone
+//     1x1 conv's fma chain) for its 16 channels x both pixel fragments; A from L2 in the conv's
+//     K-major packing (wp[k][Mp]).
+// Bit-identical to maxpool_kernel + the separate 1x1 conv (tests/test_model_gpu.py).
+#include <float.h>
+#include <hip/hip_runtime.h>
+
+#include "ore_kernels.h"
+
+namespace ore {
+
+namespace {
+
+typedef float ps4 __attribute__((ext_vector_type(4)));
+
+constexpr int PS_CH = 32;        // input channels per chunk
+constexpr int PS_ROWS = 5;       // input rows of two pooled rows (3x3, stride 2)
+constexpr int PS_WMAX = 33;      // input columns held per row (Wp <= 16)
+constexpr int PS_IN = PS_CH * PS_ROWS * PS_WMAX;  // floats of one staged chunk
+constexpr int PS_NQ = (PS_IN + 255) / 256;
+
+__global__ __launch_bounds__(256, 2) void pool_conv1x1_f32_kernel(PoolConvParams p) {
+  __shared__ float in_s[PS_IN];            // [ch][row][col]
+  __shared__ float pt[PS_CH][33];          // pooled block [ch][pixel n * 16 + col] (+1 pad)
+  const int tid = threadIdx.x, lane = tid & 63, lk = lane >> 4, lj = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bands = (p.Hp + 1) / 2;
+  const int img = blockIdx.x / bands, pr0 = (blockIdx.x - img * bands) * 2;
+  const int ih0 = pr0 * 2 - p.pt, iw0 = -p.pl;  // input coordinates of staged (row 0, col 0)
+  const int wcols = 2 * (p.Wp - 1) + 3;         // input columns the pooled row reads
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.x + (long long)img * p.x_nstride), (short)0, p.C * p.x_ps * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0, p.Kp * p.Mp * 4, 0x00020000);
+
+  // this thread's staged elements q = tid + 256 u: (channel, row, column) -> byte offset in the
+  // image minus the chunk's channel offset (or past the records: 0)
+  int qo[PS_NQ];
+#pragma unroll
+  for (int u = 0; u < PS_NQ; ++u) {
+    const int q = tid + 256 * u;
+    const int c = q / (PS_ROWS * PS_WMAX), rc = q - c * (PS_ROWS * PS_WMAX), r = rc / PS_WMAX, cc = rc - r * PS_WMAX;
+    const int ih = ih0 + r, iw = iw0 + cc;
+    const bool in = q < PS_IN && cc < wcols && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+    qo[u] = in ? (c * p.x_ps + ih * p.W + iw) * 4 : (int)0x80000000;
+  }
+  float xv[PS_NQ];
+  auto load_chunk = [&](int c0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < PS_NQ; ++u)
+      xv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            xr, qo[u] < 0 ? (int)0x80000000 : qo[u] + c0 * p.x_ps * 4, 0, 0));
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  ps4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // rows 4 lk + e of channels 16 wave .., pixel lj
+  const int nch = p.C / PS_CH;
+  const int m0 = 16 * wave;
+  // the squeeze's A values of a chunk (k = 32 ci + 4 t + lk, row m0 + lj), one chunk ahead
+  float acur[8], anxt[8];
+  auto load_a = [&](float (&dst)[8], int ci) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      dst[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                             wr, ((ci * PS_CH + 4 * t + lk) * p.Mp + m0 + lj) * 4, 0, 0));
+  };
+  load_a(acur, 0);
+  load_chunk(0);
+  for (int ci = 0; ci < nch; ++ci) {
+    __syncthreads();  // the previous chunk's staged rows are pooled
+#pragma unroll
+    for (int u = 0; u < PS_NQ; ++u)
+      if (tid + 256 * u < PS_IN) in_s[tid + 256 * u] = xv[u];
+    __syncthreads();
+    if (ci + 1 < nch) {  // in flight during this chunk
+      load_chunk((ci + 1) * PS_CH);
+      load_a(anxt, ci + 1);
+    }
+    // pooled maxima: 32 channels x 2 rows x 16 columns (columns >= Wp: column 0's value, unused)
+    for (int t = tid; t < PS_CH * 32; t += 256) {
+      const int c = t >> 5, pxi = t & 31, n = pxi >> 4, col = pxi & 15, cl = col < p.Wp ? col : 0;
+      const float* base = in_s + (c * PS_ROWS + 2 * n) * PS_WMAX + 2 * cl;
+      float m = -FLT_MAX;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) m = fmaxf(m, base[r * PS_WMAX + s]);
+      pt[c][pxi] = m;
+    }
+    __syncthreads();
+    // squeeze k-steps of this chunk: k = 32 ci + 4 t + lk
+    if (m0 < p.M) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(acur[t], pt[4 * t + lk][16 * n + lj], acc[n], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acur[t] = anxt[t];
+  }
+  // bias + Relu, NCHW stores: channel m0 + 4 lk + e, pooled pixel (pr0 + n, lj)
+  if (m0 >= p.M || lj >= p.Wp) return;
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    if (pr0 + n >= p.Hp) continue;
+    float* yp = p.y + (long long)img * p.y_nstride + (pr0 + n) * p.Wp + lj;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + 4 * lk + e;
+      if (m >= p.M) continue;
+      float v = acc[n][e] + (p.bias ? p.bias[m] : 0.0f);
+      if (p.relu) v = fmaxf(v, 0.0f);
+      yp[(long long)m * p.y_ps] = v;
+    }
+  }
+}
+
+}  // namespace
+
+bool pool_conv1x1_f32_eligible(const PoolConvParams& p) {
+  return p.C % PS_CH == 0 && p.C > 0 && p.M >= 1 && p.M <= 64 && p.Wp >= 1 && p.Wp <= 16 && p.Hp >= 1 &&
+         2 * (p.Wp - 1) + 3 <= PS_WMAX && p.pt >= 0 && p.pl >= 0 && p.pt <= 2 && p.pl <= 2 && p.x_ps >= p.H * p.W &&
+         (long long)p.C * p.x_ps * 4 < (1LL << 31) && (long long)p.Kp * p.Mp * 4 < (1LL << 31) && p.Kp >= p.C &&
+         p.Mp >= p.M && p.y_ps >= p.Hp * p.Wp;
+}
+
+void launch_pool_conv1x1_f32(const PoolConvParams& p, hipStream_t s) {
+  const long long grid = (long long)p.N * ((p.Hp + 1) / 2);
+  hipLaunchKernelGGL(pool_conv1x1_f32_kernel, dim3((unsigned)grid), dim3(256), 0, s, p);
+}
+
+}  // namespace ore

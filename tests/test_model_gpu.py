@@ -731,3 +731,76 @@ def test_squeezenet_conv1_squeeze_fused(gpu_ctx, monkeypatch):
         assert (first == "epool window f32") == (on == "1"), first
         m.close()
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def _pool_squeeze_model(C, H, W, M, pool_pads, relu=True):
+    """x -> Relu -> MaxPool 3x3 / 2 -> Conv 1x1 (M) [+ Relu] -> GAP (the pooled map's only reader is the conv)."""
+    from ore import onnx_wire as wr
+    rng = np.random.default_rng(C + H * 3 + W + M)
+    w = (rng.standard_normal((M, C, 1, 1)) * np.sqrt(2.0 / C)).astype(np.float32)
+    b = rng.uniform(-0.1, 0.1, M).astype(np.float32)
+    nodes = [wr.encode_node("Relu", ["x"], ["xr"]),
+             wr.encode_node("MaxPool", ["xr"], ["p"], attrs=[
+                 wr.encode_attr_ints("kernel_shape", [3, 3]), wr.encode_attr_ints("strides", [2, 2]),
+                 wr.encode_attr_string("auto_pad", "NOTSET"), wr.encode_attr_ints("pads", pool_pads)]),
+             wr.encode_node("Conv", ["p", "w", "b"], ["q"], attrs=[wr.encode_attr_ints("strides", [1, 1]),
+                                                                   wr.encode_attr_ints("pads", [0] * 4)])]
+    out = "q"
+    if relu:
+        nodes.append(wr.encode_node("Relu", ["q"], ["qr"]))
+        out = "qr"
+    nodes.append(wr.encode_node("GlobalAveragePool", [out], ["y"]))
+    inits = [wr.encode_tensor("w", w), wr.encode_tensor("b", b)]
+    vinfo = [wr.encode_value_info("x", (1, C, H, W)), wr.encode_value_info("w", w.shape), wr.encode_value_info("b", b.shape)]
+    return wr.encode_model("ps", nodes, inits, vinfo, [wr.encode_value_info("y", (1, M, 1, 1))]), out
+
+
+@pytest.mark.parametrize("case", [
+    (512, 27, 27, 64, [0, 0, 0, 0], True),   # SqueezeNet pool5 + fire9/squeeze1x1
+    (64, 20, 31, 48, [0, 0, 1, 1], True),    # ceil-mode pads, 16 pooled columns, M = 48
+    (32, 9, 7, 10, [1, 1, 1, 1], False),     # padded on all sides, no Relu (negative outputs), M = 10
+])
+def test_pool_squeeze_fused_bit_identical(gpu_ctx, case, monkeypatch):
+    """f32: a 3x3 / stride-2 MaxPool and the 1x1 conv that is its only reader in one launch
+    (pool_conv1x1_f32_kernel, the pooled map never stored) equal maxpool_kernel + the separate conv
+    (ORE_POOL_SQUEEZE=0) bit for bit, and the oracle within the conv tolerance."""
+    import ore
+    import oracle
+    C, H, W, M, pads, relu = case
+    mb, out = _pool_squeeze_model(C, H, W, M, pads, relu)
+    x = np.random.default_rng(C + H).standard_normal((3, C, H, W)).astype(np.float32)
+    vals = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("ORE_POOL_SQUEEZE", on)
+        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+        y = _np(m.run(_t(x)))
+        vals.append((y, m.read_value(out)))
+        if on == "1":
+            with pytest.raises(ore.OreError):
+                m.read_value("p")  # never stored
+        else:
+            assert m.read_value("p").shape[1] == C
+        m.close()
+    np.testing.assert_array_equal(vals[0][1], vals[1][1])
+    np.testing.assert_array_equal(vals[0][0], vals[1][0])
+    ref = oracle.Model(mb).run(x, M)
+    np.testing.assert_allclose(vals[0][0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_squeezenet_pool_squeeze_fused(gpu_ctx, monkeypatch):
+    """SqueezeNet-1.0 @224 f32: pool5 + fire9/squeeze1x1 in one launch; probabilities equal the plan
+    without that fusion bit for bit."""
+    import ore
+    from ore import squeezenet
+    mb = squeezenet.build(224)
+    x = _t(squeezenet.synthetic_input(3, 224, seed=31))
+    outs, nsteps = [], []
+    for on in ("1", "0"):
+        monkeypatch.setenv("ORE_POOL_SQUEEZE", on)
+        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        outs.append(_np(m.run(x)))
+        nsteps.append(len(m.tiles()))
+        m.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
+    assert nsteps[0] == nsteps[1] - 1  # pool5 is no longer a launch of its own
