@@ -18,6 +18,9 @@
 //     standalone squeeze, with its weights in the standard K-major packing (launch_pack).
 #include <hip/hip_runtime.h>
 
+#include <float.h>
+
+#include <atomic>
 #include <type_traits>
 
 #include "ore_kernels.h"
@@ -243,21 +246,286 @@ __global__ __launch_bounds__(256, ORE_FIRE_MINB) void fire_kernel(FireParams p) 
     }
 }
 
+
+// ---- pooled form: fire module -> 3x3 / stride-2 MaxPool -> the next squeeze (SqueezeNet fire4 ->
+// pool3 -> fire5/squeeze1x1).  The unfused f32 graph runs the two expands with pooled epilogues
+// (conv_pool_stream_kernel, 2 launches, the pooled concat written to HBM) and the squeeze as a third
+// launch that reads it back.  Here one workgroup (8 waves) owns a band of PR pooled rows of one image:
+//   * the band's conv rows cr0 .. cr1 are a contiguous run of the NCHW plane; wave w computes its
+//     64 pixels of it with fire_kernel's streaming K loop (same operands, same k = (c, r, s) chains);
+//   * per 64-channel chunk of the concat (e1 chunks, then e3 chunks) every wave writes bias + Relu
+//     of its pixels to an LDS conv tile [64 channels][FP_TS] (132 KB: one workgroup per CU, two
+//     waves per SIMD), barrier; then waves 0-3 take the 3x3 maxima (from -FLT_MAX, outside taps read
+//     0.0f from a zeroed pad slot: maxpool_kernel's arithmetic) of their two 16-pixel pooled
+//     fragments and run the chunk's 16 squeeze k-steps (k = concat channel, ascending over the
+//     chunks: the standalone 1x1 conv's chain) while waves 4-7 already run the next chunk's K loop;
+//   * a barrier before the next tile write frees the tile.
+// Bit-identical to the two pooled-epilogue convs + the separate squeeze (tests/test_model_gpu.py).
+constexpr int FP_WAVES = 8, FP_PIX = 64 * FP_WAVES, FP_TS = FP_PIX + 4;  // conv tile row stride (floats)
+constexpr int FP_LDS = 64 * FP_TS * 4;
+
+template <int MFS, int D>
+__global__ __launch_bounds__(512, 1) void fire_pool_kernel(FireParams p) {
+  extern __shared__ __attribute__((aligned(16))) float fp_tile[];
+  const int lane = threadIdx.x & 63, lk = lane >> 4, lj = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H = p.H, W = p.W, Wp = p.Wp;
+  const int nbands = (p.Hp + p.PR - 1) / p.PR;
+  const int img = blockIdx.x / nbands, band = blockIdx.x - img * nbands;
+  const int pr0 = band * p.PR, npr = min(p.PR, p.Hp - pr0);
+  const int cr0 = max(0, 2 * pr0 - p.ppt), cr1 = min(H - 1, 2 * (pr0 + npr - 1) - p.ppt + 2);
+  const int ncp = (cr1 - cr0 + 1) * W;  // conv pixels of the band (<= FP_PIX: host)
+  const bool clive = wave * 64 < ncp;   // a wave with none of them skips the K loops
+  if (threadIdx.x < 64)                 // the pad slots of every channel row: the pool's outside taps
+    *reinterpret_cast<fi_floatx4*>(fp_tile + threadIdx.x * FP_TS + FP_PIX) = fi_floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- expand operands (fire_kernel's): this lane's 4 conv pixels pix .. pix + 3 of the plane
+  const int pix = cr0 * W + wave * 64 + 4 * lj;
+  const int xlead = p.x_lead;
+  const int xoff1 = xlead + (img * (int)p.x_nstride + lk * p.x_ps + pix) * 4;
+  const int xoff3 = (img * (int)p.x_nstride + pix) * 4;
+  unsigned tmask[4];
+  {
+    const int oh0 = pix / W, ow0 = pix - oh0 * W;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool wrap = ow0 + q >= W;
+      const int oh = oh0 + (wrap ? 1 : 0), ow = ow0 + q - (wrap ? W : 0);
+      unsigned cm = 0, m = 0;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) cm |= ((unsigned)(ow - 1 + s) < (unsigned)W ? 1u : 0u) << s;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+        if (oh < H && (unsigned)(oh - 1 + r) < (unsigned)H) m |= cm << (r * 3);
+      tmask[q] = m;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<char*>(reinterpret_cast<const char*>(p.x) - xlead), (short)0, (int)p.x_bytes + xlead, 0x00020000);
+  const int K1 = p.C, K3 = 9 * p.C;
+  const __amdgpu_buffer_rsrc_t w1r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.w1), (short)0, ((K1 + 31) & ~31) * p.E1 * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t w3r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.w3), (short)0, ((K3 + 31) & ~31) * p.E3 * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.ws), (short)0, (((p.E1 + p.E3) + 31) & ~31) * p.Msp * 4, 0x00020000);
+  const int tap0 = xlead - (W + 1) * 4;
+
+  // ---- pooled fragments of waves 0-3: fragment 2 wave + g, pooled pixel kp = 16 (2 wave + g) + lj
+  const int P = npr * Wp, nfrag = (P + 15) >> 4;
+  const bool pwave = wave < 4 && 2 * wave < nfrag;
+  int tap[2][9];  // conv-tile offsets of the 9 window taps (channel row lk; outside taps: the pad slot)
+  int kp[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    kp[g] = 16 * (2 * wave + g) + lj;
+    const int kk = kp[g] < P ? kp[g] : 0;
+    const int pa = pr0 + kk / Wp, pb = kk - (kk / Wp) * Wp;
+    const int ih0 = 2 * pa - p.ppt, iw0 = 2 * pb - p.ppl;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int ih = ih0 + r, iw = iw0 + s;
+        const bool in = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        tap[g][3 * r + s] = lk * FP_TS + (in ? (ih - cr0) * W + iw : FP_PIX);
+      }
+  }
+  const bool g1 = 2 * wave + 1 < nfrag;  // (wave-uniform) the second fragment has pixels
+  fi_floatx4 accs[MFS][2];
+#pragma unroll
+  for (int fs = 0; fs < MFS; ++fs) accs[fs][0] = accs[fs][1] = fi_floatx4{0.f, 0.f, 0.f, 0.f};
+
+  auto chunk = [&](auto mode_tag, int c0, int cat0) __attribute__((always_inline)) {
+    constexpr int MODE = decltype(mode_tag)::value;
+    const __amdgpu_buffer_rsrc_t wr = MODE == 0 ? w1r : w3r;
+    const int Mrow = MODE == 0 ? p.E1 : p.E3;
+    const int nks = (MODE == 0 ? K1 : K3) >> 2;
+    const int aoff = (lk * Mrow + c0 + 4 * lj) * 4, astep = 16 * Mrow;
+    const int xstep = 16 * p.x_ps;
+    int tt = lk, cx = 0;
+    fi_floatx4 acc[4][4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[f][q] = fi_floatx4{0.f, 0.f, 0.f, 0.f};
+    if (clive) {
+      fi_floatx4 rb[D], ra[D];
+      int rt[D];
+#define FP_LOAD(SLOT, S)                                                                                 \
+      {                                                                                                  \
+        const int s_ = (S);                                                                              \
+        ra[SLOT] = __builtin_bit_cast(fi_floatx4, __builtin_amdgcn_raw_buffer_load_b128(wr, aoff, s_ * astep, 0)); \
+        if constexpr (MODE == 0) {                                                                       \
+          rb[SLOT] = __builtin_bit_cast(fi_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, xoff1, s_ * xstep, 0)); \
+        } else {                                                                                         \
+          const int r_ = (int)(__umul24((unsigned)tt, 11u) >> 5);                                        \
+          const int to_ = cx + tap0 + 4 * ((int)__umul24((unsigned)r_, (unsigned)(W - 3)) + tt);        \
+          rb[SLOT] = __builtin_bit_cast(fi_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, xoff3 + to_, 0, 0)); \
+          rt[SLOT] = tt;                                                                                 \
+          tt += 4;                                                                                       \
+          if (tt >= 9) { tt -= 9; cx += 4 * p.x_ps; }                                                    \
+        }                                                                                                \
+      }
+#define FP_MFMA(SLOT)                                                                                    \
+      {                                                                                                  \
+        if constexpr (MODE == 1) {                                                                       \
+          const int4 v_ = __builtin_bit_cast(int4, rb[SLOT]);                                            \
+          int4 w_;                                                                                       \
+          w_.x = v_.x & __builtin_amdgcn_sbfe((int)tmask[0], rt[SLOT], 1);                               \
+          w_.y = v_.y & __builtin_amdgcn_sbfe((int)tmask[1], rt[SLOT], 1);                               \
+          w_.z = v_.z & __builtin_amdgcn_sbfe((int)tmask[2], rt[SLOT], 1);                               \
+          w_.w = v_.w & __builtin_amdgcn_sbfe((int)tmask[3], rt[SLOT], 1);                               \
+          rb[SLOT] = __builtin_bit_cast(fi_floatx4, w_);                                                 \
+        }                                                                                                \
+        __builtin_amdgcn_s_setprio(1);                                                                   \
+        _Pragma("unroll") for (int f = 0; f < 4; ++f)                                                    \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q)                                                    \
+          acc[f][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb[SLOT][q], acc[f][q], 0, 0, 0); \
+        __builtin_amdgcn_s_setprio(0);                                                                   \
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) FP_LOAD(d, d);
+      for (int s0 = 0; s0 < nks - D; s0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          FP_MFMA(d);
+          __builtin_amdgcn_sched_barrier(0);
+          FP_LOAD(d, s0 + D + d);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) FP_MFMA(d);
+#undef FP_LOAD
+#undef FP_MFMA
+    }
+    // the squeeze's A operand of this chunk's 16 k-steps (pooling waves), in flight over the barrier
+    float asq[16][MFS];
+    if (pwave) {
+      const int saoff = ((cat0 + lk) * p.Msp + MFS * lj) * 4;
+#pragma unroll
+      for (int t = 0; t < 16; ++t)
+#pragma unroll
+        for (int fs = 0; fs < MFS; ++fs)
+          asq[t][fs] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wsr, saoff + t * 16 * p.Msp + fs * 4, 0, 0));
+    }
+    const float* __restrict__ bias = MODE == 0 ? p.b1 : p.b3;
+    float bv[4][4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[f][e] = bias[c0 + 16 * f + 4 * e + lk];
+    __syncthreads();  // the previous chunk's tile is pooled
+    // bias + Relu -> conv tile row 16 f + 4 e + lk (= channel c0 + 16 f + 4 e + lk, the permuted packing)
+    if (clive) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          fi_floatx4 v;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(acc[f][q][e] + bv[f][e], 0.0f);
+          *reinterpret_cast<fi_floatx4*>(fp_tile + (16 * f + 4 * e + lk) * FP_TS + wave * 64 + 4 * lj) = v;
+        }
+    }
+    __syncthreads();  // tile complete
+#ifndef ORE_EXP_FP_NOPOOL  // timing ablation: the pooling phase compiled out (results wrong)
+    if (pwave) {
+#else
+    if (pwave && p.N < 0) {
+#endif
+      // squeeze k-step t takes concat channel cat0 + 4 t + lk = tile row 4 t + lk (lane group lk)
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        // the k-step's row offset, opaque to the compiler: as constants, the 16 x 18 tap addresses
+        // (past the 64 KB ds_read offset range from t = 8 on) were hoisted out of the chunk loop and spilled
+        int tb = 4 * t * FP_TS;
+        __asm__ volatile("" : "+s"(tb));
+        float m[2];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          m[g] = -FLT_MAX;
+#pragma unroll
+          for (int i = 0; i < 9; ++i) m[g] = fmaxf(m[g], fp_tile[tap[g][i] + tb]);
+        }
+#pragma unroll
+        for (int fs = 0; fs < MFS; ++fs) {
+          accs[fs][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(asq[t][fs], m[0], accs[fs][0], 0, 0, 0);
+          if (g1) accs[fs][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(asq[t][fs], m[1], accs[fs][1], 0, 0, 0);
+        }
+      }
+    }
+  };
+  for (int c0 = 0; c0 < p.E1; c0 += 64) chunk(std::integral_constant<int, 0>{}, c0, c0);
+  for (int c0 = 0; c0 < p.E3; c0 += 64) chunk(std::integral_constant<int, 1>{}, c0, p.E1 + c0);
+
+  // S' = Relu(squeeze + bs): channel MFS (4 lk + e) + fs, pooled pixel kp[g] of the band
+  if (!pwave) return;
+  float* __restrict__ y = p.y + (long long)img * p.y_nstride + pr0 * Wp;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    if (kp[g] >= P) continue;
+#pragma unroll
+    for (int fs = 0; fs < MFS; ++fs)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = MFS * (4 * lk + e) + fs;
+        if (m >= p.Ms) continue;
+        y[(long long)m * p.y_ps + kp[g]] = fmaxf(accs[fs][g][e] + p.bs[m], 0.0f);
+      }
+  }
+}
+
+bool fire_pool_plan(FireParams* p) {
+  // the most pooled rows per band whose conv rows fit the 8 waves' 512 pixels and whose pooled pixels
+  // fit the 4 pooling waves' 8 fragments
+  p->PR = 0;
+  for (int r = 1; r <= p->Hp; ++r) {
+    if ((2 * r + 1) * p->W > FP_PIX || r * p->Wp > 128) break;
+    p->PR = r;
+  }
+  return p->PR > 0;
+}
+
 bool fire_eligible(const FireParams& p) {
   const uintptr_t xa = reinterpret_cast<uintptr_t>(p.x), ya = reinterpret_cast<uintptr_t>(p.y);
-  return p.E1 % 64 == 0 && p.E3 % 64 == 0 && p.E1 > 0 && p.E3 > 0 && p.Ms >= 1 && p.Ms <= 64 && p.C % 16 == 0 &&
-         p.W >= 3 && p.x_ps % 4 == 0 && p.x_nstride % 4 == 0 && (xa & 15) == 0 && p.y_ps % 4 == 0 &&
-         p.y_nstride % 4 == 0 && (ya & 15) == 0 && p.Ntot % 4 == 0 && p.Ntot >= 4 && p.x_bytes > 0 &&
-         p.x_guard >= p.x_lead && p.x_bytes + p.x_lead < (1LL << 31) && p.Msp % 4 == 0;
+  const bool common = p.E1 % 64 == 0 && p.E3 % 64 == 0 && p.E1 > 0 && p.E3 > 0 && p.Ms >= 1 && p.Ms <= 64 &&
+                      p.C % 16 == 0 && p.W >= 3 && p.x_ps % 4 == 0 && p.x_nstride % 4 == 0 && (xa & 15) == 0 &&
+                      p.x_bytes > 0 && p.x_guard >= p.x_lead && p.x_bytes + p.x_lead < (1LL << 31) && p.Msp % 4 == 0;
+  if (!common) return false;
+  if (p.pool)  // 3x3 / stride-2 windows inside the padded plane, each touching the image; scalar stores
+    return p.PR >= 1 && (2 * p.PR + 1) * p.W <= FP_PIX && p.PR * p.Wp <= 128 && p.Hp > 0 && p.Wp > 0 && p.ppt >= 0 &&
+           p.ppl >= 0 && p.ppt <= 2 && p.ppl <= 2 && 2 * (p.Hp - 1) - p.ppt < p.H && 2 * (p.Wp - 1) - p.ppl < p.W &&
+           p.y_ps >= p.Hp * p.Wp && p.N > 0;
+  return p.y_ps % 4 == 0 && p.y_nstride % 4 == 0 && (ya & 15) == 0 && p.Ntot % 4 == 0 && p.Ntot >= 4;
 }
 
 #ifndef ORE_FIRE_D
 #define ORE_FIRE_D 4  // K-loop ring depth (experiment knob)
 #endif
+#ifndef ORE_FIRE_POOL_D
+#define ORE_FIRE_POOL_D 4  // fire_pool_kernel's ring depth (experiment knob)
+#endif
 
 template <int MFS>
 static void launch_fire_cfg(const FireParams& p0, hipStream_t s) {
   FireParams p = p0;
+  if (p.pool) {
+    // 132 KB of LDS: above the default dynamic-LDS limit, raised once per device
+    static std::atomic<unsigned long long> raised{0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (!(raised.load(std::memory_order_acquire) & bit)) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fire_pool_kernel<MFS, ORE_FIRE_POOL_D>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, FP_LDS);
+      raised.fetch_or(bit, std::memory_order_acq_rel);
+    }
+    const unsigned grid = (unsigned)(p.N * ((p.Hp + p.PR - 1) / p.PR));
+    hipLaunchKernelGGL((fire_pool_kernel<MFS, ORE_FIRE_POOL_D>), dim3(grid), dim3(512), FP_LDS, s, p);
+    return;
+  }
   p.ntiles = (int)((p.Ntot + 63) / 64);
   hipLaunchKernelGGL((fire_kernel<MFS, ORE_FIRE_D>), dim3((unsigned)((p.ntiles + 3) / 4)), dim3(256), 0, s, p);
 }

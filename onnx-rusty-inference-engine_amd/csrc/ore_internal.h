@@ -130,7 +130,7 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
 ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
                     int64_t x_ps, const float* w1, const float* b1, int64_t E1, const float* w3, const float* b3,
                     int64_t E3, const float* ws, int64_t Msp, const float* bs, int64_t Ms, float* y, int64_t y_nstride,
-                    int64_t y_ps, bool wino = false);
+                    int64_t y_ps, bool wino = false, const Window* pool = nullptr);
 // the f16 fused fire module (ore_fire_f16.hip): x = S, y = S' NHWC f16 (pixel strides x_cs / y_cs,
 // image strides in elements); w1 / w3 / ws in launch_fire_pack_f16 layout; pool: a 3x3 / stride-2
 // MaxPool (window over the H x W conv plane) between the Concat and the squeeze, y on its plane

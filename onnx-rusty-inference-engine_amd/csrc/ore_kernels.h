@@ -110,9 +110,13 @@ struct FireParams {
   int x_guard, x_lead;                   // mapped bytes before x; bytes the 3x3 taps read before it
   int ntiles;                            // filled by the launcher
   int wino;                              // 1: e3 by Winograd (launch_fire_wino; w3 from launch_fire_pack_wino)
+  // pooled form (fire_pool_kernel): a 3x3 / stride-2 MaxPool (Hp x Wp, pads ppt / ppl) between the
+  // Concat and the squeeze; y is then [N][Ms][Hp][Wp]; PR pooled rows per workgroup (fire_pool_plan)
+  int pool, Hp, Wp, ppt, ppl, PR;
 };
 bool fire_eligible(const FireParams& p);
 void launch_fire(const FireParams& p, hipStream_t s);
+bool fire_pool_plan(FireParams* p);  // picks PR; false when no band shape fits
 // the fire module with its expand3x3 by Winograd F(2x2, 3x3) (ore_conv_wino.hip): w3 packed by
 // launch_fire_pack_wino ([C][4][E3][4] f32, rows of each 32-channel chunk permuted); C <= 64, E3 % 32 == 0
 bool fire_wino_eligible(const FireParams& p);
@@ -241,6 +245,8 @@ constexpr int EPOOL_TILE_BASE = 21;
 // EPOOL_WIN_TILE (after the Winograd / fused-f16 tile ids: ore.Model.TILE_NAMES "epool window f32")
 constexpr int EPOOL_WIN_VARIANT = 7, EPOOL_WIN_TILE = 44;
 inline int epool_tile_id(int variant) { return variant == EPOOL_WIN_VARIANT ? EPOOL_WIN_TILE : EPOOL_TILE_BASE + variant; }
+// the pooled f32 fire module (fire_pool_kernel): ore.Model.TILE_NAMES "fire pool f32"
+constexpr int FIRE_POOL_TILE = 45;
 // sq: the pooled map's only consumer, a 1x1 conv + Relu with <= 16 channels (ONNX weights [M][K]),
 // fused in (conv1's geometry only); the pooled map is never stored, y = the squeeze's NCHW output
 struct C1SqueezeF32 {

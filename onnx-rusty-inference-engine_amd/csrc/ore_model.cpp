@@ -96,8 +96,8 @@ struct Step {
   bool fire_wino = false;          // the e3 by Winograd (fire_wino_kernel; fire_w3 in launch_fire_pack_wino layout)
   bool fire_f16 = false;           // f16 model: fire_f16_kernel, fire_w1 / fire_w3 / fire_ws16 in launch_fire_pack_f16 layout
   const void* fire_ws16 = nullptr;
-  bool fire_pool = false;          // f16: a 3x3 / stride-2 MaxPool between the Concat and this squeeze
-  int64_t fire_H = 0, fire_W = 0;  //   (fire_pool_f16_kernel): the expands' plane and the pool window
+  bool fire_pool = false;          // a 3x3 / stride-2 MaxPool between the Concat and this squeeze
+  int64_t fire_H = 0, fire_W = 0;  //   (fire_pool_kernel / fire_pool_f16_kernel): the expands' plane and the pool window
   Window fire_pwin;
   ConvPlan plan{};        // kernel choice and weight layout for S_CONV / S_MATMUL
   float* wp = nullptr;    // packed weights (layout per plan) for S_CONV / S_MATMUL
@@ -641,6 +641,93 @@ ore_status plan(ore_model* m) {
       producer[pl.out] = pc;
       pl.kind = S_NOP;
       pl.in0 = -1;
+    }
+    count_uses(m, m->steps);
+  }
+  // (1k) f32 fire module -> 3x3 / stride-2 MaxPool -> the next squeeze in one fire_pool_kernel launch
+  // (ore_fire.hip): Concat(e1 1x1, e3 3x3 'same') (+ Relu), the pool the Concat's only reader, the
+  // squeeze (1x1 + Relu, <= 64 channels) the pool's only reader.  Bit-identical to the pooled-epilogue
+  // expands + the separate squeeze.  For expand planes of >= ORE_FIRE_POOL_MIN_HW pixels (default
+  // 1024: SqueezeNet's fire4 -> pool3 -> fire5; at 27 x 27 fire8's expand3x3 runs Winograd, cheaper
+  // than the direct K loop) and batches of >= ORE_FIRE_MIN_COLS columns, as (1d); ORE_FIRE_POOL=0
+  // turns it off.  Runs before the concat-pool pass below.
+  if ((m->fusion & ORE_FUSE_FIRE) && (m->fusion & ORE_FUSE_CONV_POOL) && (m->fusion & ORE_FUSE_CONV_RELU) &&
+      (m->fusion & ORE_FUSE_CONCAT) && !m->f16 && !m->x3_all) {
+    const char* efp = getenv("ORE_FIRE_POOL");
+    const char* emh = getenv("ORE_FIRE_POOL_MIN_HW");
+    const int64_t min_hw = emh ? atoll(emh) : 1024;
+    const char* emc = getenv("ORE_FIRE_MIN_COLS");  // as (1d): small batches keep the walkers (tests set 0)
+    const int64_t min_cols = emc ? atoll(emc) : 65536;
+    for (size_t i = 0; i < m->steps.size() && !(efp && atoi(efp) == 0); ++i) {
+      Step& cc = m->steps[i];
+      if (cc.kind != S_CONCAT || cc.axis != 1 || cc.in0 < 0 || cc.in1 < 0 || cc.in0 == cc.in1) continue;
+      const int pa = producer[cc.in0], pb = producer[cc.in1];
+      if (pa < 0 || pb < 0 || pa == pb) continue;
+      auto consumer = [&](int v, size_t from) {
+        for (size_t j = from; j < m->steps.size(); ++j)
+          if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == v || m->steps[j].in1 == v)) return int(j);
+        return -1;
+      };
+      const int pi = consumer(cc.out, i + 1);
+      if (pi < 0) continue;
+      Step& pl = m->steps[pi];
+      if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2 || pl.in0 != cc.out) continue;
+      const int qi = consumer(pl.out, size_t(pi) + 1);
+      if (qi < 0) continue;
+      Step &e1 = m->steps[pa], &e3 = m->steps[pb], &q = m->steps[qi];
+      auto is1x1 = [](const Step& s) {
+        return s.kind == S_CONV && s.relu && !s.pool && !s.epool && !s.plan.window && !s.plan.f16 && s.kh == 1 &&
+               s.kw == 1 && s.sh == 1 && s.sw == 1 && s.win.pt == 0 && s.win.pl == 0 && s.win.Ho == s.H && s.win.Wo == s.W;
+      };
+      const bool e3ok = e3.kind == S_CONV && e3.relu && !e3.pool && !e3.epool && !e3.plan.window && !e3.plan.f16 &&
+                        e3.kh == 3 && e3.kw == 3 && e3.sh == 1 && e3.sw == 1 && e3.win.pt == 1 && e3.win.pl == 1 &&
+                        e3.win.Ho == e3.H && e3.win.Wo == e3.W;
+      if (!is1x1(e1) || !e3ok || !is1x1(q) || q.in0 != pl.out || e1.in0 != e3.in0 || e1.H != e3.H || e1.W != e3.W) continue;
+      if (e1.M % 64 || e3.M % 64 || q.M > 64 || e1.C % 16 || q.C != e1.M + e3.M || pl.H != e1.H || pl.W != e1.W) continue;
+      if (e1.H * e1.W < min_hw || m->max_batch * e1.H * e1.W < min_cols || q.in2 < 0 || e1.in2 < 0 || e3.in2 < 0) continue;
+      if (padded_plane(e1.H * e1.W) % 4) continue;  // 16-B input planes (layout below)
+      FireParams fp{};
+      fp.H = int(e1.H); fp.W = int(e1.W);
+      fp.Hp = int(pl.win.Ho); fp.Wp = int(pl.win.Wo); fp.ppt = int(pl.win.pt); fp.ppl = int(pl.win.pl);
+      if (!fire_pool_plan(&fp) || fp.ppt > 2 || fp.ppl > 2 || 2 * (fp.Hp - 1) - fp.ppt >= fp.H ||
+          2 * (fp.Wp - 1) - fp.ppl >= fp.W)
+        continue;
+      const Value &va = m->values[cc.in0], &vb = m->values[cc.in1], &vc = m->values[cc.out], &vs = m->values[e1.in0];
+      const Value& vp = m->values[pl.out];
+      if (va.uses != 1 || vb.uses != 1 || vc.uses != 1 || vp.uses != 1 || va.is_output || vb.is_output ||
+          vc.is_output || vp.is_output || vs.es != 4)
+        continue;
+      bool packed_ok = true;  // the fire kernel's row-permuted expand packings (shared with (1d): key = step index)
+      for (int idx : {pa, pb}) {
+        if (m->fire_packs.count(idx)) continue;
+        const Step& e = m->steps[idx];
+        const int64_t K = e.C * e.kh * e.kw, Kp = (K + 31) / 32 * 32;
+        float* buf = nullptr;
+        if (hipMalloc(reinterpret_cast<void**>(&buf), size_t(Kp * e.M) * 4) != hipSuccess) { packed_ok = false; break; }
+        launch_fire_pack(m->values[e.in1].cptr, int(e.M), int(K), buf, m->ctx->stream);
+        m->fire_packs[idx] = buf;
+      }
+      if (!packed_ok || hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
+        return err(m, ORE_ERR_HIP, "fire weight packing failed");
+      q.kind = S_FIRE;
+      q.fire_pool = true;
+      q.fire_H = e1.H;
+      q.fire_W = e1.W;
+      q.fire_pwin = pl.win;
+      q.in0 = e1.in0;
+      q.fire_C = e1.C;
+      q.fire_E1 = e1.M;
+      q.fire_E3 = e3.M;
+      q.fire_w1 = m->fire_packs[pa];
+      q.fire_w3 = m->fire_packs[pb];
+      q.fire_b1 = m->values[e1.in2].cptr;
+      q.fire_b3 = m->values[e3.in2].cptr;
+      q.flops_per_img += e1.flops_per_img + e3.flops_per_img;
+      q.bytes_per_img = 4.0 * double(e1.C * e1.H * e1.W) + 4.0 * double(q.M * q.H * q.W);
+      q.name = e1.name.substr(0, e1.name.find('/')) + "+pool+" + q.name;
+      m->values[cc.in0].elided = m->values[cc.in1].elided = m->values[cc.out].elided = m->values[pl.out].elided = true;
+      e1.kind = e3.kind = cc.kind = pl.kind = S_NOP;
+      e1.in0 = e3.in0 = cc.in0 = cc.in1 = pl.in0 = -1;
     }
     count_uses(m, m->steps);
   }
@@ -1338,10 +1425,11 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
                             s.fire_pool ? &s.fire_pwin : nullptr);
       ctx->mapped_lo = m->arena_alloc;  // the arena and its 4 KiB lead are mapped
       ctx->mapped_hi = m->arena ? m->arena + m->arena_bytes : nullptr;
-      const ore_status st = run_fire(ctx, x.p, n, s.fire_C, s.H, s.W, x.nstride, x.ps ? x.ps : s.H * s.W, s.fire_w1,
+      const int64_t fH = s.fire_pool ? s.fire_H : s.H, fW = s.fire_pool ? s.fire_W : s.W;
+      const ore_status st = run_fire(ctx, x.p, n, s.fire_C, fH, fW, x.nstride, x.ps ? x.ps : fH * fW, s.fire_w1,
                                      s.fire_b1, s.fire_E1, s.fire_w3, s.fire_b3, s.fire_E3, s.wp, s.plan.Mp,
                                      m->values[s.in2].cptr, s.M, y.p, y.nstride, y.ps ? y.ps : s.H * s.W,
-                                     s.fire_wino);
+                                     s.fire_wino, s.fire_pool ? &s.fire_pwin : nullptr);
       ctx->mapped_lo = ctx->mapped_hi = nullptr;
       return st;
     }
@@ -1856,8 +1944,11 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
 int32_t ore_model_step_tile(ore_model* m, int32_t i) {
   if (!m || i < 0 || size_t(i) >= m->exec_steps.size()) return -1;
   const Step& s = m->steps[m->exec_steps[i]];
-  if (s.kind == S_FIRE)  // "fire" / "fire wino" / "fire f16": the fused fire kernels (ore.Model.TILE_NAMES)
-    return s.fire_f16 ? WINO_TILE_BASE + WINO_TILES_N + 1 : s.fire_wino ? WINO_TILE_BASE + WINO_TILES_N : CONV_TILES_F32;
+  if (s.kind == S_FIRE)  // "fire" / "fire wino" / "fire f16" / "fire pool f32": the fused fire kernels (ore.Model.TILE_NAMES)
+    return s.fire_f16 ? WINO_TILE_BASE + WINO_TILES_N + 1
+           : s.fire_wino ? WINO_TILE_BASE + WINO_TILES_N
+           : s.fire_pool ? FIRE_POOL_TILE
+                         : CONV_TILES_F32;
   if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.plan.epv > 0) return epool_tile_id(s.plan.epv);
   if (s.kind == S_CONV && s.epool && s.ran_tile >= 0) return s.ran_tile;
   return (s.kind == S_CONV || s.kind == S_MATMUL) ? s.plan.cfg : -1;

@@ -211,7 +211,7 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
 ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
                     int64_t x_ps, const float* w1, const float* b1, int64_t E1, const float* w3, const float* b3,
                     int64_t E3, const float* ws, int64_t Msp, const float* bs, int64_t Ms, float* y, int64_t y_nstride,
-                    int64_t y_ps, bool wino) {
+                    int64_t y_ps, bool wino, const Window* pool) {
   if (N == 0) return ORE_OK;
   FireParams p{};
   p.wino = wino ? 1 : 0;
@@ -221,6 +221,11 @@ ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t 
   p.x_ps = int(x_ps); p.y_ps = int(y_ps);
   p.x_nstride = x_nstride; p.y_nstride = y_nstride;
   p.Ntot = N * y_ps;
+  if (pool) {
+    p.pool = 1;
+    p.Hp = int(pool->Ho); p.Wp = int(pool->Wo); p.ppt = int(pool->pt); p.ppl = int(pool->pl);
+    if (wino || !fire_pool_plan(&p)) return set_error(ctx, ORE_ERR_INVALID, "internal: no band shape for the pooled fire module");
+  }
   const int64_t extent = ((N - 1) * x_nstride + C * x_ps) * 4;
   p.x_bytes = (extent > 0 && extent < (int64_t(1) << 31)) ? extent : 0;
   {  // mapped bytes before x (as run_conv): the rest of x's page or the walker's arena lead
@@ -231,7 +236,7 @@ ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t 
     p.x_guard = int(g);
   }
   p.x_lead = int(((W + 1) * 4 + 15) & ~int64_t(15));
-  if (x_ps < H * W || y_ps < H * W || !fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) ||
+  if (x_ps < H * W || y_ps < (pool ? pool->Ho * pool->Wo : H * W) || !fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) ||
       !fits_i32(p.Ntot + 256))
     return set_error(ctx, ORE_ERR_INVALID, "fire geometry exceeds 32-bit indexing");
   if (p.wino) {

@@ -3,15 +3,15 @@
 // the walker used to run maxpool_kernel (382 MB in, 95 MB out at B = 256) and then the squeeze
 // (95 MB in again)).  The pooled map never reaches HBM.
 //
-// One workgroup = two pooled rows of one image (Wp <= 16 columns each: one 16-pixel fragment per
-// row) x all M <= 64 output channels (four waves x 16 channels, v_mfma_f32_16x16x4_f32).  Per chunk
-// of 32 input channels:
-//   * the 5 input rows the two pooled rows read (columns of the whole row) go global -> registers
+// One workgroup = PS_PR (2) pooled rows of one image (Wp <= 16 columns each: one 16-pixel fragment
+// per row) x all M <= 64 output channels (four waves x 16 channels, v_mfma_f32_16x16x4_f32).  Per
+// chunk of PS_CH (16) input channels:
+//   * the 2 PS_PR + 1 input rows the pooled rows read (whole rows) go global -> registers
 //     -> LDS, raw buffer loads with outside-the-image offsets reading 0 (maxpool_kernel's zero
 //     padding); the next chunk's loads are in flight while this one pools and multiplies;
 //   * every thread takes (pooled pixel, channel) maxima from -FLT_MAX over the nine window values
-//     (maxpool_kernel's arithmetic) into an LDS block [32 channels][32 pixels];
-//   * each wave runs the chunk's 8 k-steps (k = channel, ascending over the chunks: the standalone
+//     (maxpool_kernel's arithmetic) into an LDS block [channels][16 PS_PR pixels];
+//   * each wave runs the chunk's k-steps (k = channel, ascending over the chunks: the standalone
 //     1x1 conv's fma chain) for its 16 channels x both pixel fragments; A from L2 in the conv's
 //     K-major packing (wp[k][Mp]).
 // Bit-identical to maxpool_kernel + the separate 1x1 conv (tests/test_model_gpu.py).
@@ -26,19 +26,26 @@ namespace {
 
 typedef float ps4 __attribute__((ext_vector_type(4)));
 
-constexpr int PS_CH = 32;        // input channels per chunk
-constexpr int PS_ROWS = 5;       // input rows of two pooled rows (3x3, stride 2)
-constexpr int PS_WMAX = 33;      // input columns held per row (Wp <= 16)
+#ifndef ORE_PS_PR
+#define ORE_PS_PR 2   // pooled rows per workgroup
+#endif
+#ifndef ORE_PS_CH
+#define ORE_PS_CH 16  // input channels per chunk
+#endif
+constexpr int PS_PR = ORE_PS_PR, PS_CH = ORE_PS_CH;
+constexpr int PS_ROWS = 2 * PS_PR + 1;  // input rows of PS_PR pooled rows (3x3, stride 2)
+constexpr int PS_WMAX = 33;             // input columns held per row (Wp <= 16)
 constexpr int PS_IN = PS_CH * PS_ROWS * PS_WMAX;  // floats of one staged chunk
 constexpr int PS_NQ = (PS_IN + 255) / 256;
+constexpr int PS_PX = 16 * PS_PR;       // pooled pixels (16 per row) of a workgroup
 
-__global__ __launch_bounds__(256, 2) void pool_conv1x1_f32_kernel(PoolConvParams p) {
+__global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p) {
   __shared__ float in_s[PS_IN];            // [ch][row][col]
-  __shared__ float pt[PS_CH][33];          // pooled block [ch][pixel n * 16 + col] (+1 pad)
+  __shared__ float pt[PS_CH][PS_PX + 1];   // pooled block [ch][pixel n * 16 + col] (+1 pad)
   const int tid = threadIdx.x, lane = tid & 63, lk = lane >> 4, lj = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int bands = (p.Hp + 1) / 2;
-  const int img = blockIdx.x / bands, pr0 = (blockIdx.x - img * bands) * 2;
+  const int bands = (p.Hp + PS_PR - 1) / PS_PR;
+  const int img = blockIdx.x / bands, pr0 = (blockIdx.x - img * bands) * PS_PR;
   const int ih0 = pr0 * 2 - p.pt, iw0 = -p.pl;  // input coordinates of staged (row 0, col 0)
   const int wcols = 2 * (p.Wp - 1) + 3;         // input columns the pooled row reads
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
@@ -66,14 +73,17 @@ __global__ __launch_bounds__(256, 2) void pool_conv1x1_f32_kernel(PoolConvParams
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  ps4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // rows 4 lk + e of channels 16 wave .., pixel lj
+  ps4 acc[PS_PR];  // rows 4 lk + e of channels 16 wave .., pixel lj of pooled row n
+#pragma unroll
+  for (int n = 0; n < PS_PR; ++n) acc[n] = ps4{0.f, 0.f, 0.f, 0.f};
   const int nch = p.C / PS_CH;
   const int m0 = 16 * wave;
-  // the squeeze's A values of a chunk (k = 32 ci + 4 t + lk, row m0 + lj), one chunk ahead
-  float acur[8], anxt[8];
-  auto load_a = [&](float (&dst)[8], int ci) __attribute__((always_inline)) {
+  // the squeeze's A values of a chunk (k = PS_CH ci + 4 t + lk, row m0 + lj), one chunk ahead
+  constexpr int KS = PS_CH / 4;  // k-steps per chunk
+  float acur[KS], anxt[KS];
+  auto load_a = [&](float (&dst)[KS], int ci) __attribute__((always_inline)) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
+    for (int t = 0; t < KS; ++t)
       dst[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                              wr, ((ci * PS_CH + 4 * t + lk) * p.Mp + m0 + lj) * 4, 0, 0));
   };
@@ -89,9 +99,9 @@ __global__ __launch_bounds__(256, 2) void pool_conv1x1_f32_kernel(PoolConvParams
       load_chunk((ci + 1) * PS_CH);
       load_a(anxt, ci + 1);
     }
-    // pooled maxima: 32 channels x 2 rows x 16 columns (columns >= Wp: column 0's value, unused)
-    for (int t = tid; t < PS_CH * 32; t += 256) {
-      const int c = t >> 5, pxi = t & 31, n = pxi >> 4, col = pxi & 15, cl = col < p.Wp ? col : 0;
+    // pooled maxima: channels x PS_PR rows x 16 columns (columns >= Wp: column 0's value, unused)
+    for (int t = tid; t < PS_CH * PS_PX; t += 256) {
+      const int c = t / PS_PX, pxi = t - c * PS_PX, n = pxi >> 4, col = pxi & 15, cl = col < p.Wp ? col : 0;
       const float* base = in_s + (c * PS_ROWS + 2 * n) * PS_WMAX + 2 * cl;
       float m = -FLT_MAX;
 #pragma unroll
@@ -101,21 +111,21 @@ __global__ __launch_bounds__(256, 2) void pool_conv1x1_f32_kernel(PoolConvParams
       pt[c][pxi] = m;
     }
     __syncthreads();
-    // squeeze k-steps of this chunk: k = 32 ci + 4 t + lk
+    // squeeze k-steps of this chunk: k = PS_CH ci + 4 t + lk
     if (m0 < p.M) {
 #pragma unroll
-      for (int t = 0; t < 8; ++t)
+      for (int t = 0; t < KS; ++t)
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
+        for (int n = 0; n < PS_PR; ++n)
           acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(acur[t], pt[4 * t + lk][16 * n + lj], acc[n], 0, 0, 0);
     }
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acur[t] = anxt[t];
+    for (int t = 0; t < KS; ++t) acur[t] = anxt[t];
   }
   // bias + Relu, NCHW stores: channel m0 + 4 lk + e, pooled pixel (pr0 + n, lj)
   if (m0 >= p.M || lj >= p.Wp) return;
 #pragma unroll
-  for (int n = 0; n < 2; ++n) {
+  for (int n = 0; n < PS_PR; ++n) {
     if (pr0 + n >= p.Hp) continue;
     float* yp = p.y + (long long)img * p.y_nstride + (pr0 + n) * p.Wp + lj;
 #pragma unroll
@@ -139,7 +149,7 @@ bool pool_conv1x1_f32_eligible(const PoolConvParams& p) {
 }
 
 void launch_pool_conv1x1_f32(const PoolConvParams& p, hipStream_t s) {
-  const long long grid = (long long)p.N * ((p.Hp + 1) / 2);
+  const long long grid = (long long)p.N * ((p.Hp + PS_PR - 1) / PS_PR);
   hipLaunchKernelGGL(pool_conv1x1_f32_kernel, dim3((unsigned)grid), dim3(256), 0, s, p);
 }
 

@@ -307,7 +307,8 @@ class Model:
                   "epool walk64 b3", "epool walk96 b2",
                   "x3 128x128", "x3 64x256", "x3 96x128", "x3 64x128",
                   "x3w 128x128", "x3w 64x128", "x3w 128x64", "x3w 64x64",
-                  "wino 32x32 d4", "wino 32x32 d2", "wino16 32x16", "wino16 16x32", "wino lds", "fire wino", "fire f16", "first conv pool f16", "epool window f32"]
+                  "wino 32x32 d4", "wino 32x32 d2", "wino16 32x16", "wino16 16x32", "wino lds", "fire wino", "fire f16", "first conv pool f16", "epool window f32",
+                  "fire pool f32"]
 
     def tiles(self):
         """Block tile per exec step (-1 for non-conv steps); names in TILE_NAMES."""

@@ -455,6 +455,7 @@ def test_squeezenet_concat_pool_fusion(gpu_ctx, hw, monkeypatch):
     y0 = _np(ref.run(xt))
     monkeypatch.setenv("ORE_CONV_POOL_STREAM", "3")  # the 64-channel walker (auto takes it from batch 128)
     monkeypatch.setenv("ORE_CONCAT_POOL_MIN_HW", "0")  # fire8 -> pool5 too (27 x 27 planes)
+    monkeypatch.setenv("ORE_FIRE_POOL", "0")  # fire4 -> pool3 stays with the walkers (not fire_pool_kernel)
     fused = ore.Model(gpu_ctx, mb, max_batch=3)
     fused.set_fusion(ore.FUSE_ALL | ore.FUSE_CONCAT_POOL | ore.KEEP_VALUES)
     y1 = _np(fused.run(xt))
@@ -804,3 +805,90 @@ def test_squeezenet_pool_squeeze_fused(gpu_ctx, monkeypatch):
         m.close()
     np.testing.assert_array_equal(outs[0], outs[1])
     assert nsteps[0] == nsteps[1] - 1  # pool5 is no longer a launch of its own
+
+
+def _fire_pool_model(C, H, W, S1, E1, E3, S2, pool_pads):
+    """squeeze (C -> S1) -> expand 1x1 (E1) / 3x3 pad 1 (E3) -> Concat -> MaxPool 3x3 / 2 (pool_pads)
+    -> squeeze (S2) -> GAP, all Relu (SqueezeNet's fire4 -> pool3 -> fire5/squeeze1x1 family)."""
+    from ore import onnx_wire as wr
+    rng = np.random.default_rng(C * 5 + H + W + S1 + E1 + E3 + S2)
+    shapes = {"wq": (S1, C, 1, 1), "w1": (E1, S1, 1, 1), "w3": (E3, S1, 3, 3), "wn": (S2, E1 + E3, 1, 1)}
+    inits, vinfo = [], [wr.encode_value_info("x", (1, C, H, W))]
+    for n, shp in shapes.items():
+        fan = shp[1] * shp[2] * shp[3]
+        w = (rng.standard_normal(shp) * np.sqrt(2.0 / fan)).astype(np.float32)
+        b = rng.uniform(-0.1, 0.1, shp[0]).astype(np.float32)
+        inits += [wr.encode_tensor(n, w), wr.encode_tensor("b" + n, b)]
+        vinfo += [wr.encode_value_info(n, w.shape), wr.encode_value_info("b" + n, b.shape)]
+    conv = lambda i, w, o, pads: wr.encode_node("Conv", [i, w, "b" + w], [o], attrs=[
+        wr.encode_attr_ints("pads", pads), wr.encode_attr_ints("strides", [1, 1])])
+    nodes = [conv("x", "wq", "q", [0] * 4), wr.encode_node("Relu", ["q"], ["qr"]),
+             conv("qr", "w1", "e1", [0] * 4), wr.encode_node("Relu", ["e1"], ["e1r"]),
+             conv("qr", "w3", "e3", [1] * 4), wr.encode_node("Relu", ["e3"], ["e3r"]),
+             wr.encode_node("Concat", ["e1r", "e3r"], ["cat"], attrs=[wr.encode_attr_int("axis", 1)]),
+             wr.encode_node("MaxPool", ["cat"], ["p"], attrs=[
+                 wr.encode_attr_ints("kernel_shape", [3, 3]), wr.encode_attr_ints("strides", [2, 2]),
+                 wr.encode_attr_string("auto_pad", "NOTSET"), wr.encode_attr_ints("pads", pool_pads)]),
+             conv("p", "wn", "n", [0] * 4), wr.encode_node("Relu", ["n"], ["nr"]),
+             wr.encode_node("GlobalAveragePool", ["nr"], ["y"])]
+    return wr.encode_model("firepool", nodes, inits, vinfo, [wr.encode_value_info("y", (1, S2, 1, 1))])
+
+
+@pytest.mark.parametrize("case", [
+    # C, H, W, S1, E1, E3, S2, pool pads (expand planes with H * W % 4 == 0: 16-B input planes)
+    (16, 54, 54, 32, 128, 128, 32, [0, 0, 1, 1]),  # SqueezeNet fire4 -> pool3 (ceil) -> fire5 squeeze: 4 rows / band
+    (16, 20, 21, 16, 64, 64, 48, [1, 1, 1, 1]),    # padded on all sides, odd W (row wraps in a pixel quad), MFS = 3
+    (32, 9, 8, 32, 128, 64, 16, [0, 0, 0, 0]),     # 'valid' pool, W = 8, unequal expands
+    (16, 30, 17, 16, 64, 128, 64, [0, 0, 1, 1]),   # MFS = 4, short last band
+])
+def test_fire_pool_fusion_bit_identical(gpu_ctx, case, monkeypatch):
+    """f32: fire module + 3x3 / stride-2 MaxPool + the next squeeze in one launch (fire_pool_kernel;
+    the expand outputs, their concat and the pooled map never stored) equal the pooled-epilogue
+    expands + the separate squeeze (ORE_FIRE_POOL=0) bit for bit, and the oracle within the conv
+    tolerance."""
+    import ore
+    import oracle
+    monkeypatch.setenv("ORE_FIRE_MIN_COLS", "0")
+    monkeypatch.setenv("ORE_FIRE_POOL_MIN_HW", "0")
+    C, H, W, S1, E1, E3, S2, pads = case
+    mb = _fire_pool_model(*case)
+    x = np.random.default_rng(sum(case[:7])).standard_normal((5, C, H, W)).astype(np.float32)
+    vals = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("ORE_FIRE_POOL", on)
+        m = ore.Model(gpu_ctx, mb, max_batch=5)
+        m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+        y = _np(m.run(_t(x)))
+        vals.append((y, m.read_value("nr")))
+        names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+        assert ("fire pool f32" in names) == (on == "1"), names
+        if on == "1":
+            for v in ("cat", "p"):
+                with pytest.raises(ore.OreError):
+                    m.read_value(v)  # never materialised
+        m.close()
+    np.testing.assert_array_equal(vals[0][1], vals[1][1])
+    np.testing.assert_array_equal(vals[0][0], vals[1][0])
+    ref = oracle.Model(mb).run(x, S2)
+    np.testing.assert_allclose(vals[0][0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-6)
+
+
+def test_squeezenet_fire_pool_fused(gpu_ctx, monkeypatch):
+    """SqueezeNet-1.0 @224 f32: fire4 + pool3 + fire5/squeeze1x1 in one launch (ORE_FIRE_MIN_COLS=0
+    so batch 3 fuses); probabilities equal the plan without it (ORE_FIRE_POOL=0) bit for bit."""
+    import ore
+    from ore import squeezenet
+    monkeypatch.setenv("ORE_FIRE_MIN_COLS", "0")
+    mb = squeezenet.build(224)
+    x = _t(squeezenet.synthetic_input(3, 224, seed=37))
+    outs, nsteps = [], []
+    for on in ("1", "0"):
+        monkeypatch.setenv("ORE_FIRE_POOL", on)
+        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        outs.append(_np(m.run(x)))
+        names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+        assert names.count("fire pool f32") == (1 if on == "1" else 0), names
+        nsteps.append(len(m.tiles()))
+        m.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
+    assert nsteps[0] == nsteps[1] - 2  # two expand walkers + the squeeze -> fire_pool_kernel
