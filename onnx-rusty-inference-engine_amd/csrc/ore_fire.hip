@@ -254,18 +254,25 @@ __global__ __launch_bounds__(256, ORE_FIRE_MINB) void fire_kernel(FireParams p) 
 //   * the band's conv rows cr0 .. cr1 are a contiguous run of the NCHW plane; wave w computes its
 //     64 pixels of it with fire_kernel's streaming K loop (same operands, same k = (c, r, s) chains);
 //   * per 64-channel chunk of the concat (e1 chunks, then e3 chunks) every wave writes bias + Relu
-//     of its pixels to an LDS conv tile [64 channels][FP_TS] (132 KB: one workgroup per CU, two
+//     of its pixels to an LDS conv tile [64 channels][FP_TS] (131 KB: one workgroup per CU, two
 //     waves per SIMD), barrier; then waves 0-3 take the 3x3 maxima (from -FLT_MAX, outside taps read
 //     0.0f from a zeroed pad slot: maxpool_kernel's arithmetic) of their two 16-pixel pooled
 //     fragments and run the chunk's 16 squeeze k-steps (k = concat channel, ascending over the
 //     chunks: the standalone 1x1 conv's chain) while waves 4-7 already run the next chunk's K loop;
 //   * a barrier before the next tile write frees the tile.
 // Bit-identical to the two pooled-epilogue convs + the separate squeeze (tests/test_model_gpu.py).
-constexpr int FP_WAVES = 8, FP_PIX = 64 * FP_WAVES, FP_TS = FP_PIX + 4;  // conv tile row stride (floats)
+// conv tile row stride FP_TS (floats) odd: the pooling reads (lane groups of 32 = two channel rows x 16
+// pooled pixels two columns apart) of the second row land on the odd banks; with a multiple of 4 (16-B
+// stores) both rows shared the even banks, a 2-way conflict on every read
+constexpr int FP_WAVES = 8, FP_PIX = 64 * FP_WAVES, FP_TS = FP_PIX + 1;
 constexpr int FP_LDS = 64 * FP_TS * 4;
 
+#ifndef ORE_FP_NG
+#define ORE_FP_NG 2  // pooled fragments per pooling wave (2: waves 0-3 pool, 1: all 8) (experiment knob)
+#endif
 template <int MFS, int D>
 __global__ __launch_bounds__(512, 1) void fire_pool_kernel(FireParams p) {
+  constexpr int NG = ORE_FP_NG;
   extern __shared__ __attribute__((aligned(16))) float fp_tile[];
   const int lane = threadIdx.x & 63, lk = lane >> 4, lj = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -276,8 +283,7 @@ __global__ __launch_bounds__(512, 1) void fire_pool_kernel(FireParams p) {
   const int cr0 = max(0, 2 * pr0 - p.ppt), cr1 = min(H - 1, 2 * (pr0 + npr - 1) - p.ppt + 2);
   const int ncp = (cr1 - cr0 + 1) * W;  // conv pixels of the band (<= FP_PIX: host)
   const bool clive = wave * 64 < ncp;   // a wave with none of them skips the K loops
-  if (threadIdx.x < 64)                 // the pad slots of every channel row: the pool's outside taps
-    *reinterpret_cast<fi_floatx4*>(fp_tile + threadIdx.x * FP_TS + FP_PIX) = fi_floatx4{0.f, 0.f, 0.f, 0.f};
+  if (threadIdx.x < 64) fp_tile[threadIdx.x * FP_TS + FP_PIX] = 0.0f;  // pad slots: the pool's outside taps
 
   // ---- expand operands (fire_kernel's): this lane's 4 conv pixels pix .. pix + 3 of the plane
   const int pix = cr0 * W + wave * 64 + 4 * lj;
@@ -311,14 +317,17 @@ __global__ __launch_bounds__(512, 1) void fire_pool_kernel(FireParams p) {
       const_cast<float*>(p.ws), (short)0, (((p.E1 + p.E3) + 31) & ~31) * p.Msp * 4, 0x00020000);
   const int tap0 = xlead - (W + 1) * 4;
 
-  // ---- pooled fragments of waves 0-3: fragment 2 wave + g, pooled pixel kp = 16 (2 wave + g) + lj
+  // ---- pooled fragments: waves 0 .. 8 / NG - 1 take NG 16-pixel fragments each (fragment NG wave + g,
+  // pooled pixel kp = 16 (NG wave + g) + lj of the band)
   const int P = npr * Wp, nfrag = (P + 15) >> 4;
-  const bool pwave = wave < 4 && 2 * wave < nfrag;
-  int tap[2][9];  // conv-tile offsets of the 9 window taps (channel row lk; outside taps: the pad slot)
-  int kp[2];
+  const bool pwave = wave < 8 / NG && NG * wave < nfrag;
+  int tap[NG][9];  // conv-tile offsets of the 9 window taps (channel row lk; outside taps: the pad slot)
+  int kp[NG];
+  bool gon[NG];    // (wave-uniform) fragment g has pixels
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    kp[g] = 16 * (2 * wave + g) + lj;
+  for (int g = 0; g < NG; ++g) {
+    kp[g] = 16 * (NG * wave + g) + lj;
+    gon[g] = NG * wave + g < nfrag;
     const int kk = kp[g] < P ? kp[g] : 0;
     const int pa = pr0 + kk / Wp, pb = kk - (kk / Wp) * Wp;
     const int ih0 = 2 * pa - p.ppt, iw0 = 2 * pb - p.ppl;
@@ -331,10 +340,11 @@ __global__ __launch_bounds__(512, 1) void fire_pool_kernel(FireParams p) {
         tap[g][3 * r + s] = lk * FP_TS + (in ? (ih - cr0) * W + iw : FP_PIX);
       }
   }
-  const bool g1 = 2 * wave + 1 < nfrag;  // (wave-uniform) the second fragment has pixels
-  fi_floatx4 accs[MFS][2];
+  fi_floatx4 accs[MFS][NG];
 #pragma unroll
-  for (int fs = 0; fs < MFS; ++fs) accs[fs][0] = accs[fs][1] = fi_floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int fs = 0; fs < MFS; ++fs)
+#pragma unroll
+    for (int g = 0; g < NG; ++g) accs[fs][g] = fi_floatx4{0.f, 0.f, 0.f, 0.f};
 
   auto chunk = [&](auto mode_tag, int c0, int cat0) __attribute__((always_inline)) {
     constexpr int MODE = decltype(mode_tag)::value;
@@ -416,17 +426,20 @@ __global__ __launch_bounds__(512, 1) void fire_pool_kernel(FireParams p) {
     for (int f = 0; f < 4; ++f)
 #pragma unroll
       for (int e = 0; e < 4; ++e) bv[f][e] = bias[c0 + 16 * f + 4 * e + lk];
+#ifndef ORE_EXP_FP_NOSYNC  // timing ablation: no barriers, no tile, no pooling (results wrong)
     __syncthreads();  // the previous chunk's tile is pooled
+#else
+    if (p.N >= 0) return;
+#endif
     // bias + Relu -> conv tile row 16 f + 4 e + lk (= channel c0 + 16 f + 4 e + lk, the permuted packing)
     if (clive) {
 #pragma unroll
       for (int f = 0; f < 4; ++f)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          fi_floatx4 v;
+          float* row = fp_tile + (16 * f + 4 * e + lk) * FP_TS + wave * 64 + 4 * lj;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = fmaxf(acc[f][q][e] + bv[f][e], 0.0f);
-          *reinterpret_cast<fi_floatx4*>(fp_tile + (16 * f + 4 * e + lk) * FP_TS + wave * 64 + 4 * lj) = v;
+          for (int q = 0; q < 4; ++q) row[q] = fmaxf(acc[f][q][e] + bv[f][e], 0.0f);
         }
     }
     __syncthreads();  // tile complete
@@ -435,25 +448,35 @@ __global__ __launch_bounds__(512, 1) void fire_pool_kernel(FireParams p) {
 #else
     if (pwave && p.N < 0) {
 #endif
-      // squeeze k-step t takes concat channel cat0 + 4 t + lk = tile row 4 t + lk (lane group lk)
-#pragma unroll
-      for (int t = 0; t < 16; ++t) {
-        // the k-step's row offset, opaque to the compiler: as constants, the 16 x 18 tap addresses
+      // squeeze k-step t takes concat channel cat0 + 4 t + lk = tile row 4 t + lk (lane group lk); the
+      // window reads of k-step t + 1 are issued before the maxima of t
+      float v[2][NG][9];
+      auto rd = [&](float (&d)[NG][9], int t) __attribute__((always_inline)) {
+        // the k-step's row offset, opaque to the compiler: as constants, the 16 x 9 NG tap addresses
         // (past the 64 KB ds_read offset range from t = 8 on) were hoisted out of the chunk loop and spilled
         int tb = 4 * t * FP_TS;
         __asm__ volatile("" : "+s"(tb));
-        float m[2];
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
+        for (int g = 0; g < NG; ++g)
+#pragma unroll
+          for (int i = 0; i < 9; ++i) d[g][i] = fp_tile[tap[g][i] + tb];
+      };
+      rd(v[0], 0);
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        if (t + 1 < 16) rd(v[(t + 1) & 1], t + 1);
+        float m[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
           m[g] = -FLT_MAX;
 #pragma unroll
-          for (int i = 0; i < 9; ++i) m[g] = fmaxf(m[g], fp_tile[tap[g][i] + tb]);
+          for (int i = 0; i < 9; ++i) m[g] = fmaxf(m[g], v[t & 1][g][i]);
         }
 #pragma unroll
-        for (int fs = 0; fs < MFS; ++fs) {
-          accs[fs][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(asq[t][fs], m[0], accs[fs][0], 0, 0, 0);
-          if (g1) accs[fs][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(asq[t][fs], m[1], accs[fs][1], 0, 0, 0);
-        }
+        for (int fs = 0; fs < MFS; ++fs)
+#pragma unroll
+          for (int g = 0; g < NG; ++g)
+            if (gon[g]) accs[fs][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(asq[t][fs], m[g], accs[fs][g], 0, 0, 0);
       }
     }
   };
@@ -464,7 +487,7 @@ __global__ __launch_bounds__(512, 1) void fire_pool_kernel(FireParams p) {
   if (!pwave) return;
   float* __restrict__ y = p.y + (long long)img * p.y_nstride + pr0 * Wp;
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < NG; ++g) {
     if (kp[g] >= P) continue;
 #pragma unroll
     for (int fs = 0; fs < MFS; ++fs)

@@ -18,5 +18,5 @@ while read -r GROUP; do
   rc=$?
   echo "pass $i [$GROUP] rc=$rc"
   case $rc in 124|134|137|139) echo "fatal"; exit $rc;; esac
-done < "$ROOT/tools/pmc_groups.txt"
+done < "${PMC_GROUPS:-$ROOT/tools/pmc_groups.txt}"
 exit 0
