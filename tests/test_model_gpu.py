@@ -169,8 +169,9 @@ def test_fused_padded_layout_values(gpu_ctx, hw):
             continue  # fused away (conv output feeding its relu)
         np.testing.assert_array_equal(y, ref.read_value(node.output[0]), err_msg=node.output[0])
         checked += 1
-    # @224 conv1's relu output is fused into pool1, and fire4's expand outputs and concat into pool3
-    assert checked >= (35 if hw == 224 else 39)
+    # @224 conv1's relu output is fused into pool1, pool1 into fire2's squeeze and fire4's expand
+    # outputs and concat into pool3; pool5 (both sizes) into fire9's squeeze
+    assert checked >= (33 if hw == 224 else 37)
     ref.close()
     fused.close()
 
