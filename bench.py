@@ -283,7 +283,9 @@ def main():
                      "conv_x3_kernel (f32 implicit GEMM on MFMA 16x16x32 bf16: both operands split exactly into "
                      "3 bf16 parts, 6 part products per f32 MAC; peak = 2500 / 6 TFLOP/s of f32 work" if x3 else
                      "Conv class: conv_stream_kernel (LDS-free implicit GEMM, MFMA 16x16x4 f32), fire_kernel (fire "
-                     "module + next squeeze), conv_pool_stream_kernel / conv_win_pool_f32_kernel (conv1 + pool1), "
+                     "module + next squeeze), fire_pool_kernel (fire4 + pool3 + fire5 squeeze), "
+                     "conv_win_pool_f32_kernel (conv1 + pool1 + fire2 squeeze), pool_conv1x1_f32_kernel (pool5 + "
+                     "fire9 squeeze), "
                      "conv_wino32/16_kernel (Winograd F(2x2,3x3) expand3x3, FLOPs counted as direct) and "
                      "conv_gemm_kernel (LDS-staged, MFMA 32x32x2 f32) per the autotuned tile") + f", {conv['launches']} launches/step)"
             # HBM bytes per conv launch from the PMC passes of tools/pmc.sh (FETCH_SIZE x2 +
