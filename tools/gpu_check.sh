@@ -37,7 +37,7 @@ fi
 if has prof; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \
-    python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-b1 > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_$TAG.err"
+    python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-b1 --no-f16-line > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_$TAG.err"
   rc=$?; echo "prof rc=$rc"; cat "$OUT/prof_bench_$TAG.json"
   find "$OUT/prof_$TAG" -name "*stats*" | head
   if [ $rc -ne 0 ]; then tail -20 "$OUT/prof_$TAG.err"; exit $rc; fi
