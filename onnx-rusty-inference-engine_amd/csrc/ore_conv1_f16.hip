@@ -160,10 +160,11 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
       }
     }
   };
-  load_window(blockIdx.x);
+  const int wg0 = ORE_BAND_ID();
+  load_window(wg0);
   store_window();
 
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int tile = wg0; tile < ntiles; tile += gridDim.x) {
     const int img = tile / tpi, tt = tile - img * tpi;
     const int ph0 = (tt / p.ep_tc) * C1_PR, pw0 = (tt - (tt / p.ep_tc) * p.ep_tc) * C1_PC;
     const int ohb = ph0 * 2 - p.ep_pt, owb = pw0 * 2 - p.ep_pl;  // conv coordinates of patch (0, 0)

@@ -5,6 +5,24 @@
 
 namespace ore {
 
+// XCD-aware bijective workgroup id: the hardware deals block ids round-robin over the 8 XCDs,
+// so neighbouring ids (bands or patches of one image whose input rows overlap) would fetch their
+// shared rows into two L2s.  The remap puts consecutive logical ids on one XCD.  Used by the
+// persistent f16 conv1 kernel (patches 232 -> 226 us); measured neutral on the f32 conv1 / fire_pool
+// kernels and slower on pool_conv1x1_f32 (124 -> 129 us), which keep the plain block id
+// (profiles/r02j_xcd_bands_ab.txt).
+__device__ __forceinline__ int xcd_block_id() {
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
+  return (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
+}
+
+#ifdef ORE_NO_XCD_BANDS  // experiment builds: the plain block id in the banded / patch kernels
+#define ORE_BAND_ID() ((int)blockIdx.x)
+#else
+#define ORE_BAND_ID() xcd_block_id()
+#endif
+
 struct ConvParams {
   const float* x;      // input  [N][C][H][W], image stride x_nstride
   const float* wp;     // packed weights Wp[Kp][Mp] (launch_pack_weights)
