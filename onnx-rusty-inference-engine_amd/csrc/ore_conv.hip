@@ -1120,7 +1120,11 @@ void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
   last_conv_tile = pln.cfg;
   if (pln.wino) {  // the caller (run_conv) keeps x_bytes within the buffer range
     int t = pln.cfg - WINO_TILE_BASE;
-    if (!conv_wino_eligible(p, t)) t = 2;
+    if (p.e1_y) {  // a fused 1x1 conv: tile 2 only (run_conv checked it)
+      t = 2;
+    } else if (!conv_wino_eligible(p, t)) {
+      t = 2;
+    }
     last_conv_tile = WINO_TILE_BASE + t;
     launch_conv_wino(p, t, s);
     return;

@@ -165,15 +165,21 @@ __device__ __forceinline__ void wg_window(const wg_floatx4 (&rows)[4], const WgT
   wg_input_transform(d, v);
 }
 
-// the 16 position sums of one (channel m, tile) -> bias b (+ Relu) -> the tile's (up to) 4 pixels
-__device__ __forceinline__ void wg_store(const ConvParams& p, const WgTile& w, int m, float b, const float (&mx)[16]) {
-  float o[4];
-  wg_output_transform(mx, o);
+// the window's centre values d[1 + q / 2][1 + q % 2] (as wg_window builds d), i.e. the input at the
+// tile's output pixel q: the B operand of a 1x1 conv on the same input
+__device__ __forceinline__ void wg_centres(const wg_floatx4 (&rows)[4], const WgTile& w, float (&c)[4]) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    o[q] += b;
-    if (p.relu) o[q] = fmaxf(o[q], 0.0f);
+  for (int r = 1; r < 3; ++r) {
+    const int4 q = __builtin_bit_cast(int4, rows[r]);
+    const int e0 = q.x, e1 = q.y & __builtin_amdgcn_sbfe((int)w.cmask, 1, 1);
+    const int e2 = q.z & __builtin_amdgcn_sbfe((int)w.cmask, 2, 1);
+    c[2 * (r - 1) + 0] = __builtin_bit_cast(float, w.sh1 ? e0 : e1);
+    c[2 * (r - 1) + 1] = __builtin_bit_cast(float, w.sh1 ? e1 : e2);
   }
+}
+
+// a tile's (up to) 4 output pixels o[2 i + j] of channel m -> yb (p.y's plane and image strides)
+__device__ __forceinline__ void wg_store_px(const ConvParams& p, const WgTile& w, float* yb, int m, const float (&o)[4]) {
   if (!w.tok) return;
 #ifdef ORE_EXP_WG_NOSTORE  // timing experiment only: stores skipped (kept live by a never-true test)
   if (o[0] != 1.2345e-30f) return;
@@ -181,7 +187,7 @@ __device__ __forceinline__ void wg_store(const ConvParams& p, const WgTile& w, i
   // a tile row's two pixels as one 8-B store (4-B aligned on odd planes; buffer stores take that),
   // so a wave-instruction writes whole lines: two 4-B stores per row wrote every line twice
   // (PMC WRITE_SIZE 1.5x the output, profiles/r02e_pmc_layers.txt)
-  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, 0x7FFFFFF0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(yb, (short)0, 0x7FFFFFF0, 0x00020000);
   const int yo = (w.ybase + m * p.y_ps) * 4;
   typedef int wg_i2 __attribute__((ext_vector_type(2)));
   if (w.c1ok) {
@@ -192,6 +198,18 @@ __device__ __forceinline__ void wg_store(const ConvParams& p, const WgTile& w, i
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, o[0]), yr, yo, 0, 0);
     if (w.r1ok) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, o[2]), yr, yo + p.W * 4, 0, 0);
   }
+}
+
+// the 16 position sums of one (channel m, tile) -> bias b (+ Relu) -> the tile's (up to) 4 pixels
+__device__ __forceinline__ void wg_store(const ConvParams& p, const WgTile& w, int m, float b, const float (&mx)[16]) {
+  float o[4];
+  wg_output_transform(mx, o);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    o[q] += b;
+    if (p.relu) o[q] = fmaxf(o[q], 0.0f);
+  }
+  wg_store_px(p, w, p.y, m, o);
 }
 
 // The K loop of both kernels over WG_LOAD_A(slot, step), WG_LOAD_B(slot, step), WG_MFMA(a slot, b slot)
@@ -206,6 +224,7 @@ __device__ __forceinline__ void wg_store(const ConvParams& p, const WgTile& w, i
     _Pragma("unroll") for (int s_ = 0; s_ < NKS; ++s_) {                                              \
       __builtin_amdgcn_sched_barrier(0);                                                               \
       WG_MFMAS(s_ % DA, vc_);                                                                          \
+      WG_EXTRA(s_ % DA, s_ % DB)                                                                       \
       if (s_ + 1 < NKS) { WG_WINDOWS((s_ + 1) % DB, vn_) }                                             \
       if (s_ + DA < NKS) { WG_LOAD_A(s_ % DA, s_ + DA) }                                               \
       if (s_ + DB < NKS) { WG_LOAD_B(s_ % DB, s_ + DB) }                                               \
@@ -231,6 +250,8 @@ __device__ __forceinline__ void wg_store(const ConvParams& p, const WgTile& w, i
     }                                                                                                  \
     _Pragma("unroll") for (int d_ = 0; d_ < 2; ++d_) { WG_MFMA(d_, d_); }                              \
   }
+
+#define WG_EXTRA(SA, SB)  // per-kernel hook after a k-step's MFMAs (conv_wino16_kernel E1)
 
 __device__ __forceinline__ int wg_block_wave(int* gw) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -339,9 +360,17 @@ __global__ __launch_bounds__(256, 1) void conv_wino32_kernel(ConvParams p) {
 }
 
 // 16x16x4 kernel: MF 16-channel fragments x NT 16-tile groups per wave (row slot j of fragment f is
-// channel m0 + MF j + f); k-steps of 4 channels; DA, DB, NKS as in conv_wino32_kernel
-template <int MF, int NT, int DA, int DB, int NKS>
+// channel m0 + MF j + f); k-steps of 4 channels; DA, DB, NKS as in conv_wino32_kernel.
+// E1 (NKS > 0 only): the 1x1 conv (+ bias, Relu) on the same input with the same output channels
+// (SqueezeNet's expand1x1 beside this expand3x3, ConvParams::e1_*) in the same K loop: its B operand at
+// tile pixel q is the window's centre value (already in registers, wg_centres), its A the MF
+// consecutive floats of its K-major packed weights (conv_stream_kernel's operand, one 4/8-B load per
+// k-step), 4 MF NT more 16x16x4 MFMAs per k-step in k order -- the standalone 1x1 kernels' fma chain,
+// so bit-identical -- and its pixels stored like the Winograd outputs.  The expand1x1 kernel and its
+// HBM read of the input disappear (fire8: 75 us per B = 256 step).
+template <int MF, int NT, int DA, int DB, int NKS, bool E1>
 __global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
+  static_assert(!E1 || NKS > 0, "the fused 1x1 conv needs the unrolled K loop");
   const int lane = threadIdx.x & 63;
   int gw;
   wg_block_wave(&gw);
@@ -376,12 +405,39 @@ __global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
 #pragma unroll
       for (int g = 0; g < NT; ++g) acc[xi][f][g] = wg_floatx4{0.f, 0.f, 0.f, 0.f};
   wg_floatx4 ra[DA][MF][4], rb[DB][NT][4];
+  // E1: accumulators [pixel q][f][g], biases, A ring (W1[m0 + MF lj + f][4 s + lk] at k-step s)
+  wg_floatx4 acc1[E1 ? 4 : 1][MF][NT];
+  float bias1[E1 ? MF : 1][4];
+  float ra1[E1 ? DA : 1][MF];
+  if constexpr (E1) {
+#pragma unroll
+    for (int f = 0; f < MF; ++f)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + MF * (4 * lk + e) + f;
+        bias1[f][e] = p.e1_bias && m < p.M ? p.e1_bias[m] : 0.0f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int g = 0; g < NT; ++g) acc1[q][f][g][e] = 0.0f;
+      }
+  }
+  const __amdgpu_buffer_rsrc_t e1r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(E1 ? p.e1_wp : p.wp), (short)0, E1 ? p.C * p.e1_Mp * 4 : 0, 0x00020000);
+  const int a1off = (lk * p.e1_Mp + m0 + MF * lj) * 4, a1step = 4 * p.e1_Mp * 4;
 #define WG_LOAD_A(SLOT, S)                                                                             \
   {                                                                                                    \
     const int st_ = (S);                                                                               \
     _Pragma("unroll") for (int f = 0; f < MF; ++f)                                                     \
     _Pragma("unroll") for (int i = 0; i < 4; ++i) ra[SLOT][f][i] = __builtin_bit_cast(                 \
         wg_floatx4, __builtin_amdgcn_raw_buffer_load_b128(ur, aoff + 16 * f + aq * i, st_ * astep, 0)); \
+    if constexpr (E1) {                                                                                \
+      static_assert(MF == 2, "E1: MF = 2 (one 8-B A load)");                                           \
+      typedef float wg_f2_ __attribute__((ext_vector_type(2)));                                        \
+      const wg_f2_ v_ = __builtin_bit_cast(wg_f2_, __builtin_amdgcn_raw_buffer_load_b64(e1r, a1off, st_ * a1step, 0)); \
+      ra1[SLOT][0] = v_[0];                                                                            \
+      ra1[SLOT][1] = v_[1];                                                                            \
+    }                                                                                                  \
   }
 #define WG_LOAD_B(SLOT, S)                                                                             \
   {                                                                                                    \
@@ -406,8 +462,21 @@ __global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
     _Pragma("unroll") for (int g = 0; g < NT; ++g) _Pragma("unroll") for (int i = 0; i < 16; ++i) D_[g][i] = S_[g][i];
 #define WG_NMFMA (16 * MF * NT)
 #define WG_VALU_PER_MFMA 2
+#undef WG_EXTRA
+#define WG_EXTRA(SA, SB)                                                                               \
+    if constexpr (E1) {                                                                                \
+      _Pragma("unroll") for (int g = 0; g < NT; ++g) {                                                 \
+        float c_[4];                                                                                   \
+        wg_centres(rb[SB][g], w[g], c_);                                                               \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q)                                                  \
+        _Pragma("unroll") for (int f = 0; f < MF; ++f)                                                 \
+            acc1[q][f][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra1[SA][f], c_[q], acc1[q][f][g], 0, 0, 0); \
+      }                                                                                                \
+    }
   float vc_[NT][16], vn_[NT][16];
   WG_KLOOP(p.C >> 2)
+#undef WG_EXTRA
+#define WG_EXTRA(SA, SB)
 #undef WG_MFMAS
 #undef WG_WINDOWS
 #undef WG_COPYV
@@ -429,6 +498,15 @@ __global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
 #pragma unroll
         for (int xi = 0; xi < 16; ++xi) mx[xi] = acc[xi][f][g][e];
         wg_store(p, w[g], m, bias[f][e], mx);
+        if constexpr (E1) {  // the 1x1 conv's channel m at tile lj's 4 pixels: + bias (+ Relu)
+          float o[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            o[q] = acc1[q][f][g][e] + bias1[f][e];
+            if (p.e1_relu) o[q] = fmaxf(o[q], 0.0f);
+          }
+          wg_store_px(p, w[g], p.e1_y, m, o);
+        }
       }
     }
 }
@@ -918,6 +996,13 @@ static bool wl_geom(const ConvParams& p, WlGeom* g, int* ni, size_t* lds) {
   return *lds <= 160 * 1024;
 }
 
+// the fused 1x1 conv (ConvParams::e1_*) runs in the unrolled 16x16 kernel of tile 2 (32 channels x
+// 16 tiles per wave: room for its accumulators beside the Winograd ones)
+bool conv_wino_e1_eligible(const ConvParams& p, int tile) {
+  return tile == 2 && p.C % 16 == 0 && p.C >= 16 && p.C <= 64 && p.e1_wp && p.e1_y && p.e1_Mp >= (p.M + 31) / 32 * 32 &&
+         (long long)p.C * p.e1_Mp * 4 < (1LL << 31) && conv_wino_eligible(p, tile);
+}
+
 bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo) {
   return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && Ho == H && Wo == W && C % 16 == 0 && C > 0;
 }
@@ -1006,7 +1091,17 @@ void launch_conv_wino(const ConvParams& p0, int tile, hipStream_t s) {
   const int cq = p.C % 16 == 0 && p.C <= 64 ? p.C / 16 : 0;
 #define WG_L32(DA_, DB_, CQ) hipLaunchKernelGGL((conv_wino32_kernel<DA_, DB_, 8 * CQ>), grid, dim3(256), 0, s, p)
 #define WG_L16(MF_, NT_, DA_, DB_, CQ) \
-  hipLaunchKernelGGL((conv_wino16_kernel<MF_, NT_, DA_, DB_, 4 * CQ>), grid, dim3(256), 0, s, p)
+  hipLaunchKernelGGL((conv_wino16_kernel<MF_, NT_, DA_, DB_, 4 * CQ, false>), grid, dim3(256), 0, s, p)
+#define WG_L16E(CQ) hipLaunchKernelGGL((conv_wino16_kernel<2, 1, 2, 8, 4 * CQ, true>), grid, dim3(256), 0, s, p)
+  if (p.e1_y) {  // the fused 1x1 conv: tile 2, C in 16..64 by 16 (conv_wino_e1_eligible)
+    switch (cq) {
+      case 1: WG_L16E(1); break;
+      case 2: WG_L16E(2); break;
+      case 3: WG_L16E(3); break;
+      default: WG_L16E(4); break;
+    }
+    return;
+  }
 #define WG_BY_C(L, ...)                         \
   switch (cq) {                                 \
     case 1: L(__VA_ARGS__, 1); break;           \
@@ -1023,6 +1118,7 @@ void launch_conv_wino(const ConvParams& p0, int tile, hipStream_t s) {
   }
 #undef WG_BY_C
 #undef WG_L16
+#undef WG_L16E
 #undef WG_L32
 }
 

@@ -95,7 +95,17 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
                     int64_t x_nstride, const float* wp, const int2* ktab, int64_t M, int64_t kh, int64_t kw,
                     const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, float* y,
                     int64_t y_nstride, int64_t x_ps = 0, int64_t y_ps = 0,  // plane strides, 0 = dense
-                    int x_es = 4);  // input element bytes (2: f16; only with an f16 plan, whose output is f16)
+                    int x_es = 4,   // input element bytes (2: f16; only with an f16 plan, whose output is f16)
+                    const struct ConvE1* e1 = nullptr);  // Winograd plans: a 1x1 conv fused in (ConvParams::e1_*)
+// a 1x1 conv (+ bias, Relu) on the same input as a Winograd 3x3 conv with the same output channels,
+// computed by the Winograd launch; y has the 3x3 conv output's plane and image strides
+struct ConvE1 {
+  const float* wp;  // standard K-major packing [C][Mp]
+  const float* bias;
+  float* y;
+  int64_t Mp;
+  bool relu;
+};
 // the MaxPool fused into an f16 conv's epilogue (ORE_FUSE_CONV_POOL; 3x3 / stride 2)
 struct F16Epool {
   int64_t kh, kw, sh, sw;

@@ -63,6 +63,12 @@ struct ConvParams {
   int ep_variant;      // pooled-conv kernel (launch_conv_epool): 0 auto, 1 patch, 2 / 3 row walk
   const float* wc1;    // variant 7: weights in launch_pack_c1_f32 layout (null: variant 7 unavailable)
   const struct C1SqueezeF32* sq1;  // variant 7 with the next 1x1 conv fused in (forces variant 7)
+  // Winograd 32x32 tiles: a 1x1 conv (+ bias, Relu) on the same input with the same M output channels
+  // computed in the same launch (conv_wino_e1_eligible); e1_y has y's plane and image strides
+  const float* e1_wp;  // K-major packed [C][e1_Mp] (the standard 1x1 packing)
+  const float* e1_bias;
+  float* e1_y;         // null: no fused 1x1 conv
+  int e1_Mp, e1_relu;
 };
 
 // Per-layer kernel choice and weight layout (see plan_conv in ore_conv.hip).
@@ -329,6 +335,7 @@ constexpr int WINO_TILE_BASE = X3_TILE_BASE + X3_TILES;
 constexpr int WINO_TILES_N = 5;
 bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo);
 bool conv_wino_eligible(const ConvParams& p, int tile);
+bool conv_wino_e1_eligible(const ConvParams& p, int tile);
 int wino_packed_mp(int M);
 void launch_pack_wino(const float* w, int M, int C, int Mp, float* u, hipStream_t s);
 void launch_conv_wino(const ConvParams& p, int tile, hipStream_t s);

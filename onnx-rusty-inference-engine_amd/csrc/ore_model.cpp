@@ -114,6 +114,14 @@ struct Step {
   bool has_wino = false;
   ConvPlan plan_wino{};
   float* wp_wino = nullptr;
+  // (3b) a Winograd step that also computes the 1x1 conv beside it (SqueezeNet's expand1x1 next to
+  // this expand3x3, both writing slices of one Concat): that conv's output value, packed weights
+  // (its own plan's K-major layout), row stride, bias and Relu
+  int e1_out = -1;
+  const float* e1_wp = nullptr;
+  int64_t e1_Mp = 0;
+  const float* e1_b = nullptr;
+  bool e1_relu = false;
   void* xcvt = nullptr;        // f16 F16_X_NHWC_PAIR: the f32 NCHW input converted to NHWC4 f16 (max_batch)
   const float* wc1 = nullptr;  // f32 pooled first conv: weights for pooled-conv variant 7 (launch_pack_c1_f32)
   // f16 pooled first conv with the next 1x1 conv (+ Relu) fused in (conv_pair_pool_f16_kernel SQ):
@@ -1138,6 +1146,45 @@ ore_status plan(ore_model* m) {
       s.kind = S_NOP;
     }
   }
+  // (3b) f32: a 1x1 Conv that reads the same input as a Winograd 3x3 Conv with as many output channels,
+  // both writing slices of one Concat (SqueezeNet's fire8 / fire9 expand1x1 beside expand3x3), runs
+  // inside the Winograd launch (conv_wino32_kernel E1: the 1x1 conv's B operand is the window centre
+  // the transform already loaded; its k-ordered chain is bit-identical to the standalone kernels').
+  // Opt-in (ORE_WINO_E1=1): measured equal or slower at B = 256 (fire8: 451.6 us fused vs 75.6 + 369.5
+  // separate; bench 66.1 k vs 66.3 k img/s, profiles/r02j_wino_e1_ab.txt) -- the 16x16 kernel pays
+  // the extra MFMAs in full, and the 32x32 kernels, which would hide them, have no registers left.
+  if (m->wino && (m->fusion & ORE_FUSE_CONCAT)) {
+    const char* ee = getenv("ORE_WINO_E1");
+    const bool on = ee && atoi(ee) != 0;
+    for (size_t t = 0; on && t < m->steps.size(); ++t) {
+      Step& w3 = m->steps[t];
+      if (w3.kind != S_CONV || !w3.plan.wino || w3.pool || w3.epool || w3.e1_out >= 0 || w3.C % 16 || w3.C > 64) continue;
+      const Value& b = m->values[w3.out];
+      if (!b.slice || b.alias_of < 0) continue;
+      for (size_t k = 0; k < m->steps.size(); ++k) {
+        Step& q = m->steps[k];
+        if (k == t || q.kind != S_CONV || q.in0 != w3.in0 || q.C != w3.C || q.M != w3.M || q.H != w3.H || q.W != w3.W ||
+            q.kh != 1 || q.kw != 1 || q.sh != 1 || q.sw != 1 || q.win.pt || q.win.pl || q.pool || q.epool ||
+            q.plan.window || q.plan.f16 || q.plan.x3 || q.plan.wino || !q.wp)
+          continue;
+        const Value& a = m->values[q.out];
+        if (!a.slice || a.alias_of != b.alias_of) continue;
+        w3.e1_out = q.out;
+        w3.plan.cfg = WINO_TILE_BASE + 2;  // the kernel that takes the fused conv (conv_wino_e1_eligible)
+        w3.e1_wp = q.wp;
+        w3.e1_Mp = q.plan.Mp;
+        w3.e1_b = q.in2 >= 0 ? m->values[q.in2].cptr : nullptr;
+        w3.e1_relu = q.relu;
+        w3.flops_per_img += q.flops_per_img;
+        w3.bytes_per_img += 4.0 * double(q.M * q.H * q.W);
+        w3.name = q.name + "+" + w3.name;
+        q.kind = S_NOP;
+        q.in0 = -1;
+        break;
+      }
+    }
+    count_uses(m, m->steps);
+  }
   // aliases of aliases must stay contiguous views (Reshape/Dropout of a channel slice)
   for (auto& v : m->values) {
     if (v.alias_of < 0 || v.slice) continue;
@@ -1283,7 +1330,7 @@ ore_status plan(ore_model* m) {
     for (size_t k = 0; k + 1 < m->exec_steps.size(); ++k) {
       if (k > 0 && m->pair_next[k - 1]) continue;  // pairs only
       const Step &A = m->steps[m->exec_steps[k]], &B = m->steps[m->exec_steps[k + 1]];
-      bool ok = A.out >= 0 && B.out >= 0;
+      bool ok = A.out >= 0 && B.out >= 0 && A.e1_out < 0 && B.e1_out < 0;  // (3b) steps write two values
       for (int bi : {B.in0, B.in1, B.in2}) ok = ok && !overlap(bi, A.out);
       for (int ai : {A.in0, A.in1, A.in2}) ok = ok && !overlap(ai, B.out);
       ok = ok && !overlap(A.out, B.out);
@@ -1411,8 +1458,16 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
                              s.relu, y.p, y.nstride, y.ps, x.es);
       ctx->mapped_lo = m->arena_alloc;  // the arena and its 4 KiB lead are mapped
       ctx->mapped_hi = m->arena ? m->arena + m->arena_bytes : nullptr;
+      ConvE1 e1{};
+      if (s.e1_out >= 0) {
+        const Ref y1 = ref_of(m, s.e1_out);
+        if (y1.nstride != y.nstride || y1.ps != y.ps)
+          return err(m, ORE_ERR_INVALID, "internal: fused 1x1 conv output strides differ from the 3x3 conv's");
+        e1 = ConvE1{s.e1_wp, s.e1_b, y1.p, s.e1_Mp, s.e1_relu};
+      }
       const ore_status st = run_conv(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, s.wp, s.ktab, s.M, s.kh, s.kw, bias,
-                                     s.win, s.sh, s.sw, s.relu, y.p, y.nstride, x.ps, y.ps, x.es);
+                                     s.win, s.sh, s.sw, s.relu, y.p, y.nstride, x.ps, y.ps, x.es,
+                                     s.e1_out >= 0 ? &e1 : nullptr);
       ctx->mapped_lo = ctx->mapped_hi = nullptr;
       return st;
     }
@@ -1904,7 +1959,8 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
     } else if (s.plan.wino) {  // the Winograd tiles (its packed layout); tile 4 (LDS-staged) measured
       // slower on every SqueezeNet expand3x3 (profiles/r02c_wino_tiles.txt): forced only (ORE_WINO_TILE=4)
       cands.clear();
-      for (int c = 0; c < 4; ++c) cands.push_back(WINO_TILE_BASE + c);
+      for (int c = 0; c < 4; ++c)
+        if (s.e1_out < 0 || c == 2) cands.push_back(WINO_TILE_BASE + c);  // a fused 1x1 conv: tile 2 only
     } else if (!s.plan.f16 && !(ews && !atoi(ews))) cands.insert(cands.end(), {8, 9, 10, 11});
     // the LDS-free streaming kernel (tiles 12-20) where the geometry allows it (launch_conv falls
     // back to tile 0 elsewhere, and such candidates are skipped below)

@@ -141,9 +141,10 @@ float* pack_to_scratch(ore_ctx* ctx, const ConvPlan& pln, const float* w, bool k
 ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
                     int64_t x_nstride, const float* wp, const int2* ktab, int64_t M, int64_t kh, int64_t kw,
                     const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, float* y,
-                    int64_t y_nstride, int64_t x_ps, int64_t y_ps, int x_es) {
+                    int64_t y_nstride, int64_t x_ps, int64_t y_ps, int x_es, const ConvE1* e1) {
   if (N == 0) return ORE_OK;
   if (pln.f16 || x_es != 4) return set_error(ctx, ORE_ERR_INVALID, "internal: run_conv takes f32 plans and inputs");
+  if (e1 && !pln.wino) return set_error(ctx, ORE_ERR_INVALID, "internal: a fused 1x1 conv needs a Winograd plan");
   if (x_ps == 0) x_ps = H * W;
   if (y_ps == 0) y_ps = win.Ho * win.Wo;
   ConvParams p{};
@@ -162,6 +163,9 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
   p.relu = relu ? 1 : 0;
   p.Mp = pln.Mp;
   p.x_f32 = 1;
+  if (e1) {
+    p.e1_wp = e1->wp; p.e1_bias = e1->bias; p.e1_y = e1->y; p.e1_Mp = int(e1->Mp); p.e1_relu = e1->relu ? 1 : 0;
+  }
   {  // extent of x for the B-tile DMA path's buffer resource (32-bit byte offsets)
     const int64_t extent = ((N - 1) * x_nstride + C * x_ps) * int64_t(x_es);
     p.x_bytes = (extent > 0 && extent < (int64_t(1) << 31)) ? extent : 0;
@@ -198,6 +202,11 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
       q.N = int(nc);
       q.Ntot = nc * y_ps;
       q.x_bytes = ((nc - 1) * x_nstride + C * x_ps) * 4;
+      if (e1) {
+        q.e1_y = e1->y + i0 * y_nstride;
+        if (!conv_wino_e1_eligible(q, 2))
+          return set_error(ctx, ORE_ERR_INVALID, "internal: fused 1x1 conv outside the Winograd 32x32 kernels' limits");
+      }
       launch_conv(q, pln, ctx->stream);
       ORE_HIP_CHECK(ctx, hipGetLastError());
     }
