@@ -58,6 +58,52 @@ def parse():
     return ap.parse_args()
 
 
+def lib_sha256():
+    """sha256 of the libore.so this process loaded (ties a PMC traffic file to the benched build)."""
+    import hashlib
+    from ore import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def roofline_8d(infos, per_step_ms, ms_per_step, peak_tflops, peak_gbs=PEAK_HBM_GBS):
+    """each launch is bound by its own FLOP:byte ratio, bound_time = max(algorithmic
+    FLOPs / MFMA peak, algorithmic bytes / HBM peak); achieved fraction = bound_time / measured time,
+    per launch, per op class and for the whole network (against the timed ms_per_step, launch gaps
+    included).  `issued` beside it counts the MFMA FLOPs the kernels execute (Winograd issues 16 C M
+    per 2x2 tile, not the direct 36 C M): the Winograd-honest use of the matrix cores."""
+    steps, classes = [], {}
+    tot_bound = 0.0
+    for info, ms in zip(infos, per_step_ms):
+        t_f = info["flops"] / (peak_tflops * 1e12) * 1e3
+        t_b = info["bytes"] / (peak_gbs * 1e9) * 1e3
+        bound = max(t_f, t_b)
+        tot_bound += bound
+        kind = "mfma" if t_f >= t_b else "hbm"
+        steps.append({"name": info["name"], "op": info["op"], "bound": kind, "us": round(1000 * float(ms), 1),
+                      "bound_us": round(1000 * bound, 1), "frac": round(bound / max(float(ms), 1e-9), 3)})
+        c = classes.setdefault(info["op"], {"ms": 0.0, "bound_ms": 0.0, "flops": 0.0, "mfma_flops": 0.0, "bytes": 0.0,
+                                            "launches": 0})
+        c["ms"] += float(ms)
+        c["bound_ms"] += bound
+        c["flops"] += info["flops"]
+        c["mfma_flops"] += info.get("mfma_flops", info["flops"])
+        c["bytes"] += info["bytes"]
+        c["launches"] += 1
+    per_class = {}
+    for k, c in classes.items():
+        per_class[k] = {"launches": c["launches"], "ms": round(c["ms"], 4), "bound_ms": round(c["bound_ms"], 4),
+                        "frac": round(c["bound_ms"] / max(c["ms"], 1e-9), 4),
+                        "TFLOP/s": round(c["flops"] / (c["ms"] * 1e-3) / 1e12, 2) if c["flops"] else None,
+                        "issued_TFLOP/s": round(c["mfma_flops"] / (c["ms"] * 1e-3) / 1e12, 2) if c["flops"] else None,
+                        "GB/s": round(c["bytes"] / (c["ms"] * 1e-3) / 1e9, 1)}
+    return {"peaks": {"mfma_TFLOP/s": peak_tflops, "hbm_GB/s": peak_gbs},
+            "network": {"bound_ms": round(tot_bound, 4), "ms_per_step": round(ms_per_step, 4),
+                        "frac": round(tot_bound / ms_per_step, 4),
+                        "kernel_ms": round(float(sum(per_step_ms)), 4)},
+            "per_class": per_class, "per_launch": steps}, classes
+
+
 def cpu_baseline(model_bytes, hw, threads):
     """The oracle in the reference's cost structure (per-dot heap buffer, im2col, weights decoded
     per op call), one independent batch-1 image per thread — timed on this host."""
@@ -152,13 +198,15 @@ def f16_line(ctx, model_bytes, x, B, args, ref):
     conv_ms = sum(p for p, i in zip(per, infos) if i["op"] == "Conv")
     conv_fl = sum(i["flops"] for i in infos if i["op"] == "Conv")
     achieved = conv_fl / (conv_ms * 1e-3) / 1e12
-    y = out[:2].cpu().numpy()
+    r8d, _ = roofline_8d(infos, per, 1000.0 * elapsed / args.steps, PEAK_F16_MFMA_TFLOPS)
+    y = out[:ref.shape[0]].cpu().numpy()  # the first rows of x, whose oracle rows are ref
     res = {"value": round(B * args.steps / elapsed, 2), "unit": "images/s",
            "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "dtype": "f16",
            "conv_TFLOP/s": round(achieved, 2), "roofline_frac": round(achieved / PEAK_F16_MFMA_TFLOPS, 4),
            "conv_launches": sum(1 for i in infos if i["op"] == "Conv"),
            "max_abs_diff_vs_cpu": float(np.abs(y - ref).max()),
            "top1_agrees_with_cpu": bool((y.argmax(1) == ref.argmax(1)).all()),
+           "roofline_8d": {"network": r8d["network"], "per_class": r8d["per_class"]},
            "note": "config 5 (BASELINE.json configs[4]) on the same batch; fused f16 kernels, DESIGN.md 3.1.1"}
     m.close()
     return res
@@ -171,7 +219,7 @@ def main():
     import torch.distributed as dist
 
     import ore
-    from ore import squeezenet
+    from ore import parallel, squeezenet
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -182,20 +230,32 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    # one seeded global batch of G images (config 4: --global-batch 2048 split over the GPUs; by
+    # default weak scaling, G = world x --batch), generated identically on every rank; each rank
+    # keeps its contiguous slice (ore.parallel.shard_bounds) resident in HBM
     strong = args.global_batch > 0
-    if strong and args.global_batch % world:
-        raise SystemExit(f"--global-batch {args.global_batch} does not split over {world} GPUs")
-    B = args.global_batch // world if strong else args.batch
+    G = args.global_batch if strong else world * args.batch
+    if G % world:
+        raise SystemExit(f"--global-batch {G} does not split evenly over {world} GPUs")
+    lo, hi = parallel.shard_bounds(G, world, rank)
+    B = hi - lo
     model_bytes = squeezenet.build(args.hw)
     ctx = ore.Context(local)
     model = ore.Model(ctx, model_bytes, max_batch=B, precision=args.precision, winograd=not args.no_winograd)
     f16 = args.precision == "f16"
     x3 = args.precision == "f32x3"
     g = torch.Generator(device=f"cuda:{local}")
-    g.manual_seed(1000 + rank)
-    x = (torch.rand((B, 3, args.hw, args.hw), generator=g, device=f"cuda:{local}") * 100.0 - 50.0).contiguous()
+    g.manual_seed(1000)
+    xg = torch.rand((G, 3, args.hw, args.hw), generator=g, device=f"cuda:{local}") * 100.0 - 50.0
+    x = xg[lo:hi].contiguous()
+    # the max-abs sample: the first image of rank 0's slice and the last of the last rank's, so the
+    # check covers the gathered rows of both ends of the global batch
+    sample_idx = [0, G - 1]
+    x_sample = xg[sample_idx].cpu().numpy() if rank == 0 else None
+    del xg
+    torch.cuda.empty_cache()
     out = torch.empty((B, model.output_elems), dtype=torch.float32, device=f"cuda:{local}")
-    gathered = torch.empty((world * B, model.output_elems), dtype=torch.float32, device=f"cuda:{local}") \
+    gathered = torch.empty((G, model.output_elems), dtype=torch.float32, device=f"cuda:{local}") \
         if world > 1 else out
 
     if args.fusion is not None:
@@ -211,7 +271,7 @@ def main():
     def step():
         model.run_into(x, out)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
+            parallel.gather_rows_into(gathered, out)
 
     for _ in range(args.warmup):
         step()
@@ -266,17 +326,12 @@ def main():
                                 "tile_per_conv": [ore.Model.TILE_NAMES[t] for t in model.tiles() if t >= 0]}
         if timing:
             per_step_ms /= args.steps
-            classes = {}
-            for info, ms in zip(infos, per_step_ms):
-                c = classes.setdefault(info["op"], {"ms": 0.0, "flops": 0.0, "bytes": 0.0, "launches": 0})
-                c["ms"] += float(ms)
-                c["flops"] += info["flops"]
-                c["bytes"] += info["bytes"]
-                c["launches"] += 1
-            conv = classes.get("Conv", {"ms": 1e-9, "flops": 0.0, "bytes": 0.0, "launches": 1})
-            achieved = conv["flops"] / (conv["ms"] * 1e-3) / 1e12
             # x3: every f32 MAC is six bf16 part products on the 2.5 PF/s BF16 matrix cores
             peak = PEAK_F16_MFMA_TFLOPS if f16 else PEAK_F16_MFMA_TFLOPS / 6.0 if x3 else PEAK_F32_MFMA_TFLOPS
+            r8d, classes = roofline_8d(infos, per_step_ms, 1000.0 * elapsed / args.steps, peak)
+            conv = classes.get("Conv", {"ms": 1e-9, "flops": 0.0, "mfma_flops": 0.0, "bytes": 0.0, "launches": 1})
+            achieved = conv["flops"] / (conv["ms"] * 1e-3) / 1e12
+            issued = conv["mfma_flops"] / (conv["ms"] * 1e-3) / 1e12
             kname = ("Conv class: conv_pair_pool_f16_kernel (conv1 + pool1 straight from the f32 input), "
                      "fire_f16_kernel / fire_pool_f16_kernel (fire module [+ MaxPool] + next squeeze) and "
                      "conv_f16_kernel (implicit GEMM), all MFMA 32x32x16 f16 with f32 accumulate" if f16 else
@@ -285,62 +340,66 @@ def main():
                      "Conv class: conv_stream_kernel (LDS-free implicit GEMM, MFMA 16x16x4 f32), fire_kernel (fire "
                      "module + next squeeze), fire_pool_kernel (fire4 + pool3 + fire5 squeeze), "
                      "conv_win_pool_f32_kernel (conv1 + pool1 + fire2 squeeze), pool_conv1x1_f32_kernel (pool5 + "
-                     "fire9 squeeze), "
-                     "conv_wino32/16_kernel (Winograd F(2x2,3x3) expand3x3, FLOPs counted as direct) and "
+                     "fire9 squeeze), conv_wino32/16_kernel (Winograd F(2x2,3x3) expand3x3) and "
                      "conv_gemm_kernel (LDS-staged, MFMA 32x32x2 f32) per the autotuned tile") + f", {conv['launches']} launches/step)"
             # HBM bytes per conv launch from the PMC passes of tools/pmc.sh (FETCH_SIZE x2 +
             # WRITE_SIZE, separate --pmc runs; counters cannot be read inside this timed run)
-            traffic, tsrc = None, None
+            traffic, tsrc, tsame = None, None, None
             tfile = os.path.join(REPO, "profiles", f"pmc_traffic_{args.precision}.json")
             if os.path.exists(tfile):
                 with open(tfile) as f:
                     tj = json.load(f)
                 traffic = round(tj["hbm_bytes_per_launch"])
-                tsrc = (f"profiles/pmc_traffic_{args.precision}.json: PMC FETCH_SIZE/WRITE_SIZE passes of an earlier "
-                        f"rocprofv3 run ({tj.get('source', 'tools/pmc.sh')}), not measured in this run")
+                tsame = tj.get("lib_sha256") == lib_sha256()
+                tsrc = (f"profiles/pmc_traffic_{args.precision}.json: PMC FETCH_SIZE/WRITE_SIZE passes "
+                        f"({tj.get('source', 'tools/pmc.sh')}, commit {tj.get('commit', '?')}); "
+                        f"{'the same libore.so build as this run' if tsame else 'an earlier libore.so build'}")
             result["roofline"] = {
                 "bound": "mfma", "kernel": kname,
                 "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-                "traffic_source": tsrc,
+                "traffic_source": tsrc, "traffic_same_build": tsame,
+                "achieved_is": "effective: algorithmic (direct-conv) FLOPs / measured time; Winograd layers count "
+                               "their direct FLOPs",
+                "issued_TFLOP/s": round(issued, 2), "issued_frac": round(issued / peak, 4),
                 "algorithmic_bytes_per_launch": round(conv["bytes"] / max(conv["launches"], 1)),
                 "per_launch_avg_us": round(1000.0 * conv["ms"] / conv["launches"], 2),
                 "algorithmic": "2*Cout*Ho*Wo*Cin*kh*kw per image (1.638 GFLOP/img)",
                 "kernel_timing": f"HIP events between consecutive launches on the model stream, a second pass of "
                                  f"the {args.steps} timed steps (events kept out of the value's timed loop)"}
+            result["roofline_8d"] = r8d
             if args.layers:
                 for info, ms in zip(infos, per_step_ms):
                     tf = info["flops"] / (ms * 1e-3) / 1e12 if info["flops"] else 0.0
                     gbs = info["bytes"] / (ms * 1e-3) / 1e9
                     print(f"{info['name']:24s} {info['op']:18s} {1000 * ms:9.1f} us {tf:7.1f} TF/s {gbs:8.1f} GB/s",
                           file=sys.stderr)
-            result["breakdown_ms_per_step"] = {
-                k: {"ms": round(v["ms"], 4), "launches": v["launches"],
-                    "TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["flops"] else None,
-                    "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1)} for k, v in classes.items()}
-        if world == 1:
-            # max-abs vs the CPU restatement on a bounded sample (2 images of this batch)
-            import oracle
-            torch.cuda.synchronize()
-            xs = x[:2].cpu().numpy()
-            ref = oracle.Model(model_bytes).run(xs, 1000)
-            result["max_abs_diff_vs_cpu"] = float(np.abs(out[:2].cpu().numpy() - ref).max())
-            result["max_abs_sample"] = "2 images of the timed batch vs oracle (C restatement of the reference, f32)"
-            if f16:
-                result["top1_agrees_with_cpu"] = bool((out[:2].cpu().numpy().argmax(1) == ref.argmax(1)).all())
-            if not f16 and not x3 and not args.no_f16_line:
-                result["f16"] = f16_line(ctx, model_bytes, x, B, args, ref)
-            if not args.no_b1:
-                result["b1_latency_ms"] = b1_latency(model_bytes, args.hw, local, args.precision,
-                                                     winograd=not args.no_winograd)
-            if not args.no_cpu_baseline:
-                threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-                result["cpu_baseline"] = cpu_baseline(model_bytes, args.hw, threads)
+        # max-abs vs the CPU restatement on a bounded sample: global images 0 and G - 1 as they come
+        # out of the timed steps (for N > 1 out of the gathered rows, i.e. through the collective)
+        import oracle
+        torch.cuda.synchronize()
+        got = gathered[sample_idx].cpu().numpy()
+        ref = oracle.Model(model_bytes).run(x_sample, 1000)
+        result["max_abs_diff_vs_cpu"] = float(np.abs(got - ref).max())
+        result["max_abs_sample"] = (f"global images {sample_idx} of the timed batch"
+                                    f"{' (gathered over RCCL)' if world > 1 else ''} vs the oracle "
+                                    f"(C restatement of the reference, f32)")
+        if f16:
+            result["top1_agrees_with_cpu"] = bool((got.argmax(1) == ref.argmax(1)).all())
+        if not f16 and not x3 and not args.no_f16_line:
+            result["f16"] = f16_line(ctx, model_bytes, x, B, args, ref[:1])  # global image 0 = x[0] on rank 0
+        if not args.no_b1:
+            result["b1_latency_ms"] = b1_latency(model_bytes, args.hw, local, args.precision,
+                                                 winograd=not args.no_winograd)
+        if not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            result["cpu_baseline"] = cpu_baseline(model_bytes, args.hw, threads)
         print(json.dumps(result), flush=True)
 
     model.close()
     ctx.close()
     if world > 1:
+        dist.barrier()  # the other ranks wait here while rank 0 runs the reporting legs
         dist.destroy_process_group()
 
 

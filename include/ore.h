@@ -96,12 +96,24 @@ const char* ore_last_error(ore_ctx* ctx);
 /* Conv algorithm of the per-op entry ore_conv2d_f32 on this context (extension; the reference has
  * one algorithm, im2col + per-channel dots, convolution_op.rs:224-517).  ORE_CONV_ALGO_DIRECT (the
  * default): the implicit GEMM in the reference's k order.  ORE_CONV_ALGO_WINOGRAD: 3x3 / stride-1 /
- * pad-1 convs with C % 8 == 0 by Winograd F(2x2, 3x3) in f32 (2.25x fewer MFMAs; its error against a
+ * pad-1 convs with C % 16 == 0 by Winograd F(2x2, 3x3) in f32 (2.25x fewer MFMAs; its error against a
  * float64 reference is at or below the direct f32 conv's, but results are not bit-identical to it);
  * other geometries stay direct.  Models choose per ORE_LOAD_NO_WINOGRAD instead. */
 #define ORE_CONV_ALGO_DIRECT 0
 #define ORE_CONV_ALGO_WINOGRAD 1
 ore_status ore_ctx_set_conv_algo(ore_ctx* ctx, int32_t algo);
+/* Kernel selection for parity tests and tuning (extension).  Results never depend on it: every conv
+ * tile of one algorithm computes each output by the same k-ordered chain, every MaxPool kernel the
+ * same max.
+ *  ore_ctx_set_conv_tile: every conv planned on this context afterwards -- ore_conv2d_f32 /
+ *    ore_matmul_f32 calls, and models loaded later -- uses tile id `tile` where it belongs to the
+ *    layer's kernel family (else the per-layer heuristic); -1 (default) = the heuristic.  Ids as
+ *    ore_model_step_tile reports them (0-3 LDS-staged, 12-20 streaming, 28-35 x3, 36-39 Winograd).
+ *  ore_ctx_set_pool_variant: MaxPool kernel of ore_maxpool2d_f32 and of the walker's MaxPool steps:
+ *    0 (default) = by layout, 2 one thread per output, 3 column strips, 4 plane-staged, 5
+ *    chunk-staged. */
+ore_status ore_ctx_set_conv_tile(ore_ctx* ctx, int32_t tile);
+ore_status ore_ctx_set_pool_variant(ore_ctx* ctx, int32_t variant);
 
 ore_status ore_malloc(ore_ctx* ctx, size_t bytes, void** dptr);
 ore_status ore_free(ore_ctx* ctx, void* dptr);
@@ -173,35 +185,35 @@ ore_status ore_model_parse(const void* onnx_bytes, size_t len);
  * The fire / pooled-conv fusions are f32-MFMA kernels and are not applied to an x3 model. */
 #define ORE_LOAD_X3 2
 /* ORE_LOAD_NO_WINOGRAD: an f32 model runs its 3x3 / stride-1 / pad-1 convs (SqueezeNet's
- * expand3x3) on the direct kernels only.  By default (f32 models, not x3) every such conv that no
- * direct-kernel fusion takes runs Winograd F(2x2, 3x3) in f32 (ore_conv_wino.hip; see
- * ORE_CONV_ALGO_WINOGRAD above).  The choice is made at load time, never by timing. */
+ * expand3x3) on the direct kernels only, every output in the reference's k order.  By default (f32
+ * models, not x3) every such conv with C % 16 == 0 that no direct-kernel fusion takes runs Winograd
+ * F(2x2, 3x3) in f32 (ore_conv_wino.hip; see ORE_CONV_ALGO_WINOGRAD above).  NOTE: this makes the
+ * default f32 results differ from the direct path by rounding (synthetic SqueezeNet @224: 6e-6
+ * max-abs against the oracle vs 2e-7 direct, within the 1e-5 parity bound); load with this flag for
+ * the reference's summation order.  The choice is made at load time, never by timing. */
 #define ORE_LOAD_NO_WINOGRAD 4
+/* ORE_LOAD_X3_ALL: ORE_LOAD_X3 on every conv / MatMul, with no f32-MFMA fusion (tests of the x3
+ * kernels). */
+#define ORE_LOAD_X3_ALL 8
 ore_status ore_model_load_ex(ore_ctx* ctx, const void* onnx_bytes, size_t len, int64_t max_batch, int32_t flags,
                              ore_model** out);
 ore_status ore_model_destroy(ore_model* m);
-/* flags: bit 0 = fuse Conv->Relu, bit 1 = Concat in place, bit 2 = alias Dropout/Reshape,
- * bit 5 = Conv->MaxPool (ORE_FUSE_CONV_POOL below), bit 6 = fire module + next squeeze
- * (ORE_FUSE_FIRE below), bit 7 = Concat->MaxPool in the producers (ORE_FUSE_CONCAT_POOL below).
- * ORE_FUSE_ALL is the default; 0 runs every node as its own kernel
- * (op-by-op parity). */
+/* Fusion flags (ore_model_set_fusion; ORE_FUSE_ALL is the default, 0 runs every node as its own kernel
+ * for op-by-op parity).  Every fusion is exact: the fused kernels compute each output by the same
+ * arithmetic as the separate ones, so results do not depend on the flags (tested bit for bit).
+ * bit 0 = fuse Conv->Relu, bit 1 = Concat in place (and padded channel planes), bit 2 = alias
+ * Dropout / Reshape; bits 5-10 below.  Bit 4 is retired (a MaxPool inside a 1x1 conv's operand
+ * gather, measured slower). */
 #define ORE_FUSE_CONV_RELU 1
 #define ORE_FUSE_CONCAT 2
 #define ORE_FUSE_ALIAS 4
-#define ORE_FUSE_ALL 231
-/* bit 4 (opt-in, not in ORE_FUSE_ALL): a 3x3 MaxPool whose only consumer is a 1x1 stride-1 Conv
- * runs inside that conv's operand gather (each B element = the window max of the pre-pool
- * tensor); the pooled tensor is never written.  Max is exact, so results are bit-identical.
- * Measured slower than the separate plane-staged pool on SqueezeNet (9 loads per operand
- * element lose the pool kernel's row reuse: +150 us per step at batch 256). */
-#define ORE_FUSE_POOL_CONV 16
+#define ORE_FUSE_ALL 2023
 /* bit 5 (in ORE_FUSE_ALL): Conv (-> Relu) -> 3x3 / stride-2 MaxPool as ONE launch when the conv
  * output has no other consumer: each block computes a 13 x 19 patch of conv outputs covering a
  * 6 x 9 tile of pooled outputs (the overlapping window row / column is recomputed by the
  * neighbouring tile) and stores only the pooled values; the pre-pool tensor never reaches HBM.
  * Bit-identical (same per-output MFMA chain; max is exact).  Applied when the computed columns are
- * <= ORE_EPOOL_MAX_WORK (environment, default 1.25) x the conv's own (SqueezeNet @224: conv1 +
- * pool1 only, 1.16x).  f32 models: ore_model_autotune also times the row-walking kernels
+ * <= 1.25 x the conv's own (SqueezeNet @224: conv1 + pool1 only, 1.16x).  f32 models: ore_model_autotune also times the row-walking kernels
  * (ore_conv_pool.hip: a block walks the conv plane row-major and max-reduces into an LDS ring of
  * pooled rows, nothing recomputed) and keeps the fastest -- conv1 + pool1: 96 channels x 128
  * quads per block, 1016 -> ~900 us at batch 256. */
@@ -210,19 +222,31 @@ ore_status ore_model_destroy(ore_model* m);
  * channel counts) and the 1x1 Conv + Relu (<= 64 channels) that is the Concat's only reader -- the
  * next fire's squeeze -- as ONE launch: the expand outputs and the Concat never reach HBM.
  * Bit-identical (every output keeps its k-ordered MFMA chain; the squeeze still sums the concat
- * channels in ascending order).  f32 models; applied when max_batch * H * W >= ORE_FIRE_MIN_COLS
- * (environment, default 65536: one 64-pixel wave per SIMD), below which the fused launch has too
- * few waves (batch 1 keeps the separate kernels). */
+ * channels in ascending order).  f32 (fire_kernel) and f16 (fire_f16_kernel) models; f32: applied when
+ * max_batch * H * W >= 65536 (one 64-pixel wave per SIMD), below which the fused launch has too few
+ * waves (batch 1 keeps the separate kernels). */
 #define ORE_FUSE_FIRE 64
 /* bit 7 (in ORE_FUSE_ALL): Concat(e1, e3) -> 3x3 / stride-2 MaxPool with e1 / e3 Convs
  * (+ Relu) read only by the Concat (SqueezeNet's fire4 -> pool3, fire8 -> pool5): each conv's pooled
  * epilogue (the row-walking kernel, ore_conv_pool.hip) writes its channel slice of the pool output,
  * so neither the expand outputs nor the Concat reach HBM.  Bit-identical (the pool is per channel;
- * every pooled value is the max of the same nine values).  f32 models, conv planes of at least
- * ORE_CONCAT_POOL_MIN_HW (environment, default 1024) pixels: at batch 256 fire4 -> pool3 (54 x 54)
- * saves 40 us per step, fire8 -> pool5 (27 x 27) would cost 21 us (the walker's expand3x3 runs at
- * 88-92 % of the streaming kernel's rate). */
+ * every pooled value is the max of the same nine values).  f32 models, conv planes of at least 1024
+ * pixels: at batch 256 fire4 -> pool3 (54 x 54) saves 40 us per step, fire8 -> pool5 (27 x 27)
+ * would cost 21 us (the walker's expand3x3 runs at 88-92 % of the streaming kernel's rate). */
 #define ORE_FUSE_CONCAT_POOL 128
+/* bit 8: a fire module, the 3x3 / stride-2 MaxPool of its Concat and the next squeeze as ONE launch
+ * (f32 fire_pool_kernel on expand planes of >= 1024 pixels at max_batch * H * W >= 65536: fire4 +
+ * pool3 + fire5/squeeze; f16 fire_pool_f16_kernel: also fire8 + pool5 + fire9/squeeze). */
+#define ORE_FUSE_FIRE_POOL 256
+/* bit 9: the first conv + its pooled epilogue also runs the pooled map's only reader, a 1x1 conv
+ * (+ Relu) with <= 16 (f32) / 32 (f16) channels (conv1 + pool1 + fire2/squeeze). */
+#define ORE_FUSE_FIRST_SQUEEZE 512
+/* bit 10: a 3x3 / stride-2 MaxPool read only by a 1x1 conv (+ Relu, <= 64 channels) runs inside that
+ * conv (f32 pool_conv1x1_f32_kernel: pool5 + fire9/squeeze). */
+#define ORE_FUSE_POOL_SQUEEZE 1024
+/* bit 11 (tests, not in ORE_FUSE_ALL): apply every eligible fusion regardless of the size
+ * heuristics above (batch / plane thresholds, the 1.25 patch-work bound). */
+#define ORE_FUSE_EAGER 2048
 /* debug: give every value its own storage (no liveness reuse) so any value can be read back */
 #define ORE_KEEP_VALUES 8
 ore_status ore_model_set_fusion(ore_model* m, int32_t flags);
@@ -247,6 +271,13 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
 ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, float* d_output, int32_t reps);
 /* Block tile chosen for exec step i (-1 for non-conv steps). */
 int32_t ore_model_step_tile(ore_model* m, int32_t i);
+/* Set exec step i's tile (one of the ids ore_model_autotune chooses among for that step; e.g. to
+ * restore a saved autotune result).  ORE_ERR_INVALID for an id outside the step's kernel family.
+ * Survives ore_model_set_fusion like the autotuned choice. */
+ore_status ore_model_set_step_tile(ore_model* m, int32_t i, int32_t tile);
+/* MFMA FLOPs exec step i issued in the last run: its algorithmic FLOPs (ore_model_step_info), except
+ * Winograd steps, which issue 16 C M per 2x2 output tile against the direct 36 C M. */
+ore_status ore_model_step_mfma_flops(ore_model* m, int32_t i, double* flops);
 /* Branch concurrency (the reference runs the two expand branches of a fire
  * module on threads, multithreading.rs:20-62): with 2 streams, adjacent independent steps (no
  * data dependence, no overlapping storage) run on a side stream beside the main one, joined by

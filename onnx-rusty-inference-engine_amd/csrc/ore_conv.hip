@@ -36,29 +36,6 @@ constexpr int EPOOL_PR = EPOOL_TILE_PR, EPOOL_PC = EPOOL_TILE_PC, EPOOL_RC = 2 *
 #define ORE_A_DMA 1  // A (weight) tile by 16-B LDS-DMA too (0: registers + ds_write_b128)
 #endif
 
-#ifndef ORE_DMA_ASM
-#define ORE_DMA_ASM 0  // 1: B-tile LDS-DMA by inline asm (measured equal: 5.38 vs 5.39 ms per step)
-#endif
-
-// One 4-B-per-lane LDS-DMA (lane i -> lds_addr + 4 i) through a raw buffer descriptor (offsets past
-// num_records read 0).  Inline asm rather than __builtin_amdgcn_raw_ptr_buffer_load_lds: with the
-// builtin, hipcc guards the first LDS read of every K tile with an s_waitcnt vmcnt that also waits
-// for the NEXT tile's A loads and first DMA (it cannot tell which LDS buffer a DMA writes), i.e. an
-// L2 round trip per K tile before the MFMAs start.  The kernel drains the DMA itself (vmcnt(0)
-// before the barrier that publishes the tile).  M0 is restored.
-__device__ __forceinline__ void lds_dma4(int4d rsrc, unsigned lds_addr, int voffset) {
-  int m0save;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dword %2, %3, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(m0save)
-      : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voffset), "s"(rsrc)
-      : "memory");
-}
-
 #ifdef ORE_EXP_BFIXED  // timing experiment: B loads without the gather index math
 #define ORE_EXP_BFIXED_HOOK ok = bn_ok; off = (xoff > 0 ? xoff : 0) + ((k >> 4) & 1) * XPS;  /* channel 0/1, clamped: in bounds */
 #else
@@ -78,29 +55,23 @@ __device__ __forceinline__ void lds_dma4(int4d rsrc, unsigned lds_addr, int voff
 #ifndef ORE_VEC_EPI_ON
 #define ORE_VEC_EPI_ON 1
 #endif
-// the LDS-staged 16-B epilogue costs VGPRs (128x128: 135 vs 104-117 without it); the
-// warp-specialised variant keeps the scalar epilogue for its 2 blocks/CU
-#define ORE_WS_VEC_EPI (ORE_VEC_EPI_ON && !WS)
 #ifndef ORE_CONV_MINBLOCKS
 #define ORE_CONV_MINBLOCKS 2  // __launch_bounds__ minimum blocks per CU (VGPR budget)
 #endif
 
-enum { B1X1 = 0, BGATHER = 1, BPOOL = 2 };  // BPOOL: B = 3x3 window max of the pre-pool tensor
+enum { B1X1 = 0, BGATHER = 1 };
 
 // DMA: the B tile goes global -> LDS by buffer_load ... lds (no VGPR staging, no LDS store
 // pass); a tap outside the image gets an out-of-range offset, which the buffer bounds check
 // turns into a 0 -- the reference's zero padding -- with no select.
-// WS (warp-specialised): 512 threads; waves 0-3 only read LDS and issue MFMAs, waves 4-7 only
-// gather the next K tile into the other LDS buffer.  Both roles meet at the same barrier once
-// per K tile, so the MFMA waves' instruction stream carries no global loads or gather math.
-template <int BM, int BN, int WM, int WN, int BK, int BMODE, int DMA, int WS = 0, int EP = 0>
-__global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_kernel(ConvParams p) {
+template <int BM, int BN, int WM, int WN, int BK, int BMODE, int DMA, int EP = 0>
+__global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(ConvParams p) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 32, FN = TN / 32;
   // ADMA: the A tile also goes global -> LDS by 16-B LDS-DMA (lane-linear, so unpadded rows; the
   // fragment reads -- 32 consecutive floats per half-wave -- are conflict-free without padding)
   // (measured: 96-row tiles gain 1-3 %, the 128x128 tile loses 4 % on fire4/expand3x3 -> off there)
-  constexpr bool ADMA = DMA && !WS && ORE_A_DMA && BM != 128;
+  constexpr bool ADMA = DMA && ORE_A_DMA && BM != 128;
   constexpr int AS = ADMA ? BM : BM + 4;     // LDS row stride of the A tile (16-B aligned rows)
   constexpr int BROWS = 256 / BN;            // B rows loaded per pass
   constexpr int BLOADS = BK / BROWS;         // B elements per thread per tile
@@ -110,7 +81,7 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
 
   // one LDS array: the A/B double buffers of the main loop, reused by the epilogue's per-wave
   // [32][TN] output staging (all LDS in one __shared__ object, cdna_hip_programming.md §5)
-  constexpr int NBUF = WS ? 3 : 2;  // WS: the loaders keep one K tile in flight across the barrier
+  constexpr int NBUF = 2;
   constexpr int MAIN_FLOATS = NBUF * BK * AS + NBUF * BK * BN;
   constexpr int EPI_FLOATS = 4 * 32 * TN;
   __shared__ __attribute__((aligned(16))) float smem[MAIN_FLOATS > EPI_FLOATS ? MAIN_FLOATS : EPI_FLOATS];
@@ -118,8 +89,7 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
   float(*Bs)[BK][BN] = reinterpret_cast<float(*)[BK][BN]>(smem + NBUF * BK * AS);
   __shared__ float sbias[BM];
 
-  const int tid = WS ? (threadIdx.x & 255) : threadIdx.x;  // WS: both roles index 0..255
-  const bool loader = WS && threadIdx.x >= 256;              // wave-uniform role
+  const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm0 = (wave / WN) * TM;
@@ -150,7 +120,6 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
   // element offsets fit in 32 bits (checked on the host): uniform base + 32-bit lane offset
   int xoff;
   int ih0 = 0, iw0 = 0;
-  int pmask = 0;  // BPOOL: bit r*3+s set when window tap (r, s) is inside the pre-pool plane
   // EP (pooled epilogue): N tile nt = (image, pooled tile row, pooled tile column); its BN columns
   // are an ep_rc x ep_cc patch of conv outputs (row-major), the conv pixels that the tile's
   // ep_pr x ep_pc pooled outputs read
@@ -181,16 +150,6 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
     xoff = img * (int)p.x_nstride;
     if (BMODE == B1X1) {
       xoff += pix;
-    } else if (BMODE == BPOOL) {
-      const int oh = pix / p.Wo, ow = pix - oh * p.Wo;
-      ih0 = oh * p.pool_sh - p.pool_pt;
-      iw0 = ow * p.pool_sw - p.pool_pl;
-      xoff += ih0 * p.pool_W + iw0;
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int s = 0; s < 3; ++s)
-          if ((unsigned)(ih0 + r) < (unsigned)p.pool_H && (unsigned)(iw0 + s) < (unsigned)p.pool_W) pmask |= 1 << (r * 3 + s);
     } else {
       const int oh = pix / p.Wo, ow = pix - oh * p.Wo;
       ih0 = oh * p.sh - p.pt;
@@ -206,8 +165,6 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
   // writes 64 consecutive columns of one B row
   const __amdgpu_buffer_rsrc_t xrsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
-  const unsigned long long xb_ = reinterpret_cast<unsigned long long>(p.x);
-  const int4d xdesc = {(int)(unsigned)xb_, (int)((xb_ >> 32) & 0xffff), (int)p.x_bytes, 0x00020000};
   const int wcol0 = bcol & ~63;
   // the gather table through the constant address space: k is wave-uniform, so the entries
   // come in by scalar loads (s_load) into SGPRs instead of LDS / vector round trips
@@ -238,7 +195,7 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
       const int k = k0_ + krow + j * BROWS;                                                          \
       bool ok;                                                                                       \
       int off;                                                                                       \
-      if (BMODE == B1X1 || BMODE == BPOOL) {                                                         \
+      if (BMODE == B1X1) {                                                                           \
         ok = bn_ok & (k < K);                                                                        \
         off = xoff + k * XPS;                                                                        \
       } else {                                                                                       \
@@ -249,24 +206,10 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
         off = xoff + ex_;                                                                            \
       }                                                                                              \
       ORE_EXP_BFIXED_HOOK                                                                            \
-      if (BMODE == BPOOL) {                                                                          \
-        /* the reference's MaxPool: start at -FLT_MAX, taps outside the plane read 0 */              \
-        float m_ = -FLT_MAX;                                                                         \
-        _Pragma("unroll") for (int t_ = 0; t_ < 9; ++t_) {                                           \
-          const bool in_ = ok & (((pmask >> t_) & 1) != 0);                                          \
-          const float v_ = x[(unsigned)(in_ ? off + (t_ / 3) * p.pool_W + (t_ % 3) : 0)];             \
-          m_ = fmaxf(m_, in_ ? v_ : 0.0f);                                                           \
-        }                                                                                            \
-        RB[j] = m_;                                                                                  \
-        ROK[j] = ok;                                                                                 \
-      } else if (DMA) {                                                                              \
-        if (ORE_DMA_ASM)                                                                             \
-          lds_dma4(xdesc, (unsigned)(size_t)(__attribute__((address_space(3))) float*)&Bs[(DBUF)][krow + j * BROWS][wcol0], \
-                   ok ? off * 4 : (int)0x80000000);                                                  \
-        else                                                                                         \
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                  \
-              xrsrc, (__attribute__((address_space(3))) void*)&Bs[(DBUF)][krow + j * BROWS][wcol0], 4, \
-              ok ? off * 4 : (int)0x80000000, 0, 0, 0);                                              \
+      if (DMA) {                                                                                     \
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                    \
+            xrsrc, (__attribute__((address_space(3))) void*)&Bs[(DBUF)][krow + j * BROWS][wcol0], 4,   \
+            ok ? off * 4 : (int)0x80000000, 0, 0, 0);                                                \
       } else {                                                                                       \
         RB[j] = x[(unsigned)(ok ? off : 0)];                                                         \
         ROK[j] = ok; /* the zero select happens at the LDS store, after the MFMAs */                 \
@@ -295,7 +238,7 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
   const int ntk = (K + BK - 1) / BK;
-  if (!WS || loader) {
+  {
     floatx4 ra[AVEC];
     float rb[BLOADS];
     bool rok[BLOADS];
@@ -304,13 +247,6 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
     if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the B tile has landed in LDS
   }
   __syncthreads();
-  // WS loaders: K tile 1 in flight (A in registers, B by LDS-DMA into buffer 1)
-  floatx4 wra[WS ? AVEC : 1];
-  {
-    float rb[BLOADS];
-    bool rok[BLOADS];
-    if (WS && loader && ntk > 1) ORE_LOAD_TILE(wra, rb, rok, BK, 1);
-  }
   const int lrow = lane >> 5, lcol = lane & 31;
 // fragments for k-step kk+2 are read from LDS before the MFMAs of k-step kk are issued
 // KEND: k-steps of this tile that carry data (BK except on the last tile, where the zero rows
@@ -338,34 +274,6 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
       ORE_PRIO(0);                                                                                   \
     }                                                                                                \
   }
-  if (WS) {
-    // three LDS buffers: while the MFMA waves consume tile t (buffer t % 3) the loaders retire
-    // tile t + 1 (its LDS-DMA + the A store) and issue tile t + 2, which stays in flight across
-    // the barrier (raw s_barrier, counted waits: cdna_hip_programming.md "Pipelining across
-    // barriers").  Buffer (t + 2) % 3 was last read in tile t - 1, before the previous barrier.
-    static_assert(!WS || DMA, "the warp-specialised loop streams B by LDS-DMA");
-    const int kend = __builtin_amdgcn_readfirstlane((K - (ntk - 1) * BK + 1) & ~1);
-    for (int t = 0; t < ntk; ++t) {
-      const int buf = t % 3;
-      if (loader) {
-        if (t + 1 < ntk) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t + 1: A registers + B DMA landed
-          float rb[BLOADS];
-          bool rok[BLOADS];
-          ORE_STORE_TILE(wra, rb, rok, (t + 1) % 3);
-          if (t + 2 < ntk) ORE_LOAD_TILE(wra, rb, rok, (t + 2) * BK, (t + 2) % 3);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the A stores are in LDS
-      } else {
-        ORE_COMPUTE_TILE(buf, t + 1 < ntk ? BK : kend);
-        // every read of buffer t % 3 has returned before the barrier: the loaders refill it in
-        // tile t + 1 (the asm's memory clobber also keeps the reads from sinking past it)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
-    }
-    if (loader) return;  // no block barrier follows: the epilogue is per wave
-  } else {
   // steady state: prefetch tile t+1 into registers, MFMAs on tile t, publish t+1 to LDS
   for (int t = 0; t < ntk - 1; ++t) {
     const int buf = t & 1;
@@ -389,7 +297,6 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
     const int kend = __builtin_amdgcn_readfirstlane((K - (ntk - 1) * BK + 1) & ~1);
     ORE_COMPUTE_TILE((ntk - 1) & 1, kend);
   }
-  }  // !WS
 #undef ORE_COMPUTE_TILE
 #undef ORE_LOAD_TILE
 #undef ORE_STORE_TILE
@@ -455,12 +362,12 @@ __global__ __launch_bounds__(256 * (1 + WS), ORE_CONV_MINBLOCKS) void conv_gemm_
     }
     return;
   }
-  if (ORE_WS_VEC_EPI && p.vec_out) {
+  if (ORE_VEC_EPI_ON && p.vec_out) {
     // 16-B stores: each wave stages 32 output rows x TN pixels in its own LDS slice (column
     // halves swapped every 4 rows so the two lane halves' writes hit different banks), then
     // writes whole pixel runs with float4 stores.  Host guarantees y_ps % 4 == 0, 16-B aligned
     // image/plane bases and Ntot % 4 == 0, so no float4 straddles an image.
-    if (!WS) __syncthreads();  // every wave is done with the A/B tiles (WS: the loop's last barrier)
+    __syncthreads();  // every wave is done with the A/B tiles
     float* stg = smem + wave * (32 * TN);
     constexpr int V4 = TN / 4;            // float4 per staged row
     constexpr int RPI = 64 / V4;          // rows per wave-instruction
@@ -572,316 +479,19 @@ void launch_pack_weights(const float* w, bool kmajor_src, int M, int K, int Mp, 
                      kmajor_src ? 1 : 0);
 }
 
-// ------------------------------------------------------------------ window-staged implicit GEMM
-// For k > 1 / strided convs on planes large enough to tile per image (conv1, the 54^2 and 27^2
-// 3x3 layers).  A block owns BM output channels x BN consecutive output pixels of ONE image.
-// K is walked in stages of `bch` input channels (ks = bch*kh*kw rounded up to even):
-//   * A stage: rows [stage*ks, stage*ks + ks) of the stage-major packed weights -> LDS.
-//   * B stage: the input rows those BN pixels touch (wr rows x ww columns per channel, zero
-//     outside the image) are copied ONCE into an LDS window by row-coalesced loads.
-// B fragments are then read straight from the window: lane address = per-column base
-// ((oh - oh_first)*sh*ww + ow*sw) + koff[k] (c*wr*ww + r*ww + s, an LDS table), so there is no
-// per-element bounds arithmetic and no im2col tile.  Stage s+1 is prefetched into registers
-// while stage s feeds the MFMAs.
-constexpr int WIN_MAXA = 6;   // float4 A loads per thread per stage
-constexpr int WIN_MAXW = 12;  // window loads per lane per stage
-constexpr int WIN_MAXROWS = 64;
-
-template <int BM, int BN, int WM, int WN, int WQ>  // WQ = ceil(ww / 64): loads per lane per window row
-__global__ __launch_bounds__(256, 2) void conv_win_kernel(ConvParams p) {
-  constexpr int TM = BM / WM, TN = BN / WN;
-  constexpr int FM = TM / 32, FN = TN / 32;
-  constexpr int RSLOTS = WIN_MAXW / WQ;  // window rows per wave per stage
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int KS = p.ks, BCH = p.bch, WR = p.wr, WWD = p.ww;
-  const int AFL = KS * BM;          // floats of one A stage
-  const int WFL = BCH * WR * WWD;   // floats of one window stage
-  float* As = smem;                 // [2][KS][BM]
-  float* Ws = smem + 2 * AFL;       // [2][BCH][WR][WW]
-  int* koff = reinterpret_cast<int*>(Ws + 2 * WFL);   // [KS + 8] window offset of each k (0 past KS)
-  int2* rowtab = reinterpret_cast<int2*>(koff + KS + 8);  // [WIN_MAXROWS] {input offset, channel}
-  float* sbias = reinterpret_cast<float*>(rowtab + WIN_MAXROWS);
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm0 = (wave / WN) * TM, wn0 = (wave % WN) * TN;
-  const int lrow = lane >> 5, lcol = lane & 31;
-
-  const int nwg = p.mtiles * p.ntiles;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, rr8 = nwg & 7;
-  const int wgid = (xcd < rr8 ? xcd * (q + 1) : rr8 * (q + 1) + (xcd - rr8) * q) + (bid >> 3);
-  const int mt = wgid % p.mtiles, nt = wgid / p.mtiles;
-  const int m0 = mt * BM;
-  const int img = nt / p.tiles_per_img;
-  const int p0 = (nt - img * p.tiles_per_img) * BN;
-  const int oh_first = p0 / p.Wo;
-  const int ihb = oh_first * p.sh - p.pt;  // input row of window row 0
-
-  const int KK = p.kh * p.kw;
-  for (int i = tid; i < KS + 8; i += 256) {
-    int off = 0;
-    if (i < BCH * KK) {
-      const int c = i / KK, rs = i - c * KK, r = rs / p.kw, sx = rs - r * p.kw;
-      off = (c * WR + r) * WWD + sx;
-    }
-    koff[i] = off;
-  }
-  const int wrows = BCH * WR;
-  for (int i = tid; i < WIN_MAXROWS; i += 256) {
-    // window row i = (channel c, row r): input offset relative to channel c0 of the stage;
-    // offset -1 marks rows outside the image (zero filled); c decides stage-tail rows
-    int off = -1, c = 1 << 20;
-    if (i < wrows) {
-      c = i / WR;
-      const int ih = ihb + (i - c * WR);
-      if ((unsigned)ih < (unsigned)p.H) off = c * p.x_ps + ih * p.W;
-    }
-    rowtab[i] = make_int2(off, c);
-  }
-  for (int i = tid; i < BM; i += 256) sbias[i] = (p.bias && m0 + i < p.M) ? p.bias[m0 + i] : 0.0f;
-
-  int bbase[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    int pc = p0 + wn0 + j * 32 + lcol;
-    if (pc > p.P - 1) pc = p.P - 1;  // pad columns read any valid window address
-    const int oh = pc / p.Wo, ow = pc - oh * p.Wo;
-    bbase[j] = (oh - oh_first) * p.sh * WWD + ow * p.sw;
-  }
-
-  const float* __restrict__ x = p.x;
-  const float* __restrict__ wp = p.wp;
-  const int ximg = img * (int)p.x_nstride;
-  __syncthreads();  // koff / rowtab / sbias
-  // this wave's window rows (row = wave + 4 r) for the whole block: wave-uniform, kept in SGPRs
-  int wroff[RSLOTS], wrch[RSLOTS];
-#pragma unroll
-  for (int r = 0; r < RSLOTS; ++r) {
-    const int row = wave + 4 * r;
-    const int2 rt = rowtab[row < WIN_MAXROWS ? row : 0];
-    wroff[r] = __builtin_amdgcn_readfirstlane(rt.x);
-    wrch[r] = __builtin_amdgcn_readfirstlane(rt.y);
-  }
-
-#define ORE_WIN_LOAD(RA, RW, ROK, ST)                                                                \
-  {                                                                                                  \
-    const int st_ = (ST);                                                                            \
-    const float* ws_ = wp + (unsigned)(st_ * KS * p.Mp + m0);                                        \
-    _Pragma("unroll") for (int j = 0; j < WIN_MAXA; ++j) {                                           \
-      const int e = (tid + j * 256 < AFL / 4) ? tid + j * 256 : 0; /* tail lanes reload element 0 */ \
-      const int kk = e / (BM / 4), mm = (e - kk * (BM / 4)) * 4;                                     \
-      RA[j] = *reinterpret_cast<const floatx4*>(ws_ + (unsigned)(kk * p.Mp + mm));                   \
-    }                                                                                                \
-    const int cbase_ = ximg + st_ * BCH * p.x_ps;                                                    \
-    const int cleft_ = p.C - st_ * BCH;  /* channels left in this stage */                           \
-    _Pragma("unroll") for (int r = 0; r < RSLOTS; ++r) {                                             \
-      const int row = wave + 4 * r;                                                                  \
-      if (row < wrows) { /* wave-uniform */                                                          \
-        const int roff = wroff[r];                                                                   \
-        const bool rok_ = (roff >= 0) & (wrch[r] < cleft_);                                          \
-        _Pragma("unroll") for (int qq = 0; qq < WQ; ++qq) {                                          \
-          const int col = lane + 64 * qq, iw = col - p.pl;                                           \
-          const bool ok = rok_ & (col < WWD) & ((unsigned)iw < (unsigned)p.W);                       \
-          RW[r * WQ + qq] = x[(unsigned)(ok ? cbase_ + roff + iw : 0)];                              \
-          ROK[r * WQ + qq] = ok;                                                                     \
-        }                                                                                            \
-      }                                                                                              \
-    }                                                                                                \
-  }
-#define ORE_WIN_STORE(RA, RW, ROK, BUF)                                                              \
-  {                                                                                                  \
-    float* a_ = As + (BUF) * AFL;                                                                    \
-    _Pragma("unroll") for (int j = 0; j < WIN_MAXA; ++j) {                                           \
-      const int e = tid + j * 256;                                                                   \
-      if (e < AFL / 4) *reinterpret_cast<floatx4*>(a_ + e * 4) = RA[j];                              \
-    }                                                                                                \
-    float* w_ = Ws + (BUF) * WFL;                                                                    \
-    _Pragma("unroll") for (int r = 0; r < RSLOTS; ++r) {                                             \
-      const int row = wave + 4 * r;                                                                  \
-      _Pragma("unroll") for (int qq = 0; qq < WQ; ++qq) {                                            \
-        const int col = lane + 64 * qq;                                                              \
-        if (row < wrows && col < WWD) w_[row * WWD + col] = ROK[r * WQ + qq] ? RW[r * WQ + qq] : 0.0f; \
-      }                                                                                              \
-    }                                                                                                \
-  }
-
-  floatx16 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-
-  {
-    floatx4 ra[WIN_MAXA];
-    float rw[WIN_MAXW];
-    bool rok[WIN_MAXW];
-    ORE_WIN_LOAD(ra, rw, rok, 0);
-    ORE_WIN_STORE(ra, rw, rok, 0);
-  }
-  __syncthreads();
-  const int nst = p.nst;
-  // Inner loop: 4 k values (two MFMA k-steps) per trip, software-pipelined: the fragments of
-  // trip t+1 are read from LDS while trip t's MFMAs run, and the koff entries two trips ahead
-  // (KS % 4 == 0; koff is padded with 8 zero entries so the look-ahead never leaves the table).
-#ifdef ORE_EXP_REGONLY  /* timing experiment: fragments without LDS reads */
-#define ORE_WIN_FRAGS(AF0, AF1, BF0, BF1, KQ, KK)                                                    \
-  {                                                                                                  \
-    _Pragma("unroll") for (int i = 0; i < FM; ++i) { AF0[i] = (float)(KK) + i; AF1[i] = (float)(KK) - i; } \
-    _Pragma("unroll") for (int j = 0; j < FN; ++j) { BF0[j] = (float)(KQ).x + j; BF1[j] = (float)(KQ).y - j; } \
-  }
-#else
-#define ORE_WIN_FRAGS(AF0, AF1, BF0, BF1, KQ, KK)                                                    \
-  {                                                                                                  \
-    const int lo0_ = lrow ? (KQ).y : (KQ).x, lo1_ = lrow ? (KQ).w : (KQ).z;                           \
-    _Pragma("unroll") for (int i = 0; i < FM; ++i) {                                                 \
-      AF0[i] = a_[((KK) + lrow) * BM + wm0 + i * 32 + lcol];                                         \
-      AF1[i] = a_[((KK) + 2 + lrow) * BM + wm0 + i * 32 + lcol];                                     \
-    }                                                                                                \
-    _Pragma("unroll") for (int j = 0; j < FN; ++j) {                                                 \
-      BF0[j] = w_[bbase[j] + lo0_];                                                                  \
-      BF1[j] = w_[bbase[j] + lo1_];                                                                  \
-    }                                                                                                \
-  }
-#endif
-#define ORE_WIN_MFMAS(AF0, AF1, BF0, BF1)                                                            \
-  {                                                                                                  \
-    _Pragma("unroll") for (int i = 0; i < FM; ++i)                                                   \
-    _Pragma("unroll") for (int j = 0; j < FN; ++j)                                                   \
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(AF0[i], BF0[j], acc[i][j], 0, 0, 0);          \
-    _Pragma("unroll") for (int i = 0; i < FM; ++i)                                                   \
-    _Pragma("unroll") for (int j = 0; j < FN; ++j)                                                   \
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(AF1[i], BF1[j], acc[i][j], 0, 0, 0);          \
-  }
-  // two trips per iteration with ping-pong fragment registers (no copies); an odd trip count
-  // leaves one trip for the tail.  Fragment reads past the last trip are clamped dummies.
-#define ORE_WIN_COMPUTE(BUF)                                                                         \
-  {                                                                                                  \
-    const float* a_ = As + (BUF) * AFL;                                                              \
-    const float* w_ = Ws + (BUF) * WFL;                                                              \
-    const int4* kq_ = reinterpret_cast<const int4*>(koff);                                           \
-    const int trips_ = KS >> 2, last_ = KS - 4;                                                      \
-    float ca0[FM], ca1[FM], cb0[FN], cb1[FN], na0[FM], na1[FM], nb0[FN], nb1[FN];                    \
-    int4 kq1 = kq_[1];                                                                               \
-    {                                                                                                \
-      const int4 kq0 = kq_[0];                                                                       \
-      ORE_WIN_FRAGS(ca0, ca1, cb0, cb1, kq0, 0);                                                     \
-    }                                                                                                \
-    int t_ = 0;                                                                                      \
-    for (; t_ + 2 <= trips_; t_ += 2) {                                                              \
-      const int4 kq2 = kq_[t_ + 2];                                                                  \
-      ORE_WIN_FRAGS(na0, na1, nb0, nb1, kq1, 4 * t_ + 4);                                            \
-      __builtin_amdgcn_sched_barrier(0);                                                             \
-      ORE_WIN_MFMAS(ca0, ca1, cb0, cb1);                                                             \
-      __builtin_amdgcn_sched_barrier(0);                                                             \
-      kq1 = kq_[t_ + 3];                                                                             \
-      ORE_WIN_FRAGS(ca0, ca1, cb0, cb1, kq2, (4 * t_ + 8 <= last_ ? 4 * t_ + 8 : last_));            \
-      __builtin_amdgcn_sched_barrier(0);                                                             \
-      ORE_WIN_MFMAS(na0, na1, nb0, nb1);                                                             \
-      __builtin_amdgcn_sched_barrier(0);                                                             \
-    }                                                                                                \
-    if (t_ < trips_) ORE_WIN_MFMAS(ca0, ca1, cb0, cb1);                                              \
-  }
-  for (int st = 0; st < nst - 1; ++st) {
-    const int buf = st & 1;
-#ifndef ORE_EXP_NOLOAD  // timing experiments only (tools/build_exp.sh)
-    floatx4 ra[WIN_MAXA];
-    float rw[WIN_MAXW];
-    bool rok[WIN_MAXW];
-    ORE_WIN_LOAD(ra, rw, rok, st + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    ORE_WIN_COMPUTE(buf);
-    ORE_WIN_STORE(ra, rw, rok, buf ^ 1);
-#else
-    ORE_WIN_COMPUTE(0);
-#endif
-#ifndef ORE_EXP_NOSYNC
-    __syncthreads();
-#endif
-  }
-  ORE_WIN_COMPUTE((nst - 1) & 1);
-#undef ORE_WIN_LOAD
-#undef ORE_WIN_STORE
-#undef ORE_WIN_COMPUTE
-#undef ORE_WIN_FRAGS
-#undef ORE_WIN_MFMAS
-
-  // epilogue: columns are pixels p0 + n of image img (plane stride y_ps; pixels >= P skipped)
-  float* __restrict__ y = p.y;
-  const unsigned yimg = (unsigned)(img * (int)p.y_nstride);
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int pix = p0 + wn0 + j * 32 + lcol;
-    if (pix >= p.P) continue;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int ml = wm0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lrow;
-        if (m0 + ml < p.M) {
-          float v = acc[i][j][e] + sbias[ml];
-          if (p.relu) v = fmaxf(v, 0.0f);
-#ifdef ORE_EXP_NOEPI
-          if (v == 1234.5678f)
-#endif
-          y[yimg + (unsigned)((m0 + ml) * p.y_ps + pix)] = v;
-        }
-      }
-    }
-  }
-}
-
-// window-staged packing: row stage*ks + (c - c0)*kh*kw + r*kw + s, zero for padded rows
-__global__ __launch_bounds__(256) void pack_win_kernel(const float* __restrict__ w, float* __restrict__ wp, int M,
-                                                       int C, int KK, int Mp, int bch, int ks, int nst) {
-  const long long total = (long long)nst * ks * Mp;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int row = (int)(i / Mp), m = (int)(i - (long long)row * Mp);
-    const int st = row / ks, kk = row - st * ks;
-    float v = 0.0f;
-    if (kk < bch * KK && m < M) {
-      const int c = st * bch + kk / KK, rs = kk - (kk / KK) * KK;
-      if (c < C) v = w[((long long)m * C + c) * KK + rs];
-    }
-    wp[i] = v;
-  }
-}
-
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
-template <int BM, int BN, int WM, int WN, int WS = 0>
+// the B tile by LDS-DMA (buffer_load ... lds): the host launches image chunks whose x extent fits the
+// buffer resource (run_conv), so x_bytes > 0 here
+template <int BM, int BN, int WM, int WN>
 static void launch_conv_cfg(const ConvParams& p0, hipStream_t s) {
   constexpr int BK = 16;
   ConvParams p = p0;
   p.mtiles = (p.M + BM - 1) / BM;
   p.ntiles = (int)((p.Ntot + BN - 1) / BN);
   dim3 grid(p.mtiles * p.ntiles), block(256);
-  const bool dma = p.x_bytes > 0 && env_int("ORE_CONV_DMA", 1) != 0;  // tuning knob
-  if (WS && dma && !p.pool) {  // the warp-specialised loop streams B by LDS-DMA
-    const dim3 wblock(512);
-    if (p.is1x1)
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, B1X1, 1, 1>), grid, wblock, 0, s, p);
-    else
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BGATHER, 1, 1>), grid, wblock, 0, s, p);
-    return;
-  }
-  if (p.pool) {
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BPOOL, 0>), grid, block, 0, s, p);
-  } else if (p.is1x1) {
-    if (dma)
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, B1X1, 1>), grid, block, 0, s, p);
-    else
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, B1X1, 0>), grid, block, 0, s, p);
-  } else {
-    if (dma)
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BGATHER, 1>), grid, block, 0, s, p);
-    else
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BGATHER, 0>), grid, block, 0, s, p);
-  }
+  if (p.is1x1)
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, B1X1, 1>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, BK, BGATHER, 1>), grid, block, 0, s, p);
 }
 
 // Conv + MaxPool in one launch (ORE_FUSE_CONV_POOL): 1x4-wave tiles of BM x 256 (the N tile is a
@@ -893,23 +503,14 @@ static void launch_conv_epool_cfg(const ConvParams& p0, hipStream_t s) {
   p.mtiles = (p.M + BM - 1) / BM;
   p.ntiles = p.N * p.ep_tr * p.ep_tc;
   dim3 grid(p.mtiles * p.ntiles), block(256);
-  const bool dma = p.x_bytes > 0 && env_int("ORE_CONV_DMA", 1) != 0;
-  if (p.is1x1) {
-    if (dma)
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 1, 4, BK, B1X1, 1, 0, 1>), grid, block, 0, s, p);
-    else
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 1, 4, BK, B1X1, 0, 0, 1>), grid, block, 0, s, p);
-  } else {
-    if (dma)
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 1, 4, BK, BGATHER, 1, 0, 1>), grid, block, 0, s, p);
-    else
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 1, 4, BK, BGATHER, 0, 0, 1>), grid, block, 0, s, p);
-  }
+  if (p.is1x1)
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 1, 4, BK, B1X1, 1, 1>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 1, 4, BK, BGATHER, 1, 1>), grid, block, 0, s, p);
 }
 
 void launch_conv_epool(const ConvParams& p, hipStream_t s) {
   int v = p.ep_variant;
-  if (const char* e = getenv("ORE_CONV_POOL_STREAM")) v = atoi(e) + 1;  // 0..3 -> patch / walk48 / walk96 / walk64, 6 -> window
   if (p.sq1) {  // the fused squeeze exists in the window kernel only
     if (p.wc1 && conv_win_pool_f32_eligible(p, p.sq1)) {
       launch_conv_win_pool_f32(p, p.wc1, p.sq1, s);
@@ -962,18 +563,16 @@ int conv_tile_config(int M) {
 }
 
 static const int CFG_BM[4] = {128, 96, 64, 32};
-static const int CFG_BN[4] = {128, 128, 128, 256};
 
 
 ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
-                   bool is1x1, bool f16, int xmode, bool x3, bool wino) {
+                   bool is1x1, bool f16, int xmode, bool x3, bool wino, int forced) {
   (void)pt;
   ConvPlan pln{};
   if (wino && !x3 && !f16 && conv_wino_geometry(C, kh, kw, sh, sw, pt, pl, H, W, Ho, Wo)) {
     pln.wino = 1;
     pln.cfg = WINO_TILE_BASE + 0;
-    const int forced = env_int("ORE_WINO_TILE", -1);  // tuning knob
-    if (forced >= 0 && forced < WINO_TILES_N) pln.cfg = WINO_TILE_BASE + forced;
+    if (forced >= WINO_TILE_BASE && forced < WINO_TILE_BASE + WINO_TILES_N) pln.cfg = forced;
     pln.Mp = wino_packed_mp(M);
     pln.krows = 16 * C;  // U is 16 positions x C rows of Mp floats
     return pln;
@@ -984,8 +583,9 @@ ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, i
     pln.Mp = std::max((M + 127) / 128 * 128, (M + 95) / 96 * 96);
     pln.krows = conv_packed_kp(C * kh * kw);
     // stride-1 geometry whose window fits: the window-staged kernel (each input element split once
-    // per block instead of once per tap); ORE_X3_WINDOW=0 keeps the gather kernel (experiments)
-    if (x3w_geometry(C, kh, kw, sh, sw) && env_int("ORE_X3_WINDOW", 1) != 0) {
+    // per block instead of once per tap), unless a gather tile (X3_TILE_BASE + 0..3) is forced
+    const bool gather_forced = forced >= X3_TILE_BASE && forced < X3_TILE_BASE + 4;
+    if (x3w_geometry(C, kh, kw, sh, sw) && !gather_forced) {
       const int t = (Ho * Wo < 256 ? 6 : 4) + (M <= 64 ? 1 : 0);
       if (x3w_plan_lds(Ho, Wo, kh, kw, C, t) <= 80 * 1024) {
         pln.x3 = 2;
@@ -996,8 +596,8 @@ ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, i
         pln.krows = pln.nst * pln.ks * 32;
       }
     }
-    const int forced = env_int("ORE_X3_TILE", -1);  // tuning knob (within the plan's kernel family)
-    if (forced >= 0 && forced < 4) pln.cfg = X3_TILE_BASE + forced + (pln.x3 == 2 ? 4 : 0);
+    const int fam = X3_TILE_BASE + (pln.x3 == 2 ? 4 : 0);  // forced: within the plan's kernel family
+    if (forced >= fam && forced < fam + 4) pln.cfg = forced;
     return pln;
   }
   pln.f16 = f16 ? 1 : 0;
@@ -1007,8 +607,7 @@ ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, i
   // short-K 1x1 layers (SqueezeNet's expand1x1, K <= 64) are epilogue/write bound: the 1x4-wave
   // 96-row tile measured fastest for them even with padded rows (tools/bench_ops.py)
   if (K <= 64 && M >= 64 && is1x1) pln.cfg = 1;
-  const int forced = env_int("ORE_CONV_CFG", -1);  // tuning knob
-  if (forced >= 0 && forced < (f16 ? CONV_TILES_F16 : CONV_TILES_F32)) pln.cfg = forced;
+  if (forced >= 0 && forced < (f16 ? CONV_TILES_F16 : CONV_TILES_F32) && !conv_tile_retired(forced)) pln.cfg = forced;
   // packed rows cover every block tile's rows (the 96-row tile can pass roundup(M, 128)), so
   // the tile can be changed after packing (ore_model_autotune)
   pln.Mp = conv_packed_mp(M);
@@ -1017,51 +616,6 @@ ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, i
     if (rows > pln.Mp) pln.Mp = rows;
   }
   pln.krows = conv_packed_kp(f16 ? f16_conv_k(xmode, C, kh, kw) : K);
-  pln.window = 0;
-  if (f16) return pln;
-  const int P = Ho * Wo;
-  // The window-staged kernel is opt-in (ORE_CONV_WINDOW=1): on the SqueezeNet layers it measured
-  // 5-45 % slower than the gather kernel (its 49-59 KB LDS stages allow 2-3 blocks per CU against
-  // the gather kernel's 4; profiles/r01f_window_vs_gather.txt).
-  if (is1x1 || env_int("ORE_CONV_WINDOW", 0) == 0 || P < 512) return pln;
-  if (pln.cfg >= 4) return pln;  // the direct kernel has no window variant
-  const int BM = CFG_BM[pln.cfg], BN = CFG_BN[pln.cfg];
-  const int tiles = (P + BN - 1) / BN;
-  if ((long long)tiles * BN > (long long)P * 11 / 10) return pln;  // > 10% pad columns
-  int span = 1;
-  for (int t = 0; t < tiles; ++t) {
-    const int p0 = t * BN, p1 = (p0 + BN - 1 < P - 1) ? p0 + BN - 1 : P - 1;
-    const int sp = p1 / Wo - p0 / Wo + 1;
-    if (sp > span) span = sp;
-  }
-  const int wr = (span - 1) * sh + kh;
-  const int ww = (Wo - 1) * sw + kw;
-  const int wq = (ww + 63) / 64;
-  if (wq > 4) return pln;
-  const int KK = kh * kw;
-  const size_t lds_max = (size_t)env_int("ORE_WIN_LDS_KB", 64) * 1024;  // tuning knob
-  int best = 0;
-  for (int bch = C; bch >= 1; --bch) {
-    const int ks = (bch * KK + 3) & ~3;
-    const size_t lds = ((size_t)2 * ks * BM + (size_t)2 * bch * wr * ww) * 4 + (size_t)(ks + 8) * 4 +
-                       (size_t)WIN_MAXROWS * 8 + (size_t)BM * 4;
-    const int rows = bch * wr;
-    if (lds > lds_max || rows > WIN_MAXROWS || ((rows + 3) / 4) * wq > WIN_MAXW || ks * BM / 4 > WIN_MAXA * 256)
-      continue;
-    if (!best) best = bch;
-    if (C % bch == 0 && 2 * bch >= best) { best = bch; break; }
-  }
-  if (!best) return pln;
-  pln.window = 1;
-  pln.bch = best;
-  pln.ks = (best * KK + 3) & ~3;
-  pln.nst = (C + best - 1) / best;
-  pln.wr = wr;
-  pln.ww = ww;
-  pln.wq = wq;
-  pln.krows = pln.nst * pln.ks;
-  pln.lds = ((size_t)2 * pln.ks * BM + (size_t)2 * best * wr * ww) * 4 + (size_t)(pln.ks + 8) * 4 +
-            (size_t)WIN_MAXROWS * 8 + (size_t)BM * 4;
   return pln;
 }
 
@@ -1088,30 +642,7 @@ void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, 
     launch_pack_weights_f16(w, pln.xmode, M, C, kh, kw, pln.Mp, wp, s);
     return;
   }
-  if (!pln.window) {
-    launch_pack_weights(w, kmajor_src, M, C * kh * kw, pln.Mp, wp, s);
-    return;
-  }
-  const long long total = (long long)pln.krows * pln.Mp;
-  long long blocks = (total + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(pack_win_kernel, dim3((unsigned)blocks), dim3(256), 0, s, w, wp, M, C, kh * kw, pln.Mp, pln.bch,
-                     pln.ks, pln.nst);
-}
-
-template <int BM, int BN, int WM, int WN>
-static void launch_win_cfg(const ConvParams& p0, const ConvPlan& pln, hipStream_t s) {
-  ConvParams p = p0;
-  p.bch = pln.bch; p.ks = pln.ks; p.nst = pln.nst; p.wr = pln.wr; p.ww = pln.ww;
-  p.tiles_per_img = (p.P + BN - 1) / BN;
-  p.mtiles = (p.M + BM - 1) / BM;
-  p.ntiles = p.N * p.tiles_per_img;
-  dim3 grid(p.mtiles * p.ntiles), block(256);
-  switch (pln.wq) {
-    case 1: hipLaunchKernelGGL((conv_win_kernel<BM, BN, WM, WN, 1>), grid, block, pln.lds, s, p); break;
-    case 2: hipLaunchKernelGGL((conv_win_kernel<BM, BN, WM, WN, 2>), grid, block, pln.lds, s, p); break;
-    default: hipLaunchKernelGGL((conv_win_kernel<BM, BN, WM, WN, 4>), grid, block, pln.lds, s, p); break;
-  }
+  launch_pack_weights(w, kmajor_src, M, C * kh * kw, pln.Mp, wp, s);
 }
 
 thread_local int last_conv_tile = -1;
@@ -1119,12 +650,7 @@ thread_local int last_conv_tile = -1;
 void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
   last_conv_tile = pln.cfg;
   if (pln.wino) {  // the caller (run_conv) keeps x_bytes within the buffer range
-    int t = pln.cfg - WINO_TILE_BASE;
-    if (p.e1_y) {  // a fused 1x1 conv: tile 2 only (run_conv checked it)
-      t = 2;
-    } else if (!conv_wino_eligible(p, t)) {
-      t = 2;
-    }
+    int t = pln.cfg - WINO_TILE_BASE;  // the caller (run_conv) checked conv_wino_eligible
     last_conv_tile = WINO_TILE_BASE + t;
     launch_conv_wino(p, t, s);
     return;
@@ -1156,34 +682,6 @@ void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
     ConvPlan q = pln;  // not a stream geometry: the LDS-staged kernel
     q.cfg = 0;
     launch_conv(p, q, s);
-    return;
-  }
-  if (pln.cfg >= 8) {  // warp-specialised variants of tiles 0-3
-    switch (pln.cfg) {
-      case 8: launch_conv_cfg<128, 128, 2, 2, 1>(p, s); break;
-      case 9: launch_conv_cfg<96, 128, 1, 4, 1>(p, s); break;
-      case 10: launch_conv_cfg<64, 128, 2, 2, 1>(p, s); break;
-      default: launch_conv_cfg<32, 256, 1, 4, 1>(p, s); break;
-    }
-    return;
-  }
-  if (pln.cfg >= 4) {
-    if (p.x_bytes > 0) {
-      launch_conv_direct(p, pln.cfg, s);
-      return;
-    }
-    ConvPlan q = pln;  // buffer resource unavailable (> 2 GiB input): the LDS-staged kernel
-    q.cfg = 0;
-    launch_conv(p, q, s);
-    return;
-  }
-  if (pln.window) {
-    switch (pln.cfg) {
-      case 0: launch_win_cfg<128, 128, 2, 2>(p, pln, s); break;
-      case 1: launch_win_cfg<96, 128, 1, 4>(p, pln, s); break;
-      case 2: launch_win_cfg<64, 128, 2, 2>(p, pln, s); break;
-      default: launch_win_cfg<32, 256, 1, 4>(p, pln, s); break;
-    }
     return;
   }
   switch (pln.cfg) {

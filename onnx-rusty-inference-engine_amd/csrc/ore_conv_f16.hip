@@ -672,9 +672,6 @@ __global__ __launch_bounds__(256) void pack_weights_f16_kernel(const float* __re
       if (xmode == F16_X_NHWC_PAIR) {
         const int c = k & 3, t = k >> 2, r = t / kwp, sx = t - r * kwp;
         if (r < kh && sx < kw && c < C) v = w[(((long long)m * C + c) * kh + r) * kw + sx];
-      } else if (xmode == F16_X_NHWC8) {
-        const int c = k & 7, rs = k >> 3;
-        if (rs < KK && c < C) v = w[((long long)m * C + c) * KK + rs];
       } else if (k < K) {
         v = xmode == F16_X_NCHW32 ? w[(long long)m * K + k] : w[((long long)m * C + (k % C)) * KK + k / C];
       }
@@ -684,7 +681,7 @@ __global__ __launch_bounds__(256) void pack_weights_f16_kernel(const float* __re
 }
 
 int f16_conv_k(int xmode, int C, int kh, int kw) {
-  return xmode == F16_X_NHWC_PAIR ? kh * ((kw + 1) & ~1) * 4 : xmode == F16_X_NHWC8 ? kh * kw * 8 : C * kh * kw;
+  return xmode == F16_X_NHWC_PAIR ? kh * ((kw + 1) & ~1) * 4 : C * kh * kw;
 }
 
 void launch_pack_weights_f16(const float* w, int xmode, int M, int C, int kh, int kw, int Mp, void* wh,
@@ -720,17 +717,13 @@ __global__ __launch_bounds__(256) void ktab_nhwc_kernel(int2* __restrict__ ktab,
 }
 
 void launch_ktab_nhwc(int2* ktab, int xmode, int C, int kh, int kw, int cs, int W, hipStream_t s) {
-  if (xmode == F16_X_NHWC8) {  // the 16-B gather over the 8 converted channels
-    xmode = F16_X_NHWC_VEC;
-    C = 8;
-  }
   const int n = conv_packed_kp(f16_conv_k(xmode, C, kh, kw)) / (xmode == F16_X_NHWC_ELEM ? 1 : 8);
   hipLaunchKernelGGL(ktab_nhwc_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ktab, xmode, C, kh, kw, n, cs, W);
 }
 
 // f32 NCHW (plane stride x_ps, image stride x_nstride) -> f16 NHWC with CS channels per pixel
-// (channels >= C zero): the operand of F16_X_NHWC_PAIR (CS = 4) / F16_X_NHWC8 (CS = 8) for the
-// first conv.  One thread per pixel: coalesced plane reads, one 8-B / 16-B store.
+// (channels >= C zero): the operand of F16_X_NHWC_PAIR (CS = 4) for the first conv.  One thread per
+// pixel: coalesced plane reads, one 8-B store.
 template <int CS>
 __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float* __restrict__ x, _Float16* __restrict__ y,
                                                            long long pixels, int HW, int C, long long x_nstride,
@@ -753,17 +746,9 @@ void launch_nchw_to_nhwc(const float* x, void* y, int N, int C, int HW, long lon
   if (pixels <= 0) return;
   long long b = (pixels + 255) / 256;
   if (b > 256 * 32) b = 256 * 32;
-  if (cs == 8)
-    hipLaunchKernelGGL(nchw_to_nhwc_kernel<8>, dim3((unsigned)b), dim3(256), 0, s, x, static_cast<_Float16*>(y), pixels,
-                       HW, C, x_nstride, x_ps);
-  else
-    hipLaunchKernelGGL(nchw_to_nhwc_kernel<4>, dim3((unsigned)b), dim3(256), 0, s, x, static_cast<_Float16*>(y), pixels,
-                       HW, C, x_nstride, x_ps);
-}
-
-static int env_knob_f16(const char* name, int dflt) {  // tuning knob, read per launch
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
+  (void)cs;  // 4 (F16_X_NHWC_PAIR)
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel<4>, dim3((unsigned)b), dim3(256), 0, s, x, static_cast<_Float16*>(y), pixels,
+                     HW, C, x_nstride, x_ps);
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -777,10 +762,8 @@ static void launch_f16_cfg(const ConvParams& p0, int xmode, hipStream_t s) {
     case F16_X_NHWC_ELEM: hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, WN, F16_X_NHWC_ELEM>), grid, block, 0, s, p); break;
     case F16_X_NHWC_PAIR: hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, WN, F16_X_NHWC_PAIR>), grid, block, 0, s, p); break;
     default:
-      if (p.x_bytes > 0 && env_knob_f16("ORE_F16_DMA", 1))
-        hipLaunchKernelGGL((conv_f16_dma_kernel<BM, BN, WM, WN>), grid, block, 0, s, p);
-      else
-        hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, WN, F16_X_NHWC_VEC>), grid, block, 0, s, p);
+      // LDS-DMA B tiles (run_conv_f16 launches image chunks whose extent fits the buffer resource)
+      hipLaunchKernelGGL((conv_f16_dma_kernel<BM, BN, WM, WN>), grid, block, 0, s, p);
       break;
   }
 }

@@ -46,49 +46,6 @@ typedef float cp_floatx3 __attribute__((ext_vector_type(3)));
 // 5..229 for S = 64 and 128 (4 / 7 slots for a 28-quad row).
 static int cp_nring(int qrow, int S) { return ((qrow + 2 * S - 2) / qrow + 4) / 2; }
 
-// Exact ring size for a geometry by simulating the walk (the kernel's step / flush rules): the
-// smallest nring such that no two live pooled rows share a slot and, unless a second barrier
-// separates the clears from the next step's maxima (dbar), no slot cleared after a step is
-// touched by the next one.  Used for the double-barrier variant, whose point is a smaller ring.
-static int cp_nring_exact(int qrow, int Ho, int Hp, int S, int nbands, bool dbar) {
-  int need = 2;
-  const int pbn = (Hp + nbands - 1) / nbands;
-  for (int band = 0; band < nbands; ++band) {
-    const int py0 = band * pbn, py1 = py0 + pbn < Hp ? py0 + pbn : Hp;
-    if (py0 >= py1) continue;
-    const int q0 = 2 * py0 * qrow, nq = (2 * py1 + 1 < Ho ? 2 * py1 + 1 : Ho) * qrow;
-    for (int nr = need; nr < 256; ++nr) {
-      std::vector<int> owner(nr, -1);
-      std::vector<char> cleared(nr, 0);
-      int py_next = py0;
-      bool ok = true;
-      for (int qs = q0; qs < nq && ok; qs += S) {
-        const int qe = qs + S < nq ? qs + S : nq;
-        for (int qd = qs; qd < qe && ok; ++qd) {
-          const int oy = qd / qrow, pa = oy >> 1, pbr = ((oy & 1) == 0 && oy >= 2) ? pa - 1 : -1;
-          for (int py : {pa, pbr}) {
-            if (py < py0 || py >= py1) continue;
-            const int sl = py % nr;
-            if ((owner[sl] >= 0 && owner[sl] != py) || (!dbar && cleared[sl])) { ok = false; break; }
-            owner[sl] = py;
-          }
-        }
-        const int rd = qe / qrow;
-        int pe = qe == nq ? py1 : (rd >= 3 ? ((rd - 3) >> 1) + 1 : 0);
-        if (pe > py1) pe = py1;
-        std::fill(cleared.begin(), cleared.end(), 0);
-        for (int py = py_next; py < pe; ++py) {
-          cleared[py % nr] = 1;
-          if (owner[py % nr] == py) owner[py % nr] = -1;
-        }
-        if (pe > py_next) py_next = pe;
-      }
-      if (ok) { need = nr; break; }
-    }
-  }
-  return need;
-}
-
 template <int MF>
 __device__ __forceinline__ void cp_load_a(__amdgpu_buffer_rsrc_t r, int voff, int soff, float (&a)[MF]) {
   if constexpr (MF == 6) {
@@ -121,7 +78,7 @@ enum { CP_S2 = 0, CP_1X1 = 1, CP_T3 = 2 };
 // MF: 16-channel fragments per block (every wave computes all 16 MF channels of its 16 quads);
 // D: k-steps in flight; NW: waves per block.  qrow = quads per conv row, nsteps = 16 NW-quad steps per
 // image.
-template <int MF, int D, int NW, int MODE, bool DB>
+template <int MF, int D, int NW, int MODE>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvParams p, int qrow, int nbands, int nring) {
   extern __shared__ unsigned cp_lds[];  // [nring][16 MF][Wp] pooled maxima (f32 bits)
   const int tid = threadIdx.x;
@@ -372,7 +329,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
               }
           }
           if (py_end > py_next) py_next = py_end;
-          if constexpr (DB) __syncthreads();  // the clears land before the next step's maxima
 #pragma unroll
     for (int q_ = 0; q_ < 4; ++q_) tmc[q_] = tmask[q_];
     ++cs;
@@ -415,25 +371,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
 
 // variants (ConvParams::ep_variant): 2 = 48 channels x 64 quads per block (4 waves), 3 = 96 channels
 // x 128 quads (8 waves: twice the MFMAs per operand load, one block per CU), 4 = 64 channels x 64
-// quads (4 waves), 5 = variant 4 over 3 bands of pooled rows per image (3x the blocks), 6 = 96
-// channels x 64 quads over 2 bands with a second barrier per step (the smaller ring lets two blocks
-// share a CU, so one block's MFMAs run under the other's epilogue)
+// quads (4 waves), 5 = variant 4 over 3 bands of pooled rows per image (3x the blocks).  (Variant 6,
+// 96 x 64 over 2 bands with a second barrier per step, two blocks per CU, measured slower inside the
+// graph -- 963 vs 913 us on conv1 + pool1, profiles/r01zg_conv1_walk96_b2.txt -- and is retired.)
 static void cp_shape(int variant, int M, int* mf, int* nw) {
-  *mf = (variant == 3 || variant == 6) ? 6 : (variant == 4 || variant == 5) ? 4 : (M > 32 ? 3 : 2);
+  *mf = variant == 3 ? 6 : (variant == 4 || variant == 5) ? 4 : (M > 32 ? 3 : 2);
   *nw = variant == 3 ? 8 : 4;
 }
-static int cp_bands(int variant) { return variant == 5 ? 3 : variant == 6 ? 2 : 1; }
+static int cp_bands(int variant) { return variant == 5 ? 3 : 1; }
 static int cp_ring(const ConvParams& p, int variant) {
   int mf, nw;
   cp_shape(variant, p.M, &mf, &nw);
   const int qrow = (p.Wo + 3) / 4;
-  if (variant != 6) return cp_nring(qrow, 16 * nw);
-  static thread_local int key[4] = {-1, -1, -1, -1}, val = 0;  // one geometry cached per thread
-  if (key[0] != qrow || key[1] != p.Ho || key[2] != p.ep_Ho || key[3] != 16 * nw) {
-    key[0] = qrow; key[1] = p.Ho; key[2] = p.ep_Ho; key[3] = 16 * nw;
-    val = cp_nring_exact(qrow, p.Ho, p.ep_Ho, 16 * nw, cp_bands(variant), true);
-  }
-  return val;
+  return cp_nring(qrow, 16 * nw);
 }
 static int cp_mode(const ConvParams& p);
 static size_t cp_lds_bytes(const ConvParams& p, int variant) {
@@ -464,14 +414,14 @@ static int cp_mode(const ConvParams& p) {
 }
 
 bool conv_pool_stream_eligible(const ConvParams& p, int variant) {
-  if (variant < 2 || variant > 6 || cp_mode(p) < 0) return false;
-  if ((variant == 3 || variant == 6) && (p.M < 64 || cp_mode(p) != CP_S2)) return false;  // idle rows / spills
+  if (variant < 2 || variant > 5 || cp_mode(p) < 0) return false;
+  if (variant == 3 && (p.M < 64 || cp_mode(p) != CP_S2)) return false;  // idle rows / spills
   if ((variant == 4 || variant == 5) && p.M < 48) return false;
   if (variant == 5 && p.ep_Ho < 6) return false;
   return cp_lds_bytes(p, variant) <= size_t(variant == 3 ? 152 : 78) * 1024;
 }
 
-template <int MF, int D, int NW, int MODE, bool DB>
+template <int MF, int D, int NW, int MODE>
 static void launch_cp(const ConvParams& p0, size_t lds, int nbands, int nring, hipStream_t s) {
   ConvParams p = p0;
   p.mtiles = (p.M + 16 * MF - 1) / (16 * MF);
@@ -485,24 +435,24 @@ static void launch_cp(const ConvParams& p0, size_t lds, int nbands, int nring, h
     (void)hipGetDevice(&dev);
     const unsigned long long bit = 1ull << (dev & 63);
     if (!(raised.load(std::memory_order_acquire) & bit)) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pool_stream_kernel<MF, D, NW, MODE, DB>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pool_stream_kernel<MF, D, NW, MODE>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       raised.fetch_or(bit, std::memory_order_acq_rel);
     }
   }
-  hipLaunchKernelGGL((conv_pool_stream_kernel<MF, D, NW, MODE, DB>), dim3((unsigned)(p.N * nbands * p.mtiles)),
+  hipLaunchKernelGGL((conv_pool_stream_kernel<MF, D, NW, MODE>), dim3((unsigned)(p.N * nbands * p.mtiles)),
                      dim3(64 * NW), lds, s, p, qrow, nbands, nring);
 }
 
-template <int MF, int NW, bool DB = false>
+template <int MF, int NW>
 static void launch_cp_mode(const ConvParams& p, size_t lds, int nbands, int nring, hipStream_t s) {
   if constexpr (MF == 6) {  // the 96-channel tiles: conv1 only (the stride-1 modes would spill)
-    launch_cp<MF, ORE_CP_D, NW, CP_S2, DB>(p, lds, nbands, nring, s);
+    launch_cp<MF, ORE_CP_D, NW, CP_S2>(p, lds, nbands, nring, s);
   } else {
     switch (cp_mode(p)) {
-      case CP_S2: launch_cp<MF, ORE_CP_D, NW, CP_S2, DB>(p, lds, nbands, nring, s); break;
-      case CP_1X1: launch_cp<MF, ORE_CP_D, NW, CP_1X1, DB>(p, lds, nbands, nring, s); break;
-      default: launch_cp<MF, ORE_CP_D, NW, CP_T3, DB>(p, lds, nbands, nring, s); break;
+      case CP_S2: launch_cp<MF, ORE_CP_D, NW, CP_S2>(p, lds, nbands, nring, s); break;
+      case CP_1X1: launch_cp<MF, ORE_CP_D, NW, CP_1X1>(p, lds, nbands, nring, s); break;
+      default: launch_cp<MF, ORE_CP_D, NW, CP_T3>(p, lds, nbands, nring, s); break;
     }
   }
 }
@@ -512,9 +462,7 @@ void launch_conv_pool_stream(const ConvParams& p, int variant, hipStream_t s) {
   cp_shape(variant, p.M, &mf, &nw);
   const size_t lds = cp_lds_bytes(p, variant);
   const int nb = cp_bands(variant), nr = cp_ring(p, variant);
-  if (variant == 6)
-    launch_cp_mode<6, 4, true>(p, lds, nb, nr, s);
-  else if (variant == 3)
+  if (variant == 3)
     launch_cp_mode<6, 8>(p, lds, nb, nr, s);
   else if (variant == 4 || variant == 5)
     launch_cp_mode<4, 4>(p, lds, nb, nr, s);

@@ -233,7 +233,7 @@ static int stream_lead(const ConvParams& p) { return ((p.pt * p.W + p.pl) * 4 + 
 
 // 0: not eligible, 1: S1X1, 2: STAPS
 static int stream_mode(const ConvParams& p) {
-  if (p.pool || p.x_bytes <= 0 || !p.vec_out || p.K % 16 != 0 || p.Ntot % 4 != 0 || p.Ntot < 4) return 0;
+  if (p.x_bytes <= 0 || !p.vec_out || p.K % 16 != 0 || p.Ntot % 4 != 0 || p.Ntot < 4) return 0;
   if (p.is1x1) {
     const uintptr_t xa = reinterpret_cast<uintptr_t>(p.x);
     return ((xa & 15) == 0 && p.x_ps % 4 == 0 && p.x_nstride % 4 == 0) ? 1 : 0;

@@ -606,27 +606,18 @@ static void launch_x3w(const ConvParams& p0, hipStream_t s) {
     (void)hipGetDevice(&dev);
     const unsigned long long bit = 1ull << (dev & 63);
     if (!(raised.load(std::memory_order_acquire) & bit)) {
-      const void* fns[4] = {reinterpret_cast<const void*>(&conv_x3w_kernel<FM, FN, 4, 0>),
-                            reinterpret_cast<const void*>(&conv_x3w_kernel<FM, FN, 2, 0>),
-                            reinterpret_cast<const void*>(&conv_x3w_kernel<FM, FN, 4, 1>),
+      const void* fns[2] = {reinterpret_cast<const void*>(&conv_x3w_kernel<FM, FN, 4, 1>),
                             reinterpret_cast<const void*>(&conv_x3w_kernel<FM, FN, 2, 1>)};
       for (const void* fn : fns) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       raised.fetch_or(bit, std::memory_order_acq_rel);
     }
   }
-  // block summation on by default (ORE_X3_SACC=0: one running accumulator, an experiment knob): 3x
-  // lower error than one accumulator on the SqueezeNet shapes (profiles/r02_x3_accuracy.json)
-  const bool sacc = getenv("ORE_X3_SACC") ? atoi(getenv("ORE_X3_SACC")) != 0 : true;
-  if (sacc) {
-    if (p.bch == 4)
-      hipLaunchKernelGGL((conv_x3w_kernel<FM, FN, 4, 1>), grid, block, lds, s, p);
-    else
-      hipLaunchKernelGGL((conv_x3w_kernel<FM, FN, 2, 1>), grid, block, lds, s, p);
-  } else if (p.bch == 4) {
-    hipLaunchKernelGGL((conv_x3w_kernel<FM, FN, 4, 0>), grid, block, lds, s, p);
-  } else {
-    hipLaunchKernelGGL((conv_x3w_kernel<FM, FN, 2, 0>), grid, block, lds, s, p);
-  }
+  // block summation (SACC = 1): 3x lower error than one running accumulator on the SqueezeNet shapes
+  // (profiles/r02_x3_accuracy.json; the single-accumulator form is the SACC = 0 instance)
+  if (p.bch == 4)
+    hipLaunchKernelGGL((conv_x3w_kernel<FM, FN, 4, 1>), grid, block, lds, s, p);
+  else
+    hipLaunchKernelGGL((conv_x3w_kernel<FM, FN, 2, 1>), grid, block, lds, s, p);
 }
 
 size_t x3w_plan_lds(int Ho, int Wo, int kh, int kw, int C, int tile) {

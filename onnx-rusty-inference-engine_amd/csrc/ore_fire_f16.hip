@@ -434,14 +434,6 @@ bool fire_pool_f16_plan(FireF16Params* p) {
       p->PR = PR;
     }
   }
-  if (const char* e = getenv("ORE_FIRE_POOL_SHAPE")) {
-    int f = 0, r = 0;
-    if (sscanf(e, "%d,%d", &f, &r) == 2 && f >= 2 && f <= 4 && r >= 1 && (2 * r + 1) * p->W <= 128 * f &&
-        r * p->Wp <= 128 && fire_pool_lds_bytes(p->C, p->H, p->W, r) <= FIRE_F16_LDS_MAX) {
-      p->F = f;
-      p->PR = r;
-    }
-  }
   return best > 0;
 }
 

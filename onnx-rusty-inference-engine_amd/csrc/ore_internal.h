@@ -21,7 +21,9 @@ struct ore_ctx {
   // which has a 4 KiB lead): the streaming conv may read a few bytes before an input inside it
   const char* mapped_lo = nullptr;
   const char* mapped_hi = nullptr;
-  int conv_algo = 0;  // ore_ctx_set_conv_algo (per-op ore_conv2d_f32 only)
+  int conv_algo = 0;     // ore_ctx_set_conv_algo (per-op ore_conv2d_f32 only)
+  int conv_tile = -1;    // ore_ctx_set_conv_tile: a forced tile id (-1: per-layer heuristic / autotune)
+  int pool_variant = 0;  // ore_ctx_set_pool_variant: a forced MaxPool kernel (0: by layout)
 };
 
 namespace ore {
@@ -88,32 +90,22 @@ ore_status resolve_window(ore_ctx* ctx, int auto_pad, const int64_t* pads, int n
 // ---------------------------------------------------------------- launches over resolved geometry
 // Kernel plan of a conv (or MatMul as a 1x1 conv) over resolved geometry.
 ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
-                   const Window& win, bool f16 = false, int xmode = 0, bool x3 = false, bool wino = false);
+                   const Window& win, bool f16 = false, int xmode = 0, bool x3 = false, bool wino = false,
+                   int forced = -1);
 // wp: weights packed by launch_pack for plan `pln`
 // ktab: gather table (launch_ktab) for non-1x1 geometry on the gather kernel
 ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
                     int64_t x_nstride, const float* wp, const int2* ktab, int64_t M, int64_t kh, int64_t kw,
                     const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, float* y,
                     int64_t y_nstride, int64_t x_ps = 0, int64_t y_ps = 0,  // plane strides, 0 = dense
-                    int x_es = 4,   // input element bytes (2: f16; only with an f16 plan, whose output is f16)
-                    const struct ConvE1* e1 = nullptr);  // Winograd plans: a 1x1 conv fused in (ConvParams::e1_*)
-// a 1x1 conv (+ bias, Relu) on the same input as a Winograd 3x3 conv with the same output channels,
-// computed by the Winograd launch; y has the 3x3 conv output's plane and image strides
-struct ConvE1 {
-  const float* wp;  // standard K-major packing [C][Mp]
-  const float* bias;
-  float* y;
-  int64_t Mp;
-  bool relu;
-};
+                    int x_es = 4);  // input element bytes (f32 plans only)
 // the MaxPool fused into an f16 conv's epilogue (ORE_FUSE_CONV_POOL; 3x3 / stride 2)
 struct F16Epool {
   int64_t kh, kw, sh, sw;
   Window win;  // the pool's window over the conv output
 };
 // f16 first conv + pooled epilogue straight from the f32 NCHW input (ore_conv1_f16.hip) when its
-// geometry allows; *ran = false (and ORE_OK) otherwise, for the two-launch path.  ORE_F16_C1POOL=0
-// turns it off (experiments).
+// geometry allows; *ran = false (and ORE_OK) otherwise, for the two-launch path.
 ore_status run_conv_pair_pool_f16(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H,
                                   int64_t W, int64_t x_nstride, int64_t x_ps, const void* wp, int64_t M, int64_t kh,
                                   int64_t kw, const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu,
@@ -140,7 +132,7 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
 ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
                     int64_t x_ps, const float* w1, const float* b1, int64_t E1, const float* w3, const float* b3,
                     int64_t E3, const float* ws, int64_t Msp, const float* bs, int64_t Ms, float* y, int64_t y_nstride,
-                    int64_t y_ps, bool wino = false, const Window* pool = nullptr);
+                    int64_t y_ps, const Window* pool = nullptr);
 // the f16 fused fire module (ore_fire_f16.hip): x = S, y = S' NHWC f16 (pixel strides x_cs / y_cs,
 // image strides in elements); w1 / w3 / ws in launch_fire_pack_f16 layout; pool: a 3x3 / stride-2
 // MaxPool (window over the H x W conv plane) between the Concat and the squeeze, y on its plane
@@ -153,8 +145,8 @@ ore_status run_fire_f16(ore_ctx* ctx, const void* x, int64_t N, int64_t C, int64
 // (the conv columns computed, recomputed overlap and padding included), 0 for other pools
 double epool_tile(int64_t Ho, int64_t Wo, int64_t pkh, int64_t pkw, int64_t psh, int64_t psw, const Window& pwin,
                   int* tr, int* tc);
-// 1x1 conv over the 3x3 MaxPool (window pwin, strides psh/psw) of x [C][pH][pW] (plane stride x_ps):
-// the pooled tensor is never materialised (ORE_FUSE_POOL_CONV)
+// 1x1 conv over the 3x3 / stride-2 MaxPool (window pwin) of x [C][pH][pW] (plane stride x_ps) on
+// pool_conv1x1_f32_kernel: the pooled tensor is never materialised (walker pass fuse_pool_squeeze)
 ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t pH,
                          int64_t pW, int64_t x_nstride, int64_t x_ps, const Window& pwin, int64_t psh, int64_t psw,
                          const float* wp, int64_t M, const float* bias, bool relu, float* y, int64_t y_nstride,
@@ -168,7 +160,7 @@ size_t packed_bytes(const ConvPlan& pln);
 ore_status run_maxpool(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
                        int64_t x_nstride, int64_t kh, int64_t kw, const Window& win, int64_t sh, int64_t sw,
                        float* y, int64_t y_nstride, int64_t x_ps = 0, int64_t y_ps = 0,
-                       int es = 4);  // element bytes of x and y
+                       int es = 4);  // element bytes of x and y; ctx->pool_variant selects a kernel
 // MaxPool over NHWC f16 (f16 models); x_cs / y_cs: pixel strides
 ore_status run_maxpool_nhwc(ore_ctx* ctx, const void* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
                             int64_t x_cs, int64_t kh, int64_t kw, const Window& win, int64_t sh, int64_t sw, void* y,

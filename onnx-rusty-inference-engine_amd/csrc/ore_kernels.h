@@ -50,11 +50,7 @@ struct ConvParams {
   int x_guard;         // bytes before x known to be mapped (the streaming 3x3 conv reads a few of them,
                        // zero-masked, instead of issuing negative buffer offsets)
   int x_lead;          // filled by the streaming launcher: bytes it reads before x (<= x_guard)
-  // fused MaxPool (ORE_FUSE_POOL_CONV, f32 only): x is the PRE-pool tensor [pool_H][pool_W] planes
-  // and the conv (1x1) reads each B element as the 3x3 window max at stride (pool_sh, pool_sw)
-  int pool;            // 1: BPOOL operand mode
-  int pool_sh, pool_sw, pool_pt, pool_pl, pool_H, pool_W;
-  // window-staged kernel (filled by the launcher from the ConvPlan)
+  // x3 window-staged kernel (filled by the launcher from the ConvPlan and the geometry)
   int bch, ks, nst, wr, ww, tiles_per_img;
   // pooled epilogue (ORE_FUSE_CONV_POOL, launch_conv_epool; 3x3 / stride-2 pool): y is the MaxPool
   // output [..][ep_Ho][ep_Wo] (plane stride y_ps), pool pads ep_pt / ep_pl; a block's N tile is a
@@ -63,24 +59,16 @@ struct ConvParams {
   int ep_variant;      // pooled-conv kernel (launch_conv_epool): 0 auto, 1 patch, 2 / 3 row walk
   const float* wc1;    // variant 7: weights in launch_pack_c1_f32 layout (null: variant 7 unavailable)
   const struct C1SqueezeF32* sq1;  // variant 7 with the next 1x1 conv fused in (forces variant 7)
-  // Winograd 32x32 tiles: a 1x1 conv (+ bias, Relu) on the same input with the same M output channels
-  // computed in the same launch (conv_wino_e1_eligible); e1_y has y's plane and image strides
-  const float* e1_wp;  // K-major packed [C][e1_Mp] (the standard 1x1 packing)
-  const float* e1_bias;
-  float* e1_y;         // null: no fused 1x1 conv
-  int e1_Mp, e1_relu;
 };
 
 // Per-layer kernel choice and weight layout (see plan_conv in ore_conv.hip).
 struct ConvPlan {
   int f16;             // 1: conv_f16_kernel (f16 weights Wh[Mp][Kp] and f16 NHWC output)
-  int xmode;           // f16: F16_X_NCHW32 / F16_X_NHWC_ELEM / F16_X_NHWC_VEC (operand gather, k order)
-  int window;          // 1: conv_win_kernel (stage-major packed weights), 0: conv_gemm_kernel
-  int cfg;             // block tile (0: 128x128, 1: 96x128, 2: 64x128, 3: 32x256)
-  int bch, ks, nst;    // window: channels / K rows per stage, stages
-  int wr, ww, wq;      // window rows, columns, loads per lane per row
+  int xmode;           // f16: F16_X_NCHW32 / F16_X_NHWC_ELEM / F16_X_NHWC_VEC / F16_X_NHWC_PAIR
+  int cfg;             // tile id (0-3: conv_gemm_kernel 128x128, 96x128, 64x128, 32x256; 12-20 streaming;
+                       // X3_TILE_BASE + t; WINO_TILE_BASE + t)
+  int bch, ks, nst;    // x3 window kernel: channel groups per chunk, K rows per chunk, chunks
   int Mp, krows;       // packed weights are krows x Mp floats
-  size_t lds;          // dynamic LDS bytes of the window kernel
   int epv = 0;         // pooled-epilogue steps: ConvParams::ep_variant (ore_model_autotune)
   int x3 = 0;          // 1: conv_x3_kernel (f32 on the BF16 matrix cores, ore_conv_x3.hip); cfg = X3_TILE_BASE + tile
   int wino = 0;        // 1: conv_wino_kernel (Winograd F(2x2, 3x3), ore_conv_wino.hip); cfg = WINO_TILE_BASE + tile
@@ -95,6 +83,7 @@ struct PoolParams {
   int x_ps, y_ps;      // channel-plane strides (elements)
   long long x_nstride, y_nstride;
   int es;              // element bytes: 4 (f32) or 2 (f16)
+  int variant;         // 0: by layout (launch_maxpool); 1-4 force chunk / plane / strip / direct (ore_ctx_set_pool_variant)
 };
 
 // MaxPool over channels-last f16 (f16 models): element (n, c, h, w) at n*nstride + (h*W + w)*cs + c
@@ -133,7 +122,6 @@ struct FireParams {
   long long x_bytes;                     // x's valid extent in bytes
   int x_guard, x_lead;                   // mapped bytes before x; bytes the 3x3 taps read before it
   int ntiles;                            // filled by the launcher
-  int wino;                              // 1: e3 by Winograd (launch_fire_wino; w3 from launch_fire_pack_wino)
   // pooled form (fire_pool_kernel): a 3x3 / stride-2 MaxPool (Hp x Wp, pads ppt / ppl) between the
   // Concat and the squeeze; y is then [N][Ms][Hp][Wp]; PR pooled rows per workgroup (fire_pool_plan)
   int pool, Hp, Wp, ppt, ppl, PR;
@@ -141,11 +129,6 @@ struct FireParams {
 bool fire_eligible(const FireParams& p);
 void launch_fire(const FireParams& p, hipStream_t s);
 bool fire_pool_plan(FireParams* p);  // picks PR; false when no band shape fits
-// the fire module with its expand3x3 by Winograd F(2x2, 3x3) (ore_conv_wino.hip): w3 packed by
-// launch_fire_pack_wino ([C][4][E3][4] f32, rows of each 32-channel chunk permuted); C <= 64, E3 % 32 == 0
-bool fire_wino_eligible(const FireParams& p);
-void launch_fire_wino(const FireParams& p, hipStream_t s);
-void launch_fire_pack_wino(const float* w, int M, int C, float* u, hipStream_t s);
 // W [M][K] -> the fire kernel's row-permuted K-major packing (M % 64 == 0)
 void launch_fire_pack(const float* w, int M, int K, float* wf, hipStream_t s);
 
@@ -217,8 +200,10 @@ int conv_packed_kp(int K);  // padded K of the packed weights
 // w: ONNX conv weights [M][K] (kmajor_src = false) or MatMul B [K][M] (true) -> wp[Kp][Mp]
 void launch_pack_weights(const float* w, bool kmajor_src, int M, int K, int Mp, float* wp, hipStream_t s);
 void launch_ktab(int2* ktab, int K, int kh, int kw, int x_ps, int W, hipStream_t s);
+// forced >= 0: that tile id when it belongs to the plan's kernel family (ore_ctx_set_conv_tile), else
+// the per-layer heuristic
 ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
-                   bool is1x1, bool f16 = false, int xmode = 0, bool x3 = false, bool wino = false);
+                   bool is1x1, bool f16 = false, int xmode = 0, bool x3 = false, bool wino = false, int forced = -1);
 // f16 conv operand modes (ConvPlan::xmode), chosen by the input's layout:
 enum {
   F16_X_NCHW32 = 0,     // f32 NCHW model input, per-element gather, k order (c, r, s) (the reference's)
@@ -226,12 +211,10 @@ enum {
   F16_X_NHWC_VEC = 2,   // f16 NHWC input, C % 8 == 0: one 16-B load per (pixel, 8 channels), k order (r, s, c)
   F16_X_NHWC_PAIR = 3,  // f32 NCHW input with C <= 4, converted to NHWC4 f16 (launch_nchw_to_nhwc): two
                         // 8-B taps per 8-k group, k order (r, s', c') over kw rounded up to even x 4 channels
-  F16_X_NHWC8 = 4,      // f32 NCHW input with C <= 8, converted to NHWC8 f16 (channels >= C zero): the
-                        // 16-B gather of F16_X_NHWC_VEC over 8 channels, k order (r, s, c' < 8)
 };
 // GEMM K of an f16 conv (PAIR pads the taps and channels)
 int f16_conv_k(int xmode, int C, int kh, int kw);
-// f32 NCHW -> f16 NHWC with cs (4 or 8) channels per pixel, channels >= C zero
+// f32 NCHW -> f16 NHWC with cs (4) channels per pixel, channels >= C zero
 void launch_nchw_to_nhwc(const float* x, void* y, int N, int C, int HW, long long x_nstride, int x_ps, int cs,
                          hipStream_t s);
 // Wh[Mp][Kp] = f16(W[M][C][kh][kw]) in the k order of `xmode` (MatMul stays f32)
@@ -256,13 +239,12 @@ void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s);
 // Conv (+ Relu) with the following MaxPool in its epilogue (ConvParams ep_* set; f32)
 void launch_conv_epool(const ConvParams& p, hipStream_t s);
 // Stride-2 Conv + Relu + 3x3 / stride-2 MaxPool walking the conv plane row-major with the pooled rows
-// in an LDS ring (ore_conv_pool.hip; conv1 + pool1): launch_conv_epool takes it when eligible
-// (ORE_CONV_POOL_STREAM=0 keeps conv_gemm_kernel's patch epilogue)
+// in an LDS ring (ore_conv_pool.hip; conv1 + pool1): launch_conv_epool takes it when eligible.
 // variants (ConvParams::ep_variant): 1 = the patch kernel, 2 = walk 48 channels x 64 quads per block,
-// 3 = walk 96 channels x 128 quads, 4 = walk 64 x 64, 5 = 4 over 3 bands of pooled rows, 6 = walk
-// 96 x 64 over 2 bands (two blocks per CU); 0 = the first eligible of 3, 4, 2, 1 at batch >= 128,
-// else 1.
-// ORE_CONV_POOL_STREAM=0..5 forces 1..6 (tests).  launch_conv_epool leaves last_conv_tile = EPOOL_TILE_BASE + variant run.
+// 3 = walk 96 channels x 128 quads, 4 = walk 64 x 64, 5 = 4 over 3 bands of pooled rows; 0 = the first
+// eligible of 3, 4, 2, 1 at batch >= 128, else 1.  A model sets the variant per step (autotune,
+// ore_model_set_step_tile with EPOOL_TILE_BASE + variant).  launch_conv_epool leaves last_conv_tile =
+// EPOOL_TILE_BASE + the variant run.
 constexpr int EPOOL_TILE_BASE = 21;
 // variant 7 (ore_conv1_f32.hip): the first conv (7x7 / stride 2, C in {1, 3, 4}, 64 < M <= 128) with
 // its input window in LDS, weights packed by launch_pack_c1_f32 (ConvPlan::wc1); reported as tile
@@ -289,11 +271,11 @@ bool conv_pool_stream_eligible(const ConvParams& p, int variant);
 void launch_conv_pool_stream(const ConvParams& p, int variant, hipStream_t s);
 constexpr int CONV_EPOOL_BN = 256;  // N tile of the pooled-epilogue kernel
 constexpr int EPOOL_TILE_PR = 6, EPOOL_TILE_PC = 9;  // pooled outputs per block (13 x 19 conv patch)
-// LDS-free, barrier-free variant (ore_conv_direct.hip): tiles 4-7 (needs p.x_bytes > 0)
-void launch_conv_direct(const ConvParams& p, int tile, hipStream_t s);
-constexpr int CONV_TILES_F32 = 21;  // 0-3 conv_gemm_kernel, 4-7 conv_direct_kernel (ORE_CONV_CFG only),
-                                    // 8-11 conv_gemm_kernel warp-specialised (512 threads),
-                                    // 12-20 conv_stream_kernel (stride-1 geometries only)
+// tile ids 4-11 are retired (the LDS-free direct and the warp-specialised conv_gemm variants, measured
+// slower on every SqueezeNet layer: DESIGN.md section 7.1); ore_model_set_step_tile rejects them
+constexpr int CONV_TILES_F32 = 21;  // 0-3 conv_gemm_kernel, 12-20 conv_stream_kernel (stride-1 geometries)
+constexpr int FIRE_TILE = 21;       // the fused f32 fire module (fire_kernel): ore.Model.TILE_NAMES "fire"
+inline bool conv_tile_retired(int t) { return t >= 4 && t < 12; }
 // LDS-free streaming kernel (ore_conv_stream.hip): 1x1 convs and stride-1 convs with Wo == W (every
 // expand3x3); tiles CONV_TILE_STREAM + 0..8 = 64x128, 32x256, 16x256, 48x128, 64x64, 128x64, 64x64 D8,
 // 32x128, 128x64 D2 (channels x pixels per wave); other geometries fall back to tile 0
@@ -304,7 +286,6 @@ void launch_conv_stream(const ConvParams& p, int tile, hipStream_t s);
 // tile 0); ore_model_autotune skips candidates that fell back
 extern thread_local int last_conv_tile;
 constexpr int CONV_TILES_F16 = 4;
-constexpr int CONV_TILES_AUTOTUNE = 4;  // the direct tiles measured 15-80 % slower on every SqueezeNet layer
 // f32 conv on the BF16 matrix cores by an exact three-way bf16 split of both operands (six part
 // products, f32 accumulation; ore_conv_x3.hip).  Tiles X3_TILE_BASE + 0..3 = 128x128, 64x256,
 // 96x128, 64x128 (channels x pixels per block); results do not depend on the tile.  Weights
@@ -327,15 +308,16 @@ void launch_pack_x3w(const float* w, int M, int C, int kh, int kw, int Mp, int G
                      hipStream_t s);
 void launch_conv_x3(const ConvParams& p, int tile, hipStream_t s);
 // 3x3 / stride-1 / pad-1 f32 conv by Winograd F(2x2, 3x3) on the f32 MFMA (ore_conv_wino.hip).  Tiles
-// WINO_TILE_BASE + 0..3 = 32 ch x 32 tiles (32x32x2 MFMA, ring 4 / 2), 32 x 16, 16 x 32 (16x16x4); 4 = the
-// LDS-staged persistent kernel (U resident in LDS, input rows staged by LDS-DMA; C <= 64, W <= 64);
+// WINO_TILE_BASE + 0..3 = 32 ch x 32 tiles (32x32x2 MFMA, ring 4 / 2), 32 x 16, 16 x 32 (16x16x4);
 // results do not depend on the tile (not bit-identical to the direct kernels).  Weights packed by
 // launch_pack_wino: U = G g G^T as [C][4][Mp][4] f32 (channel, position quad, m, position) (Mp = wino_packed_mp(M)).
+// (id WINO_TILE_BASE + 4, the LDS-staged variant, is retired: slower on every expand3x3.)
 constexpr int WINO_TILE_BASE = X3_TILE_BASE + X3_TILES;
-constexpr int WINO_TILES_N = 5;
+constexpr int WINO_TILES_N = 4;
+// fused-kernel ids after the Winograd tiles (ore.Model.TILE_NAMES): 41 is retired (the Winograd fire module)
+constexpr int FIRE_F16_TILE = 42, C1_POOL_F16_TILE = 43;
 bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo);
 bool conv_wino_eligible(const ConvParams& p, int tile);
-bool conv_wino_e1_eligible(const ConvParams& p, int tile);
 int wino_packed_mp(int M);
 void launch_pack_wino(const float* w, int M, int C, int Mp, float* u, hipStream_t s);
 void launch_conv_wino(const ConvParams& p, int tile, hipStream_t s);

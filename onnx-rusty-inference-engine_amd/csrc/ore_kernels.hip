@@ -55,46 +55,6 @@ __global__ __launch_bounds__(256) void maxpool_kernel(PoolParams p, int chunks) 
   }
 }
 
-// LDS-staged MaxPool: one block per (plane, band of output rows).  The band's input rows are
-// one contiguous chunk of the plane, copied to LDS with coalesced loads (each input element
-// leaves HBM once); the windows are then evaluated from LDS.  Zero padding / -FLT_MAX start as
-// above.
-constexpr int POOL_LDS_FLOATS = 8192;  // 32 KiB per block
-
-__global__ __launch_bounds__(256) void maxpool_lds_kernel(PoolParams p, int band_rows) {
-  __shared__ float tile[POOL_LDS_FLOATS];
-  const int plane = blockIdx.x;
-  const int n = plane / p.C, c = plane - n * p.C;
-  const float* __restrict__ xp = p.x + (long long)n * p.x_nstride + (long long)c * p.x_ps;
-  float* __restrict__ yp = p.y + (long long)n * p.y_nstride + (long long)c * p.y_ps;
-  const int oh0 = blockIdx.y * band_rows;
-  const int oh1 = min(p.Ho, oh0 + band_rows);
-  const int ih_lo = max(0, oh0 * p.sh - p.pt);
-  const int ih_hi = min(p.H, (oh1 - 1) * p.sh - p.pt + p.kh);
-  const int cnt = (ih_hi - ih_lo) * p.W;
-  const float* __restrict__ src = xp + ih_lo * p.W;
-  for (int i = threadIdx.x; i < cnt; i += 256) tile[i] = src[i];
-  __syncthreads();
-  const int nout = (oh1 - oh0) * p.Wo;
-  for (int idx = threadIdx.x; idx < nout; idx += 256) {
-    const int dr = idx / p.Wo, ow = idx - dr * p.Wo;
-    const int oh = oh0 + dr;
-    const int ih0 = oh * p.sh - p.pt, iw0 = ow * p.sw - p.pl;
-    float m = -FLT_MAX;
-    for (int r = 0; r < p.kh; ++r) {
-      const int ih = ih0 + r;
-      const bool rok = (unsigned)ih < (unsigned)p.H;
-      const float* row = tile + (ih - ih_lo) * p.W;
-      for (int s = 0; s < p.kw; ++s) {
-        const int iw = iw0 + s;
-        const float v = (rok && (unsigned)iw < (unsigned)p.W) ? row[iw] : 0.0f;
-        m = fmaxf(m, v);
-      }
-    }
-    yp[oh * p.Wo + ow] = m;
-  }
-}
-
 // Column-strip MaxPool: one thread per (plane, output column, band of RB output rows).  The
 // thread walks down its band; each input row is reduced across the KW window columns once
 // and the row maxima shared by consecutive windows (KH > SH) stay in registers, so an output
@@ -279,15 +239,11 @@ __global__ __launch_bounds__(256) void maxpool_chunk_kernel(PoolParams p, int pb
   }
 }
 
-// tuning knobs, read per launch so tests can switch them: ORE_POOL_VARIANT 0 auto, 1 band
-// LDS-staged, 2 direct, 3 column strip, 4 plane-staged, 5 chunk-staged (ORE_POOL_CHUNK_KB of LDS
-// per block); ORE_POOL_LDS_KB (planes per block of
-// variant 4 = budget / plane bytes); ORE_POOL_RB (output rows per thread of variant 3)
-static int env_knob(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-static int pool_variant() { return env_knob("ORE_POOL_VARIANT", 0); }
+// variants (PoolParams::variant; 0 = by layout, others forced through ore_ctx_set_pool_variant for the
+// parity tests -- max is exact, so every variant is bit-identical): 2 direct, 3 column strip, 4
+// plane-staged (one plane per block), 5 chunk-staged (12 KB of LDS per block)
+constexpr long long POOL_CHUNK_BYTES = 12 * 1024;
+constexpr int POOL_STRIP_RB = 16;  // output rows per thread of the column strip
 
 template <typename T>
 static void launch_maxpool_t(const PoolParams& p, hipStream_t s) {
@@ -295,7 +251,7 @@ static void launch_maxpool_t(const PoolParams& p, hipStream_t s) {
   const int P = p.Ho * p.Wo;
   if (planes <= 0 || P <= 0) return;
   const long long plane_bytes = (long long)p.H * p.W * (long long)sizeof(T);
-  int v = pool_variant();
+  int v = p.variant;
   if (v == 0) {
     // measured on the SqueezeNet pools (batch 256): one plane per block from LDS for planes of
     // >= 2048 elements up to 48 KB (f32 pool1 485 -> 367 us, pool3 318 -> 227 us; f16 pool1 617 ->
@@ -317,7 +273,7 @@ static void launch_maxpool_t(const PoolParams& p, hipStream_t s) {
   }
   if (v == 5) {  // chunk-staged (falls through when the planes are not evenly spaced)
     constexpr int EV = 16 / (int)sizeof(T);
-    const long long lds_budget = (long long)env_knob("ORE_POOL_CHUNK_KB", 12) * 1024;
+    const long long lds_budget = POOL_CHUNK_BYTES;
     const long long pbytes = (long long)p.x_ps * (long long)sizeof(T);
     int pb = (int)(lds_budget / pbytes);
     if (pb > 64) pb = 64;
@@ -333,19 +289,8 @@ static void launch_maxpool_t(const PoolParams& p, hipStream_t s) {
     }
     v = 2;
   }
-  if (v == 1 && sizeof(T) == 4 && POOL_LDS_FLOATS / p.W >= p.kh) {
-    const int rows_fit = POOL_LDS_FLOATS / p.W;
-    int band = (rows_fit - p.kh) / p.sh + 1;
-    if (band > p.Ho) band = p.Ho;
-    const int nb = (p.Ho + band - 1) / band;
-    hipLaunchKernelGGL(maxpool_lds_kernel, dim3((unsigned)planes, nb), dim3(256), 0, s, p, band);
-    return;
-  }
   if (v == 4 && plane_bytes <= 64 * 1024) {
-    int lds_kb = env_knob("ORE_POOL_LDS_KB", 0);
-    if (lds_kb > 64) lds_kb = 64;
-    int pb = lds_kb ? (int)((long long)lds_kb * 1024 / plane_bytes) : 1;
-    if (pb < 1) pb = 1;
+    const int pb = 1;
     const long long nblk = (planes + pb - 1) / pb;
     const size_t lds = (size_t)(pb * plane_bytes);
     if (p.kh == 3 && p.kw == 3)
@@ -355,15 +300,9 @@ static void launch_maxpool_t(const PoolParams& p, hipStream_t s) {
     return;
   }
   if (v == 3 && p.kh == 3 && p.kw == 3 && p.sh == 2) {
-    const int RB = env_knob("ORE_POOL_RB", 16);
     const long long cols = planes * p.Wo;
-    const dim3 grid((unsigned)((cols + 255) / 256), (unsigned)((p.Ho + RB - 1) / RB));
-    if (RB <= 4)
-      hipLaunchKernelGGL((maxpool_strip_kernel<T, 3, 3, 2, 4>), grid, dim3(256), 0, s, p, cols);
-    else if (RB <= 8)
-      hipLaunchKernelGGL((maxpool_strip_kernel<T, 3, 3, 2, 8>), grid, dim3(256), 0, s, p, cols);
-    else
-      hipLaunchKernelGGL((maxpool_strip_kernel<T, 3, 3, 2, 16>), grid, dim3(256), 0, s, p, cols);
+    const dim3 grid((unsigned)((cols + 255) / 256), (unsigned)((p.Ho + POOL_STRIP_RB - 1) / POOL_STRIP_RB));
+    hipLaunchKernelGGL((maxpool_strip_kernel<T, 3, 3, 2, POOL_STRIP_RB>), grid, dim3(256), 0, s, p, cols);
     return;
   }
   int chunks = (P + 255) / 256;
@@ -458,89 +397,63 @@ void launch_add_bcast(const AddParams& p, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Softmax over rows of length D.  One 256-thread block per row: the max is an exact
-// reduction; e = expf(x - max) is written to y; the denominator is formed in the reference's
-// own order (ndarray unrolled_fold: 8 partial sums over chunks of 8, combined (p0+p4),
-// (p1+p5), (p2+p6), (p3+p7), then the tail) by 8 lanes; then y = e / sum.
+// Softmax over rows of length D (softmax_wrapper, softmax_op.rs:45-57): one wavefront per row,
+// no LDS and no barrier.  Lane l owns elements i = 64 k + l (coalesced 256-B row segments).
+//  * max: each lane's running max, then a 6-step xor-shuffle butterfly (exact: max is
+//    order-free).
+//  * denominator in ndarray's unrolled_fold order, exactly: 8 partial sums p_j = e[j] + e[8 + j] +
+//    e[16 + j] + ... folded sequentially over the chunks c < D / 8, combined as
+//    ((p0 + p4) + (p1 + p5)) + (p2 + p6) + (p3 + p7), then the < 8 tail elements in order.  Since 64
+//    is a multiple of 8, element i = 64 k + l of lane l belongs to partial j = l % 8 and chunk
+//    c = 8 k + l / 8.  Per k the wave holds chunks 8k .. 8k+7 in registers; lane l folds partial
+//    l % 8 over them in ascending chunk order, fetching chunk 8k + g's element from lane
+//    8 g + l % 8 by a cross-lane shuffle (ds_bpermute).  Every lane of a partial runs the same
+//    chain, so p_j is the reference's sequential fold, bit for bit given the same exponentials.
+//  * y = e / sum (a division, as `exp_x / &sum_exp_x`); e is kept in y between the passes, re-read
+//    only by the lane that wrote it.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void softmax_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                      int D) {
-  extern __shared__ float ebuf[];  // D exponentials (the 8 summing lanes read them from LDS)
-  __shared__ float red[4];
-  __shared__ float part[8];
-  const long long row = blockIdx.x;
+                                                      long long rows, int D) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;  // wave-uniform; no barrier in this kernel
   const float* xr = x + row * D;
   float* yr = y + row * D;
-  const int tid = threadIdx.x;
 
   float m = -INFINITY;
-  for (int i = tid; i < D; i += 256) m = fmaxf(xr[i], m);
+  for (int i = lane; i < D; i += 64) m = fmaxf(xr[i], m);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-  if ((tid & 63) == 0) red[tid >> 6] = m;
-  __syncthreads();
-  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 
-  for (int i = tid; i < D; i += 256) ebuf[i] = expf(xr[i] - m);
-  __syncthreads();
-  const int nfull = D / 8;
-  if (tid < 8) {
-    float s = 0.0f;
-#pragma unroll 8
-    for (int c = 0; c < nfull; ++c) s = s + ebuf[c * 8 + tid];
-    part[tid] = s;
-  }
-  __syncthreads();
-  float sum = 0.0f;
-  sum = sum + (part[0] + part[4]);
-  sum = sum + (part[1] + part[5]);
-  sum = sum + (part[2] + part[6]);
-  sum = sum + (part[3] + part[7]);
-  for (int i = nfull * 8; i < D; ++i) sum = sum + ebuf[i];
-  for (int i = tid; i < D; i += 256) yr[i] = ebuf[i] / sum;
-}
-
-// rows whose exponentials do not fit the LDS budget: the same order, e staged in y
-__global__ __launch_bounds__(256) void softmax_big_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                          int D) {
-  __shared__ float red[4];
-  __shared__ float part[8];
-  const long long row = blockIdx.x;
-  const float* xr = x + row * D;
-  float* yr = y + row * D;
-  const int tid = threadIdx.x;
-  float m = -INFINITY;
-  for (int i = tid; i < D; i += 256) m = fmaxf(xr[i], m);
+  const int nfull8 = D / 8 * 8;  // elements inside the 8-wide chunks
+  const int j = lane & 7;
+  float s = 0.0f;
+  for (int i0 = 0; i0 < nfull8; i0 += 64) {  // wave-uniform trip count
+    const int i = i0 + lane;
+    float e = 0.0f;
+    if (i < D) {
+      e = expf(xr[i] - m);
+      yr[i] = e;
+    }
+    const float ec = i < nfull8 ? e : 0.0f;  // s + 0 == s: lanes past the chunks add nothing
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-  if ((tid & 63) == 0) red[tid >> 6] = m;
-  __syncthreads();
-  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  for (int i = tid; i < D; i += 256) yr[i] = expf(xr[i] - m);
-  __syncthreads();  // block-scope visibility of yr for the 8 summing lanes
-  const int nfull = D / 8;
-  if (tid < 8) {
-    float s = 0.0f;
-    for (int c = 0; c < nfull; ++c) s = s + yr[c * 8 + tid];
-    part[tid] = s;
+    for (int g = 0; g < 8; ++g) s = s + __shfl(ec, 8 * g + j);
   }
-  __syncthreads();
+  for (int i = (nfull8 + 63) / 64 * 64 + lane; i < D; i += 64) yr[i] = expf(xr[i] - m);  // not yet written
+  const float p0 = __shfl(s, 0), p1 = __shfl(s, 1), p2 = __shfl(s, 2), p3 = __shfl(s, 3);
+  const float p4 = __shfl(s, 4), p5 = __shfl(s, 5), p6 = __shfl(s, 6), p7 = __shfl(s, 7);
   float sum = 0.0f;
-  sum = sum + (part[0] + part[4]);
-  sum = sum + (part[1] + part[5]);
-  sum = sum + (part[2] + part[6]);
-  sum = sum + (part[3] + part[7]);
-  for (int i = nfull * 8; i < D; ++i) sum = sum + yr[i];
-  __syncthreads();
-  for (int i = tid; i < D; i += 256) yr[i] = yr[i] / sum;
+  sum = sum + (p0 + p4);
+  sum = sum + (p1 + p5);
+  sum = sum + (p2 + p6);
+  sum = sum + (p3 + p7);
+  for (int i = nfull8; i < D; ++i) sum = sum + expf(xr[i] - m);  // the tail, in order (same e values)
+  for (int i = lane; i < D; i += 64) yr[i] = yr[i] / sum;
 }
 
 void launch_softmax(const float* x, float* y, long long rows, int D, hipStream_t s) {
   if (rows <= 0) return;
-  if ((size_t)D * 4 <= 48 * 1024)
-    hipLaunchKernelGGL(softmax_kernel, dim3((unsigned)rows), dim3(256), (size_t)D * 4, s, x, y, D);
-  else
-    hipLaunchKernelGGL(softmax_big_kernel, dim3((unsigned)rows), dim3(256), 0, s, x, y, D);
+  hipLaunchKernelGGL(softmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, y, rows, D);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -589,28 +502,6 @@ __global__ __launch_bounds__(256) void gap_kernel(const T* __restrict__ x, float
   }
 }
 
-// f32 rows with 16-B aligned starts (ps % 4 == 0): one row per lane, read by float4 in order, summed
-// sequentially (the same order as gap_kernel); no LDS, 256 rows per block.  Opt-in (ORE_GAP_VEC=1):
-// measured 152 us vs the LDS-staged kernel's 60 us on SqueezeNet's pool10 at B = 256 (64 lanes
-// touching 64 different lines per load)
-__global__ __launch_bounds__(256) void gap_vec_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                      long long rows, int HW, int ps) {
-  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (r >= rows) return;
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  const float* tr = x + r * ps;
-  float s = 0.0f;
-  int i = 0;
-  for (; i + 4 <= HW; i += 4) {
-    const f4 v = *reinterpret_cast<const f4*>(tr + i);
-    s = s + v[0];
-    s = s + v[1];
-    s = s + v[2];
-    s = s + v[3];
-  }
-  for (; i < HW; ++i) s = s + tr[i];
-  y[r] = s / (float)HW;
-}
 
 template <typename T>
 __global__ __launch_bounds__(64) void gap_big_kernel(const T* __restrict__ x, float* __restrict__ y,
@@ -627,10 +518,7 @@ template <typename T>
 static void launch_gap_t(const T* x, float* y, long long rows, int HW, int ps, hipStream_t s) {
   if (rows <= 0) return;
   const size_t lds = (size_t)64 * (HW | 1) * sizeof(float);
-  if (sizeof(T) == 4 && ps % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && env_knob("ORE_GAP_VEC", 0))
-    hipLaunchKernelGGL(gap_vec_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
-                       reinterpret_cast<const float*>(x), y, rows, HW, ps);
-  else if (lds <= 64 * 1024)
+  if (lds <= 64 * 1024)
     hipLaunchKernelGGL(gap_kernel<T>, dim3((unsigned)((rows + 63) / 64)), dim3(256), lds, s, x, y, rows, HW, ps);
   else
     hipLaunchKernelGGL(gap_big_kernel<T>, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, x, y, rows, HW, ps);

@@ -77,7 +77,7 @@ struct Step {
   Window win;
   bool relu = false;
   bool w_kmajor = false;  // MatMul: the constant operand is [K][M]
-  // fused MaxPool (ORE_FUSE_POOL_CONV): in0 is the pool's input; pool geometry below
+  // fused preceding MaxPool (pass pool_squeeze, pool_conv1x1_f32_kernel): in0 is the pool's input
   bool pool = false;
   int64_t pH = 0, pW = 0, psh = 1, psw = 1;
   Window pwin;
@@ -93,7 +93,6 @@ struct Step {
   const float* fire_w3 = nullptr;
   const float* fire_b1 = nullptr;
   const float* fire_b3 = nullptr;
-  bool fire_wino = false;          // the e3 by Winograd (fire_wino_kernel; fire_w3 in launch_fire_pack_wino layout)
   bool fire_f16 = false;           // f16 model: fire_f16_kernel, fire_w1 / fire_w3 / fire_ws16 in launch_fire_pack_f16 layout
   const void* fire_ws16 = nullptr;
   bool fire_pool = false;          // a 3x3 / stride-2 MaxPool between the Concat and this squeeze
@@ -114,14 +113,6 @@ struct Step {
   bool has_wino = false;
   ConvPlan plan_wino{};
   float* wp_wino = nullptr;
-  // (3b) a Winograd step that also computes the 1x1 conv beside it (SqueezeNet's expand1x1 next to
-  // this expand3x3, both writing slices of one Concat): that conv's output value, packed weights
-  // (its own plan's K-major layout), row stride, bias and Relu
-  int e1_out = -1;
-  const float* e1_wp = nullptr;
-  int64_t e1_Mp = 0;
-  const float* e1_b = nullptr;
-  bool e1_relu = false;
   void* xcvt = nullptr;        // f16 F16_X_NHWC_PAIR: the f32 NCHW input converted to NHWC4 f16 (max_batch)
   const float* wc1 = nullptr;  // f32 pooled first conv: weights for pooled-conv variant 7 (launch_pack_c1_f32)
   // f16 pooled first conv with the next 1x1 conv (+ Relu) fused in (conv_pair_pool_f16_kernel SQ):
@@ -132,6 +123,7 @@ struct Step {
   int64_t sq_M = 0;
   int64_t axis = 1;
   double flops_per_img = 0, bytes_per_img = 0, bytes_fixed = 0;
+  double mfma_flops_per_img = -1;  // MFMA FLOPs the kernel issues when they differ from flops (Winograd)
 };
 
 }  // namespace
@@ -142,8 +134,9 @@ struct ore_model {
   int32_t fusion = ORE_FUSE_ALL;
   bool f16 = false;              // ORE_LOAD_F16: f16 conv/pool activations, f32 accumulation
   bool x3 = false;               // ORE_LOAD_X3: f32 convs / MatMuls on the BF16 matrix cores (ore_conv_x3.hip)
-  bool x3_all = false;           // ORE_X3_ALL=1 (tests, experiments): every conv on x3, no f32-MFMA fusions
+  bool x3_all = false;           // ORE_LOAD_X3_ALL: every conv on x3, no f32-MFMA fusions
   bool wino = false;             // f32 model without ORE_LOAD_NO_WINOGRAD: Winograd plans for 3x3 s1 p1 convs
+  int conv_tile = -1;            // the context's forced conv tile at load (ore_ctx_set_conv_tile)
   std::vector<Value> values;
   size_t n_base_values = 0;      // values of the graph; plan() appends views after them (pooled slices)
   std::map<std::string, int> by_name;
@@ -179,16 +172,6 @@ struct ore_model {
 };
 
 namespace {
-
-// operand mode of an f16 conv on the f32 model input: ORE_F16_FIRST=pair|nhwc8|nchw (tuning knob).
-// SqueezeNet conv1 (3 channels, 7x7/s2) at B=256: pair 355 us, nhwc8 498 us (K 392 vs 224), nchw
-// 459 us (per-element gather), conversion included (profiles/r01p_f16_first_conv.txt).
-int f16_first_mode() {
-  const char* e = getenv("ORE_F16_FIRST");
-  if (e && !strcmp(e, "nhwc8")) return F16_X_NHWC8;
-  if (e && !strcmp(e, "nchw")) return F16_X_NCHW32;
-  return F16_X_NHWC_PAIR;
-}
 
 // IEEE binary16 -> binary32 (exact)
 float half_bits_to_float(uint16_t h) {
@@ -517,6 +500,14 @@ ore_status build_node(ore_model* m, const Node& n, Step* s) {
 }
 
 // ------------------------------------------------------------------ fusion + planning
+// plan() rewrites the unfused node steps (base_steps) into the launched plan in passes, each a
+// pattern over the step list that turns a producer -> consumer chain into one kernel step (the
+// consumer steps become S_NOP, the values between them `elided`).  Every fusion is exact: the fused
+// kernels keep each output's arithmetic (same operands, same k order, the max of the same values),
+// so the result of the graph does not depend on which passes ran (tests/test_model_gpu.py checks each
+// against the unfused graph bit for bit).  Pass order matters only where two patterns overlap
+// (fire + pool + squeeze before concat + pool).  Then: algorithm selection (x3, Winograd), aliases,
+// Concat in place, the plane layout, the arena, branch pairs and the gather tables.
 void count_uses(ore_model* m, const std::vector<Step>& steps) {
   for (auto& v : m->values) v.uses = 0;
   for (auto& s : steps)
@@ -539,7 +530,7 @@ bool strided_writer(const Step& s) { return s.kind == S_CONV || s.kind == S_FIRE
 // profiles/r02*_layers*.txt): stride-1 k x k convs on the window-staged kernel (every expand3x3),
 // and 1x1 convs / MatMuls with M >= 256 and K >= 256 (conv10: MFMA-bound).  The other 1x1 convs
 // are HBM-bound, where the f32-MFMA streaming kernels are faster, and the stride-2 7x7 conv1 stays on
-// the f32-MFMA row-walking kernel with pool1 fused.  ORE_X3_ALL=1: every conv.
+// the f32-MFMA row-walking kernel with pool1 fused.  ORE_LOAD_X3_ALL: every conv.
 bool x3_wanted(const ore_model* m, const Step& s) {
   if (m->x3_all) return true;
   if (s.kind == S_MATMUL) return s.M >= 256 && s.C >= 256;
@@ -550,173 +541,159 @@ bool x3_wanted(const ore_model* m, const Step& s) {
          x3w_plan_lds(int(s.win.Ho), int(s.win.Wo), int(s.kh), int(s.kw), int(s.C), 6) <= 80 * 1024;
 }
 
-ore_status plan(ore_model* m) {
-  m->steps = m->base_steps;
-  if (!m->n_base_values) m->n_base_values = m->values.size();
-  m->values.resize(m->n_base_values);  // drop the previous plan's views
-  for (auto& v : m->values) {
-    v.alias_of = -1; v.alias_ch = 0; v.slice = false; v.ps = 0; v.elided = false; v.arena_off = -1;
-    v.nhwc = !v.is_const && v.es == 2 && v.ndim == 4;
-    v.first = v.last = -1;
-  }
-  count_uses(m, m->steps);
-  std::vector<int> producer(m->values.size(), -1);
-  for (size_t i = 0; i < m->steps.size(); ++i)
-    if (m->steps[i].out >= 0 && m->steps[i].kind != S_NOP) producer[m->steps[i].out] = int(i);
+// size heuristics of the fusion passes (measured at batch 256, DESIGN.md sections 3 and 7); ORE_FUSE_EAGER
+// (tests) applies every eligible fusion regardless
+constexpr int64_t FIRE_MIN_COLS = 65536;      // fire fusions: max_batch x H x W >= one 64-pixel wave per SIMD
+constexpr int64_t FIRE_POOL_MIN_HW = 1024;    // fire + pool + squeeze on 54 x 54 planes (at 27 x 27 Winograd wins)
+constexpr int64_t CONCAT_POOL_MIN_HW = 1024;  // concat + pool in the producers: fire4 -40 us, fire8 +21 us
+constexpr int64_t X3_FIRE_MIN_HW = 1024;      // x3 models: the f32 fire kernel beats x3 expand3x3 from 54 x 54
+constexpr double EPOOL_MAX_WORK = 1.25;       // conv + pool patch kernel: recomputed columns <= 1.25 x the conv's
 
-  // (1) Conv -> Relu
-  if (m->fusion & ORE_FUSE_CONV_RELU) {
+struct Planner {
+  ore_model* m;
+  std::vector<int> producer;  // value -> the step that writes it (-1: input / constant)
+  bool eager() const { return (m->fusion & ORE_FUSE_EAGER) != 0; }
+  bool has(int32_t flags) const { return (m->fusion & flags) == flags; }
+  Step& st(int i) { return m->steps[i]; }
+  Value& val(int i) { return m->values[i]; }
+  // the first launched step at or after `from` that reads v (in0 or in1)
+  int reader(int v, size_t from) const {
+    for (size_t j = from; j < m->steps.size(); ++j)
+      if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == v || m->steps[j].in1 == v)) return int(j);
+    return -1;
+  }
+  // a value read once, not the graph output: free to elide
+  bool private_value(int v) const { return m->values[v].uses == 1 && !m->values[v].is_output; }
+  void nop(Step& s) {
+    s.kind = S_NOP;
+    s.in0 = s.in1 = -1;
+  }
+  void recount() { count_uses(m, m->steps); }
+  // a plain f32 1x1 conv (+ Relu) on the direct kernels, output the size of its input
+  static bool plain_1x1(const Step& s) {
+    return s.kind == S_CONV && s.relu && !s.pool && !s.epool && !s.plan.f16 && s.kh == 1 && s.kw == 1 && s.sh == 1 &&
+           s.sw == 1 && s.win.pt == 0 && s.win.pl == 0 && s.win.Ho == s.H && s.win.Wo == s.W;
+  }
+  // an f32 3x3 / stride-1 'same' conv (+ Relu) on the direct kernels
+  static bool same_3x3(const Step& s) {
+    return s.kind == S_CONV && s.relu && !s.pool && !s.epool && !s.plan.f16 && s.kh == 3 && s.kw == 3 && s.sh == 1 &&
+           s.sw == 1 && s.win.pt == 1 && s.win.pl == 1 && s.win.Ho == s.H && s.win.Wo == s.W;
+  }
+  // a weight packing made once per model (fire_packs[key]); false on an allocation failure
+  template <class F>
+  bool pack_once(int key, size_t bytes, F launch) {
+    if (m->fire_packs.count(key)) return true;
+    float* buf = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&buf), bytes) != hipSuccess) return false;
+    launch(buf);
+    m->fire_packs[key] = buf;
+    return hipGetLastError() == hipSuccess && hipStreamSynchronize(m->ctx->stream) == hipSuccess;
+  }
+  // the fire modules: Concat step i of two producers (e1 a 1x1, e3 a 3x3 'same' conv of one value S)
+  bool fire_concat(int i, int* pa, int* pb) {
+    const Step& cc = st(i);
+    if (cc.kind != S_CONCAT || cc.axis != 1 || cc.in0 < 0 || cc.in1 < 0 || cc.in0 == cc.in1) return false;
+    *pa = producer[cc.in0];
+    *pb = producer[cc.in1];
+    return *pa >= 0 && *pb >= 0 && *pa != *pb;
+  }
+
+  // (1) Conv -> Relu: the Relu in the conv epilogue
+  void conv_relu() {
+    if (!has(ORE_FUSE_CONV_RELU)) return;
     for (size_t i = 0; i < m->steps.size(); ++i) {
-      Step& r = m->steps[i];
+      Step& r = st(int(i));
       if (r.kind != S_RELU) continue;
-      int v = r.in0;
-      int p = producer[v];
-      if (p < 0 || m->steps[p].kind != S_CONV || m->steps[p].relu) continue;
-      if (m->values[v].uses != 1 || m->values[v].is_output) continue;
-      m->steps[p].out = r.out;
-      m->steps[p].relu = true;
-      m->values[v].elided = true;
+      const int v = r.in0, p = producer[v];
+      if (p < 0 || st(p).kind != S_CONV || st(p).relu || !private_value(v)) continue;
+      st(p).out = r.out;
+      st(p).relu = true;
+      val(v).elided = true;
       producer[r.out] = p;
-      r.kind = S_NOP;
-      r.in0 = -1;
+      nop(r);
     }
-    count_uses(m, m->steps);
+    recount();
   }
-  // (1b) 3x3 MaxPool -> its only consumer, a plain 1x1 Conv: the pool runs in the conv's gather
-  if ((m->fusion & ORE_FUSE_POOL_CONV) && !m->f16 && !m->x3_all) {
+
+  // (2) Conv (-> Relu) -> MaxPool, the conv output read by the pool only: one launch when the
+  // recomputed patch costs <= EPOOL_MAX_WORK x the conv's columns (f32 and f16 models)
+  ore_status conv_pool() {
+    if (!has(ORE_FUSE_CONV_POOL) || m->x3_all) return ORE_OK;
     for (size_t i = 0; i < m->steps.size(); ++i) {
-      Step& pl = m->steps[i];
-      if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3) continue;
-      const int v = pl.out;
-      if (m->values[v].uses != 1 || m->values[v].is_output) continue;
-      int ci = -1;
-      for (size_t j = i + 1; j < m->steps.size(); ++j)
-        if (m->steps[j].kind != S_NOP && m->steps[j].in0 == v) { ci = int(j); break; }
-      if (ci < 0) continue;
-      Step& cv = m->steps[ci];
-      if (cv.kind != S_CONV || cv.pool || cv.kh != 1 || cv.kw != 1 || cv.sh != 1 || cv.sw != 1 || cv.win.pt != 0 ||
-          cv.win.pl != 0 || cv.win.Ho != cv.H || cv.win.Wo != cv.W || cv.plan.window)
-        continue;
-      cv.pool = true;
-      cv.in0 = pl.in0;
-      cv.pH = pl.H; cv.pW = pl.W; cv.psh = pl.sh; cv.psw = pl.sw; cv.pwin = pl.win;
-      m->values[v].elided = true;
-      pl.kind = S_NOP;
-      pl.in0 = -1;
-    }
-    count_uses(m, m->steps);
-  }
-  // (1c) Conv (-> Relu) -> MaxPool, the conv output read by the pool only: one launch when the
-  // recomputed patch costs <= ORE_EPOOL_MAX_WORK x the conv's columns (f32 and f16 models)
-  if (m->fusion & ORE_FUSE_CONV_POOL) {
-    const char* e = getenv("ORE_EPOOL_MAX_WORK");  // tuning knob
-    const double max_work = e ? atof(e) : 1.25;
-    for (size_t i = 0; i < m->steps.size(); ++i) {
-      Step& pl = m->steps[i];
+      Step& pl = st(int(i));
       if (pl.kind != S_MAXPOOL) continue;
-      const int v = pl.in0;
-      const int pc = producer[v];
-      if (pc < 0 || m->values[v].uses != 1 || m->values[v].is_output) continue;
-      Step& cv = m->steps[pc];
-      if (cv.kind != S_CONV || cv.pool || cv.epool || cv.plan.window || m->x3_all) continue;
-      if (cv.plan.f16 != (m->values[pl.out].es == 2 ? 1 : 0)) continue;  // f16 conv -> f16 pool only
+      const int v = pl.in0, pc = producer[v];
+      if (pc < 0 || !private_value(v)) continue;
+      Step& cv = st(pc);
+      if (cv.kind != S_CONV || cv.pool || cv.epool) continue;
+      if (cv.plan.f16 != (val(pl.out).es == 2 ? 1 : 0)) continue;  // f16 conv -> f16 pool only
       int a = 0, b = 0;
       const double work = epool_tile(cv.win.Ho, cv.win.Wo, pl.kh, pl.kw, pl.sh, pl.sw, pl.win, &a, &b);
-      if (work == 0.0 || work > max_work) continue;
+      if (work == 0.0 || (work > EPOOL_MAX_WORK && !eager())) continue;
       cv.epool = true;
       cv.out = pl.out;
       // f32: pack the weights for the window kernel (pooled-conv variant 7) when its geometry fits
       if (!cv.plan.f16 && cv.kh == 7 && cv.kw == 7 && cv.sh == 2 && cv.sw == 2 && cv.in1 >= 0 &&
           (cv.C == 1 || cv.C == 3 || cv.C == 4) && cv.M > 32 && cv.M <= 128) {
-        const int key = 4000000 + pc;
-        if (!m->fire_packs.count(key)) {
-          float* buf = nullptr;
-          const int K = int(cv.C * cv.kh * cv.kw);
-          if (hipMalloc(reinterpret_cast<void**>(&buf), c1_f32_pack_bytes(int(cv.M), K)) != hipSuccess)
-            return err(m, ORE_ERR_OOM, "conv weight packing allocation failed");
-          launch_pack_c1_f32(m->values[cv.in1].cptr, int(cv.M), K, buf, m->ctx->stream);
-          if (hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
-            return err(m, ORE_ERR_HIP, "conv weight packing failed");
-          m->fire_packs[key] = buf;
-        }
+        const int key = 4000000 + pc, K = int(cv.C * cv.kh * cv.kw), M = int(cv.M);
+        const float* w = val(cv.in1).cptr;
+        if (!pack_once(key, c1_f32_pack_bytes(M, K), [&](float* buf) { launch_pack_c1_f32(w, M, K, buf, m->ctx->stream); }))
+          return err(m, ORE_ERR_HIP, "conv weight packing failed");
         cv.wc1 = m->fire_packs[key];
       }
       cv.ep_kh = pl.kh; cv.ep_kw = pl.kw; cv.ep_sh = pl.sh; cv.ep_sw = pl.sw; cv.ep_win = pl.win;
       // algorithmic bytes: the conv's input + the pooled output (the pre-pool tensor never moves)
-      cv.bytes_per_img = double(m->values[cv.in0].es) * double(cv.C * cv.H * cv.W) +
-                         double(m->values[pl.out].es) * double(cv.M * pl.win.Ho * pl.win.Wo);
-      m->values[v].elided = true;
+      cv.bytes_per_img = double(val(cv.in0).es) * double(cv.C * cv.H * cv.W) +
+                         double(val(pl.out).es) * double(cv.M * pl.win.Ho * pl.win.Wo);
+      val(v).elided = true;
       producer[pl.out] = pc;
-      pl.kind = S_NOP;
-      pl.in0 = -1;
+      nop(pl);
     }
-    count_uses(m, m->steps);
+    recount();
+    return ORE_OK;
   }
-  // (1k) f32 fire module -> 3x3 / stride-2 MaxPool -> the next squeeze in one fire_pool_kernel launch
+
+  // (3) f32 fire module -> 3x3 / stride-2 MaxPool -> the next squeeze in one fire_pool_kernel launch
   // (ore_fire.hip): Concat(e1 1x1, e3 3x3 'same') (+ Relu), the pool the Concat's only reader, the
-  // squeeze (1x1 + Relu, <= 64 channels) the pool's only reader.  Bit-identical to the pooled-epilogue
-  // expands + the separate squeeze.  For expand planes of >= ORE_FIRE_POOL_MIN_HW pixels (default
-  // 1024: SqueezeNet's fire4 -> pool3 -> fire5; at 27 x 27 fire8's expand3x3 runs Winograd, cheaper
-  // than the direct K loop) and batches of >= ORE_FIRE_MIN_COLS columns, as (1d); ORE_FIRE_POOL=0
-  // turns it off.  Runs before the concat-pool pass below.
-  if ((m->fusion & ORE_FUSE_FIRE) && (m->fusion & ORE_FUSE_CONV_POOL) && (m->fusion & ORE_FUSE_CONV_RELU) &&
-      (m->fusion & ORE_FUSE_CONCAT) && !m->f16 && !m->x3_all) {
-    const char* efp = getenv("ORE_FIRE_POOL");
-    const char* emh = getenv("ORE_FIRE_POOL_MIN_HW");
-    const int64_t min_hw = emh ? atoll(emh) : 1024;
-    const char* emc = getenv("ORE_FIRE_MIN_COLS");  // as (1d): small batches keep the walkers (tests set 0)
-    const int64_t min_cols = emc ? atoll(emc) : 65536;
-    for (size_t i = 0; i < m->steps.size() && !(efp && atoi(efp) == 0); ++i) {
-      Step& cc = m->steps[i];
-      if (cc.kind != S_CONCAT || cc.axis != 1 || cc.in0 < 0 || cc.in1 < 0 || cc.in0 == cc.in1) continue;
-      const int pa = producer[cc.in0], pb = producer[cc.in1];
-      if (pa < 0 || pb < 0 || pa == pb) continue;
-      auto consumer = [&](int v, size_t from) {
-        for (size_t j = from; j < m->steps.size(); ++j)
-          if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == v || m->steps[j].in1 == v)) return int(j);
-        return -1;
-      };
-      const int pi = consumer(cc.out, i + 1);
+  // squeeze (1x1 + Relu, <= 64 channels) the pool's only reader.  Expand planes of >= FIRE_POOL_MIN_HW
+  // pixels (SqueezeNet's fire4 -> pool3 -> fire5; at 27 x 27 fire8's expand3x3 runs Winograd, cheaper
+  // than the direct K loop).  Runs before concat_pool, which would otherwise take the pattern.
+  ore_status fire_pool_f32() {
+    if (!has(ORE_FUSE_FIRE_POOL | ORE_FUSE_CONV_RELU | ORE_FUSE_CONCAT) || m->f16 || m->x3_all) return ORE_OK;
+    for (size_t i = 0; i < m->steps.size(); ++i) {
+      int pa, pb;
+      if (!fire_concat(int(i), &pa, &pb)) continue;
+      Step& cc = st(int(i));
+      const int pi = reader(cc.out, i + 1);
       if (pi < 0) continue;
-      Step& pl = m->steps[pi];
+      Step& pl = st(pi);
       if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2 || pl.in0 != cc.out) continue;
-      const int qi = consumer(pl.out, size_t(pi) + 1);
+      const int qi = reader(pl.out, size_t(pi) + 1);
       if (qi < 0) continue;
-      Step &e1 = m->steps[pa], &e3 = m->steps[pb], &q = m->steps[qi];
-      auto is1x1 = [](const Step& s) {
-        return s.kind == S_CONV && s.relu && !s.pool && !s.epool && !s.plan.window && !s.plan.f16 && s.kh == 1 &&
-               s.kw == 1 && s.sh == 1 && s.sw == 1 && s.win.pt == 0 && s.win.pl == 0 && s.win.Ho == s.H && s.win.Wo == s.W;
-      };
-      const bool e3ok = e3.kind == S_CONV && e3.relu && !e3.pool && !e3.epool && !e3.plan.window && !e3.plan.f16 &&
-                        e3.kh == 3 && e3.kw == 3 && e3.sh == 1 && e3.sw == 1 && e3.win.pt == 1 && e3.win.pl == 1 &&
-                        e3.win.Ho == e3.H && e3.win.Wo == e3.W;
-      if (!is1x1(e1) || !e3ok || !is1x1(q) || q.in0 != pl.out || e1.in0 != e3.in0 || e1.H != e3.H || e1.W != e3.W) continue;
+      Step &e1 = st(pa), &e3 = st(pb), &q = st(qi);
+      if (!plain_1x1(e1) || !same_3x3(e3) || !plain_1x1(q) || q.in0 != pl.out || e1.in0 != e3.in0 || e1.H != e3.H ||
+          e1.W != e3.W)
+        continue;
       if (e1.M % 64 || e3.M % 64 || q.M > 64 || e1.C % 16 || q.C != e1.M + e3.M || pl.H != e1.H || pl.W != e1.W) continue;
-      if (e1.H * e1.W < min_hw || m->max_batch * e1.H * e1.W < min_cols || q.in2 < 0 || e1.in2 < 0 || e3.in2 < 0) continue;
-      if (padded_plane(e1.H * e1.W) % 4) continue;  // 16-B input planes (layout below)
+      if (!eager() && (e1.H * e1.W < FIRE_POOL_MIN_HW || m->max_batch * e1.H * e1.W < FIRE_MIN_COLS)) continue;
+      if (q.in2 < 0 || e1.in2 < 0 || e3.in2 < 0 || padded_plane(e1.H * e1.W) % 4) continue;  // 16-B input planes
       FireParams fp{};
       fp.H = int(e1.H); fp.W = int(e1.W);
       fp.Hp = int(pl.win.Ho); fp.Wp = int(pl.win.Wo); fp.ppt = int(pl.win.pt); fp.ppl = int(pl.win.pl);
       if (!fire_pool_plan(&fp) || fp.ppt > 2 || fp.ppl > 2 || 2 * (fp.Hp - 1) - fp.ppt >= fp.H ||
           2 * (fp.Wp - 1) - fp.ppl >= fp.W)
         continue;
-      const Value &va = m->values[cc.in0], &vb = m->values[cc.in1], &vc = m->values[cc.out], &vs = m->values[e1.in0];
-      const Value& vp = m->values[pl.out];
-      if (va.uses != 1 || vb.uses != 1 || vc.uses != 1 || vp.uses != 1 || va.is_output || vb.is_output ||
-          vc.is_output || vp.is_output || vs.es != 4)
+      if (!private_value(cc.in0) || !private_value(cc.in1) || !private_value(cc.out) || !private_value(pl.out) ||
+          val(e1.in0).es != 4)
         continue;
-      bool packed_ok = true;  // the fire kernel's row-permuted expand packings (shared with (1d): key = step index)
-      for (int idx : {pa, pb}) {
-        if (m->fire_packs.count(idx)) continue;
-        const Step& e = m->steps[idx];
+      for (int idx : {pa, pb}) {  // the fire kernel's row-permuted expand packings (shared with fire_f32)
+        const Step& e = st(idx);
         const int64_t K = e.C * e.kh * e.kw, Kp = (K + 31) / 32 * 32;
-        float* buf = nullptr;
-        if (hipMalloc(reinterpret_cast<void**>(&buf), size_t(Kp * e.M) * 4) != hipSuccess) { packed_ok = false; break; }
-        launch_fire_pack(m->values[e.in1].cptr, int(e.M), int(K), buf, m->ctx->stream);
-        m->fire_packs[idx] = buf;
+        const float* w = val(e.in1).cptr;
+        if (!pack_once(idx, size_t(Kp * e.M) * 4,
+                       [&](float* buf) { launch_fire_pack(w, int(e.M), int(K), buf, m->ctx->stream); }))
+          return err(m, ORE_ERR_HIP, "fire weight packing failed");
       }
-      if (!packed_ok || hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
-        return err(m, ORE_ERR_HIP, "fire weight packing failed");
       q.kind = S_FIRE;
       q.fire_pool = true;
       q.fire_H = e1.H;
@@ -728,198 +705,146 @@ ore_status plan(ore_model* m) {
       q.fire_E3 = e3.M;
       q.fire_w1 = m->fire_packs[pa];
       q.fire_w3 = m->fire_packs[pb];
-      q.fire_b1 = m->values[e1.in2].cptr;
-      q.fire_b3 = m->values[e3.in2].cptr;
+      q.fire_b1 = val(e1.in2).cptr;
+      q.fire_b3 = val(e3.in2).cptr;
       q.flops_per_img += e1.flops_per_img + e3.flops_per_img;
       q.bytes_per_img = 4.0 * double(e1.C * e1.H * e1.W) + 4.0 * double(q.M * q.H * q.W);
       q.name = e1.name.substr(0, e1.name.find('/')) + "+pool+" + q.name;
-      m->values[cc.in0].elided = m->values[cc.in1].elided = m->values[cc.out].elided = m->values[pl.out].elided = true;
-      e1.kind = e3.kind = cc.kind = pl.kind = S_NOP;
-      e1.in0 = e3.in0 = cc.in0 = cc.in1 = pl.in0 = -1;
+      val(cc.in0).elided = val(cc.in1).elided = val(cc.out).elided = val(pl.out).elided = true;
+      nop(e1); nop(e3); nop(cc); nop(pl);
     }
-    count_uses(m, m->steps);
+    recount();
+    return ORE_OK;
   }
-  // (1e) Concat(e1, e3) -> 3x3 / stride-2 MaxPool, e1 / e3 Convs (+ Relu) read only by the Concat
-  // (f32; SqueezeNet's fire4 -> pool3 and fire8 -> pool5): each conv's pooled epilogue writes its
-  // channel slice of the pool output (a view appended to the values), so neither the two conv
-  // outputs nor the concat reach HBM.  The MaxPool of a Concat is the Concat of the per-slice
-  // MaxPools (the pool is per channel), so every pooled value is the same max of the same nine
-  // values.  No patch-work bound: the row-walking kernels (ore_conv_pool.hip) compute no conv output
-  // twice, and ore_model_autotune keeps the patch kernel only where it is faster.  On by default
-  // (ORE_FUSE_CONCAT_POOL is in ORE_FUSE_ALL) for pooled planes of >= 1024 pixels, i.e. fire4 ->
-  // pool3 (-40 us per B=256 step); fire8 -> pool5 (27^2 planes) stays unfused, measured slower
-  // (DESIGN.md section 9).
-  if ((m->fusion & ORE_FUSE_CONCAT_POOL) && (m->fusion & ORE_FUSE_CONV_POOL) && (m->fusion & ORE_FUSE_CONCAT) &&
-      !m->f16 && !m->x3_all) {
+
+  // (4) Concat(e1, e3) -> 3x3 / stride-2 MaxPool, e1 / e3 Convs (+ Relu) read only by the Concat (f32):
+  // each conv's pooled epilogue writes its channel slice of the pool output (a view appended to the
+  // values), so neither the two conv outputs nor the concat reach HBM.  The MaxPool of a Concat is the
+  // Concat of the per-slice MaxPools (the pool is per channel).  Conv planes of >= CONCAT_POOL_MIN_HW.
+  void concat_pool() {
+    if (!has(ORE_FUSE_CONCAT_POOL | ORE_FUSE_CONV_POOL | ORE_FUSE_CONCAT) || m->f16 || m->x3_all) return;
     for (size_t i = 0; i < m->steps.size(); ++i) {
-      Step& pl = m->steps[i];
+      Step& pl = st(int(i));
       if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2) continue;
-      const int cv = pl.in0;
-      const int ci = producer[cv];
-      if (ci < 0 || m->values[cv].uses != 1 || m->values[cv].is_output || m->values[pl.out].is_output) continue;
-      Step& cc = m->steps[ci];
-      if (cc.kind != S_CONCAT || cc.axis != 1 || cc.in0 < 0 || cc.in1 < 0 || cc.in0 == cc.in1) continue;
-      const int pa = producer[cc.in0], pb = producer[cc.in1];
-      if (pa < 0 || pb < 0 || pa == pb) continue;
-      auto ok = [&](const Step& st, int v) {
-        return st.kind == S_CONV && st.relu && !st.pool && !st.epool && !st.plan.window && !st.plan.f16 &&
-               m->values[v].uses == 1 && !m->values[v].is_output && m->values[v].ndim == 4;
+      const int cv = pl.in0, ci = producer[cv];
+      if (ci < 0 || !private_value(cv) || val(pl.out).is_output) continue;
+      int pa, pb;
+      if (!fire_concat(ci, &pa, &pb)) continue;
+      Step& cc = st(ci);
+      auto ok = [&](const Step& s, int v) {
+        return s.kind == S_CONV && s.relu && !s.pool && !s.epool && !s.plan.f16 && private_value(v) && val(v).ndim == 4;
       };
-      if (!ok(m->steps[pa], cc.in0) || !ok(m->steps[pb], cc.in1)) continue;
+      if (!ok(st(pa), cc.in0) || !ok(st(pb), cc.in1)) continue;
       int t1 = 0, t2 = 0;
-      const Step& sa = m->steps[pa];
+      const Step& sa = st(pa);
       if (epool_tile(sa.win.Ho, sa.win.Wo, pl.kh, pl.kw, pl.sh, pl.sw, pl.win, &t1, &t2) == 0.0) continue;
-      // planes below ORE_CONCAT_POOL_MIN_HW (environment, default 1024) pixels keep the separate pool:
-      // measured at batch 256, fire4 (54 x 54) -40 us, fire8 (27 x 27) +21 us per step
-      const char* mh = getenv("ORE_CONCAT_POOL_MIN_HW");
-      const int64_t min_hw = mh ? atoll(mh) : 1024;
-      if (sa.win.Ho * sa.win.Wo < min_hw) continue;
+      if (sa.win.Ho * sa.win.Wo < CONCAT_POOL_MIN_HW && !eager()) continue;
       const int pout = pl.out;
-      const int64_t Hp = m->values[pout].dims[2], Wp = m->values[pout].dims[3];
-      const int pes = m->values[pout].es;
-      const std::string pname = m->values[pout].name;
+      const int64_t Hp = val(pout).dims[2], Wp = val(pout).dims[3];
+      const int pes = val(pout).es;
+      const std::string pname = val(pout).name;
       int64_t ch0 = 0;
       for (int half = 0; half < 2; ++half) {
         const int si = half ? pb : pa, src = half ? cc.in1 : cc.in0;
         Value v;
         v.name = pname + (half ? "#slice1" : "#slice0");
         v.ndim = 4;
-        v.dims[0] = 1; v.dims[1] = m->values[src].dims[1]; v.dims[2] = Hp; v.dims[3] = Wp;
+        v.dims[0] = 1; v.dims[1] = val(src).dims[1]; v.dims[2] = Hp; v.dims[3] = Wp;
         v.es = pes;
         v.alias_of = pout; v.alias_ch = ch0; v.slice = true;
         ch0 += v.dims[1];
         m->values.push_back(v);
         producer.push_back(si);
         const int vid = int(m->values.size()) - 1;
-        Step& st = m->steps[si];
-        m->values[src].elided = true;
-        st.epool = true;
-        st.out = vid;
-        st.ep_kh = pl.kh; st.ep_kw = pl.kw; st.ep_sh = pl.sh; st.ep_sw = pl.sw; st.ep_win = pl.win;
-        st.bytes_per_img = double(m->values[st.in0].es) * double(st.C * st.H * st.W) +
-                           double(pes) * double(st.M * Hp * Wp);
+        Step& s = st(si);
+        val(src).elided = true;
+        s.epool = true;
+        s.out = vid;
+        s.ep_kh = pl.kh; s.ep_kw = pl.kw; s.ep_sh = pl.sh; s.ep_sw = pl.sw; s.ep_win = pl.win;
+        s.bytes_per_img = double(val(s.in0).es) * double(s.C * s.H * s.W) + double(pes) * double(s.M * Hp * Wp);
       }
-      m->values[cv].elided = true;
+      val(cv).elided = true;
       producer[pout] = pa;
-      cc.kind = S_NOP; cc.in0 = cc.in1 = -1;
-      pl.kind = S_NOP; pl.in0 = -1;
+      nop(cc);
+      nop(pl);
     }
-    count_uses(m, m->steps);
+    recount();
   }
-  // (1d) fire module + the next squeeze in one launch (ORE_FUSE_FIRE, f32): Concat(e1, e3) whose
-  // inputs are a 1x1 and a 3x3 'same' Conv (+ Relu) of one value S, read only by a 1x1 Conv (+ Relu)
-  // with at most 64 output channels
-  if ((m->fusion & ORE_FUSE_FIRE) && !m->f16 && !m->x3_all && (m->fusion & ORE_FUSE_CONV_RELU)) {
-    const char* e = getenv("ORE_FIRE_MIN_COLS");  // tuning knob (tests set 0)
-    const int64_t min_cols = e ? atoll(e) : 65536;
-    // x3 models: the f32-MFMA fire kernel only where it beats the x3 expand3x3 + separate 1x1s
-    // (planes of >= ORE_X3_FIRE_MIN_HW pixels, default 1024: SqueezeNet's 54 x 54 fire2 / fire3;
-    // at 27 x 27 the x3 expand3x3 wins)
-    const char* ex = getenv("ORE_X3_FIRE_MIN_HW");
-    const int64_t x3_fire_min_hw = ex ? atoll(ex) : 1024;
+
+  // (5) fire module + the next squeeze in one launch (f32, fire_kernel): Concat(e1, e3) whose inputs
+  // are a 1x1 and a 3x3 'same' Conv (+ Relu) of one value S, read only by a 1x1 Conv (+ Relu) with at
+  // most 64 output channels
+  ore_status fire_f32() {
+    if (!has(ORE_FUSE_FIRE | ORE_FUSE_CONV_RELU | ORE_FUSE_CONCAT) || m->f16 || m->x3_all) return ORE_OK;
     for (size_t i = 0; i < m->steps.size(); ++i) {
-      Step& cc = m->steps[i];
-      if (cc.kind != S_CONCAT || cc.axis != 1 || cc.in0 < 0 || cc.in1 < 0 || cc.in0 == cc.in1) continue;
-      const int pa = producer[cc.in0], pb = producer[cc.in1];
-      if (pa < 0 || pb < 0) continue;
-      int qi = -1;
-      for (size_t j = i + 1; j < m->steps.size(); ++j)
-        if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == cc.out || m->steps[j].in1 == cc.out)) { qi = int(j); break; }
+      int pa, pb;
+      if (!fire_concat(int(i), &pa, &pb)) continue;
+      Step& cc = st(int(i));
+      const int qi = reader(cc.out, i + 1);
       if (qi < 0) continue;
-      Step &e1 = m->steps[pa], &e3 = m->steps[pb], &q = m->steps[qi];
-      auto is1x1 = [](const Step& s) {
-        return s.kind == S_CONV && s.relu && !s.pool && !s.epool && !s.plan.window && !s.plan.f16 && s.kh == 1 &&
-               s.kw == 1 && s.sh == 1 && s.sw == 1 && s.win.pt == 0 && s.win.pl == 0 && s.win.Ho == s.H && s.win.Wo == s.W;
-      };
-      const bool e3ok = e3.kind == S_CONV && e3.relu && !e3.pool && !e3.epool && !e3.plan.window && !e3.plan.f16 &&
-                        e3.kh == 3 && e3.kw == 3 && e3.sh == 1 && e3.sw == 1 && e3.win.pt == 1 && e3.win.pl == 1 &&
-                        e3.win.Ho == e3.H && e3.win.Wo == e3.W;
-      if (!is1x1(e1) || !e3ok || !is1x1(q) || q.in0 != cc.out || e1.in0 != e3.in0 || e1.H != e3.H || e1.W != e3.W) continue;
+      Step &e1 = st(pa), &e3 = st(pb), &q = st(qi);
+      if (!plain_1x1(e1) || !same_3x3(e3) || !plain_1x1(q) || q.in0 != cc.out || e1.in0 != e3.in0 || e1.H != e3.H ||
+          e1.W != e3.W)
+        continue;
       if (e1.M % 64 || e3.M % 64 || q.M > 64 || e1.C % 16 || q.C != e1.M + e3.M) continue;
-      if (m->max_batch * e1.H * e1.W < min_cols) continue;
-      if (m->x3 && e3.has_x3 && e1.H * e1.W < x3_fire_min_hw) continue;
-      if (padded_plane(e1.H * e1.W) % 4 || (m->fusion & ORE_FUSE_CONCAT) == 0) continue;  // 16-B planes (layout below)
-      const Value &va = m->values[cc.in0], &vb = m->values[cc.in1], &vc = m->values[cc.out], &vs = m->values[e1.in0];
-      if (va.uses != 1 || vb.uses != 1 || vc.uses != 1 || va.is_output || vb.is_output || vc.is_output || vs.es != 4) continue;
-      // Winograd e3 (f32 models with Winograd on; the fire_wino_kernel's limits): bit-identical to the
-      // unfused graph, whose expand3x3 runs Winograd too
-      // Off by default: measured slower than the direct fire kernel on every SqueezeNet module
-      // (fire_wino_kernel runs one wave per SIMD and is vector-memory bound on the e3 operands,
-      // DESIGN.md section 3.3); ORE_FIRE_WINO=1 turns it on (tests, experiments)
-      const char* efw = getenv("ORE_FIRE_WINO");
-      const bool fw = efw && atoi(efw) != 0 && m->wino && e3.has_wino && e1.C <= 64 && e3.M % 32 == 0;
-      // the expand weights in the fire kernel's row-permuted packing (made once per model; key -1 - idx:
-      // the Winograd e3 packing)
-      bool packed_ok = true;
+      if (!eager() && m->max_batch * e1.H * e1.W < FIRE_MIN_COLS) continue;
+      // x3 models: the f32-MFMA fire kernel only where it beats the x3 expand3x3 + separate 1x1s
+      if (m->x3 && e3.has_x3 && e1.H * e1.W < X3_FIRE_MIN_HW && !eager()) continue;
+      if (padded_plane(e1.H * e1.W) % 4) continue;  // 16-B planes (layout below)
+      if (!private_value(cc.in0) || !private_value(cc.in1) || !private_value(cc.out) || val(e1.in0).es != 4) continue;
+      if (e1.in2 < 0 || e3.in2 < 0 || q.in2 < 0) continue;
       for (int idx : {pa, pb}) {
-        const bool wpack = fw && idx == pb;
-        const int key = wpack ? -1 - idx : idx;
-        if (m->fire_packs.count(key)) continue;
-        const Step& e = m->steps[idx];
+        const Step& e = st(idx);
         const int64_t K = e.C * e.kh * e.kw, Kp = (K + 31) / 32 * 32;
-        const size_t bytes = wpack ? size_t(e.C * e.M * 16) * 4 : size_t(Kp * e.M) * 4;
-        float* buf = nullptr;
-        if (hipMalloc(reinterpret_cast<void**>(&buf), bytes) != hipSuccess) { packed_ok = false; break; }
-        if (wpack) launch_fire_pack_wino(m->values[e.in1].cptr, int(e.M), int(e.C), buf, m->ctx->stream);
-        else launch_fire_pack(m->values[e.in1].cptr, int(e.M), int(K), buf, m->ctx->stream);
-        m->fire_packs[key] = buf;
+        const float* w = val(e.in1).cptr;
+        if (!pack_once(idx, size_t(Kp * e.M) * 4,
+                       [&](float* buf) { launch_fire_pack(w, int(e.M), int(K), buf, m->ctx->stream); }))
+          return err(m, ORE_ERR_HIP, "fire weight packing failed");
       }
-      if (!packed_ok || hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
-        return err(m, ORE_ERR_HIP, "fire weight packing failed");
       q.kind = S_FIRE;
       q.in0 = e1.in0;
       q.fire_C = e1.C;
       q.fire_E1 = e1.M;
       q.fire_E3 = e3.M;
       q.fire_w1 = m->fire_packs[pa];
-      q.fire_w3 = m->fire_packs[fw ? -1 - pb : pb];
-      q.fire_wino = fw;
-      q.fire_b1 = e1.in2 >= 0 ? m->values[e1.in2].cptr : nullptr;
-      q.fire_b3 = e3.in2 >= 0 ? m->values[e3.in2].cptr : nullptr;
-      if (!q.fire_b1 || !q.fire_b3 || q.in2 < 0) return err(m, ORE_ERR_UNSUPPORTED, "fused fire needs conv biases");
+      q.fire_w3 = m->fire_packs[pb];
+      q.fire_b1 = val(e1.in2).cptr;
+      q.fire_b3 = val(e3.in2).cptr;
       q.flops_per_img += e1.flops_per_img + e3.flops_per_img;
       q.bytes_per_img = 4.0 * double(e1.C * e1.H * e1.W) + 4.0 * double(q.M * q.H * q.W);
       q.name = e1.name.substr(0, e1.name.find('/')) + "+" + q.name;
-      m->values[cc.in0].elided = m->values[cc.in1].elided = m->values[cc.out].elided = true;
-      e1.kind = e3.kind = cc.kind = S_NOP;
-      e1.in0 = e3.in0 = cc.in0 = cc.in1 = -1;
+      val(cc.in0).elided = val(cc.in1).elided = val(cc.out).elided = true;
+      nop(e1); nop(e3); nop(cc);
     }
-    count_uses(m, m->steps);
+    recount();
+    return ORE_OK;
   }
-  // (1e) f16 models: the same fire module + next squeeze pattern in one fire_f16_kernel launch
+
+  // (6) f16 models: the same fire module + next squeeze pattern in one fire_f16_kernel launch
   // (ore_fire_f16.hip): expand1x1 / expand3x3 (+ Relu) on 16-B NHWC gathers, C % 16 == 0 and <= 64,
   // expands in 32-channel chunks, the squeeze <= 64 channels; bit-identical to the three
   // conv_f16_kernel launches.  With a 3x3 / stride-2 MaxPool between the Concat and the squeeze
   // (SqueezeNet fire4 -> pool3 -> fire5, fire8 -> pool5 -> fire9) the pooled kernel takes all four
-  // steps (bit-identical to the three convs + maxpool_nhwc_kernel)
-  if ((m->fusion & ORE_FUSE_FIRE) && m->f16 && (m->fusion & ORE_FUSE_CONV_RELU)) {
-    // the pooled form (fire_pool_f16_kernel) also needs ORE_FUSE_CONV_POOL; ORE_FIRE_POOL=0 turns it off
-    const char* efp = getenv("ORE_FIRE_POOL");
-    const bool fire_pool = (m->fusion & ORE_FUSE_CONV_POOL) && !(efp && atoi(efp) == 0);
+  // steps (ORE_FUSE_FIRE_POOL; bit-identical to the three convs + maxpool_nhwc_kernel)
+  ore_status fire_f16() {
+    if (!has(ORE_FUSE_FIRE | ORE_FUSE_CONV_RELU) || !m->f16) return ORE_OK;
+    const bool pooled = has(ORE_FUSE_FIRE_POOL);
     for (size_t i = 0; i < m->steps.size(); ++i) {
-      Step& cc = m->steps[i];
-      if (cc.kind != S_CONCAT || cc.axis != 1 || cc.in0 < 0 || cc.in1 < 0 || cc.in0 == cc.in1) continue;
-      const int pa = producer[cc.in0], pb = producer[cc.in1];
-      if (pa < 0 || pb < 0) continue;
-      auto consumer = [&](int v, size_t from) {
-        for (size_t j = from; j < m->steps.size(); ++j)
-          if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == v || m->steps[j].in1 == v)) return int(j);
-        return -1;
-      };
-      int qi = consumer(cc.out, i + 1), pi = -1;
+      int pa, pb;
+      if (!fire_concat(int(i), &pa, &pb)) continue;
+      Step& cc = st(int(i));
+      int qi = reader(cc.out, i + 1), pi = -1;
       if (qi < 0) continue;
-      // pooled form: Concat -> 3x3 / stride-2 MaxPool (read once) -> squeeze
-      if (m->steps[qi].kind == S_MAXPOOL) {
-        const Step& pl = m->steps[qi];
-        if (!fire_pool || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2 || pl.in0 != cc.out) continue;
-        const Value& pv = m->values[pl.out];
-        if (pv.uses != 1 || pv.is_output) continue;
+      if (st(qi).kind == S_MAXPOOL) {  // pooled form: Concat -> 3x3 / stride-2 MaxPool (read once) -> squeeze
+        const Step& pl = st(qi);
+        if (!pooled || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2 || pl.in0 != cc.out) continue;
+        if (!private_value(pl.out)) continue;
         pi = qi;
-        qi = consumer(pl.out, size_t(pi) + 1);
+        qi = reader(pl.out, size_t(pi) + 1);
         if (qi < 0) continue;
       }
-      const int qin = pi >= 0 ? m->steps[pi].out : cc.out;
-      Step &e1 = m->steps[pa], &e3 = m->steps[pb], &q = m->steps[qi];
+      const int qin = pi >= 0 ? st(pi).out : cc.out;
+      Step &e1 = st(pa), &e3 = st(pb), &q = st(qi);
       auto vec16 = [](const Step& s) {
         return s.kind == S_CONV && s.relu && !s.pool && !s.epool && s.plan.f16 && s.plan.xmode == F16_X_NHWC_VEC &&
                s.sh == 1 && s.sw == 1 && s.win.Ho == s.H && s.win.Wo == s.W;
@@ -931,7 +856,7 @@ ore_status plan(ore_model* m) {
       if (q.in2 < 0 || e1.in2 < 0 || e3.in2 < 0) continue;
       if (pi < 0 && fire_f16_lds_bytes(int(e1.C), int(e1.H), int(e1.W)) > FIRE_F16_LDS_MAX) continue;
       if (pi >= 0) {  // a band shape must fit (fire_pool_f16_plan) and every window touch the image
-        const Step& pl = m->steps[pi];
+        const Step& pl = st(pi);
         FireF16Params fp{};
         fp.C = int(e1.C); fp.H = int(e1.H); fp.W = int(e1.W);
         fp.Hp = int(pl.win.Ho); fp.Wp = int(pl.win.Wo); fp.ppt = int(pl.win.pt); fp.ppl = int(pl.win.pl);
@@ -939,36 +864,26 @@ ore_status plan(ore_model* m) {
             2 * (fp.Hp - 1) - fp.ppt >= fp.H || 2 * (fp.Wp - 1) - fp.ppl >= fp.W)
           continue;
       }
-      const Value &va = m->values[cc.in0], &vb = m->values[cc.in1], &vc = m->values[cc.out], &vs = m->values[e1.in0];
-      if (va.uses != 1 || vb.uses != 1 || vc.uses != 1 || va.is_output || vb.is_output || vc.is_output || vs.es != 2) continue;
+      if (!private_value(cc.in0) || !private_value(cc.in1) || !private_value(cc.out) || val(e1.in0).es != 2) continue;
       // the three weight packings (made once per model; keys 2000000 + expand index, 3000000 + squeeze index)
-      bool packed_ok = true;
       for (int idx : {pa, pb, qi}) {
-        const int key = (idx == qi ? 3000000 : 2000000) + idx;
-        if (m->fire_packs.count(key)) continue;
-        const Step& e = m->steps[idx];
-        const int kk = int(e.kh * e.kw);
-        float* buf = nullptr;
-        if (hipMalloc(reinterpret_cast<void**>(&buf), fire_pack_f16_bytes(int(e.M), int(e.C), kk)) != hipSuccess) {
-          packed_ok = false;
-          break;
-        }
-        launch_fire_pack_f16(m->values[e.in1].cptr, int(e.M), int(e.C), kk, buf, m->ctx->stream);
-        m->fire_packs[key] = buf;
+        const Step& e = st(idx);
+        const int kk = int(e.kh * e.kw), M = int(e.M), C = int(e.C);
+        const float* w = val(e.in1).cptr;
+        if (!pack_once((idx == qi ? 3000000 : 2000000) + idx, fire_pack_f16_bytes(M, C, kk),
+                       [&](float* buf) { launch_fire_pack_f16(w, M, C, kk, buf, m->ctx->stream); }))
+          return err(m, ORE_ERR_HIP, "f16 fire weight packing failed");
       }
-      if (!packed_ok || hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
-        return err(m, ORE_ERR_HIP, "f16 fire weight packing failed");
       q.kind = S_FIRE;
       q.fire_f16 = true;
       q.fire_pool = pi >= 0;
       q.fire_H = e1.H;
       q.fire_W = e1.W;
       if (pi >= 0) {
-        Step& pl = m->steps[pi];
+        Step& pl = st(pi);
         q.fire_pwin = pl.win;
-        m->values[pl.out].elided = true;
-        pl.kind = S_NOP;
-        pl.in0 = -1;
+        val(pl.out).elided = true;
+        nop(pl);
       }
       q.in0 = e1.in0;
       q.fire_C = e1.C;
@@ -977,238 +892,166 @@ ore_status plan(ore_model* m) {
       q.fire_w1 = m->fire_packs[2000000 + pa];
       q.fire_w3 = m->fire_packs[2000000 + pb];
       q.fire_ws16 = m->fire_packs[3000000 + qi];
-      q.fire_b1 = m->values[e1.in2].cptr;
-      q.fire_b3 = m->values[e3.in2].cptr;
+      q.fire_b1 = val(e1.in2).cptr;
+      q.fire_b3 = val(e3.in2).cptr;
       q.flops_per_img += e1.flops_per_img + e3.flops_per_img;
       q.bytes_per_img = 2.0 * double(e1.C * e1.H * e1.W) + 2.0 * double(q.M * q.H * q.W);
       q.name = e1.name.substr(0, e1.name.find('/')) + (pi >= 0 ? "+pool+" : "+") + q.name;
-      m->values[cc.in0].elided = m->values[cc.in1].elided = m->values[cc.out].elided = true;
-      e1.kind = e3.kind = cc.kind = S_NOP;
-      e1.in0 = e3.in0 = cc.in0 = cc.in1 = -1;
+      val(cc.in0).elided = val(cc.in1).elided = val(cc.out).elided = true;
+      nop(e1); nop(e3); nop(cc);
     }
-    count_uses(m, m->steps);
+    recount();
+    return ORE_OK;
   }
-  // (1h) f16 models: the first conv + pool (F16_X_NHWC_PAIR, pooled epilogue) whose pooled map is read
-  // only by a 1x1 conv (+ Relu) with <= 32 channels takes that conv into its launch
-  // (conv_pair_pool_f16_kernel SQ: SqueezeNet's conv1 + pool1 + fire2/squeeze1x1); the pooled map is
-  // never stored.  Bit-identical to the separate squeeze (same k-ordered chain over the same f16
-  // pooled values).  ORE_F16_C1POOL=0 (the two-launch first conv) turns it off.
-  if (m->f16 && (m->fusion & ORE_FUSE_CONV_POOL) && (m->fusion & ORE_FUSE_CONV_RELU)) {
-    const char* ec = getenv("ORE_F16_C1POOL");
-    const bool on = !(ec && atoi(ec) == 0);
-    for (size_t i = 0; on && i < m->steps.size(); ++i) {
-      Step& cv = m->steps[i];
-      if (cv.kind != S_CONV || !cv.plan.f16 || cv.plan.xmode != F16_X_NHWC_PAIR || !cv.epool || cv.c1sq) continue;
-      if (cv.kh != 7 || cv.kw != 7 || cv.sh != 2 || cv.sw != 2 || cv.win.pl % 2 || cv.C > 4 ||
-          (cv.M != 64 && cv.M != 96))
+
+  // (7) the first conv + pool whose pooled map is read only by a small 1x1 conv (+ Relu) takes that
+  // conv into its launch (SqueezeNet's conv1 + pool1 + fire2/squeeze1x1; the pooled map is never
+  // stored).  Bit-identical to the separate squeeze (the same k-ordered chain over the same pooled
+  // values).  f16: conv_pair_pool_f16_kernel SQ (<= 32 channels); f32: the window kernel (pooled-conv
+  // variant 7, <= 16 channels).
+  ore_status first_squeeze() {
+    if (!has(ORE_FUSE_FIRST_SQUEEZE | ORE_FUSE_CONV_POOL | ORE_FUSE_CONV_RELU) || m->x3_all) return ORE_OK;
+    for (size_t i = 0; i < m->steps.size(); ++i) {
+      Step& cv = st(int(i));
+      if (cv.kind != S_CONV || !cv.epool || cv.c1sq || !private_value(cv.out)) continue;
+      const bool f16 = cv.plan.f16 != 0;
+      if (f16 ? (cv.plan.xmode != F16_X_NHWC_PAIR || cv.kh != 7 || cv.kw != 7 || cv.sh != 2 || cv.sw != 2 ||
+                 cv.win.pl % 2 || cv.C > 4 || (cv.M != 64 && cv.M != 96))
+              : (!cv.wc1 || cv.C != 3 || cv.M != 96))
         continue;
-      const Value& pv = m->values[cv.out];
-      if (pv.uses != 1 || pv.is_output) continue;
-      int qi = -1;
-      for (size_t j = i + 1; j < m->steps.size(); ++j)
-        if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == cv.out || m->steps[j].in1 == cv.out)) { qi = int(j); break; }
+      const int qi = reader(cv.out, i + 1);
       if (qi < 0) continue;
-      Step& q = m->steps[qi];
-      if (q.kind != S_CONV || !q.relu || q.pool || q.epool || !q.plan.f16 || q.plan.xmode != F16_X_NHWC_VEC ||
-          q.kh != 1 || q.kw != 1 || q.sh != 1 || q.sw != 1 || q.win.pt || q.win.pl || q.in0 != cv.out ||
-          q.C != cv.M || q.M > 32 || q.M % 8 || q.in2 < 0)
+      Step& q = st(qi);
+      if (q.kind != S_CONV || !q.relu || q.pool || q.epool || q.kh != 1 || q.kw != 1 || q.sh != 1 || q.sw != 1 ||
+          q.win.pt || q.win.pl || q.in0 != cv.out || q.C != cv.M || q.in2 < 0 || q.in1 < 0 || !val(q.in1).cptr)
         continue;
-      const int key = 5000000 + qi;
-      if (!m->fire_packs.count(key)) {
-        float* buf = nullptr;
-        if (hipMalloc(reinterpret_cast<void**>(&buf), fire_pack_f16_bytes(int(q.M), int(q.C), 1)) != hipSuccess)
-          return err(m, ORE_ERR_OOM, "squeeze weight packing allocation failed");
-        launch_fire_pack_f16(m->values[q.in1].cptr, int(q.M), int(q.C), 1, buf, m->ctx->stream);
-        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
+      if (f16 ? (!q.plan.f16 || q.plan.xmode != F16_X_NHWC_VEC || q.M > 32 || q.M % 8) : (q.plan.f16 || q.plan.x3 || q.M > 16))
+        continue;
+      if (f16) {
+        const int key = 5000000 + qi, M = int(q.M), C = int(q.C);
+        const float* w = val(q.in1).cptr;
+        if (!pack_once(key, fire_pack_f16_bytes(M, C, 1),
+                       [&](float* buf) { launch_fire_pack_f16(w, M, C, 1, buf, m->ctx->stream); }))
           return err(m, ORE_ERR_HIP, "squeeze weight packing failed");
-        m->fire_packs[key] = buf;
+        cv.sq_w = m->fire_packs[key];
+      } else {
+        cv.sq_w = val(q.in1).cptr;  // ONNX [M][C][1][1] = [M][K]
+        cv.plan.epv = EPOOL_WIN_VARIANT;
       }
       cv.c1sq = true;
-      cv.sq_w = m->fire_packs[key];
-      cv.sq_b = m->values[q.in2].cptr;
+      cv.sq_b = val(q.in2).cptr;
       cv.sq_M = q.M;
-      m->values[cv.out].elided = true;
+      val(cv.out).elided = true;
       cv.out = q.out;
       cv.flops_per_img += q.flops_per_img;
-      cv.bytes_per_img = double(m->values[cv.in0].es) * double(cv.C * cv.H * cv.W) + 2.0 * double(q.M * q.H * q.W);
+      cv.bytes_per_img = double(val(cv.in0).es) * double(cv.C * cv.H * cv.W) + (f16 ? 2.0 : 4.0) * double(q.M * q.H * q.W);
       cv.name = cv.name + "+" + q.name;
-      q.kind = S_NOP;
-      q.in0 = -1;
+      nop(q);
     }
-    count_uses(m, m->steps);
+    recount();
+    return ORE_OK;
   }
-  // (1i) f32 models: the first conv + pool on the window kernel (pooled-conv variant 7) takes the next
-  // 1x1 conv (+ Relu, <= 16 channels) when it is the pooled map's only reader (SqueezeNet's conv1 +
-  // pool1 + fire2/squeeze1x1; the pooled map is never stored).  Bit-identical to the separate squeeze
-  // (the same k-ordered fma chain over the same pooled values).  ORE_C1_SQUEEZE=0 turns it off.
-  if (!m->f16 && !m->x3_all && (m->fusion & ORE_FUSE_CONV_POOL) && (m->fusion & ORE_FUSE_CONV_RELU)) {
-    const char* ec = getenv("ORE_C1_SQUEEZE");
-    const bool on = !(ec && atoi(ec) == 0);
-    for (size_t i = 0; on && i < m->steps.size(); ++i) {
-      Step& cv = m->steps[i];
-      if (cv.kind != S_CONV || cv.plan.f16 || !cv.epool || !cv.wc1 || cv.c1sq || cv.C != 3 || cv.M != 96) continue;
-      const Value& pv = m->values[cv.out];
-      if (pv.uses != 1 || pv.is_output) continue;
-      int qi = -1;
-      for (size_t j = i + 1; j < m->steps.size(); ++j)
-        if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == cv.out || m->steps[j].in1 == cv.out)) { qi = int(j); break; }
-      if (qi < 0) continue;
-      Step& q = m->steps[qi];
-      if (q.kind != S_CONV || !q.relu || q.pool || q.epool || q.plan.f16 || q.plan.x3 || q.kh != 1 || q.kw != 1 ||
-          q.sh != 1 || q.sw != 1 || q.win.pt || q.win.pl || q.in0 != cv.out || q.C != cv.M || q.M > 16 || q.in2 < 0 ||
-          q.in1 < 0 || !m->values[q.in1].cptr)
-        continue;
-      cv.c1sq = true;
-      cv.sq_w = m->values[q.in1].cptr;  // ONNX [M][C][1][1] = [M][K]
-      cv.sq_b = m->values[q.in2].cptr;
-      cv.sq_M = q.M;
-      cv.plan.epv = EPOOL_WIN_VARIANT;
-      m->values[cv.out].elided = true;
-      cv.out = q.out;
-      cv.flops_per_img += q.flops_per_img;
-      cv.bytes_per_img = 4.0 * double(cv.C * cv.H * cv.W) + 4.0 * double(q.M * q.H * q.W);
-      cv.name = cv.name + "+" + q.name;
-      q.kind = S_NOP;
-      q.in0 = -1;
-    }
-    count_uses(m, m->steps);
-  }
-  // (1j) f32: a 3x3 / stride-2 MaxPool left standing (SqueezeNet pool5) whose only reader is a 1x1
-  // Conv (+ Relu) with <= 64 channels runs inside that conv (pool_conv1x1_f32_kernel, the pooled map
-  // never stored; the (1b) step form, run_conv_pool).  Bit-identical to maxpool_kernel + the conv.
-  // ORE_POOL_SQUEEZE=0 turns it off.
-  if (!m->f16 && !m->x3_all && (m->fusion & ORE_FUSE_CONV_POOL)) {
-    const char* ep = getenv("ORE_POOL_SQUEEZE");
-    const bool on = !(ep && atoi(ep) == 0);
-    for (size_t i = 0; on && i < m->steps.size(); ++i) {
-      Step& pl = m->steps[i];
+
+  // (8) f32: a 3x3 / stride-2 MaxPool left standing (SqueezeNet pool5) whose only reader is a 1x1 Conv
+  // (+ Relu) with <= 64 channels runs inside that conv (pool_conv1x1_f32_kernel, the pooled map never
+  // stored).  Bit-identical to the MaxPool kernel + the conv.
+  void pool_squeeze() {
+    if (!has(ORE_FUSE_POOL_SQUEEZE) || m->f16 || m->x3_all) return;
+    for (size_t i = 0; i < m->steps.size(); ++i) {
+      Step& pl = st(int(i));
       if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2) continue;
       const int v = pl.out;
-      if (m->values[v].uses != 1 || m->values[v].is_output || m->values[pl.in0].es != 4 || m->values[pl.in0].nhwc) continue;
-      int ci = -1;
-      for (size_t j = i + 1; j < m->steps.size(); ++j)
-        if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == v || m->steps[j].in1 == v)) { ci = int(j); break; }
+      if (!private_value(v) || val(pl.in0).es != 4 || val(pl.in0).nhwc) continue;
+      const int ci = reader(v, i + 1);
       if (ci < 0) continue;
-      Step& cv = m->steps[ci];
+      Step& cv = st(ci);
       if (cv.kind != S_CONV || cv.pool || cv.epool || cv.in0 != v || cv.kh != 1 || cv.kw != 1 || cv.sh != 1 ||
-          cv.sw != 1 || cv.win.pt || cv.win.pl || cv.plan.window || cv.plan.f16 || cv.plan.x3 || cv.plan.wino ||
-          cv.M > 64 || cv.C % 32 || pl.win.Wo > 16 || pl.win.pt > 2 || pl.win.pl > 2)
+          cv.sw != 1 || cv.win.pt || cv.win.pl || cv.plan.f16 || cv.plan.x3 || cv.plan.wino || cv.M > 64 || cv.C % 32 ||
+          pl.win.Wo > 16 || pl.win.pt > 2 || pl.win.pl > 2)
         continue;
+      PoolConvParams q{};  // pool_conv1x1_f32_kernel's own limits (run_conv_pool has no other kernel)
+      q.C = int(cv.C); q.H = int(pl.H); q.W = int(pl.W); q.Hp = int(pl.win.Ho); q.Wp = int(pl.win.Wo);
+      q.pt = int(pl.win.pt); q.pl = int(pl.win.pl); q.M = int(cv.M); q.Mp = cv.plan.Mp; q.Kp = cv.plan.krows;
+      q.N = 1; q.x_ps = int(pl.H * pl.W); q.y_ps = int(pl.win.Ho * pl.win.Wo);
+      q.x_nstride = int64_t(q.C) * q.x_ps; q.y_nstride = int64_t(q.M) * q.y_ps;
+      if (!pool_conv1x1_f32_eligible(q)) continue;
       cv.pool = true;
       cv.in0 = pl.in0;
       cv.pH = pl.H; cv.pW = pl.W; cv.psh = pl.sh; cv.psw = pl.sw; cv.pwin = pl.win;
       cv.bytes_per_img = 4.0 * double(pl.C * pl.H * pl.W) + 4.0 * double(cv.M * cv.H * cv.W);
       cv.name = pl.name + "+" + cv.name;
-      m->values[v].elided = true;
-      pl.kind = S_NOP;
-      pl.in0 = -1;
+      val(v).elided = true;
+      nop(pl);
     }
-    count_uses(m, m->steps);
+    recount();
   }
-  // (1f) ORE_LOAD_X3: every conv / matmul not taken by an f32-MFMA fusion above runs its x3 plan
-  if (m->x3)
-    for (auto& st : m->steps)
-      if ((st.kind == S_CONV || st.kind == S_MATMUL) && st.has_x3 && !st.pool && !st.epool) {
-        st.plan = st.plan_x3;
-        st.wp = st.wp_x3;
-        st.ktab = st.ktab_x3;
+
+  // (9) algorithm selection, a load-time rule (never by timing): ORE_LOAD_X3 moves every conv / MatMul
+  // not taken by an f32-MFMA fusion to its x3 plan; f32 models with Winograd on run every 3x3 /
+  // stride-1 / pad-1 conv not taken by a direct-kernel fusion by Winograd F(2x2, 3x3)
+  void select_algorithms() {
+    for (auto& s : m->steps) {
+      if (m->x3 && (s.kind == S_CONV || s.kind == S_MATMUL) && s.has_x3 && !s.pool && !s.epool) {
+        s.plan = s.plan_x3;
+        s.wp = s.wp_x3;
+        s.ktab = s.ktab_x3;
       }
-  // (1g) f32 models: every 3x3 / stride-1 / pad-1 conv not taken by a direct-kernel fusion above runs
-  // Winograd F(2x2, 3x3) (a load-time rule: the algorithm never depends on timing)
-  if (m->wino)
-    for (auto& st : m->steps)
-      if (st.kind == S_CONV && st.has_wino && !st.pool && !st.epool) {
-        st.plan = st.plan_wino;
-        st.wp = st.wp_wino;
-        st.ktab = nullptr;
+      if (m->wino && s.kind == S_CONV && s.has_wino && !s.pool && !s.epool) {
+        s.plan = s.plan_wino;
+        s.wp = s.wp_wino;
+        s.ktab = nullptr;
+        // MFMA work issued: 16 positions x C x M per 2x2 output tile (the direct conv's 36 C M / 4 pixels)
+        s.mfma_flops_per_img = 2.0 * 16.0 * double(s.C) * double(s.M) * double((s.win.Ho + 1) / 2) *
+                               double((s.win.Wo + 1) / 2);
       }
-  // (2) Dropout / activation Reshape as aliases
-  if (m->fusion & ORE_FUSE_ALIAS) {
+    }
+  }
+
+  // (10) Dropout / activation Reshape as aliases
+  void alias_copies() {
+    if (!has(ORE_FUSE_ALIAS)) return;
     for (auto& s : m->steps) {
       if (s.kind != S_COPY) continue;
-      Value& y = m->values[s.out];
-      y.alias_of = s.in0;  // resolved to the root at run time; requires a contiguous source
+      val(s.out).alias_of = s.in0;  // resolved to the root at run time; requires a contiguous source
       s.kind = S_NOP;
     }
   }
-  // (3) Concat in place: producers write channel slices of the concat buffer
-  if (m->fusion & ORE_FUSE_CONCAT) {
+
+  // (11) Concat in place: producers write channel slices of the concat buffer
+  void concat_in_place() {
+    if (!has(ORE_FUSE_CONCAT)) return;
     for (auto& s : m->steps) {
       if (s.kind != S_CONCAT || s.axis != 1 || s.in0 == s.in1) continue;
-      Value &a = m->values[s.in0], &b = m->values[s.in1];
-      int pa = producer[s.in0], pb = producer[s.in1];
-      if (pa < 0 || pb < 0 || !strided_writer(m->steps[pa]) || !strided_writer(m->steps[pb])) continue;
+      Value &a = val(s.in0), &b = val(s.in1);
+      const int pa = producer[s.in0], pb = producer[s.in1];
+      if (pa < 0 || pb < 0 || !strided_writer(st(pa)) || !strided_writer(st(pb))) continue;
       if (a.uses != 1 || b.uses != 1 || a.is_output || b.is_output || a.alias_of >= 0 || b.alias_of >= 0) continue;
-      const Value& y = m->values[s.out];
-      (void)y;
       a.alias_of = s.out; a.alias_ch = 0; a.slice = true;
       b.alias_of = s.out; b.alias_ch = a.dims[1]; b.slice = true;
       s.kind = S_NOP;
     }
   }
-  // (3b) f32: a 1x1 Conv that reads the same input as a Winograd 3x3 Conv with as many output channels,
-  // both writing slices of one Concat (SqueezeNet's fire8 / fire9 expand1x1 beside expand3x3), runs
-  // inside the Winograd launch (conv_wino32_kernel E1: the 1x1 conv's B operand is the window centre
-  // the transform already loaded; its k-ordered chain is bit-identical to the standalone kernels').
-  // Opt-in (ORE_WINO_E1=1): measured equal or slower at B = 256 (fire8: 451.6 us fused vs 75.6 + 369.5
-  // separate; bench 66.1 k vs 66.3 k img/s, profiles/r02j_wino_e1_ab.txt) -- the 16x16 kernel pays
-  // the extra MFMAs in full, and the 32x32 kernels, which would hide them, have no registers left.
-  if (m->wino && (m->fusion & ORE_FUSE_CONCAT)) {
-    const char* ee = getenv("ORE_WINO_E1");
-    const bool on = ee && atoi(ee) != 0;
-    for (size_t t = 0; on && t < m->steps.size(); ++t) {
-      Step& w3 = m->steps[t];
-      if (w3.kind != S_CONV || !w3.plan.wino || w3.pool || w3.epool || w3.e1_out >= 0 || w3.C % 16 || w3.C > 64) continue;
-      const Value& b = m->values[w3.out];
-      if (!b.slice || b.alias_of < 0) continue;
-      for (size_t k = 0; k < m->steps.size(); ++k) {
-        Step& q = m->steps[k];
-        if (k == t || q.kind != S_CONV || q.in0 != w3.in0 || q.C != w3.C || q.M != w3.M || q.H != w3.H || q.W != w3.W ||
-            q.kh != 1 || q.kw != 1 || q.sh != 1 || q.sw != 1 || q.win.pt || q.win.pl || q.pool || q.epool ||
-            q.plan.window || q.plan.f16 || q.plan.x3 || q.plan.wino || !q.wp)
-          continue;
-        const Value& a = m->values[q.out];
-        if (!a.slice || a.alias_of != b.alias_of) continue;
-        w3.e1_out = q.out;
-        w3.plan.cfg = WINO_TILE_BASE + 2;  // the kernel that takes the fused conv (conv_wino_e1_eligible)
-        w3.e1_wp = q.wp;
-        w3.e1_Mp = q.plan.Mp;
-        w3.e1_b = q.in2 >= 0 ? m->values[q.in2].cptr : nullptr;
-        w3.e1_relu = q.relu;
-        w3.flops_per_img += q.flops_per_img;
-        w3.bytes_per_img += 4.0 * double(q.M * q.H * q.W);
-        w3.name = q.name + "+" + w3.name;
-        q.kind = S_NOP;
-        q.in0 = -1;
-        break;
-      }
-    }
-    count_uses(m, m->steps);
-  }
-  // aliases of aliases must stay contiguous views (Reshape/Dropout of a channel slice)
-  for (auto& v : m->values) {
-    if (v.alias_of < 0 || v.slice) continue;
-    if (m->values[v.alias_of].slice)
-      return err(m, ORE_ERR_INVALID, "internal: alias of a strided view (" + v.name + ")");
-  }
-  auto root = [&](int id) {
+
+  int root(int id) const {
     while (m->values[id].alias_of >= 0) id = m->values[id].alias_of;
     return id;
-  };
+  }
 
-  // layout: an activation touched only by Conv / MaxPool kernels gets channel planes padded to
-  // a multiple of 32 floats (128-B aligned rows for the conv epilogue and the 1x1 gathers) when
-  // that costs <= 5% extra columns; everything else stays dense NCHW.
-  {
+  // (12) layout: an activation touched only by Conv / MaxPool kernels (and f32 GlobalAveragePool)
+  // gets channel planes padded to a multiple of 32 floats (128-B aligned rows for the conv epilogue
+  // and the 1x1 gathers) when that costs <= 5 % extra columns; everything else stays dense NCHW.
+  ore_status layout_planes() {
+    for (auto& v : m->values) {  // aliases of aliases must stay contiguous views (Reshape / Dropout of a slice)
+      if (v.alias_of < 0 || v.slice) continue;
+      if (val(v.alias_of).slice) return err(m, ORE_ERR_INVALID, "internal: alias of a strided view (" + v.name + ")");
+    }
     std::vector<char> dense(m->values.size(), 0);
-    for (const Step& st : m->steps) {
-      if (st.kind == S_NOP) continue;
-      // GlobalAveragePool reads f32 planes at any stride (launch_step)
-      const bool ok = st.kind == S_CONV || st.kind == S_FIRE || st.kind == S_MAXPOOL ||
-                      (st.kind == S_GAP && !m->values[st.in0].nhwc);
-      for (int id : {st.in0, st.in2, st.out})
-        if (id >= 0 && !m->values[id].is_const && !ok) dense[root(id)] = 1;
-      if (st.in1 >= 0 && !m->values[st.in1].is_const) dense[root(st.in1)] = 1;
+    for (const Step& s : m->steps) {
+      if (s.kind == S_NOP) continue;
+      const bool ok = s.kind == S_CONV || s.kind == S_FIRE || s.kind == S_MAXPOOL || (s.kind == S_GAP && !val(s.in0).nhwc);
+      for (int id : {s.in0, s.in2, s.out})
+        if (id >= 0 && !val(id).is_const && !ok) dense[root(id)] = 1;
+      if (s.in1 >= 0 && !val(s.in1).is_const) dense[root(s.in1)] = 1;
     }
     // a contiguous view (Dropout / Reshape alias) keeps its root's planes only as a 4-D
     // intermediate; as a graph output or a reshaped 2-D value it needs the dense layout
@@ -1224,135 +1067,179 @@ ore_status plan(ore_model* m) {
         continue;
       }
       const int64_t P = v.dims[2] * v.dims[3];
-      static const bool pad_planes = getenv("ORE_PAD_PLANES") ? atoi(getenv("ORE_PAD_PLANES")) != 0 : true;  // experiment knob
-      const bool pad = pad_planes && (m->fusion & ORE_FUSE_CONCAT) && !dense[id] && !v.is_input && !v.is_output;
+      const bool pad = has(ORE_FUSE_CONCAT) && !dense[id] && !v.is_input && !v.is_output;
       v.ps = pad ? padded_plane(P) : P;
     }
-    for (auto& v : m->values)  // views inherit the plane stride of their root
-      if (v.alias_of >= 0 && v.ndim == 4) {
-        const Value& r = m->values[root(int(&v - &m->values[0]))];
-        v.ps = r.ps;
-        if (v.nhwc != r.nhwc) return err(m, ORE_ERR_INVALID, "internal: view of a different layout (" + v.name + ")");
-        if (!v.slice && r.ps != (r.nhwc ? r.dims[1] : r.dims[2] * r.dims[3]) &&
-            (v.is_output || v.dims[2] * v.dims[3] != r.dims[2] * r.dims[3]))
-          return err(m, ORE_ERR_INVALID, "internal: dense alias of a padded value (" + v.name + ")");
+    for (size_t id = 0; id < m->values.size(); ++id) {  // views inherit the plane stride of their root
+      Value& v = m->values[id];
+      if (v.alias_of < 0 || v.ndim != 4) continue;
+      const Value& r = val(root(int(id)));
+      v.ps = r.ps;
+      if (v.nhwc != r.nhwc) return err(m, ORE_ERR_INVALID, "internal: view of a different layout (" + v.name + ")");
+      if (!v.slice && r.ps != (r.nhwc ? r.dims[1] : r.dims[2] * r.dims[3]) &&
+          (v.is_output || v.dims[2] * v.dims[3] != r.dims[2] * r.dims[3]))
+        return err(m, ORE_ERR_INVALID, "internal: dense alias of a padded value (" + v.name + ")");
+    }
+    return ORE_OK;
+  }
+
+  // (13) one device arena: every materialised root value gets a slot sized for max_batch, slots reused
+  // by liveness (first fit over [first write, last read] intervals)
+  ore_status assign_arena() {
+    const int nsteps = int(m->steps.size());
+    for (int i = 0; i < nsteps; ++i) {
+      const Step& s = m->steps[i];
+      if (s.kind == S_NOP) continue;
+      for (int id : {s.in0, s.in1, s.in2}) {
+        if (id < 0 || val(id).is_const) continue;
+        Value& r = val(root(id));
+        if (r.first < 0) r.first = i;
+        r.last = std::max(r.last, i);
       }
+      if (s.out >= 0) {
+        Value& r = val(root(s.out));
+        if (r.first < 0 || r.first > i) r.first = i;
+        r.last = std::max(r.last, i);
+      }
+    }
+    // the model output stays live to the end (it may be copied out after the last step)
+    if (m->output_value >= 0) val(root(m->output_value)).last = nsteps;
+
+    struct Slot { int64_t off, size; int first, last; };
+    std::vector<int> roots;
+    for (size_t id = 0; id < m->values.size(); ++id) {
+      const Value& v = m->values[id];
+      if (v.is_const || v.is_input || v.alias_of >= 0 || v.elided || v.first < 0) continue;
+      roots.push_back(int(id));
+    }
+    // the kernels index a launch's activations with 32-bit element offsets: refuse at load a max_batch
+    // whose values exceed them (rather than failing at run time)
+    for (size_t id = 0; id < m->values.size(); ++id) {
+      const Value& v = m->values[id];
+      if (v.is_const || v.alias_of >= 0 || v.elided || (v.first < 0 && !v.is_input)) continue;
+      if (v.image_stride() * m->max_batch + 256 >= (int64_t(1) << 31))
+        return err(m, ORE_ERR_UNSUPPORTED, "max_batch " + std::to_string(m->max_batch) + " exceeds 32-bit indexing of '" +
+                                               v.name + "' (" + std::to_string(v.image_stride()) +
+                                               " elements per image); run the batch in parts");
+    }
+    std::sort(roots.begin(), roots.end(), [&](int a, int b) { return val(a).image_stride() > val(b).image_stride(); });
+    std::vector<Slot> placed;
+    int64_t arena = 0;
+    for (int id : roots) {
+      Value& v = val(id);
+      const int64_t size = ((v.image_stride() * m->max_batch * v.es) + 255) / 256 * 256;
+      std::vector<std::pair<int64_t, int64_t>> busy;  // slots whose lifetimes overlap this one
+      for (auto& s : placed)
+        if (has(ORE_KEEP_VALUES) || !(s.last < v.first || v.last < s.first)) busy.push_back({s.off, s.off + s.size});
+      std::sort(busy.begin(), busy.end());
+      int64_t off = 0;
+      for (auto& b : busy) {
+        if (off + size <= b.first) break;
+        off = std::max(off, b.second);
+      }
+      v.arena_off = off;
+      placed.push_back({off, size, v.first, v.last});
+      arena = std::max(arena, off + size);
+    }
+    if (size_t(arena) > m->arena_bytes) {
+      if (m->arena_alloc) (void)hipFree(m->arena_alloc);
+      m->arena = m->arena_alloc = nullptr;
+      m->arena_bytes = 0;
+      if (arena > 0 && hipMalloc(reinterpret_cast<void**>(&m->arena_alloc), size_t(arena) + 4096) != hipSuccess)
+        return err(m, ORE_ERR_OOM, "arena allocation of " + std::to_string(arena) + " bytes failed");
+      if (m->arena_alloc) m->arena = m->arena_alloc + 4096;
+      m->arena_bytes = size_t(arena);
+    }
+    m->exec_steps.clear();
+    for (int i = 0; i < nsteps; ++i)
+      if (m->steps[i].kind != S_NOP) m->exec_steps.push_back(i);
+    return ORE_OK;
   }
 
-  // live intervals on root storage
-  const int nsteps = int(m->steps.size());
-  for (int i = 0; i < nsteps; ++i) {
-    const Step& s = m->steps[i];
-    if (s.kind == S_NOP) continue;
-    for (int id : {s.in0, s.in1, s.in2}) {
-      if (id < 0 || m->values[id].is_const) continue;
-      Value& r = m->values[root(id)];
-      if (r.first < 0) r.first = i;
-      r.last = std::max(r.last, i);
-    }
-    if (s.out >= 0) {
-      Value& r = m->values[root(s.out)];
-      if (r.first < 0 || r.first > i) r.first = i;
-      r.last = std::max(r.last, i);
-    }
-  }
-  // the model output stays live to the end (it may be copied out after the last step)
-  if (m->output_value >= 0) m->values[root(m->output_value)].last = nsteps;
-
-  struct Slot { int64_t off, size; int first, last; };
-  std::vector<int> roots;
-  for (size_t id = 0; id < m->values.size(); ++id) {
-    Value& v = m->values[id];
-    if (v.is_const || v.is_input || v.alias_of >= 0 || v.elided || v.first < 0) continue;
-    roots.push_back(int(id));
-  }
-  std::sort(roots.begin(), roots.end(), [&](int a, int b) {
-    return m->values[a].image_stride() > m->values[b].image_stride();
-  });
-  std::vector<Slot> placed;
-  int64_t arena = 0;
-  for (int id : roots) {
-    Value& v = m->values[id];
-    const int64_t size = ((v.image_stride() * m->max_batch * v.es) + 255) / 256 * 256;
-    // first fit among the gaps left by placed slots whose lifetimes overlap this one
-    std::vector<std::pair<int64_t, int64_t>> busy;
-    for (auto& s : placed)
-      if ((m->fusion & ORE_KEEP_VALUES) || !(s.last < v.first || v.last < s.first)) busy.push_back({s.off, s.off + s.size});
-    std::sort(busy.begin(), busy.end());
-    int64_t off = 0;
-    for (auto& b : busy) {
-      if (off + size <= b.first) break;
-      off = std::max(off, b.second);
-    }
-    v.arena_off = off;
-    placed.push_back({off, size, v.first, v.last});
-    arena = std::max(arena, off + size);
-  }
-  if (size_t(arena) > m->arena_bytes) {
-    if (m->arena_alloc) (void)hipFree(m->arena_alloc);
-    m->arena = m->arena_alloc = nullptr;
-    m->arena_bytes = 0;
-    if (arena > 0 && hipMalloc(reinterpret_cast<void**>(&m->arena_alloc), size_t(arena) + 4096) != hipSuccess)
-      return err(m, ORE_ERR_OOM, "arena allocation of " + std::to_string(arena) + " bytes failed");
-    if (m->arena_alloc) m->arena = m->arena_alloc + 4096;
-    m->arena_bytes = size_t(arena);
-  }
-  m->exec_steps.clear();
-  for (int i = 0; i < nsteps; ++i)
-    if (m->steps[i].kind != S_NOP) m->exec_steps.push_back(i);
-  // independent neighbours: B reads nothing A writes, and no byte range A or B writes overlaps
-  // one the other reads or writes (arena slots are shared by liveness, so check the memory)
-  m->pair_next.assign(m->exec_steps.size(), 0);
-  {
+  // (14) independent neighbours for the two-stream issue (ore_model_set_streams): B reads nothing A
+  // writes, and no byte range A or B writes overlaps one the other reads or writes (arena slots are
+  // shared by liveness, so check the memory)
+  void pair_steps() {
+    m->pair_next.assign(m->exec_steps.size(), 0);
     auto span = [&](int id, int64_t* lo, int64_t* hi) {  // arena byte range of a value's root
-      const int r = root(id);
-      const Value& v = m->values[r];
+      const Value& v = val(root(id));
       if (v.is_const || v.arena_off < 0) return false;
       *lo = v.arena_off;
       *hi = v.arena_off + v.image_stride() * m->max_batch * v.es;
       return true;
     };
     auto overlap = [&](int a, int b) {
-      if (a < 0 || b < 0) return false;
-      if (m->values[a].is_const || m->values[b].is_const) return false;
+      if (a < 0 || b < 0 || val(a).is_const || val(b).is_const) return false;
       const int ra = root(a), rb = root(b);
-      if (m->values[ra].is_input || m->values[rb].is_input) return false;  // never written
+      if (val(ra).is_input || val(rb).is_input) return false;  // never written
       if (ra == rb) {  // channel slices of one buffer: disjoint unless the same slice
-        const Value &va = m->values[a], &vb = m->values[b];
+        const Value &va = val(a), &vb = val(b);
         if (va.slice && vb.slice) return va.alias_ch < vb.alias_ch + vb.dims[1] && vb.alias_ch < va.alias_ch + va.dims[1];
         return true;
       }
-      if (m->values[ra].is_output || m->values[rb].is_output) return true;  // conservative (may live in the arena)
+      if (val(ra).is_output || val(rb).is_output) return true;  // conservative (may live in the arena)
       int64_t a0, a1, b0, b1;
       if (!span(a, &a0, &a1) || !span(b, &b0, &b1)) return false;
       return a0 < b1 && b0 < a1;
     };
     for (size_t k = 0; k + 1 < m->exec_steps.size(); ++k) {
       if (k > 0 && m->pair_next[k - 1]) continue;  // pairs only
-      const Step &A = m->steps[m->exec_steps[k]], &B = m->steps[m->exec_steps[k + 1]];
-      bool ok = A.out >= 0 && B.out >= 0 && A.e1_out < 0 && B.e1_out < 0;  // (3b) steps write two values
+      const Step &A = st(m->exec_steps[k]), &B = st(m->exec_steps[k + 1]);
+      bool ok = A.out >= 0 && B.out >= 0;
       for (int bi : {B.in0, B.in1, B.in2}) ok = ok && !overlap(bi, A.out);
       for (int ai : {A.in0, A.in1, A.in2}) ok = ok && !overlap(ai, B.out);
       ok = ok && !overlap(A.out, B.out);
       m->pair_next[k] = ok ? 1 : 0;
     }
   }
-  // gather tables depend on the input's plane stride
-  for (const Step& st : m->steps) {
-    if (st.kind != S_CONV || !st.ktab) continue;
-    const Value& xv = m->values[st.in0];
-    int2* kt = const_cast<int2*>(st.ktab);
-    if (st.plan.f16 && st.plan.xmode != F16_X_NCHW32)
-      launch_ktab_nhwc(kt, st.plan.xmode, int(st.C), int(st.kh), int(st.kw),
-                       st.plan.xmode == F16_X_NHWC_PAIR ? 4 : st.plan.xmode == F16_X_NHWC8 ? 8 : int(xv.ps), int(st.W),
-                       m->ctx->stream);
-    else
-      launch_ktab(kt, int(st.C * st.kh * st.kw), int(st.kh), int(st.kw), int(xv.ps ? xv.ps : st.H * st.W), int(st.W),
-                  m->ctx->stream);
+
+  // (15) gather tables: they depend on the input's plane stride
+  ore_status gather_tables() {
+    for (const Step& s : m->steps) {
+      if (s.kind != S_CONV || !s.ktab) continue;
+      const Value& xv = val(s.in0);
+      int2* kt = const_cast<int2*>(s.ktab);
+      if (s.plan.f16 && s.plan.xmode != F16_X_NCHW32)
+        launch_ktab_nhwc(kt, s.plan.xmode, int(s.C), int(s.kh), int(s.kw),
+                         s.plan.xmode == F16_X_NHWC_PAIR ? 4 : int(xv.ps), int(s.W), m->ctx->stream);
+      else
+        launch_ktab(kt, int(s.C * s.kh * s.kw), int(s.kh), int(s.kw), int(xv.ps ? xv.ps : s.H * s.W), int(s.W),
+                    m->ctx->stream);
+    }
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
+      return err(m, ORE_ERR_HIP, "gather table build failed");
+    return ORE_OK;
   }
-  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(m->ctx->stream) != hipSuccess)
-    return err(m, ORE_ERR_HIP, "gather table build failed");
-  return ORE_OK;
+};
+
+ore_status plan(ore_model* m) {
+  m->steps = m->base_steps;
+  if (!m->n_base_values) m->n_base_values = m->values.size();
+  m->values.resize(m->n_base_values);  // drop the previous plan's views
+  for (auto& v : m->values) {
+    v.alias_of = -1; v.alias_ch = 0; v.slice = false; v.ps = 0; v.elided = false; v.arena_off = -1;
+    v.nhwc = !v.is_const && v.es == 2 && v.ndim == 4;
+    v.first = v.last = -1;
+  }
+  count_uses(m, m->steps);
+  Planner p{m, std::vector<int>(m->values.size(), -1)};
+  for (size_t i = 0; i < m->steps.size(); ++i)
+    if (m->steps[i].out >= 0 && m->steps[i].kind != S_NOP) p.producer[m->steps[i].out] = int(i);
+  p.conv_relu();
+  if (ore_status st = p.conv_pool()) return st;
+  if (ore_status st = p.fire_pool_f32()) return st;
+  p.concat_pool();
+  if (ore_status st = p.fire_f32()) return st;
+  if (ore_status st = p.fire_f16()) return st;
+  if (ore_status st = p.first_squeeze()) return st;
+  p.pool_squeeze();
+  p.select_algorithms();
+  p.alias_copies();
+  p.concat_in_place();
+  if (ore_status st = p.layout_planes()) return st;
+  if (ore_status st = p.assign_arena()) return st;
+  p.pair_steps();
+  return p.gather_tables();
 }
 
 // storage of a value for the current run: pointer to image 0 and per-image stride
@@ -1416,25 +1303,29 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       const Ref x = ref_of(m, s.in0);
       const float* bias = s.in2 >= 0 ? m->values[s.in2].cptr : nullptr;
       const F16Epool ep{s.ep_kh, s.ep_kw, s.ep_sh, s.ep_sw, s.ep_win};
-      if (s.plan.f16 && s.plan.xmode == F16_X_NHWC_PAIR && s.epool) {  // one launch from the f32 input
+      // the one-launch f16 first conv + pool from the f32 input (plan.epv 1: the two-launch patch path)
+      if (s.plan.f16 && s.plan.xmode == F16_X_NHWC_PAIR && s.epool && (s.c1sq || s.plan.epv != 1)) {
         bool ran = false;
         const C1Squeeze sq{s.sq_w, s.sq_b, int(s.sq_M), y.p, y.nstride, int(y.ps ? y.ps : s.sq_M)};
         const ore_status st = run_conv_pair_pool_f16(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.M, s.kh,
                                                      s.kw, bias, s.win, s.sh, s.sw, s.relu, s.c1sq ? nullptr : y.p,
                                                      y.nstride, s.c1sq ? s.M : y.ps, ep, &ran, s.c1sq ? &sq : nullptr);
-        if (ran) s.ran_tile = WINO_TILE_BASE + WINO_TILES_N + 2;  // "first conv pool f16" (ore.Model.TILE_NAMES)
+        if (ran) s.ran_tile = last_conv_tile = C1_POOL_F16_TILE;
         if (st != ORE_OK || ran) return st;
         s.ran_tile = -1;
         if (s.c1sq) return err(m, ORE_ERR_INVALID, "internal: the fused first conv + squeeze declined its launch");
       }
-      if (s.plan.f16 && (s.plan.xmode == F16_X_NHWC_PAIR || s.plan.xmode == F16_X_NHWC8)) {
-        // convert the f32 NCHW input to NHWC f16 (4 / 8 channels per pixel), then gather
-        const int cs = s.plan.xmode == F16_X_NHWC8 ? 8 : 4;
+      if (s.plan.f16 && s.plan.xmode == F16_X_NHWC_PAIR) {
+        // convert the f32 NCHW input to NHWC f16 (4 channels per pixel), then gather
+        const int cs = 4;
         launch_nchw_to_nhwc(x.p, s.xcvt, int(n), int(s.C), int(s.H * s.W), x.nstride, int(x.ps ? x.ps : s.H * s.W), cs,
                             ctx->stream);
         ORE_HIP_CHECK(ctx, hipGetLastError());
-        return run_conv_f16(ctx, s.plan, s.xcvt, n, s.C, s.H, s.W, s.H * s.W * cs, cs, s.wp, s.ktab, s.M, s.kh, s.kw,
-                            bias, s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps, s.epool ? &ep : nullptr);
+        const ore_status r = run_conv_f16(ctx, s.plan, s.xcvt, n, s.C, s.H, s.W, s.H * s.W * cs, cs, s.wp, s.ktab, s.M,
+                                          s.kh, s.kw, bias, s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps,
+                                          s.epool ? &ep : nullptr);
+        if (s.epool) s.ran_tile = last_conv_tile = EPOOL_TILE_BASE + 1;  // "epool patch": conv_f16's pooled epilogue
+        return r;
       }
       if (s.plan.f16)
         return run_conv_f16(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.ktab, s.M, s.kh, s.kw, bias,
@@ -1458,16 +1349,8 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
                              s.relu, y.p, y.nstride, y.ps, x.es);
       ctx->mapped_lo = m->arena_alloc;  // the arena and its 4 KiB lead are mapped
       ctx->mapped_hi = m->arena ? m->arena + m->arena_bytes : nullptr;
-      ConvE1 e1{};
-      if (s.e1_out >= 0) {
-        const Ref y1 = ref_of(m, s.e1_out);
-        if (y1.nstride != y.nstride || y1.ps != y.ps)
-          return err(m, ORE_ERR_INVALID, "internal: fused 1x1 conv output strides differ from the 3x3 conv's");
-        e1 = ConvE1{s.e1_wp, s.e1_b, y1.p, s.e1_Mp, s.e1_relu};
-      }
       const ore_status st = run_conv(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, s.wp, s.ktab, s.M, s.kh, s.kw, bias,
-                                     s.win, s.sh, s.sw, s.relu, y.p, y.nstride, x.ps, y.ps, x.es,
-                                     s.e1_out >= 0 ? &e1 : nullptr);
+                                     s.win, s.sh, s.sw, s.relu, y.p, y.nstride, x.ps, y.ps, x.es);
       ctx->mapped_lo = ctx->mapped_hi = nullptr;
       return st;
     }
@@ -1484,7 +1367,7 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       const ore_status st = run_fire(ctx, x.p, n, s.fire_C, fH, fW, x.nstride, x.ps ? x.ps : fH * fW, s.fire_w1,
                                      s.fire_b1, s.fire_E1, s.fire_w3, s.fire_b3, s.fire_E3, s.wp, s.plan.Mp,
                                      m->values[s.in2].cptr, s.M, y.p, y.nstride, y.ps ? y.ps : s.H * s.W,
-                                     s.fire_wino, s.fire_pool ? &s.fire_pwin : nullptr);
+                                     s.fire_pool ? &s.fire_pwin : nullptr);
       ctx->mapped_lo = ctx->mapped_hi = nullptr;
       return st;
     }
@@ -1546,6 +1429,57 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
 
 }  // namespace
 
+namespace {
+
+// the tile ids a step may run (its kernel family): autotune candidates and ore_model_set_step_tile's
+// accepted values; empty for steps with one fixed kernel
+std::vector<int> step_tile_family(const Step& s) {
+  std::vector<int> c;
+  if (s.kind != S_CONV && s.kind != S_MATMUL) return c;
+  if (s.kind == S_CONV && s.epool && !s.plan.f16) {  // f32 pooled conv: patch / row-walk variants, the window kernel
+    if (s.c1sq) return {EPOOL_WIN_TILE};            // the fused squeeze exists in the window kernel only
+    for (int v = 1; v <= 5; ++v) c.push_back(EPOOL_TILE_BASE + v);
+    if (s.wc1) c.push_back(EPOOL_WIN_TILE);
+    return c;
+  }
+  if (s.kind == S_CONV && s.epool && s.plan.f16 && s.plan.xmode == F16_X_NHWC_PAIR) {  // f16 first conv + pool
+    if (s.c1sq) return {C1_POOL_F16_TILE};
+    return {EPOOL_TILE_BASE + 1, C1_POOL_F16_TILE};  // two launches (conversion + patch kernel) / one launch
+  }
+  if (s.epool || s.pool) return c;  // other f16 pooled epilogues / the pooled 1x1: one kernel
+  if (s.plan.x3) {  // the x3 tiles of the plan's kernel family (its packed layout)
+    for (int t = 0; t < 4; ++t) c.push_back(X3_TILE_BASE + t + (s.plan.x3 == 2 ? 4 : 0));
+    return c;
+  }
+  if (s.plan.wino) {
+    for (int t = 0; t < WINO_TILES_N; ++t) c.push_back(WINO_TILE_BASE + t);
+    return c;
+  }
+  for (int t = 0; t < 4; ++t) c.push_back(t);  // the LDS-staged conv_gemm tiles
+  // the LDS-free streaming kernel (f32 convs; launch_conv falls back to tile 0 where the geometry does
+  // not allow it)
+  if (!s.plan.f16 && s.kind == S_CONV)
+    for (int t = CONV_TILE_STREAM; t < CONV_TILES_F32; ++t) c.push_back(t);
+  return c;
+}
+
+// writes tile t into the step's plan (and the base step the next plan() copies from)
+void set_tile(ore_model* m, int k, int t) {
+  Step& s = m->steps[m->exec_steps[k]];
+  Step& b = m->base_steps[m->exec_steps[k]];
+  if (s.kind == S_CONV && s.epool) {
+    const int v = t == EPOOL_WIN_TILE ? EPOOL_WIN_VARIANT : t == C1_POOL_F16_TILE ? 0 : t - EPOOL_TILE_BASE;
+    s.plan.epv = b.plan.epv = v;
+    return;
+  }
+  s.plan.cfg = t;
+  if (s.plan.x3) b.plan_x3.cfg = t;
+  else if (s.plan.wino) b.plan_wino.cfg = t;
+  else b.plan.cfg = t;
+}
+
+}  // namespace
+
 extern "C" {
 
 ore_status ore_model_load(ore_ctx* ctx, const void* bytes, size_t len, int64_t max_batch, ore_model** out) {
@@ -1563,8 +1497,9 @@ ore_status ore_model_parse(const void* bytes, size_t len) {
 ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_t max_batch, int32_t flags,
                              ore_model** out) {
   if (!ctx || !bytes || !out || max_batch <= 0) return set_error(ctx, ORE_ERR_INVALID, "invalid argument");
-  if (flags & ~(ORE_LOAD_F16 | ORE_LOAD_X3 | ORE_LOAD_NO_WINOGRAD)) return set_error(ctx, ORE_ERR_INVALID, "unknown load flags 0x%x", unsigned(flags));
-  if ((flags & ORE_LOAD_F16) && (flags & ORE_LOAD_X3))
+  if (flags & ~(ORE_LOAD_F16 | ORE_LOAD_X3 | ORE_LOAD_NO_WINOGRAD | ORE_LOAD_X3_ALL))
+    return set_error(ctx, ORE_ERR_INVALID, "unknown load flags 0x%x", unsigned(flags));
+  if ((flags & ORE_LOAD_F16) && (flags & (ORE_LOAD_X3 | ORE_LOAD_X3_ALL)))
     return set_error(ctx, ORE_ERR_INVALID, "ORE_LOAD_F16 and ORE_LOAD_X3 are exclusive");
   ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
   Graph g;
@@ -1574,11 +1509,10 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
   m->ctx = ctx;
   m->max_batch = max_batch;
   m->f16 = (flags & ORE_LOAD_F16) != 0;
-  m->x3 = (flags & ORE_LOAD_X3) != 0;
-  m->x3_all = m->x3 && getenv("ORE_X3_ALL") && atoi(getenv("ORE_X3_ALL")) != 0;
-  // ORE_NO_WINOGRAD=1 (tests of the direct-kernel fusions, experiments) acts as ORE_LOAD_NO_WINOGRAD
-  m->wino = !m->f16 && !m->x3 && (flags & ORE_LOAD_NO_WINOGRAD) == 0 &&
-            !(getenv("ORE_NO_WINOGRAD") && atoi(getenv("ORE_NO_WINOGRAD")) != 0);
+  m->x3 = (flags & (ORE_LOAD_X3 | ORE_LOAD_X3_ALL)) != 0;
+  m->x3_all = (flags & ORE_LOAD_X3_ALL) != 0;
+  m->wino = !m->f16 && !m->x3 && (flags & ORE_LOAD_NO_WINOGRAD) == 0;
+  m->conv_tile = ctx->conv_tile;
   auto fail = [&](ore_status st) {
     ore_model_destroy(m);
     return st;
@@ -1645,28 +1579,28 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
     for (auto& s : m->base_steps) {
       if (s.kind == S_CONV) {
         // f16 operand mode by the input's layout: an f32 NCHW value (the model input: converted to
-        // NHWC4 when C <= 4), or NHWC f16 (16-B channel groups when C % 8 == 0)
-        const int first = f16_first_mode();
-        const int xmode = m->values[s.in0].es == 4 ? (s.C <= 4 && first == F16_X_NHWC_PAIR ? F16_X_NHWC_PAIR
-                                                      : s.C <= 8 && first == F16_X_NHWC8   ? F16_X_NHWC8
-                                                                                           : F16_X_NCHW32)
+        // NHWC4 when C <= 4, else gathered per element), or NHWC f16 (16-B channel groups when C % 8 == 0)
+        // (SqueezeNet conv1 at B = 256: NHWC4 pairs 355 us, per-element NCHW 459 us,
+        // profiles/r01p_f16_first_conv.txt)
+        const int xmode = m->values[s.in0].es == 4 ? (s.C <= 4 ? F16_X_NHWC_PAIR : F16_X_NCHW32)
                           : s.C % 8 == 0           ? F16_X_NHWC_VEC
                                                    : F16_X_NHWC_ELEM;
-        s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, m->f16, xmode);
+        s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, m->f16, xmode, false, false, m->conv_tile);
       }
       else if (s.kind == S_MATMUL)
-        s.plan = conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win);
+        s.plan = conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win, false, 0, false, false, m->conv_tile);
       else
         continue;
       total_packed += (packed_bytes(s.plan) + 255) / 256 * 256;
       if (m->x3 && x3_wanted(m, s)) {
         s.has_x3 = true;
-        s.plan_x3 = s.kind == S_CONV ? conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, false, 0, true)
-                                     : conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win, false, 0, true);
+        s.plan_x3 = s.kind == S_CONV
+                        ? conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, false, 0, true, false, m->conv_tile)
+                        : conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win, false, 0, true, false, m->conv_tile);
         total_packed += (packed_bytes(s.plan_x3) + 255) / 256 * 256;
       }
       if (m->wino && s.kind == S_CONV) {
-        s.plan_wino = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, false, 0, false, true);
+        s.plan_wino = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, false, 0, false, true, m->conv_tile);
         s.has_wino = s.plan_wino.wino != 0;
         if (s.has_wino) total_packed += (conv_packed_bytes(s.plan_wino) + 255) / 256 * 256;
       }
@@ -1681,7 +1615,7 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
         s.wp = reinterpret_cast<float*>(base);
         launch_pack(m->values[s.in1].cptr, s.w_kmajor, int(s.M), int(s.C), int(s.kh), int(s.kw), s.plan, s.wp,
                     ctx->stream);
-        s.ktab = s.plan.window ? nullptr : reinterpret_cast<int2*>(base + conv_packed_bytes(s.plan));
+        s.ktab = reinterpret_cast<int2*>(base + conv_packed_bytes(s.plan));
         poff += (packed_bytes(s.plan) + 255) / 256 * 256;
         if (s.has_x3) {
           char* bx = reinterpret_cast<char*>(m->packed) + poff;
@@ -1701,10 +1635,9 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
       if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
         return fail(set_error(ctx, ORE_ERR_HIP, "weight packing failed"));
     }
-    for (auto& s : m->base_steps)  // NHWC4 / NHWC8 copies of f32 inputs for the PAIR / NHWC8 gathers
-      if (s.kind == S_CONV && s.plan.f16 && (s.plan.xmode == F16_X_NHWC_PAIR || s.plan.xmode == F16_X_NHWC8) &&
-          hipMalloc(&s.xcvt, size_t(max_batch) * size_t(s.H * s.W) * (s.plan.xmode == F16_X_NHWC8 ? 8 : 4) *
-                                 sizeof(uint16_t)) != hipSuccess)
+    for (auto& s : m->base_steps)  // NHWC4 copies of f32 inputs for the PAIR gather
+      if (s.kind == S_CONV && s.plan.f16 && s.plan.xmode == F16_X_NHWC_PAIR &&
+          hipMalloc(&s.xcvt, size_t(max_batch) * size_t(s.H * s.W) * 4 * sizeof(uint16_t)) != hipSuccess)
         return fail(set_error(ctx, ORE_ERR_OOM, "input conversion buffer allocation failed"));
   }
   if (g.outputs.empty()) return fail(set_error(ctx, ORE_ERR_INVALID, "model has no outputs"));
@@ -1742,8 +1675,9 @@ ore_status ore_model_destroy(ore_model* m) {
 
 ore_status ore_model_set_fusion(ore_model* m, int32_t flags) {
   if (!m) return set_error(nullptr, ORE_ERR_INVALID, "null model");
-  m->fusion = flags & (ORE_FUSE_ALL | ORE_FUSE_POOL_CONV | ORE_FUSE_CONV_POOL | ORE_FUSE_FIRE | ORE_FUSE_CONCAT_POOL |
-                       ORE_KEEP_VALUES);
+  const int32_t known = ORE_FUSE_ALL | ORE_FUSE_EAGER | ORE_KEEP_VALUES;
+  if (flags & ~known) return set_error(m->ctx, ORE_ERR_INVALID, "unknown fusion flags 0x%x", unsigned(flags & ~known));
+  m->fusion = flags;
   return plan(m);
 }
 
@@ -1906,73 +1840,26 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
   ORE_HIP_CHECK(ctx, hipEventCreate(&e0));
   ORE_HIP_CHECK(ctx, hipEventCreate(&e1));
   ore_status st = ORE_OK;
-  // steps run in order so every conv sees its real input geometry; each candidate block tile
-  // is timed on the step's own buffers and the fastest kept (results do not depend on the tile:
-  // every output is the same k-ordered MFMA chain)
+  // steps run in order so every conv sees its real input geometry; each candidate tile is timed on
+  // the step's own buffers and the fastest kept (results do not depend on the tile: every output is
+  // the same k-ordered MFMA chain, every pooled value the same max)
   for (size_t k = 0; k < m->exec_steps.size() && !st; ++k) {
     Step& s = m->steps[m->exec_steps[k]];
-    if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.c1sq) {  // the fused squeeze: the window kernel only
-      s.plan.epv = EPOOL_WIN_VARIANT;
-      m->base_steps[m->exec_steps[k]].plan.epv = EPOOL_WIN_VARIANT;
+    const std::vector<int> cands = step_tile_family(s);
+    if (cands.size() < 2) {
+      if (cands.size() == 1) set_tile(m, int(k), cands[0]);
       st = launch_step(m, s, n);
       continue;
     }
-    if (s.kind == S_CONV && s.epool && !s.plan.f16) {  // f32 pooled conv: patch vs row-walk kernels
-      int best = 0;
-      float best_ms = 1e30f;
-      // variant 6 (two 4-wave blocks per CU) wins this isolated timing on conv1 but loses inside the
-      // graph (963 vs 913 us, profiles/r01zg_conv1_walk96_b2.txt): forced only (ORE_CONV_POOL_STREAM=5)
-      for (int v : {1, 2, 3, 4, 5, EPOOL_WIN_VARIANT}) {
-        if (st) break;
-        s.plan.epv = v;
-        last_conv_tile = -1;
-        st = launch_step(m, s, n);  // warm-up
-        if (st || last_conv_tile != epool_tile_id(v)) continue;  // not eligible here
-        if (hipEventRecord(e0, ctx->stream) != hipSuccess) { st = set_error(ctx, ORE_ERR_HIP, "event record"); break; }
-        for (int r = 0; r < reps && !st; ++r) st = launch_step(m, s, n);
-        float ms = 0.f;
-        if (st || hipEventRecord(e1, ctx->stream) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
-            hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
-          if (!st) st = set_error(ctx, ORE_ERR_HIP, "autotune timing failed");
-          break;
-        }
-        if (ms < best_ms) { best_ms = ms; best = v; }
-      }
-      s.plan.epv = best;
-      m->base_steps[m->exec_steps[k]].plan.epv = best;
-      if (!st) st = launch_step(m, s, n);
-      continue;
-    }
-    if (s.kind != S_CONV || s.plan.window || s.epool) {  // f16 pooled epilogue: one tile shape
-      st = launch_step(m, s, n);
-      continue;
-    }
-    int best = s.plan.cfg;
+    int best = -1;
     float best_ms = 1e30f;
-    // candidates: the four LDS-staged tiles and, for f32, their warp-specialised forms (8-11: they
-    // win on the long-K, few-row 1x1 squeezes, e.g. fire7/8 113 -> 97 us); ORE_AUTOTUNE_WS=0 drops them
-    std::vector<int> cands = {0, 1, 2, 3};
-    const char* ews = getenv("ORE_AUTOTUNE_WS");
-    if (s.plan.x3) {  // the x3 tiles of the plan's kernel family only (its packed layout)
-      cands.clear();
-      for (int c = 0; c < 4; ++c) cands.push_back(X3_TILE_BASE + c + (s.plan.x3 == 2 ? 4 : 0));
-    } else if (s.plan.wino) {  // the Winograd tiles (its packed layout); tile 4 (LDS-staged) measured
-      // slower on every SqueezeNet expand3x3 (profiles/r02c_wino_tiles.txt): forced only (ORE_WINO_TILE=4)
-      cands.clear();
-      for (int c = 0; c < 4; ++c)
-        if (s.e1_out < 0 || c == 2) cands.push_back(WINO_TILE_BASE + c);  // a fused 1x1 conv: tile 2 only
-    } else if (!s.plan.f16 && !(ews && !atoi(ews))) cands.insert(cands.end(), {8, 9, 10, 11});
-    // the LDS-free streaming kernel (tiles 12-20) where the geometry allows it (launch_conv falls
-    // back to tile 0 elsewhere, and such candidates are skipped below)
-    if (!s.plan.f16 && !s.plan.x3 && !s.plan.wino && s.kind == S_CONV && !s.pool)
-      for (int c = CONV_TILE_STREAM; c < CONV_TILES_F32; ++c) cands.push_back(c);
     for (size_t ci = 0; ci < cands.size() && !st; ++ci) {
       const int c = cands[ci];
-      s.plan.cfg = c;
+      set_tile(m, int(k), c);
       last_conv_tile = -1;
       st = launch_step(m, s, n);  // warm-up
       if (st) break;
-      if (last_conv_tile != c) continue;  // fell back to another tile: not a distinct candidate
+      if (last_conv_tile != c) continue;  // fell back to another kernel: not a distinct candidate here
       if (hipEventRecord(e0, ctx->stream) != hipSuccess) { st = set_error(ctx, ORE_ERR_HIP, "event record"); break; }
       for (int r = 0; r < reps && !st; ++r) st = launch_step(m, s, n);
       if (st) break;
@@ -1984,12 +1871,8 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
       }
       if (ms < best_ms) { best_ms = ms; best = c; }
     }
-    s.plan.cfg = best;
-    // steps are a per-plan copy of base_steps
-    if (s.plan.x3) m->base_steps[m->exec_steps[k]].plan_x3.cfg = best;
-    else if (s.plan.wino) m->base_steps[m->exec_steps[k]].plan_wino.cfg = best;
-    else m->base_steps[m->exec_steps[k]].plan.cfg = best;
-    if (!st) st = launch_step(m, s, n);                // leave the real output for the next step
+    if (best >= 0) set_tile(m, int(k), best);
+    if (!st) st = launch_step(m, s, n);  // leave the real output for the next step
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
@@ -2000,14 +1883,28 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
 int32_t ore_model_step_tile(ore_model* m, int32_t i) {
   if (!m || i < 0 || size_t(i) >= m->exec_steps.size()) return -1;
   const Step& s = m->steps[m->exec_steps[i]];
-  if (s.kind == S_FIRE)  // "fire" / "fire wino" / "fire f16" / "fire pool f32": the fused fire kernels (ore.Model.TILE_NAMES)
-    return s.fire_f16 ? WINO_TILE_BASE + WINO_TILES_N + 1
-           : s.fire_wino ? WINO_TILE_BASE + WINO_TILES_N
-           : s.fire_pool ? FIRE_POOL_TILE
-                         : CONV_TILES_F32;
+  if (s.kind == S_FIRE) return s.fire_f16 ? FIRE_F16_TILE : s.fire_pool ? FIRE_POOL_TILE : FIRE_TILE;
   if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.plan.epv > 0) return epool_tile_id(s.plan.epv);
   if (s.kind == S_CONV && s.epool && s.ran_tile >= 0) return s.ran_tile;
   return (s.kind == S_CONV || s.kind == S_MATMUL) ? s.plan.cfg : -1;
+}
+
+ore_status ore_model_set_step_tile(ore_model* m, int32_t i, int32_t tile) {
+  if (!m || i < 0 || size_t(i) >= m->exec_steps.size()) return set_error(m ? m->ctx : nullptr, ORE_ERR_INVALID, "bad step index");
+  const std::vector<int> fam = step_tile_family(m->steps[m->exec_steps[i]]);
+  if (std::find(fam.begin(), fam.end(), int(tile)) == fam.end())
+    return set_error(m->ctx, ORE_ERR_INVALID, "tile %d is not a kernel of step %d ('%s')", int(tile), int(i),
+                     m->steps[m->exec_steps[i]].name.c_str());
+  set_tile(m, i, tile);
+  return ORE_OK;
+}
+
+ore_status ore_model_step_mfma_flops(ore_model* m, int32_t i, double* flops) {
+  if (!m || !flops || i < 0 || size_t(i) >= m->exec_steps.size())
+    return set_error(m ? m->ctx : nullptr, ORE_ERR_INVALID, "bad step index");
+  const Step& s = m->steps[m->exec_steps[i]];
+  *flops = (s.mfma_flops_per_img >= 0 ? s.mfma_flops_per_img : s.flops_per_img) * double(m->last_n);
+  return ORE_OK;
 }
 
 ore_status ore_model_set_streams(ore_model* m, int32_t streams) {

@@ -98,15 +98,28 @@ static bool contiguous(const ore_tensor* t) {
 
 static bool fits_i32(int64_t v) { return v >= 0 && v < (int64_t(1) << 31); }
 
-ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
-                   const Window& win, bool f16, int xmode, bool x3, bool wino) {
-  return plan_conv(int(M), int(C), int(H), int(W), int(kh), int(kw), int(sh), int(sw), int(win.pt), int(win.pl),
-                   int(win.Ho), int(win.Wo), kh == 1 && kw == 1, f16, xmode, x3, wino);
+// The kernels address activations through buffer resources (32-bit byte offsets, plus up to a few KB
+// read before x by the 3x3 tap loads): a batch whose input or output extent does not fit is launched
+// in image chunks that do.  Returns the images per chunk (0: one image alone is too large).
+constexpr int64_t CHUNK_LIMIT = (int64_t(1) << 31) - (int64_t(1) << 21);
+static int64_t image_chunk(int64_t N, int64_t x_nstride, int64_t x_img_bytes, int x_es, int64_t y_nstride,
+                           int64_t y_img_bytes, int y_es) {
+  auto fits = [&](int64_t nb) {
+    return (nb - 1) * x_nstride * x_es + x_img_bytes < CHUNK_LIMIT && (nb - 1) * y_nstride * y_es + y_img_bytes < CHUNK_LIMIT;
+  };
+  if (!fits(1)) return 0;
+  int64_t nb = N;
+  while (nb > 1 && !fits(nb)) nb = (nb + 1) / 2;
+  return nb;
 }
 
-size_t packed_bytes(const ConvPlan& pln) {
-  return conv_packed_bytes(pln) + size_t(pln.window ? 0 : pln.krows) * sizeof(int2);
+ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
+                   const Window& win, bool f16, int xmode, bool x3, bool wino, int forced) {
+  return plan_conv(int(M), int(C), int(H), int(W), int(kh), int(kw), int(sh), int(sw), int(win.pt), int(win.pl),
+                   int(win.Ho), int(win.Wo), kh == 1 && kw == 1, f16, xmode, x3, wino, forced);
 }
+
+size_t packed_bytes(const ConvPlan& pln) { return conv_packed_bytes(pln) + size_t(pln.krows) * sizeof(int2); }
 
 float* pack_to_scratch(ore_ctx* ctx, const ConvPlan& pln, const float* w, bool kmajor_src, int64_t M, int64_t C,
                        int64_t kh, int64_t kw, int64_t H, int64_t W, const int2** ktab) {
@@ -125,11 +138,8 @@ float* pack_to_scratch(ore_ctx* ctx, const ConvPlan& pln, const float* w, bool k
     ctx->scratch_bytes = need;
   }
   launch_pack(w, kmajor_src, int(M), int(C), int(kh), int(kw), pln, ctx->scratch, ctx->stream);
-  int2* kt = nullptr;
-  if (!pln.window) {
-    kt = reinterpret_cast<int2*>(reinterpret_cast<char*>(ctx->scratch) + conv_packed_bytes(pln));
-    launch_ktab(kt, int(C * kh * kw), int(kh), int(kw), int(H * W), int(W), ctx->stream);
-  }
+  int2* kt = reinterpret_cast<int2*>(reinterpret_cast<char*>(ctx->scratch) + conv_packed_bytes(pln));
+  launch_ktab(kt, int(C * kh * kw), int(kh), int(kw), int(H * W), int(W), ctx->stream);
   if (hipGetLastError() != hipSuccess) {
     set_error(ctx, ORE_ERR_HIP, "weight packing launch failed");
     return nullptr;
@@ -141,10 +151,9 @@ float* pack_to_scratch(ore_ctx* ctx, const ConvPlan& pln, const float* w, bool k
 ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
                     int64_t x_nstride, const float* wp, const int2* ktab, int64_t M, int64_t kh, int64_t kw,
                     const float* bias, const Window& win, int64_t sh, int64_t sw, bool relu, float* y,
-                    int64_t y_nstride, int64_t x_ps, int64_t y_ps, int x_es, const ConvE1* e1) {
+                    int64_t y_nstride, int64_t x_ps, int64_t y_ps, int x_es) {
   if (N == 0) return ORE_OK;
   if (pln.f16 || x_es != 4) return set_error(ctx, ORE_ERR_INVALID, "internal: run_conv takes f32 plans and inputs");
-  if (e1 && !pln.wino) return set_error(ctx, ORE_ERR_INVALID, "internal: a fused 1x1 conv needs a Winograd plan");
   if (x_ps == 0) x_ps = H * W;
   if (y_ps == 0) y_ps = win.Ho * win.Wo;
   ConvParams p{};
@@ -163,16 +172,8 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
   p.relu = relu ? 1 : 0;
   p.Mp = pln.Mp;
   p.x_f32 = 1;
-  if (e1) {
-    p.e1_wp = e1->wp; p.e1_bias = e1->bias; p.e1_y = e1->y; p.e1_Mp = int(e1->Mp); p.e1_relu = e1->relu ? 1 : 0;
-  }
-  {  // extent of x for the B-tile DMA path's buffer resource (32-bit byte offsets)
-    const int64_t extent = ((N - 1) * x_nstride + C * x_ps) * int64_t(x_es);
-    p.x_bytes = (extent > 0 && extent < (int64_t(1) << 31)) ? extent : 0;
-  }
   // 16-B epilogue stores of 4 floats
   p.vec_out = (y_ps % 4 == 0 && y_nstride % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
-  if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;  // tuning knob
   p.is1x1 = (kh == 1 && kw == 1 && sh == 1 && sw == 1 && win.pt == 0 && win.pl == 0 && win.Ho == H && win.Wo == W &&
              x_ps == y_ps);
   {  // mapped bytes before x: the rest of x's 4 KiB page, or the walker's arena lead
@@ -185,45 +186,39 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
   if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(int64_t(pln.krows) * pln.Mp) ||
       !fits_i32(p.Ntot + 256) || (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))
     return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
-  if (!pln.window && !pln.wino && !p.is1x1 && !ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
-  if (pln.x3 || pln.wino) {
-    // the x3 / Winograd kernels address x through a buffer resource (32-bit byte offsets): a batch
-    // whose input extent does not fit runs in image chunks that do
-    if (pln.x3 && !p.is1x1 && p.kh * p.kw > 64) return set_error(ctx, ORE_ERR_UNSUPPORTED, "x3 conv: more than 64 taps");
-    const int64_t lim = pln.wino ? (int64_t(1) << 31) - (int64_t(1) << 21) : int64_t(1) << 31;
-    int64_t nb = N;
-    while (nb > 1 && ((nb - 1) * x_nstride + C * x_ps) * 4 >= lim) nb = (nb + 1) / 2;
-    if ((C * x_ps) * 4 >= lim) return set_error(ctx, ORE_ERR_UNSUPPORTED, "x3 / Winograd conv: one image exceeds 2 GiB");
-    for (int64_t i0 = 0; i0 < N; i0 += nb) {
-      const int64_t nc = std::min(nb, N - i0);
-      ConvParams q = p;
-      q.x = x + i0 * x_nstride;
-      q.y = y + i0 * y_nstride;
-      q.N = int(nc);
-      q.Ntot = nc * y_ps;
-      q.x_bytes = ((nc - 1) * x_nstride + C * x_ps) * 4;
-      if (e1) {
-        q.e1_y = e1->y + i0 * y_nstride;
-        if (!conv_wino_e1_eligible(q, 2))
-          return set_error(ctx, ORE_ERR_INVALID, "internal: fused 1x1 conv outside the Winograd 32x32 kernels' limits");
-      }
-      launch_conv(q, pln, ctx->stream);
-      ORE_HIP_CHECK(ctx, hipGetLastError());
+  if (!pln.wino && !p.is1x1 && !ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
+  if (pln.x3 && !p.is1x1 && p.kh * p.kw > 64) return set_error(ctx, ORE_ERR_UNSUPPORTED, "x3 conv: more than 64 taps");
+  // image chunks whose x and y extents fit 32-bit byte offsets (the output may be a slice of a wider
+  // concat buffer, e.g. an expand3x3 writing channels 256..511 of 512)
+  const int64_t nb = image_chunk(N, x_nstride, C * x_ps * 4, 4, y_nstride, M * y_ps * 4, 4);
+  if (nb == 0) return set_error(ctx, ORE_ERR_UNSUPPORTED, "conv: one image exceeds 2 GiB");
+  for (int64_t i0 = 0; i0 < N; i0 += nb) {
+    const int64_t nc = std::min(nb, N - i0);
+    ConvParams q = p;
+    q.x = x + i0 * x_nstride;
+    q.y = y + i0 * y_nstride;
+    q.N = int(nc);
+    q.Ntot = nc * y_ps;
+    q.x_bytes = ((nc - 1) * x_nstride + C * x_ps) * 4;
+    ConvPlan qp = pln;
+    if (pln.wino && !conv_wino_eligible(q, qp.cfg - WINO_TILE_BASE)) {  // the first tile that takes it
+      int t = 0;
+      while (t < WINO_TILES_N && !conv_wino_eligible(q, t)) ++t;
+      if (t == WINO_TILES_N) return set_error(ctx, ORE_ERR_UNSUPPORTED, "Winograd conv: no tile takes this layout");
+      qp.cfg = WINO_TILE_BASE + t;
     }
-    return ORE_OK;
+    launch_conv(q, qp, ctx->stream);
+    ORE_HIP_CHECK(ctx, hipGetLastError());
   }
-  launch_conv(p, pln, ctx->stream);
-  ORE_HIP_CHECK(ctx, hipGetLastError());
   return ORE_OK;
 }
 
 ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int64_t x_nstride,
                     int64_t x_ps, const float* w1, const float* b1, int64_t E1, const float* w3, const float* b3,
                     int64_t E3, const float* ws, int64_t Msp, const float* bs, int64_t Ms, float* y, int64_t y_nstride,
-                    int64_t y_ps, bool wino, const Window* pool) {
+                    int64_t y_ps, const Window* pool) {
   if (N == 0) return ORE_OK;
   FireParams p{};
-  p.wino = wino ? 1 : 0;
   p.x = x; p.w1 = w1; p.b1 = b1; p.w3 = w3; p.b3 = b3; p.ws = ws; p.bs = bs; p.y = y;
   p.N = int(N); p.C = int(C); p.H = int(H); p.W = int(W);
   p.E1 = int(E1); p.E3 = int(E3); p.Ms = int(Ms); p.Msp = int(Msp);
@@ -233,10 +228,8 @@ ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t 
   if (pool) {
     p.pool = 1;
     p.Hp = int(pool->Ho); p.Wp = int(pool->Wo); p.ppt = int(pool->pt); p.ppl = int(pool->pl);
-    if (wino || !fire_pool_plan(&p)) return set_error(ctx, ORE_ERR_INVALID, "internal: no band shape for the pooled fire module");
+    if (!fire_pool_plan(&p)) return set_error(ctx, ORE_ERR_INVALID, "internal: no band shape for the pooled fire module");
   }
-  const int64_t extent = ((N - 1) * x_nstride + C * x_ps) * 4;
-  p.x_bytes = (extent > 0 && extent < (int64_t(1) << 31)) ? extent : 0;
   {  // mapped bytes before x (as run_conv): the rest of x's page or the walker's arena lead
     const char* xc = reinterpret_cast<const char*>(x);
     int64_t g = int64_t(reinterpret_cast<uintptr_t>(x) & 4095);
@@ -248,15 +241,22 @@ ore_status run_fire(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64_t 
   if (x_ps < H * W || y_ps < (pool ? pool->Ho * pool->Wo : H * W) || !fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) ||
       !fits_i32(p.Ntot + 256))
     return set_error(ctx, ORE_ERR_INVALID, "fire geometry exceeds 32-bit indexing");
-  if (p.wino) {
-    if (!fire_wino_eligible(p)) return set_error(ctx, ORE_ERR_INVALID, "internal: Winograd fire module on an unsupported layout");
-    launch_fire_wino(p, ctx->stream);
+  // the kernels address x through a buffer resource (32-bit byte offsets, plus the x_lead bytes before
+  // it): a batch whose input extent does not fit runs in image chunks that do
+  const int64_t nb = image_chunk(N, x_nstride, C * x_ps * 4, 4, y_nstride, Ms * y_ps * 4, 4);
+  if (nb == 0) return set_error(ctx, ORE_ERR_UNSUPPORTED, "fused fire module: one image exceeds 2 GiB");
+  for (int64_t i0 = 0; i0 < N; i0 += nb) {
+    const int64_t nc = std::min(nb, N - i0);
+    FireParams q = p;
+    q.x = x + i0 * x_nstride;
+    q.y = y + i0 * y_nstride;
+    q.N = int(nc);
+    q.Ntot = nc * y_ps;
+    q.x_bytes = ((nc - 1) * x_nstride + C * x_ps) * 4;
+    if (!fire_eligible(q)) return set_error(ctx, ORE_ERR_INVALID, "internal: fused fire module on an unsupported layout");
+    launch_fire(q, ctx->stream);
     ORE_HIP_CHECK(ctx, hipGetLastError());
-    return ORE_OK;
   }
-  if (!fire_eligible(p)) return set_error(ctx, ORE_ERR_INVALID, "internal: fused fire module on an unsupported layout");
-  launch_fire(p, ctx->stream);
-  ORE_HIP_CHECK(ctx, hipGetLastError());
   return ORE_OK;
 }
 
@@ -299,7 +299,7 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
                           int64_t pkh, int64_t pkw, int64_t psh, int64_t psw, const Window& pwin, float* y,
                           int64_t y_nstride, int64_t y_ps, const float* wc1, const C1SqueezeF32* sq1) {
   if (N == 0) return ORE_OK;
-  if (pln.f16 || pln.window) return set_error(ctx, ORE_ERR_INVALID, "internal: the pooled epilogue is f32 gather only");
+  if (pln.f16) return set_error(ctx, ORE_ERR_INVALID, "internal: the pooled epilogue is f32 gather only");
   if (x_ps == 0) x_ps = H * W;
   if (y_ps == 0) y_ps = pwin.Ho * pwin.Wo;
   int tr = 0, tc = 0;
@@ -320,10 +320,6 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
   p.relu = relu ? 1 : 0;
   p.Mp = pln.Mp;
   p.x_f32 = 1;
-  {
-    const int64_t extent = ((N - 1) * x_nstride + C * x_ps) * 4;
-    p.x_bytes = (extent > 0 && extent < (int64_t(1) << 31)) ? extent : 0;
-  }
   p.is1x1 = (kh == 1 && kw == 1 && sh == 1 && sw == 1 && win.pt == 0 && win.pl == 0 && win.Ho == H && win.Wo == W &&
              x_ps == H * W);
   p.ep_pt = int(pwin.pt); p.ep_pl = int(pwin.pl); p.ep_Ho = int(pwin.Ho); p.ep_Wo = int(pwin.Wo);
@@ -344,10 +340,28 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
       !fits_i32(p.Ntot + 256) || N * p.ep_tr * p.ep_tc * ((M + 31) / 32) >= (int64_t(1) << 31))
     return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
   if (!p.is1x1 && !ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
-  launch_conv_epool(p, ctx->stream);
-  ORE_HIP_CHECK(ctx, hipGetLastError());
-  if (sq1 && last_conv_tile != EPOOL_WIN_TILE)
-    return set_error(ctx, ORE_ERR_INVALID, "internal: the fused first conv + squeeze declined its launch");
+  const int64_t y_img = sq1 ? (sq1->M * int64_t(sq1->y_ps)) * 4 : M * y_ps * 4;
+  const int64_t nb = image_chunk(N, x_nstride, C * x_ps * 4, 4, sq1 ? sq1->y_nstride : y_nstride, y_img, 4);
+  if (nb == 0) return set_error(ctx, ORE_ERR_UNSUPPORTED, "pooled conv: one image exceeds 2 GiB");
+  for (int64_t i0 = 0; i0 < N; i0 += nb) {
+    const int64_t nc = std::min(nb, N - i0);
+    ConvParams q = p;
+    C1SqueezeF32 sq{};
+    q.x = x + i0 * x_nstride;
+    if (y) q.y = y + i0 * y_nstride;
+    if (sq1) {
+      sq = *sq1;
+      sq.y = sq1->y + i0 * sq1->y_nstride;
+      q.sq1 = &sq;
+    }
+    q.N = int(nc);
+    q.Ntot = nc * int64_t(p.ep_tr) * p.ep_tc * CONV_EPOOL_BN;
+    q.x_bytes = ((nc - 1) * x_nstride + C * x_ps) * 4;
+    launch_conv_epool(q, ctx->stream);
+    ORE_HIP_CHECK(ctx, hipGetLastError());
+    if (sq1 && last_conv_tile != EPOOL_WIN_TILE)
+      return set_error(ctx, ORE_ERR_INVALID, "internal: the fused first conv + squeeze declined its launch");
+  }
   return ORE_OK;
 }
 
@@ -359,50 +373,20 @@ ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int6
   if (x_ps == 0) x_ps = pH * pW;
   const int64_t P = pwin.Ho * pwin.Wo;
   if (y_ps == 0) y_ps = P;
-  if (pln.f16 || x_es != 4) return set_error(ctx, ORE_ERR_INVALID, "internal: the pooled 1x1 conv is f32 only");
-  {  // 3x3 / stride-2 pools: pool_conv1x1_f32_kernel (LDS-staged rows, MFMA squeeze), else the gather
-    PoolConvParams q{};
-    q.x = x; q.wp = wp; q.bias = bias; q.y = y;
-    q.N = int(N); q.C = int(C); q.H = int(pH); q.W = int(pW); q.Hp = int(pwin.Ho); q.Wp = int(pwin.Wo);
-    q.pt = int(pwin.pt); q.pl = int(pwin.pl); q.M = int(M); q.Mp = pln.Mp; q.Kp = pln.krows;
-    q.x_ps = int(x_ps); q.y_ps = int(y_ps); q.x_nstride = x_nstride; q.y_nstride = y_nstride;
-    q.relu = relu ? 1 : 0;
-    const char* e = getenv("ORE_POOL_CONV_GATHER");  // experiments: the conv-gather kernel instead
-    if (psh == 2 && psw == 2 && pwin.Ho > 0 && !(e && atoi(e) != 0) && fits_i32(x_nstride * N + 256) &&
-        fits_i32(y_nstride * N + 256) && pool_conv1x1_f32_eligible(q) && !pln.window && !pln.x3 && !pln.wino) {
-      // the 3x3 window is implied by the (1b) / (1j) plan (kernel_shape 3x3)
-      launch_pool_conv1x1_f32(q, ctx->stream);
-      ORE_HIP_CHECK(ctx, hipGetLastError());
-      return ORE_OK;
-    }
-  }
-  ConvParams p{};
-  p.x = x; p.wp = wp; p.ktab = nullptr; p.bias = bias; p.y = y;
-  p.N = int(N); p.C = int(C); p.H = int(pwin.Ho); p.W = int(pwin.Wo);
-  p.M = int(M); p.kh = 1; p.kw = 1; p.sh = 1; p.sw = 1; p.pt = 0; p.pl = 0;
-  p.Ho = int(pwin.Ho); p.Wo = int(pwin.Wo);
-  p.K = int(C);
-  p.P = int(P);
-  p.x_ps = int(x_ps);
-  p.y_ps = int(y_ps);
-  p.Ntot = N * y_ps;
-  p.x_nstride = x_nstride;
-  p.y_nstride = y_nstride;
-  p.relu = relu ? 1 : 0;
-  p.is1x1 = 0;
-  p.Mp = pln.Mp;
-  p.x_f32 = 1;
-  p.x_bytes = 0;  // register path: the window max needs the values
-  p.vec_out = (y_ps % 4 == 0 && y_nstride % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
-  if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;
-  p.pool = 1;
-  p.pool_sh = int(psh); p.pool_sw = int(psw); p.pool_pt = int(pwin.pt); p.pool_pl = int(pwin.pl);
-  p.pool_H = int(pH); p.pool_W = int(pW);
-  if (x_ps < pH * pW || y_ps < P) return set_error(ctx, ORE_ERR_INVALID, "plane stride below plane size");
-  if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(int64_t(pln.krows) * pln.Mp) ||
-      !fits_i32(p.Ntot + 256))
-    return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
-  launch_conv(p, pln, ctx->stream);
+  if (pln.f16 || pln.x3 || pln.wino || x_es != 4)
+    return set_error(ctx, ORE_ERR_INVALID, "internal: the pooled 1x1 conv is f32 direct only");
+  // 3x3 / stride-2 pools (the window is implied by the walker's pass, kernel_shape 3x3):
+  // pool_conv1x1_f32_kernel (LDS-staged rows, MFMA squeeze)
+  PoolConvParams q{};
+  q.x = x; q.wp = wp; q.bias = bias; q.y = y;
+  q.N = int(N); q.C = int(C); q.H = int(pH); q.W = int(pW); q.Hp = int(pwin.Ho); q.Wp = int(pwin.Wo);
+  q.pt = int(pwin.pt); q.pl = int(pwin.pl); q.M = int(M); q.Mp = pln.Mp; q.Kp = pln.krows;
+  q.x_ps = int(x_ps); q.y_ps = int(y_ps); q.x_nstride = x_nstride; q.y_nstride = y_nstride;
+  q.relu = relu ? 1 : 0;
+  if (psh != 2 || psw != 2 || pwin.Ho <= 0 || !fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) ||
+      !pool_conv1x1_f32_eligible(q))
+    return set_error(ctx, ORE_ERR_INVALID, "internal: pooled 1x1 conv outside pool_conv1x1_f32_kernel's limits");
+  launch_pool_conv1x1_f32(q, ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());
   return ORE_OK;
 }
@@ -413,9 +397,6 @@ ore_status run_conv_pair_pool_f16(ore_ctx* ctx, const ConvPlan& pln, const float
                                   void* y, int64_t y_nstride, int64_t y_ps, const F16Epool& ep, bool* ran,
                                   const C1Squeeze* sq) {
   *ran = false;
-  if (getenv("ORE_DEBUG_C1")) fprintf(stderr, "c1pool: xmode %d ep %lldx%lld\n", pln.xmode, (long long)ep.kh, (long long)ep.kw);
-  if (const char* e = getenv("ORE_F16_C1POOL"))
-    if (atoi(e) == 0 && !sq) return ORE_OK;
   if (N == 0 || !pln.f16 || pln.xmode != F16_X_NHWC_PAIR) return ORE_OK;
   if (x_ps == 0) x_ps = H * W;
   if (y_ps == 0) y_ps = M;
@@ -435,13 +416,7 @@ ore_status run_conv_pair_pool_f16(ore_ctx* ctx, const ConvPlan& pln, const float
   p.Mp = pln.Mp;
   p.ep_pt = int(ep.win.pt); p.ep_pl = int(ep.win.pl); p.ep_Ho = int(ep.win.Ho); p.ep_Wo = int(ep.win.Wo);
   p.ep_tr = tr; p.ep_tc = tc;
-  if (!conv_pair_pool_f16_eligible(p, sq)) {
-    if (getenv("ORE_DEBUG_C1"))
-      fprintf(stderr, "c1pool ineligible: C %d H %d W %d M %d k %dx%d s %d,%d p %d,%d K %d Mp %d x_ps %d y_ps %d yns %lld y %p wp %p tr %d tc %d\n",
-              p.C, p.H, p.W, p.M, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.K, p.Mp, p.x_ps, p.y_ps, p.y_nstride,
-              static_cast<void*>(p.y), static_cast<const void*>(p.wp), p.ep_tr, p.ep_tc);
-    return ORE_OK;
-  }
+  if (!conv_pair_pool_f16_eligible(p, sq)) return ORE_OK;
   launch_conv_pair_pool_f16(p, sq, ctx->stream);
   ORE_HIP_CHECK(ctx, hipGetLastError());
   *ran = true;
@@ -455,13 +430,6 @@ ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_
   if (N == 0) return ORE_OK;
   if (!pln.f16) return set_error(ctx, ORE_ERR_INVALID, "internal: run_conv_f16 needs an f16 plan");
   const bool nchw = pln.xmode == F16_X_NCHW32;
-  if (pln.xmode == F16_X_NHWC8) {  // the converted input: 8 channels (>= C zero), the 16-B gather
-    if (C > 8 || x_ps != 8) return set_error(ctx, ORE_ERR_INVALID, "internal: the NHWC8 gather needs an NHWC8 input");
-    ConvPlan q = pln;
-    q.xmode = F16_X_NHWC_VEC;
-    return run_conv_f16(ctx, q, x, N, 8, H, W, x_nstride, x_ps, wp, ktab, M, kh, kw, bias, win, sh, sw, relu, y,
-                        y_nstride, y_ps, ep);
-  }
   if (x_ps == 0) x_ps = nchw ? H * W : C;
   if (y_ps == 0) y_ps = M;
   if (nchw ? x_ps < H * W : x_ps < C) return set_error(ctx, ORE_ERR_INVALID, "input stride below its extent");
@@ -490,11 +458,6 @@ ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_
   p.Mp = pln.Mp;
   p.x_f32 = nchw ? 1 : 0;
   p.vec_out = (M % 8 == 0 && y_ps % 8 == 0 && y_nstride % 8 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) ? 1 : 0;
-  if (pln.xmode == F16_X_NHWC_VEC) {  // extent of x for the LDS-DMA kernel's buffer resource
-    const int64_t extent = ((N - 1) * x_nstride + H * W * x_ps) * 2;
-    p.x_bytes = (extent > 0 && extent < (int64_t(1) << 31)) ? extent : 0;
-  }
-  if (const char* e = getenv("ORE_CONV_VEC_OUT")) p.vec_out &= atoi(e) != 0;  // tuning knob
   if (ep) {  // pooled epilogue: y is the pool's NHWC output [pwin.Ho][pwin.Wo]
     int tr = 0, tc = 0;
     if (epool_tile(win.Ho, win.Wo, ep->kh, ep->kw, ep->sh, ep->sw, ep->win, &tr, &tc) == 0.0)
@@ -506,11 +469,27 @@ ore_status run_conv_f16(ore_ctx* ctx, const ConvPlan& pln, const void* x, int64_
   if (!fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) || !fits_i32(int64_t(pln.krows) * pln.Mp) ||
       !fits_i32(p.Ntot + 256) || (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))
     return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
-  if (ep)
-    launch_conv_f16_epool(p, pln.xmode, ctx->stream);
-  else
-    launch_conv(p, pln, ctx->stream);
-  ORE_HIP_CHECK(ctx, hipGetLastError());
+  // image chunks whose extents fit the kernels' 32-bit byte offsets (the NHWC_VEC kernel reads x
+  // through a buffer resource)
+  const int xes = nchw ? 4 : 2;
+  const int64_t x_img = (nchw ? C * x_ps : H * W * x_ps) * xes;
+  const int64_t y_img = (ep ? ep->win.Ho * ep->win.Wo : win.Ho * win.Wo) * y_ps * 2;
+  const int64_t nb = image_chunk(N, x_nstride, x_img, xes, y_nstride, y_img, 2);
+  if (nb == 0) return set_error(ctx, ORE_ERR_UNSUPPORTED, "f16 conv: one image exceeds 2 GiB");
+  for (int64_t i0 = 0; i0 < N; i0 += nb) {
+    const int64_t nc = std::min(nb, N - i0);
+    ConvParams q = p;
+    q.x = reinterpret_cast<const float*>(static_cast<const char*>(x) + i0 * x_nstride * xes);
+    q.y = reinterpret_cast<float*>(static_cast<char*>(y) + i0 * y_nstride * 2);
+    q.N = int(nc);
+    q.Ntot = ep ? nc * int64_t(p.ep_tr) * p.ep_tc * CONV_EPOOL_BN : nc * p.P;
+    q.x_bytes = (nc - 1) * x_nstride * xes + x_img;
+    if (ep)
+      launch_conv_f16_epool(q, pln.xmode, ctx->stream);
+    else
+      launch_conv(q, pln, ctx->stream);
+    ORE_HIP_CHECK(ctx, hipGetLastError());
+  }
   return ORE_OK;
 }
 
@@ -537,6 +516,7 @@ ore_status run_maxpool(ore_ctx* ctx, const float* x, int64_t N, int64_t C, int64
   if (N == 0) return ORE_OK;
   PoolParams p{};
   p.es = es;
+  p.variant = ctx->pool_variant;
   p.x_ps = int(x_ps ? x_ps : H * W);
   p.y_ps = int(y_ps ? y_ps : win.Ho * win.Wo);
   p.x = x; p.y = y;
@@ -598,6 +578,21 @@ ore_status ore_ctx_set_conv_algo(ore_ctx* ctx, int32_t algo) {
   if (algo != ORE_CONV_ALGO_DIRECT && algo != ORE_CONV_ALGO_WINOGRAD)
     return set_error(ctx, ORE_ERR_INVALID, "unknown conv algorithm %d", int(algo));
   ctx->conv_algo = algo;
+  return ORE_OK;
+}
+
+ore_status ore_ctx_set_conv_tile(ore_ctx* ctx, int32_t tile) {
+  if (!ctx) return set_error(nullptr, ORE_ERR_INVALID, "null context");
+  if (tile < -1 || tile >= WINO_TILE_BASE + WINO_TILES_N || conv_tile_retired(tile))
+    return set_error(ctx, ORE_ERR_INVALID, "conv tile %d is not a conv tile id", int(tile));
+  ctx->conv_tile = tile;
+  return ORE_OK;
+}
+
+ore_status ore_ctx_set_pool_variant(ore_ctx* ctx, int32_t variant) {
+  if (!ctx) return set_error(nullptr, ORE_ERR_INVALID, "null context");
+  if (variant != 0 && (variant < 2 || variant > 5)) return set_error(ctx, ORE_ERR_INVALID, "unknown MaxPool variant %d", int(variant));
+  ctx->pool_variant = variant;
   return ORE_OK;
 }
 
@@ -697,7 +692,8 @@ ore_status ore_conv2d_f32(ore_ctx* ctx, const ore_tensor* x, const ore_tensor* w
   if (x->dims[0] == 0) return ORE_OK;
   const int2* kt = nullptr;
   const ConvPlan pln = conv_plan(w->dims[0], w->dims[1], x->dims[2], x->dims[3], w->dims[2], w->dims[3], a->strides[0],
-                                 a->strides[1], win, false, 0, false, ctx->conv_algo == ORE_CONV_ALGO_WINOGRAD);
+                                 a->strides[1], win, false, 0, false, ctx->conv_algo == ORE_CONV_ALGO_WINOGRAD,
+                                 ctx->conv_tile);
   float* wp = pack_to_scratch(ctx, pln, w->data, false, w->dims[0], w->dims[1], w->dims[2], w->dims[3], x->dims[2],
                               x->dims[3], &kt);
   if (!wp) return ORE_ERR_OOM;
@@ -777,7 +773,7 @@ ore_status ore_matmul_f32(ore_ctx* ctx, const ore_tensor* a, const ore_tensor* b
   win.Ho = 1; win.Wo = 1;
   if (a->dims[0] == 0) return ORE_OK;
   const int2* kt = nullptr;
-  const ConvPlan pln = conv_plan(b->dims[1], b->dims[0], 1, 1, 1, 1, 1, 1, win);
+  const ConvPlan pln = conv_plan(b->dims[1], b->dims[0], 1, 1, 1, 1, 1, 1, win, false, 0, false, false, ctx->conv_tile);
   float* wp = pack_to_scratch(ctx, pln, b->data, true, b->dims[1], b->dims[0], 1, 1, 1, 1, &kt);
   if (!wp) return ORE_ERR_OOM;
   return run_conv(ctx, pln, a->data, a->dims[0], a->dims[1], 1, 1, a->dims[1], wp, kt, b->dims[1], 1, 1, nullptr, win, 1, 1,

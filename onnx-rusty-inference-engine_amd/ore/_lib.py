@@ -16,24 +16,27 @@ ORE_OK = 0
 STATUS_NAMES = {0: "ORE_OK", 1: "ORE_ERR_INVALID", 2: "ORE_ERR_UNSUPPORTED", 3: "ORE_ERR_HIP",
                 4: "ORE_ERR_OOM", 5: "ORE_ERR_PARSE"}
 
-FUSE_CONV_RELU, FUSE_CONCAT, FUSE_ALIAS, FUSE_ALL, KEEP_VALUES, FUSE_POOL_CONV, FUSE_CONV_POOL = 1, 2, 4, 231, 8, 16, 32
-FUSE_FIRE = 64
-FUSE_CONCAT_POOL = 128
+# ore_model_set_fusion flags (include/ore.h)
+FUSE_CONV_RELU, FUSE_CONCAT, FUSE_ALIAS, KEEP_VALUES, FUSE_CONV_POOL = 1, 2, 4, 8, 32
+FUSE_FIRE, FUSE_CONCAT_POOL, FUSE_FIRE_POOL, FUSE_FIRST_SQUEEZE, FUSE_POOL_SQUEEZE = 64, 128, 256, 512, 1024
+FUSE_EAGER = 2048  # tests: every eligible fusion regardless of the size heuristics
+FUSE_ALL = 2023
 LOAD_F16 = 1  # ore_model_load_ex flag: the fp16 variant
 LOAD_X3 = 2   # ore_model_load_ex flag: f32 convs on the BF16 matrix cores (exact 3-way bf16 split)
 LOAD_NO_WINOGRAD = 4  # ore_model_load_ex flag: 3x3 stride-1 convs on the direct kernels only
+LOAD_X3_ALL = 8  # ore_model_load_ex flag: every conv on x3, no f32-MFMA fusions (x3 kernel tests)
 CONV_ALGO_DIRECT, CONV_ALGO_WINOGRAD = 0, 1  # ore_ctx_set_conv_algo (per-op ore_conv2d_f32)
 PAD = {"NOTSET": 0, "NOT_SET": 0, "SAME_UPPER": 1, "SAME_LOWER": 2, "VALID": 3}
 
 # every symbol include/ore.h declares (checked by tests/test_abi.py on CPU)
 EXPORTED = [
     "ore_abi_version", "ore_ctx_create", "ore_ctx_destroy", "ore_ctx_set_stream", "ore_ctx_get_stream",
-    "ore_ctx_set_conv_algo", "ore_sync", "ore_last_error", "ore_malloc", "ore_free", "ore_upload", "ore_download",
+    "ore_ctx_set_conv_algo", "ore_ctx_set_conv_tile", "ore_ctx_set_pool_variant", "ore_sync", "ore_last_error", "ore_malloc", "ore_free", "ore_upload", "ore_download",
     "ore_conv_out_shape", "ore_pool_out_shape", "ore_conv2d_f32", "ore_maxpool2d_f32", "ore_relu_f32",
     "ore_add_f32", "ore_softmax_f32", "ore_matmul_f32", "ore_gap_f32", "ore_concat_f32", "ore_dropout_f32",
     "ore_reshape", "ore_model_parse", "ore_model_load", "ore_model_load_ex", "ore_model_destroy", "ore_model_set_fusion", "ore_model_input_dims",
     "ore_model_output_elems", "ore_model_run", "ore_model_read_value", "ore_model_autotune",
-    "ore_model_step_tile", "ore_model_set_streams",
+    "ore_model_step_tile", "ore_model_set_step_tile", "ore_model_step_mfma_flops", "ore_model_set_streams",
     "ore_model_graph_capture", "ore_model_graph_launch", "ore_model_enable_timing",
     "ore_model_step_count", "ore_model_step_info", "ore_model_step_times",
 ]
@@ -82,6 +85,8 @@ def load():
         "ore_ctx_set_stream": (i32, [vp, vp]),
         "ore_ctx_get_stream": (vp, [vp]),
         "ore_ctx_set_conv_algo": (i32, [vp, i32]),
+        "ore_ctx_set_conv_tile": (i32, [vp, i32]),
+        "ore_ctx_set_pool_variant": (i32, [vp, i32]),
         "ore_sync": (i32, [vp]),
         "ore_last_error": (cs, [vp]),
         "ore_malloc": (i32, [vp, ctypes.c_size_t, ctypes.POINTER(vp)]),
@@ -113,6 +118,8 @@ def load():
         "ore_model_set_streams": (i32, [vp, i32]),
         "ore_model_autotune": (i32, [vp, vp, i64, vp, i32]),
         "ore_model_step_tile": (i32, [vp, i32]),
+        "ore_model_set_step_tile": (i32, [vp, i32, i32]),
+        "ore_model_step_mfma_flops": (i32, [vp, i32, ctypes.POINTER(ctypes.c_double)]),
         "ore_model_graph_capture": (i32, [vp, vp, i64, vp]),
         "ore_model_graph_launch": (i32, [vp]),
         "ore_model_step_count": (i32, [vp]),

@@ -16,7 +16,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import LOAD_F16, LOAD_NO_WINOGRAD, LOAD_X3, ConvAttrs, OreError, PoolAttrs, Tensor, check, load
+from ._lib import LOAD_F16, LOAD_NO_WINOGRAD, LOAD_X3, LOAD_X3_ALL, ConvAttrs, OreError, PoolAttrs, Tensor, check, load
 
 __all__ = ["Context", "Model", "OreError", "convolution", "max_pool", "relu", "add", "softmax", "mul",
            "global_average_pool", "concatenation", "drop_out", "reshape", "inference", "conv_out_shape",
@@ -48,6 +48,17 @@ class Context:
         """ore_ctx_set_conv_algo: the per-op convolution()'s algorithm (CONV_ALGO_DIRECT, the
         reference's k order; CONV_ALGO_WINOGRAD, F(2x2, 3x3) on eligible 3x3 stride-1 convs)."""
         check(load().ore_ctx_set_conv_algo(self.h, int(algo)), self.h)
+
+    def set_conv_tile(self, tile: int = -1):
+        """ore_ctx_set_conv_tile: force a tile id on every conv planned on this context afterwards
+        (per-op calls and models loaded later); -1 = the per-layer heuristic.  Results do not depend
+        on it (parity tests sweep it)."""
+        check(load().ore_ctx_set_conv_tile(self.h, int(tile)), self.h)
+
+    def set_pool_variant(self, variant: int = 0):
+        """ore_ctx_set_pool_variant: force a MaxPool kernel (2 direct, 3 column strip, 4 plane-staged,
+        5 chunk-staged; 0 = by layout)."""
+        check(load().ore_ctx_set_pool_variant(self.h, int(variant)), self.h)
 
     @property
     def stream(self) -> int:
@@ -223,12 +234,13 @@ class Model:
     """ore_model: the device-resident walker over one ONNX graph."""
 
     def __init__(self, ctx: Context, onnx_bytes: bytes, max_batch: int, precision: str = "f32",
-                 winograd: bool = True):
+                 winograd: bool = True, x3_all: bool = False):
         """precision "f32": convs on the f32-input MFMA; "f32x3": the same f32 model with its convs /
         MatMuls on the BF16 matrix cores through an exact three-way bf16 split (ORE_LOAD_X3,
         include/ore.h); "f16": the fp16 variant (ORE_LOAD_F16).  Input / output stay f32.
         winograd (f32 only): 3x3 stride-1 pad-1 convs that no direct-kernel fusion takes run
-        Winograd F(2x2, 3x3) in f32; False = ORE_LOAD_NO_WINOGRAD (direct kernels only)."""
+        Winograd F(2x2, 3x3) in f32; False = ORE_LOAD_NO_WINOGRAD (direct kernels only).
+        x3_all (f32x3 only): every conv on the x3 kernels, no f32-MFMA fusions (ORE_LOAD_X3_ALL)."""
         if precision not in ("f32", "f32x3", "f16"):
             raise OreError(1, f"precision must be 'f32', 'f32x3' or 'f16', not {precision!r}")
         self.ctx = ctx
@@ -237,6 +249,10 @@ class Model:
         flags = {"f32": 0, "f32x3": LOAD_X3, "f16": LOAD_F16}[precision]
         if not winograd:
             flags |= LOAD_NO_WINOGRAD
+        if x3_all:
+            if precision != "f32x3":
+                raise OreError(1, "x3_all needs precision 'f32x3'")
+            flags |= LOAD_X3_ALL
         check(load().ore_model_load_ex(ctx.h, onnx_bytes, len(onnx_bytes), int(max_batch), flags, ctypes.byref(h)),
               ctx.h)
         self.h = h
@@ -298,21 +314,28 @@ class Model:
         check(load().ore_model_autotune(self.h, ctypes.c_void_p(x.data_ptr()), int(x.shape[0]),
                                         ctypes.c_void_p(out.data_ptr()), int(reps)), self.ctx.h)
 
+    # tile ids (ore_model_step_tile); None = a retired id (kernels removed after measuring slower)
     TILE_NAMES = ["128x128", "96x128", "64x128", "32x256",
-                  "direct 128x128", "direct 96x128", "direct 64x128", "direct 128x64",
-                  "ws 128x128", "ws 96x128", "ws 64x128", "ws 32x256",
+                  None, None, None, None,  # 4-7: the LDS-free direct conv
+                  None, None, None, None,  # 8-11: the warp-specialised conv_gemm_kernel
                   "stream 64x128", "stream 32x256", "stream 16x256", "stream 48x128", "stream 64x64",
                   "stream 128x64", "stream 64x64 d8", "stream 32x128", "stream 128x64 d2", "fire",
                   "epool patch", "epool walk48", "epool walk96", "epool walk64",
-                  "epool walk64 b3", "epool walk96 b2",
+                  "epool walk64 b3", None,  # 27: the 2-band walker
                   "x3 128x128", "x3 64x256", "x3 96x128", "x3 64x128",
                   "x3w 128x128", "x3w 64x128", "x3w 128x64", "x3w 64x64",
-                  "wino 32x32 d4", "wino 32x32 d2", "wino16 32x16", "wino16 16x32", "wino lds", "fire wino", "fire f16", "first conv pool f16", "epool window f32",
-                  "fire pool f32"]
+                  "wino 32x32 d4", "wino 32x32 d2", "wino16 32x16", "wino16 16x32",
+                  None, None,  # 40: the LDS-staged Winograd, 41: the Winograd fire module
+                  "fire f16", "first conv pool f16", "epool window f32", "fire pool f32"]
 
     def tiles(self):
         """Block tile per exec step (-1 for non-conv steps); names in TILE_NAMES."""
         return [load().ore_model_step_tile(self.h, i) for i in range(load().ore_model_step_count(self.h))]
+
+    def set_tile(self, step: int, tile: int):
+        """ore_model_set_step_tile: run exec step `step` on tile id `tile` (one of its autotune
+        candidates; e.g. to restore a saved autotune result)."""
+        check(load().ore_model_set_step_tile(self.h, int(step), int(tile)), self.ctx.h)
 
     def set_streams(self, streams: int):
         """2: run independent neighbouring steps (the fire modules' expand branches) on a side
@@ -343,7 +366,10 @@ class Model:
             fl, by = ctypes.c_double(), ctypes.c_double()
             check(L.ore_model_step_info(self.h, i, ctypes.byref(op), ctypes.byref(name), ctypes.byref(fl),
                                         ctypes.byref(by)), self.ctx.h)
-            out.append({"op": op.value.decode(), "name": name.value.decode(), "flops": fl.value, "bytes": by.value})
+            mf = ctypes.c_double()
+            check(L.ore_model_step_mfma_flops(self.h, i, ctypes.byref(mf)), self.ctx.h)
+            out.append({"op": op.value.decode(), "name": name.value.decode(), "flops": fl.value, "bytes": by.value,
+                        "mfma_flops": mf.value})
         return out
 
     def step_times_ms(self):

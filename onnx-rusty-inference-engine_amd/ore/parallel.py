@@ -39,6 +39,19 @@ def gather_rows(local, n_total: int, group=None):
     return torch.cat(parts, dim=0)
 
 
+def gather_rows_into(gathered, local, group=None):
+    """The per-step collective of bench.py: every rank holds an equal [n, D] block (n_total divisible
+    by the world size, shard_bounds then gives rank r rows [r n, (r + 1) n)), all-gathered in rank
+    order into the preallocated [world * n, D] `gathered` -- one all_gather_into_tensor (RCCL on
+    device tensors, gloo on host tensors), no allocation per step."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if gathered.shape[0] != world * local.shape[0] or tuple(gathered.shape[1:]) != tuple(local.shape[1:]):
+        raise ValueError(f"gathered {tuple(gathered.shape)} != world {world} x local {tuple(local.shape)}")
+    dist.all_gather_into_tensor(gathered, local, group=group)
+    return gathered
+
+
 def run_sharded(run_fn: Callable, x_global, group=None):
     """Run `run_fn(x_slice) -> [n_slice, D]` on this rank's slice of x_global and return the
     gathered [n_total, D] on every rank."""

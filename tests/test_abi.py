@@ -33,6 +33,15 @@ def test_library_exports_header():
     assert L.ore_abi_version() == 1
 
 
+def test_library_reads_no_environment():
+    """The product takes every kernel / fusion choice through the C ABI (load flags, fusion flags,
+    ore_ctx_set_conv_tile / _pool_variant, ore_model_set_step_tile): libore.so imports no getenv."""
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    imported = {line.split()[-1].split("@")[0] for line in out.stdout.splitlines() if line.strip()}
+    assert "getenv" not in imported and "secure_getenv" not in imported
+
+
 def test_library_is_gfx950():
     """The code object embedded in libore.so targets gfx950 only (no other offload arch)."""
     data = open(_lib.LIB_PATH, "rb").read()

@@ -67,3 +67,40 @@ def test_sharded_gather_matches_single_process(tmp_path, n):
     got = np.load(out)
     ref = oracle.Model(squeezenet.build(32)).run(squeezenet.synthetic_input(n, 32, seed=4), 1000)
     assert np.array_equal(got, ref)
+
+
+def _bench_leg_worker(rank, world, port, G, out_path):
+    """bench.py's N > 1 data path with the oracle standing in for the HIP model: one seeded global
+    batch, this rank's shard_bounds slice, gather_rows_into the preallocated [G, D] rows."""
+    import sys
+    sys.path.insert(0, os.path.dirname(HERE))
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "onnx-rusty-inference-engine_amd"))
+    import torch
+    import torch.distributed as dist
+    import oracle
+    from ore import squeezenet
+    from ore.parallel import gather_rows_into, shard_bounds
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    xg = squeezenet.synthetic_input(G, 32, seed=6)
+    lo, hi = shard_bounds(G, world, rank)
+    out = torch.from_numpy(oracle.Model(squeezenet.build(32)).run(xg[lo:hi], 1000))
+    gathered = torch.empty((G, 1000))
+    gather_rows_into(gathered, out)
+    with pytest.raises(ValueError):
+        gather_rows_into(torch.empty((G + 1, 1000)), out)
+    if rank == 0:
+        np.save(out_path, gathered.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_gather_leg(tmp_path):
+    import oracle
+    from ore import squeezenet
+    out = str(tmp_path / "g.npy")
+    mp.spawn(_bench_leg_worker, args=(2, _free_port(), 4, out), nprocs=2, join=True)
+    got = np.load(out)
+    ref = oracle.Model(squeezenet.build(32)).run(squeezenet.synthetic_input(4, 32, seed=6), 1000)
+    assert np.array_equal(got, ref)

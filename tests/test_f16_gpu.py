@@ -16,6 +16,8 @@ import os
 import numpy as np
 import pytest
 
+from _knobs import C1_POOL_F16, EPOOL_PATCH, conv_tile, force_tiles
+
 import oracle
 
 pytestmark = pytest.mark.gpu
@@ -83,13 +85,11 @@ def _sparse(rng, shape, nonzeros):
     (2, 3, 31, 29, 8, 3, 2, 1, 40, 3),     # 3x3/s2 -> 3x3 on C = 8 (K = 72: a partial last k stage)
     (1, 4, 12, 12, 24, 5, 1, 2, 16, 3),    # 5x5 pad 2 on 4 channels (odd kw: the PAIR padding tap)
 ])
-@pytest.mark.parametrize("first,dma", [("pair", "1"), ("nhwc8", "1"), ("nhwc8", "0"), ("nchw", "1")])
-def test_f16_conv_exact_integers(gpu_ctx, case, first, dma, monkeypatch):
-    """first: operand mode of the conv on the f32 input (ORE_F16_FIRST); dma: 16-B NHWC convs on the
-    LDS-DMA kernel (1) or the register-staged one (0)."""
+def test_f16_conv_exact_integers(gpu_ctx, case):
+    """The conv on the f32 input takes the NHWC4 tap-pair gather for C <= 4 (cases 1, 4, 5) and the
+    per-element NCHW gather above (cases 2, 3); the second conv the 16-B NHWC LDS-DMA kernel or the
+    per-element NHWC gather (C % 8 != 0)."""
     import ore
-    monkeypatch.setenv("ORE_F16_FIRST", first)
-    monkeypatch.setenv("ORE_F16_DMA", dma)
     N, C, H, W, M1, k1, s1, p1, M2, k2 = case
     rng = np.random.default_rng(hash(case) & 0xffff)
     x = _ints(rng, -2, 2, (N, C, H, W))
@@ -117,7 +117,7 @@ def test_f16_pool_relu_gap_exact(gpu_ctx):
     w2 = _sparse(rng, (8, 32, 1, 1), 8)
     mb = _chain_model((1, 4, 29, 29), [(w1, b1, [1] * 4, [1, 1], True), (w2, None, [0] * 4, [1, 1], False)],
                       pool=[0, 0, 1, 1])
-    for fusion in (ore.FUSE_ALL | ore.KEEP_VALUES, ore.KEEP_VALUES, ore.FUSE_ALL | ore.FUSE_POOL_CONV | ore.KEEP_VALUES):
+    for fusion in (ore.FUSE_ALL | ore.KEEP_VALUES, ore.KEEP_VALUES, ore.FUSE_ALL | ore.FUSE_EAGER | ore.KEEP_VALUES):
         m = ore.Model(gpu_ctx, mb, max_batch=2, precision="f16")
         m.set_fusion(fusion)
         y = _np(m.run(_t(x)))
@@ -193,19 +193,18 @@ def test_f16_rejects_f32_only_ops(gpu_ctx):
         ore.Model(gpu_ctx, mb, max_batch=1, precision="bf16")
 
 
-@pytest.mark.parametrize("cfg", ["0", "1", "2", "3"])
-def test_f16_dma_kernel_bit_identical(gpu_ctx, cfg, monkeypatch):
-    """The LDS-DMA kernel (ORE_F16_DMA=1, default) runs the same MFMA chain as the register-staged
-    one: equal outputs, every block tile (ORE_CONV_CFG)."""
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def test_f16_tiles_bit_identical(gpu_ctx, cfg):
+    """Every block tile of the f16 conv kernels (ore_ctx_set_conv_tile) runs the same MFMA chain as
+    the heuristic plan's: equal outputs and intermediate values."""
     import ore
     from ore import squeezenet
     mb = squeezenet.build(64)
     x = _t(squeezenet.synthetic_input(3, 64, seed=4))
-    monkeypatch.setenv("ORE_CONV_CFG", cfg)
     outs = []
-    for dma in ("1", "0"):
-        monkeypatch.setenv("ORE_F16_DMA", dma)
-        m = ore.Model(gpu_ctx, mb, max_batch=3, precision="f16")
+    for tile in (-1, cfg):
+        with conv_tile(gpu_ctx, tile):
+            m = ore.Model(gpu_ctx, mb, max_batch=3, precision="f16")
         m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
         outs.append((_np(m.run(x)), m.read_value("fire9/concat_1")))
         m.close()
@@ -391,12 +390,11 @@ C1POOL_CASES = [
 
 
 @pytest.mark.parametrize("case", C1POOL_CASES)
-def test_f16_first_conv_pool_fused_bit_identical(gpu_ctx, case, monkeypatch):
+def test_f16_first_conv_pool_fused_bit_identical(gpu_ctx, case):
     """f16 first conv (f32 NCHW input, <= 4 channels) + Relu + 3x3/s2 MaxPool: the one-launch kernel
     (conv_pair_pool_f16_kernel, reads the f32 input itself) equals the two-launch path (NHWC4
     conversion + conv_f16_kernel with the pooled epilogue) bit for bit."""
     import ore
-    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "8")  # pooled epilogue at these small planes too
     N, C, H, W, M, k, st, pd, pp = case
     rng = np.random.default_rng(sum(case[:8]))
     x = (rng.standard_normal((N, C, H, W)) * 20).astype(np.float32)
@@ -406,9 +404,9 @@ def test_f16_first_conv_pool_fused_bit_identical(gpu_ctx, case, monkeypatch):
     mb = _chain_model((1, C, H, W), [(w1, b1, [pd] * 4, [st, st], True), (w2, None, [0] * 4, [1, 1], False)], pool=pp)
     vals = []
     for on in ("1", "0"):
-        monkeypatch.setenv("ORE_F16_C1POOL", on)
         m = ore.Model(gpu_ctx, mb, max_batch=N, precision="f16")
-        m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+        m.set_fusion(ore.FUSE_ALL | ore.FUSE_EAGER | ore.KEEP_VALUES)  # eager: pooled epilogue at small planes
+        assert force_tiles(m, C1_POOL_F16 if on == "1" else EPOOL_PATCH) == 1  # one launch / conversion + patch
         y = _np(m.run(_t(x)))
         vals.append((y, m.read_value("p0"), m.read_value("c1")))
         assert ("first conv pool f16" in [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]) == (on == "1")
@@ -418,11 +416,9 @@ def test_f16_first_conv_pool_fused_bit_identical(gpu_ctx, case, monkeypatch):
     assert np.abs(vals[0][1]).max() > 0
 
 
-def test_f16_first_conv_pool_exact_integers(gpu_ctx, monkeypatch):
+def test_f16_first_conv_pool_exact_integers(gpu_ctx):
     """Small integers: the one-launch first conv + pool equals the f32 oracle bit for bit."""
     import ore
-    monkeypatch.setenv("ORE_F16_C1POOL", "1")
-    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "8")
     rng = np.random.default_rng(8)
     x = _ints(rng, -3, 3, (2, 3, 51, 49))
     w1, b1 = _sparse(rng, (96, 3, 7, 7), 16), _ints(rng, -8, 8, (96,))
@@ -430,7 +426,7 @@ def test_f16_first_conv_pool_exact_integers(gpu_ctx, monkeypatch):
     mb = _chain_model((1, 3, 51, 49), [(w1, b1, [0] * 4, [2, 2], True), (w2, None, [0] * 4, [1, 1], False)],
                       pool=[0, 0, 1, 1])
     m = ore.Model(gpu_ctx, mb, max_batch=2, precision="f16")
-    m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+    m.set_fusion(ore.FUSE_ALL | ore.FUSE_EAGER | ore.KEEP_VALUES)
     _np(m.run(_t(x)))
     assert ore.Model.TILE_NAMES[m.tiles()[0]] == "first conv pool f16"
     r0 = oracle.relu(oracle.conv2d(x, w1, b1, pads=[0] * 4, strides=(2, 2)))
@@ -439,7 +435,7 @@ def test_f16_first_conv_pool_exact_integers(gpu_ctx, monkeypatch):
     m.close()
 
 
-def test_f16_squeezenet_first_conv_pool_fused(gpu_ctx, monkeypatch):
+def test_f16_squeezenet_first_conv_pool_fused(gpu_ctx):
     """SqueezeNet-1.0 @224 f16: probabilities with the one-launch conv1 + pool1 equal the two-launch
     path's bit for bit."""
     import ore
@@ -448,8 +444,10 @@ def test_f16_squeezenet_first_conv_pool_fused(gpu_ctx, monkeypatch):
     x = _t(squeezenet.synthetic_input(3, 224, seed=23))
     outs = []
     for on in ("1", "0"):
-        monkeypatch.setenv("ORE_F16_C1POOL", on)
         m = ore.Model(gpu_ctx, mb, max_batch=3, precision="f16")
+        if on == "0":  # the two-launch first conv (and so no squeeze inside it)
+            m.set_fusion(ore.FUSE_ALL & ~ore.FUSE_FIRST_SQUEEZE)
+            assert force_tiles(m, EPOOL_PATCH) == 1
         outs.append(_np(m.run(x)))
         assert (ore.Model.TILE_NAMES[m.tiles()[0]] == "first conv pool f16") == (on == "1")
         m.close()
@@ -462,11 +460,10 @@ def test_f16_squeezenet_first_conv_pool_fused(gpu_ctx, monkeypatch):
     (3, 40, 33, 64, [0, 0, 1, 1], 32),   # two channel fragments in, 32 out, ceil-mode pool
     (2, 45, 52, 96, [1, 1, 1, 1], 24),   # padded pool, 24 squeeze channels (a partial store group)
 ])
-def test_f16_first_conv_pool_squeeze_fused(gpu_ctx, case, monkeypatch):
+def test_f16_first_conv_pool_squeeze_fused(gpu_ctx, case):
     """The first conv + Relu + MaxPool + the next 1x1 conv + Relu in one launch (the pooled map never
     stored) equals the two-launch first conv + the separate squeeze bit for bit."""
     import ore
-    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "8")
     N, H, W, M, pp, Q = case
     rng = np.random.default_rng(sum(case[:4]) + Q)
     x = (rng.standard_normal((N, 3, H, W)) * 20).astype(np.float32)
@@ -477,9 +474,11 @@ def test_f16_first_conv_pool_squeeze_fused(gpu_ctx, case, monkeypatch):
     mb = _chain_model((1, 3, H, W), [(w1, b1, [0] * 4, [2, 2], True), (w2, b2, [0] * 4, [1, 1], True)], pool=pp)
     vals = []
     for on in ("1", "0"):
-        monkeypatch.setenv("ORE_F16_C1POOL", on)
         m = ore.Model(gpu_ctx, mb, max_batch=N, precision="f16")
-        m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+        fusion = ore.FUSE_ALL if on == "1" else ore.FUSE_ALL & ~ore.FUSE_FIRST_SQUEEZE
+        m.set_fusion(fusion | ore.FUSE_EAGER | ore.KEEP_VALUES)
+        if on == "0":
+            assert force_tiles(m, EPOOL_PATCH) == 1  # the two-launch first conv
         y = _np(m.run(_t(x)))
         vals.append((y, m.read_value("r1")))
         names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]

@@ -5,10 +5,14 @@ against the reference's golden vectors and the oracle's committed fixtures.
   synthetic SqueezeNet-1.0 @224 vs oracle fixture: <= 1e-5 max-abs on the softmax probabilities
   full-size properties at batch 256: rows sum to 1, per-image results bit-identical to the same
   images run alone (no cross-image arithmetic), fused == unfused bit for bit."""
+import functools
 import os
 
 import numpy as np
 import pytest
+
+from _knobs import (EPOOL_PATCH, EPOOL_WALK48, EPOOL_WALK64, EPOOL_WALK64_B3, EPOOL_WALK96, EPOOL_WINDOW, conv_tile,
+                    force_tiles)
 
 pytestmark = pytest.mark.gpu
 
@@ -27,12 +31,12 @@ def _np(t):
     return t.cpu().numpy()
 
 
-@pytest.fixture(autouse=True)
-def direct_kernels(monkeypatch):
-    """These tests pin the direct kernels and their fusions (bit-identical to the unfused graph);
-    the Winograd 3x3 path, on by default for f32 models, has its own parity tests
-    (tests/test_wino_gpu.py)."""
-    monkeypatch.setenv("ORE_NO_WINOGRAD", "1")
+def _model(ctx, mb, **kw):
+    """These tests pin the direct kernels and their fusions (bit-identical to the unfused graph): every
+    model loads with ORE_LOAD_NO_WINOGRAD.  The Winograd 3x3 path, on by default for f32 models, has
+    its own parity tests (tests/test_wino_gpu.py)."""
+    import ore
+    return ore.Model(ctx, mb, winograd=False, **kw)
 
 
 def _mnist_bytes():
@@ -44,16 +48,16 @@ def _mnist_bytes():
 def squeeze224(gpu_ctx):
     import ore
     from ore import squeezenet
-    m = ore.Model(gpu_ctx, squeezenet.build(224), max_batch=256, winograd=False)
+    m = _model(gpu_ctx, squeezenet.build(224), max_batch=256)
     yield m
     m.close()
 
 
-@pytest.mark.parametrize("fusion", [23, 7, 0])  # 23 = default set + the opt-in pool fusion
+@pytest.mark.parametrize("fusion", [2023 | 2048, 2023, 7, 0])  # FUSE_ALL (| FUSE_EAGER), unfused
 def test_mnist_golden(gpu_ctx, fusion):
     import ore
     from ore import onnx_wire
-    m = ore.Model(gpu_ctx, _mnist_bytes(), max_batch=4)
+    m = _model(gpu_ctx, _mnist_bytes(), max_batch=4)
     m.set_fusion(fusion)
     x = onnx_wire.load_tensor(os.path.join(GOLD, "mnist_data_0.pb")).to_numpy()
     g = onnx_wire.load_tensor(os.path.join(GOLD, "mnist_output_0.pb")).to_numpy()
@@ -68,7 +72,7 @@ def test_mnist_oracle_batch(gpu_ctx):
     import ore
     from golden.make_golden import mnist_inputs
     ref = np.load(os.path.join(GOLD, "mnist_oracle.npz"))["output"]
-    m = ore.Model(gpu_ctx, _mnist_bytes(), max_batch=8)
+    m = _model(gpu_ctx, _mnist_bytes(), max_batch=8)
     y = _np(m.run(_t(mnist_inputs())))
     assert np.abs(y - ref).max() <= 1e-6 * np.abs(ref).max()
     m.close()
@@ -93,13 +97,13 @@ def test_squeezenet_synth_vs_oracle(squeeze224):
     assert np.array_equal(y.argmax(1), ref.argmax(1))
 
 
-@pytest.mark.parametrize("fusion", [23, 16, 7, 0, 1, 2, 4])
+@pytest.mark.parametrize("fusion", [2023 | 2048, 2023, 7, 0, 1, 2, 4, 32, 2023 & ~64])
 def test_squeezenet_mini_vs_oracle(gpu_ctx, fusion):
     import ore
     from ore import squeezenet
     from golden.make_golden import mini_inputs
     ref = np.load(os.path.join(GOLD, "squeezenet_mini_oracle.npz"))["output"]
-    m = ore.Model(gpu_ctx, squeezenet.build(64), max_batch=4)
+    m = _model(gpu_ctx, squeezenet.build(64), max_batch=4)
     m.set_fusion(fusion)
     y = _np(m.run(_t(mini_inputs())))
     assert np.abs(y - ref).max() <= 1e-5
@@ -116,7 +120,7 @@ def test_squeezenet_node_level_parity(gpu_ctx):
     mb = squeezenet.build(64)
     model = onnx_wire.decode_model(mb)
     inits = {t.name: t.to_numpy() for t in model.graph.initializer}
-    m = ore.Model(gpu_ctx, mb, max_batch=4)
+    m = _model(gpu_ctx, mb, max_batch=4)
     m.set_fusion(ore.KEEP_VALUES)  # unfused, and no storage reuse so every value can be read back
     xt = _t(mini_inputs()[:2])  # kept alive: read_value of the model input reads this buffer
     _np(m.run(xt))
@@ -155,10 +159,10 @@ def test_fused_padded_layout_values(gpu_ctx, hw):
     mb = squeezenet.build(hw)
     model = onnx_wire.decode_model(mb)
     xt = _t(squeezenet.synthetic_input(3, hw, seed=31))
-    ref = ore.Model(gpu_ctx, mb, max_batch=3)
+    ref = _model(gpu_ctx, mb, max_batch=3)
     ref.set_fusion(ore.KEEP_VALUES)
     _np(ref.run(xt))
-    fused = ore.Model(gpu_ctx, mb, max_batch=3)
+    fused = _model(gpu_ctx, mb, max_batch=3)
     fused.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
     _np(fused.run(xt))
     checked = 0
@@ -200,28 +204,25 @@ def test_squeezenet_batch256_properties(squeeze224):
 
 @pytest.mark.parametrize("precision", ["f32", "f16"])
 @pytest.mark.parametrize("hw", [64, 224])
-def test_pool_conv_fusion_bit_identical(gpu_ctx, precision, hw):
-    """ORE_FUSE_POOL_CONV (the 3x3 pools computed inside the squeeze convs' gathers) changes no
-    bit of any result; all tiles of the fused kernel agree too."""
-    import os
+def test_forced_tiles_bit_identical(gpu_ctx, precision, hw):
+    """Every conv tile forced through ore_ctx_set_conv_tile (the four LDS-staged tiles, and for f32 two
+    streaming ones) gives the heuristic plan's results bit for bit, eager fusions included."""
     import ore
     from ore import squeezenet
     mb = squeezenet.build(hw)
     x = _t(squeezenet.synthetic_input(3, hw, seed=13))
     outs = []
-    pf = ore.FUSE_ALL | ore.FUSE_POOL_CONV
-    for fusion, cfg in ((pf, None), (ore.FUSE_ALL, None), (pf, "2"), (pf, "3"), (pf, "1"), (pf, "0")):
-        if cfg is not None:
-            os.environ["ORE_CONV_CFG"] = cfg
-        try:
-            m = ore.Model(gpu_ctx, mb, max_batch=3, precision=precision)
-            m.set_fusion(fusion)
-            outs.append(_np(m.run(x)))
-            m.close()
-        finally:
-            os.environ.pop("ORE_CONV_CFG", None)
+    tiles = [None, 2, 3, 1, 0] + ([12, 14] if precision == "f32" else [])
+    for tile in tiles:
+        with conv_tile(gpu_ctx, -1 if tile is None else tile):
+            m = _model(gpu_ctx, mb, max_batch=3, precision=precision)
+        m.set_fusion(ore.FUSE_ALL | ore.FUSE_EAGER)
+        outs.append(_np(m.run(x)))
+        m.close()
     for o in outs[1:]:
         np.testing.assert_array_equal(o, outs[0])
+    with pytest.raises(ore.OreError):
+        gpu_ctx.set_conv_tile(5)  # a retired tile id
 
 
 @pytest.mark.parametrize("precision", ["f32", "f16"])
@@ -230,7 +231,7 @@ def test_autotune_keeps_results(gpu_ctx, precision):
     import torch
     import ore
     from ore import squeezenet
-    m = ore.Model(gpu_ctx, squeezenet.build(224), max_batch=8, precision=precision)
+    m = _model(gpu_ctx, squeezenet.build(224), max_batch=8, precision=precision)
     x = _t(squeezenet.synthetic_input(8, 224, seed=21))
     before = _np(m.run(x))
     tiles0 = m.tiles()
@@ -260,7 +261,7 @@ def test_real_squeezenet_golden(gpu_ctx):
     from ore import onnx_wire
     path = os.path.join(os.path.dirname(HERE), "models", "squeezenet1.0-8.onnx")
     with open(path, "rb") as f:
-        m = ore.Model(gpu_ctx, f.read(), max_batch=1)
+        m = _model(gpu_ctx, f.read(), max_batch=1)
     x = onnx_wire.load_tensor(os.path.join(GOLD, "squeezenet_data_0.pb")).to_numpy()
     g = onnx_wire.load_tensor(os.path.join(GOLD, "squeezenet_output_0.pb")).to_numpy().reshape(1, -1)
     y = _np(m.run(_t(x)))
@@ -275,15 +276,15 @@ def test_model_errors(gpu_ctx):
                               [w.encode_value_info("x", (1, 2, 4, 4))] + list(extra_inputs),
                               [w.encode_value_info("y", (1, 2, 4, 4))])
     with pytest.raises(ore.OreError, match="NOT FOUND"):
-        ore.Model(gpu_ctx, model([w.encode_node("Sigmoid", ["x"], ["y"])]), 1)
+        _model(gpu_ctx, model([w.encode_node("Sigmoid", ["x"], ["y"])]), 1)
     with pytest.raises(ore.OreError, match="CONCATENATE"):
-        ore.Model(gpu_ctx, model([w.encode_node("Concat", ["x", "x"], ["y"], attrs=[w.encode_attr_int("bogus", 1)])]), 1)
+        _model(gpu_ctx, model([w.encode_node("Concat", ["x", "x"], ["y"], attrs=[w.encode_attr_int("bogus", 1)])]), 1)
     wt = np.zeros((2, 2, 3, 3), np.float32)
     with pytest.raises(ore.OreError, match="Auto Pad"):  # Conv accepts NOT_SET, not NOTSET
-        ore.Model(gpu_ctx, model([w.encode_node("Conv", ["x", "w"], ["y"], attrs=[
+        _model(gpu_ctx, model([w.encode_node("Conv", ["x", "w"], ["y"], attrs=[
             w.encode_attr_string("auto_pad", "NOTSET"), w.encode_attr_ints("strides", [1, 1])])], [("w", wt)]), 1)
     with pytest.raises(ore.OreError):
-        ore.Model(gpu_ctx, b"\xff\xff\xff", 1)
+        _model(gpu_ctx, b"\xff\xff\xff", 1)
 
 
 def _conv_pool_model(x_shape, w, b, conv_pads, conv_strides, relu, pool_k, pool_s, pool_pads, pre_relu=False):
@@ -317,9 +318,8 @@ def _conv_pool_model(x_shape, w, b, conv_pads, conv_strides, relu, pool_k, pool_
 @pytest.mark.parametrize("precision", ["f32", "f16"])
 def test_conv_pool_fusion_bit_identical(gpu_ctx, case, precision):
     """ORE_FUSE_CONV_POOL: the pooled epilogue equals the separate conv + pool kernels bit for bit
-    (forced with ORE_EPOOL_MAX_WORK so the small planes qualify).  f16 models: the conv values are
+    (forced with ORE_FUSE_EAGER so the small planes qualify).  f16 models: the conv values are
     rounded to f16 before the max, as the separate conv stores them (NHWC f16)."""
-    import os
     import ore
     C, H, M, k, cs, cp, relu, pk, ps, ppads = case
     rng = np.random.default_rng(sum(case[:6]))
@@ -328,19 +328,16 @@ def test_conv_pool_fusion_bit_identical(gpu_ctx, case, precision):
     x = rng.standard_normal((3, C, H, H)).astype(np.float32)
     mb = _conv_pool_model((1, C, H, H), w, b, [cp] * 4, [cs, cs], relu, [pk, pk], [ps, ps], ppads)
     vals = []
-    os.environ["ORE_EPOOL_MAX_WORK"] = "100"
-    try:
-        for fusion in (ore.FUSE_ALL | ore.KEEP_VALUES, (ore.FUSE_ALL & ~ore.FUSE_CONV_POOL) | ore.KEEP_VALUES):
-            m = ore.Model(gpu_ctx, mb, max_batch=3, precision=precision)
-            m.set_fusion(fusion)
-            _np(m.run(_t(x)))
-            vals.append(m.read_value("p"))
-            if fusion & ore.FUSE_CONV_POOL and pk == 3 and ps == 2:
-                with pytest.raises(ore.OreError):
-                    m.read_value("r" if relu else "c")  # fused away: the pre-pool tensor is never stored
-            m.close()
-    finally:
-        os.environ.pop("ORE_EPOOL_MAX_WORK", None)
+    eager = ore.FUSE_EAGER | ore.KEEP_VALUES
+    for fusion in (ore.FUSE_ALL | eager, (ore.FUSE_ALL & ~ore.FUSE_CONV_POOL) | eager):
+        m = _model(gpu_ctx, mb, max_batch=3, precision=precision)
+        m.set_fusion(fusion)
+        _np(m.run(_t(x)))
+        vals.append(m.read_value("p"))
+        if fusion & ore.FUSE_CONV_POOL and pk == 3 and ps == 2:
+            with pytest.raises(ore.OreError):
+                m.read_value("r" if relu else "c")  # fused away: the pre-pool tensor is never stored
+        m.close()
     np.testing.assert_array_equal(vals[0], vals[1])
     import oracle
     c = oracle.conv2d(x, w, b, pads=[cp] * 4, strides=(cs, cs))
@@ -360,12 +357,12 @@ def test_conv_pool_fusion_bit_identical(gpu_ctx, case, precision):
     (1, 40, 128, 7),   # one input channel, 4 channel fragments (window kernel)
     (4, 37, 72, 7),    # four input channels, M = 72: a partial third fragment (window kernel)
 ])
-def test_conv_pool_walk_bit_identical(gpu_ctx, case, monkeypatch):
+def test_conv_pool_walk_bit_identical(gpu_ctx, case):
     """The row-walking conv + pool kernels (ore_conv_pool.hip, LDS-ring pooled epilogue with ds_max on
-    the f32 bits; ORE_CONV_POOL_STREAM=1: 48 channels x 64 quads per block, =2: 96 x 128) and the
-    window kernel (=6, ore_conv1_f32.hip: 7x7 / stride 2, C in {1, 3, 4}, 32 < M <= 128) equal the
-    patch-epilogue kernel (=0) and the separate conv + Relu + MaxPool kernels bit for bit, and the
-    oracle within the conv tolerance."""
+    the f32 bits; "epool walk48": 48 channels x 64 quads per block, "walk96": 96 x 128) and the
+    window kernel ("epool window f32", ore_conv1_f32.hip: 7x7 / stride 2, C in {1, 3, 4}, 32 < M <= 128)
+    forced with ore_model_set_step_tile equal the patch-epilogue kernel and the separate conv + Relu +
+    MaxPool kernels bit for bit, and the oracle within the conv tolerance."""
     import ore
     C, H, M, k = case
     rng = np.random.default_rng(sum(case))
@@ -373,18 +370,17 @@ def test_conv_pool_walk_bit_identical(gpu_ctx, case, monkeypatch):
     b = rng.uniform(-0.5, 0.5, M).astype(np.float32)
     x = rng.standard_normal((3, C, H, H)).astype(np.float32)
     mb = _conv_pool_model((1, C, H, H), w, b, [0] * 4, [2, 2], True, [3, 3], [2, 2], [0, 0, 0, 0])
-    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "100")
     vals = []
     names = ore.Model.TILE_NAMES
-    for walk, fusion in (("1", ore.FUSE_ALL), ("0", ore.FUSE_ALL), ("2", ore.FUSE_ALL), ("5", ore.FUSE_ALL),
-                         ("6", ore.FUSE_ALL), ("1", ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
-        monkeypatch.setenv("ORE_CONV_POOL_STREAM", walk)
-        m = ore.Model(gpu_ctx, mb, max_batch=3)
-        m.set_fusion(fusion | ore.KEEP_VALUES)
+    for tile, fusion in ((EPOOL_WALK48, ore.FUSE_ALL), (EPOOL_PATCH, ore.FUSE_ALL), (EPOOL_WALK96, ore.FUSE_ALL),
+                         (EPOOL_WINDOW, ore.FUSE_ALL), (EPOOL_WALK48, ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
+        m = _model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion(fusion | ore.FUSE_EAGER | ore.KEEP_VALUES)
+        forced = force_tiles(m, tile)
         _np(m.run(_t(x)))
         vals.append(m.read_value("p"))
-        if walk == "6" and k == 7 and C in (1, 3, 4) and 32 < M <= 128:  # the window kernel (variant 7) ran
-            assert [names[t] for t in m.tiles() if t >= 0] == ["epool window f32"]
+        if tile == EPOOL_WINDOW and k == 7 and C in (1, 3, 4) and 32 < M <= 128:  # the window kernel ran
+            assert forced == 1 and [names[t] for t in m.tiles() if t >= 0] == ["epool window f32"]
         m.close()
     for v in vals[1:]:
         np.testing.assert_array_equal(vals[0], v)
@@ -405,7 +401,7 @@ def test_conv_pool_walk_bit_identical(gpu_ctx, case, monkeypatch):
     (16, 9, 64, 3, 1, [0, 0, 1, 1]),     # 3 quads per row: a step spans many rows
     (7, 9, 64, 3, 1, [0, 0, 1, 1]),      # 9 C % 16 != 0: the walker declines (patch kernel)
 ])
-def test_conv_pool_walk_stride1_bit_identical(gpu_ctx, case, monkeypatch):
+def test_conv_pool_walk_stride1_bit_identical(gpu_ctx, case):
     """The row-walking conv + pool kernel's stride-1 operand modes (1x1; 3x3 'same' with per-element
     tap masks) for every block shape equal the patch-epilogue kernel and the separate kernels bit for
     bit, ceil-mode pool pads included."""
@@ -416,20 +412,21 @@ def test_conv_pool_walk_stride1_bit_identical(gpu_ctx, case, monkeypatch):
     b = rng.uniform(-0.5, 0.5, M).astype(np.float32)
     x = rng.standard_normal((3, C, H, H)).astype(np.float32)
     mb = _conv_pool_model((1, C, H, H), w, b, [cp] * 4, [1, 1], True, [3, 3], [2, 2], ppads, pre_relu=True)
-    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "100")
     vals = []
     names = ore.Model.TILE_NAMES
-    for walk, fusion in (("0", ore.FUSE_ALL), ("1", ore.FUSE_ALL), ("2", ore.FUSE_ALL), ("3", ore.FUSE_ALL),
-                         ("4", ore.FUSE_ALL), ("5", ore.FUSE_ALL), ("0", ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
-        monkeypatch.setenv("ORE_CONV_POOL_STREAM", walk)
-        m = ore.Model(gpu_ctx, mb, max_batch=3)
-        m.set_fusion(fusion | ore.KEEP_VALUES)
+    for tile, fusion in ((EPOOL_PATCH, ore.FUSE_ALL), (EPOOL_WALK48, ore.FUSE_ALL), (EPOOL_WALK96, ore.FUSE_ALL),
+                         (EPOOL_WALK64, ore.FUSE_ALL), (EPOOL_WALK64_B3, ore.FUSE_ALL),
+                         (EPOOL_PATCH, ore.FUSE_ALL & ~ore.FUSE_CONV_POOL)):
+        m = _model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion(fusion | ore.FUSE_EAGER | ore.KEEP_VALUES)
+        force_tiles(m, tile)
         _np(m.run(_t(x)))
         vals.append(m.read_value("p"))
         walkable = (k == 1 and C % 16 == 0) or (k == 3 and 9 * C % 16 == 0)  # whole ring rounds per step
-        if fusion & ore.FUSE_CONV_POOL and walk in ("1", "3", "4") and M >= 48 and (walk != "4" or H >= 12) and walkable:
+        if (fusion & ore.FUSE_CONV_POOL and tile in (EPOOL_WALK48, EPOOL_WALK64, EPOOL_WALK64_B3) and M >= 48 and
+                (tile != EPOOL_WALK64_B3 or H >= 12) and walkable):
             ran = [names[t] for t in m.tiles() if t >= names.index("epool patch")]  # the forced walker ran
-            assert ran == [names[names.index("epool patch") + int(walk)]], ran
+            assert ran == [names[tile]], ran
         m.close()
     for v in vals[1:]:
         np.testing.assert_array_equal(vals[0], v)
@@ -440,9 +437,9 @@ def test_conv_pool_walk_stride1_bit_identical(gpu_ctx, case, monkeypatch):
 
 
 @pytest.mark.parametrize("hw", [64, 224])
-def test_squeezenet_concat_pool_fusion(gpu_ctx, hw, monkeypatch):
+def test_squeezenet_concat_pool_fusion(gpu_ctx, hw):
     """ORE_FUSE_CONCAT_POOL (in FUSE_ALL; by default fire4 -> pool3 only, here forced onto fire8 ->
-    pool5 too with ORE_CONCAT_POOL_MIN_HW=0: the pools computed in the expand convs'
+    pool5 too with ORE_FUSE_EAGER: the pools computed in the expand convs'
     epilogues, the expand outputs and their concat never stored): every value the fused graph
     materialises -- pool3 / pool5 included -- and the probabilities equal the unfused run's bit
     for bit; the row-walking kernel runs for the pooled expands."""
@@ -451,14 +448,13 @@ def test_squeezenet_concat_pool_fusion(gpu_ctx, hw, monkeypatch):
     mb = squeezenet.build(hw)
     model = onnx_wire.decode_model(mb)
     xt = _t(squeezenet.synthetic_input(3, hw, seed=41))
-    ref = ore.Model(gpu_ctx, mb, max_batch=3)
+    ref = _model(gpu_ctx, mb, max_batch=3)
     ref.set_fusion(ore.KEEP_VALUES)
     y0 = _np(ref.run(xt))
-    monkeypatch.setenv("ORE_CONV_POOL_STREAM", "3")  # the 64-channel walker (auto takes it from batch 128)
-    monkeypatch.setenv("ORE_CONCAT_POOL_MIN_HW", "0")  # fire8 -> pool5 too (27 x 27 planes)
-    monkeypatch.setenv("ORE_FIRE_POOL", "0")  # fire4 -> pool3 stays with the walkers (not fire_pool_kernel)
-    fused = ore.Model(gpu_ctx, mb, max_batch=3)
-    fused.set_fusion(ore.FUSE_ALL | ore.FUSE_CONCAT_POOL | ore.KEEP_VALUES)
+    fused = _model(gpu_ctx, mb, max_batch=3)
+    # fire4 -> pool3 stays with the walkers (no fire_pool_kernel); eager: fire8 -> pool5 too (27 x 27)
+    fused.set_fusion((ore.FUSE_ALL & ~ore.FUSE_FIRE_POOL) | ore.FUSE_EAGER | ore.KEEP_VALUES)
+    force_tiles(fused, EPOOL_WALK64)  # the 64-channel walker (auto takes it from batch 128)
     y1 = _np(fused.run(xt))
     np.testing.assert_array_equal(y0, y1)
     for v in ("pool3", "pool5"):
@@ -482,7 +478,7 @@ def test_squeezenet_conv_pool_fusion(gpu_ctx, hw, precision):
     x = _t(squeezenet.synthetic_input(3, hw, seed=17))
     outs = []
     for fusion in (ore.FUSE_ALL, ore.FUSE_ALL & ~ore.FUSE_CONV_POOL):
-        m = ore.Model(gpu_ctx, mb, max_batch=3, precision=precision)
+        m = _model(gpu_ctx, mb, max_batch=3, precision=precision)
         m.set_fusion(fusion)
         outs.append(_np(m.run(x)))
         m.close()
@@ -519,19 +515,19 @@ def _fire_model(C, H, W, S1, E1, E3, S2):
     (24, 8, 7, 48, 192, 192, 64),     # fire7 -> squeeze8 (MFS = 4), W = 7
     (16, 13, 13, 16, 64, 128, 32),    # unequal expands, fire9-like 13 x 13 planes
 ])
-def test_fire_fusion_bit_identical(gpu_ctx, case, monkeypatch):
+def test_fire_fusion_bit_identical(gpu_ctx, case):
     """ORE_FUSE_FIRE: expand 1x1 + expand 3x3 + Concat + the next squeeze in one launch equals the
-    separate kernels bit for bit (forced with ORE_FIRE_MIN_COLS=0 at these small sizes), and the
+    separate kernels bit for bit (forced with ORE_FUSE_EAGER at these small sizes), and the
     oracle within the conv tolerance."""
     import ore
     import oracle
-    monkeypatch.setenv("ORE_FIRE_MIN_COLS", "0")
     C, H, W, S1, E1, E3, S2 = case
     mb = _fire_model(*case)
     x = np.random.default_rng(sum(case)).standard_normal((5, C, H, W)).astype(np.float32)
     vals = []
-    for fusion in (ore.FUSE_ALL | ore.KEEP_VALUES, (ore.FUSE_ALL & ~ore.FUSE_FIRE) | ore.KEEP_VALUES):
-        m = ore.Model(gpu_ctx, mb, max_batch=5)
+    eager = ore.FUSE_EAGER | ore.KEEP_VALUES
+    for fusion in (ore.FUSE_ALL | eager, (ore.FUSE_ALL & ~ore.FUSE_FIRE) | eager):
+        m = _model(gpu_ctx, mb, max_batch=5)
         m.set_fusion(fusion)
         y = _np(m.run(_t(x)))
         vals.append((y, m.read_value("nr")))
@@ -547,17 +543,17 @@ def test_fire_fusion_bit_identical(gpu_ctx, case, monkeypatch):
 
 
 @pytest.mark.parametrize("hw", [64, 224])
-def test_squeezenet_fire_fusion(gpu_ctx, hw, monkeypatch):
-    """SqueezeNet with the five fire + squeeze pairs fused (ORE_FIRE_MIN_COLS=0 so batch 3 fuses):
-    probabilities bit-identical to the separate kernels."""
+def test_squeezenet_fire_fusion(gpu_ctx, hw):
+    """SqueezeNet with the five fire + squeeze pairs fused (ORE_FUSE_EAGER so batch 3 fuses; the fire +
+    pool + squeeze fusion off): probabilities bit-identical to the separate kernels."""
     import ore
     from ore import squeezenet
-    monkeypatch.setenv("ORE_FIRE_MIN_COLS", "0")
     mb = squeezenet.build(hw)
     x = _t(squeezenet.synthetic_input(3, hw, seed=19))
     outs = []
-    for fusion in (ore.FUSE_ALL, ore.FUSE_ALL & ~ore.FUSE_FIRE):
-        m = ore.Model(gpu_ctx, mb, max_batch=3)
+    base = (ore.FUSE_ALL & ~ore.FUSE_FIRE_POOL) | ore.FUSE_EAGER
+    for fusion in (base, base & ~ore.FUSE_FIRE):
+        m = _model(gpu_ctx, mb, max_batch=3)
         m.set_fusion(fusion)
         outs.append(_np(m.run(x)))
         if fusion & ore.FUSE_FIRE:
@@ -572,7 +568,7 @@ def test_model_io_checks_gpu(gpu_ctx):
     walker sees the pointer (an f16 out would otherwise take 2x its size in f32 stores)."""
     import torch
     import ore
-    m = ore.Model(gpu_ctx, _mnist_bytes(), max_batch=4)
+    m = _model(gpu_ctx, _mnist_bytes(), max_batch=4)
     x = torch.zeros((2, 1, 28, 28), device="cuda")
     out = torch.zeros((2, 10), device="cuda")
     m.run_into(x, out)
@@ -596,7 +592,7 @@ def test_read_value_refuses_overwritten(gpu_ctx):
     from ore import squeezenet
     mb = squeezenet.build(64)
     x = _t(squeezenet.synthetic_input(2, 64, seed=3))
-    m = ore.Model(gpu_ctx, mb, max_batch=2)
+    m = _model(gpu_ctx, mb, max_batch=2)
     m.set_fusion(0)  # op by op: every node's output is a value of its own
     y = _np(m.run(x))
     from ore import onnx_wire
@@ -610,7 +606,7 @@ def test_read_value_refuses_overwritten(gpu_ctx):
             assert "overwritten" in str(e)
             refused += 1
     assert refused > 0  # op-by-op SqueezeNet reuses the early slots
-    keep = ore.Model(gpu_ctx, mb, max_batch=2)
+    keep = _model(gpu_ctx, mb, max_batch=2)
     keep.set_fusion(ore.KEEP_VALUES)
     np.testing.assert_array_equal(_np(keep.run(x)), y)
     for nm in names[:10]:
@@ -619,7 +615,7 @@ def test_read_value_refuses_overwritten(gpu_ctx):
     keep.close()
 
 
-def test_two_contexts_large_lds_variant(monkeypatch):
+def test_two_contexts_large_lds_variant():
     """the 152 KiB row-walking conv1 + pool1 variant raises its dynamic-LDS limit per
     device (not once per process); two contexts driven from two host threads both run the
     batch-128 conv1 + pool1 step and agree bit for bit."""
@@ -631,8 +627,6 @@ def test_two_contexts_large_lds_variant(monkeypatch):
     w = (rng.standard_normal((M, C, k, k)) * 0.3).astype(np.float32)
     b = rng.uniform(-0.5, 0.5, M).astype(np.float32)
     mb = _conv_pool_model((1, C, H, H), w, b, [0] * 4, [2, 2], True, [3, 3], [2, 2], [0, 0, 0, 0])
-    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "100")
-    monkeypatch.setenv("ORE_CONV_POOL_STREAM", "2")  # variant 3: 96 channels x 128 quads, 152 KiB of LDS
     x = torch.from_numpy(rng.standard_normal((128, C, H, H)).astype(np.float32)).cuda()
     res, errs = [None, None], []
 
@@ -640,8 +634,9 @@ def test_two_contexts_large_lds_variant(monkeypatch):
         try:
             torch.cuda.set_device(0)
             ctx = ore.Context(0, use_torch_stream=False)
-            m = ore.Model(ctx, mb, max_batch=128)
-            m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+            m = _model(ctx, mb, max_batch=128)
+            m.set_fusion(ore.FUSE_ALL | ore.FUSE_EAGER | ore.KEEP_VALUES)
+            force_tiles(m, EPOOL_WALK96)  # 96 channels x 128 quads, 152 KiB of LDS
             out = torch.empty((128, m.output_elems), device="cuda")
             m.run_into(x, out)
             ctx.sync()
@@ -686,21 +681,20 @@ def _conv_pool_squeeze_model(H, W, M, Q, pool_pads):
 
 
 @pytest.mark.parametrize("case", [(67, 71, 16, [0, 0, 0, 0]), (40, 45, 12, [0, 0, 1, 1])])
-def test_conv_pool_squeeze_fused_bit_identical(gpu_ctx, case, monkeypatch):
+def test_conv_pool_squeeze_fused_bit_identical(gpu_ctx, case):
     """f32: conv1 + Relu + pool1 + the next 1x1 conv + Relu in one window-kernel launch (pooled-conv
     variant 7 with the squeeze inside, the pooled map never stored) equals the separate launches
-    (ORE_C1_SQUEEZE=0) bit for bit, and the oracle within the conv tolerance."""
+    (without ORE_FUSE_FIRST_SQUEEZE) bit for bit, and the oracle within the conv tolerance."""
     import ore
     import oracle
-    monkeypatch.setenv("ORE_EPOOL_MAX_WORK", "8")
     H, W, Q, pads = case
     mb = _conv_pool_squeeze_model(H, W, 96, Q, pads)
     x = (np.random.default_rng(H + W).standard_normal((3, 3, H, W)) * 20).astype(np.float32)
     vals = []
     for on in ("1", "0"):
-        monkeypatch.setenv("ORE_C1_SQUEEZE", on)
-        m = ore.Model(gpu_ctx, mb, max_batch=3)
-        m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+        m = _model(gpu_ctx, mb, max_batch=3)
+        fusion = ore.FUSE_ALL if on == "1" else ore.FUSE_ALL & ~ore.FUSE_FIRST_SQUEEZE
+        m.set_fusion(fusion | ore.FUSE_EAGER | ore.KEEP_VALUES)
         y = _np(m.run(_t(x)))
         vals.append((y, m.read_value("qr")))
         names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
@@ -717,7 +711,7 @@ def test_conv_pool_squeeze_fused_bit_identical(gpu_ctx, case, monkeypatch):
     np.testing.assert_allclose(vals[0][0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-5)
 
 
-def test_squeezenet_conv1_squeeze_fused(gpu_ctx, monkeypatch):
+def test_squeezenet_conv1_squeeze_fused(gpu_ctx):
     """SqueezeNet-1.0 @224 f32: conv1 + pool1 + fire2/squeeze1x1 in one launch; probabilities equal the
     plan without that fusion bit for bit."""
     import ore
@@ -726,8 +720,8 @@ def test_squeezenet_conv1_squeeze_fused(gpu_ctx, monkeypatch):
     x = _t(squeezenet.synthetic_input(3, 224, seed=29))
     outs = []
     for on in ("1", "0"):
-        monkeypatch.setenv("ORE_C1_SQUEEZE", on)
-        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        m = _model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion(ore.FUSE_ALL if on == "1" else ore.FUSE_ALL & ~ore.FUSE_FIRST_SQUEEZE)
         outs.append(_np(m.run(x)))
         first = ore.Model.TILE_NAMES[m.tiles()[0]]
         assert (first == "epool window f32") == (on == "1"), first
@@ -762,10 +756,10 @@ def _pool_squeeze_model(C, H, W, M, pool_pads, relu=True):
     (64, 20, 31, 48, [0, 0, 1, 1], True),    # ceil-mode pads, 16 pooled columns, M = 48
     (32, 9, 7, 10, [1, 1, 1, 1], False),     # padded on all sides, no Relu (negative outputs), M = 10
 ])
-def test_pool_squeeze_fused_bit_identical(gpu_ctx, case, monkeypatch):
+def test_pool_squeeze_fused_bit_identical(gpu_ctx, case):
     """f32: a 3x3 / stride-2 MaxPool and the 1x1 conv that is its only reader in one launch
     (pool_conv1x1_f32_kernel, the pooled map never stored) equal maxpool_kernel + the separate conv
-    (ORE_POOL_SQUEEZE=0) bit for bit, and the oracle within the conv tolerance."""
+    (without ORE_FUSE_POOL_SQUEEZE) bit for bit, and the oracle within the conv tolerance."""
     import ore
     import oracle
     C, H, W, M, pads, relu = case
@@ -773,9 +767,8 @@ def test_pool_squeeze_fused_bit_identical(gpu_ctx, case, monkeypatch):
     x = np.random.default_rng(C + H).standard_normal((3, C, H, W)).astype(np.float32)
     vals = []
     for on in ("1", "0"):
-        monkeypatch.setenv("ORE_POOL_SQUEEZE", on)
-        m = ore.Model(gpu_ctx, mb, max_batch=3)
-        m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+        m = _model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion((ore.FUSE_ALL if on == "1" else ore.FUSE_ALL & ~ore.FUSE_POOL_SQUEEZE) | ore.KEEP_VALUES)
         y = _np(m.run(_t(x)))
         vals.append((y, m.read_value(out)))
         if on == "1":
@@ -790,7 +783,7 @@ def test_pool_squeeze_fused_bit_identical(gpu_ctx, case, monkeypatch):
     np.testing.assert_allclose(vals[0][0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-5)
 
 
-def test_squeezenet_pool_squeeze_fused(gpu_ctx, monkeypatch):
+def test_squeezenet_pool_squeeze_fused(gpu_ctx):
     """SqueezeNet-1.0 @224 f32: pool5 + fire9/squeeze1x1 in one launch; probabilities equal the plan
     without that fusion bit for bit."""
     import ore
@@ -799,8 +792,8 @@ def test_squeezenet_pool_squeeze_fused(gpu_ctx, monkeypatch):
     x = _t(squeezenet.synthetic_input(3, 224, seed=31))
     outs, nsteps = [], []
     for on in ("1", "0"):
-        monkeypatch.setenv("ORE_POOL_SQUEEZE", on)
-        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        m = _model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion(ore.FUSE_ALL if on == "1" else ore.FUSE_ALL & ~ore.FUSE_POOL_SQUEEZE)
         outs.append(_np(m.run(x)))
         nsteps.append(len(m.tiles()))
         m.close()
@@ -842,23 +835,21 @@ def _fire_pool_model(C, H, W, S1, E1, E3, S2, pool_pads):
     (32, 9, 8, 32, 128, 64, 16, [0, 0, 0, 0]),     # 'valid' pool, W = 8, unequal expands
     (16, 30, 17, 16, 64, 128, 64, [0, 0, 1, 1]),   # MFS = 4, short last band
 ])
-def test_fire_pool_fusion_bit_identical(gpu_ctx, case, monkeypatch):
+def test_fire_pool_fusion_bit_identical(gpu_ctx, case):
     """f32: fire module + 3x3 / stride-2 MaxPool + the next squeeze in one launch (fire_pool_kernel;
     the expand outputs, their concat and the pooled map never stored) equal the pooled-epilogue
-    expands + the separate squeeze (ORE_FIRE_POOL=0) bit for bit, and the oracle within the conv
-    tolerance."""
+    expands + the separate squeeze (without ORE_FUSE_FIRE_POOL) bit for bit, and the oracle within the
+    conv tolerance."""
     import ore
     import oracle
-    monkeypatch.setenv("ORE_FIRE_MIN_COLS", "0")
-    monkeypatch.setenv("ORE_FIRE_POOL_MIN_HW", "0")
     C, H, W, S1, E1, E3, S2, pads = case
     mb = _fire_pool_model(*case)
     x = np.random.default_rng(sum(case[:7])).standard_normal((5, C, H, W)).astype(np.float32)
     vals = []
     for on in ("1", "0"):
-        monkeypatch.setenv("ORE_FIRE_POOL", on)
-        m = ore.Model(gpu_ctx, mb, max_batch=5)
-        m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+        m = _model(gpu_ctx, mb, max_batch=5)
+        fusion = ore.FUSE_ALL if on == "1" else ore.FUSE_ALL & ~ore.FUSE_FIRE_POOL
+        m.set_fusion(fusion | ore.FUSE_EAGER | ore.KEEP_VALUES)
         y = _np(m.run(_t(x)))
         vals.append((y, m.read_value("nr")))
         names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
@@ -874,22 +865,22 @@ def test_fire_pool_fusion_bit_identical(gpu_ctx, case, monkeypatch):
     np.testing.assert_allclose(vals[0][0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-6)
 
 
-def test_squeezenet_fire_pool_fused(gpu_ctx, monkeypatch):
-    """SqueezeNet-1.0 @224 f32: fire4 + pool3 + fire5/squeeze1x1 in one launch (ORE_FIRE_MIN_COLS=0
-    so batch 3 fuses); probabilities equal the plan without it (ORE_FIRE_POOL=0) bit for bit."""
+def test_squeezenet_fire_pool_fused(gpu_ctx):
+    """SqueezeNet-1.0 @224 f32: fire4 + pool3 + fire5/squeeze1x1 and (eager: 27 x 27 planes too) fire8 +
+    pool5 + fire9/squeeze1x1 in one launch each (ORE_FUSE_EAGER so batch 3 fuses); probabilities
+    equal the plan without ORE_FUSE_FIRE_POOL bit for bit."""
     import ore
     from ore import squeezenet
-    monkeypatch.setenv("ORE_FIRE_MIN_COLS", "0")
     mb = squeezenet.build(224)
     x = _t(squeezenet.synthetic_input(3, 224, seed=37))
     outs, nsteps = [], []
     for on in ("1", "0"):
-        monkeypatch.setenv("ORE_FIRE_POOL", on)
-        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        m = _model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion((ore.FUSE_ALL if on == "1" else ore.FUSE_ALL & ~ore.FUSE_FIRE_POOL) | ore.FUSE_EAGER)
         outs.append(_np(m.run(x)))
         names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
-        assert names.count("fire pool f32") == (1 if on == "1" else 0), names
+        assert names.count("fire pool f32") == (2 if on == "1" else 0), names
         nsteps.append(len(m.tiles()))
         m.close()
     np.testing.assert_array_equal(outs[0], outs[1])
-    assert nsteps[0] == nsteps[1] - 2  # two expand walkers + the squeeze -> fire_pool_kernel
+    assert nsteps[0] == nsteps[1] - 4  # per pair: two expand walkers + the squeeze -> fire_pool_kernel

@@ -10,6 +10,8 @@ import zlib
 import numpy as np
 import pytest
 
+from _knobs import conv_tile, pool_variant
+
 import oracle
 
 pytestmark = pytest.mark.gpu
@@ -66,13 +68,10 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("window", ["0", "1"])
 @pytest.mark.parametrize("case", CONV_CASES)
 @pytest.mark.parametrize("fuse_relu", [False, True])
-def test_conv2d(gpu_ctx, case, fuse_relu, window, monkeypatch):
-    """window=1 routes planes >= 512 pixels to the (opt-in) window-staged kernel."""
+def test_conv2d(gpu_ctx, case, fuse_relu):
     import ore
-    monkeypatch.setenv("ORE_CONV_WINDOW", window)
     N, C, H, W, M, kh, kw, auto_pad, pads, strides, with_bias = case
     rng = np.random.default_rng(zlib.crc32(repr(case).encode()))
     x = rng.standard_normal((N, C, H, W)).astype(np.float32)
@@ -94,12 +93,12 @@ def test_conv2d(gpu_ctx, case, fuse_relu, window, monkeypatch):
     assert np.all(err <= 2e-6 * bound + 1e-30), f"max err {err.max()} vs bound {(2e-6 * bound).max()}"
 
 
-@pytest.mark.parametrize("tile", ["4", "5", "6", "7", "8", "9", "10", "11"])
+@pytest.mark.parametrize("tile", [1, 2, 3])
 @pytest.mark.parametrize("case", CONV_CASES[::2] + CONV_CASES[14:16])
-def test_conv2d_direct_bit_identical(gpu_ctx, case, tile, monkeypatch):
-    """The LDS-free direct kernel (tiles 4-7) and the warp-specialised kernel (tiles 8-11) run
-    the same k-ordered MFMA chain per output as the LDS-staged kernel (tile 0): bit-identical
-    outputs, and within tolerance of the oracle."""
+def test_conv2d_tiles_bit_identical(gpu_ctx, case, tile):
+    """The LDS-staged kernel's block tiles (ore_ctx_set_conv_tile) run the same k-ordered MFMA chain
+    per output as tile 0: bit-identical outputs, and within tolerance of the oracle.  (Tile ids 4-11,
+    the retired direct / warp-specialised variants, are refused.)"""
     import ore
     N, C, H, W, M, kh, kw, auto_pad, pads, strides, with_bias = case
     rng = np.random.default_rng(zlib.crc32(repr(case).encode()) ^ 0x5a5a)
@@ -107,13 +106,16 @@ def test_conv2d_direct_bit_identical(gpu_ctx, case, tile, monkeypatch):
     w = rng.standard_normal((M, C, kh, kw)).astype(np.float32)
     b = rng.standard_normal((M,)).astype(np.float32) if with_bias else None
     outs = []
-    for t in ("0", tile):
-        monkeypatch.setenv("ORE_CONV_CFG", t)
-        outs.append(_np(ore.convolution(gpu_ctx, _t(x), _t(w), _t(b) if b is not None else None, auto_pad=auto_pad,
-                                        pads=pads, strides=strides, fuse_relu=True)))
+    for t in (0, tile):
+        with conv_tile(gpu_ctx, t):
+            outs.append(_np(ore.convolution(gpu_ctx, _t(x), _t(w), _t(b) if b is not None else None, auto_pad=auto_pad,
+                                            pads=pads, strides=strides, fuse_relu=True)))
     np.testing.assert_array_equal(outs[1], outs[0])
     ref = oracle.relu(oracle.conv2d(x, w, b, auto_pad=auto_pad, pads=pads, strides=strides))
     assert np.abs(outs[1] - ref).max() <= 1e-4 * (np.abs(ref).max() + 1.0)
+    for retired in (4, 8, 11):
+        with pytest.raises(ore.OreError):
+            gpu_ctx.set_conv_tile(retired)
 
 
 STREAM_CASES = [
@@ -134,9 +136,9 @@ STREAM_CASES = [
 ]
 
 
-@pytest.mark.parametrize("tile", [str(t) for t in range(12, 21)])
+@pytest.mark.parametrize("tile", list(range(12, 21)))
 @pytest.mark.parametrize("case", STREAM_CASES)
-def test_conv_stream_bit_identical(gpu_ctx, case, tile, monkeypatch):
+def test_conv_stream_bit_identical(gpu_ctx, case, tile):
     """The LDS-free streaming kernel (ore_conv_stream.hip, 16x16x4 MFMA, tiles 12-16: 1x1 and 3x3
     'same' convs) runs the same k-ordered fmaf chain per output as the LDS-staged kernel:
     bit-identical to tile 0, and within the conv tolerance of the oracle."""
@@ -154,11 +156,11 @@ def test_conv_stream_bit_identical(gpu_ctx, case, tile, monkeypatch):
     xd = buf[1024 + 64:].view(x.shape)
     xd.copy_(_t(x))
     outs = []
-    for t in ("0", tile):
-        monkeypatch.setenv("ORE_CONV_CFG", t)
-        for relu in (False, True):
-            outs.append(_np(ore.convolution(gpu_ctx, xd, _t(w), _t(b) if b is not None else None,
-                                            auto_pad="NOTSET", pads=pads, strides=(1, 1), fuse_relu=relu)))
+    for t in (0, tile):
+        with conv_tile(gpu_ctx, t):
+            for relu in (False, True):
+                outs.append(_np(ore.convolution(gpu_ctx, xd, _t(w), _t(b) if b is not None else None,
+                                                auto_pad="NOTSET", pads=pads, strides=(1, 1), fuse_relu=relu)))
     np.testing.assert_array_equal(outs[2], outs[0])
     np.testing.assert_array_equal(outs[3], outs[1])
     ref = oracle.conv2d(x, w, b, auto_pad="NOTSET", pads=pads, strides=(1, 1))
@@ -181,18 +183,18 @@ def test_conv_integer_exact(gpu_ctx):
     np.testing.assert_array_equal(got, ref)
 
 
-@pytest.mark.parametrize("window", ["1", "0"])
-def test_conv_integer_exact_window(gpu_ctx, window, monkeypatch):
-    """Window-eligible geometry on both conv kernels (ORE_CONV_WINDOW=0 forces the gather
-    kernel): small-integer data, so both equal the oracle bit for bit."""
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 12])
+def test_conv_integer_exact_tiles(gpu_ctx, tile):
+    """A 3x3 'same' layer on every LDS-staged tile and the streaming kernel: small-integer data, so each
+    equals the oracle bit for bit."""
     import ore
-    monkeypatch.setenv("ORE_CONV_WINDOW", window)
     rng = np.random.default_rng(11)
     x = rng.integers(-4, 5, size=(2, 19, 30, 29)).astype(np.float32)
     w = rng.integers(-3, 4, size=(100, 19, 3, 3)).astype(np.float32)
     b = rng.integers(-5, 6, size=(100,)).astype(np.float32)
     ref = oracle.conv2d(x, w, b, pads=[1, 1, 1, 1], strides=(1, 1))
-    got = _np(ore.convolution(gpu_ctx, _t(x), _t(w), _t(b), pads=[1, 1, 1, 1], strides=(1, 1)))
+    with conv_tile(gpu_ctx, tile):
+        got = _np(ore.convolution(gpu_ctx, _t(x), _t(w), _t(b), pads=[1, 1, 1, 1], strides=(1, 1)))
     np.testing.assert_array_equal(got, ref)
 
 
@@ -230,19 +232,21 @@ POOL_CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "5"])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5])
 @pytest.mark.parametrize("case", POOL_CASES)
-def test_maxpool(gpu_ctx, case, variant, monkeypatch):
-    """Every MaxPool kernel (ORE_POOL_VARIANT: auto, band-LDS, direct, column strip, plane-LDS, chunk-LDS;
-    a variant that does not apply to a shape falls through to the direct kernel)."""
+def test_maxpool(gpu_ctx, case, variant):
+    """Every MaxPool kernel (ore_ctx_set_pool_variant: by layout, direct, column strip, plane-LDS,
+    chunk-LDS; a variant that does not apply to a shape falls through to the direct kernel)."""
     import ore
-    monkeypatch.setenv("ORE_POOL_VARIANT", variant)
     N, C, H, W, k, s, auto_pad, pads = case
     rng = np.random.default_rng(3)
     x = (rng.standard_normal((N, C, H, W)) - 2.0).astype(np.float32)  # mostly negative: zero padding shows
     ref = oracle.maxpool2d(x, k, s, auto_pad=auto_pad, pads=pads)
-    got = _np(ore.max_pool(gpu_ctx, _t(x), k, s, auto_pad=auto_pad, pads=pads))
+    with pool_variant(gpu_ctx, variant):
+        got = _np(ore.max_pool(gpu_ctx, _t(x), k, s, auto_pad=auto_pad, pads=pads))
     np.testing.assert_array_equal(got, ref)
+    with pytest.raises(ore.OreError):
+        gpu_ctx.set_pool_variant(1)  # the retired band kernel
 
 
 def test_relu_reference_kat(gpu_ctx):

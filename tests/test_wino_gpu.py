@@ -17,6 +17,8 @@ import os
 import numpy as np
 import pytest
 
+from _knobs import conv_tile
+
 from test_x3_gpu import _conv_model, conv_f64
 
 pytestmark = pytest.mark.gpu
@@ -34,13 +36,6 @@ def _np(t):
     import torch
     torch.cuda.synchronize()
     return t.cpu().numpy()
-
-
-@pytest.fixture(autouse=True)
-def default_algo(monkeypatch):
-    monkeypatch.delenv("ORE_NO_WINOGRAD", raising=False)
-    monkeypatch.delenv("ORE_WINO_TILE", raising=False)
-    monkeypatch.delenv("ORE_FIRE_WINO", raising=False)
 
 
 # N, C, H, W, M: the SqueezeNet expand3x3 families and ragged edges (odd planes, 1-pixel planes,
@@ -114,10 +109,9 @@ def test_wino_exact_on_small_integers(gpu_ctx):
 
 
 @pytest.mark.parametrize("ci", [0, 3, 4, 5, 9])
-def test_wino_tiles_bit_identical(gpu_ctx, ci, monkeypatch):
-    """Every Winograd tile (ORE_WINO_TILE=0..4; 4 = the LDS-staged kernel) computes each output the
-    same way: identical bits;
-    the model reports the tile it ran."""
+def test_wino_tiles_bit_identical(gpu_ctx, ci):
+    """Every Winograd tile (ore_ctx_set_conv_tile, "wino 32x32 d4" .. "wino16 16x32") computes each
+    output the same way: identical bits; the model reports the tile it ran."""
     import ore
     N, C, H, W, M = CASES[ci]
     rng = np.random.default_rng(3)
@@ -127,9 +121,9 @@ def test_wino_tiles_bit_identical(gpu_ctx, ci, monkeypatch):
     mb = _conv_model((1, C, H, W), w, b, [1] * 4, [1, 1])
     base = ore.Model.TILE_NAMES.index("wino 32x32 d4")
     outs = []
-    for t in range(5):
-        monkeypatch.setenv("ORE_WINO_TILE", str(t))
-        m = ore.Model(gpu_ctx, mb, max_batch=N)
+    for t in range(4):
+        with conv_tile(gpu_ctx, base + t):
+            m = ore.Model(gpu_ctx, mb, max_batch=N)
         outs.append(_np(m.run(_t(x))))
         assert m.tiles()[0] == base + t, (m.tiles(), base + t)
         m.close()
@@ -218,134 +212,3 @@ def test_set_conv_algo_rejects_unknown(gpu_ctx):
     import ore
     with pytest.raises(ore.OreError):
         gpu_ctx.set_conv_algo(7)
-
-
-@pytest.mark.parametrize("case", [
-    # C, H, W, S1, E1, E3, S2 (as tests/test_model_gpu.py::test_fire_fusion_bit_identical)
-    (16, 12, 12, 16, 64, 64, 16),     # fire2 -> squeeze3 family
-    (32, 9, 8, 32, 128, 128, 48),     # fire5 -> squeeze6 (MFS = 3), W = 8
-    (24, 8, 7, 48, 192, 192, 64),     # fire7 -> squeeze8 (MFS = 4), odd W: right-edge tiles half outside
-    (16, 13, 13, 16, 64, 128, 32),    # unequal expands, 13 x 13 planes (odd H and W)
-])
-def test_fire_wino_fusion_bit_identical(gpu_ctx, case, monkeypatch):
-    """The fused fire module with its expand3x3 by Winograd ("fire wino", opt-in ORE_FIRE_WINO=1) equals
-    the separate kernels (Winograd expand3x3) bit for bit, and the oracle within the conv tolerance."""
-    import ore
-    import oracle
-    from test_model_gpu import _fire_model
-    monkeypatch.setenv("ORE_FIRE_MIN_COLS", "0")
-    monkeypatch.setenv("ORE_FIRE_WINO", "1")
-    C, H, W, S1, E1, E3, S2 = case
-    mb = _fire_model(*case)
-    x = np.random.default_rng(sum(case)).standard_normal((5, C, H, W)).astype(np.float32)
-    vals = []
-    for fusion in (ore.FUSE_ALL | ore.KEEP_VALUES, (ore.FUSE_ALL & ~ore.FUSE_FIRE) | ore.KEEP_VALUES):
-        m = ore.Model(gpu_ctx, mb, max_batch=5)
-        m.set_fusion(fusion)
-        y = _np(m.run(_t(x)))
-        vals.append((y, m.read_value("nr")))
-        names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
-        if fusion & ore.FUSE_FIRE:
-            assert "fire wino" in names, names
-        else:
-            assert any(n.startswith("wino") for n in names), names
-        m.close()
-    np.testing.assert_array_equal(vals[0][1], vals[1][1])
-    np.testing.assert_array_equal(vals[0][0], vals[1][0])
-    ref = oracle.Model(mb).run(x, S2)
-    np.testing.assert_allclose(vals[0][0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-6)
-
-
-@pytest.mark.parametrize("hw", [64, 224])
-def test_squeezenet_fire_wino_fusion(gpu_ctx, hw, monkeypatch):
-    """SqueezeNet with the fire + squeeze pairs fused on the Winograd fire kernel: probabilities
-    bit-identical to the separate (Winograd) kernels."""
-    import ore
-    from ore import squeezenet
-    monkeypatch.setenv("ORE_FIRE_MIN_COLS", "0")
-    monkeypatch.setenv("ORE_FIRE_WINO", "1")
-    mb = squeezenet.build(hw)
-    x = _t(squeezenet.synthetic_input(3, hw, seed=19))
-    outs = []
-    for fusion in (ore.FUSE_ALL, ore.FUSE_ALL & ~ore.FUSE_FIRE):
-        m = ore.Model(gpu_ctx, mb, max_batch=3)
-        m.set_fusion(fusion)
-        outs.append(_np(m.run(x)))
-        if fusion & ore.FUSE_FIRE:
-            n = sum(1 for t in m.tiles() if t >= 0 and ore.Model.TILE_NAMES[t] == "fire wino")
-            assert n == (5 if hw == 224 else 2), n
-        m.close()
-    np.testing.assert_array_equal(outs[0], outs[1])
-
-
-@pytest.mark.parametrize("case", [
-    # C, H, W, S1, E1 = E3, S2 (the expands read the S1-channel squeeze output)
-    (16, 12, 12, 16, 64, 64, 16),     # fire2 family
-    (32, 9, 8, 32, 128, 128, 48),     # even W, row wraps inside a tile group
-    (16, 13, 13, 64, 256, 256, 64),   # fire9 family: odd H and W (half-outside edge tiles)
-    (16, 6, 7, 48, 40, 40, 8),        # 40 channels: a partial 32-channel m tile, odd W
-    (16, 1, 1, 16, 32, 32, 8),        # 1 x 1 plane: the centre tap only
-])
-def test_wino_e1_fusion_bit_identical(gpu_ctx, case, monkeypatch):
-    """(3b), opt-in ORE_WINO_E1=1: the expand1x1 beside a Winograd expand3x3 runs inside the Winograd
-    launch (conv_wino16_kernel E1, tile "wino16 32x16"): the Concat it writes equals the separate 1x1
-    conv's bit for bit (ORE_WINO_E1=0), the model launches one conv fewer, and the oracle agrees
-    within the conv tolerance."""
-    import ore
-    import oracle
-    from test_model_gpu import _fire_model
-    C, H, W, S1, E1, E3, S2 = case
-    mb = _fire_model(*case)
-    x = np.random.default_rng(sum(case) + 1).standard_normal((5, C, H, W)).astype(np.float32)
-    names_all, vals = [], []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("ORE_WINO_E1", flag)
-        m = ore.Model(gpu_ctx, mb, max_batch=5)
-        m.set_fusion((ore.FUSE_ALL & ~ore.FUSE_FIRE) | ore.KEEP_VALUES)
-        y = _np(m.run(_t(x)))
-        vals.append((y, m.read_value("cat")))
-        names_all.append([ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0])
-        m.close()
-    fused, plain = names_all
-    assert len(fused) == len(plain) - 1, (fused, plain)
-    assert "wino16 32x16" in fused, fused
-    np.testing.assert_array_equal(vals[0][1], vals[1][1])
-    np.testing.assert_array_equal(vals[0][0], vals[1][0])
-    ref = oracle.Model(mb).run(x, S2)
-    np.testing.assert_allclose(vals[0][0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-6)
-
-
-def test_wino_e1_needs_equal_channels(gpu_ctx, monkeypatch):
-    """Unequal expands (E1 != E3) keep the separate 1x1 conv."""
-    import ore
-    from test_model_gpu import _fire_model
-    monkeypatch.setenv("ORE_WINO_E1", "1")
-    mb = _fire_model(16, 8, 8, 16, 32, 64, 8)
-    m = ore.Model(gpu_ctx, mb, max_batch=2)
-    m.set_fusion(ore.FUSE_ALL & ~ore.FUSE_FIRE)
-    names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
-    m.close()
-    assert sum(n.startswith("wino") for n in names) == 1 and len(names) == 4, names
-
-
-def test_squeezenet_wino_e1_fusion(gpu_ctx, monkeypatch):
-    """SqueezeNet @224 default plan at B = 3 (too few columns for the fused fire kernels, so every
-    fire module's expands run separately): each expand1x1 inside its Winograd expand3x3 launch,
-    probabilities bit-identical to ORE_WINO_E1=0."""
-    import ore
-    from ore import squeezenet
-    mb = squeezenet.build(224)
-    x = _t(squeezenet.synthetic_input(3, 224, seed=29))
-    outs, counts = [], []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("ORE_WINO_E1", flag)
-        m = ore.Model(gpu_ctx, mb, max_batch=3)
-        outs.append(_np(m.run(x)))
-        counts.append(sum(1 for t in m.tiles() if t >= 0))
-        if flag == "1":
-            names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
-            nf = names.count("wino16 32x16")
-            assert nf >= 2, names  # fire8 / fire9 at least
-        m.close()
-    assert counts[0] == counts[1] - nf, counts
-    np.testing.assert_array_equal(outs[0], outs[1])

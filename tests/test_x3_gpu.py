@@ -14,6 +14,8 @@ import os
 import numpy as np
 import pytest
 
+from _knobs import conv_tile
+
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -31,14 +33,17 @@ def _np(t):
     return t.cpu().numpy()
 
 
+X3_ALL = True
+
+
 @pytest.fixture(autouse=True)
-def x3_all(monkeypatch, request):
-    """Kernel-level tests put every conv on x3 (ORE_X3_ALL=1); tests marked `hybrid` keep the
+def x3_all(request):
+    """Kernel-level tests put every conv on x3 (ORE_LOAD_X3_ALL); tests marked `hybrid` keep the
     default ORE_LOAD_X3 policy (x3 where it wins, the f32-MFMA fusions elsewhere)."""
-    if "hybrid" not in request.keywords:
-        monkeypatch.setenv("ORE_X3_ALL", "1")
-    else:
-        monkeypatch.delenv("ORE_X3_ALL", raising=False)
+    global X3_ALL
+    X3_ALL = "hybrid" not in request.keywords
+    yield
+    X3_ALL = True
 
 
 def conv_f64(x, w, b, pads, strides):
@@ -129,7 +134,7 @@ def test_x3_exact_on_small_integers(gpu_ctx):
     w = rng.integers(-4, 5, (24, 12, 3, 3)).astype(np.float32)
     b = rng.integers(-3, 4, 24).astype(np.float32)
     mb = _conv_model((1, 12, 14, 14), w, b, [1, 1, 1, 1], [1, 1])
-    m = ore.Model(gpu_ctx, mb, max_batch=2, precision="f32x3")
+    m = ore.Model(gpu_ctx, mb, max_batch=2, precision="f32x3", x3_all=X3_ALL)
     y = _np(m.run(_t(x)))
     m.close()
     ref, _ = conv_f64(x, w, b, [1] * 4, (1, 1))
@@ -148,7 +153,7 @@ def test_x3_split_is_exact_for_wide_exponents(gpu_ctx):
     for i in range(8):
         w[i, (i * 3) % 8, 0, 0] = 1.0
     mb = _conv_model((1, 8, 6, 8), w, None, [0, 0, 0, 0], [1, 1])
-    m = ore.Model(gpu_ctx, mb, max_batch=2, precision="f32x3")
+    m = ore.Model(gpu_ctx, mb, max_batch=2, precision="f32x3", x3_all=X3_ALL)
     y = _np(m.run(_t(x))).reshape(2, 8, 6, 8)
     m.close()
     for i in range(8):
@@ -156,8 +161,8 @@ def test_x3_split_is_exact_for_wide_exponents(gpu_ctx):
 
 
 @pytest.mark.parametrize("ci", [0, 1, 4, 8, 9])
-def test_x3_tiles_bit_identical(gpu_ctx, ci, monkeypatch):
-    """Every x3 tile of a kernel family (ORE_X3_TILE=0..3: the gather kernel's, or the window
+def test_x3_tiles_bit_identical(gpu_ctx, ci):
+    """Every x3 tile of a kernel family (ore_ctx_set_conv_tile: the gather kernel's, or the window
     kernel's for stride-1 geometries) runs the same per-output sequence: identical bits."""
     import ore
     case = CASES[ci]
@@ -168,11 +173,11 @@ def test_x3_tiles_bit_identical(gpu_ctx, ci, monkeypatch):
     b = rng.uniform(-0.1, 0.1, M).astype(np.float32)
     mb = _conv_model((1, C, H, W), w, b, [pd] * 4, [st, st])
     outs = []
+    base = ore.Model.TILE_NAMES.index("x3w 128x128" if ci in WINDOW else "x3 128x128")
     for t in range(4):
-        monkeypatch.setenv("ORE_X3_TILE", str(t))
-        m = ore.Model(gpu_ctx, mb, max_batch=N, precision="f32x3")
+        with conv_tile(gpu_ctx, base + t):
+            m = ore.Model(gpu_ctx, mb, max_batch=N, precision="f32x3", x3_all=X3_ALL)
         outs.append(_np(m.run(_t(x))))
-        base = ore.Model.TILE_NAMES.index("x3w 128x128" if ci in WINDOW else "x3 128x128")
         assert m.tiles()[0] == base + t, (m.tiles(), base + t)
         m.close()
     for o in outs[1:]:
@@ -180,7 +185,7 @@ def test_x3_tiles_bit_identical(gpu_ctx, ci, monkeypatch):
 
 
 @pytest.mark.parametrize("ci", sorted(WINDOW))
-def test_x3_window_vs_gather(gpu_ctx, ci, monkeypatch):
+def test_x3_window_vs_gather(gpu_ctx, ci):
     """The window kernel (k order (tap, channel)) and the gather kernel (k order (channel, tap)) on
     the same stride-1 conv: both within the f32 bar of float64 (different summation orders)."""
     import ore
@@ -192,9 +197,9 @@ def test_x3_window_vs_gather(gpu_ctx, ci, monkeypatch):
     mb = _conv_model((1, C, H, W), w, b, [pd] * 4, [st, st])
     ref, mag = conv_f64(x, w, b, [pd] * 4, (st, st))
     names = ore.Model.TILE_NAMES
-    for win in ("0", "1"):
-        monkeypatch.setenv("ORE_X3_WINDOW", win)
-        m = ore.Model(gpu_ctx, mb, max_batch=N, precision="f32x3")
+    for win in ("0", "1"):  # 0: a gather tile forced (ore_ctx_set_conv_tile), 1: the default window kernel
+        with conv_tile(gpu_ctx, names.index("x3 128x128") if win == "0" else -1):
+            m = ore.Model(gpu_ctx, mb, max_batch=N, precision="f32x3", x3_all=X3_ALL)
         y = _np(m.run(_t(x))).reshape(ref.shape)
         assert names[m.tiles()[0]].startswith("x3w" if win == "1" else "x3 "), names[m.tiles()[0]]
         m.close()
@@ -206,7 +211,7 @@ def test_x3_mnist_golden(gpu_ctx):
     import ore
     from ore import onnx_wire
     with open(os.path.join(GOLD, "mnist-8.onnx"), "rb") as f:
-        m = ore.Model(gpu_ctx, f.read(), max_batch=4, precision="f32x3")
+        m = ore.Model(gpu_ctx, f.read(), max_batch=4, precision="f32x3", x3_all=X3_ALL)
     x = onnx_wire.load_tensor(os.path.join(GOLD, "mnist_data_0.pb")).to_numpy()
     g = onnx_wire.load_tensor(os.path.join(GOLD, "mnist_output_0.pb")).to_numpy()
     y = _np(m.run(_t(x)))
@@ -223,7 +228,7 @@ def test_x3_hybrid_mnist_golden(gpu_ctx):
     import ore
     from ore import onnx_wire
     with open(os.path.join(GOLD, "mnist-8.onnx"), "rb") as f:
-        m = ore.Model(gpu_ctx, f.read(), max_batch=4, precision="f32x3")
+        m = ore.Model(gpu_ctx, f.read(), max_batch=4, precision="f32x3", x3_all=X3_ALL)
     x = onnx_wire.load_tensor(os.path.join(GOLD, "mnist_data_0.pb")).to_numpy()
     g = onnx_wire.load_tensor(os.path.join(GOLD, "mnist_output_0.pb")).to_numpy()
     y = _np(m.run(_t(x)))
@@ -236,14 +241,7 @@ def test_x3_hybrid_mnist_golden(gpu_ctx):
 def _x3_model(gpu_ctx, hybrid, max_batch):
     import ore
     from ore import squeezenet
-    if hybrid:
-        os.environ.pop("ORE_X3_ALL", None)
-    else:
-        os.environ["ORE_X3_ALL"] = "1"
-    try:
-        return ore.Model(gpu_ctx, squeezenet.build(224), max_batch=max_batch, precision="f32x3")
-    finally:
-        os.environ.pop("ORE_X3_ALL", None)
+    return ore.Model(gpu_ctx, squeezenet.build(224), max_batch=max_batch, precision="f32x3", x3_all=not hybrid)
 
 
 @pytest.mark.parametrize("hybrid", [True, False])
@@ -302,7 +300,7 @@ def test_x3_node_level_parity(gpu_ctx):
     mb = squeezenet.build(64)
     model = onnx_wire.decode_model(mb)
     inits = {t.name: t.to_numpy() for t in model.graph.initializer}
-    m = ore.Model(gpu_ctx, mb, max_batch=4, precision="f32x3")
+    m = ore.Model(gpu_ctx, mb, max_batch=4, precision="f32x3", x3_all=X3_ALL)
     m.set_fusion(ore.KEEP_VALUES)
     xt = _t(mini_inputs()[:2])
     _np(m.run(xt))

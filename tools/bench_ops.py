@@ -2,7 +2,8 @@
 """Kernel-level timing of single-node graphs (one Conv(+Relu) or MaxPool node) through the
 device walker, so weights are packed once and only the op's kernel is timed (HIP events on the
 context stream).  Shapes default to the SqueezeNet-1.0 layers at batch 256.
-usage: python tools/bench_ops.py [--batch 256] [--only conv|pool] [--reps 20]"""
+usage: python tools/bench_ops.py [--batch 256] [--only conv|pool] [--reps 20] [--tile T] [--pool-variant V]
+(--tile / --pool-variant: ore_ctx_set_conv_tile / ore_ctx_set_pool_variant)"""
 import argparse
 import os
 import sys
@@ -66,11 +67,15 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--only", default="")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--tile", type=int, default=-1)
+    ap.add_argument("--pool-variant", type=int, default=0)
     a = ap.parse_args()
     import torch
     import ore
     ctx = ore.Context(0)
-    tag = f"cfg={os.environ.get('ORE_CONV_CFG', 'auto')} pool={os.environ.get('ORE_POOL_VARIANT', '0')}"
+    ctx.set_conv_tile(a.tile)
+    ctx.set_pool_variant(a.pool_variant)
+    tag = f"tile={a.tile} pool={a.pool_variant}"
     B = a.batch
     if a.only in ("", "conv"):
         for name, cin, h, cout, k, s, p in CONVS:

@@ -20,7 +20,7 @@ if has smoke; then
   if [ $rc -ne 0 ]; then exit $rc; fi
 fi
 if has tests; then
-  timeout -k 10 900 python3 -m pytest tests -m gpu -q -p no:cacheprovider > "$OUT/pytest_gpu_$TAG.log" 2>&1
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -rf > "$OUT/pytest_gpu_$TAG.log" 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -15 "$OUT/pytest_gpu_$TAG.log"
   if fatal $rc || [ $rc -gt 1 ]; then exit $rc; fi
 fi

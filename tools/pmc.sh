@@ -6,6 +6,8 @@ ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
 TAG="${1:-pmc}"
 OUT="$ROOT/gpurun_out/pmc_$TAG"
 mkdir -p "$OUT"
+sha256sum "$ROOT/onnx-rusty-inference-engine_amd/lib/libore.so" | cut -d' ' -f1 > "$OUT/lib.sha256"
+echo "${PMC_COMMIT:-unknown}" > "$OUT/commit"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1
 echo "list rc=$?"

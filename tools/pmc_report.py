@@ -123,6 +123,9 @@ def main():
                "algorithmic_bytes_per_launch": (sum(st["bytes"] for st in steps if st["op"] == "Conv") / max(len(conv), 1)
                                                 if steps else None),
                "source": base, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, FETCH_SIZE x2 (gfx950)"}
+        for key, fn in (("lib_sha256", "lib.sha256"), ("commit", "commit")):  # the build the passes ran (tools/pmc.sh)
+            if os.path.exists(os.path.join(base, fn)):
+                out[key] = open(os.path.join(base, fn)).read().strip()
         with open(json_out, "w") as f:
             json.dump(out, f, indent=1)
         print(f"wrote {json_out}: {out['hbm_bytes_per_launch'] / 1e6:.1f} MB per conv launch")
