@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "ore_kernels.h"
@@ -436,11 +437,259 @@ __global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// LDS-staged Winograd kernel (tile 4, "wino lds").  The register-streaming kernels above move each
+// lane's own 4x4 window (four 4-B-aligned 16-B loads) and its 16 U values through the vector-memory
+// path every k-step: 8 KB per wave per 16 MFMAs, which kept the texture path ~80 % busy at ~41 % MFMA
+// (profiles/r02b_pmc_wino32_vs_gemm_f8e3.txt).  Here a workgroup of 4 waves owns 128 consecutive 2x2
+// output tiles (32 per wave, flattened over the batch) x 32 output channels, and both operands come
+// from LDS:
+//   * K is walked in chunks of WL_KC = 8 input channels, double-buffered.  Per chunk the input rows the
+//     128 tiles read (2 rows per tile row + 2, a zero row pair between images, one zero column each
+//     side) go global -> LDS by 4-B LDS-DMA (buffer_load ... lds): an offset outside the image (or a
+//     padding row / column) is given an out-of-range buffer offset and arrives as 0, so windows need
+//     no masks; U of the block's 32 channels goes global -> LDS by 16-B LDS-DMA.  The next chunk's
+//     DMAs are in flight during this chunk's MFMAs; one barrier per chunk.
+//   * per k-step (2 channels) a lane reads its window (8 ds_read_b64) and its 16 U values (4
+//     ds_read_b128) one step ahead, transforms the window (32 adds) and issues 16 v_mfma_f32_32x32x2_f32
+//     (1024 cycles per wave).  LDS traffic: 8 KB per wave per k-step (~32 B/clk per CU at full MFMA rate).
+// Same arithmetic as the other tiles: each position sums its c-ordered chain, the transforms a fixed
+// add order, so the result is bit-identical to tiles 0-3.
+constexpr int WL_KC = 8;       // input channels per K chunk
+constexpr int WL_TILES = 128;  // 2x2 tiles per workgroup (32 per wave)
+
+__device__ __forceinline__ void wl_dma4(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, int voffset, int soffset) {
+  int m0save;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dword %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(m0save)
+      : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voffset), "s"(rsrc), "s"(soffset)
+      : "memory");
+}
+
+__device__ __forceinline__ void wl_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, int voffset, int soffset) {
+  int m0save;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(m0save)
+      : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voffset), "s"(rsrc), "s"(soffset)
+      : "memory");
+}
+
+// geometry of the LDS kernel (host-computed)
+struct WlGeom {
+  int TW, TPI, HP;  // tiles per row / per image, staged row slots per image (2 * tiles per column + 2)
+  int RS;           // LDS row stride (floats, even: 8-B window reads)
+  int NG;           // 64-float DMA groups per staged channel
+  int CS;           // LDS channel stride (floats)
+  int ntg;          // tile groups of WL_TILES
+};
+
+template <int NGW>  // DMA groups per wave per channel (ceil(NG / 4))
+__global__ __launch_bounds__(256, 1) void conv_winol_kernel(ConvParams p, WlGeom g) {
+  extern __shared__ __attribute__((aligned(16))) float wl_lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // block -> (tile group, 32-channel block), the m blocks of one tile group consecutive (one XCD: they
+  // share the staged input rows in L2)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
+  const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
+  const int mt = wgid % p.mtiles, tgi = wgid / p.mtiles;
+  const int m0 = mt * 32;
+  const int T = p.N * g.TPI;
+  const int t0 = tgi * WL_TILES;
+  const int gs0 = (t0 / g.TPI) * g.HP + 2 * ((t0 % g.TPI) / g.TW);  // first staged slot (global)
+
+  float* const ibuf = wl_lds;                        // [2][WL_KC][CS] input rows
+  float* const ubuf = wl_lds + 2 * WL_KC * g.CS;     // [2][WL_KC][4 quads][32 m][4] U
+  const unsigned ibuf_a = (unsigned)(size_t)(__attribute__((address_space(3))) float*)ibuf;
+  const unsigned ubuf_a = (unsigned)(size_t)(__attribute__((address_space(3))) float*)ubuf;
+
+  // ---- DMA sources: this lane's input elements (groups j = wave + 4 u of a staged channel) and U
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0, p.C * p.Mp * 16 * 4, 0x00020000);
+  int voff[NGW];
+#pragma unroll
+  for (int u = 0; u < NGW; ++u) {
+    const int e = 64 * (wave + 4 * u) + lane;
+    const int slot = e / g.RS, col = e - slot * g.RS;
+    const int gsl = gs0 + slot, img = gsl / g.HP, r = gsl - img * g.HP - 1;
+    const bool ok = img < p.N && (unsigned)r < (unsigned)p.H && col >= 1 && col <= p.W;
+    voff[u] = ok ? (int)((img * p.x_nstride + (long long)r * p.W + (col - 1)) * 4) : WG_OOB;
+  }
+  // U: DMA d = wave + 4 v (v < 4) of a chunk: channel d / 2, quads 2 (d & 1) + (lane >> 5), m0 + (lane & 31)
+  int uoff[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int d = wave + 4 * v, cc = d >> 1, q = 2 * (d & 1) + (lane >> 5);
+    uoff[v] = ((cc * 4 + q) * p.Mp + m0 + (lane & 31)) * 16;
+  }
+  const int nchunks = p.C / WL_KC;
+  auto stage = [&](int kc, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int cc = 0; cc < WL_KC; ++cc) {
+      const int so = (kc * WL_KC + cc) * p.x_ps * 4;
+#pragma unroll
+      for (int u = 0; u < NGW; ++u)
+        if (wave + 4 * u < g.NG)
+          wl_dma4(xr, ibuf_a + ((buf * WL_KC + cc) * g.CS + 64 * (wave + 4 * u)) * 4, voff[u], so);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int d = wave + 4 * v;
+      wl_dma16(ur, ubuf_a + ((buf * WL_KC + (d >> 1)) * 512 + 256 * (d & 1)) * 4, uoff[v], kc * WL_KC * 4 * p.Mp * 16);
+    }
+  };
+
+  // ---- this lane's tile and its window in a staged channel
+  const int lr = lane >> 5, lc = lane & 31;
+  int t = t0 + wave * 32 + lc;
+  WgTile w;
+  w.tok = t < T;
+  if (!w.tok) t = T - 1;
+  const int img = t / g.TPI, rem = t - img * g.TPI, ty = rem / g.TW, tx = rem - ty * g.TW;
+  const int wslot = img * g.HP + 2 * ty - gs0;
+  const int wbase = lr * g.CS + wslot * g.RS + 2 * tx;  // channel c0 + lr of a chunk k-step
+  w.ybase = img * (int)p.y_nstride + (2 * ty) * p.W + 2 * tx;
+  w.c1ok = 2 * tx + 1 < p.W;
+  w.r1ok = 2 * ty + 1 < p.H;
+  const int ubase = lr * 512 + lc * 4;  // U[c = lr][quad][m = lc][4] of a k-step's channel pair
+
+  floatx16_t acc[16];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[xi][e] = 0.0f;
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const int buf = kc & 1;
+    if (kc + 1 < nchunks) stage(kc + 1, buf ^ 1);
+    const float* ib = ibuf + buf * WL_KC * g.CS + wbase;
+    const float* ub = ubuf + buf * WL_KC * 512 + ubase;
+    wg_floatx4 ua[2][4];
+    wg_f2 dw[2][8];
+    auto ld = [&](int s, int slot) __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ua[slot][q] = *reinterpret_cast<const wg_floatx4*>(ub + (2 * s) * 512 + q * 128);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dw[slot][2 * r] = *reinterpret_cast<const wg_f2*>(ib + (2 * s) * g.CS + r * g.RS);
+        dw[slot][2 * r + 1] = *reinterpret_cast<const wg_f2*>(ib + (2 * s) * g.CS + r * g.RS + 2);
+      }
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int s = 0; s < WL_KC / 2; ++s) {
+      const int cur = s & 1;
+      if (s + 1 < WL_KC / 2) ld(s + 1, cur ^ 1);
+      __builtin_amdgcn_sched_barrier(0);  // the next step's LDS reads stay ahead of this step's MFMAs
+      float d[4][4], v[16];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        d[r][0] = dw[cur][2 * r][0]; d[r][1] = dw[cur][2 * r][1];
+        d[r][2] = dw[cur][2 * r + 1][0]; d[r][3] = dw[cur][2 * r + 1][1];
+      }
+      wg_input_transform(d, v);
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi)
+        acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[cur][xi >> 2][xi & 3], v[xi], acc[xi], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk kc + 1 have landed
+    __syncthreads();  // ... every wave's, and every wave is done reading buffer kc & 1
+  }
+  // accumulator element e of a lane is row (e & 3) + 8 (e >> 2) + 4 lr (channel), column lc (tile)
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int r = (e & 3) + 8 * (e >> 2);
+    const int m = m0 + r + 4 * lr;
+    if (m >= p.M) continue;
+    float mx[16];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) mx[xi] = acc[xi][e];
+    wg_store(p, w, m, p.bias ? p.bias[m] : 0.0f, mx);
+  }
+}
+
+// the LDS kernel's geometry; false when the layer does not fit it
+static bool wl_geom(const ConvParams& p, WlGeom* g, size_t* lds) {
+  if (p.C % WL_KC != 0 || p.C <= 0 || p.W + 2 > 512) return false;
+  g->TW = (p.W + 1) / 2;
+  const int TH = (p.H + 1) / 2;
+  g->TPI = g->TW * TH;
+  g->HP = 2 * TH + 2;
+  g->RS = (p.W + 2 + 1) & ~1;
+  const long long T = (long long)p.N * g->TPI;
+  g->ntg = (int)((T + WL_TILES - 1) / WL_TILES);
+  // staged slots of the widest tile group (rows of the tile rows it spans + the image breaks)
+  int nslot = 0;
+  for (long long t0 = 0; t0 < T; t0 += WL_TILES) {
+    const long long t1 = std::min(T, t0 + WL_TILES) - 1;
+    const long long s0 = (t0 / g->TPI) * g->HP + 2 * ((t0 % g->TPI) / g->TW);
+    const long long s1 = (t1 / g->TPI) * g->HP + 2 * ((t1 % g->TPI) / g->TW) + 3;
+    nslot = std::max(nslot, (int)(s1 - s0 + 1));
+    if (t0 >= (long long)WL_TILES * g->TPI) break;  // group starts repeat mod TPI: every case seen
+  }
+  g->NG = (nslot * g->RS + 63) / 64;
+  g->CS = g->NG * 64 + 32;  // +32: the two lane halves' channels on opposite halves of the banks
+  *lds = ((size_t)2 * WL_KC * g->CS + (size_t)2 * WL_KC * 512) * 4;
+  return g->NG <= 32 && *lds <= 160 * 1024;
+}
+
+template <int NGW>
+static void launch_wl(const ConvParams& p0, const WlGeom& g, size_t lds, hipStream_t s) {
+  ConvParams p = p0;
+  p.mtiles = (p.M + 31) / 32;
+  if (lds > 64 * 1024) {  // above the default dynamic-LDS limit: raise it once per device
+    static std::atomic<unsigned long long> raised{0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (!(raised.load(std::memory_order_acquire) & bit)) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_winol_kernel<NGW>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      raised.fetch_or(bit, std::memory_order_acq_rel);
+    }
+  }
+  hipLaunchKernelGGL((conv_winol_kernel<NGW>), dim3((unsigned)(g.ntg * p.mtiles)), dim3(256), lds, s, p, g);
+}
+
+static void launch_winol(const ConvParams& p, hipStream_t s) {
+  WlGeom g;
+  size_t lds = 0;
+  if (!wl_geom(p, &g, &lds)) return;  // the caller checked conv_wino_eligible
+  switch ((g.NG + 3) / 4) {
+    case 1: launch_wl<1>(p, g, lds, s); break;
+    case 2: launch_wl<2>(p, g, lds, s); break;
+    case 3: launch_wl<3>(p, g, lds, s); break;
+    case 4: launch_wl<4>(p, g, lds, s); break;
+    case 5: launch_wl<5>(p, g, lds, s); break;
+    case 6: launch_wl<6>(p, g, lds, s); break;
+    case 7: launch_wl<7>(p, g, lds, s); break;
+    default: launch_wl<8>(p, g, lds, s); break;
+  }
+}
+
+
 // Winograd tiles (ConvPlan cfg = WINO_TILE_BASE + t): shape (32: 32x32x2, 16: 16x16x4), channels and
 // 2x2 tiles per wave, A / B ring depths of the unrolled K loop
 struct WinoTile { int shape, ch, tiles, da, db; };
 static const WinoTile WINO_TILES[WINO_TILES_N] = {{32, 32, 32, 2, 8}, {32, 32, 32, 2, 4}, {16, 32, 16, 2, 8},
-                                                  {16, 16, 32, 2, 4}};
+                                                  {16, 16, 32, 2, 4}, {0, 32, WL_TILES, 0, 0}};  // 4: conv_winol_kernel
 
 bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo) {
   return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && Ho == H && Wo == W && C % 16 == 0 && C > 0;
@@ -448,6 +697,15 @@ bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, i
 
 bool conv_wino_eligible(const ConvParams& p, int tile) {
   if (tile < 0 || tile >= WINO_TILES_N) return false;
+  if (tile == 4) {
+    WlGeom g;
+    size_t lds;
+    return conv_wino_geometry(p.C, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.H, p.W, p.Ho, p.Wo) && wl_geom(p, &g, &lds) &&
+           p.x_bytes > 0 && p.x_bytes < (1LL << 31) - (1LL << 21) && (reinterpret_cast<uintptr_t>(p.x) & 3) == 0 &&
+           p.Mp % 64 == 0 && (long long)p.C * p.Mp * 64 < (1LL << 31) &&
+           (long long)p.N * ((p.H + 1) / 2) * ((p.W + 1) / 2) < (1LL << 30) &&
+           (long long)p.N * p.y_nstride < (1LL << 31);
+  }
   const WinoTile& wt = WINO_TILES[tile];
   const int nks = p.C / (wt.shape == 32 ? 2 : 4);
   return conv_wino_geometry(p.C, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.H, p.W, p.Ho, p.Wo) && nks % 2 == 0 &&
@@ -465,6 +723,10 @@ static void wg_grid(ConvParams& p, int ch, int tiles, dim3* grid) {
 }
 
 void launch_conv_wino(const ConvParams& p0, int tile, hipStream_t s) {
+  if (tile == 4) {
+    launch_winol(p0, s);
+    return;
+  }
   ConvParams p = p0;
   const WinoTile& wt = WINO_TILES[tile < 0 || tile >= WINO_TILES_N ? 0 : tile];
   dim3 grid;

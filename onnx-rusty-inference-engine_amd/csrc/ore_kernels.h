@@ -309,11 +309,11 @@ void launch_pack_x3w(const float* w, int M, int C, int kh, int kw, int Mp, int G
 void launch_conv_x3(const ConvParams& p, int tile, hipStream_t s);
 // 3x3 / stride-1 / pad-1 f32 conv by Winograd F(2x2, 3x3) on the f32 MFMA (ore_conv_wino.hip).  Tiles
 // WINO_TILE_BASE + 0..3 = 32 ch x 32 tiles (32x32x2 MFMA, ring 4 / 2), 32 x 16, 16 x 32 (16x16x4);
+// 4 = the LDS-staged kernel (128 tiles x 32 channels per 4-wave block, windows and U from LDS; C % 8 == 0);
 // results do not depend on the tile (not bit-identical to the direct kernels).  Weights packed by
 // launch_pack_wino: U = G g G^T as [C][4][Mp][4] f32 (channel, position quad, m, position) (Mp = wino_packed_mp(M)).
-// (id WINO_TILE_BASE + 4, the LDS-staged variant, is retired: slower on every expand3x3.)
 constexpr int WINO_TILE_BASE = X3_TILE_BASE + X3_TILES;
-constexpr int WINO_TILES_N = 4;
+constexpr int WINO_TILES_N = 5;
 // fused-kernel ids after the Winograd tiles (ore.Model.TILE_NAMES): 41 is retired (the Winograd fire module)
 constexpr int FIRE_F16_TILE = 42, C1_POOL_F16_TILE = 43;
 bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo);

@@ -325,7 +325,7 @@ class Model:
                   "x3 128x128", "x3 64x256", "x3 96x128", "x3 64x128",
                   "x3w 128x128", "x3w 64x128", "x3w 128x64", "x3w 64x64",
                   "wino 32x32 d4", "wino 32x32 d2", "wino16 32x16", "wino16 16x32",
-                  None, None,  # 40: the LDS-staged Winograd, 41: the Winograd fire module
+                  "wino lds", None,  # 41: the Winograd fire module (retired)
                   "fire f16", "first conv pool f16", "epool window f32", "fire pool f32"]
 
     def tiles(self):

@@ -108,10 +108,10 @@ def test_wino_exact_on_small_integers(gpu_ctx):
     np.testing.assert_array_equal(y, ref.astype(np.float32))
 
 
-@pytest.mark.parametrize("ci", [0, 3, 4, 5, 9])
+@pytest.mark.parametrize("ci", list(range(10)))
 def test_wino_tiles_bit_identical(gpu_ctx, ci):
-    """Every Winograd tile (ore_ctx_set_conv_tile, "wino 32x32 d4" .. "wino16 16x32") computes each
-    output the same way: identical bits; the model reports the tile it ran."""
+    """Every Winograd tile (ore_ctx_set_conv_tile, "wino 32x32 d4" .. "wino16 16x32", "wino lds")
+    computes each output the same way: identical bits; the model reports the tile it ran."""
     import ore
     N, C, H, W, M = CASES[ci]
     rng = np.random.default_rng(3)
@@ -121,7 +121,7 @@ def test_wino_tiles_bit_identical(gpu_ctx, ci):
     mb = _conv_model((1, C, H, W), w, b, [1] * 4, [1, 1])
     base = ore.Model.TILE_NAMES.index("wino 32x32 d4")
     outs = []
-    for t in range(4):
+    for t in range(5):  # 4: the LDS-staged kernel
         with conv_tile(gpu_ctx, base + t):
             m = ore.Model(gpu_ctx, mb, max_batch=N)
         outs.append(_np(m.run(_t(x))))
