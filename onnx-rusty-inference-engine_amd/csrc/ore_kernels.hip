@@ -409,9 +409,10 @@ void launch_add_bcast(const AddParams& p, hipStream_t s) {
 //    l % 8 over them in ascending chunk order, fetching chunk 8k + g's element from lane
 //    8 g + l % 8 by a cross-lane shuffle (ds_bpermute).  Every lane of a partial runs the same
 //    chain, so p_j is the reference's sequential fold, bit for bit given the same exponentials.
-//  * y = e / sum (a division, as `exp_x / &sum_exp_x`); e is kept in y between the passes, re-read
-//    only by the lane that wrote it.
+//  * y = e / sum (a division, as `exp_x / &sum_exp_x`).  Rows up to 1024 keep x and e in registers
+//    (one read of x, one write of y); longer rows stage e in y, re-read only by the lane that wrote it.
 // ------------------------------------------------------------------------------------------
+template <int NE>  // elements per lane held in registers: D <= 64 NE
 __global__ __launch_bounds__(256) void softmax_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                       long long rows, int D) {
   const int lane = threadIdx.x & 63;
@@ -419,27 +420,78 @@ __global__ __launch_bounds__(256) void softmax_kernel(const float* __restrict__ 
   if (row >= rows) return;  // wave-uniform; no barrier in this kernel
   const float* xr = x + row * D;
   float* yr = y + row * D;
-
+  float e[NE];
+#pragma unroll
+  for (int k = 0; k < NE; ++k) e[k] = 64 * k + lane < D ? xr[64 * k + lane] : -INFINITY;  // all loads in flight
   float m = -INFINITY;
-  for (int i = lane; i < D; i += 64) m = fmaxf(xr[i], m);
+#pragma unroll
+  for (int k = 0; k < NE; ++k) m = fmaxf(e[k], m);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
 
   const int nfull8 = D / 8 * 8;  // elements inside the 8-wide chunks
   const int j = lane & 7;
   float s = 0.0f;
-  for (int i0 = 0; i0 < nfull8; i0 += 64) {  // wave-uniform trip count
+#pragma unroll
+  for (int k = 0; k < NE; ++k) {
+    const int i = 64 * k + lane;
+    e[k] = i < D ? expf(e[k] - m) : 0.0f;
+    const float ec = i < nfull8 ? e[k] : 0.0f;  // s + 0 == s: elements past the chunks add nothing
+    if (64 * k < nfull8) {  // wave-uniform
+      float sh[8];
+#pragma unroll
+      for (int g = 0; g < 8; ++g) sh[g] = __shfl(ec, 8 * g + j);  // chunks 8k .. 8k+7 of partial j
+#pragma unroll
+      for (int g = 0; g < 8; ++g) s = s + sh[g];
+    }
+  }
+  const float p0 = __shfl(s, 0), p1 = __shfl(s, 1), p2 = __shfl(s, 2), p3 = __shfl(s, 3);
+  const float p4 = __shfl(s, 4), p5 = __shfl(s, 5), p6 = __shfl(s, 6), p7 = __shfl(s, 7);
+  float sum = 0.0f;
+  sum = sum + (p0 + p4);
+  sum = sum + (p1 + p5);
+  sum = sum + (p2 + p6);
+  sum = sum + (p3 + p7);
+  // the < 8 tail elements share one register slot (nfull8 is a multiple of 8); select it without
+  // dynamic register indexing, then fold the tail in order
+  const int kt = nfull8 / 64;
+  float et = 0.0f;
+#pragma unroll
+  for (int k = 0; k < NE; ++k) et = k == kt ? e[k] : et;
+  for (int i = nfull8; i < D; ++i) sum = sum + __shfl(et, i % 64);
+#pragma unroll
+  for (int k = 0; k < NE; ++k)
+    if (64 * k + lane < D) yr[64 * k + lane] = e[k] / sum;
+}
+
+// rows longer than 1024: the same order, e staged in y (re-read only by the lane that wrote it)
+__global__ __launch_bounds__(256) void softmax_long_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                           long long rows, int D) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + row * D;
+  float* yr = y + row * D;
+  float m = -INFINITY;
+  for (int i = lane; i < D; i += 64) m = fmaxf(xr[i], m);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  const int nfull8 = D / 8 * 8;
+  const int j = lane & 7;
+  float s = 0.0f;
+  for (int i0 = 0; i0 < D; i0 += 64) {  // wave-uniform trip count
     const int i = i0 + lane;
     float e = 0.0f;
     if (i < D) {
       e = expf(xr[i] - m);
       yr[i] = e;
     }
-    const float ec = i < nfull8 ? e : 0.0f;  // s + 0 == s: lanes past the chunks add nothing
+    const float ec = i < nfull8 ? e : 0.0f;
+    if (i0 < nfull8) {
 #pragma unroll
-    for (int g = 0; g < 8; ++g) s = s + __shfl(ec, 8 * g + j);
+      for (int g = 0; g < 8; ++g) s = s + __shfl(ec, 8 * g + j);
+    }
   }
-  for (int i = (nfull8 + 63) / 64 * 64 + lane; i < D; i += 64) yr[i] = expf(xr[i] - m);  // not yet written
   const float p0 = __shfl(s, 0), p1 = __shfl(s, 1), p2 = __shfl(s, 2), p3 = __shfl(s, 3);
   const float p4 = __shfl(s, 4), p5 = __shfl(s, 5), p6 = __shfl(s, 6), p7 = __shfl(s, 7);
   float sum = 0.0f;
@@ -453,7 +505,13 @@ __global__ __launch_bounds__(256) void softmax_kernel(const float* __restrict__ 
 
 void launch_softmax(const float* x, float* y, long long rows, int D, hipStream_t s) {
   if (rows <= 0) return;
-  hipLaunchKernelGGL(softmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, y, rows, D);
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  if (D <= 256)
+    hipLaunchKernelGGL(softmax_kernel<4>, grid, dim3(256), 0, s, x, y, rows, D);
+  else if (D <= 1024)
+    hipLaunchKernelGGL(softmax_kernel<16>, grid, dim3(256), 0, s, x, y, rows, D);
+  else
+    hipLaunchKernelGGL(softmax_long_kernel, grid, dim3(256), 0, s, x, y, rows, D);
 }
 
 // ------------------------------------------------------------------------------------------

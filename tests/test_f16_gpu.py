@@ -124,8 +124,7 @@ def test_f16_pool_relu_gap_exact(gpu_ctx):
         r0 = oracle.relu(oracle.conv2d(x, w1, b1, pads=[1] * 4, strides=(1, 1)))
         p0 = oracle.maxpool2d(r0, (3, 3), (2, 2), auto_pad="NOTSET", pads=[0, 0, 1, 1])
         c1 = oracle.conv2d(p0, w2, None, pads=[0] * 4, strides=(1, 1))
-        if not fusion & ore.FUSE_POOL_CONV:  # fused: the pooled tensor is never materialised
-            np.testing.assert_array_equal(m.read_value("p0"), p0)
+        np.testing.assert_array_equal(m.read_value("p0"), p0)
         np.testing.assert_array_equal(m.read_value("c1"), c1)
         np.testing.assert_array_equal(y.reshape(2, 8), oracle.gap(c1).reshape(2, 8))  # exact: f32 sums of ints
         m.close()

@@ -31,12 +31,12 @@ def _np(t):
     return t.cpu().numpy()
 
 
-def _model(ctx, mb, **kw):
+def _model(ctx, mb, *args, **kw):
     """These tests pin the direct kernels and their fusions (bit-identical to the unfused graph): every
     model loads with ORE_LOAD_NO_WINOGRAD.  The Winograd 3x3 path, on by default for f32 models, has
     its own parity tests (tests/test_wino_gpu.py)."""
     import ore
-    return ore.Model(ctx, mb, winograd=False, **kw)
+    return ore.Model(ctx, mb, *args, winograd=False, **kw)
 
 
 def _mnist_bytes():

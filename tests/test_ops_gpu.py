@@ -289,7 +289,8 @@ def test_softmax_reference_kat(gpu_ctx):
     np.testing.assert_allclose(got, ref, atol=2e-7, rtol=0)
 
 
-@pytest.mark.parametrize("rows,d", [(1, 1000), (256, 1000), (3, 7), (5, 8), (2, 17), (4, 5000), (2, 20000)])
+@pytest.mark.parametrize("rows,d", [(1, 1000), (256, 1000), (3, 7), (5, 8), (2, 17), (3, 64), (3, 255), (3, 256), (3, 257),
+                                    (5, 1020), (5, 1024), (5, 1025), (4, 5000), (2, 20000)])
 def test_softmax(gpu_ctx, rows, d):
     import ore
     x = (np.random.default_rng(d).standard_normal((rows, d, 1, 1)) * 5).astype(np.float32)
