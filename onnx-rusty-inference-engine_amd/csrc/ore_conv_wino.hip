@@ -439,39 +439,31 @@ __global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
 
 // ---------------------------------------------------------------------------------------------------
 // LDS-staged Winograd kernel (tile 4, "wino lds").  The register-streaming kernels above move each
-// lane's own 4x4 window (four 4-B-aligned 16-B loads) and its 16 U values through the vector-memory
-// path every k-step: 8 KB per wave per 16 MFMAs, which kept the texture path ~80 % busy at ~41 % MFMA
-// (profiles/r02b_pmc_wino32_vs_gemm_f8e3.txt).  Here a workgroup of 4 waves owns 128 consecutive 2x2
-// output tiles (32 per wave, flattened over the batch) x 32 output channels, and both operands come
-// from LDS:
-//   * K is walked in chunks of WL_KC = 8 input channels, double-buffered.  Per chunk the input rows the
-//     128 tiles read (2 rows per tile row + 2, a zero row pair between images, one zero column each
-//     side) go global -> LDS by 4-B LDS-DMA (buffer_load ... lds): an offset outside the image (or a
-//     padding row / column) is given an out-of-range buffer offset and arrives as 0, so windows need
-//     no masks; U of the block's 32 channels goes global -> LDS by 16-B LDS-DMA.  The next chunk's
-//     DMAs are in flight during this chunk's MFMAs; one barrier per chunk.
-//   * per k-step (2 channels) a lane reads its window (8 ds_read_b64) and its 16 U values (4
-//     ds_read_b128) one step ahead, transforms the window (32 adds) and issues 16 v_mfma_f32_32x32x2_f32
-//     (1024 cycles per wave).  LDS traffic: 8 KB per wave per k-step (~32 B/clk per CU at full MFMA rate).
-// Same arithmetic as the other tiles: each position sums its c-ordered chain, the transforms a fixed
-// add order, so the result is bit-identical to tiles 0-3.
-constexpr int WL_KC = 8;       // input channels per K chunk
-constexpr int WL_TILES = 128;  // 2x2 tiles per workgroup (32 per wave)
+// lane's own window and U values through the vector-memory path every k-step (the texture path ran
+// ~80 % busy at ~41-45 % MFMA, profiles/r02b_pmc_wino32_vs_gemm_f8e3.txt, profiles/r03_pmc_wino_tiles.txt);
+// a first LDS kernel with 32x32x2 tiles (512 registers, one wave per SIMD) lost to them: its
+// per-workgroup prologue and epilogue were never overlapped (profiles/r03_wino_lds_ablation.txt).
+// This one runs two waves per SIMD (<= 256 registers) and two workgroups per CU:
+//   * a workgroup of 4 waves owns 64 consecutive 2x2 tiles (16 per wave, flattened over the batch) x 32
+//     output channels; lane (lk, lj) of the 16x16x4 MFMAs supplies channel k = lk and tile / output row
+//     lj, the wave's two 16-channel fragments are channels m0 + lj and m0 + 16 + lj;
+//   * K in chunks of WM_KC = 8 input channels, double-buffered in LDS.  Per chunk and channel the input
+//     rows the 64 tiles read are copied as contiguous runs (one per image the group touches, rows clamped
+//     to the image) global -> LDS by 16-B LDS-DMA; U of the 32 channels likewise.  The next chunk's DMAs
+//     are in flight during this chunk's MFMAs; one barrier per chunk.  Window rows outside the image
+//     read a zero block at the start of the channel's area; window columns outside the image are
+//     zeroed by per-lane selects (exact zeros: the other tiles' zero padding);
+//   * per k-step (4 channels) a lane reads its 4x4 window (ds_read2_b32) and 8 U quads (ds_read_b128),
+//     transforms the window (32 adds) and issues 32 v_mfma_f32_16x16x4_f32 (1024 cycles per wave); the
+//     next k-step's U quads are read as the MFMAs that used the current ones issue.
+// Each position is the same c-ordered fma chain and the transforms the same add order as tiles 0-3:
+// bit-identical to them.
+constexpr int WM_KC = 8;      // input channels per K chunk (2 k-steps of 4)
+constexpr int WM_TILES = 64;  // 2x2 tiles per workgroup (16 per wave)
+constexpr int WM_CH = 32;     // output channels per workgroup
+constexpr int WM_ZL = 4;      // zero floats at the start of a staged channel (rows outside the image)
 
-__device__ __forceinline__ void wl_dma4(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, int voffset, int soffset) {
-  int m0save;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dword %2, %3, %4 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(m0save)
-      : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voffset), "s"(rsrc), "s"(soffset)
-      : "memory");
-}
-
-__device__ __forceinline__ void wl_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, int voffset, int soffset) {
+__device__ __forceinline__ void wm_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, int voffset, int soffset) {
   int m0save;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
@@ -480,216 +472,278 @@ __device__ __forceinline__ void wl_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned l
       "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(m0save)
-      : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voffset), "s"(rsrc), "s"(soffset)
+      : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voffset), "s"(rsrc),
+        "s"(__builtin_amdgcn_readfirstlane(soffset))
       : "memory");
 }
 
 // geometry of the LDS kernel (host-computed)
-struct WlGeom {
-  int TW, TPI, HP;  // tiles per row / per image, staged row slots per image (2 * tiles per column + 2)
-  int RS;           // LDS row stride (floats, even: 8-B window reads)
-  int NG;           // 64-float DMA groups per staged channel
-  int CS;           // LDS channel stride (floats)
-  int ntg;          // tile groups of WL_TILES
+struct WmGeom {
+  int TW, TPI;  // tiles per row / per image
+  int CS;       // LDS floats per staged channel: zero block + the longest run set + slack (= 32 mod 64)
+  int ntg;      // tile groups of WM_TILES
 };
 
-template <int NGW>  // DMA groups per wave per channel (ceil(NG / 4))
-__global__ __launch_bounds__(256, 1) void conv_winol_kernel(ConvParams p, WlGeom g) {
-  extern __shared__ __attribute__((aligned(16))) float wl_lds[];
+// rows of image `img` staged for the tile group [t0, t1]: [rs, re], clamped to the image
+__host__ __device__ __forceinline__ void wm_rows(int img, int img0, int ty0, int img1, int ty1, int H, int* rs, int* re) {
+  *rs = img == img0 ? max(0, 2 * ty0 - 1) : 0;
+  *re = img == img1 ? min(H - 1, 2 * ty1 + 2) : H - 1;
+}
+
+// floats staged per channel for the tile group starting at t0 (each image's run rounded up to 4)
+static int wm_group_floats(long long t0, long long T, int TPI, int TW, int H, int W) {
+  const long long t1 = std::min(T, t0 + WM_TILES) - 1;
+  const int img0 = (int)(t0 / TPI), ty0 = (int)(t0 % TPI) / TW;
+  const int img1 = (int)(t1 / TPI), ty1 = (int)(t1 % TPI) / TW;
+  int total = 0;
+  for (int i = img0; i <= img1; ++i) {
+    int rs, re;
+    wm_rows(i, img0, ty0, img1, ty1, H, &rs, &re);
+    total += ((re - rs + 1) * W + 3) & ~3;
+  }
+  return total;
+}
+
+template <int NDMA>  // 256-float DMA pieces per staged channel (ceil(longest run set / 256))
+__global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom g) {
+  extern __shared__ __attribute__((aligned(16))) float wm_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // block -> (tile group, 32-channel block), the m blocks of one tile group consecutive (one XCD: they
-  // share the staged input rows in L2)
+  // block -> (tile group, 32-channel block), the channel blocks of a tile group consecutive (one XCD:
+  // they share the staged rows in L2)
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
   const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
   const int mt = wgid % p.mtiles, tgi = wgid / p.mtiles;
-  const int m0 = mt * 32;
+  const int m0 = mt * WM_CH;
   const int T = p.N * g.TPI;
-  const int t0 = tgi * WL_TILES;
-  const int gs0 = (t0 / g.TPI) * g.HP + 2 * ((t0 % g.TPI) / g.TW);  // first staged slot (global)
+  const int t0 = tgi * WM_TILES, t1 = min(T, t0 + WM_TILES) - 1;
+  const int img0 = t0 / g.TPI, ty0 = (t0 - img0 * g.TPI) / g.TW;
+  const int img1 = t1 / g.TPI, ty1 = (t1 - img1 * g.TPI) / g.TW;
+  const int SS = WM_KC * (g.CS + 512);  // floats per stage: [channel][CS] windows, then [channel][4 quads][32 m][4] U
 
-  float* const ibuf = wl_lds;                        // [2][WL_KC][CS] input rows
-  float* const ubuf = wl_lds + 2 * WL_KC * g.CS;     // [2][WL_KC][4 quads][32 m][4] U
-  const unsigned ibuf_a = (unsigned)(size_t)(__attribute__((address_space(3))) float*)ibuf;
-  const unsigned ubuf_a = (unsigned)(size_t)(__attribute__((address_space(3))) float*)ubuf;
+  // the zero blocks (never written by the DMAs)
+  if (threadIdx.x < 2 * WM_KC * WM_ZL)
+    wm_lds[(threadIdx.x >> 5) * SS + ((threadIdx.x >> 2) & 7) * g.CS + (threadIdx.x & 3)] = 0.0f;
 
-  // ---- DMA sources: this lane's input elements (groups j = wave + 4 u of a staged channel) and U
-  const __amdgpu_buffer_rsrc_t xr =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t ur =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0, p.C * p.Mp * 16 * 4, 0x00020000);
-  int voff[NGW];
-#pragma unroll
-  for (int u = 0; u < NGW; ++u) {
-    const int e = 64 * (wave + 4 * u) + lane;
-    const int slot = e / g.RS, col = e - slot * g.RS;
-    const int gsl = gs0 + slot, img = gsl / g.HP, r = gsl - img * g.HP - 1;
-    const bool ok = img < p.N && (unsigned)r < (unsigned)p.H && col >= 1 && col <= p.W;
-    voff[u] = ok ? (int)((img * p.x_nstride + (long long)r * p.W + (col - 1)) * 4) : WG_OOB;
-  }
-  // U: DMA d = wave + 4 v (v < 4) of a chunk: channel d / 2, quads 2 (d & 1) + (lane >> 5), m0 + (lane & 31)
-  int uoff[4];
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    const int d = wave + 4 * v, cc = d >> 1, q = 2 * (d & 1) + (lane >> 5);
-    uoff[v] = ((cc * 4 + q) * p.Mp + m0 + (lane & 31)) * 16;
-  }
-  const int nchunks = p.C / WL_KC;
-  auto stage = [&](int kc, int buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int cc = 0; cc < WL_KC; ++cc) {
-      const int so = (kc * WL_KC + cc) * p.x_ps * 4;
-#pragma unroll
-      for (int u = 0; u < NGW; ++u)
-        if (wave + 4 * u < g.NG)
-          wl_dma4(xr, ibuf_a + ((buf * WL_KC + cc) * g.CS + 64 * (wave + 4 * u)) * 4, voff[u], so);
-    }
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int d = wave + 4 * v;
-      wl_dma16(ur, ubuf_a + ((buf * WL_KC + (d >> 1)) * 512 + 256 * (d & 1)) * 4, uoff[v], kc * WL_KC * 4 * p.Mp * 16);
-    }
-  };
-
-  // ---- this lane's tile and its window in a staged channel
-  const int lr = lane >> 5, lc = lane & 31;
-  int t = t0 + wave * 32 + lc;
+  // ---- this lane's tile (lj of the wave's 16) and the run layout of the group
+  const int lk = lane >> 4, lj = lane & 15;
+  int t = t0 + 16 * wave + lj;
   WgTile w;
   w.tok = t < T;
   if (!w.tok) t = T - 1;
   const int img = t / g.TPI, rem = t - img * g.TPI, ty = rem / g.TW, tx = rem - ty * g.TW;
-  const int wslot = img * g.HP + 2 * ty - gs0;
-  const int wbase = lr * g.CS + wslot * g.RS + 2 * tx;  // channel c0 + lr of a chunk k-step
+  // DMA piece gi of a channel: floats [4 (64 gi + lane), +4) of the run set
+  int voff[NDMA];
+#pragma unroll
+  for (int gi = 0; gi < NDMA; ++gi) voff[gi] = -1;
+  int my_lb = 0, my_rs = 0;
+  int lb = 0;
+  for (int i = img0; i <= img1; ++i) {
+    int rs, re;
+    wm_rows(i, img0, ty0, img1, ty1, p.H, &rs, &re);
+    const int len = (re - rs + 1) * p.W;
+#pragma unroll
+    for (int gi = 0; gi < NDMA; ++gi) {
+      const int k4 = 4 * (64 * gi + lane);
+      if (k4 >= lb && k4 < lb + len) voff[gi] = (int)((i * p.x_nstride + (long long)rs * p.W + (k4 - lb)) * 4);
+    }
+    if (i == img) {
+      my_lb = lb;
+      my_rs = rs;
+    }
+    lb += (len + 3) & ~3;
+  }
+  // window rows (floats from the channel's area; rows outside the image -> the zero block)
+  int aw[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int gr = 2 * ty - 1 + r;
+    const int rel = (unsigned)gr < (unsigned)p.H ? WM_ZL + my_lb + (gr - my_rs) * p.W + 2 * tx - 1 : 0;
+    aw[r] = (lk * g.CS + rel) * 4;  // bytes, channel lk of a k-step
+  }
+  const bool c0ok = tx > 0, c2ok = 2 * tx + 1 < p.W, c3ok = 2 * tx + 2 < p.W;
   w.ybase = img * (int)p.y_nstride + (2 * ty) * p.W + 2 * tx;
   w.c1ok = 2 * tx + 1 < p.W;
   w.r1ok = 2 * ty + 1 < p.H;
-  const int ubase = lr * 512 + lc * 4;  // U[c = lr][quad][m = lc][4] of a k-step's channel pair
+  const int au = (WM_KC * g.CS + lk * 512 + lj * 4) * 4;  // bytes: U[c = lk][quad 0][m = lj] of a k-step
 
-  floatx16_t acc[16];
+  // ---- DMA sources: wave w stages channels w and w + 4 of a chunk, and U pieces d = w + 4 v
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0, p.C * p.Mp * 16 * 4, 0x00020000);
+  const int uq = 2 * (wave & 1) + (lane >> 5);
+  const int uoff = (uq * p.Mp + m0 + (lane & 31)) * 16;
+  const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) float*)wm_lds;
+  const int nchunks = p.C / WM_KC;
+  auto stage = [&](int kc, int st) __attribute__((always_inline)) {
+    const unsigned sb = lds0 + (unsigned)(st * SS) * 4;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int cc = wave + 4 * h;
+      const int so = (kc * WM_KC + cc) * p.x_ps * 4;
+#pragma unroll
+      for (int gi = 0; gi < NDMA; ++gi)
+        if (voff[gi] >= 0) wm_dma16(xr, sb + (cc * g.CS + WM_ZL + 256 * gi) * 4, voff[gi], so);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int d = wave + 4 * v, cc = d >> 1;
+      wm_dma16(ur, sb + (WM_KC * g.CS + (cc * 4 + 2 * (d & 1)) * 128) * 4, uoff, (kc * WM_KC + cc) * 4 * p.Mp * 16);
+    }
+  };
+
+  wg_floatx4 acc[16][2];
 #pragma unroll
   for (int xi = 0; xi < 16; ++xi)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[xi][e] = 0.0f;
+    for (int f = 0; f < 2; ++f) acc[xi][f] = wg_floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const char* lds_b = reinterpret_cast<const char*>(wm_lds);
+  auto load_win = [&](int sto, float (&d)[4][4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[r][j] = *reinterpret_cast<const float*>(lds_b + aw[r] + sto + 4 * j);
+  };
+  auto load_u = [&](int sto, int f, int q) __attribute__((always_inline)) {
+    return *reinterpret_cast<const wg_floatx4*>(lds_b + au + sto + q * 512 + f * 64);
+  };
+  auto xform = [&](float (&d)[4][4], float (&v)[16]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      d[r][0] = c0ok ? d[r][0] : 0.0f;
+      d[r][2] = c2ok ? d[r][2] : 0.0f;
+      d[r][3] = c3ok ? d[r][3] : 0.0f;
+    }
+    wg_input_transform(d, v);
+  };
 
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kc = 0; kc < nchunks; ++kc) {
-    const int buf = kc & 1;
-    if (kc + 1 < nchunks) stage(kc + 1, buf ^ 1);
-    const float* ib = ibuf + buf * WL_KC * g.CS + wbase;
-    const float* ub = ubuf + buf * WL_KC * 512 + ubase;
+    const int st = kc & 1;
+#ifndef ORE_EXP_WM_NODMA  // timing experiments only (tools/build_exp.sh): no DMA after the prologue
+    if (kc + 1 < nchunks) stage(kc + 1, st ^ 1);
+#endif
+    const int sto0 = st * SS * 4, sto1 = sto0 + 4 * g.CS * 4;  // k-step 1: channels 4 .. 7 of the chunk
     wg_floatx4 ua[2][4];
-    wg_f2 dw[2][8];
-    auto ld = [&](int s, int slot) __attribute__((always_inline)) {
+    float d0[4][4], d1[4][4], v[16];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) ua[slot][q] = *reinterpret_cast<const wg_floatx4*>(ub + (2 * s) * 512 + q * 128);
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        dw[slot][2 * r] = *reinterpret_cast<const wg_f2*>(ib + (2 * s) * g.CS + r * g.RS);
-        dw[slot][2 * r + 1] = *reinterpret_cast<const wg_f2*>(ib + (2 * s) * g.CS + r * g.RS + 2);
-      }
-    };
-    ld(0, 0);
+      for (int f = 0; f < 2; ++f) ua[f][q] = load_u(sto0, f, q);
+    load_win(sto0, d0);
+    xform(d0, v);
+    load_win(sto1, d1);
+    __builtin_amdgcn_sched_barrier(0);
+    // k-step 0; U of k-step 1 (its channels' quads at +4 * 512 floats) replaces each quad once used
 #pragma unroll
-    for (int s = 0; s < WL_KC / 2; ++s) {
-      const int cur = s & 1;
-      if (s + 1 < WL_KC / 2) ld(s + 1, cur ^ 1);
-      __builtin_amdgcn_sched_barrier(0);  // the next step's LDS reads stay ahead of this step's MFMAs
-      float d[4][4], v[16];
+    for (int q = 0; q < 4; ++q) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        d[r][0] = dw[cur][2 * r][0]; d[r][1] = dw[cur][2 * r][1];
-        d[r][2] = dw[cur][2 * r + 1][0]; d[r][3] = dw[cur][2 * r + 1][1];
-      }
-      wg_input_transform(d, v);
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int xi = 0; xi < 16; ++xi)
-        acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[cur][xi >> 2][xi & 3], v[xi], acc[xi], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
+        for (int f = 0; f < 2; ++f)
+          acc[4 * q + j][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][q][j], v[4 * q + j], acc[4 * q + j][f], 0, 0, 0);
+#pragma unroll
+      for (int f = 0; f < 2; ++f) ua[f][q] = load_u(sto0 + 4 * 512 * 4, f, q);
     }
+    __builtin_amdgcn_sched_barrier(0);
+    xform(d1, v);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+          acc[4 * q + j][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][q][j], v[4 * q + j], acc[4 * q + j][f], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk kc + 1 have landed
-    __syncthreads();  // ... every wave's, and every wave is done reading buffer kc & 1
+    __syncthreads();  // ... every wave's, and every wave is done reading stage kc & 1
   }
-  // accumulator element e of a lane is row (e & 3) + 8 (e >> 2) + 4 lr (channel), column lc (tile)
+  // lane (lk, lj) of fragment f holds rows 4 lk + e = channel m0 + 16 f + 4 lk + e of tile lj
+  float bv[2][4];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int r = (e & 3) + 8 * (e >> 2);
-    const int m = m0 + r + 4 * lr;
-    if (m >= p.M) continue;
-    float mx[16];
+  for (int f = 0; f < 2; ++f)
 #pragma unroll
-    for (int xi = 0; xi < 16; ++xi) mx[xi] = acc[xi][e];
-    wg_store(p, w, m, p.bias ? p.bias[m] : 0.0f, mx);
-  }
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + 16 * f + 4 * lk + e;
+      bv[f][e] = p.bias && m < p.M ? p.bias[m] : 0.0f;
+    }
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + 16 * f + 4 * lk + e;
+      if (m >= p.M) continue;
+      float mx[16];
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) mx[xi] = acc[xi][f][e];
+      wg_store(p, w, m, bv[f][e], mx);
+    }
 }
 
 // the LDS kernel's geometry; false when the layer does not fit it
-static bool wl_geom(const ConvParams& p, WlGeom* g, size_t* lds) {
-  if (p.C % WL_KC != 0 || p.C <= 0 || p.W + 2 > 512) return false;
+static bool wm_geom(const ConvParams& p, WmGeom* g, size_t* lds, int* ndma) {
+  if (p.C % WM_KC != 0 || p.C <= 0 || p.H <= 0 || p.W <= 0) return false;
   g->TW = (p.W + 1) / 2;
   const int TH = (p.H + 1) / 2;
   g->TPI = g->TW * TH;
-  g->HP = 2 * TH + 2;
-  g->RS = (p.W + 2 + 1) & ~1;
   const long long T = (long long)p.N * g->TPI;
-  g->ntg = (int)((T + WL_TILES - 1) / WL_TILES);
-  // staged slots of the widest tile group (rows of the tile rows it spans + the image breaks)
-  int nslot = 0;
-  for (long long t0 = 0; t0 < T; t0 += WL_TILES) {
-    const long long t1 = std::min(T, t0 + WL_TILES) - 1;
-    const long long s0 = (t0 / g->TPI) * g->HP + 2 * ((t0 % g->TPI) / g->TW);
-    const long long s1 = (t1 / g->TPI) * g->HP + 2 * ((t1 % g->TPI) / g->TW) + 3;
-    nslot = std::max(nslot, (int)(s1 - s0 + 1));
-    if (t0 >= (long long)WL_TILES * g->TPI) break;  // group starts repeat mod TPI: every case seen
-  }
-  g->NG = (nslot * g->RS + 63) / 64;
-  g->CS = g->NG * 64 + 32;  // +32: the two lane halves' channels on opposite halves of the banks
-  *lds = ((size_t)2 * WL_KC * g->CS + (size_t)2 * WL_KC * 512) * 4;
-  return g->NG <= 32 && *lds <= 160 * 1024;
+  g->ntg = (int)((T + WM_TILES - 1) / WM_TILES);
+  // group starts repeat modulo TPI (period TPI / gcd(64, TPI)): every case is among the first TPI
+  int tmax = 0;
+  const long long ng = std::min<long long>(g->ntg, g->TPI);
+  for (long long gi = 0; gi < ng; ++gi)
+    tmax = std::max(tmax, wm_group_floats(gi * WM_TILES, T, g->TPI, g->TW, p.H, p.W));
+  *ndma = (tmax + 255) / 256;
+  g->CS = (WM_ZL + tmax + 4 + 31) / 64 * 64 + 32;
+  *lds = (size_t)2 * WM_KC * (g->CS + 512) * 4;
+  return *ndma <= 8 && *lds <= 160 * 1024;
 }
 
-template <int NGW>
-static void launch_wl(const ConvParams& p0, const WlGeom& g, size_t lds, hipStream_t s) {
+template <int NDMA>
+static void launch_wm(const ConvParams& p0, const WmGeom& g, size_t lds, hipStream_t s) {
   ConvParams p = p0;
-  p.mtiles = (p.M + 31) / 32;
+  p.mtiles = (p.M + WM_CH - 1) / WM_CH;
   if (lds > 64 * 1024) {  // above the default dynamic-LDS limit: raise it once per device
     static std::atomic<unsigned long long> raised{0};
     int dev = 0;
     (void)hipGetDevice(&dev);
     const unsigned long long bit = 1ull << (dev & 63);
     if (!(raised.load(std::memory_order_acquire) & bit)) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_winol_kernel<NGW>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_winol_kernel<NDMA>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       raised.fetch_or(bit, std::memory_order_acq_rel);
     }
   }
-  hipLaunchKernelGGL((conv_winol_kernel<NGW>), dim3((unsigned)(g.ntg * p.mtiles)), dim3(256), lds, s, p, g);
+  hipLaunchKernelGGL((conv_winol_kernel<NDMA>), dim3((unsigned)(g.ntg * p.mtiles)), dim3(256), lds, s, p, g);
 }
 
 static void launch_winol(const ConvParams& p, hipStream_t s) {
-  WlGeom g;
+  WmGeom g;
   size_t lds = 0;
-  if (!wl_geom(p, &g, &lds)) return;  // the caller checked conv_wino_eligible
-  switch ((g.NG + 3) / 4) {
-    case 1: launch_wl<1>(p, g, lds, s); break;
-    case 2: launch_wl<2>(p, g, lds, s); break;
-    case 3: launch_wl<3>(p, g, lds, s); break;
-    case 4: launch_wl<4>(p, g, lds, s); break;
-    case 5: launch_wl<5>(p, g, lds, s); break;
-    case 6: launch_wl<6>(p, g, lds, s); break;
-    case 7: launch_wl<7>(p, g, lds, s); break;
-    default: launch_wl<8>(p, g, lds, s); break;
+  int ndma = 0;
+  if (!wm_geom(p, &g, &lds, &ndma)) return;  // the caller checked conv_wino_eligible
+  switch (ndma) {
+    case 1: launch_wm<1>(p, g, lds, s); break;
+    case 2: launch_wm<2>(p, g, lds, s); break;
+    case 3: launch_wm<3>(p, g, lds, s); break;
+    case 4: launch_wm<4>(p, g, lds, s); break;
+    case 5: launch_wm<5>(p, g, lds, s); break;
+    case 6: launch_wm<6>(p, g, lds, s); break;
+    case 7: launch_wm<7>(p, g, lds, s); break;
+    default: launch_wm<8>(p, g, lds, s); break;
   }
 }
-
 
 // Winograd tiles (ConvPlan cfg = WINO_TILE_BASE + t): shape (32: 32x32x2, 16: 16x16x4), channels and
 // 2x2 tiles per wave, A / B ring depths of the unrolled K loop
 struct WinoTile { int shape, ch, tiles, da, db; };
 static const WinoTile WINO_TILES[WINO_TILES_N] = {{32, 32, 32, 2, 8}, {32, 32, 32, 2, 4}, {16, 32, 16, 2, 8},
-                                                  {16, 16, 32, 2, 4}, {0, 32, WL_TILES, 0, 0}};  // 4: conv_winol_kernel
+                                                  {16, 16, 32, 2, 4}, {0, WM_CH, WM_TILES, 0, 0}};  // 4: conv_winol_kernel
 
 bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo) {
   return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && Ho == H && Wo == W && C % 16 == 0 && C > 0;
@@ -698,9 +752,10 @@ bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, i
 bool conv_wino_eligible(const ConvParams& p, int tile) {
   if (tile < 0 || tile >= WINO_TILES_N) return false;
   if (tile == 4) {
-    WlGeom g;
+    WmGeom g;
     size_t lds;
-    return conv_wino_geometry(p.C, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.H, p.W, p.Ho, p.Wo) && wl_geom(p, &g, &lds) &&
+    int ndma;
+    return conv_wino_geometry(p.C, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.H, p.W, p.Ho, p.Wo) && wm_geom(p, &g, &lds, &ndma) &&
            p.x_bytes > 0 && p.x_bytes < (1LL << 31) - (1LL << 21) && (reinterpret_cast<uintptr_t>(p.x) & 3) == 0 &&
            p.Mp % 64 == 0 && (long long)p.C * p.Mp * 64 < (1LL << 31) &&
            (long long)p.N * ((p.H + 1) / 2) * ((p.W + 1) / 2) < (1LL << 30) &&

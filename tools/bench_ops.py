@@ -2,7 +2,8 @@
 """Kernel-level timing of single-node graphs (one Conv(+Relu) or MaxPool node) through the
 device walker, so weights are packed once and only the op's kernel is timed (HIP events on the
 context stream).  Shapes default to the SqueezeNet-1.0 layers at batch 256.
-usage: python tools/bench_ops.py [--batch 256] [--only conv|pool] [--reps 20] [--tile T] [--pool-variant V]
+usage: python tools/bench_ops.py [--batch 256] [--only conv|pool] [--names f8.e3,..] [--reps 20] [--tile T]
+       [--pool-variant V]
 (--tile / --pool-variant: ore_ctx_set_conv_tile / ore_ctx_set_pool_variant)"""
 import argparse
 import os
@@ -69,7 +70,9 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tile", type=int, default=-1)
     ap.add_argument("--pool-variant", type=int, default=0)
+    ap.add_argument("--names", default="", help="comma-separated layer names (default: all)")
     a = ap.parse_args()
+    keep = set(a.names.split(",")) if a.names else None
     import torch
     import ore
     ctx = ore.Context(0)
@@ -79,6 +82,8 @@ def main():
     B = a.batch
     if a.only in ("", "conv"):
         for name, cin, h, cout, k, s, p in CONVS:
+            if keep is not None and name not in keep:
+                continue
             x = torch.randn((B, cin, h, h), device="cuda")
             us = time_model(ctx, conv_graph(cin, h, cout, k, s, p), x, a.reps)
             ho = (h + 2 * p - k) // s + 1
@@ -86,6 +91,8 @@ def main():
             print(f"{tag} {name:8s} {us:9.1f} us {tf:7.1f} TF/s", flush=True)
     if a.only in ("", "pool"):
         for name, c, h, pads in POOLS:
+            if keep is not None and name not in keep:
+                continue
             x = torch.randn((B, c, h, h), device="cuda")
             us = time_model(ctx, pool_graph(c, h, pads), x, a.reps)
             ho = (h + pads[2] - 3) // 2 + 1
