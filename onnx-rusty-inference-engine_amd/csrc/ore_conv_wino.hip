@@ -608,7 +608,7 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
       for (int j = 0; j < 4; ++j) d[r][j] = *reinterpret_cast<const float*>(lds_b + aw[r] + sto + 4 * j);
   };
   auto load_u = [&](int sto, int f, int q) __attribute__((always_inline)) {
-    return *reinterpret_cast<const wg_floatx4*>(lds_b + au + sto + q * 512 + f * 64);
+    return *reinterpret_cast<const wg_floatx4*>(lds_b + au + sto + q * 512 + f * 256);  // m = 16 f + lj
   };
   auto xform = [&](float (&d)[4][4], float (&v)[16]) __attribute__((always_inline)) {
 #pragma unroll
