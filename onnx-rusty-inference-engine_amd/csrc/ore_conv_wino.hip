@@ -605,12 +605,22 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) d[r][j] = *reinterpret_cast<const float*>(lds_b + aw[r] + sto + 4 * j);
+      for (int j = 0; j < 4; ++j)
+#ifndef ORE_EXP_WM_NOWIN  // timing experiments only (tools/build_exp.sh)
+        d[r][j] = *reinterpret_cast<const float*>(lds_b + aw[r] + sto + 4 * j);
+#else
+        d[r][j] = (float)(aw[r] + sto + j);
+#endif
   };
   auto load_u = [&](int sto, int f, int q) __attribute__((always_inline)) {
+#ifndef ORE_EXP_WM_NOU
     return *reinterpret_cast<const wg_floatx4*>(lds_b + au + sto + q * 512 + f * 256);  // m = 16 f + lj
+#else
+    return wg_floatx4{(float)(au + sto + q), (float)f, 1.0f, 2.0f};
+#endif
   };
   auto xform = [&](float (&d)[4][4], float (&v)[16]) __attribute__((always_inline)) {
+#ifndef ORE_EXP_WM_NOXF
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       d[r][0] = c0ok ? d[r][0] : 0.0f;
@@ -618,6 +628,10 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
       d[r][3] = c3ok ? d[r][3] : 0.0f;
     }
     wg_input_transform(d, v);
+#else
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = d[i >> 2][i & 3];
+#endif
   };
 
   stage(0, 0);
@@ -681,6 +695,9 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
       float mx[16];
 #pragma unroll
       for (int xi = 0; xi < 16; ++xi) mx[xi] = acc[xi][f][e];
+#ifdef ORE_EXP_WM_NOEPI  // timing experiment only: the epilogue skipped (kept live by a never-true test)
+      if (mx[0] + mx[5] + mx[10] + mx[15] != 1.2345e-30f) continue;
+#endif
       wg_store(p, w, m, bv[f][e], mx);
     }
 }
