@@ -461,7 +461,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
 constexpr int WM_KC = 8;      // input channels per K chunk (2 k-steps of 4)
 constexpr int WM_TILES = 64;  // 2x2 tiles per workgroup (16 per wave)
 constexpr int WM_CH = 32;     // output channels per workgroup
-constexpr int WM_ZL = 4;      // zero floats at the start of a staged channel (rows outside the image)
+constexpr int WM_ZL = 8;      // zero floats at the start of a staged channel (rows outside the image)
 
 __device__ __forceinline__ void wm_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, int voffset, int soffset) {
   int m0save;
@@ -490,7 +490,7 @@ __host__ __device__ __forceinline__ void wm_rows(int img, int img0, int ty0, int
   *re = img == img1 ? min(H - 1, 2 * ty1 + 2) : H - 1;
 }
 
-// floats staged per channel for the tile group starting at t0 (each image's run rounded up to 4)
+// floats staged per channel for the tile group starting at t0 (each image's run + 1, rounded up to 4)
 static int wm_group_floats(long long t0, long long T, int TPI, int TW, int H, int W) {
   const long long t1 = std::min(T, t0 + WM_TILES) - 1;
   const int img0 = (int)(t0 / TPI), ty0 = (int)(t0 % TPI) / TW;
@@ -499,7 +499,7 @@ static int wm_group_floats(long long t0, long long T, int TPI, int TW, int H, in
   for (int i = img0; i <= img1; ++i) {
     int rs, re;
     wm_rows(i, img0, ty0, img1, ty1, H, &rs, &re);
-    total += ((re - rs + 1) * W + 3) & ~3;
+    total += ((re - rs + 1) * W + 4) & ~3;  // one spare float: odd channels' shifted last element
   }
   return total;
 }
@@ -524,7 +524,7 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
 
   // the zero blocks (never written by the DMAs)
   if (threadIdx.x < 2 * WM_KC * WM_ZL)
-    wm_lds[(threadIdx.x >> 5) * SS + ((threadIdx.x >> 2) & 7) * g.CS + (threadIdx.x & 3)] = 0.0f;
+    wm_lds[(threadIdx.x >> 6) * SS + ((threadIdx.x >> 3) & 7) * g.CS + (threadIdx.x & 7)] = 0.0f;
 
   // ---- this lane's tile (lj of the wave's 16) and the run layout of the group
   const int lk = lane >> 4, lj = lane & 15;
@@ -546,20 +546,22 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
 #pragma unroll
     for (int gi = 0; gi < NDMA; ++gi) {
       const int k4 = 4 * (64 * gi + lane);
-      if (k4 >= lb && k4 < lb + len) voff[gi] = (int)((i * p.x_nstride + (long long)rs * p.W + (k4 - lb)) * 4);
+      if (k4 >= lb && k4 <= lb + len) voff[gi] = (int)((i * p.x_nstride + (long long)rs * p.W + (k4 - lb)) * 4);
     }
     if (i == img) {
       my_lb = lb;
       my_rs = rs;
     }
-    lb += (len + 3) & ~3;
+    lb += (len + 4) & ~3;  // runs of len + 1 floats (odd channels land one float later), rounded to 4
   }
   // window rows (floats from the channel's area; rows outside the image -> the zero block)
   int aw[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int gr = 2 * ty - 1 + r;
-    const int rel = (unsigned)gr < (unsigned)p.H ? WM_ZL + my_lb + (gr - my_rs) * p.W + 2 * tx - 1 : 0;
+    // odd channels are staged one float later (their DMA source starts one float early), so the two
+    // channels of a ds_read_b32 lane group (lk = 0, 1: CS = 0 mod 32 apart) use opposite bank parities
+    const int rel = ((unsigned)gr < (unsigned)p.H ? WM_ZL + my_lb + (gr - my_rs) * p.W + 2 * tx - 1 : 0) + (lk & 1);
     aw[r] = (lk * g.CS + rel) * 4;  // bytes, channel lk of a k-step
   }
   const bool c0ok = tx > 0, c2ok = 2 * tx + 1 < p.W, c3ok = 2 * tx + 2 < p.W;
@@ -582,7 +584,7 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int cc = wave + 4 * h;
-      const int so = (kc * WM_KC + cc) * p.x_ps * 4;
+      const int so = (kc * WM_KC + cc) * p.x_ps * 4 - 4 * (cc & 1);  // odd channels: one float early (>= 0)
 #pragma unroll
       for (int gi = 0; gi < NDMA; ++gi)
         if (voff[gi] >= 0) wm_dma16(xr, sb + (cc * g.CS + WM_ZL + 256 * gi) * 4, voff[gi], so);
@@ -716,7 +718,7 @@ static bool wm_geom(const ConvParams& p, WmGeom* g, size_t* lds, int* ndma) {
   for (long long gi = 0; gi < ng; ++gi)
     tmax = std::max(tmax, wm_group_floats(gi * WM_TILES, T, g->TPI, g->TW, p.H, p.W));
   *ndma = (tmax + 255) / 256;
-  g->CS = (WM_ZL + tmax + 4 + 31) / 64 * 64 + 32;
+  g->CS = (WM_ZL + tmax + 5 + 31) / 64 * 64 + 32;  // + 1: odd channels' shift, + 4: the last window's overrun
   *lds = (size_t)2 * WM_KC * (g->CS + 512) * 4;
   return *ndma <= 8 && *lds <= 160 * 1024;
 }
