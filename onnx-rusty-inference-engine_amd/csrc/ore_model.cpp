@@ -548,6 +548,9 @@ constexpr int64_t FIRE_POOL_MIN_HW = 1024;    // fire + pool + squeeze on 54 x 5
 constexpr int64_t CONCAT_POOL_MIN_HW = 1024;  // concat + pool in the producers: fire4 -40 us, fire8 +21 us
 constexpr int64_t X3_FIRE_MIN_HW = 1024;      // x3 models: the f32 fire kernel beats x3 expand3x3 from 54 x 54
 constexpr double EPOOL_MAX_WORK = 1.25;       // conv + pool patch kernel: recomputed columns <= 1.25 x the conv's
+constexpr int64_t WINO_SPLIT_MIN_C = 48;      // fire + squeeze on planes < FIRE_POOL_MIN_HW with >= 48 squeeze
+                                              // channels: expand1x1 + Winograd expand3x3 + squeeze as three launches
+                                              // (fire6 / fire7: 328 / 323 us vs 345 / 362 fused; fire5 at C = 32: 192 vs 173)
 
 struct Planner {
   ore_model* m;
@@ -788,6 +791,8 @@ struct Planner {
         continue;
       if (e1.M % 64 || e3.M % 64 || q.M > 64 || e1.C % 16 || q.C != e1.M + e3.M) continue;
       if (!eager() && m->max_batch * e1.H * e1.W < FIRE_MIN_COLS) continue;
+      // Winograd expand3x3 (f32 models with Winograd on): the split is cheaper on small planes with wide inputs
+      if (!eager() && m->wino && e3.has_wino && e1.H * e1.W < FIRE_POOL_MIN_HW && e1.C >= WINO_SPLIT_MIN_C) continue;
       // x3 models: the f32-MFMA fire kernel only where it beats the x3 expand3x3 + separate 1x1s
       if (m->x3 && e3.has_x3 && e1.H * e1.W < X3_FIRE_MIN_HW && !eager()) continue;
       if (padded_plane(e1.H * e1.W) % 4) continue;  // 16-B planes (layout below)
