@@ -136,14 +136,23 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wc), (short)0, G::KQ * Mp32 * 32, 0x00020000);
   const int aoff = (lr * 2 + h) * 16;  // + ((q * Mp32 + 32 i) * 2) * 16
 
-  load_window(blockIdx.x);
+  // the workgroups of XCD x (blockIdx % 8; the grid is a multiple of 8) walk a contiguous eighth of
+  // the tiles, neighbouring patches at the same time: their shared window rows and columns meet in
+  // one L2
+  const bool grouped = (gridDim.x & 7) == 0;
+  const int xg = grouped ? (int)(blockIdx.x & 7) : 0;
+  const int nslot = grouped ? (int)(gridDim.x >> 3) : (int)gridDim.x;
+  const int tlo = (int)((long long)ntiles * xg / (grouped ? 8 : 1));
+  const int thi = grouped ? (int)((long long)ntiles * (xg + 1) / 8) : ntiles;
+  const int tfirst = tlo + (grouped ? (int)(blockIdx.x >> 3) : (int)blockIdx.x);
+  load_window(tfirst < thi ? tfirst : ntiles);
   store_window();
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int tile = tfirst; tile < thi; tile += nslot) {
     const int img = tile / tpi, tt = tile - img * tpi;
     const int ph0 = (tt / p.ep_tc) * C3_PR, pw0 = (tt - (tt / p.ep_tc) * p.ep_tc) * C3_PC;
     const int ohb = ph0 * 2 - p.ep_pt, owb = pw0 * 2 - p.ep_pl;
     __syncthreads();  // this tile's window is in LDS; the previous tile's pool readers are done
-    load_window(tile + gridDim.x);
+    load_window(tile + nslot < thi ? tile + nslot : ntiles);
 
     c3f16 acc[MF][2];
 #pragma unroll
@@ -328,8 +337,10 @@ static bool c3_launch(const ConvParams& p, const float* wc, const C1SqueezeF32& 
 #ifdef ORE_C3_WPC
   per_cu = ORE_C3_WPC;  // experiment knob
 #endif
-  const unsigned grid = (unsigned)std::min<long long>(tiles, (long long)per_cu * ncu);
-  hipLaunchKernelGGL((conv_win_pool_f32_kernel<MF, C, 7, 7, 2, SQ>), dim3(grid), dim3(256), lds, s, p, wc, sq);
+  long long grid = std::min<long long>(tiles, (long long)per_cu * ncu);
+  if (grid >= 8) grid &= ~7LL;  // a multiple of 8: XCD-grouped tile ranges
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((conv_win_pool_f32_kernel<MF, C, 7, 7, 2, SQ>), dim3((unsigned)grid), dim3(256), lds, s, p, wc, sq);
   return true;
 }
 

@@ -45,7 +45,12 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
   const int tid = threadIdx.x, lane = tid & 63, lk = lane >> 4, lj = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bands = (p.Hp + PS_PR - 1) / PS_PR;
-  const int img = blockIdx.x / bands, pr0 = (blockIdx.x - img * bands) * PS_PR;
+  // XCD-aware bijective block remap (consecutive bands of an image on one XCD: the input row a band
+  // shares with the next one is read once from HBM)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
+  const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
+  const int img = wgid / bands, pr0 = (wgid - img * bands) * PS_PR;
   const int ih0 = pr0 * 2 - p.pt, iw0 = -p.pl;  // input coordinates of staged (row 0, col 0)
   const int wcols = 2 * (p.Wp - 1) + 3;         // input columns the pooled row reads
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(

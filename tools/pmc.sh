@@ -20,5 +20,5 @@ while read -r GROUP; do
   rc=$?
   echo "pass $i [$GROUP] rc=$rc"
   case $rc in 124|134|137|139) echo "fatal"; exit $rc;; esac
-done < "${PMC_GROUPS:-$ROOT/tools/pmc_groups.txt}"
+done < "$ROOT/${PMC_GROUPS:-tools/pmc_groups.txt}"
 exit 0

@@ -18,6 +18,6 @@ for T in "$@"; do
     rc=$?
     echo "tile $T pass $i rc=$rc"
     case $rc in 0) ;; *) echo "fatal"; exit $rc;; esac
-  done < "${PMC_GROUPS:-$ROOT/tools/pmc_groups_sq.txt}"
+  done < "$ROOT/${PMC_GROUPS:-tools/pmc_groups_sq.txt}"
 done
 exit 0
