@@ -108,7 +108,8 @@ ore_status ore_ctx_set_conv_algo(ore_ctx* ctx, int32_t algo);
  *  ore_ctx_set_conv_tile: every conv planned on this context afterwards -- ore_conv2d_f32 /
  *    ore_matmul_f32 calls, and models loaded later -- uses tile id `tile` where it belongs to the
  *    layer's kernel family (else the per-layer heuristic); -1 (default) = the heuristic.  Ids as
- *    ore_model_step_tile reports them (0-3 LDS-staged, 12-20 streaming, 28-35 x3, 36-39 Winograd).
+ *    ore_model_step_tile reports them (0-3 LDS-staged, 12-20 streaming, 28-35 x3, 36-40 Winograd,
+ *    46-48 persistent streaming 1x1).
  *  ore_ctx_set_pool_variant: MaxPool kernel of ore_maxpool2d_f32 and of the walker's MaxPool steps:
  *    0 (default) = by layout, 2 one thread per output, 3 column strips, 4 plane-staged, 5
  *    chunk-staged. */

@@ -608,6 +608,7 @@ ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, i
   // 96-row tile measured fastest for them even with padded rows (tools/bench_ops.py)
   if (K <= 64 && M >= 64 && is1x1) pln.cfg = 1;
   if (forced >= 0 && forced < (f16 ? CONV_TILES_F16 : CONV_TILES_F32) && !conv_tile_retired(forced)) pln.cfg = forced;
+  if (!f16 && is1x1 && forced >= CONV_TILE_SP && forced < CONV_TILE_SP + CONV_TILES_SP) pln.cfg = forced;
   // packed rows cover every block tile's rows (the 96-row tile can pass roundup(M, 128)), so
   // the tile can be changed after packing (ore_model_autotune)
   pln.Mp = conv_packed_mp(M);

@@ -25,6 +25,8 @@
 // pixel tile share the block when M > 16*MF, so the B rows they read hit the CU's L1).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "ore_kernels.h"
 
 namespace ore {
@@ -228,6 +230,141 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(ConvParams p) {
     }
 }
 
+// Persistent 1x1 variant (S1X1 only; tiles CONV_TILE_SP + 0..2): the HBM-bound 1x1 layers with a
+// short K (squeeze / expand1x1: 16-64 k-steps) spent each wave's start waiting for its first loads and
+// its end on stores with nothing else in flight.  Here a wave keeps its 16 MF output channels and walks
+// pixel tiles ct = cs, cs + ncs, ... (ncs = resident waves / m tiles); the operand ring runs across
+// tiles, so the next tile's first D k-steps are loading during this tile's last MFMAs and its stores.
+// The same operands, k order and epilogue as conv_stream_kernel: bit-identical.
+template <int MF, int NB, int D>
+__global__ __launch_bounds__(256, 2) void conv_stream1x1_persist_kernel(ConvParams p) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
+  const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
+  const int gw = wgid * 4 + wave;
+  const int ncs = (nwg * 4) / p.mtiles;  // host: nwg * 4 >= mtiles
+  const int mt = gw % p.mtiles, cs = gw / p.mtiles;
+  if (cs >= ncs || cs >= p.ntiles) return;  // wave-uniform; no barrier in this kernel
+  const int m0 = mt * (16 * MF);
+  const int YPS = p.y_ps;
+  const int lk = lane >> 4, lj = lane & 15;
+  const int ntot = (int)p.Ntot;
+  // a pixel tile's per-lane input / output offsets (clamped columns re-read valid data, masked at the store)
+  auto geo = [&](int ct, int (&xo)[NB], int (&yo)[NB], bool (&ok)[NB]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < NB; ++g) {
+      int col = ct * (64 * NB) + 64 * g + 4 * lj;
+      ok[g] = col < ntot;
+      if (!ok[g]) col = ntot - 4;
+      const int img = col / YPS;
+      const int pix = col - img * YPS;
+      yo[g] = img * (int)p.y_nstride + pix;
+      xo[g] = (img * (int)p.x_nstride + lk * p.x_ps + pix) * 4;
+    }
+  };
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
+  const int kp = (p.K + 31) & ~31;
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0, kp * p.Mp * 4, 0x00020000);
+  const int aoff = (lk * p.Mp + m0 + MF * lj) * 4;
+  const int xstep = 16 * p.x_ps, astep = 16 * p.Mp;
+  const int nks = p.K >> 2;  // host: nks % D == 0, nks >= D
+
+  float bias[MF][4];
+#pragma unroll
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + MF * (4 * lk + e) + f;
+      bias[f][e] = p.bias && m < p.M ? p.bias[m] : 0.0f;
+    }
+
+  cs_floatx4 acc[MF][NB][4];
+  cs_floatx4 rb[D][NB];
+  float ra[D][MF];
+  int xoff[NB], yoff[NB];
+  bool cok[NB];
+  int ct = cs;
+  geo(ct, xoff, yoff, cok);
+#define SP_LOAD(SLOT, S, XO)                                                                      \
+  {                                                                                               \
+    cs_load_a<MF>(wr, aoff, (S) * astep, ra[SLOT]);                                               \
+    _Pragma("unroll") for (int g = 0; g < NB; ++g) rb[SLOT][g] = __builtin_bit_cast(              \
+        cs_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, XO[g], (S) * xstep, 0));             \
+  }
+#define SP_MFMA(SLOT)                                                                             \
+  __builtin_amdgcn_s_setprio(1);                                                                  \
+  _Pragma("unroll") for (int f = 0; f < MF; ++f)                                                  \
+  _Pragma("unroll") for (int g = 0; g < NB; ++g)                                                  \
+  _Pragma("unroll") for (int q = 0; q < 4; ++q)                                                   \
+      acc[f][g][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[SLOT][f], rb[SLOT][g][q], acc[f][g][q], 0, 0, 0); \
+  __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+  for (int d = 0; d < D; ++d) SP_LOAD(d, d, xoff);
+  while (true) {
+#pragma unroll
+    for (int f = 0; f < MF; ++f)
+#pragma unroll
+      for (int g = 0; g < NB; ++g)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[f][g][q] = cs_floatx4{0.f, 0.f, 0.f, 0.f};
+    const int ctn = ct + ncs;
+    const bool hasn = ctn < p.ntiles;  // wave-uniform
+    int xoffn[NB], yoffn[NB];
+    bool cokn[NB];
+    geo(hasn ? ctn : ct, xoffn, yoffn, cokn);
+    for (int s0 = 0; s0 < nks - D; s0 += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        SP_MFMA(d);
+        __builtin_amdgcn_sched_barrier(0);
+        SP_LOAD(d, s0 + D + d, xoff);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // the last D k-steps; each slot refills with the next tile's k-step d
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      SP_MFMA(d);
+      __builtin_amdgcn_sched_barrier(0);
+      if (hasn) SP_LOAD(d, d, xoffn);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // epilogue (conv_stream_kernel's): lane (lk, lj) of fragment f holds channel m0 + MF (4 lk + e) + f,
+    // pixels 4 lj + q of each group
+    float* __restrict__ y = p.y;
+#pragma unroll
+    for (int f = 0; f < MF; ++f)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + MF * (4 * lk + e) + f;
+        if (m >= p.M) continue;
+        const float b = bias[f][e];
+#pragma unroll
+        for (int g = 0; g < NB; ++g) {
+          cs_floatx4 v = {acc[f][g][0][e] + b, acc[f][g][1][e] + b, acc[f][g][2][e] + b, acc[f][g][3][e] + b};
+          if (p.relu) {
+            v[0] = fmaxf(v[0], 0.0f); v[1] = fmaxf(v[1], 0.0f); v[2] = fmaxf(v[2], 0.0f); v[3] = fmaxf(v[3], 0.0f);
+          }
+          if (cok[g]) *reinterpret_cast<cs_floatx4*>(y + (unsigned)(yoff[g] + m * YPS)) = v;
+        }
+      }
+    if (!hasn) break;
+    ct = ctn;
+#pragma unroll
+    for (int g = 0; g < NB; ++g) {
+      xoff[g] = xoffn[g];
+      yoff[g] = yoffn[g];
+      cok[g] = cokn[g];
+    }
+  }
+#undef SP_LOAD
+#undef SP_MFMA
+}
+
 // bytes read before x by a 3x3 'same' conv: tap (0, 0) of output pixel 0, rounded to 16
 static int stream_lead(const ConvParams& p) { return ((p.pt * p.W + p.pl) * 4 + 15) & ~15; }
 
@@ -248,9 +385,29 @@ static int stream_depth(int tile) {
   return t == 6 ? 8 : t == 8 ? 2 : 4;
 }
 
-// the geometry allows the streaming kernel and the tile's ring depth divides the K steps
+// the geometry allows the streaming kernel and the tile's ring depth divides the K steps; the
+// persistent tiles (CONV_TILE_SP + t) run 1x1 convs only
 bool conv_stream_eligible(const ConvParams& p, int tile) {
+  if (tile >= CONV_TILE_SP) return stream_mode(p) == 1 && (p.K / 4) % 4 == 0 && p.K >= 16;
   return stream_mode(p) != 0 && (p.K / 4) % stream_depth(tile) == 0;
+}
+
+template <int MF, int NB, int D>
+static void launch_sp(const ConvParams& p0, hipStream_t s) {
+  ConvParams p = p0;
+  p.mtiles = (p.M + 16 * MF - 1) / (16 * MF);
+  p.ntiles = (int)((p.Ntot + 64 * NB - 1) / (64 * NB));
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
+  }
+  // resident waves (2 workgroups per CU), at least one per m tile, at most one per (m tile, pixel tile)
+  const long long need = (long long)p.mtiles * p.ntiles;
+  long long waves = std::min<long long>(8LL * ncu, need);
+  waves = std::max<long long>(waves, p.mtiles);
+  const unsigned grid = (unsigned)((waves + 3) / 4);
+  hipLaunchKernelGGL((conv_stream1x1_persist_kernel<MF, NB, D>), dim3(grid), dim3(256), 0, s, p);
 }
 
 template <int MF, int NB, int D>
@@ -270,6 +427,14 @@ static void launch_cs(const ConvParams& p0, hipStream_t s) {
 // tiles CONV_TILE_STREAM + 0..8 (ConvPlan::cfg); 16 x 512 tiles (NB = 8) measured no faster
 // on the 54 x 54 squeezes (tools/bench_1x1.py, profiles/r01y_bench_1x1.txt); the caller checks conv_stream_eligible
 void launch_conv_stream(const ConvParams& p, int tile, hipStream_t s) {
+  if (tile >= CONV_TILE_SP) {
+    switch (tile - CONV_TILE_SP) {
+      case 0: launch_sp<2, 2, 4>(p, s); break;  // 32 x 128
+      case 1: launch_sp<4, 1, 4>(p, s); break;  // 64 x 64
+      default: launch_sp<1, 4, 4>(p, s); break; // 16 x 256
+    }
+    return;
+  }
   switch (tile - CONV_TILE_STREAM) {
     case 0: launch_cs<4, 2, 4>(p, s); break;   // 64 x 128
     case 1: launch_cs<2, 4, 4>(p, s); break;   // 32 x 256

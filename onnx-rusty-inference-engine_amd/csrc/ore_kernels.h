@@ -280,6 +280,9 @@ inline bool conv_tile_retired(int t) { return t >= 4 && t < 12; }
 // expand3x3); tiles CONV_TILE_STREAM + 0..8 = 64x128, 32x256, 16x256, 48x128, 64x64, 128x64, 64x64 D8,
 // 32x128, 128x64 D2 (channels x pixels per wave); other geometries fall back to tile 0
 constexpr int CONV_TILE_STREAM = 12;
+// persistent 1x1 streaming tiles (conv_stream1x1_persist_kernel): 32x128, 64x64, 16x256; ids after the
+// fused-kernel ids (ore.Model.TILE_NAMES "stream1x1 persist ...")
+constexpr int CONV_TILE_SP = 46, CONV_TILES_SP = 3;
 bool conv_stream_eligible(const ConvParams& p, int tile);
 void launch_conv_stream(const ConvParams& p, int tile, hipStream_t s);
 // the tile launch_conv actually ran last on this thread (a 1x1 tile on an ineligible geometry runs

@@ -1465,6 +1465,8 @@ std::vector<int> step_tile_family(const Step& s) {
   // not allow it)
   if (!s.plan.f16 && s.kind == S_CONV)
     for (int t = CONV_TILE_STREAM; t < CONV_TILES_F32; ++t) c.push_back(t);
+  if (!s.plan.f16 && s.kind == S_CONV && s.kh == 1 && s.kw == 1)  // the persistent 1x1 tiles
+    for (int t = CONV_TILE_SP; t < CONV_TILE_SP + CONV_TILES_SP; ++t) c.push_back(t);
   return c;
 }
 

@@ -583,7 +583,8 @@ ore_status ore_ctx_set_conv_algo(ore_ctx* ctx, int32_t algo) {
 
 ore_status ore_ctx_set_conv_tile(ore_ctx* ctx, int32_t tile) {
   if (!ctx) return set_error(nullptr, ORE_ERR_INVALID, "null context");
-  if (tile < -1 || tile >= WINO_TILE_BASE + WINO_TILES_N || conv_tile_retired(tile))
+  const bool sp = tile >= CONV_TILE_SP && tile < CONV_TILE_SP + CONV_TILES_SP;
+  if (!sp && (tile < -1 || tile >= WINO_TILE_BASE + WINO_TILES_N || conv_tile_retired(tile)))
     return set_error(ctx, ORE_ERR_INVALID, "conv tile %d is not a conv tile id", int(tile));
   ctx->conv_tile = tile;
   return ORE_OK;

@@ -326,7 +326,8 @@ class Model:
                   "x3w 128x128", "x3w 64x128", "x3w 128x64", "x3w 64x64",
                   "wino 32x32 d4", "wino 32x32 d2", "wino16 32x16", "wino16 16x32",
                   "wino lds", None,  # 41: the Winograd fire module (retired)
-                  "fire f16", "first conv pool f16", "epool window f32", "fire pool f32"]
+                  "fire f16", "first conv pool f16", "epool window f32", "fire pool f32",
+                  "stream1x1 persist 32x128", "stream1x1 persist 64x64", "stream1x1 persist 16x256"]
 
     def tiles(self):
         """Block tile per exec step (-1 for non-conv steps); names in TILE_NAMES."""

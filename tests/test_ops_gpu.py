@@ -128,6 +128,8 @@ STREAM_CASES = [
     (3, 32, 16, 16, 16, 1, 0, True),     # 768 columns over 3 images
     (2, 48, 7, 4, 48, 1, 0, True),       # fewer columns than one wave tile
     (2, 16, 13, 13, 24, 1, 0, True),     # 169-pixel planes: not eligible, falls back to tile 0
+    (3, 16, 64, 64, 1024, 1, 0, True),   # more pixel tiles than resident waves per m tile: the
+                                         # persistent tiles (46-48) walk 2 tiles per wave
     (2, 16, 12, 12, 64, 3, 1, True),     # expand3x3 (STAPS): zero-padded taps, row wraps
     (3, 32, 10, 10, 128, 3, 1, False),   # 300 columns over 3 images
     (1, 48, 7, 8, 192, 3, 1, True),      # W = 8: 4-pixel groups straddle rows
@@ -136,12 +138,13 @@ STREAM_CASES = [
 ]
 
 
-@pytest.mark.parametrize("tile", list(range(12, 21)))
+@pytest.mark.parametrize("tile", list(range(12, 21)) + [46, 47, 48])
 @pytest.mark.parametrize("case", STREAM_CASES)
 def test_conv_stream_bit_identical(gpu_ctx, case, tile):
-    """The LDS-free streaming kernel (ore_conv_stream.hip, 16x16x4 MFMA, tiles 12-16: 1x1 and 3x3
-    'same' convs) runs the same k-ordered fmaf chain per output as the LDS-staged kernel:
-    bit-identical to tile 0, and within the conv tolerance of the oracle."""
+    """The LDS-free streaming kernel (ore_conv_stream.hip, 16x16x4 MFMA, tiles 12-20: 1x1 and 3x3
+    'same' convs; 46-48: the persistent 1x1 variant, which walks several pixel tiles per wave) runs
+    the same k-ordered fmaf chain per output as the LDS-staged kernel: bit-identical to tile 0, and
+    within the conv tolerance of the oracle (the persistent tiles fall back to tile 0 on 3x3 layers)."""
     import ore
     N, C, H, W, M, k, pad, with_bias = case
     rng = np.random.default_rng(zlib.crc32(repr(case).encode()) ^ 0x1111)
