@@ -601,6 +601,29 @@ struct Planner {
     return *pa >= 0 && *pb >= 0 && *pa != *pb;
   }
 
+  // MaxPool step pl (3x3 / stride 2, f32 NCHW input) feeding 1x1 conv cv fits pool_conv1x1_f32_kernel
+  bool pool_squeeze_fits(const Step& pl, const Step& cv) const {
+    if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2) return false;
+    if (m->values[pl.in0].es != 4 || m->values[pl.in0].nhwc) return false;
+    if (cv.kind != S_CONV || cv.pool || cv.epool || cv.kh != 1 || cv.kw != 1 || cv.sh != 1 || cv.sw != 1 ||
+        cv.win.pt || cv.win.pl || cv.plan.f16 || cv.plan.x3 || cv.plan.wino || cv.M > 64 || cv.C % 32 ||
+        pl.win.pt > 2 || pl.win.pl > 2)
+      return false;
+    PoolConvParams q{};  // pool_conv1x1_f32_kernel's own limits (run_conv_pool has no other kernel)
+    q.C = int(cv.C); q.H = int(pl.H); q.W = int(pl.W); q.Hp = int(pl.win.Ho); q.Wp = int(pl.win.Wo);
+    q.pt = int(pl.win.pt); q.pl = int(pl.win.pl); q.M = int(cv.M); q.Mp = cv.plan.Mp; q.Kp = cv.plan.krows;
+    q.N = 1; q.x_ps = int(pl.H * pl.W); q.y_ps = int(pl.win.Ho * pl.win.Wo);
+    q.x_nstride = int64_t(q.C) * q.x_ps; q.y_nstride = int64_t(q.M) * q.y_ps;
+    return pool_conv1x1_f32_eligible(q);
+  }
+  // Winograd models: a fire module -> MaxPool -> squeeze runs cheaper as expand1x1 + Winograd
+  // expand3x3 + the pooled squeeze (pool_squeeze) than in the direct-kernel fusions (fire4 -> pool3
+  // -> fire5: 105 + 344 + pool and squeeze vs 713 us fused, profiles/r03_fusion_split.txt)
+  bool wino_pool_split(const Step& e3, const Step& pl, int qi) const {
+    return !eager() && m->wino && e3.has_wino && has(ORE_FUSE_POOL_SQUEEZE) && qi >= 0 &&
+           private_value(pl.out) && m->steps[qi].in0 == pl.out && pool_squeeze_fits(pl, m->steps[qi]);
+  }
+
   // (1) Conv -> Relu: the Relu in the conv epilogue
   void conv_relu() {
     if (!has(ORE_FUSE_CONV_RELU)) return;
@@ -679,6 +702,7 @@ struct Planner {
         continue;
       if (e1.M % 64 || e3.M % 64 || q.M > 64 || e1.C % 16 || q.C != e1.M + e3.M || pl.H != e1.H || pl.W != e1.W) continue;
       if (!eager() && (e1.H * e1.W < FIRE_POOL_MIN_HW || m->max_batch * e1.H * e1.W < FIRE_MIN_COLS)) continue;
+      if (wino_pool_split(e3, pl, qi)) continue;
       if (q.in2 < 0 || e1.in2 < 0 || e3.in2 < 0 || padded_plane(e1.H * e1.W) % 4) continue;  // 16-B input planes
       FireParams fp{};
       fp.H = int(e1.H); fp.W = int(e1.W);
@@ -742,6 +766,7 @@ struct Planner {
       const Step& sa = st(pa);
       if (epool_tile(sa.win.Ho, sa.win.Wo, pl.kh, pl.kw, pl.sh, pl.sw, pl.win, &t1, &t2) == 0.0) continue;
       if (sa.win.Ho * sa.win.Wo < CONCAT_POOL_MIN_HW && !eager()) continue;
+      if (wino_pool_split(st(pb), pl, reader(pl.out, i + 1))) continue;
       const int pout = pl.out;
       const int64_t Hp = val(pout).dims[2], Wp = val(pout).dims[3];
       const int pes = val(pout).es;
@@ -970,16 +995,7 @@ struct Planner {
       const int ci = reader(v, i + 1);
       if (ci < 0) continue;
       Step& cv = st(ci);
-      if (cv.kind != S_CONV || cv.pool || cv.epool || cv.in0 != v || cv.kh != 1 || cv.kw != 1 || cv.sh != 1 ||
-          cv.sw != 1 || cv.win.pt || cv.win.pl || cv.plan.f16 || cv.plan.x3 || cv.plan.wino || cv.M > 64 || cv.C % 32 ||
-          pl.win.Wo > 16 || pl.win.pt > 2 || pl.win.pl > 2)
-        continue;
-      PoolConvParams q{};  // pool_conv1x1_f32_kernel's own limits (run_conv_pool has no other kernel)
-      q.C = int(cv.C); q.H = int(pl.H); q.W = int(pl.W); q.Hp = int(pl.win.Ho); q.Wp = int(pl.win.Wo);
-      q.pt = int(pl.win.pt); q.pl = int(pl.win.pl); q.M = int(cv.M); q.Mp = cv.plan.Mp; q.Kp = cv.plan.krows;
-      q.N = 1; q.x_ps = int(pl.H * pl.W); q.y_ps = int(pl.win.Ho * pl.win.Wo);
-      q.x_nstride = int64_t(q.C) * q.x_ps; q.y_nstride = int64_t(q.M) * q.y_ps;
-      if (!pool_conv1x1_f32_eligible(q)) continue;
+      if (cv.in0 != v || !pool_squeeze_fits(pl, cv)) continue;
       cv.pool = true;
       cv.in0 = pl.in0;
       cv.pH = pl.H; cv.pW = pl.W; cv.psh = pl.sh; cv.psw = pl.sw; cv.pwin = pl.win;

@@ -3,9 +3,9 @@
 // the walker used to run maxpool_kernel (382 MB in, 95 MB out at B = 256) and then the squeeze
 // (95 MB in again)).  The pooled map never reaches HBM.
 //
-// One workgroup = PS_PR (2) pooled rows of one image (Wp <= 16 columns each: one 16-pixel fragment
-// per row) x all M <= 64 output channels (four waves x 16 channels, v_mfma_f32_16x16x4_f32).  Per
-// chunk of PS_CH (16) input channels:
+// One workgroup = PS_PR (2) pooled rows of one image (Wp <= 16 NF columns each: NF 16-pixel
+// fragments per row; NF = 1 for pool5's 13 columns, 2 for pool3's 27) x all M <= 64 output channels
+// (four waves x 16 channels, v_mfma_f32_16x16x4_f32).  Per chunk of PS_CH (16) input channels:
 //   * the 2 PS_PR + 1 input rows the pooled rows read (whole rows) go global -> registers
 //     -> LDS, raw buffer loads with outside-the-image offsets reading 0 (maxpool_kernel's zero
 //     padding); the next chunk's loads are in flight while this one pools and multiplies;
@@ -34,14 +34,16 @@ typedef float ps4 __attribute__((ext_vector_type(4)));
 #endif
 constexpr int PS_PR = ORE_PS_PR, PS_CH = ORE_PS_CH;
 constexpr int PS_ROWS = 2 * PS_PR + 1;  // input rows of PS_PR pooled rows (3x3, stride 2)
-constexpr int PS_WMAX = 33;             // input columns held per row (Wp <= 16)
-constexpr int PS_IN = PS_CH * PS_ROWS * PS_WMAX;  // floats of one staged chunk
-constexpr int PS_NQ = (PS_IN + 255) / 256;
-constexpr int PS_PX = 16 * PS_PR;       // pooled pixels (16 per row) of a workgroup
 
+template <int NF>  // 16-pixel fragments per pooled row (Wp <= 16 NF)
 __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p) {
+  constexpr int PS_WMAX = 32 * NF + 1;              // input columns held per row
+  constexpr int PS_IN = PS_CH * PS_ROWS * PS_WMAX;  // floats of one staged chunk
+  constexpr int PS_NQ = (PS_IN + 255) / 256;
+  constexpr int PS_RW = 16 * NF;                    // pooled pixels held per row
+  constexpr int PS_PX = PS_RW * PS_PR;              // pooled pixels of a workgroup
   __shared__ float in_s[PS_IN];            // [ch][row][col]
-  __shared__ float pt[PS_CH][PS_PX + 1];   // pooled block [ch][pixel n * 16 + col] (+1 pad)
+  __shared__ float pt[PS_CH][PS_PX + 1];   // pooled block [ch][pixel n * PS_RW + col] (+1 pad)
   const int tid = threadIdx.x, lane = tid & 63, lk = lane >> 4, lj = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bands = (p.Hp + PS_PR - 1) / PS_PR;
@@ -78,9 +80,9 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  ps4 acc[PS_PR];  // rows 4 lk + e of channels 16 wave .., pixel lj of pooled row n
+  ps4 acc[PS_PR * NF];  // rows 4 lk + e of channels 16 wave .., pixel 16 fr + lj of pooled row n
 #pragma unroll
-  for (int n = 0; n < PS_PR; ++n) acc[n] = ps4{0.f, 0.f, 0.f, 0.f};
+  for (int n = 0; n < PS_PR * NF; ++n) acc[n] = ps4{0.f, 0.f, 0.f, 0.f};
   const int nch = p.C / PS_CH;
   const int m0 = 16 * wave;
   // the squeeze's A values of a chunk (k = PS_CH ci + 4 t + lk, row m0 + lj), one chunk ahead
@@ -104,9 +106,9 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
       load_chunk((ci + 1) * PS_CH);
       load_a(anxt, ci + 1);
     }
-    // pooled maxima: channels x PS_PR rows x 16 columns (columns >= Wp: column 0's value, unused)
+    // pooled maxima: channels x PS_PR rows x PS_RW columns (columns >= Wp: column 0's value, unused)
     for (int t = tid; t < PS_CH * PS_PX; t += 256) {
-      const int c = t / PS_PX, pxi = t - c * PS_PX, n = pxi >> 4, col = pxi & 15, cl = col < p.Wp ? col : 0;
+      const int c = t / PS_PX, pxi = t - c * PS_PX, n = pxi / PS_RW, col = pxi - n * PS_RW, cl = col < p.Wp ? col : 0;
       const float* base = in_s + (c * PS_ROWS + 2 * n) * PS_WMAX + 2 * cl;
       float m = -FLT_MAX;
 #pragma unroll
@@ -121,18 +123,19 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
 #pragma unroll
       for (int t = 0; t < KS; ++t)
 #pragma unroll
-        for (int n = 0; n < PS_PR; ++n)
+        for (int n = 0; n < PS_PR * NF; ++n)
           acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(acur[t], pt[4 * t + lk][16 * n + lj], acc[n], 0, 0, 0);
     }
 #pragma unroll
     for (int t = 0; t < KS; ++t) acur[t] = anxt[t];
   }
-  // bias + Relu, NCHW stores: channel m0 + 4 lk + e, pooled pixel (pr0 + n, lj)
-  if (m0 >= p.M || lj >= p.Wp) return;
+  // bias + Relu, NCHW stores: channel m0 + 4 lk + e, pooled pixel (pr0 + n / NF, 16 (n % NF) + lj)
+  if (m0 >= p.M) return;
 #pragma unroll
-  for (int n = 0; n < PS_PR; ++n) {
-    if (pr0 + n >= p.Hp) continue;
-    float* yp = p.y + (long long)img * p.y_nstride + (pr0 + n) * p.Wp + lj;
+  for (int n = 0; n < PS_PR * NF; ++n) {
+    const int prow = pr0 + n / NF, pcol = 16 * (n % NF) + lj;
+    if (prow >= p.Hp || pcol >= p.Wp) continue;
+    float* yp = p.y + (long long)img * p.y_nstride + prow * p.Wp + pcol;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int m = m0 + 4 * lk + e;
@@ -147,15 +150,18 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
 }  // namespace
 
 bool pool_conv1x1_f32_eligible(const PoolConvParams& p) {
-  return p.C % PS_CH == 0 && p.C > 0 && p.M >= 1 && p.M <= 64 && p.Wp >= 1 && p.Wp <= 16 && p.Hp >= 1 &&
-         2 * (p.Wp - 1) + 3 <= PS_WMAX && p.pt >= 0 && p.pl >= 0 && p.pt <= 2 && p.pl <= 2 && p.x_ps >= p.H * p.W &&
+  return p.C % PS_CH == 0 && p.C > 0 && p.M >= 1 && p.M <= 64 && p.Wp >= 1 && p.Wp <= 32 && p.Hp >= 1 &&
+         p.pt >= 0 && p.pl >= 0 && p.pt <= 2 && p.pl <= 2 && p.x_ps >= p.H * p.W &&
          (long long)p.C * p.x_ps * 4 < (1LL << 31) && (long long)p.Kp * p.Mp * 4 < (1LL << 31) && p.Kp >= p.C &&
          p.Mp >= p.M && p.y_ps >= p.Hp * p.Wp;
 }
 
 void launch_pool_conv1x1_f32(const PoolConvParams& p, hipStream_t s) {
   const long long grid = (long long)p.N * ((p.Hp + PS_PR - 1) / PS_PR);
-  hipLaunchKernelGGL(pool_conv1x1_f32_kernel, dim3((unsigned)grid), dim3(256), 0, s, p);
+  if (p.Wp <= 16)
+    hipLaunchKernelGGL(pool_conv1x1_f32_kernel<1>, dim3((unsigned)grid), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(pool_conv1x1_f32_kernel<2>, dim3((unsigned)grid), dim3(256), 0, s, p);
 }
 
 }  // namespace ore

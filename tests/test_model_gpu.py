@@ -755,6 +755,8 @@ def _pool_squeeze_model(C, H, W, M, pool_pads, relu=True):
     (512, 27, 27, 64, [0, 0, 0, 0], True),   # SqueezeNet pool5 + fire9/squeeze1x1
     (64, 20, 31, 48, [0, 0, 1, 1], True),    # ceil-mode pads, 16 pooled columns, M = 48
     (32, 9, 7, 10, [1, 1, 1, 1], False),     # padded on all sides, no Relu (negative outputs), M = 10
+    (256, 54, 54, 32, [0, 0, 1, 1], True),   # SqueezeNet pool3 + fire5/squeeze1x1: 27 pooled columns (2 fragments)
+    (64, 40, 61, 24, [1, 1, 1, 1], False),   # 31 pooled columns, padded on all sides
 ])
 def test_pool_squeeze_fused_bit_identical(gpu_ctx, case):
     """f32: a 3x3 / stride-2 MaxPool and the 1x1 conv that is its only reader in one launch
