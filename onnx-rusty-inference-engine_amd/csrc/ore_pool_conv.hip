@@ -7,8 +7,9 @@
 // fragments per row; NF = 1 for pool5's 13 columns, 2 for pool3's 27) x all M <= 64 output channels
 // (four waves x 16 channels, v_mfma_f32_16x16x4_f32).  Per chunk of PS_CH (16) input channels:
 //   * the 2 PS_PR + 1 input rows the pooled rows read (whole rows) go global -> registers
-//     -> LDS, raw buffer loads with outside-the-image offsets reading 0 (maxpool_kernel's zero
-//     padding); the next chunk's loads are in flight while this one pools and multiplies;
+//     -> LDS as 16-B groups (4-B aligned raw buffer loads; rows outside the image read 0 past the
+//     records, columns outside it are zeros in LDS: maxpool_kernel's zero padding); the next
+//     chunk's loads are in flight while this one pools and multiplies;
 //   * every thread takes (pooled pixel, channel) maxima from -FLT_MAX over the nine window values
 //     (maxpool_kernel's arithmetic) into an LDS block [channels][16 PS_PR pixels];
 //   * each wave runs the chunk's k-steps (k = channel, ascending over the chunks: the standalone
@@ -37,12 +38,16 @@ constexpr int PS_ROWS = 2 * PS_PR + 1;  // input rows of PS_PR pooled rows (3x3,
 
 template <int NF>  // 16-pixel fragments per pooled row (Wp <= 16 NF)
 __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p) {
-  constexpr int PS_WMAX = 32 * NF + 1;              // input columns held per row
-  constexpr int PS_IN = PS_CH * PS_ROWS * PS_WMAX;  // floats of one staged chunk
-  constexpr int PS_NQ = (PS_IN + 255) / 256;
-  constexpr int PS_RW = 16 * NF;                    // pooled pixels held per row
-  constexpr int PS_PX = PS_RW * PS_PR;              // pooled pixels of a workgroup
-  __shared__ float in_s[PS_IN];            // [ch][row][col]
+  // staged rows: input column iw at LDS column iw + PS_LC; columns left of the image and right of
+  // the loaded 16-B groups are zero once (never written), loaded columns >= W are zeroed per element
+  constexpr int PS_LC = 4;
+  constexpr int PS_NQMAX = (32 * NF + 1 + 3) / 4;             // 16-B groups of the widest row
+  constexpr int PS_RS = PS_LC + 4 * PS_NQMAX + 4;            // LDS row stride (floats, 16-B multiple)
+  constexpr int PS_IN = PS_CH * PS_ROWS * PS_RS;             // floats of one staged chunk
+  constexpr int PS_NQ = (PS_CH * PS_ROWS * PS_NQMAX + 255) / 256;  // 16-B loads per thread per chunk
+  constexpr int PS_RW = 16 * NF;                             // pooled pixels held per row
+  constexpr int PS_PX = PS_RW * PS_PR;                       // pooled pixels of a workgroup
+  __shared__ __attribute__((aligned(16))) float in_s[PS_IN];  // [ch][row][col]
   __shared__ float pt[PS_CH][PS_PX + 1];   // pooled block [ch][pixel n * PS_RW + col] (+1 pad)
   const int tid = threadIdx.x, lane = tid & 63, lk = lane >> 4, lj = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -53,30 +58,38 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
   const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
   const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
   const int img = wgid / bands, pr0 = (wgid - img * bands) * PS_PR;
-  const int ih0 = pr0 * 2 - p.pt, iw0 = -p.pl;  // input coordinates of staged (row 0, col 0)
-  const int wcols = 2 * (p.Wp - 1) + 3;         // input columns the pooled row reads
+  const int ih0 = pr0 * 2 - p.pt;  // input row of staged row 0
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(p.x + (long long)img * p.x_nstride), (short)0, p.C * p.x_ps * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0, p.Kp * p.Mp * 4, 0x00020000);
+  for (int i = tid; i < PS_IN; i += 256) in_s[i] = 0.0f;
 
-  // this thread's staged elements q = tid + 256 u: (channel, row, column) -> byte offset in the
-  // image minus the chunk's channel offset (or past the records: 0)
-  int qo[PS_NQ];
+  // this thread's 16-B groups q = tid + 256 u: (channel, row, group j) -> byte offset in the image
+  // minus the chunk's channel offset (rows outside the image: past the records, 0), LDS float offset
+  // and the mask of the group's elements inside the row (a group may run into the next row)
+  const int nq = (p.W + 3) / 4, nld = PS_CH * PS_ROWS * nq;
+  int qo[PS_NQ], qs[PS_NQ];
+  unsigned qm[PS_NQ];
 #pragma unroll
   for (int u = 0; u < PS_NQ; ++u) {
     const int q = tid + 256 * u;
-    const int c = q / (PS_ROWS * PS_WMAX), rc = q - c * (PS_ROWS * PS_WMAX), r = rc / PS_WMAX, cc = rc - r * PS_WMAX;
-    const int ih = ih0 + r, iw = iw0 + cc;
-    const bool in = q < PS_IN && cc < wcols && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-    qo[u] = in ? (c * p.x_ps + ih * p.W + iw) * 4 : (int)0x80000000;
+    const int c = q / (PS_ROWS * nq), rc = q - c * (PS_ROWS * nq), r = rc / nq, j = rc - r * nq;
+    const int ih = ih0 + r;
+    const bool rin = (unsigned)ih < (unsigned)p.H;
+    qo[u] = q < nld ? (rin ? (c * p.x_ps + ih * p.W + 4 * j) * 4 : (int)0x80000000) : -1;
+    qs[u] = (c * PS_ROWS + r) * PS_RS + PS_LC + 4 * j;
+    unsigned mk = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) mk |= (4 * j + e < p.W ? 1u : 0u) << e;
+    qm[u] = mk;
   }
-  float xv[PS_NQ];
+  ps4 xv[PS_NQ];
   auto load_chunk = [&](int c0) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < PS_NQ; ++u)
-      xv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                            xr, qo[u] < 0 ? (int)0x80000000 : qo[u] + c0 * p.x_ps * 4, 0, 0));
+      xv[u] = __builtin_bit_cast(ps4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          xr, qo[u] < 0 ? (int)0x80000000 : qo[u] + c0 * p.x_ps * 4, 0, 0));
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -99,8 +112,13 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
   for (int ci = 0; ci < nch; ++ci) {
     __syncthreads();  // the previous chunk's staged rows are pooled
 #pragma unroll
-    for (int u = 0; u < PS_NQ; ++u)
-      if (tid + 256 * u < PS_IN) in_s[tid + 256 * u] = xv[u];
+    for (int u = 0; u < PS_NQ; ++u) {
+      if (qo[u] == -1) continue;  // no group
+      ps4 v = xv[u];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (qm[u] >> e) & 1 ? v[e] : 0.0f;
+      *reinterpret_cast<ps4*>(in_s + qs[u]) = v;
+    }
     __syncthreads();
     if (ci + 1 < nch) {  // in flight during this chunk
       load_chunk((ci + 1) * PS_CH);
@@ -109,12 +127,12 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
     // pooled maxima: channels x PS_PR rows x PS_RW columns (columns >= Wp: column 0's value, unused)
     for (int t = tid; t < PS_CH * PS_PX; t += 256) {
       const int c = t / PS_PX, pxi = t - c * PS_PX, n = pxi / PS_RW, col = pxi - n * PS_RW, cl = col < p.Wp ? col : 0;
-      const float* base = in_s + (c * PS_ROWS + 2 * n) * PS_WMAX + 2 * cl;
+      const float* base = in_s + (c * PS_ROWS + 2 * n) * PS_RS + PS_LC + 2 * cl - p.pl;
       float m = -FLT_MAX;
 #pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
-        for (int s = 0; s < 3; ++s) m = fmaxf(m, base[r * PS_WMAX + s]);
+        for (int s = 0; s < 3; ++s) m = fmaxf(m, base[r * PS_RS + s]);
       pt[c][pxi] = m;
     }
     __syncthreads();
@@ -151,6 +169,7 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
 
 bool pool_conv1x1_f32_eligible(const PoolConvParams& p) {
   return p.C % PS_CH == 0 && p.C > 0 && p.M >= 1 && p.M <= 64 && p.Wp >= 1 && p.Wp <= 32 && p.Hp >= 1 &&
+         p.W <= 2 * (p.Wp <= 16 ? 16 : 32) + 1 && 2 * (p.Wp - 1) + 2 - p.pl <= p.W + 1 &&
          p.pt >= 0 && p.pl >= 0 && p.pt <= 2 && p.pl <= 2 && p.x_ps >= p.H * p.W &&
          (long long)p.C * p.x_ps * 4 < (1LL << 31) && (long long)p.Kp * p.Mp * 4 < (1LL << 31) && p.Kp >= p.C &&
          p.Mp >= p.M && p.y_ps >= p.Hp * p.Wp;
