@@ -71,21 +71,28 @@ def roofline_8d(infos, per_step_ms, ms_per_step, peak_tflops, peak_gbs=PEAK_HBM_
     FLOPs / MFMA peak, algorithmic bytes / HBM peak); achieved fraction = bound_time / measured time,
     per launch, per op class and for the whole network (against the timed ms_per_step, launch gaps
     included).  `issued` beside it counts the MFMA FLOPs the kernels execute (Winograd issues 16 C M
-    per 2x2 tile, not the direct 36 C M): the Winograd-honest use of the matrix cores."""
+    per 2x2 tile, not the direct 36 C M): the Winograd-honest use of the matrix cores; issued_frac is
+    the same fraction with that work as the FLOP bound (a Winograd layer's `frac` can exceed 1, its
+    issued_frac cannot)."""
     steps, classes = [], {}
-    tot_bound = 0.0
+    tot_bound = tot_ibound = 0.0
     for info, ms in zip(infos, per_step_ms):
         t_f = info["flops"] / (peak_tflops * 1e12) * 1e3
+        t_i = info.get("mfma_flops", info["flops"]) / (peak_tflops * 1e12) * 1e3  # MFMA work issued
         t_b = info["bytes"] / (peak_gbs * 1e9) * 1e3
-        bound = max(t_f, t_b)
+        bound, ibound = max(t_f, t_b), max(t_i, t_b)
         tot_bound += bound
+        tot_ibound += ibound
         kind = "mfma" if t_f >= t_b else "hbm"
         steps.append({"name": info["name"], "op": info["op"], "bound": kind, "us": round(1000 * float(ms), 1),
-                      "bound_us": round(1000 * bound, 1), "frac": round(bound / max(float(ms), 1e-9), 3)})
-        c = classes.setdefault(info["op"], {"ms": 0.0, "bound_ms": 0.0, "flops": 0.0, "mfma_flops": 0.0, "bytes": 0.0,
-                                            "launches": 0})
+                      "bound_us": round(1000 * bound, 1), "frac": round(bound / max(float(ms), 1e-9), 3),
+                      "issued_bound_us": round(1000 * ibound, 1),
+                      "issued_frac": round(ibound / max(float(ms), 1e-9), 3)})
+        c = classes.setdefault(info["op"], {"ms": 0.0, "bound_ms": 0.0, "ibound_ms": 0.0, "flops": 0.0,
+                                            "mfma_flops": 0.0, "bytes": 0.0, "launches": 0})
         c["ms"] += float(ms)
         c["bound_ms"] += bound
+        c["ibound_ms"] += ibound
         c["flops"] += info["flops"]
         c["mfma_flops"] += info.get("mfma_flops", info["flops"])
         c["bytes"] += info["bytes"]
@@ -94,12 +101,15 @@ def roofline_8d(infos, per_step_ms, ms_per_step, peak_tflops, peak_gbs=PEAK_HBM_
     for k, c in classes.items():
         per_class[k] = {"launches": c["launches"], "ms": round(c["ms"], 4), "bound_ms": round(c["bound_ms"], 4),
                         "frac": round(c["bound_ms"] / max(c["ms"], 1e-9), 4),
+                        "issued_bound_ms": round(c["ibound_ms"], 4),
+                        "issued_frac": round(c["ibound_ms"] / max(c["ms"], 1e-9), 4),
                         "TFLOP/s": round(c["flops"] / (c["ms"] * 1e-3) / 1e12, 2) if c["flops"] else None,
                         "issued_TFLOP/s": round(c["mfma_flops"] / (c["ms"] * 1e-3) / 1e12, 2) if c["flops"] else None,
                         "GB/s": round(c["bytes"] / (c["ms"] * 1e-3) / 1e9, 1)}
     return {"peaks": {"mfma_TFLOP/s": peak_tflops, "hbm_GB/s": peak_gbs},
             "network": {"bound_ms": round(tot_bound, 4), "ms_per_step": round(ms_per_step, 4),
                         "frac": round(tot_bound / ms_per_step, 4),
+                        "issued_bound_ms": round(tot_ibound, 4), "issued_frac": round(tot_ibound / ms_per_step, 4),
                         "kernel_ms": round(float(sum(per_step_ms)), 4)},
             "per_class": per_class, "per_launch": steps}, classes
 
@@ -337,10 +347,10 @@ def main():
                      "conv_f16_kernel (implicit GEMM), all MFMA 32x32x16 f16 with f32 accumulate" if f16 else
                      "conv_x3_kernel (f32 implicit GEMM on MFMA 16x16x32 bf16: both operands split exactly into "
                      "3 bf16 parts, 6 part products per f32 MAC; peak = 2500 / 6 TFLOP/s of f32 work" if x3 else
-                     "Conv class: conv_stream_kernel (LDS-free implicit GEMM, MFMA 16x16x4 f32), fire_kernel (fire "
-                     "module + next squeeze), fire_pool_kernel (fire4 + pool3 + fire5 squeeze), "
-                     "conv_win_pool_f32_kernel (conv1 + pool1 + fire2 squeeze), pool_conv1x1_f32_kernel (pool5 + "
-                     "fire9 squeeze), conv_wino32/16_kernel (Winograd F(2x2,3x3) expand3x3) and "
+                     "Conv class: conv_win_pool_f32_kernel (conv1 + pool1 + fire2 squeeze), fire_kernel (fire "
+                     "module + next squeeze), conv_winol_kernel (Winograd F(2x2,3x3) expand3x3, LDS-staged, MFMA "
+                     "16x16x4 f32), conv_stream_kernel / conv_stream1x1_persist_kernel (LDS-free implicit GEMM, "
+                     "MFMA 16x16x4 f32), pool_conv1x1_f32_kernel (pool3 / pool5 + the next squeeze) and "
                      "conv_gemm_kernel (LDS-staged, MFMA 32x32x2 f32) per the autotuned tile") + f", {conv['launches']} launches/step)"
             # HBM bytes per conv launch from the PMC passes of tools/pmc.sh (FETCH_SIZE x2 +
             # WRITE_SIZE, separate --pmc runs; counters cannot be read inside this timed run)
