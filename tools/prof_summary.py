@@ -11,7 +11,7 @@ import json
 import os
 import sys
 
-CLASSES = [("conv (f32 MFMA)", ("conv_gemm_kernel", "conv_stream_kernel", "fire_kernel", "conv_pool_stream_kernel",
+CLASSES = [("conv (f32 MFMA)", ("conv_gemm_kernel", "conv_stream_kernel", "conv_stream1x1_persist_kernel", "fire_kernel", "conv_pool_stream_kernel",
                                 "conv_wino32_kernel", "conv_wino16_kernel", "conv_winol_kernel", "fire_wino_kernel",
                                 "conv_win_pool_f32_kernel", "fire_pool_kernel", "pool_conv1x1_f32_kernel")),
            ("conv (f16 MFMA)", ("conv_f16_kernel", "conv_f16_dma_kernel", "conv_f16_epool", "fire_f16_kernel",
