@@ -18,8 +18,9 @@
 //   * per channel fragment the conv values (bias, Relu, f16; 0 outside the conv plane) go to an LDS
 //     tile [pixel][32 channels] and each (pooled output, 8 channels) takes its 3x3 max from -FLT_MAX
 //     in f32 (the EP kernel's arithmetic) and leaves by one 16-B NHWC store.
-// Same operands (the PAIR padding tap zeroed as the gather does), same k order, same MFMA chain and
-// epilogue as the two-launch path: bit-identical output (tests/test_f16_gpu.py).
+// Same operands (the PAIR padding tap meets a zero weight; the gather path zeroes the operand too:
+// zero products either way), same k order, same MFMA chain and epilogue as the two-launch path:
+// bit-identical output (tests/test_f16_gpu.py).
 #include <float.h>
 #include <hip/hip_runtime.h>
 
@@ -34,11 +35,46 @@ namespace {
 typedef _Float16 c1h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 c1h4 __attribute__((ext_vector_type(4)));
 typedef float c1f16 __attribute__((ext_vector_type(16)));
-
 constexpr int C1_PR = EPOOL_TILE_PR, C1_PC = EPOOL_TILE_PC;                // pooled outputs per tile
 constexpr int C1_RC = 2 * C1_PR + 1, C1_CC = 2 * C1_PC + 1, C1_NPX = C1_RC * C1_CC;  // conv patch (13 x 19)
 constexpr int C1_TS = 40;                                                  // conv tile pixel stride (halves)
 static_assert(C1_NPX <= 256, "one 256-pixel patch per tile (8 fragments)");
+
+typedef unsigned short c1u8 __attribute__((ext_vector_type(8)));
+
+// 3x3 max of 8 channels of conv-tile pixels (row stride C1_CC pixels of C1_TS halves) from -FLT_MAX in
+// f32 (the separate pool's arithmetic).  After the Relu every value is +0 or positive, so its f16 bits
+// order like the value: the max is then 4 v_pk_max_u16 per tap on the raw bits (exact; the f32 route
+// costs 8 conversions and 8 maxima per tap)
+__device__ __forceinline__ c1h8 c1_pool8(const _Float16* base, bool relu) {
+  if (relu) {
+    c1u8 m = __builtin_bit_cast(c1u8, *reinterpret_cast<const c1h8*>(base));
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+        if (r || s)
+          m = __builtin_elementwise_max(m, __builtin_bit_cast(c1u8, *reinterpret_cast<const c1h8*>(
+                                                                   base + (r * C1_CC + s) * C1_TS)));
+    return __builtin_bit_cast(c1h8, m);
+  }
+  float mx[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) mx[e] = -FLT_MAX;
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const c1h8 v = *reinterpret_cast<const c1h8*>(base + (r * C1_CC + s) * C1_TS);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], (float)v[e]);
+    }
+  c1h8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = (_Float16)mx[e];
+  return o;
+}
+
 
 struct C1Geom {
   int KS;      // k-steps of 16
@@ -180,16 +216,13 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
         for (int e = 0; e < 16; ++e) acc[i][f][e] = 0.0f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
+      // the padding tap s + 1 = KW (odd KW) is read as it lies in the window (a finite value: image
+      // data or an outside-the-image zero) and meets a zero weight (pack_weights_f16_kernel): its
+      // products are zeros, as the gather path's zeroed operand gives
       const int pair = 2 * ks + h, tap = 2 * pair, r = tap / KWP, s = tap - r * KWP;
-      const bool pad1 = s + 1 >= KW;
       c1h8 b[2];
 #pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        b[f] = *reinterpret_cast<const c1h8*>(halo + bofs[f] + (r * HC + s) * 4);
-        if (pad1) {
-          b[f][4] = b[f][5] = b[f][6] = b[f][7] = (_Float16)0.0f;
-        }
-      }
+      for (int f = 0; f < 2; ++f) b[f] = *reinterpret_cast<const c1h8*>(halo + bofs[f] + (r * HC + s) * 4);
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
         const c1h8 a = *reinterpret_cast<const c1h8*>(Ws + ((ks * MF + i) * 32 + lr) * 16 + 8 * h);
@@ -234,9 +267,10 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
           for (int e = 0; e < 8; ++e) {
             float v = acc[i][f][8 * g + e] + bv[8 * g + e];
             if (p.relu) v = fmaxf(v, 0.0f);
-            o[e] = cok ? (_Float16)v : (_Float16)0.0f;
+            o[e] = (_Float16)v;
           }
-          *reinterpret_cast<c1h8*>(ct + tpx[f] + 16 * g) = o;
+          const c1h8 zero = {};
+          *reinterpret_cast<c1h8*>(ct + tpx[f] + 16 * g) = cok ? o : zero;  // 0 outside the conv plane
         }
       }
       __syncthreads();
@@ -245,21 +279,8 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
         {  // every thread: one (pooled pixel, 8 channels) of the 64 x 32 block (pixels >= 54: pixel 0)
           const int k = tid >> 2, cg = tid & 3, kc = k < C1_PR * C1_PC ? k : 0;
           const int a = kc / C1_PC, b = kc - a * C1_PC;
-          float mx[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) mx[e] = -FLT_MAX;
-#pragma unroll
-          for (int r = 0; r < 3; ++r)
-#pragma unroll
-            for (int s = 0; s < 3; ++s) {
-              const c1h8 v = *reinterpret_cast<const c1h8*>(ct + ((2 * a + r) * C1_CC + 2 * b + s) * C1_TS + cg * 8);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], (float)v[e]);
-            }
-          c1h8 o;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = (_Float16)mx[e];
-          *reinterpret_cast<c1h8*>(pt + k * C1_TS + cg * 8) = o;
+          *reinterpret_cast<c1h8*>(pt + k * C1_TS + cg * 8) =
+              c1_pool8(ct + ((2 * a) * C1_CC + 2 * b) * C1_TS + cg * 8, p.relu != 0);
         }
         __syncthreads();
         if (wave < 2) {
@@ -278,24 +299,10 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
 #endif
         const int pp = tid >> 2, cg = tid & 3;
         const int a = pp / C1_PC, b = pp - a * C1_PC;
-        float mx[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) mx[e] = -FLT_MAX;
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int s = 0; s < 3; ++s) {
-            const c1h8 v = *reinterpret_cast<const c1h8*>(ct + ((2 * a + r) * C1_CC + 2 * b + s) * C1_TS + cg * 8);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], (float)v[e]);
-          }
+        const c1h8 o = c1_pool8(ct + ((2 * a) * C1_CC + 2 * b) * C1_TS + cg * 8, p.relu != 0);
         const int ph = ph0 + a, pw = pw0 + b, m = 32 * i + cg * 8;
-        if (ph < p.ep_Ho && pw < p.ep_Wo && m < p.M) {
-          c1h8 o;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = (_Float16)mx[e];
+        if (ph < p.ep_Ho && pw < p.ep_Wo && m < p.M)
           *reinterpret_cast<c1h8*>(y + (long long)img * p.y_nstride + (ph * p.ep_Wo + pw) * p.y_ps + m) = o;
-        }
       }
       if (i + 1 < MF) __syncthreads();  // the conv tile is rewritten by the next fragment
     }

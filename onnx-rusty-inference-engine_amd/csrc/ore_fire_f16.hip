@@ -40,6 +40,7 @@ namespace {
 
 typedef _Float16 fh8 __attribute__((ext_vector_type(8)));
 typedef float ff16 __attribute__((ext_vector_type(16)));
+typedef unsigned short fu8 __attribute__((ext_vector_type(8)));
 
 constexpr int FF_PIX = 256;  // pixels per workgroup
 
@@ -345,23 +346,20 @@ __global__ __launch_bounds__(256, 2) void fire_pool_f16_kernel(FireF16Params p) 
         for (int i = 0; i < MSF; ++i) aq[t][i] = ld_g(ws + ((cat0 / 16 + t) * p.Msp + 32 * i) * 16 + arow);
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
-        float m[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) m[e] = -FLT_MAX;
+        // the 3x3 max (from -FLT_MAX in f32 in the separate pool, window taps outside the image read
+        // as 0): after the Relu every value is +0 or positive and its f16 bits order like the value,
+        // so the max is v_pk_max_u16 on the raw bits from +0 (exact; no f32 round trip)
+        fu8 m = {};
 #pragma unroll
         for (int r = 0; r < 3; ++r)
 #pragma unroll
           for (int s = 0; s < 3; ++s) {
             const int ih = ih0 + r, iw = iw0 + s;
-            fh8 v = {};
             if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-              v = ld_s(tile + ((ih - cr0) * W + iw) * TS + 16 * g + 8 * h);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], (float)v[e]);
+              m = __builtin_elementwise_max(
+                  m, __builtin_bit_cast(fu8, ld_s(tile + ((ih - cr0) * W + iw) * TS + 16 * g + 8 * h)));
           }
-        fh8 bq;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) bq[e] = (_Float16)m[e];
+        const fh8 bq = __builtin_bit_cast(fh8, m);
 #pragma unroll
         for (int i = 0; i < MSF; ++i) sacc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aq[g][i], bq, sacc[i][0], 0, 0, 0);
       }
