@@ -82,12 +82,21 @@ struct C1Geom {
   int w_halves, halo_halves, lds_bytes;
 };
 
+// A fragments: staged in LDS once per persistent workgroup (default), or read from L2 per k-step
+// (-DORE_EXP_C1_WL2, a timing experiment: three workgroups per CU instead of two by LDS, but 158
+// VGPRs; measured 236 vs 179 us for conv1 + pool1 + squeeze at B = 256)
+#ifdef ORE_EXP_C1_WL2
+constexpr bool C1_WLDS = false;
+#else
+constexpr bool C1_WLDS = true;
+#endif
+
 __host__ __device__ inline C1Geom c1_geom(int MF, int kh, int kwp, int sh, int sw, bool sq = false) {
   C1Geom g;
   g.KS = kh * kwp * 4 / 16;
   g.hr = (C1_RC - 1) * sh + kh;
   g.hc = (C1_CC - 1) * sw + kwp;
-  g.w_halves = g.KS * MF * 32 * 16;
+  g.w_halves = C1_WLDS ? g.KS * MF * 32 * 16 : 0;
   g.halo_halves = (g.hr * g.hc * 4 + 7) / 8 * 8;
   g.lds_bytes = (g.w_halves + g.halo_halves + C1_NPX * C1_TS) * 2 + MF * 32 * 4 + (sq ? 64 * C1_TS * 2 + 32 * 4 : 0);
   return g;
@@ -100,7 +109,7 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
   constexpr int NQ = (HR * HC + 255) / 256;                              // window pixels per thread
   static_assert(KH * KWP % 4 == 0, "whole k-steps");
   extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
-  constexpr int W_HALVES = KS * MF * 32 * 16, HALO_HALVES = (HR * HC * 4 + 7) / 8 * 8;
+  constexpr int W_HALVES = C1_WLDS ? KS * MF * 32 * 16 : 0, HALO_HALVES = (HR * HC * 4 + 7) / 8 * 8;
   _Float16* Ws = smem;                      // [KS][MF * 32][16]
   _Float16* halo = smem + W_HALVES;         // [HR][HC][4]
   _Float16* ct = halo + HALO_HALVES;        // [C1_NPX][C1_TS]
@@ -116,7 +125,7 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
 
   // weights once: LDS row R of each 32-row block <- packed row (R & ~31) + 16 (i >> 1) + 8 hh +
   // 4 (i & 1) + j for R % 32 = 8 i + 4 hh + j (rows past M zero)
-  for (int q = tid; q < KS * MF * 64; q += 256) {
+  for (int q = tid; C1_WLDS && q < KS * MF * 64; q += 256) {
     const int t = q / (MF * 64), rem = q - t * (MF * 64), R = rem >> 1, hh8 = rem & 1;
     const int r = R & 31, i = r >> 3, hq = (r >> 2) & 1, j = r & 3;
     const int m = (R & ~31) + 16 * (i >> 1) + 8 * hq + 4 * (i & 1) + j;
@@ -131,6 +140,15 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
   }
   const _Float16* __restrict__ wq = static_cast<const _Float16*>(sq.w);
 
+  // L2 weights: this lane's packed row of each fragment (the LDS permutation above, row lr of the
+  // fragment), its 8 halves of a k-step at + 16 ks + 8 h; rows past M read a zero row (Mp >= 32 MF)
+  const _Float16* arow_g[MF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    const int r = lr, ii = r >> 3, hq = (r >> 2) & 1, j = r & 3;
+    const int m = 32 * i + 16 * (ii >> 1) + 8 * hq + 4 * (ii & 1) + j;
+    arow_g[i] = wh + (long long)m * Kp + 8 * h;
+  }
   // this lane's two patch pixels (fragments 2 wave, 2 wave + 1)
   int bofs[2], tpx[2];
   bool pin[2];
@@ -214,8 +232,19 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
       for (int f = 0; f < 2; ++f)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][f][e] = 0.0f;
+    c1h8 ag[2][MF];  // L2 weights: k-step ks + 1's fragments in flight during k-step ks
+    if constexpr (!C1_WLDS) {
+#pragma unroll
+      for (int i = 0; i < MF; ++i) ag[0][i] = *reinterpret_cast<const c1h8*>(arow_g[i]);
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
+      if constexpr (!C1_WLDS) {
+        if (ks + 1 < KS) {
+#pragma unroll
+          for (int i = 0; i < MF; ++i) ag[(ks + 1) & 1][i] = *reinterpret_cast<const c1h8*>(arow_g[i] + 16 * (ks + 1));
+        }
+      }
       // the padding tap s + 1 = KW (odd KW) is read as it lies in the window (a finite value: image
       // data or an outside-the-image zero) and meets a zero weight (pack_weights_f16_kernel): its
       // products are zeros, as the gather path's zeroed operand gives
@@ -225,7 +254,7 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
       for (int f = 0; f < 2; ++f) b[f] = *reinterpret_cast<const c1h8*>(halo + bofs[f] + (r * HC + s) * 4);
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
-        const c1h8 a = *reinterpret_cast<const c1h8*>(Ws + ((ks * MF + i) * 32 + lr) * 16 + 8 * h);
+        const c1h8 a = C1_WLDS ? *reinterpret_cast<const c1h8*>(Ws + ((ks * MF + i) * 32 + lr) * 16 + 8 * h) : ag[ks & 1][i];
 #pragma unroll
         for (int f = 0; f < 2; ++f)
 #ifdef ORE_EXP_C1_NOMFMA  // timing experiments only (tools/build_exp.sh)
@@ -366,7 +395,17 @@ void launch_conv_pair_pool_f16(const ConvParams& p, const C1Squeeze* sq, hipStre
     int v = 0;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
   }
-  const unsigned grid = (unsigned)std::min<long long>(tiles, 2LL * ncu);  // persistent: weights staged once
+  // persistent: the workgroups resident at once (two per CU with the weights staged in LDS; registers
+  // and LDS decide without), from the occupancy API
+  int per_cu = 0;
+  {
+    const void* fn = sq ? (MF == 2 ? reinterpret_cast<const void*>(&conv_pair_pool_f16_kernel<2, 7, 7, 2, 1>)
+                                   : reinterpret_cast<const void*>(&conv_pair_pool_f16_kernel<3, 7, 7, 2, 1>))
+                        : reinterpret_cast<const void*>(&conv_pair_pool_f16_kernel<3, 7, 7, 2, 0>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, g.lds_bytes) != hipSuccess || per_cu < 1)
+      per_cu = 2;
+  }
+  const unsigned grid = (unsigned)std::min<long long>(tiles, (long long)per_cu * ncu);
   const C1Squeeze none{};
   if (sq) {
     if (MF == 2) c1_dispatch<2, 1>(p, *sq, grid, g.lds_bytes, s);
