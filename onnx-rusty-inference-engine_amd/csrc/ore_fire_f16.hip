@@ -411,7 +411,6 @@ bool fire_pool_f16_plan(FireF16Params* p) {
   // per F (conv fragments per wave): the largest band whose conv rows fit 128 F pixels, whose pooled
   // pixels fit the 4 waves' squeeze fragments and whose halo + conv tile fit the LDS budget; the
   // shape computing the fewest 32-pixel conv fragments (+ 4 per band: staging, barriers) wins
-  // (ORE_FIRE_POOL_SHAPE=F,PR forces one: experiments)
   long long best = -1;
   for (int F = 2; F <= 4; ++F) {
     int PR = 0;

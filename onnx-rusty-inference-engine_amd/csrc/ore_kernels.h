@@ -169,7 +169,10 @@ struct FireF16Params {
   // (fire_pool_f16_plan)
   int pool, Hp, Wp, ppt, ppl, PR, F;
 };
-constexpr int FIRE_F16_LDS_MAX = 80 * 1024;  // the input halo of one workgroup (two per CU)
+#ifndef ORE_FIRE_F16_LDS_KB
+#define ORE_FIRE_F16_LDS_KB 80  // build knob (timing experiments, tools/build_exp.sh)
+#endif
+constexpr int FIRE_F16_LDS_MAX = ORE_FIRE_F16_LDS_KB * 1024;  // the input halo of one workgroup (two per CU)
 int fire_f16_lds_bytes(int C, int H, int W);
 // pooled variant: picks p->F / p->PR (false: no band shape fits the LDS budget)
 bool fire_pool_f16_plan(FireF16Params* p);
