@@ -42,6 +42,7 @@ def parse():
                     help="skip the per-kernel HIP-event pass (no roofline / breakdown)")
     ap.add_argument("--layers", action="store_true", help="print per-kernel-step times to stderr")
     ap.add_argument("--no-b1", action="store_true", help="skip the batch-1 latency probe")
+    ap.add_argument("--graph", action="store_true", help="time one HIP-graph replay per step instead of plain launches")
     ap.add_argument("--no-autotune", action="store_true", help="keep the heuristic per-layer conv tiles")
     ap.add_argument("--dump-steps", default="", help="write the plan's kernel steps (op, name, flops, bytes) as JSON")
     ap.add_argument("--streams", type=int, default=1,
@@ -237,6 +238,9 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     torch.cuda.set_device(local)
+    # one non-default stream for everything (the model's launches, RCCL, torch ops): HIP-graph
+    # capture needs a capturable stream
+    torch.cuda.set_stream(torch.cuda.Stream(device=local))
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
@@ -278,8 +282,18 @@ def main():
         with open(args.dump_steps, "w") as f:
             json.dump(model.steps(), f)
 
-    def step():
-        model.run_into(x, out)
+    # --graph: the step's kernels as one HIP graph (ore_model_graph_capture), replayed per step.
+    # Measured no faster at B = 256 (69.9 k vs 70.2 k img/s: the 21 launches queue ahead of the GPU),
+    # so the default times plain launches
+    use_graph = args.graph
+    if use_graph:
+        model.capture(x, out)
+
+    def step(graph=use_graph):
+        if graph:
+            model.replay()
+        else:
+            model.run_into(x, out)
         if world > 1:
             parallel.gather_rows_into(gathered, out)
 
@@ -313,7 +327,7 @@ def main():
     if timing:
         model.enable_timing(True)
         for _ in range(args.steps):
-            step()
+            step(graph=False)  # the event hooks run between plain launches
             per_step_ms += np.asarray(model.step_times_ms())  # waits on the step's last event only
         torch.cuda.synchronize()
         model.enable_timing(False)
@@ -330,7 +344,8 @@ def main():
                                    f"inference, batch {B} per GPU, 3x{args.hw}x{args.hw}",
                        "model": "squeezenet1.0-8 topology, synthetic weights", "global_batch": world * B,
                        "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}",
-                       "collective": f"RCCL all_gather of [{B},1000] logits per step" if world > 1 else None},
+                       "collective": f"RCCL all_gather of [{B},1000] logits per step" if world > 1 else None,
+                       "launch": "one HIP-graph replay per step" if use_graph else "plain launches"},
         }
         result["conv_tiles"] = {"autotuned": not args.no_autotune,
                                 "tile_per_conv": [ore.Model.TILE_NAMES[t] for t in model.tiles() if t >= 0]}
