@@ -47,6 +47,30 @@ def test_two_streams_bit_identical(stream_ctx, precision, batch):
     np.testing.assert_array_equal(outs[0], outs[1])
 
 
+def test_two_streams_headline_plan(stream_ctx):
+    """The bench's headline plan (SqueezeNet @224, batch 256, Winograd, the split fire modules whose
+    expand1x1 / Winograd expand3x3 pairs run on two streams): bit-identical to one stream."""
+    import torch
+    import ore
+    from ore import squeezenet
+    ctx, s = stream_ctx
+    mb = squeezenet.build(224)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    x = torch.rand((256, 3, 224, 224), generator=g, device="cuda") * 100.0 - 50.0
+    outs, paired = [], []
+    for streams in (1, 2):
+        m = ore.Model(ctx, mb, max_batch=256)
+        m.set_streams(streams)
+        out = torch.empty((256, m.output_elems), device="cuda")
+        torch.cuda.synchronize()
+        m.run_into(x, out)
+        s.synchronize()
+        outs.append(out.cpu().numpy())
+        m.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("streams", [1, 2])
 def test_graph_replay_matches_run(stream_ctx, streams):
     import torch
