@@ -16,7 +16,7 @@ while read -r GROUP; do
   [ -z "$GROUP" ] && continue
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $GROUP --kernel-trace --output-format csv -d "$OUT/p$i" -o run -- \
-    python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-step-timing --no-b1 --no-f16-line --dump-steps "$OUT/steps.json" ${PMC_BENCH_ARGS:-} > "$OUT/p$i.log" 2>&1
+    python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-step-timing --no-b1 --no-f16-line --streams 1 --dump-steps "$OUT/steps.json" ${PMC_BENCH_ARGS:-} > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "pass $i [$GROUP] rc=$rc"
   case $rc in 124|134|137|139) echo "fatal"; exit $rc;; esac
