@@ -522,10 +522,6 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   const int img1 = t1 / g.TPI, ty1 = (t1 - img1 * g.TPI) / g.TW;
   const int SS = WM_KC * (g.CS + 512);  // floats per stage: [channel][CS] windows, then [channel][4 quads][32 m][4] U
 
-#ifdef ORE_EXP_WM_STAGGER  // experiment: half of the first-round workgroups start later
-  if (blockIdx.x < ORE_EXP_WM_STAGGER && (blockIdx.x & 8))
-    for (int i = 0; i < 2; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
   // the zero blocks (never written by the DMAs)
   if (threadIdx.x < 2 * WM_KC * WM_ZL)
     wm_lds[(threadIdx.x >> 6) * SS + ((threadIdx.x >> 3) & 7) * g.CS + (threadIdx.x & 7)] = 0.0f;
@@ -680,8 +676,10 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
         for (int f = 0; f < 2; ++f)
           acc[4 * q + j][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][q][j], v[4 * q + j], acc[4 * q + j][f], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
+#ifndef ORE_EXP_WM_NOSYNC  // timing experiment only
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk kc + 1 have landed
     __syncthreads();  // ... every wave's, and every wave is done reading stage kc & 1
+#endif
   }
   // lane (lk, lj) of fragment f holds rows 4 lk + e = channel m0 + 16 f + 4 lk + e of tile lj
   float bv[2][4];

@@ -212,3 +212,37 @@ def test_set_conv_algo_rejects_unknown(gpu_ctx):
     import ore
     with pytest.raises(ore.OreError):
         gpu_ctx.set_conv_algo(7)
+
+
+@pytest.mark.parametrize("tile", [None, 4])
+def test_wino_output_past_2gib(gpu_ctx, tile):
+    """A Winograd conv whose output passes 2 GiB (fire8 / expand3x3 geometry at batch 2900: 2.16 GB
+    out, 0.54 GB in): the launch is split into image chunks (32-bit buffer offsets), so the first
+    and the last images equal the same images run on their own, bit for bit."""
+    import torch
+    import ore
+    from _knobs import conv_tile
+    N, C, H, W, M = 2900, 64, 27, 27, 256
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    x = torch.randn((N, C, H, W), generator=g, device="cuda")
+    w = torch.randn((M, C, 3, 3), generator=g, device="cuda") * 0.05
+    b = torch.randn((M,), generator=g, device="cuda") * 0.1
+    assert N * M * H * W * 4 > 2 ** 31
+    gpu_ctx.set_conv_algo(ore.CONV_ALGO_WINOGRAD)
+    try:
+        def conv(t):
+            kw = dict(auto_pad="NOTSET", pads=[1, 1, 1, 1], strides=(1, 1))
+            if tile is None:
+                return ore.convolution(gpu_ctx, t, w, b, **kw)
+            with conv_tile(gpu_ctx, 36 + tile):
+                return ore.convolution(gpu_ctx, t, w, b, **kw)
+        y = conv(x)
+        for sl in (slice(0, 2), slice(N - 3, N)):
+            ys = conv(x[sl].contiguous())
+            torch.cuda.synchronize()
+            assert torch.equal(y[sl], ys)
+        del y
+    finally:
+        gpu_ctx.set_conv_algo(ore.CONV_ALGO_DIRECT)
+        torch.cuda.empty_cache()
