@@ -25,6 +25,12 @@ METRIC = "SqueezeNet-1.0 fp32 images/s at batch 256, 1/2/4/8 MI355X; max-abs dif
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
 PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: f16/bf16 MFMA dense peak (no sparsity)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec peak
+# achievable peaks measured on MI355X by this repo's probes ("measure achievable
+# peaks (copy kernel, MFMA loop) and report both"): tools/peaks.sh (profiles/r01_peaks.txt: dependent-
+# free f32 / f16 MFMA loops) and tools/hbm_probe.hip (profiles/r03k_hbm_probe.txt: 2 GiB streams,
+# best of 4 / 8 / 16 workgroups per CU: read 6.1, write 4.6, copy 5.0 TB/s)
+ACHIEVABLE = {"f32_mfma_TFLOP/s": 143.5, "f16_mfma_TFLOP/s": 2037.6, "hbm_copy_GB/s": 5024.0,
+              "hbm_read_GB/s": 6149.0, "hbm_write_GB/s": 4634.0}
 
 
 def parse():
@@ -69,7 +75,7 @@ def lib_sha256():
         return hashlib.sha256(f.read()).hexdigest()
 
 
-def roofline_8d(infos, per_step_ms, ms_per_step, peak_tflops, peak_gbs=PEAK_HBM_GBS):
+def roofline_8d(infos, per_step_ms, ms_per_step, peak_tflops, peak_gbs=PEAK_HBM_GBS, ach_tflops=None):
     """each launch is bound by its own FLOP:byte ratio, bound_time = max(algorithmic
     FLOPs / MFMA peak, algorithmic bytes / HBM peak); achieved fraction = bound_time / measured time,
     per launch, per op class and for the whole network (against the timed ms_per_step, launch gaps
@@ -78,7 +84,7 @@ def roofline_8d(infos, per_step_ms, ms_per_step, peak_tflops, peak_gbs=PEAK_HBM_
     the same fraction with that work as the FLOP bound (a Winograd layer's `frac` can exceed 1, its
     issued_frac cannot)."""
     steps, classes = [], {}
-    tot_bound = tot_ibound = 0.0
+    tot_bound = tot_ibound = tot_abound = 0.0
     for info, ms in zip(infos, per_step_ms):
         t_f = info["flops"] / (peak_tflops * 1e12) * 1e3
         t_i = info.get("mfma_flops", info["flops"]) / (peak_tflops * 1e12) * 1e3  # MFMA work issued
@@ -86,6 +92,9 @@ def roofline_8d(infos, per_step_ms, ms_per_step, peak_tflops, peak_gbs=PEAK_HBM_
         bound, ibound = max(t_f, t_b), max(t_i, t_b)
         tot_bound += bound
         tot_ibound += ibound
+        if ach_tflops:  # the same issued-work bound against the measured achievable peaks (copy rate)
+            tot_abound += max(info.get("mfma_flops", info["flops"]) / (ach_tflops * 1e12) * 1e3,
+                              info["bytes"] / (ACHIEVABLE["hbm_copy_GB/s"] * 1e9) * 1e3)
         kind = "mfma" if t_f >= t_b else "hbm"
         steps.append({"name": info["name"], "op": info["op"], "bound": kind, "us": round(1000 * float(ms), 1),
                       "bound_us": round(1000 * bound, 1), "frac": round(bound / max(float(ms), 1e-9), 3),
@@ -109,11 +118,18 @@ def roofline_8d(infos, per_step_ms, ms_per_step, peak_tflops, peak_gbs=PEAK_HBM_
                         "TFLOP/s": round(c["flops"] / (c["ms"] * 1e-3) / 1e12, 2) if c["flops"] else None,
                         "issued_TFLOP/s": round(c["mfma_flops"] / (c["ms"] * 1e-3) / 1e12, 2) if c["flops"] else None,
                         "GB/s": round(c["bytes"] / (c["ms"] * 1e-3) / 1e9, 1)}
-    return {"peaks": {"mfma_TFLOP/s": peak_tflops, "hbm_GB/s": peak_gbs},
-            "network": {"bound_ms": round(tot_bound, 4), "ms_per_step": round(ms_per_step, 4),
-                        "frac": round(tot_bound / ms_per_step, 4),
-                        "issued_bound_ms": round(tot_ibound, 4), "issued_frac": round(tot_ibound / ms_per_step, 4),
-                        "kernel_ms": round(float(sum(per_step_ms)), 4)},
+    net = {"bound_ms": round(tot_bound, 4), "ms_per_step": round(ms_per_step, 4),
+           "frac": round(tot_bound / ms_per_step, 4),
+           "issued_bound_ms": round(tot_ibound, 4), "issued_frac": round(tot_ibound / ms_per_step, 4),
+           "kernel_ms": round(float(sum(per_step_ms)), 4)}
+    peaks = {"mfma_TFLOP/s": peak_tflops, "hbm_GB/s": peak_gbs}
+    if ach_tflops:
+        net["achievable_bound_ms"] = round(tot_abound, 4)
+        net["achievable_frac"] = round(tot_abound / ms_per_step, 4)
+        peaks["achievable"] = dict(ACHIEVABLE, used={"mfma_TFLOP/s": ach_tflops, "hbm_GB/s": ACHIEVABLE["hbm_copy_GB/s"]},
+                                   source="tools/peaks.sh (profiles/r01_peaks.txt), tools/hbm_probe.hip "
+                                          "(profiles/r03k_hbm_probe.txt)")
+    return {"peaks": peaks, "network": net,
             "per_class": per_class, "per_launch": steps}, classes
 
 
@@ -211,7 +227,8 @@ def f16_line(ctx, model_bytes, x, B, args, ref):
     conv_ms = sum(p for p, i in zip(per, infos) if i["op"] == "Conv")
     conv_fl = sum(i["flops"] for i in infos if i["op"] == "Conv")
     achieved = conv_fl / (conv_ms * 1e-3) / 1e12
-    r8d, _ = roofline_8d(infos, per, 1000.0 * elapsed / args.steps, PEAK_F16_MFMA_TFLOPS)
+    r8d, _ = roofline_8d(infos, per, 1000.0 * elapsed / args.steps, PEAK_F16_MFMA_TFLOPS,
+                         ach_tflops=ACHIEVABLE["f16_mfma_TFLOP/s"])
     y = out[:ref.shape[0]].cpu().numpy()  # the first rows of x, whose oracle rows are ref
     res = {"value": round(B * args.steps / elapsed, 2), "unit": "images/s",
            "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "dtype": "f16",
@@ -360,7 +377,8 @@ def main():
             per_step_ms /= args.steps
             # x3: every f32 MAC is six bf16 part products on the 2.5 PF/s BF16 matrix cores
             peak = PEAK_F16_MFMA_TFLOPS if f16 else PEAK_F16_MFMA_TFLOPS / 6.0 if x3 else PEAK_F32_MFMA_TFLOPS
-            r8d, classes = roofline_8d(infos, per_step_ms, 1000.0 * elapsed / args.steps, peak)
+            ach = ACHIEVABLE["f16_mfma_TFLOP/s"] if f16 else None if x3 else ACHIEVABLE["f32_mfma_TFLOP/s"]
+            r8d, classes = roofline_8d(infos, per_step_ms, 1000.0 * elapsed / args.steps, peak, ach_tflops=ach)
             conv = classes.get("Conv", {"ms": 1e-9, "flops": 0.0, "mfma_flops": 0.0, "bytes": 0.0, "launches": 1})
             achieved = conv["flops"] / (conv["ms"] * 1e-3) / 1e12
             issued = conv["mfma_flops"] / (conv["ms"] * 1e-3) / 1e12

@@ -139,6 +139,17 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
     for (int q = tid; q < 32; q += 256) qbias[q] = q < sq.M ? sq.bias[q] : 0.0f;
   }
   const _Float16* __restrict__ wq = static_cast<const _Float16*>(sq.w);
+  // the squeeze's A fragments (waves 0 and 1), loaded once per persistent workgroup: an L2 load per
+  // fragment inside the epilogue sat between two barriers on every tile
+  c1h8 aqr[SQ ? MF : 1][2];
+  if constexpr (SQ) {
+#ifndef ORE_EXP_C1_AQL2
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) aqr[i][t] = *reinterpret_cast<const c1h8*>(wq + ((2 * i + t) * 32 + lr) * 16 + 8 * h);
+#endif
+  }
 
   // L2 weights: this lane's packed row of each fragment (the LDS permutation above, row lr of the
   // fragment), its 8 halves of a k-step at + 16 ks + 8 h; rows past M read a zero row (Mp >= 32 MF)
@@ -291,13 +302,10 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
         const bool cok = (unsigned)(ohb + pr) < (unsigned)p.Ho && (unsigned)(owb + pc) < (unsigned)p.Wo;
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
-          c1h8 o;
+          float av[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            float v = acc[i][f][8 * g + e] + bv[8 * g + e];
-            if (p.relu) v = fmaxf(v, 0.0f);
-            o[e] = (_Float16)v;
-          }
+          for (int e = 0; e < 8; ++e) av[e] = acc[i][f][8 * g + e];
+          const c1h8 o = ore_f16_epilogue8(av, bv + 8 * g, p.relu != 0);
           const c1h8 zero = {};
           *reinterpret_cast<c1h8*>(ct + tpx[f] + 16 * g) = cok ? o : zero;  // 0 outside the conv plane
         }
@@ -312,14 +320,20 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
               c1_pool8(ct + ((2 * a) * C1_CC + 2 * b) * C1_TS + cg * 8, p.relu != 0);
         }
         __syncthreads();
+#ifndef ORE_EXP_C1_NOSQ
         if (wave < 2) {
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
             const c1h8 bq = *reinterpret_cast<const c1h8*>(pt + (32 * wave + lr) * C1_TS + 16 * t + 8 * h);
+#ifdef ORE_EXP_C1_AQL2
             const c1h8 aq = *reinterpret_cast<const c1h8*>(wq + ((2 * i + t) * 32 + lr) * 16 + 8 * h);
+#else
+            const c1h8 aq = aqr[i][t];
+#endif
             sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(aq, bq, sacc, 0, 0, 0);
           }
         }
+#endif
       }
 #ifdef ORE_EXP_C1_NOPOOL
       if (tid < 0) {
@@ -344,10 +358,10 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
         for (int g = 0; g < 2; ++g) {
           const int ch = 16 * g + 8 * h;
           if (ch >= sq.M) continue;
-          c1h8 o;
+          float av[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = (_Float16)fmaxf(sacc[8 * g + e] + qbias[ch + e], 0.0f);
-          *reinterpret_cast<c1h8*>(yq + ch) = o;
+          for (int e = 0; e < 8; ++e) av[e] = sacc[8 * g + e];
+          *reinterpret_cast<c1h8*>(yq + ch) = ore_f16_epilogue8(av, qbias + ch, true);
         }
       }
     }

@@ -185,10 +185,10 @@ __device__ __forceinline__ void ff_store_squeeze(const ff16 (&sacc)[MSF][F], con
 #pragma unroll
       for (int f = 0; f < F; ++f) {
         if (!pok[f]) continue;
-        fh8 o;
+        float av[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (_Float16)fmaxf(sacc[i][f][8 * g + e] + bv[e], 0.0f);
-        *reinterpret_cast<fh8*>(y + yo[f] + 32 * i + 16 * g) = o;
+        for (int e = 0; e < 8; ++e) av[e] = sacc[i][f][8 * g + e];
+        *reinterpret_cast<fh8*>(y + yo[f] + 32 * i + 16 * g) = ore_f16_epilogue8<false>(av, bv, true);
       }
     }
 }
@@ -243,7 +243,12 @@ __global__ __launch_bounds__(256, 2) void fire_f16_kernel(FireF16Params p) {
 #pragma unroll
     for (int f = 0; f < 2; ++f)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) bq[e >> 3][f][e & 7] = (_Float16)fmaxf(acc[f][e] + bv[e], 0.0f);
+      for (int t = 0; t < 2; ++t) {
+        float av[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) av[e] = acc[f][8 * t + e];
+        bq[t][f] = ore_f16_epilogue8<false>(av, bv + 8 * t, true);
+      }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -315,6 +320,20 @@ __global__ __launch_bounds__(256, 2) void fire_pool_f16_kernel(FireF16Params p) 
   const int pa = pr0 + kk / Wp, pb = kk - (kk / Wp) * Wp;
   const int ih0 = 2 * pa - p.ppt, iw0 = 2 * pb - p.ppl;
   int yo[1] = {(pa * Wp + pb) * p.y_cs + 8 * h};
+  // the 3x3 window's conv-tile offsets (chunk-invariant; taps outside the image read a zero block past
+  // the tile: with the max from +0 over Relu outputs that is the separate pool's skipped tap).  Nine
+  // branch-free reads: behind per-tap bounds branches the compiler waited for every read in turn.
+  const int zslot = crmax * W * TS;  // 32 zero halves (both 16-channel halves g, both lane halves h)
+  int toff[9];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int ih = ih0 + r, iw = iw0 + s;
+      const bool in = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      toff[3 * r + s] = (in ? ((ih - cr0) * W + iw) * TS : zslot) + 8 * h;
+    }
+  if (threadIdx.x < 4) *reinterpret_cast<fh8*>(tile + zslot + 8 * threadIdx.x) = fh8{};  // before the halo barrier
   const int ctr = (W2 + 1) * PS;
   const _Float16* __restrict__ ws = static_cast<const _Float16*>(p.ws);
   const int arow = lr * 16 + 8 * h;
@@ -331,14 +350,16 @@ __global__ __launch_bounds__(256, 2) void fire_pool_f16_kernel(FireF16Params p) 
       if (!cok[f]) continue;
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
-        fh8 o;
+        float av[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (_Float16)fmaxf(acc[f][8 * g + e] + bv[8 * g + e], 0.0f);
-        *reinterpret_cast<fh8*>(tile + tj[f] + 16 * g) = o;
+        for (int e = 0; e < 8; ++e) av[e] = acc[f][8 * g + e];
+        *reinterpret_cast<fh8*>(tile + tj[f] + 16 * g) = ore_f16_epilogue8<false>(av, bv + 8 * g, true);
       }
     }
     __syncthreads();  // conv tile of the chunk complete
     if (wact) {
+      // (the A fragments loaded here, behind the barrier: hoisted ahead of the chunk's expand MFMAs
+      // they measured slower, 115 -> 128 us for fire8 + pool at 16 more registers)
       fh8 aq[2][MSF];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -349,16 +370,12 @@ __global__ __launch_bounds__(256, 2) void fire_pool_f16_kernel(FireF16Params p) 
         // the 3x3 max (from -FLT_MAX in f32 in the separate pool, window taps outside the image read
         // as 0): after the Relu every value is +0 or positive and its f16 bits order like the value,
         // so the max is v_pk_max_u16 on the raw bits from +0 (exact; no f32 round trip)
-        fu8 m = {};
+        fu8 v[9];
 #pragma unroll
-        for (int r = 0; r < 3; ++r)
+        for (int t = 0; t < 9; ++t) v[t] = __builtin_bit_cast(fu8, ld_s(tile + toff[t] + 16 * g));
+        fu8 m = v[0];
 #pragma unroll
-          for (int s = 0; s < 3; ++s) {
-            const int ih = ih0 + r, iw = iw0 + s;
-            if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-              m = __builtin_elementwise_max(
-                  m, __builtin_bit_cast(fu8, ld_s(tile + ((ih - cr0) * W + iw) * TS + 16 * g + 8 * h)));
-          }
+        for (int t = 1; t < 9; ++t) m = __builtin_elementwise_max(m, v[t]);
         const fh8 bq = __builtin_bit_cast(fh8, m);
 #pragma unroll
         for (int i = 0; i < MSF; ++i) sacc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aq[g][i], bq, sacc[i][0], 0, 0, 0);
@@ -404,7 +421,7 @@ int fire_f16_lds_bytes(int C, int H, int W) { return ff_halo_rows(H, W) * (W + 2
 
 static int fire_pool_lds_bytes(int C, int H, int W, int PR) {
   const int crmax = std::min(H, 2 * PR + 1);
-  return ((crmax + 2) * (W + 2) * (C + 8) + 7) / 8 * 8 * 2 + crmax * W * 40 * 2;
+  return ((crmax + 2) * (W + 2) * (C + 8) + 7) / 8 * 8 * 2 + crmax * W * 40 * 2 + 64;  // + the zero block
 }
 
 bool fire_pool_f16_plan(FireF16Params* p) {

@@ -17,6 +17,38 @@ __device__ __forceinline__ int xcd_block_id() {
   return (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
 }
 
+// f16 epilogue of 8 f32 accumulators: + bias, one rounding to f16, Relu -- as packed pairs
+// (v_pk_add_f32, v_cvt_pk_f16_f32, v_pk_max_i16: 1.5 VALU per value against 3 for add / max / cvt).
+// Relu after the rounding on the f16 bits as int16 (max with 0) equals Relu before it for every
+// finite value: round-to-nearest keeps the sign, a negative or -0 result becomes +0 either way.
+// PK_ADD = false keeps the bias adds scalar (v_add_f32): inside kernels whose epilogue runs beside
+// MFMAs, where packed f32 VALU costs more than scalar pairs (MI355X_MICROARCH.md 'price of one filler
+// beside MFMAs'; measured: the fire f16 kernels 10-20 % slower with v_pk_add_f32)
+typedef _Float16 ore_h8 __attribute__((ext_vector_type(8)));
+template <bool PK_ADD = true>
+__device__ __forceinline__ ore_h8 ore_f16_epilogue8(const float* a, const float* b, bool relu) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  typedef short s8 __attribute__((ext_vector_type(8)));
+  s8 o;
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    f2 v;
+    if constexpr (PK_ADD) {
+      v = f2{a[e], a[e + 1]} + f2{b[e], b[e + 1]};
+    } else {
+      v[0] = a[e] + b[e];
+      v[1] = a[e + 1] + b[e + 1];
+    }
+    s2 q = __builtin_bit_cast(s2, __builtin_convertvector(v, h2));
+    if (relu) q = __builtin_elementwise_max(q, s2{0, 0});
+    o[e] = q[0];
+    o[e + 1] = q[1];
+  }
+  return __builtin_bit_cast(ore_h8, o);
+}
+
 #ifdef ORE_NO_XCD_BANDS  // experiment builds: the plain block id in the banded / patch kernels
 #define ORE_BAND_ID() ((int)blockIdx.x)
 #else
@@ -42,6 +74,7 @@ struct ConvParams {
   int is1x1;           // kh = kw = 1, stride 1, no padding, Ho*Wo == H*W
   int Mp;              // row stride of wp (conv_packed_mp(M))
   int mtiles, ntiles;  // filled by the launcher
+  int rev;             // streaming launcher: walk the pixel tiles from the last image back (see launch_conv_stream)
   int vec_out;         // 16-B epilogue stores (y_ps, y_nstride % 4 == 0 and a 16-B aligned y)
   int x_f32;           // f16 kernel: the input is the f32 NCHW model input (rounded to f16 while staging);
                        // otherwise f16 NHWC with pixel stride x_ps (f16 kernels always write NHWC,

@@ -526,7 +526,7 @@ __global__ __launch_bounds__(256) void gap_kernel(const T* __restrict__ x, float
   // coalesced loads along the row
   extern __shared__ float tile[];  // 64 * (HW | 1) floats
   const int ls = HW | 1;
-  const long long r0 = (long long)blockIdx.x * 64;
+  const long long r0 = (long long)blockIdx.x * 64;  // (reverse order measured equal: 39.7 vs 39.5 us)
   const int nr = (int)(rows - r0 < 64 ? rows - r0 : 64);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (HW <= 256) {  // every load of the wave's 16 rows in flight before the first LDS store
