@@ -67,9 +67,8 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(ConvParams p) {
   const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
   const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
   const int gw = wgid * 4 + wave;
-  const int mt = gw % p.mtiles, ct0 = gw / p.mtiles;
-  if (ct0 >= p.ntiles) return;  // wave-uniform; no barrier anywhere in this kernel
-  const int ct = p.rev ? p.ntiles - 1 - ct0 : ct0;
+  const int mt = gw % p.mtiles, ct = gw / p.mtiles;
+  if (ct >= p.ntiles) return;  // wave-uniform; no barrier anywhere in this kernel
   const int m0 = mt * (16 * MF);
   const int YPS = p.y_ps;      // output plane stride = columns per image (S1X1: == x_ps)
   const int lk = lane >> 4, lj = lane & 15;
@@ -253,8 +252,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream1x1_persist_kernel(ConvPara
   const int lk = lane >> 4, lj = lane & 15;
   const int ntot = (int)p.Ntot;
   // a pixel tile's per-lane input / output offsets (clamped columns re-read valid data, masked at the store)
-  auto geo = [&](int ct0, int (&xo)[NB], int (&yo)[NB], bool (&ok)[NB]) __attribute__((always_inline)) {
-    const int ct = p.rev ? p.ntiles - 1 - ct0 : ct0;
+  auto geo = [&](int ct, int (&xo)[NB], int (&yo)[NB], bool (&ok)[NB]) __attribute__((always_inline)) {
 #pragma unroll
     for (int g = 0; g < NB; ++g) {
       int col = ct * (64 * NB) + 64 * g + 4 * lj;
@@ -428,12 +426,10 @@ static void launch_cs(const ConvParams& p0, hipStream_t s) {
 
 // tiles CONV_TILE_STREAM + 0..8 (ConvPlan::cfg); 16 x 512 tiles (NB = 8) measured no faster
 // on the 54 x 54 squeezes (tools/bench_1x1.py, profiles/r01y_bench_1x1.txt); the caller checks conv_stream_eligible
-void launch_conv_stream(const ConvParams& p0, int tile, hipStream_t s) {
-  ConvParams p = p0;
-  // p.rev (pixel tiles from the last image back, so that the producers' last-written images are read
-  // while still in the Infinity Cache) measured no faster on the fire7 / fire8 squeezes (85 vs 85 us)
-  // and slowed the next expand1x1 (46 -> 52 us); kept off -- unlike pool_conv1x1_f32_kernel's reverse
-  // image order, which pays (ore_pool_conv.hip)
+void launch_conv_stream(const ConvParams& p, int tile, hipStream_t s) {
+  // (walking the pixel tiles from the last image back -- reading the producers' last-written images
+  // while they are still in the Infinity Cache, as pool_conv1x1_f32_kernel does -- measured no faster
+  // on the fire7 / fire8 squeezes, 85 vs 85 us, and slowed the next expand1x1, 46 -> 52 us)
   if (tile >= CONV_TILE_SP) {
     switch (tile - CONV_TILE_SP) {
       case 0: launch_sp<2, 2, 4>(p, s); break;  // 32 x 128

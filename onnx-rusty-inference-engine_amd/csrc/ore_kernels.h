@@ -74,7 +74,6 @@ struct ConvParams {
   int is1x1;           // kh = kw = 1, stride 1, no padding, Ho*Wo == H*W
   int Mp;              // row stride of wp (conv_packed_mp(M))
   int mtiles, ntiles;  // filled by the launcher
-  int rev;             // streaming launcher: walk the pixel tiles from the last image back (see launch_conv_stream)
   int vec_out;         // 16-B epilogue stores (y_ps, y_nstride % 4 == 0 and a 16-B aligned y)
   int x_f32;           // f16 kernel: the input is the f32 NCHW model input (rounded to f16 while staging);
                        // otherwise f16 NHWC with pixel stride x_ps (f16 kernels always write NHWC,
