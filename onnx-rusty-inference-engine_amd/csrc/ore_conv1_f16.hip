@@ -115,7 +115,7 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
   _Float16* ct = halo + HALO_HALVES;        // [C1_NPX][C1_TS]
   float* sbias = reinterpret_cast<float*>(ct + C1_NPX * C1_TS);  // [MF * 32]
   // SQ: the pooled values of one fragment [64 pixels][40] (all four waves pool, waves 0 and 1 run the
-  // squeeze's MFMAs with its weights from L2) and the squeeze bias
+  // squeeze's MFMAs, its weights in registers) and the squeeze bias
   _Float16* pt = reinterpret_cast<_Float16*>(sbias + MF * 32);
   float* qbias = reinterpret_cast<float*>(pt + (SQ ? 64 * C1_TS : 0));
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, h = lane >> 5;
@@ -143,12 +143,10 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
   // fragment inside the epilogue sat between two barriers on every tile
   c1h8 aqr[SQ ? MF : 1][2];
   if constexpr (SQ) {
-#ifndef ORE_EXP_C1_AQL2
 #pragma unroll
     for (int i = 0; i < MF; ++i)
 #pragma unroll
       for (int t = 0; t < 2; ++t) aqr[i][t] = *reinterpret_cast<const c1h8*>(wq + ((2 * i + t) * 32 + lr) * 16 + 8 * h);
-#endif
   }
 
   // L2 weights: this lane's packed row of each fragment (the LDS permutation above, row lr of the
@@ -320,20 +318,15 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
               c1_pool8(ct + ((2 * a) * C1_CC + 2 * b) * C1_TS + cg * 8, p.relu != 0);
         }
         __syncthreads();
-#ifndef ORE_EXP_C1_NOSQ
+        // (waves 0 and 1 pooling their own squeeze operand from the conv tile, two 3x3 maxima per lane,
+        // without this LDS block and barrier measured slower: 196-204 -> 203-212 us)
         if (wave < 2) {
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
             const c1h8 bq = *reinterpret_cast<const c1h8*>(pt + (32 * wave + lr) * C1_TS + 16 * t + 8 * h);
-#ifdef ORE_EXP_C1_AQL2
-            const c1h8 aq = *reinterpret_cast<const c1h8*>(wq + ((2 * i + t) * 32 + lr) * 16 + 8 * h);
-#else
-            const c1h8 aq = aqr[i][t];
-#endif
-            sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(aq, bq, sacc, 0, 0, 0);
+            sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(aqr[i][t], bq, sacc, 0, 0, 0);
           }
         }
-#endif
       }
 #ifdef ORE_EXP_C1_NOPOOL
       if (tid < 0) {

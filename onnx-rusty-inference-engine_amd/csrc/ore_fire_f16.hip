@@ -43,6 +43,9 @@ typedef float ff16 __attribute__((ext_vector_type(16)));
 typedef unsigned short fu8 __attribute__((ext_vector_type(8)));
 
 constexpr int FF_PIX = 256;  // pixels per workgroup
+// the expand biases (E1 + E3 <= FF_BIAS floats) are staged in LDS once per workgroup: read from L2 per
+// chunk, their latency sat between the chunk's expand MFMAs and its squeeze
+constexpr int FF_BIAS = 512;
 
 // rows of the LDS halo for a tile of FF_PIX pixels of a W-wide image with H rows (host and device)
 __host__ __device__ inline int ff_halo_rows(int H, int W) {
@@ -206,6 +209,8 @@ __global__ __launch_bounds__(256, 2) void fire_f16_kernel(FireF16Params p) {
   const int hr0 = q0 / W - 1;  // image row of halo row 0
   ff_stage_halo<NKC, PS>(halo, static_cast<const _Float16*>(p.x) + (long long)img * p.x_nstride, p.x_cs, H, W, hr0,
                          qlast / W - q0 / W + 3);
+  float* sb = reinterpret_cast<float*>(halo + ff_halo_rows(H, W) * W2 * PS);  // [E1 + E3] biases
+  for (int q = threadIdx.x; q < p.E1 + p.E3; q += 256) sb[q] = q < p.E1 ? p.b1[q] : p.b3[q - p.E1];
   __syncthreads();
   if (q0 + 64 * wave >= HW) return;  // no pixel of this wave (after the only barrier)
 
@@ -260,12 +265,12 @@ __global__ __launch_bounds__(256, 2) void fire_f16_kernel(FireF16Params p) {
   for (int c0 = 0; c0 < p.E1; c0 += 32) {  // expand1x1 chunks
     ff16 acc[2];
     ff_e1_chunk<NKC, 2>(acc, static_cast<const _Float16*>(p.w1), p.E1, c0, arow, halo, hb, ctr);
-    feed(acc, p.b1, c0, c0);
+    feed(acc, sb, c0, c0);
   }
   for (int c0 = 0; c0 < p.E3; c0 += 32) {  // expand3x3 chunks
     ff16 acc[2];
     ff_e3_chunk<NKC, 2, PS>(acc, static_cast<const _Float16*>(p.w3), p.E3, c0, arow, halo, hb, W2);
-    feed(acc, p.b3, c0, p.E1 + c0);
+    feed(acc, sb + p.E1, c0, p.E1 + c0);
   }
   ff_store_squeeze<MSF, 2>(sacc, p, static_cast<_Float16*>(p.y) + (long long)img * p.y_nstride, yo, pok, h);
 }
@@ -334,6 +339,8 @@ __global__ __launch_bounds__(256, 2) void fire_pool_f16_kernel(FireF16Params p) 
       toff[3 * r + s] = (in ? ((ih - cr0) * W + iw) * TS : zslot) + 8 * h;
     }
   if (threadIdx.x < 4) *reinterpret_cast<fh8*>(tile + zslot + 8 * threadIdx.x) = fh8{};  // before the halo barrier
+  float* sb = reinterpret_cast<float*>(tile + zslot + 32);  // [E1 + E3] biases
+  for (int q = threadIdx.x; q < p.E1 + p.E3; q += 256) sb[q] = q < p.E1 ? p.b1[q] : p.b3[q - p.E1];
   const int ctr = (W2 + 1) * PS;
   const _Float16* __restrict__ ws = static_cast<const _Float16*>(p.ws);
   const int arow = lr * 16 + 8 * h;
@@ -387,12 +394,12 @@ __global__ __launch_bounds__(256, 2) void fire_pool_f16_kernel(FireF16Params p) 
   for (int c0 = 0; c0 < p.E1; c0 += 32) {
     ff16 acc[F];
     if (clive) ff_e1_chunk<NKC, F>(acc, static_cast<const _Float16*>(p.w1), p.E1, c0, arow, halo, hb, ctr);
-    pool_feed(acc, p.b1, c0, c0);
+    pool_feed(acc, sb, c0, c0);
   }
   for (int c0 = 0; c0 < p.E3; c0 += 32) {
     ff16 acc[F];
     if (clive) ff_e3_chunk<NKC, F, PS>(acc, static_cast<const _Float16*>(p.w3), p.E3, c0, arow, halo, hb, W2);
-    pool_feed(acc, p.b3, c0, p.E1 + c0);
+    pool_feed(acc, sb + p.E1, c0, p.E1 + c0);
   }
   if (wact) ff_store_squeeze<MSF, 1>(sacc, p, static_cast<_Float16*>(p.y) + (long long)img * p.y_nstride, yo, pok, h);
 }
@@ -417,11 +424,11 @@ __global__ __launch_bounds__(256) void fire_pack_f16_kernel(const float* __restr
 
 }  // namespace
 
-int fire_f16_lds_bytes(int C, int H, int W) { return ff_halo_rows(H, W) * (W + 2) * (C + 8) * 2; }
+int fire_f16_lds_bytes(int C, int H, int W) { return ff_halo_rows(H, W) * (W + 2) * (C + 8) * 2 + FF_BIAS * 4; }
 
 static int fire_pool_lds_bytes(int C, int H, int W, int PR) {
   const int crmax = std::min(H, 2 * PR + 1);
-  return ((crmax + 2) * (W + 2) * (C + 8) + 7) / 8 * 8 * 2 + crmax * W * 40 * 2 + 64;  // + the zero block
+  return ((crmax + 2) * (W + 2) * (C + 8) + 7) / 8 * 8 * 2 + crmax * W * 40 * 2 + 64 + FF_BIAS * 4;  // + zero block, biases
 }
 
 bool fire_pool_f16_plan(FireF16Params* p) {
@@ -454,6 +461,7 @@ bool fire_pool_f16_plan(FireF16Params* p) {
 bool fire_f16_eligible(const FireF16Params& p) {
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   const bool common = p.C % 16 == 0 && p.C >= 16 && p.C <= 64 && p.E1 % 32 == 0 && p.E3 % 32 == 0 && p.E1 > 0 &&
+                      p.E1 + p.E3 <= FF_BIAS &&
                       p.E3 > 0 && p.Ms % 8 == 0 && p.Ms > 0 && p.Ms <= 64 && p.Msp == (p.Ms + 31) / 32 * 32 &&
                       p.x_cs % 8 == 0 && p.y_cs % 8 == 0 && p.x_cs >= p.C && p.y_cs >= p.Ms && p.x_nstride % 8 == 0 &&
                       p.y_nstride % 8 == 0 && al16(p.x) && al16(p.y) && al16(p.w1) && al16(p.w3) && al16(p.ws) &&

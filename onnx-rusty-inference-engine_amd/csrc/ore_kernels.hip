@@ -536,7 +536,8 @@ __global__ __launch_bounds__(256) void gap_kernel(const T* __restrict__ x, float
       const int r = wave + 4 * j;
       const T* __restrict__ src = x + (r0 + (r < nr ? r : 0)) * ps;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[j][u] = (lane + 64 * u < HW) ? (float)src[lane + 64 * u] : 0.0f;
+      // non-temporal loads (read once): 39.3 -> 36.8 us for SqueezeNet's pool10 at B = 256
+      for (int u = 0; u < 4; ++u) v[j][u] = (lane + 64 * u < HW) ? (float)__builtin_nontemporal_load(src + lane + 64 * u) : 0.0f;
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
