@@ -130,6 +130,33 @@ def test_f16_pool_relu_gap_exact(gpu_ctx):
         m.close()
 
 
+@pytest.mark.parametrize("m2", [8, 7])  # even: two channels per lane (gap_nhwc2_kernel); odd: one
+def test_f16_gap_sequential_sum(gpu_ctx, m2):
+    """The f16 GlobalAveragePool is the reference's sequential f32 sum (global_average_pool_op.rs:44-48)
+    over the f16 values, bit for bit, on non-integer data (an order-sensitive check)."""
+    import ore
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((2, 4, 29, 29)).astype(np.float32)
+    w1 = (rng.standard_normal((32, 4, 3, 3)) * 0.3).astype(np.float32)
+    b1 = rng.standard_normal((32,)).astype(np.float32)
+    w2 = (rng.standard_normal((m2, 32, 1, 1)) * 0.2).astype(np.float32)
+    mb = _chain_model((1, 4, 29, 29), [(w1, b1, [1] * 4, [1, 1], True), (w2, None, [0] * 4, [1, 1], False)],
+                      pool=[0, 0, 1, 1])
+    m = ore.Model(gpu_ctx, mb, max_batch=2, precision="f16")
+    m.set_fusion(ore.FUSE_ALL | ore.KEEP_VALUES)
+    y = _np(m.run(_t(x))).reshape(2, m2)
+    c1 = m.read_value("c1").astype(np.float32)  # the f16 values the GAP reads, [2, m2, 15, 15]
+    ref = np.zeros((2, m2), np.float32)
+    for n in range(2):
+        for c in range(m2):
+            s = np.float32(0.0)
+            for v in c1[n, c].reshape(-1):
+                s = np.float32(s + v)
+            ref[n, c] = np.float32(s / np.float32(c1.shape[2] * c1.shape[3]))
+    np.testing.assert_array_equal(y, ref)
+    m.close()
+
+
 @pytest.fixture(scope="module")
 def squeeze_f16(gpu_ctx):
     import ore
