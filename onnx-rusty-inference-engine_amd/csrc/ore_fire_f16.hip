@@ -54,7 +54,15 @@ __host__ __device__ inline int ff_halo_rows(int H, int W) {
   return r + 2;
 }
 
-__device__ __forceinline__ fh8 ld_g(const _Float16* p) { return *reinterpret_cast<const fh8*>(p); }
+// A-operand (weight) loads as raw buffer loads: the lane's constant byte offset in a VGPR, the
+// uniform fragment / k-step offset in an SGPR -- no per-load 64-bit address VALU (a flat global
+// pointer per load cost a v_lshl_add_u64 each)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ff_rsrc(const void* w) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(w), (short)0, 0x7FFFFFF0, 0x00020000);
+}
+__device__ __forceinline__ fh8 ld_w(__amdgpu_buffer_rsrc_t r, int vbytes, int shalves) {
+  return __builtin_bit_cast(fh8, __builtin_amdgcn_raw_buffer_load_b128(r, vbytes, shalves * 2, 0));
+}
 __device__ __forceinline__ fh8 ld_s(const _Float16* p) { return *reinterpret_cast<const fh8*>(p); }
 
 // Stage input rows hr0 .. hr0 + nrows - 1 (columns -1 .. W, zeros outside the image) of image x into
@@ -99,11 +107,11 @@ __device__ __forceinline__ void ff_zero(ff16 (&acc)[F]) {
 // One 32-channel chunk (rows c0 .. c0 + 31 of the permuted packing) of expand1x1 over F pixel
 // fragments: NKC k-steps on the centre tap (hb[f] + ctr)
 template <int NKC, int F>
-__device__ __forceinline__ void ff_e1_chunk(ff16 (&acc)[F], const _Float16* __restrict__ w1, int E1, int c0, int arow,
+__device__ __forceinline__ void ff_e1_chunk(ff16 (&acc)[F], __amdgpu_buffer_rsrc_t w1, int E1, int c0, int arow,
                                             const _Float16* halo, const int (&hb)[F], int ctr) {
   fh8 a[NKC];
 #pragma unroll
-  for (int s = 0; s < NKC; ++s) a[s] = ld_g(w1 + (s * E1 + c0) * 16 + arow);
+  for (int s = 0; s < NKC; ++s) a[s] = ld_w(w1, 2 * arow, (s * E1 + c0) * 16);
   ff_zero(acc);
 #pragma unroll
   for (int s = 0; s < NKC; ++s) {
@@ -126,12 +134,12 @@ __device__ __forceinline__ void ff_e1_chunk(ff16 (&acc)[F], const _Float16* __re
 #define ORE_FF_PD 8
 #endif
 template <int NKC, int F, int PS>
-__device__ __forceinline__ void ff_e3_chunk(ff16 (&acc)[F], const _Float16* __restrict__ w3, int E3, int c0, int arow,
+__device__ __forceinline__ void ff_e3_chunk(ff16 (&acc)[F], __amdgpu_buffer_rsrc_t w3, int E3, int c0, int arow,
                                             const _Float16* halo, const int (&hb)[F], int W2) {
   constexpr int NS3 = 9 * NKC, PD = ORE_FF_PD < NS3 ? ORE_FF_PD : NS3, BD = ORE_FF_BD;
   fh8 a[PD];
 #pragma unroll
-  for (int s = 0; s < PD; ++s) a[s] = ld_g(w3 + (s * E3 + c0) * 16 + arow);
+  for (int s = 0; s < PD; ++s) a[s] = ld_w(w3, 2 * arow, (s * E3 + c0) * 16);
   ff_zero(acc);
   auto boff = [&](int s) __attribute__((always_inline)) {
     const int tap = s / NKC, cs = s - tap * NKC;
@@ -149,7 +157,7 @@ __device__ __forceinline__ void ff_e3_chunk(ff16 (&acc)[F], const _Float16* __re
     fh8 b[F];
 #pragma unroll
     for (int f = 0; f < F; ++f) b[f] = bn[s % BD][f];
-    if (s + PD < NS3) a[s % PD] = ld_g(w3 + ((s + PD) * E3 + c0) * 16 + arow);
+    if (s + PD < NS3) a[s % PD] = ld_w(w3, 2 * arow, ((s + PD) * E3 + c0) * 16);
     if (s + BD < NS3) {
 #pragma unroll
       for (int f = 0; f < F; ++f) bn[s % BD][f] = ld_s(halo + hb[f] + boff(s + BD));
@@ -227,7 +235,7 @@ __global__ __launch_bounds__(256, 2) void fire_f16_kernel(FireF16Params p) {
     yo[f] = qq * p.y_cs + 8 * h;
   }
   const int ctr = (W2 + 1) * PS;  // tap (1, 1)
-  const _Float16* __restrict__ ws = static_cast<const _Float16*>(p.ws);
+  const __amdgpu_buffer_rsrc_t wsr = ff_rsrc(p.ws), w1r = ff_rsrc(p.w1), w3r = ff_rsrc(p.w3);
   const int arow = lr * 16 + 8 * h;  // this lane's 8 halves inside a [row][16] fragment block
 
   ff16 sacc[MSF][2];
@@ -241,7 +249,7 @@ __global__ __launch_bounds__(256, 2) void fire_f16_kernel(FireF16Params p) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < MSF; ++i) aq[t][i] = ld_g(ws + ((cat0 / 16 + t) * p.Msp + 32 * i) * 16 + arow);
+      for (int i = 0; i < MSF; ++i) aq[t][i] = ld_w(wsr, 2 * arow, ((cat0 / 16 + t) * p.Msp + 32 * i) * 16);
     float bv[16];
     ff_bias16(bv, bias, c0, h);
     fh8 bq[2][2];
@@ -264,12 +272,12 @@ __global__ __launch_bounds__(256, 2) void fire_f16_kernel(FireF16Params p) {
 
   for (int c0 = 0; c0 < p.E1; c0 += 32) {  // expand1x1 chunks
     ff16 acc[2];
-    ff_e1_chunk<NKC, 2>(acc, static_cast<const _Float16*>(p.w1), p.E1, c0, arow, halo, hb, ctr);
+    ff_e1_chunk<NKC, 2>(acc, w1r, p.E1, c0, arow, halo, hb, ctr);
     feed(acc, sb, c0, c0);
   }
   for (int c0 = 0; c0 < p.E3; c0 += 32) {  // expand3x3 chunks
     ff16 acc[2];
-    ff_e3_chunk<NKC, 2, PS>(acc, static_cast<const _Float16*>(p.w3), p.E3, c0, arow, halo, hb, W2);
+    ff_e3_chunk<NKC, 2, PS>(acc, w3r, p.E3, c0, arow, halo, hb, W2);
     feed(acc, sb + p.E1, c0, p.E1 + c0);
   }
   ff_store_squeeze<MSF, 2>(sacc, p, static_cast<_Float16*>(p.y) + (long long)img * p.y_nstride, yo, pok, h);
@@ -342,7 +350,7 @@ __global__ __launch_bounds__(256, 2) void fire_pool_f16_kernel(FireF16Params p) 
   float* sb = reinterpret_cast<float*>(tile + zslot + 32);  // [E1 + E3] biases
   for (int q = threadIdx.x; q < p.E1 + p.E3; q += 256) sb[q] = q < p.E1 ? p.b1[q] : p.b3[q - p.E1];
   const int ctr = (W2 + 1) * PS;
-  const _Float16* __restrict__ ws = static_cast<const _Float16*>(p.ws);
+  const __amdgpu_buffer_rsrc_t wsr = ff_rsrc(p.ws), w1r = ff_rsrc(p.w1), w3r = ff_rsrc(p.w3);
   const int arow = lr * 16 + 8 * h;
   ff16 sacc[MSF][1];
 #pragma unroll
@@ -371,7 +379,7 @@ __global__ __launch_bounds__(256, 2) void fire_pool_f16_kernel(FireF16Params p) 
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int i = 0; i < MSF; ++i) aq[t][i] = ld_g(ws + ((cat0 / 16 + t) * p.Msp + 32 * i) * 16 + arow);
+        for (int i = 0; i < MSF; ++i) aq[t][i] = ld_w(wsr, 2 * arow, ((cat0 / 16 + t) * p.Msp + 32 * i) * 16);
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
         // the 3x3 max (from -FLT_MAX in f32 in the separate pool, window taps outside the image read
@@ -393,12 +401,12 @@ __global__ __launch_bounds__(256, 2) void fire_pool_f16_kernel(FireF16Params p) 
 
   for (int c0 = 0; c0 < p.E1; c0 += 32) {
     ff16 acc[F];
-    if (clive) ff_e1_chunk<NKC, F>(acc, static_cast<const _Float16*>(p.w1), p.E1, c0, arow, halo, hb, ctr);
+    if (clive) ff_e1_chunk<NKC, F>(acc, w1r, p.E1, c0, arow, halo, hb, ctr);
     pool_feed(acc, sb, c0, c0);
   }
   for (int c0 = 0; c0 < p.E3; c0 += 32) {
     ff16 acc[F];
-    if (clive) ff_e3_chunk<NKC, F, PS>(acc, static_cast<const _Float16*>(p.w3), p.E3, c0, arow, halo, hb, W2);
+    if (clive) ff_e3_chunk<NKC, F, PS>(acc, w3r, p.E3, c0, arow, halo, hb, W2);
     pool_feed(acc, sb + p.E1, c0, p.E1 + c0);
   }
   if (wact) ff_store_squeeze<MSF, 1>(sacc, p, static_cast<_Float16*>(p.y) + (long long)img * p.y_nstride, yo, pok, h);

@@ -130,7 +130,7 @@ def test_f16_pool_relu_gap_exact(gpu_ctx):
         m.close()
 
 
-@pytest.mark.parametrize("m2", [8, 7])  # even: two channels per lane (gap_nhwc2_kernel); odd: one
+@pytest.mark.parametrize("m2", [8, 7])
 def test_f16_gap_sequential_sum(gpu_ctx, m2):
     """The f16 GlobalAveragePool is the reference's sequential f32 sum (global_average_pool_op.rs:44-48)
     over the f16 values, bit for bit, on non-integer data (an order-sensitive check)."""
