@@ -57,8 +57,9 @@ __device__ __forceinline__ void cs_load_a(__amdgpu_buffer_rsrc_t r, int voff, in
   }
 }
 
-// MF: 16-row fragments per wave (channels MF*j + f), NB: 64-pixel groups per wave, D: ring depth
-template <int MF, int NB, int D, int MODE>
+// MF: 16-row fragments per wave (channels MF*j + f), NB: 64-pixel groups per wave, D: ring depth,
+// NT: non-temporal B loads (1x1 convs whose single m tile reads every input element once)
+template <int MF, int NB, int D, int MODE, int NT = 0>
 __global__ __launch_bounds__(256, 2) void conv_stream_kernel(ConvParams p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(ConvParams p) {
     cs_load_a<MF>(wr, aoff, s_ * astep, ra[SLOT]);                                                \
     if constexpr (MODE == S1X1) {                                                                 \
       _Pragma("unroll") for (int g = 0; g < NB; ++g) rb[SLOT][g] = __builtin_bit_cast(          \
-          cs_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, xoff[g], s_ * xstep, 0));         \
+          cs_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, xoff[g], s_ * xstep, NT ? 2 : 0)); \
     } else {                                                                                      \
       /* tt / 3 for tt < 9, 24-bit multiplies (v_mul_u32_u24, full rate; v_mul_lo_u32 is 1/4) */  \
       const int r_ = (int)(__umul24((unsigned)tt, 11u) >> 5);                                     \
@@ -236,7 +237,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(ConvParams p) {
 // pixel tiles ct = cs, cs + ncs, ... (ncs = resident waves / m tiles); the operand ring runs across
 // tiles, so the next tile's first D k-steps are loading during this tile's last MFMAs and its stores.
 // The same operands, k order and epilogue as conv_stream_kernel: bit-identical.
-template <int MF, int NB, int D>
+template <int MF, int NB, int D, int NT = 0>
 __global__ __launch_bounds__(256, 2) void conv_stream1x1_persist_kernel(ConvParams p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -293,7 +294,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream1x1_persist_kernel(ConvPara
   {                                                                                               \
     cs_load_a<MF>(wr, aoff, (S) * astep, ra[SLOT]);                                               \
     _Pragma("unroll") for (int g = 0; g < NB; ++g) rb[SLOT][g] = __builtin_bit_cast(              \
-        cs_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, XO[g], (S) * xstep, 0));             \
+        cs_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, XO[g], (S) * xstep, NT ? 2 : 0));    \
   }
 #define SP_MFMA(SLOT)                                                                             \
   __builtin_amdgcn_s_setprio(1);                                                                  \
@@ -407,7 +408,10 @@ static void launch_sp(const ConvParams& p0, hipStream_t s) {
   long long waves = std::min<long long>(8LL * ncu, need);
   waves = std::max<long long>(waves, p.mtiles);
   const unsigned grid = (unsigned)((waves + 3) / 4);
-  hipLaunchKernelGGL((conv_stream1x1_persist_kernel<MF, NB, D>), dim3(grid), dim3(256), 0, s, p);
+  if (p.mtiles == 1)  // every input element read once: non-temporal loads
+    hipLaunchKernelGGL((conv_stream1x1_persist_kernel<MF, NB, D, 1>), dim3(grid), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_stream1x1_persist_kernel<MF, NB, D, 0>), dim3(grid), dim3(256), 0, s, p);
 }
 
 template <int MF, int NB, int D>
@@ -418,7 +422,9 @@ static void launch_cs(const ConvParams& p0, hipStream_t s) {
   p.ntiles = (int)((p.Ntot + 64 * NB - 1) / (64 * NB));
   const long long waves = (long long)p.mtiles * p.ntiles;
   const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
-  if (stream_mode(p) == 1)
+  if (stream_mode(p) == 1 && p.mtiles == 1)  // every input element read once: non-temporal loads
+    hipLaunchKernelGGL((conv_stream_kernel<MF, NB, D, S1X1, 1>), grid, block, 0, s, p);
+  else if (stream_mode(p) == 1)
     hipLaunchKernelGGL((conv_stream_kernel<MF, NB, D, S1X1>), grid, block, 0, s, p);
   else
     hipLaunchKernelGGL((conv_stream_kernel<MF, NB, D, STAPS>), grid, block, 0, s, p);
