@@ -208,7 +208,7 @@ ore_status ore_model_destroy(ore_model* m);
 #define ORE_FUSE_CONV_RELU 1
 #define ORE_FUSE_CONCAT 2
 #define ORE_FUSE_ALIAS 4
-#define ORE_FUSE_ALL 2023
+#define ORE_FUSE_ALL 6119
 /* bit 5 (in ORE_FUSE_ALL): Conv (-> Relu) -> 3x3 / stride-2 MaxPool as ONE launch when the conv
  * output has no other consumer: each block computes a 13 x 19 patch of conv outputs covering a
  * 6 x 9 tile of pooled outputs (the overlapping window row / column is recomputed by the
@@ -245,6 +245,9 @@ ore_status ore_model_destroy(ore_model* m);
 /* bit 10: a 3x3 / stride-2 MaxPool read only by a 1x1 conv (+ Relu, <= 64 channels) runs inside that
  * conv (f32 pool_conv1x1_f32_kernel: pool5 + fire9/squeeze). */
 #define ORE_FUSE_POOL_SQUEEZE 1024
+/* bit 12: f16 models: a 1x1 conv (+ Relu) whose only reader is GlobalAveragePool runs with the GAP in
+ * its epilogue (conv1x1_gap_f16_kernel: conv10 + relu10 + pool10; not under ORE_KEEP_VALUES). */
+#define ORE_FUSE_CONV_GAP 4096
 /* bit 11 (tests, not in ORE_FUSE_ALL): apply every eligible fusion regardless of the size
  * heuristics above (batch / plane thresholds, the 1.25 patch-work bound). */
 #define ORE_FUSE_EAGER 2048

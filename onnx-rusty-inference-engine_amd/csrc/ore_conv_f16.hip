@@ -906,6 +906,149 @@ void launch_gap_nhwc(const void* x, float* y, int N, int C, int HW, int cs, long
                      HW, cs, nstride);
 }
 
+// ------------------------------------------------------------------ 1x1 conv + Relu + GAP (f16)
+// SqueezeNet's conv10 (512 -> 1000, 13 x 13) -> relu10 -> pool10 in one launch.  The separate path is
+// conv_f16_dma_kernel (128 x 128 tiles, a barrier per 32 k: 8 MFMAs per wave between barriers) writing
+// the 87 MB f16 map, then gap_nhwc_kernel reading it back.  Here one workgroup owns one image's P <= 32 NF
+// pixels x 128 output channels (4 waves x 32): per 64-channel K chunk the image's pixels are staged
+// in LDS (double-buffered, the next chunk's loads in flight) and each wave runs 4 k-steps x NF
+// v_mfma_f32_32x32x16_f16 (A = its 32 weight rows from L2, one chunk ahead) -- 24 MFMAs per barrier.
+// Epilogue: bias + Relu + one rounding to f16 (what conv_f16 stores), the wave's [pixels][32 channels]
+// tile to LDS, then lane c < 32 sums its channel over the pixels in order in f32 and divides by P
+// (gap_nhwc_kernel's arithmetic).  Same operands, k order and MFMA chain as the separate conv, the
+// same f16 values in the same order into the same sum: bit-identical.
+template <int NF>
+__global__ __launch_bounds__(256, 2) void conv1x1_gap_f16_kernel(Conv1x1GapF16 p) {
+  constexpr int KC = 64, BS = KC + 8;      // K chunk; LDS pixel stride (halves, 144 B)
+  constexpr int NPX = 32 * NF, STAGE = NPX * BS, TS = 36;  // staged pixels; GAP tile pixel stride
+  static_assert(4 * NPX * TS <= 2 * STAGE, "the GAP tiles fit the stage buffers");
+  extern __shared__ __attribute__((aligned(16))) _Float16 gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mblocks = (p.M + 127) / 128;
+  const int img = blockIdx.x / mblocks, m0 = (blockIdx.x - img * mblocks) * 128 + 32 * wave;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<_Float16*>(static_cast<const _Float16*>(p.x) + (long long)img * p.x_nstride), (short)0,
+      p.P * p.x_cs * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.wp), (short)0, p.Mp * p.Kp * 2, 0x00020000);
+  // this thread's staged 16-B groups q = tid + 256 u: pixel q >> 3 (>= P: zeros), channels 8 (q & 7)
+  int xo[NF], so[NF];
+#pragma unroll
+  for (int u = 0; u < NF; ++u) {
+    const int q = tid + 256 * u, px = q >> 3, g = q & 7;
+    xo[u] = px < p.P ? (px * p.x_cs + 8 * g) * 2 : (int)0x80000000;
+    so[u] = px * BS + 8 * g;
+  }
+  const int aoff = ((m0 + lr) * p.Kp + 8 * h) * 2;  // rows past Mp read 0 (buffer range)
+  half8 xv[NF], a[2][4];
+  auto load = [&](int c, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NF; ++u)
+      xv[u] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(xr, xo[u], c * KC * 2, 0));
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      a[slot][t] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(wr, aoff, (c * KC + 16 * t) * 2, 0));
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NF; ++u) *reinterpret_cast<half8*>(gsm + buf * STAGE + so[u]) = xv[u];
+  };
+  floatx16h acc[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.0f;
+  const int nch = p.C / KC;
+  // chunk c from stage buffer BUF (a compile-time constant after inlining: the register rings stay
+  // statically indexed)
+  auto chunk = [&](int c, int BUF) __attribute__((always_inline)) {
+    if (c + 1 < nch) load(c + 1, BUF ^ 1);  // in flight during this chunk's MFMAs
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      half8 b[NF];
+#pragma unroll
+      for (int j = 0; j < NF; ++j) b[j] = *reinterpret_cast<const half8*>(gsm + BUF * STAGE + (32 * j + lr) * BS + 16 * t + 8 * h);
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[BUF][t], b[j], acc[j], 0, 0, 0);
+    }
+    if (c + 1 < nch) store(BUF ^ 1);  // that buffer was last read in chunk c - 1 (the barrier below it)
+    __syncthreads();
+  };
+  load(0, 0);
+  store(0);
+  __syncthreads();
+  for (int c = 0; c < nch; c += 2) {
+    chunk(c, 0);
+    if (c + 1 < nch) chunk(c + 1, 1);
+  }
+  // epilogue: element i of lane (lr, h) in fragment j = channel m0 + 8 (i >> 2) + 4 h + (i & 3) at
+  // pixel 32 j + lr; the wave's tile [pixel][32 channels] (f16) in the stage buffers
+  _Float16* tl = gsm + wave * NPX * TS;
+  float bv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int m = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
+    bv[i] = (p.bias && m < p.M) ? p.bias[m] : 0.0f;
+  }
+#pragma unroll
+  for (int j = 0; j < NF; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      half4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = acc[j][4 * q + e] + bv[4 * q + e];
+        if (p.relu) v = fmaxf(v, 0.0f);
+        o[e] = (_Float16)v;
+      }
+      *reinterpret_cast<half4*>(tl + (32 * j + lr) * TS + 8 * q + 4 * h) = o;
+    }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane < 32 && m0 + lane < p.M) {  // one lane per channel: the pixels in order, as gap_nhwc_kernel
+    float s = 0.0f;
+    int px = 0;
+    for (; px + 8 <= p.P; px += 8) {  // 8 LDS reads in flight ahead of the (sequential) adds
+      _Float16 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = tl[(px + u) * TS + lane];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s = s + (float)v[u];
+    }
+    for (; px < p.P; ++px) s = s + (float)tl[px * TS + lane];
+    p.y[(long long)img * p.y_nstride + m0 + lane] = s / (float)p.P;
+  }
+}
+
+bool conv1x1_gap_f16_eligible(const Conv1x1GapF16& p) {
+  return p.N > 0 && p.C > 0 && p.C % 64 == 0 && p.P >= 1 && p.P <= 256 && p.M >= 1 && p.x_cs % 8 == 0 &&
+         p.x_cs >= p.C && p.x_nstride % 8 == 0 && (reinterpret_cast<uintptr_t>(p.x) & 15) == 0 && p.Kp >= p.C &&
+         p.Kp % 8 == 0 && p.Mp >= p.M && (long long)p.P * p.x_cs * 2 < (1LL << 31) &&
+         (long long)p.Mp * p.Kp * 2 < (1LL << 31) && p.y_nstride >= p.M;
+}
+
+template <int NF>
+static void launch_cg(const Conv1x1GapF16& p, hipStream_t s) {
+  const size_t lds = size_t(2) * 32 * NF * (64 + 8) * 2;
+  const unsigned grid = (unsigned)(p.N * ((p.M + 127) / 128));
+  hipLaunchKernelGGL((conv1x1_gap_f16_kernel<NF>), dim3(grid), dim3(256), lds, s, p);
+}
+
+void launch_conv1x1_gap_f16(const Conv1x1GapF16& p, hipStream_t s) {
+  switch ((p.P + 31) / 32) {
+    case 1: launch_cg<1>(p, s); break;
+    case 2: launch_cg<2>(p, s); break;
+    case 3: launch_cg<3>(p, s); break;
+    case 4: launch_cg<4>(p, s); break;
+    case 5: launch_cg<5>(p, s); break;
+    case 6: launch_cg<6>(p, s); break;
+    case 7: launch_cg<7>(p, s); break;
+    default: launch_cg<8>(p, s); break;
+  }
+}
+
 // Concat along channels of two dense NHWC values into a dense y (Ca + Cb channels per pixel).
 __global__ __launch_bounds__(256) void concat_nhwc_kernel(const _Float16* __restrict__ a, const _Float16* __restrict__ b,
                                                           _Float16* __restrict__ y, long long pixels, int Ca, int Cb) {

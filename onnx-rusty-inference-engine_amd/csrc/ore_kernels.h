@@ -260,6 +260,19 @@ void launch_ktab_nhwc(int2* ktab, int xmode, int C, int kh, int kw, int cs, int 
 void launch_maxpool_nhwc(const NhwcPoolParams& p, hipStream_t s);
 // GlobalAveragePool of NHWC f16 -> f32 y[n][c]
 void launch_gap_nhwc(const void* x, float* y, int N, int C, int HW, int cs, long long nstride, hipStream_t s);
+// f16 models: a 1x1 conv (+ Relu) whose only reader is GlobalAveragePool, in one launch
+// (conv1x1_gap_f16_kernel, ore_conv_f16.hip): SqueezeNet's conv10 -> relu10 -> pool10.  x NHWC f16
+// [N][P][x_cs], wp the f16 conv packing Wh[Mp][Kp] (K = C), y f32 [N][M] (image stride y_nstride)
+struct Conv1x1GapF16 {
+  const void* x;
+  const void* wp;
+  const float* bias;
+  float* y;
+  int N, C, P, M, Mp, Kp, x_cs, relu;
+  long long x_nstride, y_nstride;
+};
+bool conv1x1_gap_f16_eligible(const Conv1x1GapF16& p);
+void launch_conv1x1_gap_f16(const Conv1x1GapF16& p, hipStream_t s);
 // Concat along channels of two dense NHWC f16 values (pixels = N*H*W)
 void launch_concat_nhwc(const void* a, const void* b, void* y, long long pixels, int Ca, int Cb, hipStream_t s);
 void launch_conv_f16(const ConvParams& p, int cfg, int xmode, hipStream_t s);
@@ -354,6 +367,7 @@ constexpr int WINO_TILE_BASE = X3_TILE_BASE + X3_TILES;
 constexpr int WINO_TILES_N = 5;
 // fused-kernel ids after the Winograd tiles (ore.Model.TILE_NAMES): 41 is retired (the Winograd fire module)
 constexpr int FIRE_F16_TILE = 42, C1_POOL_F16_TILE = 43;
+constexpr int CONV_GAP_F16_TILE = 49;  // conv1x1_gap_f16_kernel: ore.Model.TILE_NAMES "conv1x1 gap f16"
 bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo);
 bool conv_wino_eligible(const ConvParams& p, int tile);
 int wino_packed_mp(int M);

@@ -118,6 +118,9 @@ struct Step {
   // f16 pooled first conv with the next 1x1 conv (+ Relu) fused in (conv_pair_pool_f16_kernel SQ):
   // out is that conv's output; the squeeze weights in launch_fire_pack_f16 layout
   bool c1sq = false;
+  // f16 1x1 conv (+ Relu) whose only reader was GlobalAveragePool (ORE_FUSE_CONV_GAP,
+  // conv1x1_gap_f16_kernel): out is the GAP's f32 [N][M] output
+  bool gap = false;
   const void* sq_w = nullptr;
   const float* sq_b = nullptr;
   int64_t sq_M = 0;
@@ -1007,6 +1010,32 @@ struct Planner {
     recount();
   }
 
+  // (8b) f16: a 1x1 conv (+ Relu) whose only reader is GlobalAveragePool runs with the GAP in its
+  // epilogue (conv1x1_gap_f16_kernel: SqueezeNet conv10 -> relu10 -> pool10; the 87 MB map is never
+  // stored).  Bit-identical to conv_f16 + gap_nhwc_kernel.  Not under ORE_KEEP_VALUES (the conv output
+  // would not exist to read back).
+  void conv_gap() {
+    if (!has(ORE_FUSE_CONV_GAP) || !m->f16 || has(ORE_KEEP_VALUES)) return;
+    for (size_t i = 0; i < m->steps.size(); ++i) {
+      Step& g = st(int(i));
+      if (g.kind != S_GAP) continue;
+      const int v = g.in0;
+      if (v < 0 || !private_value(v) || !val(v).nhwc || val(v).es != 2 || producer[v] < 0) continue;
+      Step& cv = st(producer[v]);
+      if (cv.kind != S_CONV || cv.out != v || !cv.plan.f16 || cv.plan.xmode != F16_X_NHWC_VEC || cv.epool || cv.pool ||
+          cv.c1sq || cv.kh != 1 || cv.kw != 1 || cv.sh != 1 || cv.sw != 1 || cv.win.pt != 0 || cv.win.pl != 0 ||
+          cv.win.Ho != cv.H || cv.win.Wo != cv.W || cv.C % 64 != 0 || cv.H * cv.W > 256)
+        continue;
+      cv.gap = true;
+      cv.out = g.out;
+      cv.bytes_per_img = 2.0 * double(cv.C * cv.H * cv.W) + 4.0 * double(cv.M);
+      cv.name = cv.name + "+" + g.name;
+      val(v).elided = true;
+      nop(g);
+    }
+    recount();
+  }
+
   // (9) algorithm selection, a load-time rule (never by timing): ORE_LOAD_X3 moves every conv / MatMul
   // not taken by an f32-MFMA fusion to its x3 plan; f32 models with Winograd on run every 3x3 /
   // stride-1 / pad-1 conv not taken by a direct-kernel fusion by Winograd F(2x2, 3x3)
@@ -1254,6 +1283,7 @@ ore_status plan(ore_model* m) {
   if (ore_status st = p.fire_f16()) return st;
   if (ore_status st = p.first_squeeze()) return st;
   p.pool_squeeze();
+  p.conv_gap();
   p.select_algorithms();
   p.alias_copies();
   p.concat_in_place();
@@ -1347,6 +1377,15 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
                                           s.epool ? &ep : nullptr);
         if (s.epool) s.ran_tile = last_conv_tile = EPOOL_TILE_BASE + 1;  // "epool patch": conv_f16's pooled epilogue
         return r;
+      }
+      if (s.plan.f16 && s.gap) {
+        const Conv1x1GapF16 q{x.p, s.wp, bias, y.p, int(n), int(s.C), int(s.H * s.W), int(s.M), s.plan.Mp,
+                              int((s.C + 31) / 32 * 32), int(x.ps), s.relu ? 1 : 0, x.nstride, y.nstride};
+        if (!conv1x1_gap_f16_eligible(q)) return err(m, ORE_ERR_INVALID, "internal: conv + GAP on an unsupported layout");
+        launch_conv1x1_gap_f16(q, ctx->stream);
+        ORE_HIP_CHECK(ctx, hipGetLastError());
+        s.ran_tile = last_conv_tile = CONV_GAP_F16_TILE;
+        return ORE_OK;
       }
       if (s.plan.f16)
         return run_conv_f16(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.ktab, s.M, s.kh, s.kw, bias,
@@ -1467,7 +1506,7 @@ std::vector<int> step_tile_family(const Step& s) {
     if (s.c1sq) return {C1_POOL_F16_TILE};
     return {EPOOL_TILE_BASE + 1, C1_POOL_F16_TILE};  // two launches (conversion + patch kernel) / one launch
   }
-  if (s.epool || s.pool) return c;  // other f16 pooled epilogues / the pooled 1x1: one kernel
+  if (s.epool || s.pool || s.gap) return c;  // other f16 pooled epilogues / the pooled 1x1 / conv + GAP: one kernel
   if (s.plan.x3) {  // the x3 tiles of the plan's kernel family (its packed layout)
     for (int t = 0; t < 4; ++t) c.push_back(X3_TILE_BASE + t + (s.plan.x3 == 2 ? 4 : 0));
     return c;
@@ -1909,6 +1948,7 @@ int32_t ore_model_step_tile(ore_model* m, int32_t i) {
   if (s.kind == S_FIRE) return s.fire_f16 ? FIRE_F16_TILE : s.fire_pool ? FIRE_POOL_TILE : FIRE_TILE;
   if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.plan.epv > 0) return epool_tile_id(s.plan.epv);
   if (s.kind == S_CONV && s.epool && s.ran_tile >= 0) return s.ran_tile;
+  if (s.kind == S_CONV && s.gap) return CONV_GAP_F16_TILE;
   return (s.kind == S_CONV || s.kind == S_MATMUL) ? s.plan.cfg : -1;
 }
 

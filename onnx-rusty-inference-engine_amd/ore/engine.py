@@ -327,7 +327,8 @@ class Model:
                   "wino 32x32 d4", "wino 32x32 d2", "wino16 32x16", "wino16 16x32",
                   "wino lds", None,  # 41: the Winograd fire module (retired)
                   "fire f16", "first conv pool f16", "epool window f32", "fire pool f32",
-                  "stream1x1 persist 32x128", "stream1x1 persist 64x64", "stream1x1 persist 16x256"]
+                  "stream1x1 persist 32x128", "stream1x1 persist 64x64", "stream1x1 persist 16x256",
+                  "conv1x1 gap f16"]
 
     def tiles(self):
         """Block tile per exec step (-1 for non-conv steps); names in TILE_NAMES."""

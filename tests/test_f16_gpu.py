@@ -209,6 +209,45 @@ def test_f16_fused_equals_unfused(gpu_ctx):
     np.testing.assert_array_equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("shape", [(3, 128, 7, 7, 200, True), (2, 64, 16, 16, 96, False), (1, 192, 1, 1, 33, True)])
+def test_f16_conv_gap_fused_equals_unfused(gpu_ctx, shape):
+    """ORE_FUSE_CONV_GAP (conv1x1_gap_f16_kernel: 1x1 conv + Relu + GlobalAveragePool in one launch) is
+    bit-identical to conv_f16 + gap_nhwc_kernel: partial 128-channel blocks, 1-8 pixel fragments, no Relu."""
+    import ore
+    N, C, H, W, M, relu = shape
+    rng = np.random.default_rng(C + M)
+    x = rng.standard_normal((N, 8, H, W)).astype(np.float32)
+    w0 = (rng.standard_normal((C, 8, 1, 1)) * 0.5).astype(np.float32)
+    b0 = rng.standard_normal((C,)).astype(np.float32)
+    w1 = (rng.standard_normal((M, C, 1, 1)) * 0.2).astype(np.float32)
+    b1 = rng.standard_normal((M,)).astype(np.float32)
+    mb = _chain_model((1, 8, H, W), [(w0, b0, [0] * 4, [1, 1], True), (w1, b1, [0] * 4, [1, 1], relu)])
+    outs, tiles = [], []
+    for fusion in (ore.FUSE_ALL, ore.FUSE_ALL & ~ore.FUSE_CONV_GAP):
+        m = ore.Model(gpu_ctx, mb, max_batch=N, precision="f16")
+        m.set_fusion(fusion)
+        outs.append(_np(m.run(_t(x))).reshape(N, M))
+        tiles.append([ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0])
+        m.close()
+    assert "conv1x1 gap f16" in tiles[0] and "conv1x1 gap f16" not in tiles[1]
+    np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def test_f16_conv_gap_squeezenet224(gpu_ctx):
+    """SqueezeNet @224 f16: conv10 + relu10 + pool10 fused == unfused, bit for bit."""
+    import ore
+    from ore import squeezenet
+    mb = squeezenet.build(224)
+    x = _t(squeezenet.synthetic_input(4, 224, seed=21))
+    outs = []
+    for fusion in (ore.FUSE_ALL, ore.FUSE_ALL & ~ore.FUSE_CONV_GAP):
+        m = ore.Model(gpu_ctx, mb, max_batch=4, precision="f16")
+        m.set_fusion(fusion)
+        outs.append(_np(m.run(x)))
+        m.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
+
+
 def test_f16_rejects_f32_only_ops(gpu_ctx):
     import ore
     with open(os.path.join(GOLD, "mnist-8.onnx"), "rb") as f:
