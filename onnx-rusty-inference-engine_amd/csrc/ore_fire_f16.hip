@@ -238,14 +238,18 @@ __global__ __launch_bounds__(256, 2) void fire_f16_kernel(FireF16Params p) {
   const __amdgpu_buffer_rsrc_t wsr = ff_rsrc(p.ws), w1r = ff_rsrc(p.w1), w3r = ff_rsrc(p.w3);
   const int arow = lr * 16 + 8 * h;  // this lane's 8 halves inside a [row][16] fragment block
 
-  ff16 sacc[MSF][2];
+  // MSF = 0: no squeeze -- the module writes its Concat (NHWC, pixel stride y_cs) instead (SqueezeNet
+  // fire9, whose reader conv10 is no small squeeze)
+  constexpr int MSA = MSF ? MSF : 1;
+  ff16 sacc[MSA][2];
 #pragma unroll
   for (int i = 0; i < MSF; ++i) ff_zero(sacc[i]);
+  _Float16* __restrict__ yimg = static_cast<_Float16*>(p.y) + (long long)img * p.y_nstride;
 
   // bias + Relu + one rounding of a finished 32-channel chunk (c0 inside its conv, cat0 inside the
-  // concat), then the squeeze's two k-steps over it
+  // concat), then the squeeze's two k-steps over it (MSF = 0: its 16-B stores into the concat)
   auto feed = [&](const ff16 (&acc)[2], const float* __restrict__ bias, int c0, int cat0) __attribute__((always_inline)) {
-    fh8 aq[2][MSF];
+    fh8 aq[2][MSA];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -262,6 +266,13 @@ __global__ __launch_bounds__(256, 2) void fire_f16_kernel(FireF16Params p) {
         for (int e = 0; e < 8; ++e) av[e] = acc[f][8 * t + e];
         bq[t][f] = ore_f16_epilogue8<false>(av, bv + 8 * t, true);
       }
+    if constexpr (MSF == 0) {
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          if (pok[f]) *reinterpret_cast<fh8*>(yimg + yo[f] + cat0 + 16 * t) = bq[t][f];
+    }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -280,7 +291,7 @@ __global__ __launch_bounds__(256, 2) void fire_f16_kernel(FireF16Params p) {
     ff_e3_chunk<NKC, 2, PS>(acc, w3r, p.E3, c0, arow, halo, hb, W2);
     feed(acc, sb + p.E1, c0, p.E1 + c0);
   }
-  ff_store_squeeze<MSF, 2>(sacc, p, static_cast<_Float16*>(p.y) + (long long)img * p.y_nstride, yo, pok, h);
+  if constexpr (MSF > 0) ff_store_squeeze<MSF, 2>(sacc, p, yimg, yo, pok, h);
 }
 
 // The pooled variant: Concat(e1, e3) -> 3x3 / stride-2 MaxPool -> squeeze.  One workgroup = a band
@@ -469,11 +480,13 @@ bool fire_pool_f16_plan(FireF16Params* p) {
 bool fire_f16_eligible(const FireF16Params& p) {
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   const bool common = p.C % 16 == 0 && p.C >= 16 && p.C <= 64 && p.E1 % 32 == 0 && p.E3 % 32 == 0 && p.E1 > 0 &&
-                      p.E1 + p.E3 <= FF_BIAS &&
-                      p.E3 > 0 && p.Ms % 8 == 0 && p.Ms > 0 && p.Ms <= 64 && p.Msp == (p.Ms + 31) / 32 * 32 &&
-                      p.x_cs % 8 == 0 && p.y_cs % 8 == 0 && p.x_cs >= p.C && p.y_cs >= p.Ms && p.x_nstride % 8 == 0 &&
-                      p.y_nstride % 8 == 0 && al16(p.x) && al16(p.y) && al16(p.w1) && al16(p.w3) && al16(p.ws) &&
-                      al16(p.b1) && al16(p.b3) && al16(p.bs) && p.H > 0 && p.W > 0 && p.N > 0 &&
+                      p.E1 + p.E3 <= FF_BIAS && p.E3 > 0 &&
+                      (p.Ms == 0 ? !p.pool && p.y_cs >= p.E1 + p.E3  // no squeeze: the Concat is the output
+                                 : p.Ms % 8 == 0 && p.Ms <= 64 && p.Msp == (p.Ms + 31) / 32 * 32 && p.y_cs >= p.Ms &&
+                                       al16(p.ws) && al16(p.bs)) &&
+                      p.x_cs % 8 == 0 && p.y_cs % 8 == 0 && p.x_cs >= p.C && p.x_nstride % 8 == 0 &&
+                      p.y_nstride % 8 == 0 && al16(p.x) && al16(p.y) && al16(p.w1) && al16(p.w3) &&
+                      al16(p.b1) && al16(p.b3) && p.H > 0 && p.W > 0 && p.N > 0 &&
                       (long long)p.H * p.W * p.x_cs < (1LL << 30) && (long long)p.H * p.W * p.y_cs < (1LL << 30);
   if (!common) return false;
   if (!p.pool) return fire_f16_lds_bytes(p.C, p.H, p.W) <= FIRE_F16_LDS_MAX;
@@ -500,7 +513,23 @@ static void launch_ff(FireF16Params p, hipStream_t s) {
   hipLaunchKernelGGL((fire_f16_kernel<NKC, MSF>), dim3((unsigned)(p.N * p.tiles_per_img)), dim3(256), lds, s, p);
 }
 
+template <int NKC>
+static void launch_ff_concat(FireF16Params p, hipStream_t s) {
+  p.tiles_per_img = (p.H * p.W + FF_PIX - 1) / FF_PIX;
+  const unsigned lds = (unsigned)fire_f16_lds_bytes(p.C, p.H, p.W);
+  hipLaunchKernelGGL((fire_f16_kernel<NKC, 0>), dim3((unsigned)(p.N * p.tiles_per_img)), dim3(256), lds, s, p);
+}
+
 void launch_fire_f16(const FireF16Params& p, hipStream_t s) {
+  if (p.Ms == 0) {  // the module without a squeeze: expands + Concat in one launch
+    switch (p.C / 16) {
+      case 1: launch_ff_concat<1>(p, s); break;
+      case 2: launch_ff_concat<2>(p, s); break;
+      case 3: launch_ff_concat<3>(p, s); break;
+      default: launch_ff_concat<4>(p, s); break;
+    }
+    return;
+  }
   const int msf = (p.Ms + 31) / 32;
   switch (p.C / 16 * 2 + msf - 1) {
     case 2: launch_ff<1, 1>(p, s); break;

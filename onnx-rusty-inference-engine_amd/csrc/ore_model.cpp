@@ -937,6 +937,62 @@ struct Planner {
     return ORE_OK;
   }
 
+  // (6b) f16 models: a fire module whose Concat no squeeze takes (SqueezeNet fire9, read by conv10):
+  // expand1x1 + expand3x3 (+ Relu) + Concat in one fire_f16_kernel<NKC, 0> launch that writes the
+  // Concat (NHWC) -- the two conv_f16 launches' arithmetic, bit-identical
+  ore_status fire_f16_concat() {
+    if (!has(ORE_FUSE_FIRE | ORE_FUSE_CONV_RELU) || !m->f16) return ORE_OK;
+    for (size_t i = 0; i < m->steps.size(); ++i) {
+      int pa, pb;
+      if (!fire_concat(int(i), &pa, &pb)) continue;
+      Step& cc = st(int(i));
+      Step &e1 = st(pa), &e3 = st(pb);
+      auto vec16 = [](const Step& s) {
+        return s.kind == S_CONV && s.relu && !s.pool && !s.epool && s.plan.f16 && s.plan.xmode == F16_X_NHWC_VEC &&
+               s.sh == 1 && s.sw == 1 && s.win.Ho == s.H && s.win.Wo == s.W;
+      };
+      const bool e1ok = vec16(e1) && e1.kh == 1 && e1.kw == 1 && e1.win.pt == 0 && e1.win.pl == 0;
+      const bool e3ok = vec16(e3) && e3.kh == 3 && e3.kw == 3 && e3.win.pt == 1 && e3.win.pl == 1;
+      if (!e1ok || !e3ok || e1.in0 != e3.in0 || e1.H != e3.H || e1.W != e3.W || e1.C != e3.C) continue;
+      if (e1.C % 16 || e1.C > 64 || e1.M % 32 || e3.M % 32 || e1.M + e3.M > 512 || e1.in2 < 0 || e3.in2 < 0) continue;
+      if (fire_f16_lds_bytes(int(e1.C), int(e1.H), int(e1.W)) > FIRE_F16_LDS_MAX) continue;
+      if (!private_value(cc.in0) || !private_value(cc.in1) || val(e1.in0).es != 2) continue;
+      for (int idx : {pa, pb}) {
+        const Step& e = st(idx);
+        const int kk = int(e.kh * e.kw), M = int(e.M), C = int(e.C);
+        const float* w = val(e.in1).cptr;
+        if (!pack_once(2000000 + idx, fire_pack_f16_bytes(M, C, kk),
+                       [&](float* buf) { launch_fire_pack_f16(w, M, C, kk, buf, m->ctx->stream); }))
+          return err(m, ORE_ERR_HIP, "f16 fire weight packing failed");
+      }
+      cc.kind = S_FIRE;
+      cc.fire_f16 = true;
+      cc.fire_pool = false;
+      cc.fire_H = e1.H;
+      cc.fire_W = e1.W;
+      cc.H = e1.H;
+      cc.W = e1.W;
+      cc.M = 0;  // no squeeze: the Concat is the output
+      cc.in0 = e1.in0;
+      cc.in1 = cc.in2 = -1;
+      cc.fire_C = e1.C;
+      cc.fire_E1 = e1.M;
+      cc.fire_E3 = e3.M;
+      cc.fire_w1 = m->fire_packs[2000000 + pa];
+      cc.fire_w3 = m->fire_packs[2000000 + pb];
+      cc.fire_ws16 = nullptr;
+      cc.fire_b1 = val(e1.in2).cptr;
+      cc.fire_b3 = val(e3.in2).cptr;
+      cc.flops_per_img = e1.flops_per_img + e3.flops_per_img;
+      cc.bytes_per_img = 2.0 * double(e1.C * e1.H * e1.W) + 2.0 * double((e1.M + e3.M) * e1.H * e1.W);
+      cc.name = e1.name.substr(0, e1.name.find('/')) + "/expand+concat";
+      val(e1.out).elided = val(e3.out).elided = true;
+      nop(e1); nop(e3);
+    }
+    recount();
+    return ORE_OK;
+  }
+
   // (7) the first conv + pool whose pooled map is read only by a small 1x1 conv (+ Relu) takes that
   // conv into its launch (SqueezeNet's conv1 + pool1 + fire2/squeeze1x1; the pooled map is never
   // stored).  Bit-identical to the separate squeeze (the same k-ordered chain over the same pooled
@@ -1281,6 +1337,7 @@ ore_status plan(ore_model* m) {
   p.concat_pool();
   if (ore_status st = p.fire_f32()) return st;
   if (ore_status st = p.fire_f16()) return st;
+  if (ore_status st = p.fire_f16_concat()) return st;
   if (ore_status st = p.first_squeeze()) return st;
   p.pool_squeeze();
   p.conv_gap();
@@ -1419,7 +1476,8 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       if (s.fire_f16)
         return run_fire_f16(ctx, x.p, n, s.fire_C, s.fire_pool ? s.fire_H : s.H, s.fire_pool ? s.fire_W : s.W,
                             x.nstride, x.ps ? x.ps : s.fire_C, s.fire_w1, s.fire_b1, s.fire_E1, s.fire_w3, s.fire_b3,
-                            s.fire_E3, s.fire_ws16, m->values[s.in2].cptr, s.M, y.p, y.nstride, y.ps ? y.ps : s.M,
+                            s.fire_E3, s.fire_ws16, s.in2 >= 0 ? m->values[s.in2].cptr : nullptr, s.M, y.p,
+                            y.nstride, y.ps ? y.ps : (s.M ? s.M : s.fire_E1 + s.fire_E3),
                             s.fire_pool ? &s.fire_pwin : nullptr);
       ctx->mapped_lo = m->arena_alloc;  // the arena and its 4 KiB lead are mapped
       ctx->mapped_hi = m->arena ? m->arena + m->arena_bytes : nullptr;

@@ -370,8 +370,8 @@ def test_f16_fire_fusion_exact_integers(gpu_ctx, case):
 
 def test_f16_squeezenet_fire_fusion(gpu_ctx):
     """SqueezeNet-1.0 @224, f16: the five fire + squeeze pairs run fire_f16_kernel, fire4 / fire8 with
-    their MaxPool and the next squeeze fire_pool_f16_kernel (fire9 feeds conv10: unfused), and the
-    probabilities equal the unfused graph's bit for bit."""
+    their MaxPool and the next squeeze fire_pool_f16_kernel, fire9 (read by conv10, no squeeze)
+    fire_f16_kernel's Concat-writing form, and the probabilities equal the unfused graph's bit for bit."""
     import ore
     from ore import squeezenet
     mb = squeezenet.build(224)
@@ -382,7 +382,7 @@ def test_f16_squeezenet_fire_fusion(gpu_ctx):
         m.set_fusion(fusion)
         outs.append(_np(m.run(x)))
         n = sum(1 for t in m.tiles() if t >= 0 and ore.Model.TILE_NAMES[t] == "fire f16")
-        assert n == (7 if fusion & ore.FUSE_FIRE else 0)  # + fire4 -> pool3 -> fire5, fire8 -> pool5 -> fire9
+        assert n == (8 if fusion & ore.FUSE_FIRE else 0)  # + fire4 -> pool3 -> fire5, fire8 -> pool5 -> fire9, fire9
         m.close()
     np.testing.assert_array_equal(outs[0], outs[1])
 
