@@ -25,12 +25,15 @@ METRIC = "SqueezeNet-1.0 fp32 images/s at batch 256, 1/2/4/8 MI355X; max-abs dif
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
 PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: f16/bf16 MFMA dense peak (no sparsity)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec peak
-# achievable peaks measured on MI355X by this repo's probes ("measure achievable
-# peaks (copy kernel, MFMA loop) and report both"): tools/peaks.sh (profiles/r01_peaks.txt: dependent-
-# free f32 / f16 MFMA loops) and tools/hbm_probe.hip (profiles/r03k_hbm_probe.txt: 2 GiB streams,
-# best of 4 / 8 / 16 workgroups per CU: read 6.1, write 4.6, copy 5.0 TB/s)
-ACHIEVABLE = {"f32_mfma_TFLOP/s": 143.5, "f16_mfma_TFLOP/s": 2037.6, "hbm_copy_GB/s": 5024.0,
-              "hbm_read_GB/s": 6149.0, "hbm_write_GB/s": 4634.0}
+# achievable peaks ("measure achievable peaks (copy kernel, MFMA loop) and report
+# both"): MI355X_MICROARCH.md's measured figures where it has one -- f32 MFMA 155 TF/s
+# (v_mfma_f32_32x32x2_f32 / 16x16x4_f32 back to back, 99 % of spec) and 6.29 TB/s (float4 copy) --
+# and this repo's probe for the f16 MFMA loop, which the guide does not measure (tools/peaks.sh,
+# profiles/r01_peaks.txt); this repo's read / write streams for reference (profiles/r03k_hbm_probe.txt)
+ACHIEVABLE = {"f32_mfma_TFLOP/s": 155.0, "f16_mfma_TFLOP/s": 2037.6, "hbm_copy_GB/s": 6290.0,
+              "hbm_read_GB/s": 6149.0, "hbm_write_GB/s": 4634.0,
+              "source": "MI355X_MICROARCH.md (f32 MFMA 155 TF/s, float4 copy 6.29 TB/s); f16 MFMA loop and "
+                        "read / write streams: this repo's probes (profiles/r01_peaks.txt, r03k_hbm_probe.txt)"}
 
 
 def parse():
@@ -43,7 +46,11 @@ def parse():
                     help="strong scaling: this many images per step split over the GPUs (SURVEY §8(d) B=2048)")
     ap.add_argument("--hw", type=int, default=224)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every CPU this process may use (affinity and cgroup quota; see usable_cpus)")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N > 1 collective: nccl = RCCL all_gather of the device rows (the product path); gloo = the "
+                         "rows staged through host memory (exercises the N > 1 branch with several ranks on one GPU)")
     ap.add_argument("--no-step-timing", action="store_true",
                     help="skip the per-kernel HIP-event pass (no roofline / breakdown)")
     ap.add_argument("--layers", action="store_true", help="print per-kernel-step times to stderr")
@@ -56,14 +63,14 @@ def parse():
                          "modules' expand1x1 beside their Winograd expand3x3 -- on a side stream (bit-identical; "
                          "71.1 k vs 70.5 k img/s at B = 256); 1: one stream")
     ap.add_argument("--no-f16-line", action="store_true",
-                    help="skip the config-5 fp16 measurement reported under \"f16\" of the f32 line (N=1 only)")
+                    help="skip the config-5 fp16 measurement reported under \"f16\" of the f32 line (run at N = 1 "
+                         "only, like the batch-1 probe and the CPU baseline)")
     ap.add_argument("--no-winograd", action="store_true",
                     help="f32: 3x3 stride-1 convs on the direct kernels only (ORE_LOAD_NO_WINOGRAD)")
     ap.add_argument("--fusion", type=int, default=None, help="ore_model_set_fusion flags (experiments; default: the model's)")
-    ap.add_argument("--precision", choices=["f32", "f32x3", "f16"], default="f32",
-                    help="f32: convs on the f32-input MFMA; f32x3: the same f32 model with its convs on the BF16 "
-                         "matrix cores by an exact 3-way bf16 split (ORE_LOAD_X3); f16: the fp16 variant "
-                         "(SURVEY.md §8(f)3, config 5)")
+    ap.add_argument("--precision", choices=["f32", "f16"], default="f32",
+                    help="f32: convs on the f32-input MFMA (the headline); f16: the fp16 variant (SURVEY.md §8(f)3, "
+                         "config 5)")
     return ap.parse_args()
 
 
@@ -76,35 +83,34 @@ def lib_sha256():
 
 
 def roofline_8d(infos, per_step_ms, ms_per_step, peak_tflops, peak_gbs=PEAK_HBM_GBS, ach_tflops=None):
-    """each launch is bound by its own FLOP:byte ratio, bound_time = max(algorithmic
-    FLOPs / MFMA peak, algorithmic bytes / HBM peak); achieved fraction = bound_time / measured time,
-    per launch, per op class and for the whole network (against the timed ms_per_step, launch gaps
-    included).  `issued` beside it counts the MFMA FLOPs the kernels execute (Winograd issues 16 C M
-    per 2x2 tile, not the direct 36 C M): the Winograd-honest use of the matrix cores; issued_frac is
-    the same fraction with that work as the FLOP bound (a Winograd layer's `frac` can exceed 1, its
-    issued_frac cannot)."""
+    """each launch is bound by its own FLOP:byte ratio, bound_time = max(MFMA FLOPs /
+    MFMA peak, algorithmic bytes / HBM peak); frac = bound_time / measured time, per launch, per op
+    class and for the whole network (against the timed ms_per_step, launch gaps included).  The FLOPs
+    are the MFMA work the kernels issue ("issued"): a direct conv issues its algorithmic 2 C M kh kw
+    per output, a Winograd F(2x2, 3x3) layer 16 C M per 2x2 tile instead of the direct 36 C M, so no
+    frac can exceed 1.  `effective_frac` beside it credits every layer with the direct-conv FLOPs (a
+    Winograd launch's can pass 1: it does less work than it is credited with)."""
     steps, classes = [], {}
-    tot_bound = tot_ibound = tot_abound = 0.0
+    tot_bound = tot_ebound = tot_abound = 0.0
     for info, ms in zip(infos, per_step_ms):
-        t_f = info["flops"] / (peak_tflops * 1e12) * 1e3
-        t_i = info.get("mfma_flops", info["flops"]) / (peak_tflops * 1e12) * 1e3  # MFMA work issued
+        t_e = info["flops"] / (peak_tflops * 1e12) * 1e3                              # algorithmic (direct)
+        t_i = info.get("mfma_flops", info["flops"]) / (peak_tflops * 1e12) * 1e3      # MFMA work issued
         t_b = info["bytes"] / (peak_gbs * 1e9) * 1e3
-        bound, ibound = max(t_f, t_b), max(t_i, t_b)
+        bound, ebound = max(t_i, t_b), max(t_e, t_b)
         tot_bound += bound
-        tot_ibound += ibound
-        if ach_tflops:  # the same issued-work bound against the measured achievable peaks (copy rate)
+        tot_ebound += ebound
+        if ach_tflops:  # the same bound against the measured achievable peaks (MFMA loop, copy rate)
             tot_abound += max(info.get("mfma_flops", info["flops"]) / (ach_tflops * 1e12) * 1e3,
                               info["bytes"] / (ACHIEVABLE["hbm_copy_GB/s"] * 1e9) * 1e3)
-        kind = "mfma" if t_f >= t_b else "hbm"
+        kind = "mfma" if t_i >= t_b else "hbm"
         steps.append({"name": info["name"], "op": info["op"], "bound": kind, "us": round(1000 * float(ms), 1),
                       "bound_us": round(1000 * bound, 1), "frac": round(bound / max(float(ms), 1e-9), 3),
-                      "issued_bound_us": round(1000 * ibound, 1),
-                      "issued_frac": round(ibound / max(float(ms), 1e-9), 3)})
-        c = classes.setdefault(info["op"], {"ms": 0.0, "bound_ms": 0.0, "ibound_ms": 0.0, "flops": 0.0,
+                      "effective_frac": round(ebound / max(float(ms), 1e-9), 3)})
+        c = classes.setdefault(info["op"], {"ms": 0.0, "bound_ms": 0.0, "ebound_ms": 0.0, "flops": 0.0,
                                             "mfma_flops": 0.0, "bytes": 0.0, "launches": 0})
         c["ms"] += float(ms)
         c["bound_ms"] += bound
-        c["ibound_ms"] += ibound
+        c["ebound_ms"] += ebound
         c["flops"] += info["flops"]
         c["mfma_flops"] += info.get("mfma_flops", info["flops"])
         c["bytes"] += info["bytes"]
@@ -113,24 +119,46 @@ def roofline_8d(infos, per_step_ms, ms_per_step, peak_tflops, peak_gbs=PEAK_HBM_
     for k, c in classes.items():
         per_class[k] = {"launches": c["launches"], "ms": round(c["ms"], 4), "bound_ms": round(c["bound_ms"], 4),
                         "frac": round(c["bound_ms"] / max(c["ms"], 1e-9), 4),
-                        "issued_bound_ms": round(c["ibound_ms"], 4),
-                        "issued_frac": round(c["ibound_ms"] / max(c["ms"], 1e-9), 4),
-                        "TFLOP/s": round(c["flops"] / (c["ms"] * 1e-3) / 1e12, 2) if c["flops"] else None,
+                        "effective_frac": round(c["ebound_ms"] / max(c["ms"], 1e-9), 4),
                         "issued_TFLOP/s": round(c["mfma_flops"] / (c["ms"] * 1e-3) / 1e12, 2) if c["flops"] else None,
+                        "effective_TFLOP/s": round(c["flops"] / (c["ms"] * 1e-3) / 1e12, 2) if c["flops"] else None,
                         "GB/s": round(c["bytes"] / (c["ms"] * 1e-3) / 1e9, 1)}
     net = {"bound_ms": round(tot_bound, 4), "ms_per_step": round(ms_per_step, 4),
            "frac": round(tot_bound / ms_per_step, 4),
-           "issued_bound_ms": round(tot_ibound, 4), "issued_frac": round(tot_ibound / ms_per_step, 4),
+           "effective_bound_ms": round(tot_ebound, 4), "effective_frac": round(tot_ebound / ms_per_step, 4),
            "kernel_ms": round(float(sum(per_step_ms)), 4)}
     peaks = {"mfma_TFLOP/s": peak_tflops, "hbm_GB/s": peak_gbs}
     if ach_tflops:
         net["achievable_bound_ms"] = round(tot_abound, 4)
         net["achievable_frac"] = round(tot_abound / ms_per_step, 4)
-        peaks["achievable"] = dict(ACHIEVABLE, used={"mfma_TFLOP/s": ach_tflops, "hbm_GB/s": ACHIEVABLE["hbm_copy_GB/s"]},
-                                   source="tools/peaks.sh (profiles/r01_peaks.txt), tools/hbm_probe.hip "
-                                          "(profiles/r03k_hbm_probe.txt)")
+        peaks["achievable"] = dict(ACHIEVABLE, used={"mfma_TFLOP/s": ach_tflops, "hbm_GB/s": ACHIEVABLE["hbm_copy_GB/s"]})
     return {"peaks": peaks, "network": net,
             "per_class": per_class, "per_launch": steps}, classes
+
+
+def usable_cpus():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota (v2 cpu.max or v1
+    cfs_quota / cfs_period) -- on the GPU box os.cpu_count() shows the whole machine, far more than the
+    share this job gets.  Returns (usable, details)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                p = int(f.read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    return usable, {"host_cpu_count": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota}
 
 
 def cpu_baseline(model_bytes, hw, threads):
@@ -256,12 +284,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
+    gloo = world > 1 and args.dist_backend == "gloo"
+    # gloo: ranks may share a GPU (the N > 1 branch rehearsed on a one-GPU box); nccl: one GPU per rank
+    dev = local % max(1, torch.cuda.device_count()) if gloo else local
+    torch.cuda.set_device(dev)
     # one non-default stream for everything (the model's launches, RCCL, torch ops): HIP-graph
     # capture needs a capturable stream
-    torch.cuda.set_stream(torch.cuda.Stream(device=local))
+    torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
 
     # one seeded global batch of G images (config 4: --global-batch 2048 split over the GPUs; by
     # default weak scaling, G = world x --batch), generated identically on every rank; each rank
@@ -273,13 +307,12 @@ def main():
     lo, hi = parallel.shard_bounds(G, world, rank)
     B = hi - lo
     model_bytes = squeezenet.build(args.hw)
-    ctx = ore.Context(local)
+    ctx = ore.Context(dev)
     model = ore.Model(ctx, model_bytes, max_batch=B, precision=args.precision, winograd=not args.no_winograd)
     f16 = args.precision == "f16"
-    x3 = args.precision == "f32x3"
-    g = torch.Generator(device=f"cuda:{local}")
+    g = torch.Generator(device=f"cuda:{dev}")
     g.manual_seed(1000)
-    xg = torch.rand((G, 3, args.hw, args.hw), generator=g, device=f"cuda:{local}") * 100.0 - 50.0
+    xg = torch.rand((G, 3, args.hw, args.hw), generator=g, device=f"cuda:{dev}") * 100.0 - 50.0
     x = xg[lo:hi].contiguous()
     # the max-abs sample: the first image of rank 0's slice and the last of the last rank's, so the
     # check covers the gathered rows of both ends of the global batch
@@ -287,9 +320,14 @@ def main():
     x_sample = xg[sample_idx].cpu().numpy() if rank == 0 else None
     del xg
     torch.cuda.empty_cache()
-    out = torch.empty((B, model.output_elems), dtype=torch.float32, device=f"cuda:{local}")
-    gathered = torch.empty((G, model.output_elems), dtype=torch.float32, device=f"cuda:{local}") \
-        if world > 1 else out
+    out = torch.empty((B, model.output_elems), dtype=torch.float32, device=f"cuda:{dev}")
+    if world == 1:
+        gathered = out
+    elif gloo:  # the rows staged through host memory for the gloo all-gather
+        out_host = torch.empty((B, model.output_elems), dtype=torch.float32)
+        gathered = torch.empty((G, model.output_elems), dtype=torch.float32)
+    else:
+        gathered = torch.empty((G, model.output_elems), dtype=torch.float32, device=f"cuda:{dev}")
 
     if args.fusion is not None:
         model.set_fusion(args.fusion)
@@ -314,7 +352,11 @@ def main():
         else:
             model.run_into(x, out)
         if world > 1:
-            parallel.gather_rows_into(gathered, out)
+            if gloo:
+                out_host.copy_(out)
+                parallel.gather_rows_into(gathered, out_host)
+            else:
+                parallel.gather_rows_into(gathered, out)
 
     for _ in range(args.warmup):
         step()
@@ -331,8 +373,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+    if world > 1:  # the max over ranks
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else f"cuda:{dev}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -348,7 +390,7 @@ def main():
             model.set_streams(1)  # the events sit between consecutive launches of one stream
         model.enable_timing(True)
         for _ in range(args.steps):
-            step(graph=False)  # the event hooks run between plain launches
+            model.run_into(x, out)  # the event hooks run between plain launches
             per_step_ms += np.asarray(model.step_times_ms())  # waits on the step's last event only
         torch.cuda.synchronize()
         model.enable_timing(False)
@@ -356,18 +398,19 @@ def main():
             model.set_streams(args.streams)
 
     if rank == 0:
-        value = world * B * args.steps / elapsed
+        value = G * args.steps / elapsed
         result = {
             "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f16" if f16 else "f32",
             "data": "synthetic (seeded U(-50,50) 3x224x224 images; seeded He-normal SqueezeNet-1.0 weights)",
             "config": {"workload": f"SqueezeNet-1.0 (66 nodes, 818.9 MMAC/img) "
-                                   f"{'fp16 (config 5: f16 activations/weights, f32 accumulate)' if f16 else 'fp32 (convs: exact 3-way bf16 split, 6 part products, f32 accumulate)' if x3 else 'fp32'} "
+                                   f"{'fp16 (config 5: f16 activations/weights, f32 accumulate)' if f16 else 'fp32'} "
                                    f"inference, batch {B} per GPU, 3x{args.hw}x{args.hw}",
-                       "model": "squeezenet1.0-8 topology, synthetic weights", "global_batch": world * B,
-                       "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}",
-                       "collective": f"RCCL all_gather of [{B},1000] logits per step" if world > 1 else None,
+                       "model": "squeezenet1.0-8 topology, synthetic weights", "global_batch": G,
+                       "per_gpu_batch": B, "run_batch": model.run_batch, "seq_len": None, "parallelism": f"dp{world}",
+                       "collective": (f"{'gloo (host-staged)' if gloo else 'RCCL'} all_gather of [{B},1000] logits per step"
+                                      if world > 1 else None),
                        "launch": "one HIP-graph replay per step" if use_graph else "plain launches",
                        "streams": args.streams},
         }
@@ -375,18 +418,15 @@ def main():
                                 "tile_per_conv": [ore.Model.TILE_NAMES[t] for t in model.tiles() if t >= 0]}
         if timing:
             per_step_ms /= args.steps
-            # x3: every f32 MAC is six bf16 part products on the 2.5 PF/s BF16 matrix cores
-            peak = PEAK_F16_MFMA_TFLOPS if f16 else PEAK_F16_MFMA_TFLOPS / 6.0 if x3 else PEAK_F32_MFMA_TFLOPS
-            ach = ACHIEVABLE["f16_mfma_TFLOP/s"] if f16 else None if x3 else ACHIEVABLE["f32_mfma_TFLOP/s"]
+            peak = PEAK_F16_MFMA_TFLOPS if f16 else PEAK_F32_MFMA_TFLOPS
+            ach = ACHIEVABLE["f16_mfma_TFLOP/s"] if f16 else ACHIEVABLE["f32_mfma_TFLOP/s"]
             r8d, classes = roofline_8d(infos, per_step_ms, 1000.0 * elapsed / args.steps, peak, ach_tflops=ach)
             conv = classes.get("Conv", {"ms": 1e-9, "flops": 0.0, "mfma_flops": 0.0, "bytes": 0.0, "launches": 1})
-            achieved = conv["flops"] / (conv["ms"] * 1e-3) / 1e12
+            effective = conv["flops"] / (conv["ms"] * 1e-3) / 1e12
             issued = conv["mfma_flops"] / (conv["ms"] * 1e-3) / 1e12
             kname = ("Conv class: conv_pair_pool_f16_kernel (conv1 + pool1 straight from the f32 input), "
                      "fire_f16_kernel / fire_pool_f16_kernel (fire module [+ MaxPool] + next squeeze) and "
                      "conv_f16_kernel (implicit GEMM), all MFMA 32x32x16 f16 with f32 accumulate" if f16 else
-                     "conv_x3_kernel (f32 implicit GEMM on MFMA 16x16x32 bf16: both operands split exactly into "
-                     "3 bf16 parts, 6 part products per f32 MAC; peak = 2500 / 6 TFLOP/s of f32 work" if x3 else
                      "Conv class: conv_win_pool_f32_kernel (conv1 + pool1 + fire2 squeeze), fire_kernel (fire "
                      "module + next squeeze), conv_winol_kernel (Winograd F(2x2,3x3) expand3x3, LDS-staged, MFMA "
                      "16x16x4 f32), conv_stream_kernel / conv_stream1x1_persist_kernel (LDS-free implicit GEMM, "
@@ -406,15 +446,17 @@ def main():
                         f"{'the same libore.so build as this run' if tsame else 'an earlier libore.so build'}")
             result["roofline"] = {
                 "bound": "mfma", "kernel": kname,
-                "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                "achieved": round(issued, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(issued / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                 "traffic_source": tsrc, "traffic_same_build": tsame,
-                "achieved_is": "effective: algorithmic (direct-conv) FLOPs / measured time; Winograd layers count "
-                               "their direct FLOPs",
-                "issued_TFLOP/s": round(issued, 2), "issued_frac": round(issued / peak, 4),
+                "achieved_is": "MFMA work the conv launches issue / their measured time (direct convs: 2*Cout*Ho*Wo*Cin*kh*kw; "
+                               "Winograd F(2x2,3x3) expand3x3: 16*C*M per 2x2 output tile)",
+                "effective_TFLOP/s": round(effective, 2), "effective_frac": round(effective / peak, 4),
+                "effective_is": "algorithmic direct-conv FLOPs (1.638 GFLOP/img) / the same time: credits Winograd "
+                                "layers with 2.25x the work they issue",
+                "achievable_peak": ach, "achievable_frac": round(issued / ach, 4),
                 "algorithmic_bytes_per_launch": round(conv["bytes"] / max(conv["launches"], 1)),
                 "per_launch_avg_us": round(1000.0 * conv["ms"] / conv["launches"], 2),
-                "algorithmic": "2*Cout*Ho*Wo*Cin*kh*kw per image (1.638 GFLOP/img)",
                 "kernel_timing": f"HIP events between consecutive launches on the model stream (one stream), a second pass of "
                                  f"the {args.steps} timed steps (events kept out of the value's timed loop)"}
             result["roofline_8d"] = r8d
@@ -432,24 +474,29 @@ def main():
         ref = oracle.Model(model_bytes).run(x_sample, 1000)
         result["max_abs_diff_vs_cpu"] = float(np.abs(got - ref).max())
         result["max_abs_sample"] = (f"global images {sample_idx} of the timed batch"
-                                    f"{' (gathered over RCCL)' if world > 1 else ''} vs the oracle "
-                                    f"(C restatement of the reference, f32)")
+                                    f"{' (gathered over ' + ('gloo' if gloo else 'RCCL') + ')' if world > 1 else ''} vs "
+                                    f"the oracle (C restatement of the reference, f32)")
         if f16:
             result["top1_agrees_with_cpu"] = bool((got.argmax(1) == ref.argmax(1)).all())
-        if not f16 and not x3 and not args.no_f16_line:
-            result["f16"] = f16_line(ctx, model_bytes, x, B, args, ref[:1])  # global image 0 = x[0] on rank 0
-        if not args.no_b1:
-            result["b1_latency_ms"] = b1_latency(model_bytes, args.hw, local, args.precision,
-                                                 winograd=not args.no_winograd)
-        if not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            result["cpu_baseline"] = cpu_baseline(model_bytes, args.hw, threads)
+        # the reporting legs run at N = 1 only (the CPU baseline on rank 0 at N = 1), so no
+        # rank waits on the others' collectives meanwhile
+        if world == 1:
+            if not f16 and not args.no_f16_line:
+                result["f16"] = f16_line(ctx, model_bytes, x, B, args, ref[:1])  # global image 0 = x[0]
+            if not args.no_b1:
+                result["b1_latency_ms"] = b1_latency(model_bytes, args.hw, dev, args.precision,
+                                                     winograd=not args.no_winograd)
+            if not args.no_cpu_baseline:
+                usable, cpu_info = usable_cpus()
+                threads = args.cpu_threads or usable
+                result["cpu_baseline"] = cpu_baseline(model_bytes, args.hw, threads)
+                result["cpu_baseline"].update(cpu_info, usable_cpus=usable)
         print(json.dumps(result), flush=True)
 
     model.close()
     ctx.close()
     if world > 1:
-        dist.barrier()  # the other ranks wait here while rank 0 runs the reporting legs
+        dist.barrier()
         dist.destroy_process_group()
 
 

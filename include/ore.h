@@ -32,7 +32,13 @@
 extern "C" {
 #endif
 
-#define ORE_ABI_VERSION 1
+/* ABI 2 (round 4) against ABI 1: the opt-in bf16x3 kernels are gone -- load flags 2 / 8 (ABI 1's
+ * ORE_LOAD_X3 / ORE_LOAD_X3_ALL) and conv tile ids 28-35 are rejected with ORE_ERR_UNSUPPORTED; so are
+ * ABI 1's retired fusion bit 16 (ORE_FUSE_POOL_CONV), MaxPool variant 1 and conv tile ids 4-11, which
+ * ABI 1 builds already refused.  ore_model_load accepts any max_batch: a batch whose activations
+ * would pass the kernels' 32-bit offsets runs in image chunks inside ore_model_run.  Every other
+ * entry point and value is unchanged. */
+#define ORE_ABI_VERSION 2
 
 typedef enum ore_status {
   ORE_OK = 0,
@@ -108,11 +114,11 @@ ore_status ore_ctx_set_conv_algo(ore_ctx* ctx, int32_t algo);
  *  ore_ctx_set_conv_tile: every conv planned on this context afterwards -- ore_conv2d_f32 /
  *    ore_matmul_f32 calls, and models loaded later -- uses tile id `tile` where it belongs to the
  *    layer's kernel family (else the per-layer heuristic); -1 (default) = the heuristic.  Ids as
- *    ore_model_step_tile reports them (0-3 LDS-staged, 12-20 streaming, 28-35 x3, 36-40 Winograd,
- *    46-48 persistent streaming 1x1).
+ *    ore_model_step_tile reports them (0-3 LDS-staged, 12-20 streaming, 36-40 Winograd, 46-48
+ *    persistent streaming 1x1); the retired ids 4-11 and 28-35 return ORE_ERR_UNSUPPORTED.
  *  ore_ctx_set_pool_variant: MaxPool kernel of ore_maxpool2d_f32 and of the walker's MaxPool steps:
  *    0 (default) = by layout, 2 one thread per output, 3 column strips, 4 plane-staged, 5
- *    chunk-staged. */
+ *    chunk-staged (1 is retired: ORE_ERR_UNSUPPORTED). */
 ore_status ore_ctx_set_conv_tile(ore_ctx* ctx, int32_t tile);
 ore_status ore_ctx_set_pool_variant(ore_ctx* ctx, int32_t variant);
 
@@ -159,7 +165,9 @@ ore_status ore_reshape(const ore_tensor* x, const int64_t* shape, int32_t n_shap
 
 /* ------------------------------------------------------------------ graph walker (inference()) */
 /* Parse an ONNX ModelProto (bytes), upload every initializer to HBM once, plan the value
- * buffers for up to max_batch images, and prepare the node list in file order.
+ * buffers for up to max_batch images, and prepare the node list in file order.  Any max_batch is
+ * accepted: the arena holds run_batch = min(max_batch, the largest batch whose every activation fits
+ * the kernels' 32-bit byte offsets) images (ore_model_run_batch), and larger runs go in image chunks.
  * Unsupported ops/attributes fail here (the reference panics when it reaches them). */
 ore_status ore_model_load(ore_ctx* ctx, const void* onnx_bytes, size_t len, int64_t max_batch,
                           ore_model** out);
@@ -175,27 +183,16 @@ ore_status ore_model_parse(const void* onnx_bytes, size_t len);
  * stay f32 (Add / MatMul / Softmax on an f16 value is rejected).  The model input and
  * graph.output[0] stay f32 (an f16 graph output is rejected). */
 #define ORE_LOAD_F16 1
-/* ORE_LOAD_X3: the f32 model on the BF16 matrix cores.  gfx950's f32-input MFMA runs at 1/16 of
- * the BF16 rate; every f32 weight and activation operand of a Conv / MatMul is split exactly into
- * three bf16 parts (hi + mid + lo) and the six part products whose orders sum to <= 2 are
- * accumulated in f32 (v_mfma_f32_16x16x32_bf16).  The dropped products are below 2^-24 of each
- * a*b, so every output is the f32 dot product to within f32 accumulation rounding (tested against a
- * float64 reference next to the f32-MFMA kernels' own error, tests/test_x3_gpu.py), at 0.375 of the
- * f32-MFMA cost.  Storage, every other op and the model input / output stay f32; results are
- * tile-independent but not bit-identical to the f32-MFMA kernels (a different summation order).
- * The fire / pooled-conv fusions are f32-MFMA kernels and are not applied to an x3 model. */
-#define ORE_LOAD_X3 2
 /* ORE_LOAD_NO_WINOGRAD: an f32 model runs its 3x3 / stride-1 / pad-1 convs (SqueezeNet's
  * expand3x3) on the direct kernels only, every output in the reference's k order.  By default (f32
- * models, not x3) every such conv with C % 16 == 0 that no direct-kernel fusion takes runs Winograd
+ * models) every such conv with C % 16 == 0 that no direct-kernel fusion takes runs Winograd
  * F(2x2, 3x3) in f32 (ore_conv_wino.hip; see ORE_CONV_ALGO_WINOGRAD above).  NOTE: this makes the
  * default f32 results differ from the direct path by rounding (synthetic SqueezeNet @224: 6e-6
  * max-abs against the oracle vs 2e-7 direct, within the 1e-5 parity bound); load with this flag for
  * the reference's summation order.  The choice is made at load time, never by timing. */
 #define ORE_LOAD_NO_WINOGRAD 4
-/* ORE_LOAD_X3_ALL: ORE_LOAD_X3 on every conv / MatMul, with no f32-MFMA fusion (tests of the x3
- * kernels). */
-#define ORE_LOAD_X3_ALL 8
+/* ABI 1's ORE_LOAD_X3 (2) and ORE_LOAD_X3_ALL (8): retired, rejected with ORE_ERR_UNSUPPORTED. */
+#define ORE_LOAD_RETIRED_MASK 10
 ore_status ore_model_load_ex(ore_ctx* ctx, const void* onnx_bytes, size_t len, int64_t max_batch, int32_t flags,
                              ore_model** out);
 ore_status ore_model_destroy(ore_model* m);
@@ -203,8 +200,8 @@ ore_status ore_model_destroy(ore_model* m);
  * for op-by-op parity).  Every fusion is exact: the fused kernels compute each output by the same
  * arithmetic as the separate ones, so results do not depend on the flags (tested bit for bit).
  * bit 0 = fuse Conv->Relu, bit 1 = Concat in place (and padded channel planes), bit 2 = alias
- * Dropout / Reshape; bits 5-10 below.  Bit 4 is retired (a MaxPool inside a 1x1 conv's operand
- * gather, measured slower). */
+ * Dropout / Reshape; bits 5-10 and 12 below.  Bit 4 (ABI 1's ORE_FUSE_POOL_CONV, a MaxPool inside a
+ * 1x1 conv's operand gather, measured slower) is retired: ORE_ERR_UNSUPPORTED. */
 #define ORE_FUSE_CONV_RELU 1
 #define ORE_FUSE_CONCAT 2
 #define ORE_FUSE_ALIAS 4
@@ -225,7 +222,9 @@ ore_status ore_model_destroy(ore_model* m);
  * Bit-identical (every output keeps its k-ordered MFMA chain; the squeeze still sums the concat
  * channels in ascending order).  f32 (fire_kernel) and f16 (fire_f16_kernel) models; f32: applied when
  * max_batch * H * W >= 65536 (one 64-pixel wave per SIMD), below which the fused launch has too few
- * waves (batch 1 keeps the separate kernels). */
+ * waves (batch 1 keeps the separate kernels).  f16 models also take a fire module whose Concat is
+ * read by something other than a squeeze (SqueezeNet's fire9, read by conv10): its expands and the
+ * Concat run as one fire_f16_kernel launch that stores the Concat. */
 #define ORE_FUSE_FIRE 64
 /* bit 7 (in ORE_FUSE_ALL): Concat(e1, e3) -> 3x3 / stride-2 MaxPool with e1 / e3 Convs
  * (+ Relu) read only by the Concat (SqueezeNet's fire4 -> pool3, fire8 -> pool5): each conv's pooled
@@ -260,10 +259,15 @@ ore_status ore_model_input_dims(ore_model* m, int64_t dims[4]);
 /* Elements per image of graph.output[0] (the reference only prints it; we keep it). */
 ore_status ore_model_output_elems(ore_model* m, int64_t* elems);
 /* Run all nodes on n <= max_batch images.  d_input/d_output are device pointers
- * (n * input elems / n * output elems).  Asynchronous on the context stream. */
+ * (n * input elems / n * output elems).  Asynchronous on the context stream.  n > run_batch runs the
+ * graph once per chunk of at most run_batch consecutive images (each image's arithmetic is the same
+ * in any chunk). */
 ore_status ore_model_run(ore_model* m, const float* d_input, int64_t n, float* d_output);
+/* Images one pass of the graph covers (see ore_model_load). */
+int64_t ore_model_run_batch(ore_model* m);
 /* Copy a named value of the last run to host memory (for node-level parity checks; values
- * elided by fusion are unavailable -> ORE_ERR_INVALID).  Synchronises. */
+ * elided by fusion, and values of a run chunked over run_batch, are unavailable -> ORE_ERR_INVALID).
+ * Synchronises. */
 ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst, size_t cap_elems,
                                 int64_t dims[4], int32_t* ndim);
 /* Per-node timing with HIP events on the context stream (enable, run, then query).

@@ -32,32 +32,9 @@ typedef int int4d __attribute__((ext_vector_type(4)));
 // from a 13 x 19 = 247-column conv-output patch of a 256-column N tile
 constexpr int EPOOL_PR = EPOOL_TILE_PR, EPOOL_PC = EPOOL_TILE_PC, EPOOL_RC = 2 * EPOOL_PR + 1, EPOOL_CC = 2 * EPOOL_PC + 1;
 
-#ifndef ORE_A_DMA
-#define ORE_A_DMA 1  // A (weight) tile by 16-B LDS-DMA too (0: registers + ds_write_b128)
-#endif
-
-#ifdef ORE_EXP_BFIXED  // timing experiment: B loads without the gather index math
-#define ORE_EXP_BFIXED_HOOK ok = bn_ok; off = (xoff > 0 ? xoff : 0) + ((k >> 4) & 1) * XPS;  /* channel 0/1, clamped: in bounds */
-#else
-#define ORE_EXP_BFIXED_HOOK
-#endif
-#ifdef ORE_EXP_SETPRIO  // timing experiment: raise wave priority around MFMA clusters
-#define ORE_PRIO(X) __builtin_amdgcn_s_setprio(X)
-#else
-#define ORE_PRIO(X)
-#endif
-
-#ifndef ORE_NO_FRAG_PIN
+constexpr bool A_DMA = true;  // A (weight) tile by 16-B LDS-DMA too (false: registers + ds_write_b128)
 #define ORE_FRAG_PIN __builtin_amdgcn_sched_barrier(0)
-#else
-#define ORE_FRAG_PIN
-#endif
-#ifndef ORE_VEC_EPI_ON
-#define ORE_VEC_EPI_ON 1
-#endif
-#ifndef ORE_CONV_MINBLOCKS
-#define ORE_CONV_MINBLOCKS 2  // __launch_bounds__ minimum blocks per CU (VGPR budget)
-#endif
+constexpr int CONV_MINBLOCKS = 2;  // __launch_bounds__ minimum blocks per CU (VGPR budget)
 
 enum { B1X1 = 0, BGATHER = 1 };
 
@@ -65,13 +42,13 @@ enum { B1X1 = 0, BGATHER = 1 };
 // pass); a tap outside the image gets an out-of-range offset, which the buffer bounds check
 // turns into a 0 -- the reference's zero padding -- with no select.
 template <int BM, int BN, int WM, int WN, int BK, int BMODE, int DMA, int EP = 0>
-__global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(ConvParams p) {
+__global__ __launch_bounds__(256, CONV_MINBLOCKS) void conv_gemm_kernel(ConvParams p) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 32, FN = TN / 32;
   // ADMA: the A tile also goes global -> LDS by 16-B LDS-DMA (lane-linear, so unpadded rows; the
   // fragment reads -- 32 consecutive floats per half-wave -- are conflict-free without padding)
   // (measured: 96-row tiles gain 1-3 %, the 128x128 tile loses 4 % on fire4/expand3x3 -> off there)
-  constexpr bool ADMA = DMA && ORE_A_DMA && BM != 128;
+  constexpr bool ADMA = DMA && A_DMA && BM != 128;
   constexpr int AS = ADMA ? BM : BM + 4;     // LDS row stride of the A tile (16-B aligned rows)
   constexpr int BROWS = 256 / BN;            // B rows loaded per pass
   constexpr int BLOADS = BK / BROWS;         // B elements per thread per tile
@@ -205,7 +182,6 @@ __global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(Conv
         ok = bn_ok & ((unsigned)(ih0 + r) < (unsigned)p.H) & ((unsigned)(iw0 + s) < (unsigned)p.W);  \
         off = xoff + ex_;                                                                            \
       }                                                                                              \
-      ORE_EXP_BFIXED_HOOK                                                                            \
       if (DMA) {                                                                                     \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                    \
             xrsrc, (__attribute__((address_space(3))) void*)&Bs[(DBUF)][krow + j * BROWS][wcol0], 4,   \
@@ -265,19 +241,16 @@ __global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(Conv
           bf[cur ^ 1][j] = Bs[BUF][kk + 2 + lrow][wn0 + j * 32 + lcol];                              \
       }                                                                                              \
       ORE_FRAG_PIN; /* next k-step's fragment reads stay ahead of this k-step's MFMAs */             \
-      ORE_PRIO(1);                                                                                   \
       if (kk < (KEND)) {                                                                             \
         _Pragma("unroll") for (int i = 0; i < FM; ++i)                                               \
         _Pragma("unroll") for (int j = 0; j < FN; ++j)                                               \
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0); \
       }                                                                                              \
-      ORE_PRIO(0);                                                                                   \
     }                                                                                                \
   }
   // steady state: prefetch tile t+1 into registers, MFMAs on tile t, publish t+1 to LDS
   for (int t = 0; t < ntk - 1; ++t) {
     const int buf = t & 1;
-#ifndef ORE_EXP_NOLOAD  // timing experiments only (tools/build_exp.sh)
     floatx4 ra[AVEC];
     float rb[BLOADS];
     bool rok[BLOADS];
@@ -285,13 +258,8 @@ __global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(Conv
     __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads ahead of this tile's MFMAs
     ORE_COMPUTE_TILE(buf, BK);
     ORE_STORE_TILE(ra, rb, rok, buf ^ 1);
-#else
-    ORE_COMPUTE_TILE(0, BK);
-#endif
-#ifndef ORE_EXP_NOSYNC
     if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-#endif
   }
   {
     const int kend = __builtin_amdgcn_readfirstlane((K - (ntk - 1) * BK + 1) & ~1);
@@ -312,16 +280,6 @@ __global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(Conv
     constexpr int SROW = BN + 4;
     static_assert(32 * SROW <= MAIN_FLOATS && EPOOL_RC * EPOOL_CC <= BN, "pooled epilogue staging");
     __syncthreads();  // every wave is done with the A/B tiles
-#ifdef ORE_EXP_EP_NOPOOL  // timing experiment: main loop only
-    {
-      float t_ = 0.0f;
-      for (int i = 0; i < FM; ++i)
-        for (int j = 0; j < FN; ++j)
-          for (int e = 0; e < 16; ++e) t_ += acc[i][j][e];
-      if (t_ == 1234.5f) y[tid] = t_;
-    }
-    return;
-#endif
     const int ohb = ep_ph0 * 2 - p.ep_pt, owb = ep_pw0 * 2 - p.ep_pl;  // conv position of patch (0, 0)
     bool cok[FN];
 #pragma unroll
@@ -362,7 +320,7 @@ __global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(Conv
     }
     return;
   }
-  if (ORE_VEC_EPI_ON && p.vec_out) {
+  if (p.vec_out) {
     // 16-B stores: each wave stages 32 output rows x TN pixels in its own LDS slice (column
     // halves swapped every 4 rows so the two lane halves' writes hit different banks), then
     // writes whole pixel runs with float4 stores.  Host guarantees y_ps % 4 == 0, 16-B aligned
@@ -423,9 +381,6 @@ __global__ __launch_bounds__(256, ORE_CONV_MINBLOCKS) void conv_gemm_kernel(Conv
         if (m0 + ml < p.M) {
           float v = acc[i][j][e] + sbias[ml];
           if (p.relu) v = fmaxf(v, 0.0f);
-#ifdef ORE_EXP_NOEPI
-          if (v == 1234.5678f)
-#endif
           y[yb + (unsigned)((m0 + ml) * YPS)] = v;
         }
       }
@@ -566,38 +521,15 @@ static const int CFG_BM[4] = {128, 96, 64, 32};
 
 
 ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
-                   bool is1x1, bool f16, int xmode, bool x3, bool wino, int forced) {
+                   bool is1x1, bool f16, int xmode, bool wino, int forced) {
   (void)pt;
   ConvPlan pln{};
-  if (wino && !x3 && !f16 && conv_wino_geometry(C, kh, kw, sh, sw, pt, pl, H, W, Ho, Wo)) {
+  if (wino && !f16 && conv_wino_geometry(C, kh, kw, sh, sw, pt, pl, H, W, Ho, Wo)) {
     pln.wino = 1;
     pln.cfg = WINO_TILE_BASE + 0;
     if (forced >= WINO_TILE_BASE && forced < WINO_TILE_BASE + WINO_TILES_N) pln.cfg = forced;
     pln.Mp = wino_packed_mp(M);
     pln.krows = 16 * C;  // U is 16 positions x C rows of Mp floats
-    return pln;
-  }
-  if (x3 && !f16) {  // ore_conv_x3.hip: packed rows cover every x3 tile (64 / 96 / 128 rows)
-    pln.x3 = 1;
-    pln.cfg = X3_TILE_BASE + x3_tile_config(M);
-    pln.Mp = std::max((M + 127) / 128 * 128, (M + 95) / 96 * 96);
-    pln.krows = conv_packed_kp(C * kh * kw);
-    // stride-1 geometry whose window fits: the window-staged kernel (each input element split once
-    // per block instead of once per tap), unless a gather tile (X3_TILE_BASE + 0..3) is forced
-    const bool gather_forced = forced >= X3_TILE_BASE && forced < X3_TILE_BASE + 4;
-    if (x3w_geometry(C, kh, kw, sh, sw) && !gather_forced) {
-      const int t = (Ho * Wo < 256 ? 6 : 4) + (M <= 64 ? 1 : 0);
-      if (x3w_plan_lds(Ho, Wo, kh, kw, C, t) <= 80 * 1024) {
-        pln.x3 = 2;
-        pln.cfg = X3_TILE_BASE + t;
-        pln.bch = x3w_groups(C);
-        pln.nst = (C + 8 * pln.bch - 1) / (8 * pln.bch);
-        pln.ks = (kh * kw * pln.bch + 3) / 4;
-        pln.krows = pln.nst * pln.ks * 32;
-      }
-    }
-    const int fam = X3_TILE_BASE + (pln.x3 == 2 ? 4 : 0);  // forced: within the plan's kernel family
-    if (forced >= fam && forced < fam + 4) pln.cfg = forced;
     return pln;
   }
   pln.f16 = f16 ? 1 : 0;
@@ -621,21 +553,13 @@ ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, i
 }
 
 size_t conv_packed_bytes(const ConvPlan& pln) {
-  return (size_t)pln.krows * pln.Mp * (pln.x3 ? 3 * 2 : pln.f16 ? sizeof(_Float16) : sizeof(float));
+  return (size_t)pln.krows * pln.Mp * (pln.f16 ? sizeof(_Float16) : sizeof(float));
 }
 
 void launch_pack(const float* w, bool kmajor_src, int M, int C, int kh, int kw, const ConvPlan& pln, float* wp,
                  hipStream_t s) {
   if (pln.wino) {
     launch_pack_wino(w, M, C, pln.Mp, wp, s);
-    return;
-  }
-  if (pln.x3 == 2) {
-    launch_pack_x3w(w, M, C, kh, kw, pln.Mp, pln.bch, pln.ks, pln.nst, wp, s);
-    return;
-  }
-  if (pln.x3) {
-    launch_pack_x3(w, kmajor_src, M, C * kh * kw, pln.Mp, wp, s);
     return;
   }
   if (pln.f16) {
@@ -654,21 +578,6 @@ void launch_conv(const ConvParams& p, const ConvPlan& pln, hipStream_t s) {
     int t = pln.cfg - WINO_TILE_BASE;  // the caller (run_conv) checked conv_wino_eligible
     last_conv_tile = WINO_TILE_BASE + t;
     launch_conv_wino(p, t, s);
-    return;
-  }
-  if (pln.x3) {  // the caller (run_conv) checked conv_x3_eligible
-    int t = pln.cfg - X3_TILE_BASE;
-    if (pln.x3 == 2) {
-      ConvParams q = p;
-      q.bch = pln.bch; q.nst = pln.nst; q.ks = pln.ks;
-      if (t < 4 || !conv_x3w_eligible(q, t)) t = conv_x3w_eligible(q, 6) ? 6 : 7;  // a window tile that fits
-      last_conv_tile = X3_TILE_BASE + t;
-      launch_conv_x3(q, t, s);
-      return;
-    }
-    if (t >= 4) t = 0;
-    last_conv_tile = X3_TILE_BASE + t;
-    launch_conv_x3(p, t, s);
     return;
   }
   if (pln.f16) {

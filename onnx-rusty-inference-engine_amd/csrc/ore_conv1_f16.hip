@@ -82,14 +82,10 @@ struct C1Geom {
   int w_halves, halo_halves, lds_bytes;
 };
 
-// A fragments: staged in LDS once per persistent workgroup (default), or read from L2 per k-step
-// (-DORE_EXP_C1_WL2, a timing experiment: three workgroups per CU instead of two by LDS, but 158
-// VGPRs; measured 236 vs 179 us for conv1 + pool1 + squeeze at B = 256)
-#ifdef ORE_EXP_C1_WL2
-constexpr bool C1_WLDS = false;
-#else
+// A fragments: staged in LDS once per persistent workgroup (read from L2 per k-step instead, three
+// workgroups per CU fit by LDS but 158 VGPRs: measured 236 vs 179 us for conv1 + pool1 + squeeze at
+// B = 256)
 constexpr bool C1_WLDS = true;
-#endif
 
 __host__ __device__ inline C1Geom c1_geom(int MF, int kh, int kwp, int sh, int sw, bool sq = false) {
   C1Geom g;
@@ -203,11 +199,7 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
       const int o = in ? (ih * p.W + iw) * 4 : (int)0x80000000;
 #pragma unroll
       for (int ch = 0; ch < 4; ++ch)
-#ifdef ORE_EXP_C1_NOLOAD
-        xv[u][ch] = (in && ch < p.C) ? (float)(ih + iw + ch) : 0.0f;
-#else
         xv[u][ch] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, o, ch * p.x_ps * 4, 0));
-#endif
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -266,11 +258,7 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
         const c1h8 a = C1_WLDS ? *reinterpret_cast<const c1h8*>(Ws + ((ks * MF + i) * 32 + lr) * 16 + 8 * h) : ag[ks & 1][i];
 #pragma unroll
         for (int f = 0; f < 2; ++f)
-#ifdef ORE_EXP_C1_NOMFMA  // timing experiments only (tools/build_exp.sh)
-          acc[i][f][0] += (float)a[0] * (float)b[f][1];
-#else
           acc[i][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[f], acc[i][f], 0, 0, 0);
-#endif
       }
     }
 
@@ -328,11 +316,7 @@ __global__ __launch_bounds__(256, 2) void conv_pair_pool_f16_kernel(ConvParams p
           }
         }
       }
-#ifdef ORE_EXP_C1_NOPOOL
-      if (tid < 0) {
-#else
       if (!SQ && tid < ctile_tasks) {
-#endif
         const int pp = tid >> 2, cg = tid & 3;
         const int a = pp / C1_PC, b = pp - a * C1_PC;
         const c1h8 o = c1_pool8(ct + ((2 * a) * C1_CC + 2 * b) * C1_TS + cg * 8, p.relu != 0);

@@ -190,11 +190,7 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
       for (int i = 0; i < MF; ++i)
 #pragma unroll
         for (int f = 0; f < 2; ++f)
-#ifdef ORE_EXP_C3_NOMFMA
-          acc[i][f][0] += a[q & 1][i][ii] * b[f];
-#else
           acc[i][f] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q & 1][i][ii], b[f], acc[i][f], 0, 0, 0);
-#endif
       if (ii == 3 && q + 2 < G::KQ) {
 #pragma unroll
         for (int i = 0; i < MF; ++i)
@@ -262,11 +258,7 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
           sacc = __builtin_amdgcn_mfma_f32_16x16x4f32(aq, bq, sacc, 0, 0, 0);
         }
       }
-#ifdef ORE_EXP_C3_NOPOOL  // timing experiments only (tools/build_exp.sh)
-      for (int t = tid; t < 0; t += 256) {
-#else
       for (int t = tid; !SQ && t < C3_PR * C3_PC * 8; t += 256) {
-#endif
         const int cg = t / (C3_PR * C3_PC), pp = t - cg * (C3_PR * C3_PC);
         const int aa = pp / C3_PC, bb = pp - aa * C3_PC;
         c3f4 mx = {-FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX};
@@ -334,9 +326,6 @@ static bool c3_launch(const ConvParams& p, const float* wc, const C1SqueezeF32& 
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_win_pool_f32_kernel<MF, C, 7, 7, 2, SQ>, 256, lds) !=
           hipSuccess || per_cu < 1)
     per_cu = 2;
-#ifdef ORE_C3_WPC
-  per_cu = ORE_C3_WPC;  // experiment knob
-#endif
   long long grid = std::min<long long>(tiles, (long long)per_cu * ncu);
   if (grid >= 8) grid &= ~7LL;  // a multiple of 8: XCD-grouped tile ranges
   if (grid < 1) grid = 1;

@@ -31,9 +31,6 @@
 
 #include "ore_kernels.h"
 
-#ifndef ORE_H_PREFETCH2
-#define ORE_H_PREFETCH2 0  // 1: two K stages of loads in flight (measured slower; see the main loop)
-#endif
 
 namespace ore {
 
@@ -162,22 +159,8 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
       const int c = (ACH % 256 == 0 || tid + v * 256 < ACH) ? tid + v * 256 : 0;
-#ifdef ORE_EXP_H_NOA
-      ra[v] = (half8){} + (_Float16)(k0 + c);
-#else
       ra[v] = *reinterpret_cast<const half8*>(wh + (unsigned)((m0 + (c >> 2)) * Kp + k0 + (c & 3) * 8));
-#endif
     }
-#ifdef ORE_EXP_H_NOB
-    if constexpr (XMODE == F16_X_NHWC_VEC) {
-#pragma unroll
-      for (int u = 0; u < BV; ++u) {
-        rb.v[u] = (half8){} + (_Float16)(k0 + u);
-        rb.ok[u] = nok[u];
-      }
-      return;
-    }
-#endif
     if constexpr (LANEG) {
       // the stage's four group entries by scalar loads; this lane's picked by g
       const int kb = k0 >> 3;
@@ -260,42 +243,12 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-#ifdef ORE_EXP_H_NOMFMA
-          acc[i][j][0] += (float)af[i][0] * (float)bf[j][1];
-#else
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-#endif
     }
   };
 
   const int ntk = Kp / BK;
   __syncthreads();  // sbias
-#if ORE_H_PREFETCH2
-  // Two stages of loads in flight: at stage t the registers of slot t & 1 are refilled with
-  // stage t + 2 while stage t + 1 (loaded one stage earlier) is published to the other LDS buffer
-  // after the MFMAs of stage t.  Unrolled by two so the register slots are static.  Opt-in: it
-  // raised the 128x128 kernel from 132 to 206 VGPRs and measured slower.
-  half8 ra0[AV], ra1[AV];
-  BStage<XMODE, BV> rb0, rb1;
-  load_stage(ra0, rb0, 0);
-  if (ntk > 1) load_stage(ra1, rb1, BK);
-  store_stage(ra0, rb0, 0);
-  __syncthreads();
-  for (int t = 0; t < ntk; t += 2) {
-    if (t + 2 < ntk) load_stage(ra0, rb0, (t + 2) * BK);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(0);
-    if (t + 1 >= ntk) break;
-    store_stage(ra1, rb1, 1);
-    __syncthreads();
-    if (t + 3 < ntk) load_stage(ra1, rb1, (t + 3) * BK);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(1);
-    if (t + 2 >= ntk) break;
-    store_stage(ra0, rb0, 0);
-    __syncthreads();
-  }
-#else
   // stage t + 1 is loaded into registers ahead of stage t's MFMAs and published to the other
   // LDS buffer after them
   half8 ra[AV];
@@ -309,13 +262,10 @@ __global__ __launch_bounds__(256, 2) void conv_f16_kernel(ConvParams p) {
     __builtin_amdgcn_sched_barrier(0);  // the next stage's loads issue ahead of this stage's MFMAs
     compute(t & 1);
     if (more) {
-#ifndef ORE_EXP_H_NOSTORE  // timing experiments only (tools/build_exp.sh)
       store_stage(ra, rb, (t + 1) & 1);
-#endif
       __syncthreads();
     }
   }
-#endif
 
   if constexpr (EP) {
     // pooled epilogue: every conv position of the patch goes to LDS as [position][channel] f16

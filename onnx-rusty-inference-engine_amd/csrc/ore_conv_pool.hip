@@ -71,9 +71,7 @@ __device__ __forceinline__ void cp_load_a(__amdgpu_buffer_rsrc_t r, int voff, in
 // stride 1 'same' (pads <= 1; taps outside the image zeroed per element from a per-pixel tap mask, as
 // conv_stream_kernel's STAPS mode) -- the last two are SqueezeNet's expand convs ahead of pool3 / pool5
 enum { CP_S2 = 0, CP_1X1 = 1, CP_T3 = 2 };
-#ifndef ORE_CP_D
-#define ORE_CP_D 4  // k-steps in flight (build knob)
-#endif
+constexpr int CP_D = 4;  // k-steps in flight
 
 // MF: 16-channel fragments per block (every wave computes all 16 MF channels of its 16 quads);
 // D: k-steps in flight; NW: waves per block.  qrow = quads per conv row, nsteps = 16 NW-quad steps per
@@ -182,12 +180,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
   cp_floatx3 rb1[MODE == CP_S2 ? D : 1];
   int rt[MODE == CP_T3 ? D : 1];  // CP_T3: the tap of each ring slot's k (for its zero mask)
 
-#ifndef ORE_EXP_CP_ONELOAD
 #define CP_LOAD_B1(SLOT) \
   rb1[SLOT] = __builtin_bit_cast(cp_floatx3, __builtin_amdgcn_raw_buffer_load_b96(xr, o_ + 16, 0, 0));
-#else  // timing experiment only (tools/build_exp.sh): one 16-B operand load per k-step
-#define CP_LOAD_B1(SLOT) rb1[SLOT] = cp_floatx3{rb0[SLOT][1], rb0[SLOT][2], rb0[SLOT][3]};
-#endif
 #define CP_LOAD(SLOT)                                                                                  \
   {                                                                                                    \
     cp_load_a<MF>(wr, aoff, lt * astep, ra[SLOT]);                                                     \
@@ -287,10 +281,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
               const unsigned nb = (unsigned)__builtin_amdgcn_update_dpp((int)c2, (int)c2, 0x101, 0xf, 0xf, false);
               const unsigned c1 = __float_as_uint(fmaxf(v[2], v[3])) > nb || !right ? __float_as_uint(fmaxf(v[2], v[3]))
                                                                                   : nb;
-#ifdef ORE_EXP_CP_NOEPI  // timing experiment only: no pooled maxima
-              if (c0 == 0x7f7f7f7fu && c1 == c2) p.y[cl] = 0.0f;
-              continue;
-#endif
               if (oka) {
                 unsigned* row = cp_lds + sa + cl * Wp;
                 if (px0 < Wp) atomicMax(row + px0, c0);
@@ -308,11 +298,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_pool_stream_kernel(ConvP
           for (int f = 0; f < MF; ++f)
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[f][q] = cp_floatx4{0.f, 0.f, 0.f, 0.f};
-#ifndef ORE_EXP_CP_LGKMBAR
           __syncthreads();
-#else  // experiment: publish the LDS maxima only (the next step's operand loads stay in flight)
-          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
           // ---- store the pooled rows whose conv rows 2py .. 2py + 2 are all done ----
           const int qend = q0 + (cs + 1) * (16 * NW) < nq ? q0 + (cs + 1) * (16 * NW) : nq;
           const int rows_done = qend / qrow;
@@ -405,10 +391,10 @@ static int cp_mode(const ConvParams& p) {
       2 * (p.Wo - 1) + p.kw <= p.W)
     return CP_S2;
   if (p.kh == 1 && p.kw == 1 && p.sh == 1 && p.sw == 1 && p.pt == 0 && p.pl == 0 && p.Ho == p.H && p.Wo == p.W &&
-      p.C % (4 * ORE_CP_D) == 0)
+      p.C % (4 * CP_D) == 0)
     return CP_1X1;
   if (p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.pt <= 1 && p.pl <= 1 && p.Wo == p.W && p.Ho == p.H &&
-      p.W >= 3 && p.x_guard >= cp_lead(p) && p.x_bytes + cp_lead(p) < (1LL << 31) && (9 * p.C) % (4 * ORE_CP_D) == 0)
+      p.W >= 3 && p.x_guard >= cp_lead(p) && p.x_bytes + cp_lead(p) < (1LL << 31) && (9 * p.C) % (4 * CP_D) == 0)
     return CP_T3;
   return -1;
 }
@@ -447,12 +433,12 @@ static void launch_cp(const ConvParams& p0, size_t lds, int nbands, int nring, h
 template <int MF, int NW>
 static void launch_cp_mode(const ConvParams& p, size_t lds, int nbands, int nring, hipStream_t s) {
   if constexpr (MF == 6) {  // the 96-channel tiles: conv1 only (the stride-1 modes would spill)
-    launch_cp<MF, ORE_CP_D, NW, CP_S2>(p, lds, nbands, nring, s);
+    launch_cp<MF, CP_D, NW, CP_S2>(p, lds, nbands, nring, s);
   } else {
     switch (cp_mode(p)) {
-      case CP_S2: launch_cp<MF, ORE_CP_D, NW, CP_S2>(p, lds, nbands, nring, s); break;
-      case CP_1X1: launch_cp<MF, ORE_CP_D, NW, CP_1X1>(p, lds, nbands, nring, s); break;
-      default: launch_cp<MF, ORE_CP_D, NW, CP_T3>(p, lds, nbands, nring, s); break;
+      case CP_S2: launch_cp<MF, CP_D, NW, CP_S2>(p, lds, nbands, nring, s); break;
+      case CP_1X1: launch_cp<MF, CP_D, NW, CP_1X1>(p, lds, nbands, nring, s); break;
+      default: launch_cp<MF, CP_D, NW, CP_T3>(p, lds, nbands, nring, s); break;
     }
   }
 }

@@ -170,17 +170,9 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(ConvParams p) {
       rb[SLOT][g] = __builtin_bit_cast(cs_floatx4, w_);                                           \
     }                                                                                             \
   }
-#ifdef ORE_EXP_SNOMASK  // timing experiment only (tools/build_exp.sh): no zero-padding masks
-#undef CS_MASK
-#define CS_MASK(SLOT)
-#endif
 // the wave's priority is raised around its MFMA group (the SIMD's arbiter then prefers a wave that
 // is about to feed the matrix core over one doing address/mask VALU): 1-3 % on the 3x3 layers
-#ifndef ORE_EXP_SNOPRIO
 #define CS_PRIO(X) __builtin_amdgcn_s_setprio(X);
-#else
-#define CS_PRIO(X)
-#endif
 #define CS_MFMA(SLOT)                                                                             \
   CS_MASK(SLOT)                                                                                   \
   CS_PRIO(1)                                                                                      \

@@ -167,9 +167,6 @@ __device__ __forceinline__ void wg_window(const wg_floatx4 (&rows)[4], const WgT
 // a tile's (up to) 4 output pixels o[2 i + j] of channel m -> yb (p.y's plane and image strides)
 __device__ __forceinline__ void wg_store_px(const ConvParams& p, const WgTile& w, float* yb, int m, const float (&o)[4]) {
   if (!w.tok) return;
-#ifdef ORE_EXP_WG_NOSTORE  // timing experiment only: stores skipped (kept live by a never-true test)
-  if (o[0] != 1.2345e-30f) return;
-#endif
   // a tile row's two pixels as one 8-B store (4-B aligned on odd planes; buffer stores take that),
   // so a wave-instruction writes whole lines: two 4-B stores per row wrote every line twice
   // (PMC WRITE_SIZE 1.5x the output, profiles/r02e_pmc_layers.txt)
@@ -281,40 +278,21 @@ __global__ __launch_bounds__(256, 1) void conv_wino32_kernel(ConvParams p) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[xi][e] = 0.0f;
   wg_floatx4 ra[DA][4], rb[DB][4];
-#ifndef ORE_EXP_WG_NOA
 #define WG_LOAD_A(SLOT, S_)                                                                            \
     _Pragma("unroll") for (int i = 0; i < 4; ++i) ra[SLOT][i] = __builtin_bit_cast(                    \
         wg_floatx4, __builtin_amdgcn_raw_buffer_load_b128(ur, aoff + aq * i, (S_) * astep, 0));
-#else  // timing experiment only (tools/build_exp.sh): no A loads
-#define WG_LOAD_A(SLOT, S_)                                                                            \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) ra[SLOT][i] = wg_floatx4{(float)(S_), 1.f, 2.f, 3.f};
-#endif
-#if !defined(ORE_EXP_WG_NOB) && !defined(ORE_EXP_WG_ALIGNB)
 #define WG_LOAD_B(SLOT, S_)                                                                            \
     _Pragma("unroll") for (int r = 0; r < 4; ++r) rb[SLOT][r] = __builtin_bit_cast(                    \
         wg_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, w.roff[r], (S_) * xstep, 0));
-#elif defined(ORE_EXP_WG_ALIGNB)  // timing experiment only: the B rows loaded from 16-B aligned offsets
-#define WG_LOAD_B(SLOT, S_)                                                                            \
-    _Pragma("unroll") for (int r = 0; r < 4; ++r) rb[SLOT][r] = __builtin_bit_cast(                    \
-        wg_floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr, w.roff[r] & ~15, (S_) * xstep, 0));
-#else  // timing experiment only: no B loads
-#define WG_LOAD_B(SLOT, S_)                                                                            \
-    _Pragma("unroll") for (int r = 0; r < 4; ++r) rb[SLOT][r] = wg_floatx4{(float)(S_), (float)lane, 2.f, 3.f};
-#endif
 #define WG_MFMA(SA, SB)                                                                                \
   {                                                                                                    \
     float v_[16];                                                                                      \
     wg_window(rb[SB], w, v_);                                                                          \
     WG_MFMAS(SA, v_)                                                                                   \
   }
-#ifndef ORE_EXP_WG_NOMFMA
 #define WG_MFMAS(SA, V)                                                                                \
     _Pragma("unroll") for (int xi = 0; xi < 16; ++xi)                                                  \
         acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[SA][xi >> 2][xi & 3], V[xi], acc[xi], 0, 0, 0);
-#else  // timing experiment only: operands consumed by one VALU op each instead of the MFMAs
-#define WG_MFMAS(SA, V)                                                                                \
-    _Pragma("unroll") for (int xi = 0; xi < 16; ++xi) acc[xi][xi] += ra[SA][xi >> 2][xi & 3] * V[xi];
-#endif
 #define WG_WINDOWS(SB, V) wg_window(rb[SB], w, V);
 #define WG_COPYV(D_, S_) _Pragma("unroll") for (int i = 0; i < 16; ++i) D_[i] = S_[i];
 #define WG_NMFMA 16
@@ -608,21 +586,12 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-#ifndef ORE_EXP_WM_NOWIN  // timing experiments only (tools/build_exp.sh)
         d[r][j] = *reinterpret_cast<const float*>(lds_b + aw[r] + sto + 4 * j);
-#else
-        d[r][j] = (float)(aw[r] + sto + j);
-#endif
   };
   auto load_u = [&](int sto, int f, int q) __attribute__((always_inline)) {
-#ifndef ORE_EXP_WM_NOU
     return *reinterpret_cast<const wg_floatx4*>(lds_b + au + sto + q * 512 + f * 256);  // m = 16 f + lj
-#else
-    return wg_floatx4{(float)(au + sto + q), (float)f, 1.0f, 2.0f};
-#endif
   };
   auto xform = [&](float (&d)[4][4], float (&v)[16]) __attribute__((always_inline)) {
-#ifndef ORE_EXP_WM_NOXF
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       d[r][0] = c0ok ? d[r][0] : 0.0f;
@@ -630,10 +599,6 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
       d[r][3] = c3ok ? d[r][3] : 0.0f;
     }
     wg_input_transform(d, v);
-#else
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = d[i >> 2][i & 3];
-#endif
   };
 
   stage(0, 0);
@@ -641,9 +606,7 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   __syncthreads();
   for (int kc = 0; kc < nchunks; ++kc) {
     const int st = kc & 1;
-#ifndef ORE_EXP_WM_NODMA  // timing experiments only (tools/build_exp.sh): no DMA after the prologue
     if (kc + 1 < nchunks) stage(kc + 1, st ^ 1);
-#endif
     const int sto0 = st * SS * 4, sto1 = sto0 + 4 * g.CS * 4;  // k-step 1: channels 4 .. 7 of the chunk
     wg_floatx4 ua[2][4];
     float d0[4][4], d1[4][4], v[16];
@@ -676,10 +639,8 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
         for (int f = 0; f < 2; ++f)
           acc[4 * q + j][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][q][j], v[4 * q + j], acc[4 * q + j][f], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
-#ifndef ORE_EXP_WM_NOSYNC  // timing experiment only
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk kc + 1 have landed
     __syncthreads();  // ... every wave's, and every wave is done reading stage kc & 1
-#endif
   }
   // lane (lk, lj) of fragment f holds rows 4 lk + e = channel m0 + 16 f + 4 lk + e of tile lj
   float bv[2][4];
@@ -699,9 +660,6 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
       float mx[16];
 #pragma unroll
       for (int xi = 0; xi < 16; ++xi) mx[xi] = acc[xi][f][e];
-#ifdef ORE_EXP_WM_NOEPI  // timing experiment only: the epilogue skipped (kept live by a never-true test)
-      if (mx[0] + mx[5] + mx[10] + mx[15] != 1.2345e-30f) continue;
-#endif
       wg_store(p, w, m, bv[f][e], mx);
     }
 }

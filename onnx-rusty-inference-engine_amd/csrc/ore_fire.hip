@@ -50,9 +50,7 @@ void launch_fire_pack(const float* w, int M, int K, float* wf, hipStream_t s) {
 }
 
 // MFS: 16-row fragments of the squeeze output (Ms <= 16 MFS), D: K-loop ring depth
-#ifndef ORE_FIRE_MINB
-#define ORE_FIRE_MINB 2  // __launch_bounds__ minimum blocks per CU (experiment knob)
-#endif
+#define ORE_FIRE_MINB 2  // __launch_bounds__ minimum blocks per CU
 template <int MFS, int D>
 __global__ __launch_bounds__(256, ORE_FIRE_MINB) void fire_kernel(FireParams p) {
   const int lane = threadIdx.x & 63;
@@ -267,9 +265,7 @@ __global__ __launch_bounds__(256, ORE_FIRE_MINB) void fire_kernel(FireParams p) 
 constexpr int FP_WAVES = 8, FP_PIX = 64 * FP_WAVES, FP_TS = FP_PIX + 1;
 constexpr int FP_LDS = 64 * FP_TS * 4;
 
-#ifndef ORE_FP_NG
-#define ORE_FP_NG 2  // pooled fragments per pooling wave (2: waves 0-3 pool, 1: all 8) (experiment knob)
-#endif
+#define ORE_FP_NG 2  // pooled fragments per pooling wave (2: waves 0-3 pool, 1: all 8)
 template <int MFS, int D>
 __global__ __launch_bounds__(512, 1) void fire_pool_kernel(FireParams p) {
   constexpr int NG = ORE_FP_NG;
@@ -426,11 +422,7 @@ __global__ __launch_bounds__(512, 1) void fire_pool_kernel(FireParams p) {
     for (int f = 0; f < 4; ++f)
 #pragma unroll
       for (int e = 0; e < 4; ++e) bv[f][e] = bias[c0 + 16 * f + 4 * e + lk];
-#ifndef ORE_EXP_FP_NOSYNC  // timing ablation: no barriers, no tile, no pooling (results wrong)
     __syncthreads();  // the previous chunk's tile is pooled
-#else
-    if (p.N >= 0) return;
-#endif
     // bias + Relu -> conv tile row 16 f + 4 e + lk (= channel c0 + 16 f + 4 e + lk, the permuted packing)
     if (clive) {
 #pragma unroll
@@ -443,11 +435,7 @@ __global__ __launch_bounds__(512, 1) void fire_pool_kernel(FireParams p) {
         }
     }
     __syncthreads();  // tile complete
-#ifndef ORE_EXP_FP_NOPOOL  // timing ablation: the pooling phase compiled out (results wrong)
     if (pwave) {
-#else
-    if (pwave && p.N < 0) {
-#endif
       // squeeze k-step t takes concat channel cat0 + 4 t + lk = tile row 4 t + lk (lane group lk); the
       // window reads of k-step t + 1 are issued before the maxima of t
       float v[2][NG][9];
@@ -524,12 +512,8 @@ bool fire_eligible(const FireParams& p) {
   return p.y_ps % 4 == 0 && p.y_nstride % 4 == 0 && (ya & 15) == 0 && p.Ntot % 4 == 0 && p.Ntot >= 4;
 }
 
-#ifndef ORE_FIRE_D
-#define ORE_FIRE_D 4  // K-loop ring depth (experiment knob)
-#endif
-#ifndef ORE_FIRE_POOL_D
-#define ORE_FIRE_POOL_D 4  // fire_pool_kernel's ring depth (experiment knob)
-#endif
+#define ORE_FIRE_D 4  // K-loop ring depth
+#define ORE_FIRE_POOL_D 4  // fire_pool_kernel's ring depth
 
 template <int MFS>
 static void launch_fire_cfg(const FireParams& p0, hipStream_t s) {

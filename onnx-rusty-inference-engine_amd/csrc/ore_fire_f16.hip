@@ -127,12 +127,8 @@ __device__ __forceinline__ void ff_e1_chunk(ff16 (&acc)[F], __amdgpu_buffer_rsrc
 // ahead, A PD steps ahead; the scheduling barrier keeps every step's loads in it (unpinned, the
 // scheduler hoists all F x 9 NKC LDS reads and spills).  One step of B prefetch left the LDS latency
 // exposed behind an lgkmcnt(0) per step (2 MFMAs cover ~64 clocks).
-#ifndef ORE_FF_BD
 #define ORE_FF_BD 2
-#endif
-#ifndef ORE_FF_PD
 #define ORE_FF_PD 8
-#endif
 template <int NKC, int F, int PS>
 __device__ __forceinline__ void ff_e3_chunk(ff16 (&acc)[F], __amdgpu_buffer_rsrc_t w3, int E3, int c0, int arow,
                                             const _Float16* halo, const int (&hb)[F], int W2) {

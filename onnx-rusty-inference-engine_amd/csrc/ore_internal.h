@@ -90,7 +90,7 @@ ore_status resolve_window(ore_ctx* ctx, int auto_pad, const int64_t* pads, int n
 // ---------------------------------------------------------------- launches over resolved geometry
 // Kernel plan of a conv (or MatMul as a 1x1 conv) over resolved geometry.
 ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
-                   const Window& win, bool f16 = false, int xmode = 0, bool x3 = false, bool wino = false,
+                   const Window& win, bool f16 = false, int xmode = 0, bool wino = false,
                    int forced = -1);
 // wp: weights packed by launch_pack for plan `pln`
 // ktab: gather table (launch_ktab) for non-1x1 geometry on the gather kernel

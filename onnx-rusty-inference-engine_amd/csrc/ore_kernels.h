@@ -49,11 +49,7 @@ __device__ __forceinline__ ore_h8 ore_f16_epilogue8(const float* a, const float*
   return __builtin_bit_cast(ore_h8, o);
 }
 
-#ifdef ORE_NO_XCD_BANDS  // experiment builds: the plain block id in the banded / patch kernels
-#define ORE_BAND_ID() ((int)blockIdx.x)
-#else
 #define ORE_BAND_ID() xcd_block_id()
-#endif
 
 struct ConvParams {
   const float* x;      // input  [N][C][H][W], image stride x_nstride
@@ -82,8 +78,6 @@ struct ConvParams {
   int x_guard;         // bytes before x known to be mapped (the streaming 3x3 conv reads a few of them,
                        // zero-masked, instead of issuing negative buffer offsets)
   int x_lead;          // filled by the streaming launcher: bytes it reads before x (<= x_guard)
-  // x3 window-staged kernel (filled by the launcher from the ConvPlan and the geometry)
-  int bch, ks, nst, wr, ww, tiles_per_img;
   // pooled epilogue (ORE_FUSE_CONV_POOL, launch_conv_epool; 3x3 / stride-2 pool): y is the MaxPool
   // output [..][ep_Ho][ep_Wo] (plane stride y_ps), pool pads ep_pt / ep_pl; a block's N tile is a
   // 13 x 19 patch of conv outputs feeding a 6 x 9 tile of pooled outputs, ep_tr x ep_tc tiles per image
@@ -98,11 +92,9 @@ struct ConvPlan {
   int f16;             // 1: conv_f16_kernel (f16 weights Wh[Mp][Kp] and f16 NHWC output)
   int xmode;           // f16: F16_X_NCHW32 / F16_X_NHWC_ELEM / F16_X_NHWC_VEC / F16_X_NHWC_PAIR
   int cfg;             // tile id (0-3: conv_gemm_kernel 128x128, 96x128, 64x128, 32x256; 12-20 streaming;
-                       // X3_TILE_BASE + t; WINO_TILE_BASE + t)
-  int bch, ks, nst;    // x3 window kernel: channel groups per chunk, K rows per chunk, chunks
+                       // WINO_TILE_BASE + t)
   int Mp, krows;       // packed weights are krows x Mp floats
   int epv = 0;         // pooled-epilogue steps: ConvParams::ep_variant (ore_model_autotune)
-  int x3 = 0;          // 1: conv_x3_kernel (f32 on the BF16 matrix cores, ore_conv_x3.hip); cfg = X3_TILE_BASE + tile
   int wino = 0;        // 1: conv_wino_kernel (Winograd F(2x2, 3x3), ore_conv_wino.hip); cfg = WINO_TILE_BASE + tile
 };
 
@@ -201,9 +193,7 @@ struct FireF16Params {
   // (fire_pool_f16_plan)
   int pool, Hp, Wp, ppt, ppl, PR, F;
 };
-#ifndef ORE_FIRE_F16_LDS_KB
-#define ORE_FIRE_F16_LDS_KB 80  // build knob (timing experiments, tools/build_exp.sh)
-#endif
+#define ORE_FIRE_F16_LDS_KB 80  // LDS budget per workgroup (two per CU)
 constexpr int FIRE_F16_LDS_MAX = ORE_FIRE_F16_LDS_KB * 1024;  // the input halo of one workgroup (two per CU)
 int fire_f16_lds_bytes(int C, int H, int W);
 // pooled variant: picks p->F / p->PR (false: no band shape fits the LDS budget)
@@ -238,7 +228,7 @@ void launch_ktab(int2* ktab, int K, int kh, int kw, int x_ps, int W, hipStream_t
 // forced >= 0: that tile id when it belongs to the plan's kernel family (ore_ctx_set_conv_tile), else
 // the per-layer heuristic
 ConvPlan plan_conv(int M, int C, int H, int W, int kh, int kw, int sh, int sw, int pt, int pl, int Ho, int Wo,
-                   bool is1x1, bool f16 = false, int xmode = 0, bool x3 = false, bool wino = false, int forced = -1);
+                   bool is1x1, bool f16 = false, int xmode = 0, bool wino = false, int forced = -1);
 // f16 conv operand modes (ConvPlan::xmode), chosen by the input's layout:
 enum {
   F16_X_NCHW32 = 0,     // f32 NCHW model input, per-element gather, k order (c, r, s) (the reference's)
@@ -320,10 +310,11 @@ void launch_conv_pool_stream(const ConvParams& p, int variant, hipStream_t s);
 constexpr int CONV_EPOOL_BN = 256;  // N tile of the pooled-epilogue kernel
 constexpr int EPOOL_TILE_PR = 6, EPOOL_TILE_PC = 9;  // pooled outputs per block (13 x 19 conv patch)
 // tile ids 4-11 are retired (the LDS-free direct and the warp-specialised conv_gemm variants, measured
-// slower on every SqueezeNet layer: DESIGN.md section 7.1); ore_model_set_step_tile rejects them
+// slower on every SqueezeNet layer: DESIGN.md section 7.1), and so are 28-35 (ABI 1's bf16x3 kernels);
+// ore_ctx_set_conv_tile / ore_model_set_step_tile reject them
 constexpr int CONV_TILES_F32 = 21;  // 0-3 conv_gemm_kernel, 12-20 conv_stream_kernel (stride-1 geometries)
 constexpr int FIRE_TILE = 21;       // the fused f32 fire module (fire_kernel): ore.Model.TILE_NAMES "fire"
-inline bool conv_tile_retired(int t) { return t >= 4 && t < 12; }
+inline bool conv_tile_retired(int t) { return (t >= 4 && t < 12) || (t >= 28 && t < 36); }
 // LDS-free streaming kernel (ore_conv_stream.hip): 1x1 convs and stride-1 convs with Wo == W (every
 // expand3x3); tiles CONV_TILE_STREAM + 0..8 = 64x128, 32x256, 16x256, 48x128, 64x64, 128x64, 64x64 D8,
 // 32x128, 128x64 D2 (channels x pixels per wave); other geometries fall back to tile 0
@@ -337,33 +328,13 @@ void launch_conv_stream(const ConvParams& p, int tile, hipStream_t s);
 // tile 0); ore_model_autotune skips candidates that fell back
 extern thread_local int last_conv_tile;
 constexpr int CONV_TILES_F16 = 4;
-// f32 conv on the BF16 matrix cores by an exact three-way bf16 split of both operands (six part
-// products, f32 accumulation; ore_conv_x3.hip).  Tiles X3_TILE_BASE + 0..3 = 128x128, 64x256,
-// 96x128, 64x128 (channels x pixels per block); results do not depend on the tile.  Weights
-// packed by launch_pack_x3: [Kp / 32][3][Mp][32] bf16 (6 bytes per packed f32 weight).
-// Window-staged variant (stride-1 convs with C % 8 == 0, ConvPlan::x3 == 2): tiles X3_TILE_BASE + 4..7 =
-// 128x128, 64x128, 128x64, 64x64; weights packed by launch_pack_x3w per k-step of (tap, 8-channel
-// group) pairs: [nchunks * nsteps][3][Mp][32] bf16 (ConvPlan bch = groups G per chunk, nst = chunks,
-// ks = k-steps per chunk; the same fields go to ConvParams).
-constexpr int X3_TILE_BASE = 28;
-constexpr int X3_TILES = 8;
-int x3_tile_config(int M);  // 0..3 (gather tiles)
-int x3_tile_rows(int tile);
-bool conv_x3_eligible(const ConvParams& p);
-bool conv_x3w_eligible(const ConvParams& p, int tile);
-bool x3w_geometry(int C, int kh, int kw, int sh, int sw);
-int x3w_groups(int C);
-size_t x3w_plan_lds(int Ho, int Wo, int kh, int kw, int C, int tile);  // dynamic LDS of window tile `tile`
-void launch_pack_x3(const float* w, bool kmajor_src, int M, int K, int Mp, void* wx, hipStream_t s);
-void launch_pack_x3w(const float* w, int M, int C, int kh, int kw, int Mp, int G, int nsteps, int nchunks, void* wq,
-                     hipStream_t s);
-void launch_conv_x3(const ConvParams& p, int tile, hipStream_t s);
 // 3x3 / stride-1 / pad-1 f32 conv by Winograd F(2x2, 3x3) on the f32 MFMA (ore_conv_wino.hip).  Tiles
 // WINO_TILE_BASE + 0..3 = 32 ch x 32 tiles (32x32x2 MFMA, ring 4 / 2), 32 x 16, 16 x 32 (16x16x4);
 // 4 = the LDS-staged kernel (128 tiles x 32 channels per 4-wave block, windows and U from LDS; C % 8 == 0);
 // results do not depend on the tile (not bit-identical to the direct kernels).  Weights packed by
 // launch_pack_wino: U = G g G^T as [C][4][Mp][4] f32 (channel, position quad, m, position) (Mp = wino_packed_mp(M)).
-constexpr int WINO_TILE_BASE = X3_TILE_BASE + X3_TILES;
+// tile ids 28-35 are retired (ABI 1's opt-in bf16x3 kernels, ORE_LOAD_X3)
+constexpr int WINO_TILE_BASE = 36;
 constexpr int WINO_TILES_N = 5;
 // fused-kernel ids after the Winograd tiles (ore.Model.TILE_NAMES): 41 is retired (the Winograd fire module)
 constexpr int FIRE_F16_TILE = 42, C1_POOL_F16_TILE = 43;

@@ -101,19 +101,12 @@ struct Step {
   ConvPlan plan{};        // kernel choice and weight layout for S_CONV / S_MATMUL
   float* wp = nullptr;    // packed weights (layout per plan) for S_CONV / S_MATMUL
   const int2* ktab = nullptr;  // gather table (follows wp in the packed allocation; gather kernel only)
-  // ORE_LOAD_X3: the x3 plan of this conv (ore_conv_x3.hip), packed next to the f32-MFMA one; plan()
-  // switches an unfused conv to it (x3_wanted), a conv taken by an f32-MFMA fusion keeps `plan`
-  bool has_x3 = false;
-  ConvPlan plan_x3{};
-  float* wp_x3 = nullptr;
-  const int2* ktab_x3 = nullptr;
   // f32 models (not x3, not ORE_LOAD_NO_WINOGRAD): the Winograd F(2x2, 3x3) plan of a 3x3 / stride-1 /
   // pad-1 conv (ore_conv_wino.hip), packed next to the direct one; plan() switches a conv that no
   // direct-kernel fusion takes to it
   bool has_wino = false;
   ConvPlan plan_wino{};
   float* wp_wino = nullptr;
-  void* xcvt = nullptr;        // f16 F16_X_NHWC_PAIR: the f32 NCHW input converted to NHWC4 f16 (max_batch)
   const float* wc1 = nullptr;  // f32 pooled first conv: weights for pooled-conv variant 7 (launch_pack_c1_f32)
   // f16 pooled first conv with the next 1x1 conv (+ Relu) fused in (conv_pair_pool_f16_kernel SQ):
   // out is that conv's output; the squeeze weights in launch_fire_pack_f16 layout
@@ -134,10 +127,11 @@ struct Step {
 struct ore_model {
   ore_ctx* ctx = nullptr;
   int64_t max_batch = 0;
+  int64_t run_batch = 0;         // images per pass of the graph (the arena's size; ore_model_run chunks above it)
+  void* xcvt = nullptr;          // f16 F16_X_NHWC_PAIR: the f32 NCHW input converted to NHWC4 f16 (run_batch)
+  size_t xcvt_bytes = 0;
   int32_t fusion = ORE_FUSE_ALL;
   bool f16 = false;              // ORE_LOAD_F16: f16 conv/pool activations, f32 accumulation
-  bool x3 = false;               // ORE_LOAD_X3: f32 convs / MatMuls on the BF16 matrix cores (ore_conv_x3.hip)
-  bool x3_all = false;           // ORE_LOAD_X3_ALL: every conv on x3, no f32-MFMA fusions
   bool wino = false;             // f32 model without ORE_LOAD_NO_WINOGRAD: Winograd plans for 3x3 s1 p1 convs
   int conv_tile = -1;            // the context's forced conv tile at load (ore_ctx_set_conv_tile)
   std::vector<Value> values;
@@ -166,12 +160,14 @@ struct ore_model {
   // captured run (ore_model_graph_capture)
   hipGraph_t graph = nullptr;
   hipGraphExec_t graph_exec = nullptr;
+  int timed_chunks = 0;          // image chunks of the last timed run (events: chunk x (exec_steps + 1))
   std::vector<int> exec_steps;   // indices into steps of launched (non-NOP) steps
   // run-time binding
   const float* cur_in = nullptr;
   float* cur_out = nullptr;
   bool out_bound = false;
   int64_t last_n = 0;
+  bool last_chunked = false;     // the last run went in image chunks (arena values hold only the last one)
 };
 
 namespace {
@@ -509,7 +505,7 @@ ore_status build_node(ore_model* m, const Node& n, Step* s) {
 // kernels keep each output's arithmetic (same operands, same k order, the max of the same values),
 // so the result of the graph does not depend on which passes ran (tests/test_model_gpu.py checks each
 // against the unfused graph bit for bit).  Pass order matters only where two patterns overlap
-// (fire + pool + squeeze before concat + pool).  Then: algorithm selection (x3, Winograd), aliases,
+// (fire + pool + squeeze before concat + pool).  Then: algorithm selection (Winograd), aliases,
 // Concat in place, the plane layout, the arena, branch pairs and the gather tables.
 void count_uses(ore_model* m, const std::vector<Step>& steps) {
   for (auto& v : m->values) v.uses = 0;
@@ -529,27 +525,11 @@ int64_t padded_plane(int64_t P) {
 
 bool strided_writer(const Step& s) { return s.kind == S_CONV || s.kind == S_FIRE || s.kind == S_MAXPOOL; }
 
-// ORE_LOAD_X3: convs whose x3 kernel beats the f32-MFMA one at SqueezeNet's shapes (batch 256,
-// profiles/r02*_layers*.txt): stride-1 k x k convs on the window-staged kernel (every expand3x3),
-// and 1x1 convs / MatMuls with M >= 256 and K >= 256 (conv10: MFMA-bound).  The other 1x1 convs
-// are HBM-bound, where the f32-MFMA streaming kernels are faster, and the stride-2 7x7 conv1 stays on
-// the f32-MFMA row-walking kernel with pool1 fused.  ORE_LOAD_X3_ALL: every conv.
-bool x3_wanted(const ore_model* m, const Step& s) {
-  if (m->x3_all) return true;
-  if (s.kind == S_MATMUL) return s.M >= 256 && s.C >= 256;
-  if (s.kind != S_CONV) return false;
-  const bool k1 = s.kh == 1 && s.kw == 1 && s.sh == 1 && s.sw == 1;
-  if (k1) return s.M >= 256 && s.C >= 256;
-  return x3w_geometry(int(s.C), int(s.kh), int(s.kw), int(s.sh), int(s.sw)) &&
-         x3w_plan_lds(int(s.win.Ho), int(s.win.Wo), int(s.kh), int(s.kw), int(s.C), 6) <= 80 * 1024;
-}
-
 // size heuristics of the fusion passes (measured at batch 256, DESIGN.md sections 3 and 7); ORE_FUSE_EAGER
 // (tests) applies every eligible fusion regardless
 constexpr int64_t FIRE_MIN_COLS = 65536;      // fire fusions: max_batch x H x W >= one 64-pixel wave per SIMD
 constexpr int64_t FIRE_POOL_MIN_HW = 1024;    // fire + pool + squeeze on 54 x 54 planes (at 27 x 27 Winograd wins)
 constexpr int64_t CONCAT_POOL_MIN_HW = 1024;  // concat + pool in the producers: fire4 -40 us, fire8 +21 us
-constexpr int64_t X3_FIRE_MIN_HW = 1024;      // x3 models: the f32 fire kernel beats x3 expand3x3 from 54 x 54
 constexpr double EPOOL_MAX_WORK = 1.25;       // conv + pool patch kernel: recomputed columns <= 1.25 x the conv's
 constexpr int64_t WINO_SPLIT_MIN_C = 48;      // fire + squeeze on planes < FIRE_POOL_MIN_HW with >= 48 squeeze
                                               // channels: expand1x1 + Winograd expand3x3 + squeeze as three launches
@@ -609,7 +589,7 @@ struct Planner {
     if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2) return false;
     if (m->values[pl.in0].es != 4 || m->values[pl.in0].nhwc) return false;
     if (cv.kind != S_CONV || cv.pool || cv.epool || cv.kh != 1 || cv.kw != 1 || cv.sh != 1 || cv.sw != 1 ||
-        cv.win.pt || cv.win.pl || cv.plan.f16 || cv.plan.x3 || cv.plan.wino || cv.M > 64 || cv.C % 32 ||
+        cv.win.pt || cv.win.pl || cv.plan.f16 || cv.plan.wino || cv.M > 64 || cv.C % 32 ||
         pl.win.pt > 2 || pl.win.pl > 2)
       return false;
     PoolConvParams q{};  // pool_conv1x1_f32_kernel's own limits (run_conv_pool has no other kernel)
@@ -647,7 +627,7 @@ struct Planner {
   // (2) Conv (-> Relu) -> MaxPool, the conv output read by the pool only: one launch when the
   // recomputed patch costs <= EPOOL_MAX_WORK x the conv's columns (f32 and f16 models)
   ore_status conv_pool() {
-    if (!has(ORE_FUSE_CONV_POOL) || m->x3_all) return ORE_OK;
+    if (!has(ORE_FUSE_CONV_POOL)) return ORE_OK;
     for (size_t i = 0; i < m->steps.size(); ++i) {
       Step& pl = st(int(i));
       if (pl.kind != S_MAXPOOL) continue;
@@ -688,7 +668,7 @@ struct Planner {
   // pixels (SqueezeNet's fire4 -> pool3 -> fire5; at 27 x 27 fire8's expand3x3 runs Winograd, cheaper
   // than the direct K loop).  Runs before concat_pool, which would otherwise take the pattern.
   ore_status fire_pool_f32() {
-    if (!has(ORE_FUSE_FIRE_POOL | ORE_FUSE_CONV_RELU | ORE_FUSE_CONCAT) || m->f16 || m->x3_all) return ORE_OK;
+    if (!has(ORE_FUSE_FIRE_POOL | ORE_FUSE_CONV_RELU | ORE_FUSE_CONCAT) || m->f16) return ORE_OK;
     for (size_t i = 0; i < m->steps.size(); ++i) {
       int pa, pb;
       if (!fire_concat(int(i), &pa, &pb)) continue;
@@ -752,7 +732,7 @@ struct Planner {
   // values), so neither the two conv outputs nor the concat reach HBM.  The MaxPool of a Concat is the
   // Concat of the per-slice MaxPools (the pool is per channel).  Conv planes of >= CONCAT_POOL_MIN_HW.
   void concat_pool() {
-    if (!has(ORE_FUSE_CONCAT_POOL | ORE_FUSE_CONV_POOL | ORE_FUSE_CONCAT) || m->f16 || m->x3_all) return;
+    if (!has(ORE_FUSE_CONCAT_POOL | ORE_FUSE_CONV_POOL | ORE_FUSE_CONCAT) || m->f16) return;
     for (size_t i = 0; i < m->steps.size(); ++i) {
       Step& pl = st(int(i));
       if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2) continue;
@@ -806,7 +786,7 @@ struct Planner {
   // are a 1x1 and a 3x3 'same' Conv (+ Relu) of one value S, read only by a 1x1 Conv (+ Relu) with at
   // most 64 output channels
   ore_status fire_f32() {
-    if (!has(ORE_FUSE_FIRE | ORE_FUSE_CONV_RELU | ORE_FUSE_CONCAT) || m->f16 || m->x3_all) return ORE_OK;
+    if (!has(ORE_FUSE_FIRE | ORE_FUSE_CONV_RELU | ORE_FUSE_CONCAT) || m->f16) return ORE_OK;
     for (size_t i = 0; i < m->steps.size(); ++i) {
       int pa, pb;
       if (!fire_concat(int(i), &pa, &pb)) continue;
@@ -821,8 +801,6 @@ struct Planner {
       if (!eager() && m->max_batch * e1.H * e1.W < FIRE_MIN_COLS) continue;
       // Winograd expand3x3 (f32 models with Winograd on): the split is cheaper on small planes with wide inputs
       if (!eager() && m->wino && e3.has_wino && e1.H * e1.W < FIRE_POOL_MIN_HW && e1.C >= WINO_SPLIT_MIN_C) continue;
-      // x3 models: the f32-MFMA fire kernel only where it beats the x3 expand3x3 + separate 1x1s
-      if (m->x3 && e3.has_x3 && e1.H * e1.W < X3_FIRE_MIN_HW && !eager()) continue;
       if (padded_plane(e1.H * e1.W) % 4) continue;  // 16-B planes (layout below)
       if (!private_value(cc.in0) || !private_value(cc.in1) || !private_value(cc.out) || val(e1.in0).es != 4) continue;
       if (e1.in2 < 0 || e3.in2 < 0 || q.in2 < 0) continue;
@@ -999,7 +977,7 @@ struct Planner {
   // values).  f16: conv_pair_pool_f16_kernel SQ (<= 32 channels); f32: the window kernel (pooled-conv
   // variant 7, <= 16 channels).
   ore_status first_squeeze() {
-    if (!has(ORE_FUSE_FIRST_SQUEEZE | ORE_FUSE_CONV_POOL | ORE_FUSE_CONV_RELU) || m->x3_all) return ORE_OK;
+    if (!has(ORE_FUSE_FIRST_SQUEEZE | ORE_FUSE_CONV_POOL | ORE_FUSE_CONV_RELU)) return ORE_OK;
     for (size_t i = 0; i < m->steps.size(); ++i) {
       Step& cv = st(int(i));
       if (cv.kind != S_CONV || !cv.epool || cv.c1sq || !private_value(cv.out)) continue;
@@ -1014,7 +992,7 @@ struct Planner {
       if (q.kind != S_CONV || !q.relu || q.pool || q.epool || q.kh != 1 || q.kw != 1 || q.sh != 1 || q.sw != 1 ||
           q.win.pt || q.win.pl || q.in0 != cv.out || q.C != cv.M || q.in2 < 0 || q.in1 < 0 || !val(q.in1).cptr)
         continue;
-      if (f16 ? (!q.plan.f16 || q.plan.xmode != F16_X_NHWC_VEC || q.M > 32 || q.M % 8) : (q.plan.f16 || q.plan.x3 || q.M > 16))
+      if (f16 ? (!q.plan.f16 || q.plan.xmode != F16_X_NHWC_VEC || q.M > 32 || q.M % 8) : (q.plan.f16 || q.M > 16))
         continue;
       if (f16) {
         const int key = 5000000 + qi, M = int(q.M), C = int(q.C);
@@ -1045,7 +1023,7 @@ struct Planner {
   // (+ Relu) with <= 64 channels runs inside that conv (pool_conv1x1_f32_kernel, the pooled map never
   // stored).  Bit-identical to the MaxPool kernel + the conv.
   void pool_squeeze() {
-    if (!has(ORE_FUSE_POOL_SQUEEZE) || m->f16 || m->x3_all) return;
+    if (!has(ORE_FUSE_POOL_SQUEEZE) || m->f16) return;
     for (size_t i = 0; i < m->steps.size(); ++i) {
       Step& pl = st(int(i));
       if (pl.kind != S_MAXPOOL || pl.kh != 3 || pl.kw != 3 || pl.sh != 2 || pl.sw != 2) continue;
@@ -1092,16 +1070,10 @@ struct Planner {
     recount();
   }
 
-  // (9) algorithm selection, a load-time rule (never by timing): ORE_LOAD_X3 moves every conv / MatMul
-  // not taken by an f32-MFMA fusion to its x3 plan; f32 models with Winograd on run every 3x3 /
-  // stride-1 / pad-1 conv not taken by a direct-kernel fusion by Winograd F(2x2, 3x3)
+  // (9) algorithm selection, a load-time rule (never by timing): f32 models with Winograd on run every
+  // 3x3 / stride-1 / pad-1 conv not taken by a direct-kernel fusion by Winograd F(2x2, 3x3)
   void select_algorithms() {
     for (auto& s : m->steps) {
-      if (m->x3 && (s.kind == S_CONV || s.kind == S_MATMUL) && s.has_x3 && !s.pool && !s.epool) {
-        s.plan = s.plan_x3;
-        s.wp = s.wp_x3;
-        s.ktab = s.ktab_x3;
-      }
       if (m->wino && s.kind == S_CONV && s.has_wino && !s.pool && !s.epool) {
         s.plan = s.plan_wino;
         s.wp = s.wp_wino;
@@ -1189,7 +1161,7 @@ struct Planner {
     return ORE_OK;
   }
 
-  // (13) one device arena: every materialised root value gets a slot sized for max_batch, slots reused
+  // (13) one device arena: every materialised root value gets a slot sized for run_batch, slots reused
   // by liveness (first fit over [first write, last read] intervals)
   ore_status assign_arena() {
     const int nsteps = int(m->steps.size());
@@ -1218,22 +1190,37 @@ struct Planner {
       if (v.is_const || v.is_input || v.alias_of >= 0 || v.elided || v.first < 0) continue;
       roots.push_back(int(id));
     }
-    // the kernels index a launch's activations with 32-bit element offsets: refuse at load a max_batch
-    // whose values exceed them (rather than failing at run time)
+    // the kernels address a launch's activations through buffer resources and 32-bit offsets: one pass
+    // of the graph covers run_batch images, the largest batch whose every value (the caller's input and
+    // output included) and the f16 input conversion stay below RUN_LIMIT bytes; ore_model_run runs
+    // larger batches in image chunks (config 4's 2048 images per GPU: fire4's concat is 3 MB per image)
+    constexpr int64_t RUN_LIMIT = (int64_t(1) << 31) - (int64_t(1) << 21);
+    int64_t per_img_max = 0;
     for (size_t id = 0; id < m->values.size(); ++id) {
       const Value& v = m->values[id];
       if (v.is_const || v.alias_of >= 0 || v.elided || (v.first < 0 && !v.is_input)) continue;
-      if (v.image_stride() * m->max_batch + 256 >= (int64_t(1) << 31))
-        return err(m, ORE_ERR_UNSUPPORTED, "max_batch " + std::to_string(m->max_batch) + " exceeds 32-bit indexing of '" +
-                                               v.name + "' (" + std::to_string(v.image_stride()) +
-                                               " elements per image); run the batch in parts");
+      per_img_max = std::max(per_img_max, v.image_stride() * v.es);
+    }
+    int64_t xcvt_img = 0;
+    for (const Step& s : m->steps)
+      if (s.kind == S_CONV && s.plan.f16 && s.plan.xmode == F16_X_NHWC_PAIR) xcvt_img = std::max(xcvt_img, s.H * s.W * 4 * 2);
+    per_img_max = std::max(per_img_max, xcvt_img);
+    if (per_img_max >= RUN_LIMIT) return err(m, ORE_ERR_UNSUPPORTED, "one image's activations exceed 2 GiB");
+    m->run_batch = std::min<int64_t>(m->max_batch, per_img_max > 0 ? RUN_LIMIT / per_img_max : m->max_batch);
+    if (xcvt_img && size_t(xcvt_img * m->run_batch) > m->xcvt_bytes) {
+      if (m->xcvt) (void)hipFree(m->xcvt);
+      m->xcvt = nullptr;
+      m->xcvt_bytes = 0;
+      if (hipMalloc(&m->xcvt, size_t(xcvt_img * m->run_batch)) != hipSuccess)
+        return err(m, ORE_ERR_OOM, "input conversion buffer allocation failed");
+      m->xcvt_bytes = size_t(xcvt_img * m->run_batch);
     }
     std::sort(roots.begin(), roots.end(), [&](int a, int b) { return val(a).image_stride() > val(b).image_stride(); });
     std::vector<Slot> placed;
     int64_t arena = 0;
     for (int id : roots) {
       Value& v = val(id);
-      const int64_t size = ((v.image_stride() * m->max_batch * v.es) + 255) / 256 * 256;
+      const int64_t size = ((v.image_stride() * m->run_batch * v.es) + 255) / 256 * 256;
       std::vector<std::pair<int64_t, int64_t>> busy;  // slots whose lifetimes overlap this one
       for (auto& s : placed)
         if (has(ORE_KEEP_VALUES) || !(s.last < v.first || v.last < s.first)) busy.push_back({s.off, s.off + s.size});
@@ -1271,7 +1258,7 @@ struct Planner {
       const Value& v = val(root(id));
       if (v.is_const || v.arena_off < 0) return false;
       *lo = v.arena_off;
-      *hi = v.arena_off + v.image_stride() * m->max_batch * v.es;
+      *hi = v.arena_off + v.image_stride() * m->run_batch * v.es;
       return true;
     };
     auto overlap = [&](int a, int b) {
@@ -1426,10 +1413,10 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
       if (s.plan.f16 && s.plan.xmode == F16_X_NHWC_PAIR) {
         // convert the f32 NCHW input to NHWC f16 (4 channels per pixel), then gather
         const int cs = 4;
-        launch_nchw_to_nhwc(x.p, s.xcvt, int(n), int(s.C), int(s.H * s.W), x.nstride, int(x.ps ? x.ps : s.H * s.W), cs,
+        launch_nchw_to_nhwc(x.p, m->xcvt, int(n), int(s.C), int(s.H * s.W), x.nstride, int(x.ps ? x.ps : s.H * s.W), cs,
                             ctx->stream);
         ORE_HIP_CHECK(ctx, hipGetLastError());
-        const ore_status r = run_conv_f16(ctx, s.plan, s.xcvt, n, s.C, s.H, s.W, s.H * s.W * cs, cs, s.wp, s.ktab, s.M,
+        const ore_status r = run_conv_f16(ctx, s.plan, m->xcvt, n, s.C, s.H, s.W, s.H * s.W * cs, cs, s.wp, s.ktab, s.M,
                                           s.kh, s.kw, bias, s.win, s.sh, s.sw, s.relu, y.p, y.nstride, y.ps,
                                           s.epool ? &ep : nullptr);
         if (s.epool) s.ran_tile = last_conv_tile = EPOOL_TILE_BASE + 1;  // "epool patch": conv_f16's pooled epilogue
@@ -1565,10 +1552,6 @@ std::vector<int> step_tile_family(const Step& s) {
     return {EPOOL_TILE_BASE + 1, C1_POOL_F16_TILE};  // two launches (conversion + patch kernel) / one launch
   }
   if (s.epool || s.pool || s.gap) return c;  // other f16 pooled epilogues / the pooled 1x1 / conv + GAP: one kernel
-  if (s.plan.x3) {  // the x3 tiles of the plan's kernel family (its packed layout)
-    for (int t = 0; t < 4; ++t) c.push_back(X3_TILE_BASE + t + (s.plan.x3 == 2 ? 4 : 0));
-    return c;
-  }
   if (s.plan.wino) {
     for (int t = 0; t < WINO_TILES_N; ++t) c.push_back(WINO_TILE_BASE + t);
     return c;
@@ -1593,8 +1576,7 @@ void set_tile(ore_model* m, int k, int t) {
     return;
   }
   s.plan.cfg = t;
-  if (s.plan.x3) b.plan_x3.cfg = t;
-  else if (s.plan.wino) b.plan_wino.cfg = t;
+  if (s.plan.wino) b.plan_wino.cfg = t;
   else b.plan.cfg = t;
 }
 
@@ -1617,10 +1599,11 @@ ore_status ore_model_parse(const void* bytes, size_t len) {
 ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_t max_batch, int32_t flags,
                              ore_model** out) {
   if (!ctx || !bytes || !out || max_batch <= 0) return set_error(ctx, ORE_ERR_INVALID, "invalid argument");
-  if (flags & ~(ORE_LOAD_F16 | ORE_LOAD_X3 | ORE_LOAD_NO_WINOGRAD | ORE_LOAD_X3_ALL))
+  if (flags & ORE_LOAD_RETIRED_MASK)
+    return set_error(ctx, ORE_ERR_UNSUPPORTED, "load flags 0x%x were retired in ABI 2 (the bf16x3 kernels, ORE_LOAD_X3)",
+                     unsigned(flags & ORE_LOAD_RETIRED_MASK));
+  if (flags & ~(ORE_LOAD_F16 | ORE_LOAD_NO_WINOGRAD))
     return set_error(ctx, ORE_ERR_INVALID, "unknown load flags 0x%x", unsigned(flags));
-  if ((flags & ORE_LOAD_F16) && (flags & (ORE_LOAD_X3 | ORE_LOAD_X3_ALL)))
-    return set_error(ctx, ORE_ERR_INVALID, "ORE_LOAD_F16 and ORE_LOAD_X3 are exclusive");
   ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
   Graph g;
   std::string perr;
@@ -1629,9 +1612,7 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
   m->ctx = ctx;
   m->max_batch = max_batch;
   m->f16 = (flags & ORE_LOAD_F16) != 0;
-  m->x3 = (flags & (ORE_LOAD_X3 | ORE_LOAD_X3_ALL)) != 0;
-  m->x3_all = (flags & ORE_LOAD_X3_ALL) != 0;
-  m->wino = !m->f16 && !m->x3 && (flags & ORE_LOAD_NO_WINOGRAD) == 0;
+  m->wino = !m->f16 && (flags & ORE_LOAD_NO_WINOGRAD) == 0;
   m->conv_tile = ctx->conv_tile;
   auto fail = [&](ore_status st) {
     ore_model_destroy(m);
@@ -1705,22 +1686,15 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
         const int xmode = m->values[s.in0].es == 4 ? (s.C <= 4 ? F16_X_NHWC_PAIR : F16_X_NCHW32)
                           : s.C % 8 == 0           ? F16_X_NHWC_VEC
                                                    : F16_X_NHWC_ELEM;
-        s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, m->f16, xmode, false, false, m->conv_tile);
+        s.plan = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, m->f16, xmode, false, m->conv_tile);
       }
       else if (s.kind == S_MATMUL)
-        s.plan = conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win, false, 0, false, false, m->conv_tile);
+        s.plan = conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win, false, 0, false, m->conv_tile);
       else
         continue;
       total_packed += (packed_bytes(s.plan) + 255) / 256 * 256;
-      if (m->x3 && x3_wanted(m, s)) {
-        s.has_x3 = true;
-        s.plan_x3 = s.kind == S_CONV
-                        ? conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, false, 0, true, false, m->conv_tile)
-                        : conv_plan(s.M, s.C, 1, 1, 1, 1, 1, 1, s.win, false, 0, true, false, m->conv_tile);
-        total_packed += (packed_bytes(s.plan_x3) + 255) / 256 * 256;
-      }
       if (m->wino && s.kind == S_CONV) {
-        s.plan_wino = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, false, 0, false, true, m->conv_tile);
+        s.plan_wino = conv_plan(s.M, s.C, s.H, s.W, s.kh, s.kw, s.sh, s.sw, s.win, false, 0, true, m->conv_tile);
         s.has_wino = s.plan_wino.wino != 0;
         if (s.has_wino) total_packed += (conv_packed_bytes(s.plan_wino) + 255) / 256 * 256;
       }
@@ -1737,14 +1711,6 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
                     ctx->stream);
         s.ktab = reinterpret_cast<int2*>(base + conv_packed_bytes(s.plan));
         poff += (packed_bytes(s.plan) + 255) / 256 * 256;
-        if (s.has_x3) {
-          char* bx = reinterpret_cast<char*>(m->packed) + poff;
-          s.wp_x3 = reinterpret_cast<float*>(bx);
-          launch_pack(m->values[s.in1].cptr, s.w_kmajor, int(s.M), int(s.C), int(s.kh), int(s.kw), s.plan_x3, s.wp_x3,
-                      ctx->stream);
-          s.ktab_x3 = reinterpret_cast<int2*>(bx + conv_packed_bytes(s.plan_x3));
-          poff += (packed_bytes(s.plan_x3) + 255) / 256 * 256;
-        }
         if (s.has_wino) {
           s.wp_wino = reinterpret_cast<float*>(reinterpret_cast<char*>(m->packed) + poff);
           launch_pack(m->values[s.in1].cptr, false, int(s.M), int(s.C), int(s.kh), int(s.kw), s.plan_wino, s.wp_wino,
@@ -1755,10 +1721,6 @@ ore_status ore_model_load_ex(ore_ctx* ctx, const void* bytes, size_t len, int64_
       if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
         return fail(set_error(ctx, ORE_ERR_HIP, "weight packing failed"));
     }
-    for (auto& s : m->base_steps)  // NHWC4 copies of f32 inputs for the PAIR gather
-      if (s.kind == S_CONV && s.plan.f16 && s.plan.xmode == F16_X_NHWC_PAIR &&
-          hipMalloc(&s.xcvt, size_t(max_batch) * size_t(s.H * s.W) * 4 * sizeof(uint16_t)) != hipSuccess)
-        return fail(set_error(ctx, ORE_ERR_OOM, "input conversion buffer allocation failed"));
   }
   if (g.outputs.empty()) return fail(set_error(ctx, ORE_ERR_INVALID, "model has no outputs"));
   m->output_value = value_id(m, g.outputs[0].name);
@@ -1787,8 +1749,7 @@ ore_status ore_model_destroy(ore_model* m) {
   if (m->consts) (void)hipFree(m->consts);
   if (m->packed) (void)hipFree(m->packed);
   for (auto& kv : m->fire_packs) (void)hipFree(kv.second);
-  for (auto& s : m->base_steps)
-    if (s.xcvt) (void)hipFree(s.xcvt);
+  if (m->xcvt) (void)hipFree(m->xcvt);
   delete m;
   return ORE_OK;
 }
@@ -1796,6 +1757,7 @@ ore_status ore_model_destroy(ore_model* m) {
 ore_status ore_model_set_fusion(ore_model* m, int32_t flags) {
   if (!m) return set_error(nullptr, ORE_ERR_INVALID, "null model");
   const int32_t known = ORE_FUSE_ALL | ORE_FUSE_EAGER | ORE_KEEP_VALUES;
+  if (flags & 16) return set_error(m->ctx, ORE_ERR_UNSUPPORTED, "fusion bit 16 (ORE_FUSE_POOL_CONV) was retired (ABI 2)");
   if (flags & ~known) return set_error(m->ctx, ORE_ERR_INVALID, "unknown fusion flags 0x%x", unsigned(flags & ~known));
   m->fusion = flags;
   return plan(m);
@@ -1813,30 +1775,15 @@ ore_status ore_model_output_elems(ore_model* m, int64_t* elems) {
   return ORE_OK;
 }
 
-ore_status ore_model_run(ore_model* m, const float* d_input, int64_t n, float* d_output) {
-  if (!m || !d_input || !d_output) return set_error(m ? m->ctx : nullptr, ORE_ERR_INVALID, "null argument");
+// one pass of the graph over n <= run_batch images; ev: this pass's timing events (exec_steps + 1)
+static ore_status run_pass(ore_model* m, const float* d_input, int64_t n, float* d_output, hipEvent_t* ev) {
   ore_ctx* ctx = m->ctx;
-  if (n < 0 || n > m->max_batch) return set_error(ctx, ORE_ERR_INVALID, "batch %lld exceeds max_batch %lld", (long long)n, (long long)m->max_batch);
-  ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
   m->cur_in = d_input;
   m->cur_out = d_output;
-  m->last_n = n;
   const Value& ov = m->values[m->output_value];
-  // bind the output buffer directly when its producer writes a plain contiguous tensor
-  m->out_bound = ov.alias_of < 0 && !ov.elided;
-  if (m->timing && m->events.size() < m->exec_steps.size() + 1) {
-    for (auto e : m->events) (void)hipEventDestroy(e);
-    m->events.assign(m->exec_steps.size() + 1, nullptr);
-    for (auto& e : m->events) ORE_HIP_CHECK(ctx, hipEventCreate(&e));
-  }
   const bool branches = m->streams > 1 && !m->timing;
-  if (branches && !m->side) {
-    ORE_HIP_CHECK(ctx, hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking));
-    ORE_HIP_CHECK(ctx, hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
-    ORE_HIP_CHECK(ctx, hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming));
-  }
   for (size_t k = 0; k < m->exec_steps.size(); ++k) {
-    if (m->timing) ORE_HIP_CHECK(ctx, hipEventRecord(m->events[k], ctx->stream));
+    if (m->timing) ORE_HIP_CHECK(ctx, hipEventRecord(ev[k], ctx->stream));
     if (branches && m->pair_next[k]) {
       // fork: step k on the side stream, step k + 1 on the main stream, then join
       ORE_HIP_CHECK(ctx, hipEventRecord(m->ev_fork, ctx->stream));
@@ -1856,7 +1803,7 @@ ore_status ore_model_run(ore_model* m, const float* d_input, int64_t n, float* d
     ore_status st = launch_step(m, m->steps[m->exec_steps[k]], n);
     if (st) return st;
   }
-  if (m->timing) ORE_HIP_CHECK(ctx, hipEventRecord(m->events[m->exec_steps.size()], ctx->stream));
+  if (m->timing) ORE_HIP_CHECK(ctx, hipEventRecord(ev[m->exec_steps.size()], ctx->stream));
   if (!m->out_bound) {
     const Ref r = ref_of(m, m->output_value);
     const int64_t pe = ov.per_image();
@@ -1870,6 +1817,42 @@ ore_status ore_model_run(ore_model* m, const float* d_input, int64_t n, float* d
   return ORE_OK;
 }
 
+ore_status ore_model_run(ore_model* m, const float* d_input, int64_t n, float* d_output) {
+  if (!m || !d_input || !d_output) return set_error(m ? m->ctx : nullptr, ORE_ERR_INVALID, "null argument");
+  ore_ctx* ctx = m->ctx;
+  if (n < 0 || n > m->max_batch) return set_error(ctx, ORE_ERR_INVALID, "batch %lld exceeds max_batch %lld", (long long)n, (long long)m->max_batch);
+  ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+  m->last_n = n;
+  const Value& ov = m->values[m->output_value];
+  // bind the output buffer directly when its producer writes a plain contiguous tensor
+  m->out_bound = ov.alias_of < 0 && !ov.elided;
+  // n > run_batch: equal chunks of consecutive images, at most run_batch each (every image's
+  // arithmetic is independent of the batch it runs in)
+  const int64_t nchunks = n > m->run_batch ? (n + m->run_batch - 1) / m->run_batch : 1;
+  const int64_t chunk = (n + nchunks - 1) / nchunks;
+  m->last_chunked = nchunks > 1;
+  const size_t nev = m->exec_steps.size() + 1;
+  if (m->timing && m->events.size() < nev * size_t(nchunks)) {
+    for (auto e : m->events) (void)hipEventDestroy(e);
+    m->events.assign(nev * size_t(nchunks), nullptr);
+    for (auto& e : m->events) ORE_HIP_CHECK(ctx, hipEventCreate(&e));
+  }
+  m->timed_chunks = m->timing ? int(nchunks) : 0;
+  if (m->streams > 1 && !m->timing && !m->side) {
+    ORE_HIP_CHECK(ctx, hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking));
+    ORE_HIP_CHECK(ctx, hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
+    ORE_HIP_CHECK(ctx, hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming));
+  }
+  const int64_t in_img = m->values[m->input_value].per_image(), out_img = ov.per_image();
+  for (int64_t c = 0, i0 = 0; c < nchunks; ++c, i0 += chunk) {
+    const int64_t nc = std::min(chunk, n - i0);
+    if (ore_status st = run_pass(m, d_input + i0 * in_img, nc, d_output + i0 * out_img,
+                                 m->timing ? m->events.data() + size_t(c) * nev : nullptr))
+      return st;
+  }
+  return ORE_OK;
+}
+
 ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst, size_t cap, int64_t dims[4],
                                 int32_t* ndim) {
   if (!m || !name) return set_error(nullptr, ORE_ERR_INVALID, "null argument");
@@ -1878,6 +1861,9 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
   if (id < 0) return set_error(ctx, ORE_ERR_INVALID, "no value named '%s'", name);
   const Value& v = m->values[id];
   if (v.elided) return set_error(ctx, ORE_ERR_INVALID, "value '%s' is fused away", name);
+  if (!v.is_const && m->last_chunked)
+    return set_error(ctx, ORE_ERR_INVALID, "the last run went in image chunks of %lld: value '%s' holds only the last one",
+                     (long long)m->run_batch, name);
   const int64_t n = v.is_const ? 1 : m->last_n;
   if (dims) {
     for (int i = 0; i < 4; ++i) dims[i] = v.dims[i];
@@ -1898,7 +1884,7 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
     // rather than return stale data.
     if (!(m->fusion & ORE_KEEP_VALUES) && rv.arena_off >= 0) {
       auto extent = [&](const Value& x) {
-        return ((x.image_stride() * m->max_batch * x.es) + 255) / 256 * 256;
+        return ((x.image_stride() * m->run_batch * x.es) + 255) / 256 * 256;
       };
       const int64_t lo = rv.arena_off, hi = rv.arena_off + extent(rv);
       for (size_t j = 0; j < m->values.size(); ++j) {
@@ -1950,6 +1936,11 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
   ore_ctx* ctx = m->ctx;
   if (n < 1 || n > m->max_batch) return set_error(ctx, ORE_ERR_INVALID, "batch out of range");
   if (reps < 1) reps = 3;
+  if (n > m->run_batch) {  // tuned on one chunk of the chunked run (ore_model_run)
+    const int64_t nchunks = (n + m->run_batch - 1) / m->run_batch;
+    n = (n + nchunks - 1) / nchunks;
+  }
+  m->last_chunked = false;
   ORE_HIP_CHECK(ctx, hipSetDevice(ctx->device));
   m->cur_in = d_input;
   m->cur_out = d_output;
@@ -2076,6 +2067,8 @@ ore_status ore_model_enable_timing(ore_model* m, int32_t on) {
 
 int32_t ore_model_step_count(ore_model* m) { return m ? int32_t(m->exec_steps.size()) : 0; }
 
+int64_t ore_model_run_batch(ore_model* m) { return m ? m->run_batch : 0; }
+
 ore_status ore_model_step_info(ore_model* m, int32_t i, const char** op, const char** name, double* flops, double* bytes) {
   if (!m || i < 0 || size_t(i) >= m->exec_steps.size()) return set_error(nullptr, ORE_ERR_INVALID, "bad step index");
   const Step& s = m->steps[m->exec_steps[i]];
@@ -2095,10 +2088,18 @@ ore_status ore_model_step_info(ore_model* m, int32_t i, const char** op, const c
 
 ore_status ore_model_step_times(ore_model* m, float* ms, int32_t cap) {
   if (!m || !ms) return set_error(nullptr, ORE_ERR_INVALID, "null argument");
-  if (!m->timing || m->events.size() < m->exec_steps.size() + 1) return set_error(m->ctx, ORE_ERR_INVALID, "timing not enabled");
-  ORE_HIP_CHECK(m->ctx, hipEventSynchronize(m->events[m->exec_steps.size()]));
-  for (size_t k = 0; k < m->exec_steps.size() && int32_t(k) < cap; ++k)
-    ORE_HIP_CHECK(m->ctx, hipEventElapsedTime(&ms[k], m->events[k], m->events[k + 1]));
+  const size_t nev = m->exec_steps.size() + 1;
+  if (!m->timing || m->timed_chunks < 1 || m->events.size() < nev * size_t(m->timed_chunks))
+    return set_error(m->ctx, ORE_ERR_INVALID, "timing not enabled");
+  ORE_HIP_CHECK(m->ctx, hipEventSynchronize(m->events[nev * size_t(m->timed_chunks) - 1]));
+  for (size_t k = 0; k < m->exec_steps.size() && int32_t(k) < cap; ++k) {
+    ms[k] = 0.f;
+    for (int c = 0; c < m->timed_chunks; ++c) {  // summed over the run's image chunks
+      float t = 0.f;
+      ORE_HIP_CHECK(m->ctx, hipEventElapsedTime(&t, m->events[c * nev + k], m->events[c * nev + k + 1]));
+      ms[k] += t;
+    }
+  }
   return ORE_OK;
 }
 

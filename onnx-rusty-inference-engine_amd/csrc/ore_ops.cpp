@@ -114,9 +114,9 @@ static int64_t image_chunk(int64_t N, int64_t x_nstride, int64_t x_img_bytes, in
 }
 
 ConvPlan conv_plan(int64_t M, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
-                   const Window& win, bool f16, int xmode, bool x3, bool wino, int forced) {
+                   const Window& win, bool f16, int xmode, bool wino, int forced) {
   return plan_conv(int(M), int(C), int(H), int(W), int(kh), int(kw), int(sh), int(sw), int(win.pt), int(win.pl),
-                   int(win.Ho), int(win.Wo), kh == 1 && kw == 1, f16, xmode, x3, wino, forced);
+                   int(win.Ho), int(win.Wo), kh == 1 && kw == 1, f16, xmode, wino, forced);
 }
 
 size_t packed_bytes(const ConvPlan& pln) { return conv_packed_bytes(pln) + size_t(pln.krows) * sizeof(int2); }
@@ -187,7 +187,6 @@ ore_status run_conv(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N
       !fits_i32(p.Ntot + 256) || (p.Ntot + 127) / 128 * ((M + 31) / 32) >= (int64_t(1) << 31))
     return set_error(ctx, ORE_ERR_INVALID, "conv geometry exceeds 32-bit indexing");
   if (!pln.wino && !p.is1x1 && !ktab) return set_error(ctx, ORE_ERR_INVALID, "internal: gather table missing");
-  if (pln.x3 && !p.is1x1 && p.kh * p.kw > 64) return set_error(ctx, ORE_ERR_UNSUPPORTED, "x3 conv: more than 64 taps");
   // image chunks whose x and y extents fit 32-bit byte offsets (the output may be a slice of a wider
   // concat buffer, e.g. an expand3x3 writing channels 256..511 of 512)
   const int64_t nb = image_chunk(N, x_nstride, C * x_ps * 4, 4, y_nstride, M * y_ps * 4, 4);
@@ -373,7 +372,7 @@ ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int6
   if (x_ps == 0) x_ps = pH * pW;
   const int64_t P = pwin.Ho * pwin.Wo;
   if (y_ps == 0) y_ps = P;
-  if (pln.f16 || pln.x3 || pln.wino || x_es != 4)
+  if (pln.f16 || pln.wino || x_es != 4)
     return set_error(ctx, ORE_ERR_INVALID, "internal: the pooled 1x1 conv is f32 direct only");
   // 3x3 / stride-2 pools (the window is implied by the walker's pass, kernel_shape 3x3):
   // pool_conv1x1_f32_kernel (LDS-staged rows, MFMA squeeze)
@@ -584,7 +583,8 @@ ore_status ore_ctx_set_conv_algo(ore_ctx* ctx, int32_t algo) {
 ore_status ore_ctx_set_conv_tile(ore_ctx* ctx, int32_t tile) {
   if (!ctx) return set_error(nullptr, ORE_ERR_INVALID, "null context");
   const bool sp = tile >= CONV_TILE_SP && tile < CONV_TILE_SP + CONV_TILES_SP;
-  if (!sp && (tile < -1 || tile >= WINO_TILE_BASE + WINO_TILES_N || conv_tile_retired(tile)))
+  if (conv_tile_retired(tile)) return set_error(ctx, ORE_ERR_UNSUPPORTED, "conv tile %d was retired (ABI 2)", int(tile));
+  if (!sp && (tile < -1 || tile >= WINO_TILE_BASE + WINO_TILES_N))
     return set_error(ctx, ORE_ERR_INVALID, "conv tile %d is not a conv tile id", int(tile));
   ctx->conv_tile = tile;
   return ORE_OK;
@@ -592,6 +592,7 @@ ore_status ore_ctx_set_conv_tile(ore_ctx* ctx, int32_t tile) {
 
 ore_status ore_ctx_set_pool_variant(ore_ctx* ctx, int32_t variant) {
   if (!ctx) return set_error(nullptr, ORE_ERR_INVALID, "null context");
+  if (variant == 1) return set_error(ctx, ORE_ERR_UNSUPPORTED, "MaxPool variant 1 was retired (ABI 2)");
   if (variant != 0 && (variant < 2 || variant > 5)) return set_error(ctx, ORE_ERR_INVALID, "unknown MaxPool variant %d", int(variant));
   ctx->pool_variant = variant;
   return ORE_OK;
@@ -693,7 +694,7 @@ ore_status ore_conv2d_f32(ore_ctx* ctx, const ore_tensor* x, const ore_tensor* w
   if (x->dims[0] == 0) return ORE_OK;
   const int2* kt = nullptr;
   const ConvPlan pln = conv_plan(w->dims[0], w->dims[1], x->dims[2], x->dims[3], w->dims[2], w->dims[3], a->strides[0],
-                                 a->strides[1], win, false, 0, false, ctx->conv_algo == ORE_CONV_ALGO_WINOGRAD,
+                                 a->strides[1], win, false, 0, ctx->conv_algo == ORE_CONV_ALGO_WINOGRAD,
                                  ctx->conv_tile);
   float* wp = pack_to_scratch(ctx, pln, w->data, false, w->dims[0], w->dims[1], w->dims[2], w->dims[3], x->dims[2],
                               x->dims[3], &kt);
@@ -774,7 +775,7 @@ ore_status ore_matmul_f32(ore_ctx* ctx, const ore_tensor* a, const ore_tensor* b
   win.Ho = 1; win.Wo = 1;
   if (a->dims[0] == 0) return ORE_OK;
   const int2* kt = nullptr;
-  const ConvPlan pln = conv_plan(b->dims[1], b->dims[0], 1, 1, 1, 1, 1, 1, win, false, 0, false, false, ctx->conv_tile);
+  const ConvPlan pln = conv_plan(b->dims[1], b->dims[0], 1, 1, 1, 1, 1, 1, win, false, 0, false, ctx->conv_tile);
   float* wp = pack_to_scratch(ctx, pln, b->data, true, b->dims[1], b->dims[0], 1, 1, 1, 1, &kt);
   if (!wp) return ORE_ERR_OOM;
   return run_conv(ctx, pln, a->data, a->dims[0], a->dims[1], 1, 1, a->dims[1], wp, kt, b->dims[1], 1, 1, nullptr, win, 1, 1,

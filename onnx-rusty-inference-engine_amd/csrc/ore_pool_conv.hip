@@ -27,12 +27,8 @@ namespace {
 
 typedef float ps4 __attribute__((ext_vector_type(4)));
 
-#ifndef ORE_PS_PR
 #define ORE_PS_PR 2   // pooled rows per workgroup
-#endif
-#ifndef ORE_PS_CH
 #define ORE_PS_CH 16  // input channels per chunk
-#endif
 constexpr int PS_PR = ORE_PS_PR, PS_CH = ORE_PS_CH;
 // input loads non-temporal (cache policy nt): read once, and a streamed read measured 10 % faster
 // with it (profiles/r03k_hbm_probe.txt); pool5 + squeeze 110.3 -> 105.7 us, pool3 205 -> 204 us

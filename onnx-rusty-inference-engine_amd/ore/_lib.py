@@ -9,7 +9,7 @@ import ctypes
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# ORE_LIB selects another build of the same library (tools/build_exp.sh timing variants)
+# ORE_LIB selects another build of the same library (tools/build_exp.sh A/B variants)
 LIB_PATH = os.environ.get("ORE_LIB") or os.path.join(PKG_ROOT, "lib", "libore.so")
 
 ORE_OK = 0
@@ -23,9 +23,9 @@ FUSE_CONV_GAP = 4096
 FUSE_EAGER = 2048  # tests: every eligible fusion regardless of the size heuristics
 FUSE_ALL = 6119
 LOAD_F16 = 1  # ore_model_load_ex flag: the fp16 variant
-LOAD_X3 = 2   # ore_model_load_ex flag: f32 convs on the BF16 matrix cores (exact 3-way bf16 split)
 LOAD_NO_WINOGRAD = 4  # ore_model_load_ex flag: 3x3 stride-1 convs on the direct kernels only
-LOAD_X3_ALL = 8  # ore_model_load_ex flag: every conv on x3, no f32-MFMA fusions (x3 kernel tests)
+LOAD_RETIRED_MASK = 10  # ABI 1's LOAD_X3 / LOAD_X3_ALL: rejected (ORE_ERR_UNSUPPORTED) since ABI 2
+ABI_VERSION = 2  # ORE_ABI_VERSION this binding was written against
 CONV_ALGO_DIRECT, CONV_ALGO_WINOGRAD = 0, 1  # ore_ctx_set_conv_algo (per-op ore_conv2d_f32)
 PAD = {"NOTSET": 0, "NOT_SET": 0, "SAME_UPPER": 1, "SAME_LOWER": 2, "VALID": 3}
 
@@ -39,7 +39,7 @@ EXPORTED = [
     "ore_model_output_elems", "ore_model_run", "ore_model_read_value", "ore_model_autotune",
     "ore_model_step_tile", "ore_model_set_step_tile", "ore_model_step_mfma_flops", "ore_model_set_streams",
     "ore_model_graph_capture", "ore_model_graph_launch", "ore_model_enable_timing",
-    "ore_model_step_count", "ore_model_step_info", "ore_model_step_times",
+    "ore_model_step_count", "ore_model_step_info", "ore_model_step_times", "ore_model_run_batch",
 ]
 
 
@@ -124,6 +124,7 @@ def load():
         "ore_model_graph_capture": (i32, [vp, vp, i64, vp]),
         "ore_model_graph_launch": (i32, [vp]),
         "ore_model_step_count": (i32, [vp]),
+        "ore_model_run_batch": (i64, [vp]),
         "ore_model_step_info": (i32, [vp, i32, ctypes.POINTER(cs), ctypes.POINTER(cs),
                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
         "ore_model_step_times": (i32, [vp, ctypes.POINTER(ctypes.c_float), i32]),

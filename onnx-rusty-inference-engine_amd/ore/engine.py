@@ -16,7 +16,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import LOAD_F16, LOAD_NO_WINOGRAD, LOAD_X3, LOAD_X3_ALL, ConvAttrs, OreError, PoolAttrs, Tensor, check, load
+from ._lib import LOAD_F16, LOAD_NO_WINOGRAD, ConvAttrs, OreError, PoolAttrs, Tensor, check, load
 
 __all__ = ["Context", "Model", "OreError", "convolution", "max_pool", "relu", "add", "softmax", "mul",
            "global_average_pool", "concatenation", "drop_out", "reshape", "inference", "conv_out_shape",
@@ -234,29 +234,25 @@ class Model:
     """ore_model: the device-resident walker over one ONNX graph."""
 
     def __init__(self, ctx: Context, onnx_bytes: bytes, max_batch: int, precision: str = "f32",
-                 winograd: bool = True, x3_all: bool = False):
-        """precision "f32": convs on the f32-input MFMA; "f32x3": the same f32 model with its convs /
-        MatMuls on the BF16 matrix cores through an exact three-way bf16 split (ORE_LOAD_X3,
-        include/ore.h); "f16": the fp16 variant (ORE_LOAD_F16).  Input / output stay f32.
-        winograd (f32 only): 3x3 stride-1 pad-1 convs that no direct-kernel fusion takes run
-        Winograd F(2x2, 3x3) in f32; False = ORE_LOAD_NO_WINOGRAD (direct kernels only).
-        x3_all (f32x3 only): every conv on the x3 kernels, no f32-MFMA fusions (ORE_LOAD_X3_ALL)."""
-        if precision not in ("f32", "f32x3", "f16"):
-            raise OreError(1, f"precision must be 'f32', 'f32x3' or 'f16', not {precision!r}")
+                 winograd: bool = True):
+        """precision "f32": convs on the f32-input MFMA; "f16": the fp16 variant (ORE_LOAD_F16).
+        Input / output stay f32.  winograd (f32 only): 3x3 stride-1 pad-1 convs that no direct-kernel
+        fusion takes run Winograd F(2x2, 3x3) in f32; False = ORE_LOAD_NO_WINOGRAD (direct kernels
+        only).  Any max_batch loads: batches past run_batch run in image chunks (ore_model_run)."""
+        if precision not in ("f32", "f16"):
+            raise OreError(1, f"precision must be 'f32' or 'f16', not {precision!r}")
         self.ctx = ctx
         self.precision = precision
         h = ctypes.c_void_p()
-        flags = {"f32": 0, "f32x3": LOAD_X3, "f16": LOAD_F16}[precision]
+        flags = {"f32": 0, "f16": LOAD_F16}[precision]
         if not winograd:
             flags |= LOAD_NO_WINOGRAD
-        if x3_all:
-            if precision != "f32x3":
-                raise OreError(1, "x3_all needs precision 'f32x3'")
-            flags |= LOAD_X3_ALL
         check(load().ore_model_load_ex(ctx.h, onnx_bytes, len(onnx_bytes), int(max_batch), flags, ctypes.byref(h)),
               ctx.h)
         self.h = h
         self.max_batch = max_batch
+        # images per pass of the graph: larger batches run in image chunks inside ore_model_run
+        self.run_batch = int(load().ore_model_run_batch(h))
         d = (ctypes.c_int64 * 4)()
         check(load().ore_model_input_dims(self.h, d), ctx.h)
         self.input_dims = tuple(d)[1:]
@@ -322,8 +318,7 @@ class Model:
                   "stream 128x64", "stream 64x64 d8", "stream 32x128", "stream 128x64 d2", "fire",
                   "epool patch", "epool walk48", "epool walk96", "epool walk64",
                   "epool walk64 b3", None,  # 27: the 2-band walker
-                  "x3 128x128", "x3 64x256", "x3 96x128", "x3 64x128",
-                  "x3w 128x128", "x3w 64x128", "x3w 128x64", "x3w 64x64",
+                  None, None, None, None, None, None, None, None,  # 28-35: ABI 1's bf16x3 kernels
                   "wino 32x32 d4", "wino 32x32 d2", "wino16 32x16", "wino16 16x32",
                   "wino lds", None,  # 41: the Winograd fire module (retired)
                   "fire f16", "first conv pool f16", "epool window f32", "fire pool f32",

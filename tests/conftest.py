@@ -13,7 +13,6 @@ for p in (REPO, PKG):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through the C ABI)")
-    config.addinivalue_line("markers", "hybrid: x3 test on the default ORE_LOAD_X3 policy (not ORE_LOAD_X3_ALL)")
 
 
 @pytest.fixture(scope="session")

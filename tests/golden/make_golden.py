@@ -4,6 +4,9 @@ restatement of the reference, oracle/).  Run from the repo root:  python tests/g
   squeezenet_synth_oracle.npz  synthetic SqueezeNet-1.0 (ore.squeezenet.build(224), seed 1234),
                                input = [zoo image squeezenet_data_0.pb, synthetic_input(1, seed 0)],
                                output = oracle softmax rows [2, 1000]
+  squeezenet_synth8_oracle.npz the same model on 8 images: the zoo image + synthetic_input(7, seed 21)
+                               (the benched plan's parity margin, tests/test_config4_gpu.py); also
+                               squeezenet_synth8_f64.npz, the float64 executor's output (f64_ref.py)
   squeezenet_mini_oracle.npz   the same topology at 64x64 input, 4 seeded images; also every
                                intermediate value of image 0 (for node-level parity)
   mnist_oracle.npz             mnist-8.onnx on mnist_data_0.pb and 3 derived images
@@ -30,6 +33,11 @@ def squeezenet_inputs():
     return np.concatenate([zoo, squeezenet.synthetic_input(1, 224, seed=0)]).astype(np.float32)
 
 
+def squeezenet_inputs8():
+    zoo = onnx_wire.load_tensor(os.path.join(HERE, "squeezenet_data_0.pb")).to_numpy()
+    return np.concatenate([zoo, squeezenet.synthetic_input(7, 224, seed=21)]).astype(np.float32)
+
+
 def mini_inputs():
     return squeezenet.synthetic_input(4, 64, seed=5)
 
@@ -41,7 +49,22 @@ def mnist_inputs():
     return np.concatenate([x, extra]).astype(np.float32)
 
 
+def synth8():
+    import f64_ref
+    model = squeezenet.build(224)
+    x = squeezenet_inputs8()
+    y = oracle.Model(model).run(x, 1000)
+    np.savez_compressed(os.path.join(HERE, "squeezenet_synth8_oracle.npz"), output=y)
+    y64 = np.concatenate([f64_ref.run(model, x[i:i + 1]) for i in range(x.shape[0])])
+    np.savez_compressed(os.path.join(HERE, "squeezenet_synth8_f64.npz"), output=y64)
+
+
 def main():
+    if "--only-synth8" in sys.argv:
+        synth8()
+        print("wrote synth8 fixtures")
+        return
+    synth8()
     m = oracle.Model(squeezenet.build(224))
     y = m.run(squeezenet_inputs(), 1000)
     np.savez_compressed(os.path.join(HERE, "squeezenet_synth_oracle.npz"), output=y)

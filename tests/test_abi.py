@@ -30,7 +30,12 @@ def test_library_exports_header():
     for n in names:
         assert hasattr(L, n), f"libore.so does not export {n}"
     assert sorted(_lib.EXPORTED) == names
-    assert L.ore_abi_version() == 1
+    assert L.ore_abi_version() == ore.ABI_VERSION == 2
+    # the header's constants the binding mirrors (ABI 2: retired load flags rejected)
+    defs = dict(re.findall(r"#define (ORE_\w+) (-?\d+)", open(HEADER).read()))
+    assert int(defs["ORE_ABI_VERSION"]) == ore.ABI_VERSION
+    assert int(defs["ORE_LOAD_RETIRED_MASK"]) == _lib.LOAD_RETIRED_MASK == 2 | 8
+    assert int(defs["ORE_FUSE_ALL"]) == ore.FUSE_ALL and int(defs["ORE_LOAD_F16"]) == ore.LOAD_F16
 
 
 def test_library_reads_no_environment():

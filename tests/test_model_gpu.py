@@ -11,6 +11,8 @@ import os
 import numpy as np
 import pytest
 
+from ore import FUSE_ALL, FUSE_EAGER, FUSE_FIRE
+
 from _knobs import (EPOOL_PATCH, EPOOL_WALK48, EPOOL_WALK64, EPOOL_WALK64_B3, EPOOL_WALK96, EPOOL_WINDOW, conv_tile,
                     force_tiles)
 
@@ -53,7 +55,7 @@ def squeeze224(gpu_ctx):
     m.close()
 
 
-@pytest.mark.parametrize("fusion", [2023 | 2048, 2023, 7, 0])  # FUSE_ALL (| FUSE_EAGER), unfused
+@pytest.mark.parametrize("fusion", [FUSE_ALL | FUSE_EAGER, FUSE_ALL, 7, 0])  # 7: relu + concat + alias; 0 unfused
 def test_mnist_golden(gpu_ctx, fusion):
     import ore
     from ore import onnx_wire
@@ -97,7 +99,7 @@ def test_squeezenet_synth_vs_oracle(squeeze224):
     assert np.array_equal(y.argmax(1), ref.argmax(1))
 
 
-@pytest.mark.parametrize("fusion", [2023 | 2048, 2023, 7, 0, 1, 2, 4, 32, 2023 & ~64])
+@pytest.mark.parametrize("fusion", [FUSE_ALL | FUSE_EAGER, FUSE_ALL, 7, 0, 1, 2, 4, 32, FUSE_ALL & ~FUSE_FIRE])
 def test_squeezenet_mini_vs_oracle(gpu_ctx, fusion):
     import ore
     from ore import squeezenet
@@ -886,3 +888,26 @@ def test_squeezenet_fire_pool_fused(gpu_ctx):
         m.close()
     np.testing.assert_array_equal(outs[0], outs[1])
     assert nsteps[0] == nsteps[1] - 4  # per pair: two expand walkers + the squeeze -> fire_pool_kernel
+
+
+def test_abi2_retired_values(gpu_ctx):
+    """ABI 2 (include/ore.h): ABI 1's retired values fail with ORE_ERR_UNSUPPORTED and a message
+    naming the retirement -- the bf16x3 load flags (2, 8) and tiles 28-35, fusion bit 16
+    (ORE_FUSE_POOL_CONV), MaxPool variant 1 and tiles 4-11."""
+    import ctypes
+    import ore
+    from ore import _lib, squeezenet
+    L = ore.load()
+    for t in (4, 11, 28, 35):
+        assert L.ore_ctx_set_conv_tile(gpu_ctx.h, t) == 2 and b"retired" in L.ore_last_error(gpu_ctx.h)
+    assert L.ore_ctx_set_conv_tile(gpu_ctx.h, -1) == 0
+    assert L.ore_ctx_set_pool_variant(gpu_ctx.h, 1) == 2 and b"retired" in L.ore_last_error(gpu_ctx.h)
+    mb = squeezenet.build(32)
+    h = ctypes.c_void_p()
+    for flags in (2, 8, 2 | 8):
+        assert L.ore_model_load_ex(gpu_ctx.h, mb, len(mb), 2, flags, ctypes.byref(h)) == 2
+        assert b"retired" in L.ore_last_error(gpu_ctx.h)
+    assert _lib.LOAD_RETIRED_MASK == 10
+    m = ore.Model(gpu_ctx, mb, max_batch=2)
+    assert L.ore_model_set_fusion(m.h, ore.FUSE_ALL | 16) == 2 and b"retired" in L.ore_last_error(gpu_ctx.h)
+    m.close()

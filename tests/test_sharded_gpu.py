@@ -1,8 +1,11 @@
-"""SURVEY.md §8(e) correctness check on the HIP path: a global batch split over 2 ranks (two
-processes on GPU 0, gloo for the collective -- the RCCL all-gather of bench.py is the same
-ore.parallel.gather_rows call on device tensors), each rank running its slice through the HIP
-model, must gather to exactly the rows of a single-process HIP run of the whole batch, bit for bit.
-Uses the headline plan (max_batch 256: fused kernels, Winograd on) in every process."""
+"""SURVEY.md §8(e) correctness check on the HIP path: a global batch split unevenly (3 / 2 images)
+over 2 ranks (two processes on GPU 0), each rank running its slice through the HIP model, must gather
+to exactly the rows of a single-process HIP run of the whole batch, bit for bit.  The collective here
+is ore.parallel.run_sharded / gather_rows over gloo on host tensors (uneven blocks, padded); bench.py's
+per-step gather_rows_into (all_gather_into_tensor, even blocks) runs over gloo in
+tests/test_config4_gpu.py::test_bench_world2_gloo.  The RCCL all-gather of device tensors needs one
+GPU per rank and is not covered on the one-GPU test box.  Uses the headline plan (max_batch 256:
+fused kernels, Winograd on) in every process."""
 import os
 import socket
 

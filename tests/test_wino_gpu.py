@@ -19,7 +19,7 @@ import pytest
 
 from _knobs import conv_tile
 
-from test_x3_gpu import _conv_model, conv_f64
+from _convref import _conv_model, conv_f64
 
 pytestmark = pytest.mark.gpu
 
