@@ -1,0 +1,32 @@
+#!/bin/bash
+# Host-side ASan + UBSan builds of the ONNX parser (CPU) and of the whole library for the planner
+# driver (GPU box; device code is built normally -- GPU ASan / xnack are not available on this pool).
+# Outputs under tools/asan/build/ (git-ignored).  Usage: bash tools/asan/build.sh [parse|model|all]
+set -eu
+HERE="$(cd "$(dirname "$0")" && pwd)"
+CSRC="$HERE/../../onnx-rusty-inference-engine_amd/csrc"
+B="$HERE/build"
+mkdir -p "$B"
+SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=all -Xarch_host -fno-omit-frame-pointer"
+HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 -O1 -g -I$CSRC -I$HERE/../../include"
+what="${1:-parse}"
+if [ "$what" = parse ] || [ "$what" = all ]; then
+  # host only: the parser has no device code
+  $HIPCC --offload-host-only -x hip -fsanitize=address,undefined -fno-sanitize-recover=all -fno-omit-frame-pointer \
+    "$HERE/parse_fuzz.cpp" "$CSRC/ore_onnx.cpp" -o "$B/parse_fuzz"
+  echo "$B/parse_fuzz"
+fi
+if [ "$what" = model ] || [ "$what" = all ]; then
+  objs=()
+  for src in "$CSRC"/*.hip "$CSRC"/*.cpp; do
+    f=$(basename "${src%.*}")
+    extra=""
+    case "$src" in *ore_fire_f16.hip) extra="-fno-slp-vectorize";; esac
+    $HIPCC -O3 -x hip $SAN $extra -c "$src" -o "$B/$f.o" &
+    objs+=("$B/$f.o")
+  done
+  wait
+  $HIPCC -O1 -x hip $SAN -c "$HERE/model_fuzz.cpp" -o "$B/model_fuzz.o"
+  $HIPCC "${objs[@]}" "$B/model_fuzz.o" -fsanitize=address,undefined -o "$B/model_fuzz"
+  echo "$B/model_fuzz"
+fi
