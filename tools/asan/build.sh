@@ -12,7 +12,7 @@ HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 -O1 -g -I$CSRC -I$HE
 what="${1:-parse}"
 if [ "$what" = parse ] || [ "$what" = all ]; then
   # host only: the parser has no device code
-  $HIPCC --offload-host-only -x hip -fsanitize=address,undefined -fno-sanitize-recover=all -fno-omit-frame-pointer \
+  $HIPCC --offload-host-only -x hip -fno-gpu-sanitize -fsanitize=address,undefined -fno-sanitize-recover=all -fno-omit-frame-pointer \
     "$HERE/parse_fuzz.cpp" "$CSRC/ore_onnx.cpp" -o "$B/parse_fuzz"
   echo "$B/parse_fuzz"
 fi
@@ -27,6 +27,6 @@ if [ "$what" = model ] || [ "$what" = all ]; then
   done
   wait
   $HIPCC -O1 -x hip $SAN -c "$HERE/model_fuzz.cpp" -o "$B/model_fuzz.o"
-  $HIPCC "${objs[@]}" "$B/model_fuzz.o" -fsanitize=address,undefined -o "$B/model_fuzz"
+  $HIPCC "${objs[@]}" "$B/model_fuzz.o" -fno-gpu-sanitize -fsanitize=address,undefined -o "$B/model_fuzz"
   echo "$B/model_fuzz"
 fi
