@@ -278,12 +278,15 @@ def test_f16_tiles_bit_identical(gpu_ctx, cfg):
 
 
 def _fire_model_f16(C, H, W, S1, E1, E3, S2, ints=False, seed=0, pool=None):
+    # S2 None: no squeeze after the Concat (GAP reads it)
     """squeeze (C -> S1) -> expand 1x1 (E1) / 3x3 pad 1 (E3) -> Concat [-> 3x3 / stride-2 MaxPool with
     pads `pool`] -> squeeze (S2) -> GAP, all Relu; ints: sparse {-1, 0, 1} weights and small integer
     biases (every value exact in f16).  Returns (model bytes, {name: (w, b)})."""
     from ore import onnx_wire as wr
-    rng = np.random.default_rng(seed + C * 7 + H + W + S1 + E1 + E3 + S2)
-    shapes = {"wq": (S1, C, 1, 1), "w1": (E1, S1, 1, 1), "w3": (E3, S1, 3, 3), "wn": (S2, E1 + E3, 1, 1)}
+    rng = np.random.default_rng(seed + C * 7 + H + W + S1 + E1 + E3 + (S2 or 0))
+    shapes = {"wq": (S1, C, 1, 1), "w1": (E1, S1, 1, 1), "w3": (E3, S1, 3, 3)}
+    if S2 is not None:
+        shapes["wn"] = (S2, E1 + E3, 1, 1)
     params, inits, vinfo = {}, [], [wr.encode_value_info("x", (1, C, H, W))]
     for n, shp in shapes.items():
         if ints:
@@ -305,6 +308,9 @@ def _fire_model_f16(C, H, W, S1, E1, E3, S2, ints=False, seed=0, pool=None):
         nodes.append(wr.encode_node("MaxPool", ["cat"], ["pc"], attrs=[
             wr.encode_attr_ints("kernel_shape", [3, 3]), wr.encode_attr_ints("strides", [2, 2]),
             wr.encode_attr_string("auto_pad", "NOTSET"), wr.encode_attr_ints("pads", pool)]))
+    if S2 is None:  # the Concat read by something other than a squeeze (GAP): fire_f16_kernel's Concat form
+        nodes.append(wr.encode_node("GlobalAveragePool", ["cat"], ["y"]))
+        return wr.encode_model("fire", nodes, inits, vinfo, [wr.encode_value_info("y", (1, E1 + E3, 1, 1))]), params
     nodes += [conv("pc" if pool is not None else "cat", "wn", "n", [0] * 4), wr.encode_node("Relu", ["n"], ["nr"]),
               wr.encode_node("GlobalAveragePool", ["nr"], ["y"])]
     return wr.encode_model("fire", nodes, inits, vinfo, [wr.encode_value_info("y", (1, S2, 1, 1))]), params
@@ -344,6 +350,39 @@ def test_f16_fire_fusion_bit_identical(gpu_ctx, case):
     np.testing.assert_array_equal(vals[0][1], vals[1][1])
     np.testing.assert_array_equal(vals[0][0], vals[1][0])
     assert np.abs(vals[0][1]).max() > 0  # not a dead (all-Relu-zero) module
+
+
+FIRE_F16_CONCAT_CASES = [
+    # C, H, W, S1, E1, E3 -> fire_f16_kernel<S1 / 16, 0> (no squeeze: the kernel stores the Concat)
+    (8, 13, 13, 16, 64, 96),      # S1 = 16, unequal expands, 169 pixels (one partial 256-pixel tile)
+    (16, 10, 11, 32, 128, 64),    # S1 = 32, E1 > E3, 110 pixels
+    (24, 9, 7, 48, 96, 192),      # S1 = 48, W = 7, 63 pixels
+    (16, 27, 27, 64, 128, 256),   # S1 = 64 (SqueezeNet fire9's instance), 3 tiles per image, the last partial
+]
+
+
+@pytest.mark.parametrize("case", FIRE_F16_CONCAT_CASES)
+def test_f16_fire_concat_form_bit_identical(gpu_ctx, case):
+    """fire_f16_kernel's no-squeeze form (planner pass 6b) -- expands + Concat in one launch,
+    the Concat read by a non-squeeze (GAP here, conv10 in SqueezeNet) -- equals the two separate
+    conv_f16 launches bit for bit (the Concat itself and the GAP of it), at every squeeze width 16 / 32 /
+    48 / 64, unequal expands and plane sizes that are not a multiple of the 256-pixel tile."""
+    import ore
+    C, H, W, S1, E1, E3 = case
+    mb, _ = _fire_model_f16(C, H, W, S1, E1, E3, None)
+    x = np.random.default_rng(sum(case)).standard_normal((3, C, H, W)).astype(np.float32)
+    vals = []
+    for fusion in (ore.FUSE_ALL | ore.KEEP_VALUES, (ore.FUSE_ALL & ~ore.FUSE_FIRE) | ore.KEEP_VALUES):
+        m = ore.Model(gpu_ctx, mb, max_batch=3, precision="f16")
+        m.set_fusion(fusion)
+        y = _np(m.run(_t(x)))
+        names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+        vals.append((y, m.read_value("cat"), names))
+        m.close()
+    assert "fire f16" in vals[0][2] and "fire f16" not in vals[1][2], (vals[0][2], vals[1][2])
+    np.testing.assert_array_equal(vals[0][1], vals[1][1])
+    np.testing.assert_array_equal(vals[0][0], vals[1][0])
+    assert np.isfinite(vals[0][0]).all() and vals[0][1].shape == (3, E1 + E3, H, W)
 
 
 @pytest.mark.parametrize("case", [FIRE_F16_CASES[1], FIRE_F16_CASES[4]])
