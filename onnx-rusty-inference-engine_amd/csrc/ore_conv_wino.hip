@@ -440,9 +440,6 @@ constexpr int WM_KC = 8;      // input channels per K chunk (2 k-steps of 4)
 constexpr int WM_TILES = 64;  // 2x2 tiles per workgroup (16 per wave)
 constexpr int WM_CH = 32;     // output channels per workgroup
 constexpr int WM_ZL = 8;      // zero floats at the start of a staged channel (rows outside the image)
-#ifndef WM_PIPE
-#define WM_PIPE true
-#endif
 
 __device__ __forceinline__ void wm_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, int voffset, int soffset) {
   int m0save;
@@ -485,7 +482,7 @@ static int wm_group_floats(long long t0, long long T, int TPI, int TW, int H, in
   return total;
 }
 
-template <int NDMA, bool PIPE>  // NDMA: 256-float DMA pieces per staged channel (ceil(longest run set / 256))
+template <int NDMA>  // 256-float DMA pieces per staged channel (ceil(longest run set / 256))
 __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom g) {
   extern __shared__ __attribute__((aligned(16))) float wm_lds[];
   const int lane = threadIdx.x & 63;
@@ -604,92 +601,6 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
     wg_input_transform(d, v);
   };
 
-  if constexpr (PIPE) {
-    // k-step pipeline across chunk boundaries: k-step s's MFMAs run on operands read and transformed
-    // during k-step s - 1 (U quads replaced in place as each is consumed); the chunk barrier sits after
-    // the first quad of each chunk's second k-step, so the next chunk's reads issue under that k-step's
-    // MFMAs, and the DMA of chunk kc + 2 (into the stage chunk kc used) goes out right after it
-    float vc[16], vn[16], dn[4][4];
-    wg_floatx4 ua[2][4];
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (nchunks > 1) stage(1, 1);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int f = 0; f < 2; ++f) ua[f][q] = load_u(0, f, q);
-    load_win(0, dn);
-    xform(dn, vc);
-    for (int kc = 0; kc < nchunks; ++kc) {
-      const int st = kc & 1;
-      const int sto0 = st * SS * 4, sto1 = sto0 + 4 * g.CS * 4, ston = (st ^ 1) * SS * 4;
-      const bool more = kc + 1 < nchunks;
-      // ---- k-step 0: MFMAs on (ua, vc); k-step 1's window -> dn -> vn, its U in place
-      __builtin_amdgcn_sched_barrier(0);
-      load_win(sto1, dn);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int f = 0; f < 2; ++f)
-            acc[4 * q + j][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][q][j], vc[4 * q + j], acc[4 * q + j][f], 0, 0, 0);
-#pragma unroll
-        for (int f = 0; f < 2; ++f) ua[f][q] = load_u(sto0 + 4 * 512 * 4, f, q);
-      }
-      xform(dn, vn);
-      __builtin_amdgcn_sched_group_barrier(0x100, 8, 1);  // the window reads first
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          if (q > 0) __builtin_amdgcn_sched_group_barrier(0x002, 2, 1);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // ---- k-step 1: MFMAs on (ua, vn); after its first quad the chunk barrier, then chunk kc + 1
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int f = 0; f < 2; ++f)
-          acc[j][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][0][j], vn[j], acc[j][f], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (more) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk kc + 1 have landed
-        __syncthreads();  // ... every wave's, and every wave is done reading stage st
-        if (kc + 2 < nchunks) stage(kc + 2, st);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // chunk kc + 1's k-step 0 operands (after the last chunk: reads of the idle stage, never used)
-      load_win(ston, dn);
-#pragma unroll
-      for (int f = 0; f < 2; ++f) ua[f][0] = load_u(ston, f, 0);
-#pragma unroll
-      for (int q = 1; q < 4; ++q) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int f = 0; f < 2; ++f)
-            acc[4 * q + j][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][q][j], vn[4 * q + j], acc[4 * q + j][f], 0, 0, 0);
-#pragma unroll
-        for (int f = 0; f < 2; ++f) ua[f][q] = load_u(ston, f, q);
-      }
-      xform(dn, vc);
-#pragma unroll
-      for (int q = 1; q < 4; ++q) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
-          __builtin_amdgcn_sched_group_barrier(0x002, 2, 2);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -730,7 +641,6 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk kc + 1 have landed
     __syncthreads();  // ... every wave's, and every wave is done reading stage kc & 1
-  }
   }
   // lane (lk, lj) of fragment f holds rows 4 lk + e = channel m0 + 16 f + 4 lk + e of tile lj
   float bv[2][4];
@@ -783,12 +693,12 @@ static void launch_wm(const ConvParams& p0, const WmGeom& g, size_t lds, hipStre
     (void)hipGetDevice(&dev);
     const unsigned long long bit = 1ull << (dev & 63);
     if (!(raised.load(std::memory_order_acquire) & bit)) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_winol_kernel<NDMA, WM_PIPE>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_winol_kernel<NDMA>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       raised.fetch_or(bit, std::memory_order_acq_rel);
     }
   }
-  hipLaunchKernelGGL((conv_winol_kernel<NDMA, WM_PIPE>), dim3((unsigned)(g.ntg * p.mtiles)), dim3(256), lds, s, p, g);
+  hipLaunchKernelGGL((conv_winol_kernel<NDMA>), dim3((unsigned)(g.ntg * p.mtiles)), dim3(256), lds, s, p, g);
 }
 
 static void launch_winol(const ConvParams& p, hipStream_t s) {

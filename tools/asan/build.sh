@@ -21,7 +21,7 @@ if [ "$what" = model ] || [ "$what" = all ]; then
   for src in "$CSRC"/*.hip "$CSRC"/*.cpp; do
     f=$(basename "${src%.*}")
     extra=""
-    case "$src" in *ore_fire_f16.hip) extra="-fno-slp-vectorize";; esac
+    case "$src" in *ore_fire_f16.hip|*ore_conv_wino.hip) extra="-fno-slp-vectorize";; esac
     $HIPCC -O3 -x hip $SAN $extra -c "$src" -o "$B/$f.o" &
     objs+=("$B/$f.o")
   done

@@ -13,7 +13,7 @@ for src in "$PKG"/csrc/*.hip "$PKG"/csrc/*.cpp; do
   f=$(basename "${src%.*}")
   if [ -n "$ONLY" ] && [[ " $ONLY " != *" $f "* ]]; then continue; fi
   case "$src" in
-    *ore_fire_f16.hip) /opt/rocm/bin/hipcc $HIPFLAGS -fno-slp-vectorize -c "$src" -o "$B/$f.o" & ;;
+    *ore_fire_f16.hip|*ore_conv_wino.hip) /opt/rocm/bin/hipcc $HIPFLAGS -fno-slp-vectorize -c "$src" -o "$B/$f.o" & ;;
     *.cpp) /opt/rocm/bin/hipcc $HIPFLAGS -x hip -c "$src" -o "$B/$f.o" & ;;
     *) /opt/rocm/bin/hipcc $HIPFLAGS -c "$src" -o "$B/$f.o" & ;;
   esac
