@@ -37,7 +37,7 @@ extern "C" {
  * ABI 1's retired fusion bit 16 (ORE_FUSE_POOL_CONV), MaxPool variant 1 and conv tile ids 4-11, which
  * ABI 1 builds already refused.  ore_model_load accepts any max_batch: a batch whose activations
  * would pass the kernels' 32-bit offsets runs in image chunks inside ore_model_run.  Every other
- * entry point and value is unchanged (INTEGRATION.md section 5). */
+ * entry point and value is unchanged (INTEGRATION.md section 6). */
 #define ORE_ABI_VERSION 2
 
 typedef enum ore_status {
@@ -244,8 +244,10 @@ ore_status ore_model_destroy(ore_model* m);
 /* bit 10: a 3x3 / stride-2 MaxPool read only by a 1x1 conv (+ Relu, <= 64 channels) runs inside that
  * conv (f32 pool_conv1x1_f32_kernel: pool5 + fire9/squeeze). */
 #define ORE_FUSE_POOL_SQUEEZE 1024
-/* bit 12: f16 models: a 1x1 conv (+ Relu) whose only reader is GlobalAveragePool runs with the GAP in
- * its epilogue (conv1x1_gap_f16_kernel: conv10 + relu10 + pool10; not under ORE_KEEP_VALUES). */
+/* bit 12: a 1x1 conv (+ Relu) whose only reader is GlobalAveragePool runs with the GAP in its
+ * epilogue: conv10 + relu10 + pool10 in one launch, the conv map never stored (f16 models:
+ * conv1x1_gap_f16_kernel; f32 models since round 4: conv1x1_gap_f32_kernel, input channels a multiple
+ * of 32, <= 256 pixels).  Bit-identical to the separate launches; not under ORE_KEEP_VALUES. */
 #define ORE_FUSE_CONV_GAP 4096
 /* bit 11 (tests, not in ORE_FUSE_ALL): apply every eligible fusion regardless of the size
  * heuristics above (batch / plane thresholds, the 1.25 patch-work bound). */
@@ -277,7 +279,8 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
  * a benchmark-mode convolution search).  Results do not depend on the tile.  Synchronous.
  * reps: timed launches per candidate (<= 0: 3).  The choice survives ore_model_set_fusion. */
 ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, float* d_output, int32_t reps);
-/* Block tile chosen for exec step i (-1 for non-conv steps). */
+/* Block tile chosen for exec step i (-1 for non-conv steps); steps with one fixed kernel report its
+ * id (e.g. 49 / 50: conv + GlobalAveragePool, f16 / f32). */
 int32_t ore_model_step_tile(ore_model* m, int32_t i);
 /* Set exec step i's tile (one of the ids ore_model_autotune chooses among for that step; e.g. to
  * restore a saved autotune result).  ORE_ERR_INVALID for an id outside the step's kernel family.

@@ -442,17 +442,7 @@ constexpr int WM_CH = 32;     // output channels per workgroup
 constexpr int WM_ZL = 8;      // zero floats at the start of a staged channel (rows outside the image)
 
 __device__ __forceinline__ void wm_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, int voffset, int soffset) {
-  int m0save;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(m0save)
-      : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voffset), "s"(rsrc),
-        "s"(__builtin_amdgcn_readfirstlane(soffset))
-      : "memory");
+  ore_lds_dma16(rsrc, lds_addr, voffset, soffset);
 }
 
 // geometry of the LDS kernel (host-computed)

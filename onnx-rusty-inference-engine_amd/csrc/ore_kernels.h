@@ -51,6 +51,24 @@ __device__ __forceinline__ ore_h8 ore_f16_epilogue8(const float* a, const float*
 
 #define ORE_BAND_ID() xcd_block_id()
 
+// 16-B LDS-DMA (buffer_load_dwordx4 ... lds): lane i's 16 bytes from rsrc + voffset + soffset land at
+// LDS byte lds_addr + 16 i (lds_addr, soffset wave-uniform); offsets past the records read 0.  Counted by
+// vmcnt like any buffer load; nothing orders a later ds_read behind it but the issuing wave's vmcnt
+// (and a barrier for the other waves).
+__device__ __forceinline__ void ore_lds_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, int voffset, int soffset) {
+  int m0save;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(m0save)
+      : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voffset), "s"(rsrc),
+        "s"(__builtin_amdgcn_readfirstlane(soffset))
+      : "memory");
+}
+
 struct ConvParams {
   const float* x;      // input  [N][C][H][W], image stride x_nstride
   const float* wp;     // packed weights Wp[Kp][Mp] (launch_pack_weights)
@@ -263,6 +281,18 @@ struct Conv1x1GapF16 {
 };
 bool conv1x1_gap_f16_eligible(const Conv1x1GapF16& p);
 void launch_conv1x1_gap_f16(const Conv1x1GapF16& p, hipStream_t s);
+// f32 models: the same fusion (conv1x1_gap_f32_kernel, ore_conv_gap.hip): x f32 NCHW [N][C][x_ps] (P <= 256
+// pixels per plane), wc the weights in launch_pack_c1_f32's layout, y f32 [N][M] (image stride y_nstride)
+struct Conv1x1GapF32 {
+  const float* x;
+  const float* wc;
+  const float* bias;
+  float* y;
+  int N, C, P, M, x_ps, relu;
+  long long x_nstride, y_nstride;
+};
+bool conv1x1_gap_f32_eligible(const Conv1x1GapF32& p);
+void launch_conv1x1_gap_f32(const Conv1x1GapF32& p, hipStream_t s);
 // Concat along channels of two dense NHWC f16 values (pixels = N*H*W)
 void launch_concat_nhwc(const void* a, const void* b, void* y, long long pixels, int Ca, int Cb, hipStream_t s);
 void launch_conv_f16(const ConvParams& p, int cfg, int xmode, hipStream_t s);
@@ -339,6 +369,7 @@ constexpr int WINO_TILES_N = 5;
 // fused-kernel ids after the Winograd tiles (ore.Model.TILE_NAMES): 41 is retired (the Winograd fire module)
 constexpr int FIRE_F16_TILE = 42, C1_POOL_F16_TILE = 43;
 constexpr int CONV_GAP_F16_TILE = 49;  // conv1x1_gap_f16_kernel: ore.Model.TILE_NAMES "conv1x1 gap f16"
+constexpr int CONV_GAP_F32_TILE = 50;  // conv1x1_gap_f32_kernel: ore.Model.TILE_NAMES "conv1x1 gap f32"
 bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo);
 bool conv_wino_eligible(const ConvParams& p, int tile);
 int wino_packed_mp(int M);

@@ -1048,12 +1048,32 @@ struct Planner {
   // epilogue (conv1x1_gap_f16_kernel: SqueezeNet conv10 -> relu10 -> pool10; the 87 MB map is never
   // stored).  Bit-identical to conv_f16 + gap_nhwc_kernel.  Not under ORE_KEEP_VALUES (the conv output
   // would not exist to read back).
-  void conv_gap() {
-    if (!has(ORE_FUSE_CONV_GAP) || !m->f16 || has(ORE_KEEP_VALUES)) return;
+  ore_status conv_gap() {
+    if (!has(ORE_FUSE_CONV_GAP) || has(ORE_KEEP_VALUES)) return ORE_OK;
     for (size_t i = 0; i < m->steps.size(); ++i) {
       Step& g = st(int(i));
       if (g.kind != S_GAP) continue;
       const int v = g.in0;
+      if (!m->f16) {  // f32: conv1x1_gap_f32_kernel (the conv's weights in launch_pack_c1_f32's layout)
+        if (v < 0 || !private_value(v) || val(v).es != 4 || val(v).nhwc || producer[v] < 0) continue;
+        Step& cv = st(producer[v]);
+        if (cv.kind != S_CONV || cv.out != v || cv.plan.f16 || cv.plan.wino || cv.epool || cv.pool || cv.c1sq ||
+            cv.kh != 1 || cv.kw != 1 || cv.sh != 1 || cv.sw != 1 || cv.win.pt != 0 || cv.win.pl != 0 ||
+            cv.win.Ho != cv.H || cv.win.Wo != cv.W || cv.C % 32 != 0 || cv.H * cv.W > 256 || val(cv.in0).es != 4)
+          continue;
+        const int key = 4000000 + producer[v], M = int(cv.M), K = int(cv.C);
+        const float* w = val(cv.in1).cptr;
+        if (!pack_once(key, c1_f32_pack_bytes(M, K), [&](float* buf) { launch_pack_c1_f32(w, M, K, buf, m->ctx->stream); }))
+          return err(m, ORE_ERR_HIP, "conv + GAP weight packing failed");
+        cv.wc1 = m->fire_packs[key];
+        cv.gap = true;
+        cv.out = g.out;
+        cv.bytes_per_img = 4.0 * double(cv.C * cv.H * cv.W) + 4.0 * double(cv.M);
+        cv.name = cv.name + "+" + g.name;
+        val(v).elided = true;
+        nop(g);
+        continue;
+      }
       if (v < 0 || !private_value(v) || !val(v).nhwc || val(v).es != 2 || producer[v] < 0) continue;
       Step& cv = st(producer[v]);
       if (cv.kind != S_CONV || cv.out != v || !cv.plan.f16 || cv.plan.xmode != F16_X_NHWC_VEC || cv.epool || cv.pool ||
@@ -1068,6 +1088,7 @@ struct Planner {
       nop(g);
     }
     recount();
+    return ORE_OK;
   }
 
   // (9) algorithm selection, a load-time rule (never by timing): f32 models with Winograd on run every
@@ -1327,7 +1348,7 @@ ore_status plan(ore_model* m) {
   if (ore_status st = p.fire_f16_concat()) return st;
   if (ore_status st = p.first_squeeze()) return st;
   p.pool_squeeze();
-  p.conv_gap();
+  if (ore_status st = p.conv_gap()) return st;
   p.select_algorithms();
   p.alias_copies();
   p.concat_in_place();
@@ -1429,6 +1450,15 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
         launch_conv1x1_gap_f16(q, ctx->stream);
         ORE_HIP_CHECK(ctx, hipGetLastError());
         s.ran_tile = last_conv_tile = CONV_GAP_F16_TILE;
+        return ORE_OK;
+      }
+      if (s.gap) {  // f32: conv1x1_gap_f32_kernel
+        const Conv1x1GapF32 q{x.p, s.wc1, bias, y.p, int(n), int(s.C), int(s.H * s.W), int(s.M),
+                              int(x.ps ? x.ps : s.H * s.W), s.relu ? 1 : 0, x.nstride, y.nstride};
+        if (!conv1x1_gap_f32_eligible(q)) return err(m, ORE_ERR_INVALID, "internal: conv + GAP on an unsupported layout");
+        if (n > 0) launch_conv1x1_gap_f32(q, ctx->stream);
+        ORE_HIP_CHECK(ctx, hipGetLastError());
+        s.ran_tile = last_conv_tile = CONV_GAP_F32_TILE;
         return ORE_OK;
       }
       if (s.plan.f16)
@@ -1997,7 +2027,7 @@ int32_t ore_model_step_tile(ore_model* m, int32_t i) {
   if (s.kind == S_FIRE) return s.fire_f16 ? FIRE_F16_TILE : s.fire_pool ? FIRE_POOL_TILE : FIRE_TILE;
   if (s.kind == S_CONV && s.epool && !s.plan.f16 && s.plan.epv > 0) return epool_tile_id(s.plan.epv);
   if (s.kind == S_CONV && s.epool && s.ran_tile >= 0) return s.ran_tile;
-  if (s.kind == S_CONV && s.gap) return CONV_GAP_F16_TILE;
+  if (s.kind == S_CONV && s.gap) return s.plan.f16 ? CONV_GAP_F16_TILE : CONV_GAP_F32_TILE;
   return (s.kind == S_CONV || s.kind == S_MATMUL) ? s.plan.cfg : -1;
 }
 
