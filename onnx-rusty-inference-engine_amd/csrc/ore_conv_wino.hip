@@ -436,6 +436,16 @@ __global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
 //     next k-step's U quads are read as the MFMAs that used the current ones issue.
 // Each position is the same c-ordered fma chain and the transforms the same add order as tiles 0-3:
 // bit-identical to them.
+#ifdef ORE_STAMPS
+__device__ unsigned long long ore_wino_stamps[1 << 17];
+extern "C" int ore_debug_stamps_wino(void* dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ore_wino_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int ore_debug_stamps_wino_clear() {
+  static unsigned long long zero[1 << 17];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(ore_wino_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+#endif
 constexpr int WM_KC = 8;      // input channels per K chunk (2 k-steps of 4)
 constexpr int WM_TILES = 64;  // 2x2 tiles per workgroup (16 per wave)
 constexpr int WM_CH = 32;     // output channels per workgroup
@@ -477,6 +487,12 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   extern __shared__ __attribute__((aligned(16))) float wm_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifdef ORE_STAMPS
+  if (wave == 0) {
+    ore_stamp(ore_wino_stamps, blockIdx.x * 8LL);
+    ore_stamp_ids(ore_wino_stamps, blockIdx.x * 8LL + 4);
+  }
+#endif
   // block -> (tile group, 32-channel block), the channel blocks of a tile group consecutive (one XCD:
   // they share the staged rows in L2)
   const int nwg = gridDim.x, bid = blockIdx.x;
@@ -564,11 +580,10 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
     }
   };
 
+  // accumulators: no zeroing -- chunk 0's first k-step takes C = 0 (an inline operand of the MFMA; 128
+  // v_mov per wave otherwise, and f32 MFMAs and VALU share the SIMD's issue, nothing overlaps them)
   wg_floatx4 acc[16][2];
-#pragma unroll
-  for (int xi = 0; xi < 16; ++xi)
-#pragma unroll
-    for (int f = 0; f < 2; ++f) acc[xi][f] = wg_floatx4{0.f, 0.f, 0.f, 0.f};
+  const wg_floatx4 zero4 = {0.f, 0.f, 0.f, 0.f};
 
   const char* lds_b = reinterpret_cast<const char*>(wm_lds);
   auto load_win = [&](int sto, float (&d)[4][4]) __attribute__((always_inline)) {
@@ -590,11 +605,9 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
     }
     wg_input_transform(d, v);
   };
-
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kc = 0; kc < nchunks; ++kc) {
+  // one chunk (two k-steps of 4 channels); FIRST: chunk 0, its first k-step starts the accumulators
+  auto chunk = [&](int kc, auto first) __attribute__((always_inline)) {
+    constexpr bool FIRST = decltype(first)::value;
     const int st = kc & 1;
     if (kc + 1 < nchunks) stage(kc + 1, st ^ 1);
     const int sto0 = st * SS * 4, sto1 = sto0 + 4 * g.CS * 4;  // k-step 1: channels 4 .. 7 of the chunk
@@ -615,7 +628,8 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int f = 0; f < 2; ++f)
-          acc[4 * q + j][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][q][j], v[4 * q + j], acc[4 * q + j][f], 0, 0, 0);
+          acc[4 * q + j][f] =
+              __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][q][j], v[4 * q + j], FIRST ? zero4 : acc[4 * q + j][f], 0, 0, 0);
 #pragma unroll
       for (int f = 0; f < 2; ++f) ua[f][q] = load_u(sto0 + 4 * 512 * 4, f, q);
     }
@@ -631,7 +645,19 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk kc + 1 have landed
     __syncthreads();  // ... every wave's, and every wave is done reading stage kc & 1
-  }
+  };
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#ifdef ORE_STAMPS
+  if (wave == 0) ore_stamp(ore_wino_stamps, blockIdx.x * 8LL + 1);
+#endif
+  chunk(0, std::true_type{});
+  for (int kc = 1; kc < nchunks; ++kc) chunk(kc, std::false_type{});
+#ifdef ORE_STAMPS
+  if (wave == 0) ore_stamp(ore_wino_stamps, blockIdx.x * 8LL + 2);
+#endif
   // lane (lk, lj) of fragment f holds rows 4 lk + e = channel m0 + 16 f + 4 lk + e of tile lj
   float bv[2][4];
 #pragma unroll
@@ -652,6 +678,9 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
       for (int xi = 0; xi < 16; ++xi) mx[xi] = acc[xi][f][e];
       wg_store(p, w, m, bv[f][e], mx);
     }
+#ifdef ORE_STAMPS
+  if (wave == 0) ore_stamp(ore_wino_stamps, blockIdx.x * 8LL + 3);
+#endif
 }
 
 // the LDS kernel's geometry; false when the layer does not fit it

@@ -55,6 +55,17 @@ __device__ __forceinline__ ore_h8 ore_f16_epilogue8(const float* a, const float*
 // LDS byte lds_addr + 16 i (lds_addr, soffset wave-uniform); offsets past the records read 0.  Counted by
 // vmcnt like any buffer load; nothing orders a later ds_read behind it but the issuing wave's vmcnt
 // (and a barrier for the other waves).
+#ifdef ORE_STAMPS  // timing experiments only (tools/stamps.py): per-workgroup s_memtime stamps
+__device__ __forceinline__ void ore_stamp(unsigned long long* buf, long long idx) {
+  if ((threadIdx.x & 63) == 0) buf[idx] = __builtin_amdgcn_s_memtime();
+}
+__device__ __forceinline__ void ore_stamp_ids(unsigned long long* buf, long long idx) {
+  if ((threadIdx.x & 63) == 0) {
+    buf[idx] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    buf[idx + 1] = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+  }
+}
+#endif
 __device__ __forceinline__ void ore_lds_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, int voffset, int soffset) {
   int m0save;
   asm volatile(
