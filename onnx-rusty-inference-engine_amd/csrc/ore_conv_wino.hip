@@ -195,6 +195,19 @@ __device__ __forceinline__ void wg_store(const ConvParams& p, const WgTile& w, i
   wg_store_px(p, w, p.y, m, o);
 }
 
+// wg_store with the Relu a compile-time choice (a runtime one costs a select per pixel)
+template <bool RELU>
+__device__ __forceinline__ void wg_store_t(const ConvParams& p, const WgTile& w, int m, float b, const float (&mx)[16]) {
+  float o[4];
+  wg_output_transform(mx, o);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    o[q] += b;
+    if constexpr (RELU) o[q] = fmaxf(o[q], 0.0f);
+  }
+  wg_store_px(p, w, p.y, m, o);
+}
+
 // The K loop of both kernels over WG_LOAD_A(slot, step), WG_LOAD_B(slot, step), WG_MFMA(a slot, b slot)
 #define WG_KLOOP(NKS_RT)                                                                               \
   if constexpr (NKS > 0) {                                                                             \
@@ -482,7 +495,7 @@ static int wm_group_floats(long long t0, long long T, int TPI, int TW, int H, in
   return total;
 }
 
-template <int NDMA>  // 256-float DMA pieces per staged channel (ceil(longest run set / 256))
+template <int NDMA, bool RELU>  // NDMA: 256-float DMA pieces per staged channel (ceil(longest run set / 256))
 __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom g) {
   extern __shared__ __attribute__((aligned(16))) float wm_lds[];
   const int lane = threadIdx.x & 63;
@@ -676,7 +689,7 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
       float mx[16];
 #pragma unroll
       for (int xi = 0; xi < 16; ++xi) mx[xi] = acc[xi][f][e];
-      wg_store(p, w, m, bv[f][e], mx);
+      wg_store_t<RELU>(p, w, m, bv[f][e], mx);
     }
 #ifdef ORE_STAMPS
   if (wave == 0) ore_stamp(ore_wino_stamps, blockIdx.x * 8LL + 3);
@@ -702,8 +715,8 @@ static bool wm_geom(const ConvParams& p, WmGeom* g, size_t* lds, int* ndma) {
   return *ndma <= 8 && *lds <= 160 * 1024;
 }
 
-template <int NDMA>
-static void launch_wm(const ConvParams& p0, const WmGeom& g, size_t lds, hipStream_t s) {
+template <int NDMA, bool RELU>
+static void launch_wm_r(const ConvParams& p0, const WmGeom& g, size_t lds, hipStream_t s) {
   ConvParams p = p0;
   p.mtiles = (p.M + WM_CH - 1) / WM_CH;
   if (lds > 64 * 1024) {  // above the default dynamic-LDS limit: raise it once per device
@@ -712,12 +725,20 @@ static void launch_wm(const ConvParams& p0, const WmGeom& g, size_t lds, hipStre
     (void)hipGetDevice(&dev);
     const unsigned long long bit = 1ull << (dev & 63);
     if (!(raised.load(std::memory_order_acquire) & bit)) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_winol_kernel<NDMA>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_winol_kernel<NDMA, RELU>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       raised.fetch_or(bit, std::memory_order_acq_rel);
     }
   }
-  hipLaunchKernelGGL((conv_winol_kernel<NDMA>), dim3((unsigned)(g.ntg * p.mtiles)), dim3(256), lds, s, p, g);
+  hipLaunchKernelGGL((conv_winol_kernel<NDMA, RELU>), dim3((unsigned)(g.ntg * p.mtiles)), dim3(256), lds, s, p, g);
+}
+
+template <int NDMA>
+static void launch_wm(const ConvParams& p, const WmGeom& g, size_t lds, hipStream_t s) {
+  if (p.relu)
+    launch_wm_r<NDMA, true>(p, g, lds, s);
+  else
+    launch_wm_r<NDMA, false>(p, g, lds, s);
 }
 
 static void launch_winol(const ConvParams& p, hipStream_t s) {
