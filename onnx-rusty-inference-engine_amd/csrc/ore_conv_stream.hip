@@ -375,7 +375,7 @@ static int stream_mode(const ConvParams& p) {
 
 static int stream_depth(int tile) {
   const int t = tile - CONV_TILE_STREAM;
-  return t == 6 ? 8 : t == 8 ? 2 : 4;
+  return t == 6 ? 8 : 4;
 }
 
 // the geometry allows the streaming kernel and the tile's ring depth divides the K steps; the
@@ -445,7 +445,7 @@ void launch_conv_stream(const ConvParams& p, int tile, hipStream_t s) {
     case 5: launch_cs<8, 1, 4>(p, s); break;   // 128 x 64
     case 6: launch_cs<4, 1, 8>(p, s); break;   // 64 x 64, 8 k-steps in flight
     case 7: launch_cs<2, 2, 4>(p, s); break;   // 32 x 128
-    default: launch_cs<8, 1, 2>(p, s); break;  // 128 x 64, 2 k-steps in flight
+    default: launch_cs<3, 1, 4>(p, s); break;  // 48 x 64 (round 4; was 128 x 64 with 2 k-steps in flight)
   }
 }
 

@@ -358,7 +358,7 @@ constexpr int FIRE_TILE = 21;       // the fused f32 fire module (fire_kernel): 
 inline bool conv_tile_retired(int t) { return (t >= 4 && t < 12) || (t >= 28 && t < 36); }
 // LDS-free streaming kernel (ore_conv_stream.hip): 1x1 convs and stride-1 convs with Wo == W (every
 // expand3x3); tiles CONV_TILE_STREAM + 0..8 = 64x128, 32x256, 16x256, 48x128, 64x64, 128x64, 64x64 D8,
-// 32x128, 128x64 D2 (channels x pixels per wave); other geometries fall back to tile 0
+// 32x128, 48x64 (round 4; 128x64 D2 before) (channels x pixels per wave); other geometries fall back to tile 0
 constexpr int CONV_TILE_STREAM = 12;
 // persistent 1x1 streaming tiles (conv_stream1x1_persist_kernel): 32x128, 64x64, 16x256; ids after the
 // fused-kernel ids (ore.Model.TILE_NAMES "stream1x1 persist ...")

@@ -315,7 +315,7 @@ class Model:
                   None, None, None, None,  # 4-7: the LDS-free direct conv
                   None, None, None, None,  # 8-11: the warp-specialised conv_gemm_kernel
                   "stream 64x128", "stream 32x256", "stream 16x256", "stream 48x128", "stream 64x64",
-                  "stream 128x64", "stream 64x64 d8", "stream 32x128", "stream 128x64 d2", "fire",
+                  "stream 128x64", "stream 64x64 d8", "stream 32x128", "stream 48x64", "fire",
                   "epool patch", "epool walk48", "epool walk96", "epool walk64",
                   "epool walk64 b3", None,  # 27: the 2-band walker
                   None, None, None, None, None, None, None, None,  # 28-35: ABI 1's bf16x3 kernels
