@@ -36,6 +36,7 @@ typedef float c3f16 __attribute__((ext_vector_type(16)));
 
 constexpr int C3_PR = EPOOL_TILE_PR, C3_PC = EPOOL_TILE_PC;  // pooled outputs per tile (6 x 9)
 constexpr int C3_RC = 2 * C3_PR + 1, C3_CC = 2 * C3_PC + 1, C3_NPX = C3_RC * C3_CC;  // 13 x 19 conv patch
+constexpr int C3_OOB = 0x40000000;  // a window byte offset past any image (C x_ps 4 < 2^30, eligibility)
 constexpr int C3_TS = 36;  // conv tile pixel stride (floats): 144 B, 16-B aligned, an odd multiple of 16 B
 
 template <int C, int KH, int KW, int S>
@@ -53,7 +54,7 @@ struct C3Geo {
   }
 };
 
-template <int MF, int C, int KH, int KW, int S, int SQ>
+template <int MF, int C, int KH, int KW, int S, int SQ, bool RELU, bool IN>  // IN: every tile's window inside the image
 __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p, const float* __restrict__ wc,
                                                                    C1SqueezeF32 sq) {
   using G = C3Geo<C, KH, KW, S>;
@@ -100,13 +101,18 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
     bk3[f] = base * 4;
     tpx[f] = pq * C3_TS;
   }
-  // this thread's window elements q = tid + 256 u: (plane, row, column)
+  // this thread's window elements q = tid + 256 u, (plane c, row r, column cc).  IN: the byte offset
+  // (c x_ps + r W + cc) 4 from the window's origin in the image (past the window: C3_OOB, which reads
+  // 0); else the packed (c, r, cc) for the per-element bounds
   int wq[G::NQ];
 #pragma unroll
   for (int u = 0; u < G::NQ; ++u) {
     const int q = tid + 256 * u;
     const int c = q / G::PLANE, rc = q - c * G::PLANE, r = rc / G::HC, cc = rc - r * G::HC;
-    wq[u] = q < G::WIN ? (c << 24) | (r << 12) | cc : -1;
+    if constexpr (IN)
+      wq[u] = q < G::WIN ? (c * p.x_ps + r * p.W + cc) * 4 : C3_OOB;
+    else
+      wq[u] = q < G::WIN ? (c << 24) | (r << 12) | cc : -1;
   }
   const int tpi = p.ep_tr * p.ep_tc, ntiles = p.N * tpi;
   float xv[G::NQ];
@@ -117,12 +123,22 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
     const int ihb = (ph0 * 2 - p.ep_pt) * S - p.pt, iwb = (pw0 * 2 - p.ep_pl) * S - p.pl;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(p.x + (long long)img * p.x_nstride), (short)0, C * p.x_ps * 4, 0x00020000);
+    if constexpr (IN) {
+      // every window lies inside the image (conv1 of a 224 x 224 SqueezeNet input): the tile's origin
+      // is the scalar offset of each load, no per-element VALU (f32 MFMAs hold the SIMD's VALU,
+      // DESIGN.md section 3.7)
+      const int so = (ihb * p.W + iwb) * 4;
 #pragma unroll
-    for (int u = 0; u < G::NQ; ++u) {
-      const int e = wq[u], c = e >> 24, ih = ihb + ((e >> 12) & 0xfff), iw = iwb + (e & 0xfff);
-      const bool in = e >= 0 && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-      xv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                            rs, in ? (c * p.x_ps + ih * p.W + iw) * 4 : (int)0x80000000, 0, 0));
+      for (int u = 0; u < G::NQ; ++u)
+        xv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, wq[u], so, 0));
+    } else {  // per-element bounds (offsets outside the image read 0: the conv's zero padding)
+#pragma unroll
+      for (int u = 0; u < G::NQ; ++u) {
+        const int e = wq[u], c = e >> 24, ih = ihb + ((e >> 12) & 0xfff), iw = iwb + (e & 0xfff);
+        const bool in = e >= 0 && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        xv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                              rs, in ? (c * p.x_ps + ih * p.W + iw) * 4 : (int)0x80000000, 0, 0));
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -213,16 +229,21 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
         if (!pin[f]) continue;
         const int px = (2 * wave + f) * 32 + lr, pr = px / C3_CC, pc = px - pr * C3_CC;
         const bool cok = (unsigned)(ohb + pr) < (unsigned)p.Ho && (unsigned)(owb + pc) < (unsigned)p.Wo;
+        // Relu and the zero outside the conv plane in one v_med3_f32: median(v, 0, +inf) = max(v, 0),
+        // median(v, 0, 0) = 0; the bias adds on packed f32 (f32 MFMAs hold the SIMD's VALU, so every
+        // epilogue instruction is paid in full)
+        const float top = cok ? __builtin_inff() : 0.0f;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int ch = 8 * g + 4 * h;  // accumulator rows 8 g + 4 h + 0..3
-          c3f4 o;
+          const c3f4 sb = *reinterpret_cast<const c3f4*>(sbias + 32 * i + ch);
+          c3f4 o = c3f4{acc[i][f][4 * g], acc[i][f][4 * g + 1], acc[i][f][4 * g + 2], acc[i][f][4 * g + 3]} + sb;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int m = 32 * i + ch + e;
-            float v = acc[i][f][4 * g + e] + sbias[m];
-            if (p.relu) v = fmaxf(v, 0.0f);
-            o[e] = cok ? v : 0.0f;
+            if constexpr (RELU)
+              o[e] = __builtin_amdgcn_fmed3f(o[e], 0.0f, top);
+            else
+              o[e] = cok ? o[e] : 0.0f;
           }
           *reinterpret_cast<c3f4*>(ct + tpx[f] + ch) = o;
         }
@@ -310,7 +331,7 @@ __global__ __launch_bounds__(256) void pack_c1_f32_kernel(const float* __restric
   }
 }
 
-template <int MF, int C, int SQ>
+template <int MF, int C, int SQ, bool RELU, bool IN>
 static bool c3_launch(const ConvParams& p, const float* wc, const C1SqueezeF32& sq, hipStream_t s) {
   using G = C3Geo<C, 7, 7, 2>;
   const long long tiles = (long long)p.N * p.ep_tr * p.ep_tc;
@@ -323,14 +344,27 @@ static bool c3_launch(const ConvParams& p, const float* wc, const C1SqueezeF32& 
   // conv1's 96 channels), each taking every grid-th tile
   const unsigned lds = G::LDS + MF * 32 * 4 + (SQ ? 64 * C3_TS * 4 + 16 * 4 : 0);
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_win_pool_f32_kernel<MF, C, 7, 7, 2, SQ>, 256, lds) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_win_pool_f32_kernel<MF, C, 7, 7, 2, SQ, RELU, IN>, 256, lds) !=
           hipSuccess || per_cu < 1)
     per_cu = 2;
   long long grid = std::min<long long>(tiles, (long long)per_cu * ncu);
   if (grid >= 8) grid &= ~7LL;  // a multiple of 8: XCD-grouped tile ranges
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((conv_win_pool_f32_kernel<MF, C, 7, 7, 2, SQ>), dim3((unsigned)grid), dim3(256), lds, s, p, wc, sq);
+  hipLaunchKernelGGL((conv_win_pool_f32_kernel<MF, C, 7, 7, 2, SQ, RELU, IN>), dim3((unsigned)grid), dim3(256), lds, s, p, wc, sq);
   return true;
+}
+
+template <int MF, int C, int SQ>
+static bool c3_launch_r(const ConvParams& p, const float* wc, const C1SqueezeF32& sq, hipStream_t s) {
+  // every tile's input window [ihb, ihb + HR) x [iwb, iwb + HC) inside the image?
+  using G = C3Geo<C, 7, 7, 2>;
+  const long long ih0 = -(long long)p.ep_pt * 2 - p.pt, iw0 = -(long long)p.ep_pl * 2 - p.pl;
+  const long long ih1 = ((long long)(p.ep_tr - 1) * C3_PR * 2 - p.ep_pt) * 2 - p.pt + G::HR;
+  const long long iw1 = ((long long)(p.ep_tc - 1) * C3_PC * 2 - p.ep_pl) * 2 - p.pl + G::HC;
+  const bool in = ih0 >= 0 && iw0 >= 0 && ih1 <= p.H && iw1 <= p.W;
+  if (p.relu)
+    return in ? c3_launch<MF, C, SQ, true, true>(p, wc, sq, s) : c3_launch<MF, C, SQ, true, false>(p, wc, sq, s);
+  return in ? c3_launch<MF, C, SQ, false, true>(p, wc, sq, s) : c3_launch<MF, C, SQ, false, false>(p, wc, sq, s);
 }
 
 }  // namespace
@@ -351,7 +385,7 @@ bool conv_win_pool_f32_eligible(const ConvParams& p, const C1SqueezeF32* sq) {
              p.C != 3))
     return false;
   return p.kh == 7 && p.kw == 7 && p.sh == 2 && p.sw == 2 && (p.C == 1 || p.C == 3 || p.C == 4) && MF >= 2 &&
-         MF <= 4 && p.ep_tr > 0 && p.ep_tc > 0 && p.x_ps >= p.H * p.W && (long long)p.C * p.x_ps * 4 < (1LL << 31) &&
+         MF <= 4 && p.ep_tr > 0 && p.ep_tc > 0 && p.x_ps >= p.H * p.W && (long long)p.C * p.x_ps * 4 < (1LL << 30) &&
          p.H < 4096 && p.W < 4096;
 }
 
@@ -359,19 +393,19 @@ void launch_conv_win_pool_f32(const ConvParams& p, const float* wc, const C1Sque
   const int MF = (p.M + 31) / 32;
   const C1SqueezeF32 none{};
   if (sq) {  // the fused squeeze: conv1's geometry (96 channels, 3 inputs)
-    c3_launch<3, 3, 1>(p, wc, *sq, s);
+    c3_launch_r<3, 3, 1>(p, wc, *sq, s);
     return;
   }
   switch (MF * 8 + p.C) {
-    case 2 * 8 + 1: c3_launch<2, 1, 0>(p, wc, none, s); break;
-    case 2 * 8 + 3: c3_launch<2, 3, 0>(p, wc, none, s); break;
-    case 2 * 8 + 4: c3_launch<2, 4, 0>(p, wc, none, s); break;
-    case 3 * 8 + 1: c3_launch<3, 1, 0>(p, wc, none, s); break;
-    case 3 * 8 + 3: c3_launch<3, 3, 0>(p, wc, none, s); break;
-    case 3 * 8 + 4: c3_launch<3, 4, 0>(p, wc, none, s); break;
-    case 4 * 8 + 1: c3_launch<4, 1, 0>(p, wc, none, s); break;
-    case 4 * 8 + 3: c3_launch<4, 3, 0>(p, wc, none, s); break;
-    default: c3_launch<4, 4, 0>(p, wc, none, s); break;
+    case 2 * 8 + 1: c3_launch_r<2, 1, 0>(p, wc, none, s); break;
+    case 2 * 8 + 3: c3_launch_r<2, 3, 0>(p, wc, none, s); break;
+    case 2 * 8 + 4: c3_launch_r<2, 4, 0>(p, wc, none, s); break;
+    case 3 * 8 + 1: c3_launch_r<3, 1, 0>(p, wc, none, s); break;
+    case 3 * 8 + 3: c3_launch_r<3, 3, 0>(p, wc, none, s); break;
+    case 3 * 8 + 4: c3_launch_r<3, 4, 0>(p, wc, none, s); break;
+    case 4 * 8 + 1: c3_launch_r<4, 1, 0>(p, wc, none, s); break;
+    case 4 * 8 + 3: c3_launch_r<4, 3, 0>(p, wc, none, s); break;
+    default: c3_launch_r<4, 4, 0>(p, wc, none, s); break;
   }
 }
 

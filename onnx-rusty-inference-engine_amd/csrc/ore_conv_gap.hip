@@ -10,8 +10,8 @@
 // LDS-DMA into a double-buffered stage (the next chunk in flight during this one; plain loads when the
 // planes are not 16-B aligned, e.g. an unpadded 13x13 map).  B (pixels) from the stage by one
 // ds_read_b32 per fragment and k-step, each feeding both row tiles, the next k-step's read issued as
-// the current one's MFMAs go out; A (weights) from L2 in launch_pack_c1_f32's layout (one 16-B load per
-// lane and row tile covers two k-steps).  The m-blocks of one image run consecutively on one XCD, so
+// the current one's MFMAs go out; A (weights) from L2 in launch_pack_cg_f32's layout (one 16-B load per
+// lane and row tile covers four k-steps, in the lane's own k order: no selects).  The m-blocks of one image run consecutively on one XCD, so
 // the image's map is read from HBM about once.  Epilogue: bias + Relu into an LDS tile [16 channels]
 // [pixels] per wave (two passes), then one lane per channel sums the P pixels in order (gap_kernel's
 // sequential sum) and divides by P.  Same operands, k order and f32 fma chain as the streaming conv
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(CG_NT, (CG_RT * NF > 22 ? 2 : 3)) void conv1x1_gap_
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(p.x + (long long)img * p.x_nstride), (short)0, p.C * p.x_ps * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(p.wc), (short)0, ((p.C + 7) / 8) * Mp32 * 32, 0x00020000);
+      const_cast<float*>(p.wc), (short)0, ((p.C + 15) / 16) * Mp32 * 64, 0x00020000);
   const int chunk_bytes = CG_KC * p.x_ps * 4;
   const int ndma = (chunk_bytes + 1023) / 1024;  // 1 KiB per DMA instruction
   const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) float*)cg_lds;
@@ -62,17 +62,16 @@ __global__ __launch_bounds__(CG_NT, (CG_RT * NF > 22 ? 2 : 3)) void conv1x1_gap_
     }
   };
   // A (v_mfma_f32_16x16x4f32: lane (lc, kq) holds row lc, k = 4 s + kq of k-step s): row tile r is rows
-  // m0 + 16 r .. + 15.  In the pack [k/8][row][h][t] = W[row][8 q + 2 t + h] the k-steps 2 q, 2 q + 1
-  // of lane kq are entries (q, row, kq & 1, (kq >> 1) + 2 u), u = 0, 1: one 16-B load per lane and row
-  // tile covers two k-steps
+  // m0 + 16 r .. + 15.  The pack [k/16][row][kq][s] = W[row][16 q + 4 s + kq]: one 16-B load per lane and
+  // row tile holds k-steps 4 q .. 4 q + 3 of the lane's kq, element s for k-step 4 q + s
   int arow[CG_RT];
 #pragma unroll
   for (int r = 0; r < CG_RT; ++r) arow[r] = m0 + 16 * r + lc < Mp32 ? m0 + 16 * r + lc : 0;
   auto load_a = [&](int q, int r) __attribute__((always_inline)) {
-    return __builtin_bit_cast(cg4, __builtin_amdgcn_raw_buffer_load_b128(wr, ((arow[r] * 2 + (kq & 1)) * 4) * 4,
-                                                                          q * Mp32 * 32, 0));
+    return __builtin_bit_cast(cg4, __builtin_amdgcn_raw_buffer_load_b128(wr, ((arow[r] * 4 + kq) * 4) * 4,
+                                                                          q * Mp32 * 64, 0));
   };
-  const int nq = (p.C + 7) / 8;
+  const int nq = (p.C + 15) / 16;
   cg4 acc[CG_RT][NF];
 #pragma unroll
   for (int r = 0; r < CG_RT; ++r)
@@ -81,7 +80,6 @@ __global__ __launch_bounds__(CG_NT, (CG_RT * NF > 22 ? 2 : 3)) void conv1x1_gap_
   const int nch = p.C / CG_KC;
   const int bo = (kq * p.x_ps + lc) * 4;  // B: channel 4 j + kq, pixel 16 f + lc of the stage (bytes)
   const char* lb = reinterpret_cast<const char*>(cg_lds);
-  const bool hi = (kq >> 1) != 0;
   stage(0, 0);
   cg4 a[2][CG_RT];  // [group parity][row tile]
 #pragma unroll
@@ -100,18 +98,18 @@ __global__ __launch_bounds__(CG_NT, (CG_RT * NF > 22 ? 2 : 3)) void conv1x1_gap_
     for (int f = 0; f < NF; ++f) b[f] = *reinterpret_cast<const float*>(sb + f * 64);
 #pragma unroll
     for (int j = 0; j < CG_KC / 4; ++j) {
-      const int g = j >> 1, u = j & 1;  // group within the chunk (its parity = the global group's)
+      const int g = j >> 2, u = j & 3;  // group within the chunk (its parity = the global group's)
       float av[CG_RT];
 #pragma unroll
-      for (int r = 0; r < CG_RT; ++r) av[r] = hi ? a[g & 1][r][1 + 2 * u] : a[g & 1][r][2 * u];
+      for (int r = 0; r < CG_RT; ++r) av[r] = a[g & 1][r][u];
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
 #pragma unroll
         for (int r = 0; r < CG_RT; ++r) acc[r][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], b[f], acc[r][f], 0, 0, 0);
         if (j + 1 < CG_KC / 4) b[f] = *reinterpret_cast<const float*>(sb + (4 * (j + 1) * p.x_ps) * 4 + f * 64);
       }
-      if (u == 1) {  // group consumed: refill its slot with the group two ahead
-        const int q2 = ci * (CG_KC / 8) + g + 2;
+      if (u == 3) {  // group consumed: refill its slot with the group two ahead
+        const int q2 = ci * (CG_KC / 16) + g + 2;
         if (q2 < nq) {
 #pragma unroll
           for (int r = 0; r < CG_RT; ++r) a[g & 1][r] = load_a(q2, r);
@@ -200,6 +198,29 @@ static void cg_dispatch(const Conv1x1GapF32& p, hipStream_t s) {
 }
 
 }  // namespace
+
+namespace {
+__global__ __launch_bounds__(256) void pack_cg_f32_kernel(const float* __restrict__ w, int M, int K, int Mp32,
+                                                          float* __restrict__ out) {
+  const long long total = (long long)((K + 15) / 16) * Mp32 * 16;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int s = (int)(i & 3), kq = (int)((i >> 2) & 3);
+    const long long rq = i >> 4;
+    const int row = (int)(rq % Mp32), q = (int)(rq / Mp32);
+    const int k = 16 * q + 4 * s + kq;
+    out[i] = (row < M && k < K) ? w[(long long)row * K + k] : 0.0f;
+  }
+}
+}  // namespace
+
+size_t cg_f32_pack_bytes(int M, int K) { return size_t((K + 15) / 16) * size_t((M + 31) / 32 * 32) * 64; }
+
+void launch_pack_cg_f32(const float* w, int M, int K, float* out, hipStream_t s) {
+  const int Mp32 = (M + 31) / 32 * 32;
+  long long blocks = ((long long)((K + 15) / 16) * Mp32 * 16 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pack_cg_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, w, M, K, Mp32, out);
+}
 
 bool conv1x1_gap_f32_eligible(const Conv1x1GapF32& p) {
   return p.x && p.wc && p.y && p.N >= 1 && p.C >= CG_KC && p.C % CG_KC == 0 && p.P >= 1 && p.P <= 256 &&

@@ -42,7 +42,9 @@ typedef float wg_floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16_t __attribute__((ext_vector_type(16)));
 typedef float wg_f2 __attribute__((ext_vector_type(2)));
 
-// U[((c * 4 + xi / 4) * Mp + m) * 4 + xi % 4] = (G g_mc G^T)[xi / 4][xi % 4] (f64, rounded once): for a
+// U[((c * 4 + xi / 4) * Mp + m) * 4 + xi % 4] = s_xi (G g_mc G^T)[xi / 4][xi % 4] (f64, rounded once; the
+// sign s_xi = -1 for xi % 4 == 3, +1 otherwise, and V is stored with the same signs, so every product
+// U_xi V_xi is the unsigned one exactly; the packed input transform needs it, wg_input_transform_pk): for a
 // fixed (channel, position quad) the channels' 16-B quads are contiguous, so the A loads of a wave
 // (one quad per lane, consecutive channels in consecutive lanes) are 512-B runs;
 // G = [[1, 0, 0], [1/2, 1/2, 1/2], [1/2, -1/2, 1/2], [0, 0, 1]]; rows m >= M are zero
@@ -64,6 +66,7 @@ __global__ __launch_bounds__(256) void wino_pack_kernel(const float* __restrict_
       for (int p = 0; p < 3; ++p)
         for (int q = 0; q < 3; ++q) s += G[a][p] * (double)g[p * 3 + q] * G[b][q];
       v = (float)s;
+      if ((i & 3) == 3) v = -v;  // positions 4 i + 3 carry the sign (V likewise, wg_input_transform)
     }
     u[i] = v;
   }
@@ -78,7 +81,7 @@ void launch_pack_wino(const float* w, int M, int C, int Mp, float* u, hipStream_
 }
 
 // V = B^T d B of a 4x4 window (rows i, columns j), B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]];
-// v[4 i + j]
+// v[4 i + j] = s_(4 i + j) V[i][j] (the packing's signs: column 3 negated)
 __device__ __forceinline__ void wg_input_transform(const float (&d)[4][4], float (&v)[16]) {
   float t[4][4];
 #pragma unroll
@@ -93,13 +96,52 @@ __device__ __forceinline__ void wg_input_transform(const float (&d)[4][4], float
     v[4 * i + 0] = t[i][0] - t[i][2];
     v[4 * i + 1] = t[i][1] + t[i][2];
     v[4 * i + 2] = t[i][2] - t[i][1];
-    v[4 * i + 3] = t[i][1] - t[i][3];
+    v[4 * i + 3] = t[i][3] - t[i][1];  // -(t1 - t3), exactly
+  }
+}
+
+// wg_input_transform on packed f32 (v_pk_add_f32 / v_pk_fma_f32: two lanes' worth of adds per VALU
+// instruction; the same adds on the same operands, so bit-identical): d[i][h] = (d[i][2h], d[i][2h + 1]),
+// v[2 i + h] = (v[4 i + 2h], v[4 i + 2h + 1]).  The row pass pairs two columns.  The column pass takes
+// (t0 - t2, t1 + t2) = t2 * (-1, 1) + (t0, t1) (a product by +-1 is exact, one rounding: the sum) and,
+// thanks to the negated position 3, (t2 - t1, t3 - t1) = (t2, t3) - t1: two instructions per row.
+// (Inline-asm packed adds with op_sel would do the same, but the compiler's hazard recognizer does not
+// see inline asm as VALU, and MFMA operands read beside them came out wrong on gfx950.)
+__device__ __forceinline__ void wg_input_transform_pk(const wg_f2 (&d)[4][2], wg_f2 (&v)[8]) {
+  wg_f2 tr[4][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    tr[0][h] = d[0][h] - d[2][h];
+    tr[1][h] = d[1][h] + d[2][h];
+    tr[2][h] = d[2][h] - d[1][h];
+    tr[3][h] = d[1][h] - d[3][h];
+  }
+  const wg_f2 pm = {-1.0f, 1.0f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const wg_f2 a = tr[i][0], b = tr[i][1];  // (t0, t1), (t2, t3)
+    v[2 * i] = __builtin_elementwise_fma(__builtin_shufflevector(b, b, 0, 0), pm, a);
+    v[2 * i + 1] = b - __builtin_shufflevector(a, a, 1, 1);
   }
 }
 
 // Y = A^T M A, A^T = [[1,1,1,0],[0,1,-1,-1]]: y[2 i + j] (i = row, j = column of the 2x2 tile)
 __device__ __forceinline__ void wg_output_transform(const float (&mx)[16], float (&y)[4]) {
   float t0[4], t1[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    t0[j] = mx[j] + mx[4 + j] + mx[8 + j];
+    t1[j] = mx[4 + j] - mx[8 + j] - mx[12 + j];
+  }
+  y[0] = t0[0] + t0[1] + t0[2];
+  y[1] = t0[1] - t0[2] - t0[3];
+  y[2] = t1[0] + t1[1] + t1[2];
+  y[3] = t1[1] - t1[2] - t1[3];
+}
+
+// wg_output_transform of two (channel, tile) pairs at once (packed f32, the same adds in the same order)
+__device__ __forceinline__ void wg_output_transform_pk(const wg_f2 (&mx)[16], wg_f2 (&y)[4]) {
+  wg_f2 t0[4], t1[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     t0[j] = mx[j] + mx[4 + j] + mx[8 + j];
@@ -599,33 +641,33 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   const wg_floatx4 zero4 = {0.f, 0.f, 0.f, 0.f};
 
   const char* lds_b = reinterpret_cast<const char*>(wm_lds);
-  auto load_win = [&](int sto, float (&d)[4][4]) __attribute__((always_inline)) {
+  auto load_win = [&](int sto, wg_f2 (&d)[4][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        d[r][j] = *reinterpret_cast<const float*>(lds_b + aw[r] + sto + 4 * j);
+        d[r][j >> 1][j & 1] = *reinterpret_cast<const float*>(lds_b + aw[r] + sto + 4 * j);
   };
   auto load_u = [&](int sto, int f, int q) __attribute__((always_inline)) {
     return *reinterpret_cast<const wg_floatx4*>(lds_b + au + sto + q * 512 + f * 256);  // m = 16 f + lj
   };
-  auto xform = [&](float (&d)[4][4], float (&v)[16]) __attribute__((always_inline)) {
+  auto xform = [&](wg_f2 (&d)[4][2], wg_f2 (&v)[8]) __attribute__((always_inline)) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      d[r][0] = c0ok ? d[r][0] : 0.0f;
-      d[r][2] = c2ok ? d[r][2] : 0.0f;
-      d[r][3] = c3ok ? d[r][3] : 0.0f;
+      d[r][0][0] = c0ok ? d[r][0][0] : 0.0f;
+      d[r][1][0] = c2ok ? d[r][1][0] : 0.0f;
+      d[r][1][1] = c3ok ? d[r][1][1] : 0.0f;
     }
-    wg_input_transform(d, v);
+    wg_input_transform_pk(d, v);
   };
   // one chunk (two k-steps of 4 channels); FIRST: chunk 0, its first k-step starts the accumulators
-  auto chunk = [&](int kc, auto first) __attribute__((always_inline)) {
+  auto chunk = [&](int kc, auto first, auto stc) __attribute__((always_inline)) {
     constexpr bool FIRST = decltype(first)::value;
-    const int st = kc & 1;
+    constexpr int st = decltype(stc)::value;  // kc & 1, a constant: the stage's LDS bases are loop-invariant
     if (kc + 1 < nchunks) stage(kc + 1, st ^ 1);
     const int sto0 = st * SS * 4, sto1 = sto0 + 4 * g.CS * 4;  // k-step 1: channels 4 .. 7 of the chunk
     wg_floatx4 ua[2][4];
-    float d0[4][4], d1[4][4], v[16];
+    wg_f2 d0[4][2], d1[4][2], v[8];  // v[2 i + h][e]: position 4 i + 2 h + e
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -642,7 +684,7 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
 #pragma unroll
         for (int f = 0; f < 2; ++f)
           acc[4 * q + j][f] =
-              __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][q][j], v[4 * q + j], FIRST ? zero4 : acc[4 * q + j][f], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][q][j], v[2 * q + (j >> 1)][j & 1], FIRST ? zero4 : acc[4 * q + j][f], 0, 0, 0);
 #pragma unroll
       for (int f = 0; f < 2; ++f) ua[f][q] = load_u(sto0 + 4 * 512 * 4, f, q);
     }
@@ -654,7 +696,7 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int f = 0; f < 2; ++f)
-          acc[4 * q + j][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][q][j], v[4 * q + j], acc[4 * q + j][f], 0, 0, 0);
+          acc[4 * q + j][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][q][j], v[2 * q + (j >> 1)][j & 1], acc[4 * q + j][f], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk kc + 1 have landed
     __syncthreads();  // ... every wave's, and every wave is done reading stage kc & 1
@@ -666,8 +708,15 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
 #ifdef ORE_STAMPS
   if (wave == 0) ore_stamp(ore_wino_stamps, blockIdx.x * 8LL + 1);
 #endif
-  chunk(0, std::true_type{});
-  for (int kc = 1; kc < nchunks; ++kc) chunk(kc, std::false_type{});
+  using st0 = std::integral_constant<int, 0>;
+  using st1 = std::integral_constant<int, 1>;
+  chunk(0, std::true_type{}, st0{});
+  int kc = 1;
+  for (; kc + 1 < nchunks; kc += 2) {  // chunk pairs: odd, even
+    chunk(kc, std::false_type{}, st1{});
+    chunk(kc + 1, std::false_type{}, st0{});
+  }
+  if (kc < nchunks) chunk(kc, std::false_type{}, st1{});
 #ifdef ORE_STAMPS
   if (wave == 0) ore_stamp(ore_wino_stamps, blockIdx.x * 8LL + 2);
 #endif
@@ -680,16 +729,30 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
       const int m = m0 + 16 * f + 4 * lk + e;
       bv[f][e] = p.bias && m < p.M ? p.bias[m] : 0.0f;
     }
+  // the output transform and bias of channels (e, e + 1) on packed f32 (acc[xi][f] holds e = 0 .. 3 in
+  // consecutive registers); the same adds in the same order as wg_store_t
 #pragma unroll
   for (int f = 0; f < 2; ++f)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int m = m0 + 16 * f + 4 * lk + e;
-      if (m >= p.M) continue;
-      float mx[16];
+    for (int ep = 0; ep < 4; ep += 2) {
+      const int mp = m0 + 16 * f + 4 * lk + ep;
+      if (mp >= p.M) continue;
+      wg_f2 mx[16], y[4];
 #pragma unroll
-      for (int xi = 0; xi < 16; ++xi) mx[xi] = acc[xi][f][e];
-      wg_store_t<RELU>(p, w, m, bv[f][e], mx);
+      for (int xi = 0; xi < 16; ++xi) mx[xi] = ep == 0 ? acc[xi][f].xy : acc[xi][f].zw;
+      wg_output_transform_pk(mx, y);
+      const wg_f2 b2 = {bv[f][ep], bv[f][ep + 1]};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (mp + h >= p.M) continue;
+        float o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          o[q] = (y[q] + b2)[h];
+          if constexpr (RELU) o[q] = fmaxf(o[q], 0.0f);
+        }
+        wg_store_px(p, w, p.y, mp + h, o);
+      }
     }
 #ifdef ORE_STAMPS
   if (wave == 0) ore_stamp(ore_wino_stamps, blockIdx.x * 8LL + 3);

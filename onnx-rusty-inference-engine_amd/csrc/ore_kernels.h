@@ -293,7 +293,7 @@ struct Conv1x1GapF16 {
 bool conv1x1_gap_f16_eligible(const Conv1x1GapF16& p);
 void launch_conv1x1_gap_f16(const Conv1x1GapF16& p, hipStream_t s);
 // f32 models: the same fusion (conv1x1_gap_f32_kernel, ore_conv_gap.hip): x f32 NCHW [N][C][x_ps] (P <= 256
-// pixels per plane), wc the weights in launch_pack_c1_f32's layout, y f32 [N][M] (image stride y_nstride)
+// pixels per plane), wc the weights in launch_pack_cg_f32's layout, y f32 [N][M] (image stride y_nstride)
 struct Conv1x1GapF32 {
   const float* x;
   const float* wc;
@@ -303,6 +303,9 @@ struct Conv1x1GapF32 {
   long long x_nstride, y_nstride;
 };
 bool conv1x1_gap_f32_eligible(const Conv1x1GapF32& p);
+// conv1x1_gap_f32_kernel's weights: [ceil(K/16)][Mp32][4 kq][4 s] = W[row][16 q + 4 s + kq] (zeros past M, K)
+size_t cg_f32_pack_bytes(int M, int K);
+void launch_pack_cg_f32(const float* w, int M, int K, float* out, hipStream_t s);
 void launch_conv1x1_gap_f32(const Conv1x1GapF32& p, hipStream_t s);
 // Concat along channels of two dense NHWC f16 values (pixels = N*H*W)
 void launch_concat_nhwc(const void* a, const void* b, void* y, long long pixels, int Ca, int Cb, hipStream_t s);

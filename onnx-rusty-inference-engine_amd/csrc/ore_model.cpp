@@ -1054,16 +1054,16 @@ struct Planner {
       Step& g = st(int(i));
       if (g.kind != S_GAP) continue;
       const int v = g.in0;
-      if (!m->f16) {  // f32: conv1x1_gap_f32_kernel (the conv's weights in launch_pack_c1_f32's layout)
+      if (!m->f16) {  // f32: conv1x1_gap_f32_kernel (the conv's weights in launch_pack_cg_f32's layout)
         if (v < 0 || !private_value(v) || val(v).es != 4 || val(v).nhwc || producer[v] < 0) continue;
         Step& cv = st(producer[v]);
         if (cv.kind != S_CONV || cv.out != v || cv.plan.f16 || cv.plan.wino || cv.epool || cv.pool || cv.c1sq ||
             cv.kh != 1 || cv.kw != 1 || cv.sh != 1 || cv.sw != 1 || cv.win.pt != 0 || cv.win.pl != 0 ||
             cv.win.Ho != cv.H || cv.win.Wo != cv.W || cv.C % 32 != 0 || cv.H * cv.W > 256 || val(cv.in0).es != 4)
           continue;
-        const int key = 4000000 + producer[v], M = int(cv.M), K = int(cv.C);
+        const int key = 4100000 + producer[v], M = int(cv.M), K = int(cv.C);
         const float* w = val(cv.in1).cptr;
-        if (!pack_once(key, c1_f32_pack_bytes(M, K), [&](float* buf) { launch_pack_c1_f32(w, M, K, buf, m->ctx->stream); }))
+        if (!pack_once(key, cg_f32_pack_bytes(M, K), [&](float* buf) { launch_pack_cg_f32(w, M, K, buf, m->ctx->stream); }))
           return err(m, ORE_ERR_HIP, "conv + GAP weight packing failed");
         cv.wc1 = m->fire_packs[key];
         cv.gap = true;
