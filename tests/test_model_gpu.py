@@ -392,6 +392,39 @@ def test_conv_pool_walk_bit_identical(gpu_ctx, case):
     np.testing.assert_allclose(vals[0], ref, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("H", [40, 79])
+@pytest.mark.parametrize("relu", [False, True])
+def test_conv_pool_window_variants(gpu_ctx, H, relu):
+    """The window kernel's compile-time forms (round 4): Relu or not (Relu and the zero outside the conv
+    plane as one v_med3_f32, else a select), and IN -- every tile's input window inside the image, loads
+    at a scalar tile origin -- (H = 79: 18 x 18 pooled = 3 x 2 whole tiles, the last window ending on the
+    last row / column) or per-element bounds (H = 40).  Bit for bit the patch-epilogue kernel's output,
+    and the oracle within the conv tolerance."""
+    import ore
+    C, M, k = 3, 96, 7
+    rng = np.random.default_rng(H + relu)
+    w = (rng.standard_normal((M, C, k, k)) * 0.3).astype(np.float32)
+    b = rng.uniform(-0.5, 0.5, M).astype(np.float32)
+    x = rng.standard_normal((3, C, H, H)).astype(np.float32)
+    mb = _conv_pool_model((1, C, H, H), w, b, [0] * 4, [2, 2], relu, [3, 3], [2, 2], [0, 0, 0, 0])
+    names = ore.Model.TILE_NAMES
+    vals = []
+    for tile in (EPOOL_PATCH, EPOOL_WINDOW):
+        m = _model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion(ore.FUSE_ALL | ore.FUSE_EAGER | ore.KEEP_VALUES)
+        forced = force_tiles(m, tile)
+        _np(m.run(_t(x)))
+        vals.append(m.read_value("p"))
+        if tile == EPOOL_WINDOW:
+            assert forced == 1 and [names[t] for t in m.tiles() if t >= 0] == ["epool window f32"]
+        m.close()
+    np.testing.assert_array_equal(vals[0], vals[1])
+    import oracle
+    c = oracle.conv2d(x, w, b, pads=[0] * 4, strides=(2, 2))
+    ref = oracle.maxpool2d(oracle.relu(c) if relu else c, (3, 3), (2, 2), auto_pad="NOTSET", pads=[0, 0, 0, 0])
+    np.testing.assert_allclose(vals[1], ref, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("case", [
     # C, H, M, k, conv pad, pool pads: stride-1 convs + Relu + 3x3 / stride-2 pool (operand modes 1x1 / 3x3)
     (32, 54, 128, 1, 0, [0, 0, 1, 1]),   # fire4 expand1x1 -> pool3 (ceil-mode bottom / right pad)
