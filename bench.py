@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="N > 1 collective: nccl = RCCL all_gather of the device rows (the product path); gloo = the "
                          "rows staged through host memory (exercises the N > 1 branch with several ranks on one GPU)")
+    ap.add_argument("--dist", action="store_true",
+                    help="take the N > 1 path (process group, per-step all-gather, max over ranks) even at N = 1: a "
+                         "one-rank RCCL communicator runs the product collective on a one-GPU box")
     ap.add_argument("--no-step-timing", action="store_true",
                     help="skip the per-kernel HIP-event pass (no roofline / breakdown)")
     ap.add_argument("--layers", action="store_true", help="print per-kernel-step times to stderr")
@@ -191,6 +194,17 @@ def cpu_baseline(model_bytes, hw, threads):
                       f"{float(np.median(done)):.2f} s"}
 
 
+def fixture_images(hw):
+    """The 16 images of the strict-parity fixture (zoo image + 15 U(-50, 50) draws) at 224; else none."""
+    import numpy as np
+    from ore import onnx_wire, squeezenet
+    if hw != 224:
+        return np.zeros((16, 3, hw, hw), dtype=np.float32)
+    # = tests/golden/make_golden.py squeezenet_inputs_calib16()
+    zoo = onnx_wire.load_tensor(os.path.join(REPO, "tests", "golden", "squeezenet_data_0.pb")).to_numpy()
+    return np.concatenate([zoo, squeezenet.synthetic_input(15, 224, seed=31)]).astype(np.float32)
+
+
 def b1_latency(model_bytes, hw, local, precision, winograd=True, iters=200):
     """Batch-1 latency (SURVEY.md §8(d) B = 1 config): one image per synchronous call, issued
     as plain launches, as one HIP-graph replay, and as a graph with the fire modules' expand
@@ -224,7 +238,7 @@ def b1_latency(model_bytes, hw, local, precision, winograd=True, iters=200):
     return res
 
 
-def f16_line(ctx, model_bytes, x, B, args, ref):
+def f16_line(ctx, model_bytes, x, B, args, ref, pos):
     """Config 5 (SqueezeNet-1.0 fp16: f16 activations / weights, f32 accumulate) on the same input
     batch, measured like the headline: autotune, warmup, K timed steps, then a HIP-event pass for
     the conv class's TF/s against the 2.5 PF/s f16 peak; max-abs and top-1 against the f32 oracle
@@ -257,7 +271,7 @@ def f16_line(ctx, model_bytes, x, B, args, ref):
     achieved = conv_fl / (conv_ms * 1e-3) / 1e12
     r8d, _ = roofline_8d(infos, per, 1000.0 * elapsed / args.steps, PEAK_F16_MFMA_TFLOPS,
                          ach_tflops=ACHIEVABLE["f16_mfma_TFLOP/s"])
-    y = out[:ref.shape[0]].cpu().numpy()  # the first rows of x, whose oracle rows are ref
+    y = out[pos].cpu().numpy()  # the fixture images' rows (N = 1: x is the whole global batch)
     res = {"value": round(B * args.steps / elapsed, 2), "unit": "images/s",
            "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "dtype": "f16",
            "conv_TFLOP/s": round(achieved, 2), "roofline_frac": round(achieved / PEAK_F16_MFMA_TFLOPS, 4),
@@ -284,14 +298,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    gloo = world > 1 and args.dist_backend == "gloo"
+    use_dist = world > 1 or args.dist  # the process group and the per-step all-gather
+    gloo = use_dist and args.dist_backend == "gloo"
     # gloo: ranks may share a GPU (the N > 1 branch rehearsed on a one-GPU box); nccl: one GPU per rank
     dev = local % max(1, torch.cuda.device_count()) if gloo else local
     torch.cuda.set_device(dev)
     # one non-default stream for everything (the model's launches, RCCL, torch ops): HIP-graph
     # capture needs a capturable stream
     torch.cuda.set_stream(torch.cuda.Stream(device=dev))
-    if world > 1:
+    if use_dist:
         if gloo:
             dist.init_process_group("gloo")
         else:
@@ -306,22 +321,30 @@ def main():
         raise SystemExit(f"--global-batch {G} does not split evenly over {world} GPUs")
     lo, hi = parallel.shard_bounds(G, world, rank)
     B = hi - lo
-    model_bytes = squeezenet.build(args.hw)
+    # the zoo-calibrated synthetic SqueezeNet (conv10 x ZOO_LOGIT_GAIN: the zoo image's softmax peaks at
+    # 0.074 like squeezenet_output_0.pb), so the max-abs sample below sits well above the f32 noise floor
+    model_bytes = squeezenet.build_calibrated(args.hw)
     ctx = ore.Context(dev)
     model = ore.Model(ctx, model_bytes, max_batch=B, precision=args.precision, winograd=not args.no_winograd)
     f16 = args.precision == "f16"
     g = torch.Generator(device=f"cuda:{dev}")
     g.manual_seed(1000)
     xg = torch.rand((G, 3, args.hw, args.hw), generator=g, device=f"cuda:{dev}") * 100.0 - 50.0
+    # the max-abs sample: the strict-parity fixture images (tests/golden/make_golden.py calib16: the zoo
+    # image squeezenet_data_0.pb + 15 U(-50, 50) draws) placed at evenly spread positions of the global
+    # batch, so the check covers every rank's gathered rows; other sizes: the seeded images at those positions
+    x_sample = fixture_images(args.hw)
+    sample_idx = sorted({int(round(i * (G - 1) / max(1, min(G, len(x_sample)) - 1))) for i in range(min(G, len(x_sample)))})
+    x_sample = x_sample[:len(sample_idx)]
+    if args.hw == 224:
+        xg[sample_idx] = torch.from_numpy(x_sample).to(xg.device)
+    else:
+        x_sample = xg[sample_idx].cpu().numpy()
     x = xg[lo:hi].contiguous()
-    # the max-abs sample: the first image of rank 0's slice and the last of the last rank's, so the
-    # check covers the gathered rows of both ends of the global batch
-    sample_idx = [0, G - 1]
-    x_sample = xg[sample_idx].cpu().numpy() if rank == 0 else None
     del xg
     torch.cuda.empty_cache()
     out = torch.empty((B, model.output_elems), dtype=torch.float32, device=f"cuda:{dev}")
-    if world == 1:
+    if not use_dist:
         gathered = out
     elif gloo:  # the rows staged through host memory for the gloo all-gather
         out_host = torch.empty((B, model.output_elems), dtype=torch.float32)
@@ -351,7 +374,7 @@ def main():
             model.replay()
         else:
             model.run_into(x, out)
-        if world > 1:
+        if use_dist:
             if gloo:
                 out_host.copy_(out)
                 parallel.gather_rows_into(gathered, out_host)
@@ -363,17 +386,17 @@ def main():
     torch.cuda.synchronize()
 
     # the timed region: K steps back to back, nothing else on the stream
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:  # the max over ranks
+    if use_dist:  # the max over ranks
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else f"cuda:{dev}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -403,14 +426,16 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f16" if f16 else "f32",
-            "data": "synthetic (seeded U(-50,50) 3x224x224 images; seeded He-normal SqueezeNet-1.0 weights)",
+            "data": "synthetic (seeded U(-50,50) 3x224x224 images with the 16 parity-fixture images inside; seeded "
+                    "He-normal SqueezeNet-1.0 weights, conv10 scaled by ZOO_LOGIT_GAIN = "
+                    f"{squeezenet.ZOO_LOGIT_GAIN} so the zoo image's softmax peaks at 0.074 as with the real weights)",
             "config": {"workload": f"SqueezeNet-1.0 (66 nodes, 818.9 MMAC/img) "
                                    f"{'fp16 (config 5: f16 activations/weights, f32 accumulate)' if f16 else 'fp32'} "
                                    f"inference, batch {B} per GPU, 3x{args.hw}x{args.hw}",
                        "model": "squeezenet1.0-8 topology, synthetic weights", "global_batch": G,
                        "per_gpu_batch": B, "run_batch": model.run_batch, "seq_len": None, "parallelism": f"dp{world}",
                        "collective": (f"{'gloo (host-staged)' if gloo else 'RCCL'} all_gather of [{B},1000] logits per step"
-                                      if world > 1 else None),
+                                      if use_dist else None),
                        "launch": "one HIP-graph replay per step" if use_graph else "plain launches",
                        "streams": args.streams},
         }
@@ -432,33 +457,53 @@ def main():
                      "16x16x4 f32), conv_stream_kernel / conv_stream1x1_persist_kernel (LDS-free implicit GEMM, "
                      "MFMA 16x16x4 f32), pool_conv1x1_f32_kernel (pool3 / pool5 + the next squeeze) and "
                      "conv_gemm_kernel (LDS-staged, MFMA 32x32x2 f32) per the autotuned tile") + f", {conv['launches']} launches/step)"
-            # HBM bytes per conv launch from the PMC passes of tools/pmc.sh (FETCH_SIZE x2 +
-            # WRITE_SIZE, separate --pmc runs; counters cannot be read inside this timed run)
-            traffic, tsrc, tsame = None, None, None
+            # HBM bytes per launch from the PMC passes of tools/pmc.sh (FETCH_SIZE x2 + WRITE_SIZE, separate
+            # --pmc runs; counters cannot be read inside this timed run), per step and for the conv class
+            tj, tsrc, tsame = None, None, None
             tfile = os.path.join(REPO, "profiles", f"pmc_traffic_{args.precision}.json")
             if os.path.exists(tfile):
                 with open(tfile) as f:
                     tj = json.load(f)
-                traffic = round(tj["hbm_bytes_per_launch"])
                 tsame = tj.get("lib_sha256") == lib_sha256()
                 tsrc = (f"profiles/pmc_traffic_{args.precision}.json: PMC FETCH_SIZE/WRITE_SIZE passes "
                         f"({tj.get('source', 'tools/pmc.sh')}, commit {tj.get('commit', '?')}); "
                         f"{'the same libore.so build as this run' if tsame else 'an earlier libore.so build'}")
+            # the dominant kernel: the launch with the largest share of the step (one kernel per launch)
+            di = int(np.argmax(per_step_ms))
+            dinfo, dms = infos[di], float(per_step_ms[di])
+            tiles = model.tiles()
+            dtile = ore.Model.TILE_NAMES[tiles[di]] if di < len(tiles) and tiles[di] >= 0 else None
+            d_issued = dinfo.get("mfma_flops", dinfo["flops"])
+            d_traffic = None
+            if tj and tj.get("per_step") and len(tj["per_step"]) == len(infos) and tj["per_step"][di]["name"] == dinfo["name"]:
+                d_traffic = round(tj["per_step"][di]["hbm_bytes"])
+            d_bound_hbm = dinfo["bytes"] / (PEAK_HBM_GBS * 1e9) > d_issued / (peak * 1e12)
             result["roofline"] = {
-                "bound": "mfma", "kernel": kname,
-                "achieved": round(issued, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(issued / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-                "traffic_source": tsrc, "traffic_same_build": tsame,
-                "achieved_is": "MFMA work the conv launches issue / their measured time (direct convs: 2*Cout*Ho*Wo*Cin*kh*kw; "
-                               "Winograd F(2x2,3x3) expand3x3: 16*C*M per 2x2 output tile)",
-                "effective_TFLOP/s": round(effective, 2), "effective_frac": round(effective / peak, 4),
-                "effective_is": "algorithmic direct-conv FLOPs (1.638 GFLOP/img) / the same time: credits Winograd "
-                                "layers with 2.25x the work they issue",
-                "achievable_peak": ach, "achievable_frac": round(issued / ach, 4),
-                "algorithmic_bytes_per_launch": round(conv["bytes"] / max(conv["launches"], 1)),
-                "per_launch_avg_us": round(1000.0 * conv["ms"] / conv["launches"], 2),
-                "kernel_timing": f"HIP events between consecutive launches on the model stream (one stream), a second pass of "
-                                 f"the {args.steps} timed steps (events kept out of the value's timed loop)"}
+                "bound": "hbm" if d_bound_hbm else "mfma",
+                "kernel": f"step '{dinfo['name']}' ({dinfo['op']}), tile '{dtile}': the longest launch of the step "
+                          f"({100.0 * dms / float(per_step_ms.sum()):.1f} % of the kernel time)",
+                "achieved": round((dinfo["bytes"] / (dms * 1e-3) / 1e9) if d_bound_hbm else (d_issued / (dms * 1e-3) / 1e12), 2),
+                "peak": PEAK_HBM_GBS if d_bound_hbm else peak, "unit": "GB/s" if d_bound_hbm else "TFLOP/s",
+                "frac": round((dinfo["bytes"] / (PEAK_HBM_GBS * 1e9) if d_bound_hbm else d_issued / (peak * 1e12)) / (dms * 1e-3), 4),
+                "traffic": d_traffic, "traffic_unit": "bytes/launch", "traffic_source": tsrc, "traffic_same_build": tsame,
+                "algorithmic_flops_per_launch": d_issued, "algorithmic_bytes_per_launch": dinfo["bytes"],
+                "launch_us": round(1000.0 * dms, 2),
+                "achievable_peak": ach, "achievable_frac": round(d_issued / (ach * 1e12) / (dms * 1e-3), 4),
+                "kernel_timing": f"HIP events between consecutive launches on the model stream, a separate ONE-STREAM pass of "
+                                 f"the {args.steps} timed steps (events kept out of the value's timed loop; the value's loop runs "
+                                 f"{args.streams} stream(s), so per-launch times describe the one-stream schedule)",
+                "conv_class": {
+                    "kernel": kname, "launches": conv["launches"],
+                    "achieved": round(issued, 2), "unit": "TFLOP/s", "peak": peak, "frac": round(issued / peak, 4),
+                    "achieved_is": "MFMA work the conv launches issue / their measured time (direct convs: "
+                                   "2*Cout*Ho*Wo*Cin*kh*kw; Winograd F(2x2,3x3) expand3x3: 16*C*M per 2x2 output tile)",
+                    "effective_TFLOP/s": round(effective, 2), "effective_frac": round(effective / peak, 4),
+                    "effective_is": "algorithmic direct-conv FLOPs (1.638 GFLOP/img) / the same time: credits Winograd "
+                                    "layers with 2.25x the work they issue",
+                    "achievable_frac": round(issued / ach, 4),
+                    "traffic": round(tj["hbm_bytes_per_launch"]) if tj else None,
+                    "algorithmic_bytes_per_launch": round(conv["bytes"] / max(conv["launches"], 1)),
+                    "per_launch_avg_us": round(1000.0 * conv["ms"] / conv["launches"], 2)}}
             result["roofline_8d"] = r8d
             if args.layers:
                 for info, ms in zip(infos, per_step_ms):
@@ -466,23 +511,25 @@ def main():
                     gbs = info["bytes"] / (ms * 1e-3) / 1e9
                     print(f"{info['name']:24s} {info['op']:18s} {1000 * ms:9.1f} us {tf:7.1f} TF/s {gbs:8.1f} GB/s",
                           file=sys.stderr)
-        # max-abs vs the CPU restatement on a bounded sample: global images 0 and G - 1 as they come
-        # out of the timed steps (for N > 1 out of the gathered rows, i.e. through the collective)
+        # max-abs vs the CPU restatement on a bounded sample: the fixture images at their global positions as
+        # they come out of the timed steps (for N > 1 out of the gathered rows, i.e. through the collective)
         import oracle
         torch.cuda.synchronize()
         got = gathered[sample_idx].cpu().numpy()
         ref = oracle.Model(model_bytes).run(x_sample, 1000)
-        result["max_abs_diff_vs_cpu"] = float(np.abs(got - ref).max())
-        result["max_abs_sample"] = (f"global images {sample_idx} of the timed batch"
-                                    f"{' (gathered over ' + ('gloo' if gloo else 'RCCL') + ')' if world > 1 else ''} vs "
-                                    f"the oracle (C restatement of the reference, f32)")
-        if f16:
-            result["top1_agrees_with_cpu"] = bool((got.argmax(1) == ref.argmax(1)).all())
+        per_img = np.abs(got - ref).max(axis=1)
+        result["max_abs_diff_vs_cpu"] = float(per_img.max())
+        result["max_abs_per_image"] = [float(v) for v in per_img]
+        result["top1_agrees_with_cpu"] = bool((got.argmax(1) == ref.argmax(1)).all())
+        result["max_abs_sample"] = (f"{len(sample_idx)} images at global positions {sample_idx} of the timed batch"
+                                    f"{' (gathered over ' + ('gloo' if gloo else 'RCCL') + ')' if use_dist else ''}: "
+                                    f"{'the strict-parity fixture (zoo image + 15 U(-50,50) draws; zoo-calibrated model, softmax max 0.074 on the zoo image)' if args.hw == 224 else 'seeded U(-50,50) images'}"
+                                    f" vs the oracle (C restatement of the reference, f32) run live on this host")
         # the reporting legs run at N = 1 only (the CPU baseline on rank 0 at N = 1), so no
         # rank waits on the others' collectives meanwhile
         if world == 1:
             if not f16 and not args.no_f16_line:
-                result["f16"] = f16_line(ctx, model_bytes, x, B, args, ref[:1])  # global image 0 = x[0]
+                result["f16"] = f16_line(ctx, model_bytes, x, B, args, ref, sample_idx)
             if not args.no_b1:
                 result["b1_latency_ms"] = b1_latency(model_bytes, args.hw, dev, args.precision,
                                                      winograd=not args.no_winograd)
@@ -495,7 +542,7 @@ def main():
 
     model.close()
     ctx.close()
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 

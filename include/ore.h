@@ -277,7 +277,9 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
 /* Measure every Conv step's candidate block tiles (128x128, 96x128, 64x128, 32x256) on a real
  * run of n images (d_input / d_output as for ore_model_run) and keep the fastest per layer (like
  * a benchmark-mode convolution search).  Results do not depend on the tile.  Synchronous.
- * reps: timed launches per candidate (<= 0: 3).  The choice survives ore_model_set_fusion. */
+ * reps: timed launches per candidate (<= 0: 3).  The choice survives ore_model_set_fusion.  A batch
+ * above run_batch is tuned on its first chunk, then run whole once, so on return d_output holds the
+ * output of all n images either way. */
 ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, float* d_output, int32_t reps);
 /* Block tile chosen for exec step i (-1 for non-conv steps); steps with one fixed kernel report its
  * id (e.g. 49 / 50: conv + GlobalAveragePool, f16 / f32). */

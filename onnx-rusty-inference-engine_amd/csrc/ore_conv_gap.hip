@@ -168,9 +168,10 @@ template <int NF, bool DMA>
 static void cg_launch(const Conv1x1GapF32& p, hipStream_t s) {
   const int stg = (CG_KC * p.x_ps + 255) / 256 * 256 + 256;  // floats per stage (+ the last fragment's overrun)
   const size_t lds = (size_t)std::max(2 * stg, CG_NW * CG_EPR * cg_ts(NF)) * 4;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_gap_f32_kernel<NF, DMA>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (lds > 64 * 1024) {  // above the default dynamic-LDS limit: raised once per device
+    static std::atomic<unsigned long long> raised{0};
+    ore_raise_lds_once(raised, reinterpret_cast<const void*>(&conv1x1_gap_f32_kernel<NF, DMA>), 160 * 1024);
+  }
   const long long grid = (long long)p.N * ((p.M + CG_MB - 1) / CG_MB);
   hipLaunchKernelGGL((conv1x1_gap_f32_kernel<NF, DMA>), dim3((unsigned)grid), dim3(CG_NT), lds, s, p, stg);
 }

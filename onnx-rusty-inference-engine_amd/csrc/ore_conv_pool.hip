@@ -417,14 +417,7 @@ static void launch_cp(const ConvParams& p0, size_t lds, int nbands, int nring, h
     // above the default dynamic-LDS limit: raise it once per DEVICE and instantiation (the
     // attribute binds to the current device; one ore_ctx per device may call from its own thread)
     static std::atomic<unsigned long long> raised{0};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const unsigned long long bit = 1ull << (dev & 63);
-    if (!(raised.load(std::memory_order_acquire) & bit)) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pool_stream_kernel<MF, D, NW, MODE>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      raised.fetch_or(bit, std::memory_order_acq_rel);
-    }
+    ore_raise_lds_once(raised, reinterpret_cast<const void*>(&conv_pool_stream_kernel<MF, D, NW, MODE>), 160 * 1024);
   }
   hipLaunchKernelGGL((conv_pool_stream_kernel<MF, D, NW, MODE>), dim3((unsigned)(p.N * nbands * p.mtiles)),
                      dim3(64 * NW), lds, s, p, qrow, nbands, nring);

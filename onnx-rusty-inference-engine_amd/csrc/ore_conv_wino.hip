@@ -491,16 +491,6 @@ __global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
 //     next k-step's U quads are read as the MFMAs that used the current ones issue.
 // Each position is the same c-ordered fma chain and the transforms the same add order as tiles 0-3:
 // bit-identical to them.
-#ifdef ORE_STAMPS
-__device__ unsigned long long ore_wino_stamps[1 << 17];
-extern "C" int ore_debug_stamps_wino(void* dst, size_t bytes) {
-  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ore_wino_stamps), bytes, 0, hipMemcpyDeviceToHost);
-}
-extern "C" int ore_debug_stamps_wino_clear() {
-  static unsigned long long zero[1 << 17];
-  return (int)hipMemcpyToSymbol(HIP_SYMBOL(ore_wino_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
-}
-#endif
 constexpr int WM_KC = 8;      // input channels per K chunk (2 k-steps of 4)
 constexpr int WM_TILES = 64;  // 2x2 tiles per workgroup (16 per wave)
 constexpr int WM_CH = 32;     // output channels per workgroup
@@ -542,12 +532,6 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   extern __shared__ __attribute__((aligned(16))) float wm_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#ifdef ORE_STAMPS
-  if (wave == 0) {
-    ore_stamp(ore_wino_stamps, blockIdx.x * 8LL);
-    ore_stamp_ids(ore_wino_stamps, blockIdx.x * 8LL + 4);
-  }
-#endif
   // block -> (tile group, 32-channel block), the channel blocks of a tile group consecutive (one XCD:
   // they share the staged rows in L2)
   const int nwg = gridDim.x, bid = blockIdx.x;
@@ -705,9 +689,6 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-#ifdef ORE_STAMPS
-  if (wave == 0) ore_stamp(ore_wino_stamps, blockIdx.x * 8LL + 1);
-#endif
   using st0 = std::integral_constant<int, 0>;
   using st1 = std::integral_constant<int, 1>;
   chunk(0, std::true_type{}, st0{});
@@ -717,9 +698,6 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
     chunk(kc + 1, std::false_type{}, st0{});
   }
   if (kc < nchunks) chunk(kc, std::false_type{}, st1{});
-#ifdef ORE_STAMPS
-  if (wave == 0) ore_stamp(ore_wino_stamps, blockIdx.x * 8LL + 2);
-#endif
   // lane (lk, lj) of fragment f holds rows 4 lk + e = channel m0 + 16 f + 4 lk + e of tile lj
   float bv[2][4];
 #pragma unroll
@@ -754,9 +732,6 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
         wg_store_px(p, w, p.y, mp + h, o);
       }
     }
-#ifdef ORE_STAMPS
-  if (wave == 0) ore_stamp(ore_wino_stamps, blockIdx.x * 8LL + 3);
-#endif
 }
 
 // the LDS kernel's geometry; false when the layer does not fit it
@@ -784,14 +759,7 @@ static void launch_wm_r(const ConvParams& p0, const WmGeom& g, size_t lds, hipSt
   p.mtiles = (p.M + WM_CH - 1) / WM_CH;
   if (lds > 64 * 1024) {  // above the default dynamic-LDS limit: raise it once per device
     static std::atomic<unsigned long long> raised{0};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const unsigned long long bit = 1ull << (dev & 63);
-    if (!(raised.load(std::memory_order_acquire) & bit)) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_winol_kernel<NDMA, RELU>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      raised.fetch_or(bit, std::memory_order_acq_rel);
-    }
+    ore_raise_lds_once(raised, reinterpret_cast<const void*>(&conv_winol_kernel<NDMA, RELU>), 160 * 1024);
   }
   hipLaunchKernelGGL((conv_winol_kernel<NDMA, RELU>), dim3((unsigned)(g.ntg * p.mtiles)), dim3(256), lds, s, p, g);
 }

@@ -521,14 +521,7 @@ static void launch_fire_cfg(const FireParams& p0, hipStream_t s) {
   if (p.pool) {
     // 132 KB of LDS: above the default dynamic-LDS limit, raised once per device
     static std::atomic<unsigned long long> raised{0};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const unsigned long long bit = 1ull << (dev & 63);
-    if (!(raised.load(std::memory_order_acquire) & bit)) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fire_pool_kernel<MFS, ORE_FIRE_POOL_D>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, FP_LDS);
-      raised.fetch_or(bit, std::memory_order_acq_rel);
-    }
+    ore_raise_lds_once(raised, reinterpret_cast<const void*>(&fire_pool_kernel<MFS, ORE_FIRE_POOL_D>), FP_LDS);
     const unsigned grid = (unsigned)(p.N * ((p.Hp + p.PR - 1) / p.PR));
     hipLaunchKernelGGL((fire_pool_kernel<MFS, ORE_FIRE_POOL_D>), dim3(grid), dim3(512), FP_LDS, s, p);
     return;

@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 namespace ore {
 
 // XCD-aware bijective workgroup id: the hardware deals block ids round-robin over the 8 XCDs,
@@ -51,21 +53,23 @@ __device__ __forceinline__ ore_h8 ore_f16_epilogue8(const float* a, const float*
 
 #define ORE_BAND_ID() xcd_block_id()
 
+// Raise a kernel's dynamic-LDS limit (hipFuncAttributeMaxDynamicSharedMemorySize) once per device and
+// template instance: the attribute binds to the current device, and one ore_ctx per device may launch
+// from its own thread.  `raised` is the caller's per-instance static bit set (one bit per device).
+inline void ore_raise_lds_once(std::atomic<unsigned long long>& raised, const void* kernel, int bytes) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const unsigned long long bit = 1ull << (dev & 63);
+  if (!(raised.load(std::memory_order_acquire) & bit)) {
+    (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    raised.fetch_or(bit, std::memory_order_acq_rel);
+  }
+}
+
 // 16-B LDS-DMA (buffer_load_dwordx4 ... lds): lane i's 16 bytes from rsrc + voffset + soffset land at
 // LDS byte lds_addr + 16 i (lds_addr, soffset wave-uniform); offsets past the records read 0.  Counted by
 // vmcnt like any buffer load; nothing orders a later ds_read behind it but the issuing wave's vmcnt
 // (and a barrier for the other waves).
-#ifdef ORE_STAMPS  // timing experiments only (tools/stamps.py): per-workgroup s_memtime stamps
-__device__ __forceinline__ void ore_stamp(unsigned long long* buf, long long idx) {
-  if ((threadIdx.x & 63) == 0) buf[idx] = __builtin_amdgcn_s_memtime();
-}
-__device__ __forceinline__ void ore_stamp_ids(unsigned long long* buf, long long idx) {
-  if ((threadIdx.x & 63) == 0) {
-    buf[idx] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-    buf[idx + 1] = __builtin_amdgcn_s_getreg((3 << 11) | 20);
-  }
-}
-#endif
 __device__ __forceinline__ void ore_lds_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, int voffset, int soffset) {
   int m0save;
   asm volatile(
@@ -374,9 +378,11 @@ extern thread_local int last_conv_tile;
 constexpr int CONV_TILES_F16 = 4;
 // 3x3 / stride-1 / pad-1 f32 conv by Winograd F(2x2, 3x3) on the f32 MFMA (ore_conv_wino.hip).  Tiles
 // WINO_TILE_BASE + 0..3 = 32 ch x 32 tiles (32x32x2 MFMA, ring 4 / 2), 32 x 16, 16 x 32 (16x16x4);
-// 4 = the LDS-staged kernel (128 tiles x 32 channels per 4-wave block, windows and U from LDS; C % 8 == 0);
+// 4 = the LDS-staged kernel (64 tiles x 32 channels per 4-wave block, windows and U from LDS; C % 8 == 0);
 // results do not depend on the tile (not bit-identical to the direct kernels).  Weights packed by
-// launch_pack_wino: U = G g G^T as [C][4][Mp][4] f32 (channel, position quad, m, position) (Mp = wino_packed_mp(M)).
+// launch_pack_wino: U = s_xi (G g G^T)[xi] as [C][4][Mp][4] f32 (channel, position quad, m, position)
+// (Mp = wino_packed_mp(M)), with the sign s_xi = -1 for positions xi % 4 == 3 (+1 otherwise): every kernel's
+// V carries the same sign (wg_input_transform / _pk), so each product U_xi V_xi is the unsigned one.
 // tile ids 28-35 are retired (ABI 1's opt-in bf16x3 kernels, ORE_LOAD_X3)
 constexpr int WINO_TILE_BASE = 36;
 constexpr int WINO_TILES_N = 5;

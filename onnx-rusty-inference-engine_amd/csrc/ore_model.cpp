@@ -1966,6 +1966,7 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
   ore_ctx* ctx = m->ctx;
   if (n < 1 || n > m->max_batch) return set_error(ctx, ORE_ERR_INVALID, "batch out of range");
   if (reps < 1) reps = 3;
+  const int64_t n_all = n;
   if (n > m->run_batch) {  // tuned on one chunk of the chunked run (ore_model_run)
     const int64_t nchunks = (n + m->run_batch - 1) / m->run_batch;
     n = (n + nchunks - 1) / nchunks;
@@ -2018,6 +2019,9 @@ ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, flo
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   if (!st && hipStreamSynchronize(ctx->stream) != hipSuccess) st = set_error(ctx, ORE_ERR_HIP, "autotune sync");
+  // tuned on the first chunk only: run the whole batch once so d_output holds every image's output
+  if (!st && n_all > n) st = ore_model_run(m, d_input, n_all, d_output);
+  if (!st && n_all > n && hipStreamSynchronize(ctx->stream) != hipSuccess) st = set_error(ctx, ORE_ERR_HIP, "autotune sync");
   return st;
 }
 

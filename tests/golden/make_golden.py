@@ -7,6 +7,11 @@ restatement of the reference, oracle/).  Run from the repo root:  python tests/g
   squeezenet_synth8_oracle.npz the same model on 8 images: the zoo image + synthetic_input(7, seed 21)
                                (the benched plan's parity margin, tests/test_config4_gpu.py); also
                                squeezenet_synth8_f64.npz, the float64 executor's output (f64_ref.py)
+  squeezenet_calib16_oracle.npz the zoo-calibrated model (ore.squeezenet.build_calibrated(): conv10 x
+                               ZOO_LOGIT_GAIN, zoo-image softmax max 0.074 like squeezenet_output_0.pb)
+                               on 16 images: the zoo image + synthetic_input(15, seed 31); the strict
+                               1e-5 parity set of bench.py's plan (tests/test_config4_gpu.py) and
+                               bench.py's max-abs sample; also squeezenet_calib16_f64.npz (f64_ref.py)
   squeezenet_mini_oracle.npz   the same topology at 64x64 input, 4 seeded images; also every
                                intermediate value of image 0 (for node-level parity)
   mnist_oracle.npz             mnist-8.onnx on mnist_data_0.pb and 3 derived images
@@ -38,6 +43,11 @@ def squeezenet_inputs8():
     return np.concatenate([zoo, squeezenet.synthetic_input(7, 224, seed=21)]).astype(np.float32)
 
 
+def squeezenet_inputs_calib16():
+    zoo = onnx_wire.load_tensor(os.path.join(HERE, "squeezenet_data_0.pb")).to_numpy()
+    return np.concatenate([zoo, squeezenet.synthetic_input(15, 224, seed=31)]).astype(np.float32)
+
+
 def mini_inputs():
     return squeezenet.synthetic_input(4, 64, seed=5)
 
@@ -59,12 +69,27 @@ def synth8():
     np.savez_compressed(os.path.join(HERE, "squeezenet_synth8_f64.npz"), output=y64)
 
 
+def calib16():
+    import f64_ref
+    model = squeezenet.build_calibrated(224)
+    x = squeezenet_inputs_calib16()
+    y = oracle.Model(model).run(x, 1000)
+    np.savez_compressed(os.path.join(HERE, "squeezenet_calib16_oracle.npz"), output=y)
+    y64 = np.concatenate([f64_ref.run(model, x[i:i + 1]) for i in range(x.shape[0])])
+    np.savez_compressed(os.path.join(HERE, "squeezenet_calib16_f64.npz"), output=y64)
+
+
 def main():
     if "--only-synth8" in sys.argv:
         synth8()
         print("wrote synth8 fixtures")
         return
+    if "--only-calib16" in sys.argv:
+        calib16()
+        print("wrote calib16 fixtures")
+        return
     synth8()
+    calib16()
     m = oracle.Model(squeezenet.build(224))
     y = m.run(squeezenet_inputs(), 1000)
     np.savez_compressed(os.path.join(HERE, "squeezenet_synth_oracle.npz"), output=y)

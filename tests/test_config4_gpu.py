@@ -16,6 +16,12 @@ GPUs) and the exact plan bench.py times, on the one GPU of the test box.
                                               probability 0.62-0.95) reaches 8.7e-6 by itself;
     |gpu - f64| <= 1e-5 (Winograd, the default plan) / 2e-5 (winograd=False, the reference's k order
                                               on 9C-long f32 chains); same argmax.
+* the same plan on bench.py's own model, the zoo-calibrated SqueezeNet, on the 16 images of
+  tests/golden/squeezenet_calib16_*.npz (zoo image + 15 U(-50,50) draws): the plain north_star bound
+  max |gpu - oracle| <= 1e-5 per image, same argmax (the oracle is within 1.4e-6 of float64 there, so a
+  ~1e-5 regression cannot hide in rounding).
+* bench.py's collective path at world size 1 (--dist): a one-rank RCCL communicator and the device-tensor
+  all-gather, launched by torch.distributed.run.
 * bench.py's N > 1 branch (global-batch slicing, the per-step all-gather, the max over ranks, the
   gathered max-abs sample) as two processes on this GPU, over gloo (--dist-backend gloo: the rows staged
   through host memory; the RCCL leg needs one GPU per rank).
@@ -59,11 +65,15 @@ def test_config4_per_gpu_batch(gpu_ctx, B):
     x[B - 1] = fx[1]
     out = torch.empty((B, m.output_elems), device="cuda")
     m.set_streams(2)
+    out.fill_(float("nan"))
     m.autotune(x, out)
+    torch.cuda.synchronize()
+    y_tuned = out.cpu().numpy()  # autotune leaves every image's output, chunked batches included
     m.run_into(x, out)
     torch.cuda.synchronize()
     y = out.cpu().numpy()
     assert np.isfinite(y).all()
+    np.testing.assert_array_equal(y_tuned, y)
     np.testing.assert_allclose(y.sum(axis=1), 1.0, atol=1e-4)
     ref = np.load(os.path.join(GOLD, "squeezenet_synth_oracle.npz"))["output"]
     err = float(np.abs(y[[0, B - 1]] - ref).max())
@@ -143,6 +153,65 @@ def test_benched_plan_parity(gpu_ctx, winograd):
         assert r["vs_f64"] <= (1e-5 if winograd else 2e-5), r
     assert np.array_equal(y.argmax(1), ref.argmax(1))
     m.close()
+
+
+@pytest.mark.parametrize("winograd", [True, False])
+def test_benched_plan_parity_calibrated(gpu_ctx, winograd):
+    """The strict north_star bound on bench.py's exact plan and model: the zoo-calibrated SqueezeNet
+    (squeezenet.build_calibrated: the zoo image's softmax peaks at 0.074, like squeezenet_output_0.pb),
+    max_batch 256, autotuned on bench.py's seeded B = 256 batch with the 16 fixture images at bench.py's
+    sample positions, two streams, run twice.  Every image: max |gpu - oracle| <= 1e-5 (no allowance for
+    the oracle's own rounding: on this set the oracle is within 1.4e-6 of float64), same argmax."""
+    import torch
+    import ore
+    from ore import squeezenet
+    from golden.make_golden import squeezenet_inputs_calib16
+    ref = np.load(os.path.join(GOLD, "squeezenet_calib16_oracle.npz"))["output"]
+    ref64 = np.load(os.path.join(GOLD, "squeezenet_calib16_f64.npz"))["output"]
+    assert float(np.abs(ref - ref64).max()) <= 2e-6  # the fixture sits far below the bound
+    B = 256
+    m = ore.Model(gpu_ctx, squeezenet.build_calibrated(224), max_batch=B, winograd=winograd)
+    m.set_streams(2)
+    x = _batch(B, 1000)  # bench.py's seeded batch
+    pos = sorted({int(round(i * (B - 1) / 15)) for i in range(16)})  # bench.py's sample_idx at G = 256
+    assert len(pos) == 16
+    x[pos] = torch.from_numpy(squeezenet_inputs_calib16()).cuda()
+    out = torch.empty((B, m.output_elems), device="cuda")
+    m.autotune(x, out)
+    for _ in range(2):
+        m.run_into(x, out)
+    torch.cuda.synchronize()
+    y = out.cpu().numpy()[pos]
+    rows = _margins(y, ref, ref64)
+    print(json.dumps({"winograd": winograd, "margins": rows}))
+    for r in rows:
+        assert r["vs_oracle"] <= 1e-5, r
+    assert np.array_equal(y.argmax(1), ref.argmax(1))
+    m.close()
+
+
+def test_bench_world1_rccl():
+    """bench.py's collective path at world size 1 on this GPU (--dist): torch.distributed.run with one
+    process, init_process_group("nccl", device_id=...) -- a one-rank RCCL communicator -- and the
+    per-step all_gather_into_tensor of the device rows (ore.parallel.gather_rows_into), the max over
+    ranks, and the max-abs sample taken from the gathered rows."""
+    env = dict(os.environ)
+    env["MASTER_ADDR"] = "127.0.0.1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "1", "--dist", "--dist-backend", "nccl", "--steps", "3", "--warmup", "1", "--batch", "64",
+           "--no-cpu-baseline", "--no-b1", "--no-f16-line", "--no-step-timing"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    print(json.dumps({k: res[k] for k in ("value", "ms_per_step", "max_abs_diff_vs_cpu")} | {"collective": res["config"]["collective"]}))
+    assert res["n_gpus"] == 1 and res["config"]["global_batch"] == 64
+    assert res["config"]["collective"].startswith("RCCL all_gather"), res["config"]
+    assert "gathered over RCCL" in res["max_abs_sample"], res["max_abs_sample"]
+    assert res["max_abs_diff_vs_cpu"] <= 1e-5 and res["top1_agrees_with_cpu"], res["max_abs_per_image"]
+    assert res["value"] > 0
 
 
 def _free_port():

@@ -8,7 +8,8 @@ CSRC="$HERE/../../onnx-rusty-inference-engine_amd/csrc"
 B="$HERE/build"
 mkdir -p "$B"
 SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=all -Xarch_host -fno-omit-frame-pointer"
-HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 -O1 -g -I$CSRC -I$HERE/../../include"
+# debug info on the host side only: device debug info would put ~45 MB into the driver binary
+HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 -O1 -Xarch_host -g -I$CSRC -I$HERE/../../include"
 what="${1:-parse}"
 if [ "$what" = parse ] || [ "$what" = all ]; then
   # host only: the parser has no device code
@@ -18,14 +19,17 @@ if [ "$what" = parse ] || [ "$what" = all ]; then
 fi
 if [ "$what" = model ] || [ "$what" = all ]; then
   objs=()
+  pids=()
+  rm -f "$B"/*.o "$B/model_fuzz"  # never link a stale object of an earlier build
   for src in "$CSRC"/*.hip "$CSRC"/*.cpp; do
     f=$(basename "${src%.*}")
     extra=""
     case "$src" in *ore_fire_f16.hip|*ore_conv_wino.hip) extra="-fno-slp-vectorize";; esac
     $HIPCC -O3 -x hip $SAN $extra -c "$src" -o "$B/$f.o" &
+    pids+=($!)
     objs+=("$B/$f.o")
   done
-  wait
+  for pid in "${pids[@]}"; do wait "$pid"; done  # set -e: a failed compile ends the script
   $HIPCC -O1 -x hip $SAN -c "$HERE/model_fuzz.cpp" -o "$B/model_fuzz.o"
   $HIPCC "${objs[@]}" "$B/model_fuzz.o" -fno-gpu-sanitize -fsanitize=address,undefined -o "$B/model_fuzz"
   echo "$B/model_fuzz"

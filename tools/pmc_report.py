@@ -123,6 +123,11 @@ def main():
                "algorithmic_bytes_per_launch": (sum(st["bytes"] for st in steps if st["op"] == "Conv") / max(len(conv), 1)
                                                 if steps else None),
                "source": base, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, FETCH_SIZE x2 (gfx950)"}
+        if steps:  # per launch, in the plan's step order (bench.py reports the dominant launch's traffic)
+            out["per_step"] = [{"name": st["name"], "op": st["op"], "algorithmic_bytes": st["bytes"],
+                                "hbm_bytes": 2 * r.get("FETCH_SIZE", 0) * 1024 + r.get("WRITE_SIZE", 0) * 1024,
+                                "fetch_bytes": 2 * r.get("FETCH_SIZE", 0) * 1024, "write_bytes": r.get("WRITE_SIZE", 0) * 1024}
+                               for r, st in zip(merged, steps)]
         for key, fn in (("lib_sha256", "lib.sha256"), ("commit", "commit")):  # the build the passes ran (tools/pmc.sh)
             if os.path.exists(os.path.join(base, fn)):
                 out[key] = open(os.path.join(base, fn)).read().strip()

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Phase timing from s_memtime stamps (experiment build only: tools/build_exp.sh stamps "-DORE_STAMPS"
+"""Phase timing from s_memtime stamps (experiment build only: PATCHES=tools/patches/stamps.patch tools/build_exp.sh stamps "-DORE_STAMPS"
 "ore_conv_wino ore_conv1_f32", run with ORE_LIB=lib/exp/libore_stamps.so).  Wave 0 of each workgroup
 stamps kernel entry, the end of its prologue, its K loop(s) and its exit; the hardware ids say which
 CU it ran on.  Prints per-phase medians and how many workgroups overlapped on a CU.
