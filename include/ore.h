@@ -205,7 +205,7 @@ ore_status ore_model_destroy(ore_model* m);
 #define ORE_FUSE_CONV_RELU 1
 #define ORE_FUSE_CONCAT 2
 #define ORE_FUSE_ALIAS 4
-#define ORE_FUSE_ALL 6119
+#define ORE_FUSE_ALL 14311
 /* bit 5 (in ORE_FUSE_ALL): Conv (-> Relu) -> 3x3 / stride-2 MaxPool as ONE launch when the conv
  * output has no other consumer: each block computes a 13 x 19 patch of conv outputs covering a
  * 6 x 9 tile of pooled outputs (the overlapping window row / column is recomputed by the
@@ -249,6 +249,12 @@ ore_status ore_model_destroy(ore_model* m);
  * conv1x1_gap_f16_kernel; f32 models since round 4: conv1x1_gap_f32_kernel, input channels a multiple
  * of 32, <= 256 pixels).  Bit-identical to the separate launches; not under ORE_KEEP_VALUES. */
 #define ORE_FUSE_CONV_GAP 4096
+/* bit 13 (round 5): with ORE_FUSE_POOL_SQUEEZE, a pool whose input is Concat(e1, e3) with e1 a 1x1
+ * conv (+ Relu) of 32 / 64 channels read only by the Concat: e1 is recomputed inside the pooled
+ * squeeze from its own input, so its map is never stored (SqueezeNet fire4 -> pool3 -> fire5 and
+ * fire8 -> pool5 -> fire9 when their expand3x3 runs Winograd).  Bit-identical; f32 models; not
+ * under ORE_KEEP_VALUES. */
+#define ORE_FUSE_POOL_EXPAND 8192
 /* bit 11 (tests, not in ORE_FUSE_ALL): apply every eligible fusion regardless of the size
  * heuristics above (batch / plane thresholds, the 1.25 patch-work bound). */
 #define ORE_FUSE_EAGER 2048

@@ -145,12 +145,21 @@ ore_status run_fire_f16(ore_ctx* ctx, const void* x, int64_t N, int64_t C, int64
 // (the conv columns computed, recomputed overlap and padding included), 0 for other pools
 double epool_tile(int64_t Ho, int64_t Wo, int64_t pkh, int64_t pkw, int64_t psh, int64_t psw, const Window& pwin,
                   int* tr, int* tc);
+// the pooled squeeze's recomputed expand1x1 (walker pass pool_expand): x's first E1 channels are
+// relu(w1 s + b1) of s [C1][pH][pW] (plane stride s_ps, image stride s_nstride), w1 K-major [k][w1_Mp]
+struct PoolExpand {
+  const float* s;
+  const float* w1;
+  const float* b1;
+  int C1, E1, w1_Mp;
+  int64_t s_ps, s_nstride;
+};
 // 1x1 conv over the 3x3 / stride-2 MaxPool (window pwin) of x [C][pH][pW] (plane stride x_ps) on
 // pool_conv1x1_f32_kernel: the pooled tensor is never materialised (walker pass fuse_pool_squeeze)
 ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t pH,
                          int64_t pW, int64_t x_nstride, int64_t x_ps, const Window& pwin, int64_t psh, int64_t psw,
                          const float* wp, int64_t M, const float* bias, bool relu, float* y, int64_t y_nstride,
-                         int64_t y_ps, int x_es);
+                         int64_t y_ps, int x_es, const PoolExpand* pe = nullptr);
 // packs w (and the gather table for an input of H x W) into the context scratch buffer;
 // returns the packed weights (or null with the error set), *ktab receives the table
 float* pack_to_scratch(ore_ctx* ctx, const ConvPlan& pln, const float* w, bool kmajor_src, int64_t M, int64_t C,

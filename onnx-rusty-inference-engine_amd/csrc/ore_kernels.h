@@ -201,6 +201,14 @@ struct PoolConvParams {
   int x_ps, y_ps;
   long long x_nstride, y_nstride;
   int relu;
+  // ORE_FUSE_POOL_EXPAND: the pool input's first E1 channels (a Concat's expand1x1 slice) are not read
+  // from x but recomputed from that conv's own input s (C1 = 32 / 64 channels on the pool input's
+  // plane): relu(w1 s + b1) with w1 the conv's K-major packing [k][w1_Mp].  E1 = 0: all from x.
+  const float* s;
+  const float* w1;
+  const float* b1;
+  int C1, E1, w1_Mp, s_ps;
+  long long s_nstride;
 };
 bool pool_conv1x1_f32_eligible(const PoolConvParams& p);
 void launch_pool_conv1x1_f32(const PoolConvParams& p, hipStream_t s);

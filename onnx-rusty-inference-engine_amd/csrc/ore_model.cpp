@@ -72,6 +72,7 @@ struct Step {
   StepKind kind = S_NOP;
   std::string op, name;
   int in0 = -1, in1 = -1, in2 = -1, out = -1;
+  int in3 = -1;  // a fourth activation input: the recomputed expand1x1's input S (pe1)
   // conv / pool geometry (per image)
   int64_t C = 0, H = 0, W = 0, M = 0, kh = 0, kw = 0, sh = 1, sw = 1;
   Window win;
@@ -81,6 +82,13 @@ struct Step {
   bool pool = false;
   int64_t pH = 0, pW = 0, psh = 1, psw = 1;
   Window pwin;
+  // ... whose input is Concat(e1, e3) with e1 (a 1x1 conv + Relu of in3) recomputed inside the kernel
+  // (pass pool_expand, ORE_FUSE_POOL_EXPAND): e1's K-major packing, its bias and shape
+  bool pe1 = false;
+  const float* pe1_w = nullptr;
+  const float* pe1_b = nullptr;
+  int64_t pe1_C = 0, pe1_E = 0;
+  int pe1_Mp = 0;
   // fused following MaxPool (ORE_FUSE_CONV_POOL): out is the pool's output; pool geometry below
   bool epool = false;
   mutable int ran_tile = -1;  // pooled conv: the kernel variant its last launch took (EPOOL_TILE_BASE + v)
@@ -510,7 +518,7 @@ ore_status build_node(ore_model* m, const Node& n, Step* s) {
 void count_uses(ore_model* m, const std::vector<Step>& steps) {
   for (auto& v : m->values) v.uses = 0;
   for (auto& s : steps)
-    for (int id : {s.in0, s.in1, s.in2})
+    for (int id : {s.in0, s.in1, s.in2, s.in3})
       if (id >= 0) m->values[id].uses++;
 }
 
@@ -545,14 +553,15 @@ struct Planner {
   // the first launched step at or after `from` that reads v (in0 or in1)
   int reader(int v, size_t from) const {
     for (size_t j = from; j < m->steps.size(); ++j)
-      if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == v || m->steps[j].in1 == v)) return int(j);
+      if (m->steps[j].kind != S_NOP && (m->steps[j].in0 == v || m->steps[j].in1 == v || m->steps[j].in3 == v))
+        return int(j);
     return -1;
   }
   // a value read once, not the graph output: free to elide
   bool private_value(int v) const { return m->values[v].uses == 1 && !m->values[v].is_output; }
   void nop(Step& s) {
     s.kind = S_NOP;
-    s.in0 = s.in1 = -1;
+    s.in0 = s.in1 = s.in3 = -1;
   }
   void recount() { count_uses(m, m->steps); }
   // a plain f32 1x1 conv (+ Relu) on the direct kernels, output the size of its input
@@ -1044,6 +1053,61 @@ struct Planner {
     recount();
   }
 
+  // (8a) f32: the pooled squeeze of (8) whose pool reads Concat(e1, e3), e1 a 1x1 conv + Relu of 32 / 64
+  // channels read only by the Concat (SqueezeNet fire4 -> pool3 -> fire5, fire8 -> pool5 -> fire9 under
+  // Winograd, wino_pool_split): e1 is recomputed inside pool_conv1x1_f32_kernel from its own input, so
+  // its map (fire4: 128 x 54 x 54 floats per image) is neither written nor read back.  The Concat is
+  // placed in memory here (e3 writes its slice; e1's slice is never materialised).  Bit-identical: the
+  // same k-ordered MFMA chain, bias and Relu as the streaming 1x1 conv, the max of the same nine values.
+  // Not under ORE_KEEP_VALUES (e1's output would not exist to read back).
+  void pool_expand() {
+    if (!has(ORE_FUSE_POOL_EXPAND | ORE_FUSE_POOL_SQUEEZE | ORE_FUSE_CONV_RELU | ORE_FUSE_CONCAT) ||
+        has(ORE_KEEP_VALUES) || m->f16)
+      return;
+    for (size_t i = 0; i < m->steps.size(); ++i) {
+      Step& cv = st(int(i));
+      if (cv.kind != S_CONV || !cv.pool || cv.pe1 || cv.in0 < 0) continue;
+      const int ci = producer[cv.in0];
+      int pa, pb;
+      if (ci < 0 || !fire_concat(ci, &pa, &pb)) continue;
+      Step &cc = st(ci), &e1 = st(pa), &e3 = st(pb);
+      if (!plain_1x1(e1) || e1.in2 < 0 || !e1.wp || (e1.C != 32 && e1.C != 64) || e1.M % 16 || e1.H != cv.pH ||
+          e1.W != cv.pW || e3.kind != S_CONV || e3.epool || e3.pool)
+        continue;
+      if (!private_value(cc.in0) || !private_value(cc.in1) || val(e1.in0).es != 4 || val(e1.in0).nhwc ||
+          val(cc.in0).alias_of >= 0 || val(cc.in1).alias_of >= 0)
+        continue;
+      PoolConvParams q{};  // the kernel's limits with e1 inside
+      q.C = int(cv.C); q.H = int(cv.pH); q.W = int(cv.pW); q.Hp = int(cv.pwin.Ho); q.Wp = int(cv.pwin.Wo);
+      q.pt = int(cv.pwin.pt); q.pl = int(cv.pwin.pl); q.M = int(cv.M); q.Mp = cv.plan.Mp; q.Kp = cv.plan.krows;
+      q.N = 1; q.x_ps = int(q.H * q.W); q.y_ps = int(q.Hp * q.Wp);
+      q.x_nstride = int64_t(q.C) * q.x_ps; q.y_nstride = int64_t(q.M) * q.y_ps;
+      q.s = q.w1 = q.b1 = e1.wp; q.C1 = int(e1.C); q.E1 = int(e1.M); q.w1_Mp = e1.plan.Mp; q.s_ps = q.H * q.W;
+      if (!pool_conv1x1_f32_eligible(q)) continue;
+      cv.pe1 = true;
+      cv.in3 = e1.in0;
+      cv.pe1_w = e1.wp;
+      cv.pe1_b = val(e1.in2).cptr;
+      cv.pe1_C = e1.C;
+      cv.pe1_E = e1.M;
+      cv.pe1_Mp = e1.plan.Mp;
+      // work: e1 per band row it stages (2 PR + 1 input rows per PR pooled rows, neighbouring bands share one)
+      const double rows = double((cv.pwin.Ho + 1) / 2 * 5);
+      cv.mfma_flops_per_img = (cv.mfma_flops_per_img < 0 ? cv.flops_per_img : cv.mfma_flops_per_img) +
+                              e1.flops_per_img * rows / double(e1.H);
+      cv.flops_per_img += e1.flops_per_img;
+      cv.bytes_per_img = 4.0 * double((cv.C - e1.M + e1.C) * cv.pH * cv.pW) + 4.0 * double(cv.M * cv.H * cv.W);
+      cv.name = e1.name + "+" + cv.name;
+      // Concat in place, e1's slice never written
+      Value &a = val(cc.in0), &b = val(cc.in1);
+      a.alias_of = cc.out; a.alias_ch = 0; a.slice = true; a.elided = true;
+      b.alias_of = cc.out; b.alias_ch = a.dims[1]; b.slice = true;
+      nop(cc);
+      nop(e1);
+    }
+    recount();
+  }
+
   // (8b) f16: a 1x1 conv (+ Relu) whose only reader is GlobalAveragePool runs with the GAP in its
   // epilogue (conv1x1_gap_f16_kernel: SqueezeNet conv10 -> relu10 -> pool10; the 87 MB map is never
   // stored).  Bit-identical to conv_f16 + gap_nhwc_kernel.  Not under ORE_KEEP_VALUES (the conv output
@@ -1148,7 +1212,7 @@ struct Planner {
     for (const Step& s : m->steps) {
       if (s.kind == S_NOP) continue;
       const bool ok = s.kind == S_CONV || s.kind == S_FIRE || s.kind == S_MAXPOOL || (s.kind == S_GAP && !val(s.in0).nhwc);
-      for (int id : {s.in0, s.in2, s.out})
+      for (int id : {s.in0, s.in2, s.in3, s.out})
         if (id >= 0 && !val(id).is_const && !ok) dense[root(id)] = 1;
       if (s.in1 >= 0 && !val(s.in1).is_const) dense[root(s.in1)] = 1;
     }
@@ -1189,7 +1253,7 @@ struct Planner {
     for (int i = 0; i < nsteps; ++i) {
       const Step& s = m->steps[i];
       if (s.kind == S_NOP) continue;
-      for (int id : {s.in0, s.in1, s.in2}) {
+      for (int id : {s.in0, s.in1, s.in2, s.in3}) {
         if (id < 0 || val(id).is_const) continue;
         Value& r = val(root(id));
         if (r.first < 0) r.first = i;
@@ -1300,8 +1364,8 @@ struct Planner {
       if (k > 0 && m->pair_next[k - 1]) continue;  // pairs only
       const Step &A = st(m->exec_steps[k]), &B = st(m->exec_steps[k + 1]);
       bool ok = A.out >= 0 && B.out >= 0;
-      for (int bi : {B.in0, B.in1, B.in2}) ok = ok && !overlap(bi, A.out);
-      for (int ai : {A.in0, A.in1, A.in2}) ok = ok && !overlap(ai, B.out);
+      for (int bi : {B.in0, B.in1, B.in2, B.in3}) ok = ok && !overlap(bi, A.out);
+      for (int ai : {A.in0, A.in1, A.in2, A.in3}) ok = ok && !overlap(ai, B.out);
       ok = ok && !overlap(A.out, B.out);
       m->pair_next[k] = ok ? 1 : 0;
     }
@@ -1348,6 +1412,7 @@ ore_status plan(ore_model* m) {
   if (ore_status st = p.fire_f16_concat()) return st;
   if (ore_status st = p.first_squeeze()) return st;
   p.pool_squeeze();
+  p.pool_expand();
   if (ore_status st = p.conv_gap()) return st;
   p.select_algorithms();
   p.alias_copies();
@@ -1478,9 +1543,16 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
         s.ran_tile = last_conv_tile;
         return r;
       }
-      if (s.pool)
+      if (s.pool) {
+        PoolExpand pe{};
+        if (s.pe1) {
+          const Ref sv = ref_of(m, s.in3);
+          pe = {sv.p, s.pe1_w, s.pe1_b, int(s.pe1_C), int(s.pe1_E), s.pe1_Mp,
+                sv.ps ? sv.ps : s.pH * s.pW, sv.nstride};
+        }
         return run_conv_pool(ctx, s.plan, x.p, n, s.C, s.pH, s.pW, x.nstride, x.ps, s.pwin, s.psh, s.psw, s.wp, s.M, bias,
-                             s.relu, y.p, y.nstride, y.ps, x.es);
+                             s.relu, y.p, y.nstride, y.ps, x.es, s.pe1 ? &pe : nullptr);
+      }
       ctx->mapped_lo = m->arena_alloc;  // the arena and its 4 KiB lead are mapped
       ctx->mapped_hi = m->arena ? m->arena + m->arena_bytes : nullptr;
       const ore_status st = run_conv(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, s.wp, s.ktab, s.M, s.kh, s.kw, bias,

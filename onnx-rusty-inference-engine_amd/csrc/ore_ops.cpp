@@ -367,7 +367,7 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
 ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int64_t N, int64_t C, int64_t pH,
                          int64_t pW, int64_t x_nstride, int64_t x_ps, const Window& pwin, int64_t psh, int64_t psw,
                          const float* wp, int64_t M, const float* bias, bool relu, float* y, int64_t y_nstride,
-                         int64_t y_ps, int x_es) {
+                         int64_t y_ps, int x_es, const PoolExpand* pe) {
   if (N == 0) return ORE_OK;
   if (x_ps == 0) x_ps = pH * pW;
   const int64_t P = pwin.Ho * pwin.Wo;
@@ -382,6 +382,12 @@ ore_status run_conv_pool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int6
   q.pt = int(pwin.pt); q.pl = int(pwin.pl); q.M = int(M); q.Mp = pln.Mp; q.Kp = pln.krows;
   q.x_ps = int(x_ps); q.y_ps = int(y_ps); q.x_nstride = x_nstride; q.y_nstride = y_nstride;
   q.relu = relu ? 1 : 0;
+  if (pe) {
+    q.s = pe->s; q.w1 = pe->w1; q.b1 = pe->b1; q.C1 = pe->C1; q.E1 = pe->E1; q.w1_Mp = pe->w1_Mp;
+    q.s_ps = int(pe->s_ps); q.s_nstride = pe->s_nstride;
+    if (!fits_i32(pe->s_nstride * N + 256) || !fits_i32(pe->s_ps))
+      return set_error(ctx, ORE_ERR_INVALID, "internal: recomputed expand input past 2 GiB");
+  }
   if (psh != 2 || psw != 2 || pwin.Ho <= 0 || !fits_i32(x_nstride * N + 256) || !fits_i32(y_nstride * N + 256) ||
       !pool_conv1x1_f32_eligible(q))
     return set_error(ctx, ORE_ERR_INVALID, "internal: pooled 1x1 conv outside pool_conv1x1_f32_kernel's limits");

@@ -19,9 +19,9 @@ STATUS_NAMES = {0: "ORE_OK", 1: "ORE_ERR_INVALID", 2: "ORE_ERR_UNSUPPORTED", 3: 
 # ore_model_set_fusion flags (include/ore.h)
 FUSE_CONV_RELU, FUSE_CONCAT, FUSE_ALIAS, KEEP_VALUES, FUSE_CONV_POOL = 1, 2, 4, 8, 32
 FUSE_FIRE, FUSE_CONCAT_POOL, FUSE_FIRE_POOL, FUSE_FIRST_SQUEEZE, FUSE_POOL_SQUEEZE = 64, 128, 256, 512, 1024
-FUSE_CONV_GAP = 4096
+FUSE_CONV_GAP, FUSE_POOL_EXPAND = 4096, 8192
 FUSE_EAGER = 2048  # tests: every eligible fusion regardless of the size heuristics
-FUSE_ALL = 6119
+FUSE_ALL = 14311
 LOAD_F16 = 1  # ore_model_load_ex flag: the fp16 variant
 LOAD_NO_WINOGRAD = 4  # ore_model_load_ex flag: 3x3 stride-1 convs on the direct kernels only
 LOAD_RETIRED_MASK = 10  # ABI 1's LOAD_X3 / LOAD_X3_ALL: rejected (ORE_ERR_UNSUPPORTED) since ABI 2

@@ -923,6 +923,63 @@ def test_squeezenet_fire_pool_fused(gpu_ctx):
     assert nsteps[0] == nsteps[1] - 4  # per pair: two expand walkers + the squeeze -> fire_pool_kernel
 
 
+@pytest.mark.parametrize("case", [
+    # C, H, W, S1, E1, E3, S2, pool pads (S1 = C1 of the recomputed expand1x1: 32 or 64)
+    (16, 54, 54, 32, 128, 128, 32, [0, 0, 1, 1]),  # SqueezeNet fire4 -> pool3 (ceil) -> fire5 squeeze (NF = 2)
+    (32, 27, 27, 64, 256, 256, 64, [0, 0, 0, 0]),  # fire8 -> pool5 -> fire9 squeeze (C1 = 64, NF = 1)
+    (16, 20, 21, 32, 64, 64, 48, [1, 1, 1, 1]),    # padded on all sides, odd W: band pixels wrap rows in a fragment
+    (16, 9, 8, 64, 48, 80, 16, [0, 0, 0, 0]),      # E1 = 48 (3 recomputed chunks), E3 = 80, W = 8
+    (16, 30, 17, 32, 32, 96, 64, [0, 0, 1, 1]),    # one recomputed chunk, short last band
+])
+def test_pool_expand_fused_bit_identical(gpu_ctx, case):
+    """ORE_FUSE_POOL_EXPAND: the pooled squeeze (pool_conv1x1_f32_kernel) recomputes the Concat's
+    expand1x1 slice from the fire module's squeeze output instead of reading it back; the output
+    equals the plan without that bit (expand1x1 as its own launch, its map stored) bit for bit, the
+    step count drops by one, and the oracle agrees within the conv tolerance (expand3x3 on Winograd)."""
+    import ore
+    import oracle
+    C, H, W, S1, E1, E3, S2, pads = case
+    mb = _fire_pool_model(*case)
+    x = np.random.default_rng(sum(case[:7]) + 3).standard_normal((5, C, H, W)).astype(np.float32)
+    outs, nsteps = [], []
+    for on in ("1", "0"):
+        m = _model(gpu_ctx, mb, max_batch=5)
+        m.set_fusion(ore.FUSE_ALL if on == "1" else ore.FUSE_ALL & ~ore.FUSE_POOL_EXPAND)
+        outs.append(_np(m.run(_t(x))))
+        nsteps.append(len(m.tiles()))
+        m.close()
+    assert nsteps[0] == nsteps[1] - 1, nsteps  # the expand1x1 launch is gone
+    np.testing.assert_array_equal(outs[0], outs[1])
+    ref = oracle.Model(mb).run(x, S2)
+    np.testing.assert_allclose(outs[0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("B", [3, 256])
+def test_squeezenet_pool_expand_fused(gpu_ctx, B):
+    """SqueezeNet-1.0 @224 f32 (Winograd plan): fire4/expand1x1 inside pool3 + fire5/squeeze1x1 and
+    fire8/expand1x1 inside pool5 + fire9/squeeze1x1; probabilities equal the plan without
+    ORE_FUSE_POOL_EXPAND bit for bit, with two launches fewer (B = 256: the headline plan, 2 streams)."""
+    import ore
+    import torch
+    from ore import squeezenet
+    mb = squeezenet.build_calibrated(224)
+    x = _t(squeezenet.synthetic_input(min(B, 4), 224, seed=41))
+    if B > 4:
+        x = torch.cat([x] * (B // 4 + 1))[:B].contiguous()
+    outs, nsteps, names = [], [], []
+    for on in ("1", "0"):
+        m = _model(gpu_ctx, mb, max_batch=B)
+        m.set_fusion(ore.FUSE_ALL if on == "1" else ore.FUSE_ALL & ~ore.FUSE_POOL_EXPAND)
+        m.set_streams(2)
+        outs.append(_np(m.run(x)))
+        nsteps.append(len(m.tiles()))
+        names.append([st["name"] for st in m.steps()])
+        m.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
+    assert nsteps[0] == nsteps[1] - 2, (nsteps, names)
+    assert "fire4/expand1x1+pool3+fire5/squeeze1x1" in names[0] and "fire8/expand1x1+pool5+fire9/squeeze1x1" in names[0], names[0]
+
+
 def test_abi2_retired_values(gpu_ctx):
     """ABI 2 (include/ore.h): ABI 1's retired values fail with ORE_ERR_UNSUPPORTED and a message
     naming the retirement -- the bf16x3 load flags (2, 8) and tiles 28-35, fusion bit 16
