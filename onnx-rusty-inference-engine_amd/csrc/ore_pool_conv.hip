@@ -19,9 +19,11 @@
 //
 // ORE_FUSE_POOL_EXPAND (KS1 > 0): the pool input is a fire module's Concat(e1, e3) whose e1 slice (the
 // expand1x1, E1 channels) is never stored: chunks ci < E1 / 16 are recomputed here from e1's own input
-// S (C1 = 4 KS1 channels, the squeeze output of the same fire module), staged once per workgroup for
-// the band's 2 PS_PR + 1 rows.  Per such chunk every wave runs 16x16x4 MFMAs over its pixel fragments
-// (16 channels x 16 band pixels, k = 4 t + lk ascending from zero: the streaming 1x1 conv's fma chain),
+// S (C1 = 4 KS1 channels, the squeeze output of the same fire module): each wave loads its FRW 16-pixel
+// fragments of the band's 2 PS_PR + 1 rows once, straight into the MFMA B registers (no LDS: the
+// workgroup keeps the plain kernel's LDS size and occupancy).  Per such chunk every wave runs 16x16x4
+// MFMAs over those fragments (16 channels x 16 band pixels, k = 4 t + lk ascending from zero, the
+// fragments' chains interleaved: the streaming 1x1 conv's fma chain),
 // adds the bias and applies the Relu exactly as conv_stream_kernel's epilogue, and writes the values
 // into the staged rows (rows outside the image: the pool's zero padding); pooling and the squeeze then
 // run as for a loaded chunk.  fire4 -> pool3 -> fire5 and fire8 -> pool5 -> fire9 no longer write and
@@ -29,7 +31,8 @@
 #include <float.h>
 #include <hip/hip_runtime.h>
 
-#include <atomic>
+#include <type_traits>
+
 
 #include "ore_kernels.h"
 
@@ -47,15 +50,9 @@ constexpr int PS_PR = ORE_PS_PR, PS_CH = ORE_PS_CH;
 constexpr int PS_AUX = 2;
 constexpr int PS_ROWS = 2 * PS_PR + 1;  // input rows of PS_PR pooled rows (3x3, stride 2)
 
-// LDS floats of the staged S band (KS1 > 0): C1 channels x PXS pixels; PXS = the band's 2 PS_PR + 1
-// rows of W pixels rounded up to 16-pixel fragments, = 16 mod 32 (the lane groups lk = 0 / 1 of a
-// ds_read_b32 hit opposite halves of the banks)
-__host__ __device__ constexpr int ps_pxs(int W) {
-  const int fr = ((2 * ORE_PS_PR + 1) * W + 15) / 16 * 16;
-  return fr % 32 == 16 ? fr : fr + 16;
-}
-
-template <int NF, int KS1>  // NF: 16-pixel fragments per pooled row (Wp <= 16 NF); KS1: e1's k-steps (0: no e1)
+// NF: 16-pixel fragments per pooled row (Wp <= 16 NF); KS1: e1's k-steps (0: no e1); FRW: e1 pixel fragments
+// per wave (>= ceil(ceil((2 PS_PR + 1) W / 16) / 4))
+template <int NF, int KS1, int FRW>
 __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p) {
   // staged rows: input column iw at LDS column iw + PS_LC; columns left of the image and right of
   // the loaded 16-B groups are zero once (never written), loaded columns >= W are zeroed per element
@@ -87,30 +84,29 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0, p.Kp * p.Mp * 4, 0x00020000);
   for (int i = tid; i < PS_IN; i += 256) in_s[i] = 0.0f;
 
-  // e1 recomputed (KS1 > 0): S's band rows [ih0, ih0 + PS_ROWS) as [C1][PXS] (dynamic LDS; rows outside
-  // the image and the fragment padding are 0), e1's bias at the end
-  extern __shared__ __attribute__((aligned(16))) float e1_s[];
+  // e1 recomputed (KS1 > 0): this wave's band pixels 16 (wave + 4 i) + lj of S's rows [ih0, ih0 + PS_ROWS),
+  // k = 4 t + lk, as MFMA B operands (pixels past the band or rows outside the image read 0); e1's bias in LDS
+  constexpr int KA1 = KS1 > 0 ? KS1 : 1, FA1 = KS1 > 0 ? FRW : 1;
+  __shared__ float b1_s[KS1 > 0 ? 256 : 1];
   const int ne1 = KS1 > 0 ? p.E1 / PS_CH : 0;  // recomputed chunks
-  const int pxs = ps_pxs(p.W), bpx = PS_ROWS * p.W;
-  float* b1_s = e1_s + 4 * KS1 * pxs;
+  const int bpx = PS_ROWS * p.W;
+  float sb[FA1][KA1];
+  int e1_off[FA1];  // in_s offset of the lane's pixel of fragment i (channel 0), -1: past the band
+  bool e1_rin[FA1];
   if constexpr (KS1 > 0) {
     const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(p.s + (long long)img * p.s_nstride), (short)0, 4 * KS1 * p.s_ps * 4, 0x00020000);
-    const int hw = p.H * p.W, g0 = ih0 * p.W;
-    for (int i0 = 0; i0 < 4 * KS1 * pxs; i0 += 256 * 8) {
-      float v[8];
+    const int hw = p.H * p.W;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {  // 8 loads in flight per thread
-        const int i = i0 + 256 * u + tid, c = i / pxs, px = i - c * pxs, g = g0 + px;
-        const bool in = i < 4 * KS1 * pxs && px < bpx && g >= 0 && g < hw;
-        v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                             sr, in ? (c * p.s_ps + g) * 4 : (int)0x80000000, 0, 0));
-      }
+    for (int i = 0; i < FRW; ++i) {
+      const int px = 16 * (wave + 4 * i) + lj, r = px / p.W, g = ih0 * p.W + px;
+      const bool in = px < bpx && g >= 0 && g < hw;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = i0 + 256 * u + tid;
-        if (i < 4 * KS1 * pxs) e1_s[i] = v[u];
-      }
+      for (int t = 0; t < KS1; ++t)
+        sb[i][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                 sr, in ? ((4 * t + lk) * p.s_ps + g) * 4 : (int)0x80000000, 0, 0));
+      e1_off[i] = px < bpx ? r * PS_RS + PS_LC + (px - r * p.W) : -1;
+      e1_rin[i] = (unsigned)(ih0 + r) < (unsigned)p.H;
     }
     for (int i = tid; i < p.E1; i += 256) b1_s[i] = p.b1[i];
   }
@@ -158,7 +154,6 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
                                              wr, ((ci * PS_CH + 4 * t + lk) * p.Mp + m0 + lj) * 4, 0, 0));
   };
   // e1's A values of a recomputed chunk (k = 4 t + lk, row 16 ci + lj of the K-major packing), one chunk ahead
-  constexpr int KA1 = KS1 > 0 ? KS1 : 1;
   float a1cur[KA1], a1nxt[KA1];
   const __amdgpu_buffer_rsrc_t w1r = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(KS1 > 0 ? p.w1 : p.wp), (short)0, 4 * KS1 * p.w1_Mp * 4, 0x00020000);
@@ -173,26 +168,31 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
     load_a1(a1cur, 0);
   else
     load_chunk(0);
-  const int nfr1 = (bpx + 15) / 16;  // e1 pixel fragments of the band
-  for (int ci = 0; ci < nch; ++ci) {
-    __syncthreads();  // the previous chunk's staged rows are pooled (and, before chunk 0, S is staged)
-    if (KS1 > 0 && ci < ne1) {
-      // e1 channels 16 ci + 4 lk + e at band pixel 16 fr + lj: the 1x1 conv, bias, Relu -> staged rows
-      for (int fr = wave; fr < nfr1; fr += 4) {
-        ps4 a = ps4{0.f, 0.f, 0.f, 0.f};
+  // one chunk; RC: a recomputed e1 chunk (the two kinds run as two loops, so e1's B registers and the
+  // loaded chunks' staging registers are never live together)
+  auto chunk = [&](int ci, auto rc) __attribute__((always_inline)) {
+    constexpr bool RC = decltype(rc)::value;
+    __syncthreads();  // the previous chunk's staged rows are pooled
+    if constexpr (RC) {
+      // e1 channels 16 ci + 4 lk + e at the wave's band pixels: the 1x1 conv, bias, Relu -> staged rows
+      ps4 a[FA1];
 #pragma unroll
-        for (int t = 0; t < KS1; ++t)
-          a = __builtin_amdgcn_mfma_f32_16x16x4f32(a1cur[t], e1_s[(4 * t + lk) * pxs + 16 * fr + lj], a, 0, 0, 0);
-        const int px = 16 * fr + lj, r = px / p.W, col = px - r * p.W;
-        if (px < bpx) {
-          const bool rin = (unsigned)(ih0 + r) < (unsigned)p.H;
+      for (int i = 0; i < FA1; ++i) a[i] = ps4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int ch = 4 * lk + e;
-            float v = a[e] + b1_s[PS_CH * ci + ch];
-            v = fmaxf(v, 0.0f);
-            in_s[(ch * PS_ROWS + r) * PS_RS + PS_LC + col] = rin ? v : 0.0f;
-          }
+      for (int t = 0; t < KA1; ++t)
+#pragma unroll
+        for (int i = 0; i < FA1; ++i) a[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1cur[t], sb[i][t], a[i], 0, 0, 0);
+      float bb[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bb[e] = b1_s[PS_CH * ci + 4 * lk + e];
+#pragma unroll
+      for (int i = 0; i < FA1; ++i) {
+        if (e1_off[i] < 0) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = a[i][e] + bb[e];
+          v = fmaxf(v, 0.0f);
+          in_s[(4 * lk + e) * PS_ROWS * PS_RS + e1_off[i]] = e1_rin[i] ? v : 0.0f;
         }
       }
     } else {
@@ -235,11 +235,15 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
     }
 #pragma unroll
     for (int t = 0; t < KS; ++t) acur[t] = anxt[t];
-    if (KS1 > 0 && ci + 1 < ne1) {
+    if (RC && ci + 1 < ne1) {
 #pragma unroll
-      for (int t = 0; t < KS1; ++t) a1cur[t] = a1nxt[t];
+      for (int t = 0; t < KA1; ++t) a1cur[t] = a1nxt[t];
     }
-  }
+  };
+  int ci = 0;
+  if constexpr (KS1 > 0)
+    for (; ci < ne1; ++ci) chunk(ci, std::true_type{});
+  for (; ci < nch; ++ci) chunk(ci, std::false_type{});
   // bias + Relu, NCHW stores: channel m0 + 4 lk + e, pooled pixel (pr0 + n / NF, 16 (n % NF) + lj)
   if (m0 >= p.M) return;
 #pragma unroll
@@ -260,14 +264,14 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
 
 }  // namespace
 
-// dynamic LDS of the recomputed-e1 variant: the S band and e1's bias
-static size_t ps_e1_lds(const PoolConvParams& p) { return ((size_t)p.C1 * ps_pxs(p.W) + p.E1) * 4; }
+// e1 pixel fragments per wave of the recomputed-e1 variant (the band's (2 PS_PR + 1) W pixels over 4 waves)
+static int ps_frw(const PoolConvParams& p) { return ((PS_ROWS * p.W + 15) / 16 + 3) / 4; }
 
 bool pool_conv1x1_f32_eligible(const PoolConvParams& p) {
   const bool e1ok = p.E1 == 0 ||
                     ((p.C1 == 32 || p.C1 == 64) && p.E1 % PS_CH == 0 && p.E1 <= p.C && p.s && p.w1 && p.b1 &&
                      p.w1_Mp >= p.E1 && p.s_ps >= p.H * p.W && (long long)p.C1 * p.s_ps * 4 < (1LL << 31) &&
-                     (long long)p.C1 * p.w1_Mp * 4 < (1LL << 31) && ps_e1_lds(p) <= 64 * 1024);
+                     (long long)p.C1 * p.w1_Mp * 4 < (1LL << 31) && p.E1 <= 256 && ps_frw(p) <= 6);
   return p.C % PS_CH == 0 && p.C > 0 && p.M >= 1 && p.M <= 64 && p.Wp >= 1 && p.Wp <= 32 && p.Hp >= 1 &&
          p.W <= 2 * (p.Wp <= 16 ? 16 : 32) + 1 && 2 * (p.Wp - 1) + 2 - p.pl <= p.W + 1 &&
          p.pt >= 0 && p.pl >= 0 && p.pt <= 2 && p.pl <= 2 && p.x_ps >= p.H * p.W &&
@@ -275,24 +279,30 @@ bool pool_conv1x1_f32_eligible(const PoolConvParams& p) {
          p.Mp >= p.M && p.y_ps >= p.Hp * p.Wp && e1ok;
 }
 
-template <int NF, int KS1>
+template <int NF, int KS1, int FRW>
 static void ps_launch(const PoolConvParams& p, long long grid, hipStream_t s) {
-  const size_t lds = KS1 > 0 ? ps_e1_lds(p) : 0;
-  if (lds > 32 * 1024) {  // with the static arrays above the default 64 KB: raised once per device
-    static std::atomic<unsigned long long> raised{0};
-    ore_raise_lds_once(raised, reinterpret_cast<const void*>(&pool_conv1x1_f32_kernel<NF, KS1>), 96 * 1024);
+  hipLaunchKernelGGL((pool_conv1x1_f32_kernel<NF, KS1, FRW>), dim3((unsigned)grid), dim3(256), 0, s, p);
+}
+
+template <int NF, int KS1>
+static void ps_dispatch_frw(const PoolConvParams& p, long long grid, hipStream_t s) {
+  switch (ps_frw(p)) {  // the fewest fragments per wave that cover the band
+    case 1: case 2: ps_launch<NF, KS1, 2>(p, grid, s); break;
+    case 3: ps_launch<NF, KS1, 3>(p, grid, s); break;
+    case 4: ps_launch<NF, KS1, 4>(p, grid, s); break;
+    case 5: ps_launch<NF, KS1, 5>(p, grid, s); break;
+    default: ps_launch<NF, KS1, 6>(p, grid, s); break;
   }
-  hipLaunchKernelGGL((pool_conv1x1_f32_kernel<NF, KS1>), dim3((unsigned)grid), dim3(256), lds, s, p);
 }
 
 template <int NF>
 static void ps_dispatch(const PoolConvParams& p, long long grid, hipStream_t s) {
   if (p.E1 == 0)
-    ps_launch<NF, 0>(p, grid, s);
+    ps_launch<NF, 0, 0>(p, grid, s);
   else if (p.C1 == 32)
-    ps_launch<NF, 8>(p, grid, s);
+    ps_dispatch_frw<NF, 8>(p, grid, s);
   else
-    ps_launch<NF, 16>(p, grid, s);
+    ps_dispatch_frw<NF, 16>(p, grid, s);
 }
 
 void launch_pool_conv1x1_f32(const PoolConvParams& p, hipStream_t s) {

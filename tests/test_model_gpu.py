@@ -830,7 +830,8 @@ def test_squeezenet_pool_squeeze_fused(gpu_ctx):
     outs, nsteps = [], []
     for on in ("1", "0"):
         m = _model(gpu_ctx, mb, max_batch=3)
-        m.set_fusion(ore.FUSE_ALL if on == "1" else ore.FUSE_ALL & ~ore.FUSE_POOL_SQUEEZE)
+        base = ore.FUSE_ALL & ~ore.FUSE_POOL_EXPAND  # (with it, fire8's expand1x1 would join as well)
+        m.set_fusion(base if on == "1" else base & ~ore.FUSE_POOL_SQUEEZE)
         outs.append(_np(m.run(x)))
         nsteps.append(len(m.tiles()))
         m.close()
@@ -935,23 +936,27 @@ def test_pool_expand_fused_bit_identical(gpu_ctx, case):
     """ORE_FUSE_POOL_EXPAND: the pooled squeeze (pool_conv1x1_f32_kernel) recomputes the Concat's
     expand1x1 slice from the fire module's squeeze output instead of reading it back; the output
     equals the plan without that bit (expand1x1 as its own launch, its map stored) bit for bit, the
-    step count drops by one, and the oracle agrees within the conv tolerance (expand3x3 on Winograd)."""
+    step count drops by one, and the oracle agrees within the conv tolerance.  Winograd and direct
+    expand3x3 plans (the direct one with the 54 x 54 case taken by the Concat + pool fusion instead)."""
     import ore
     import oracle
     C, H, W, S1, E1, E3, S2, pads = case
     mb = _fire_pool_model(*case)
     x = np.random.default_rng(sum(case[:7]) + 3).standard_normal((5, C, H, W)).astype(np.float32)
     outs, nsteps = [], []
-    for on in ("1", "0"):
-        m = _model(gpu_ctx, mb, max_batch=5)
-        m.set_fusion(ore.FUSE_ALL if on == "1" else ore.FUSE_ALL & ~ore.FUSE_POOL_EXPAND)
-        outs.append(_np(m.run(_t(x))))
-        nsteps.append(len(m.tiles()))
-        m.close()
-    assert nsteps[0] == nsteps[1] - 1, nsteps  # the expand1x1 launch is gone
-    np.testing.assert_array_equal(outs[0], outs[1])
     ref = oracle.Model(mb).run(x, S2)
-    np.testing.assert_allclose(outs[0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-5)
+    for wino in (True, False):
+        outs, nsteps = [], []
+        for on in ("1", "0"):
+            m = ore.Model(gpu_ctx, mb, max_batch=5, winograd=wino)
+            m.set_fusion(ore.FUSE_ALL if on == "1" else ore.FUSE_ALL & ~ore.FUSE_POOL_EXPAND)
+            outs.append(_np(m.run(_t(x))))
+            nsteps.append(len(m.tiles()))
+            m.close()
+        if wino or H * W < 1024:
+            assert nsteps[0] == nsteps[1] - 1, (wino, nsteps)  # the expand1x1 launch is gone
+        np.testing.assert_array_equal(outs[0], outs[1])
+        np.testing.assert_allclose(outs[0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("B", [3, 256])
@@ -968,7 +973,7 @@ def test_squeezenet_pool_expand_fused(gpu_ctx, B):
         x = torch.cat([x] * (B // 4 + 1))[:B].contiguous()
     outs, nsteps, names = [], [], []
     for on in ("1", "0"):
-        m = _model(gpu_ctx, mb, max_batch=B)
+        m = ore.Model(gpu_ctx, mb, max_batch=B)  # the default (Winograd) plan
         m.set_fusion(ore.FUSE_ALL if on == "1" else ore.FUSE_ALL & ~ore.FUSE_POOL_EXPAND)
         m.set_streams(2)
         outs.append(_np(m.run(x)))
