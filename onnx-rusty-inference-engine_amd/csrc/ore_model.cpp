@@ -1071,6 +1071,9 @@ struct Planner {
       int pa, pb;
       if (ci < 0 || !fire_concat(ci, &pa, &pb)) continue;
       Step &cc = st(ci), &e1 = st(pa), &e3 = st(pb);
+      // C1 = 64 (fire8 -> pool5) holds 48 B registers per lane and halves the launch's occupancy: 218 us
+      // against 74 + 106 for the separate launches (profiles/r05_ab_pool_expand.txt), so 32 only unless eager
+      if (!eager() && e1.C != 32) continue;
       if (!plain_1x1(e1) || e1.in2 < 0 || !e1.wp || (e1.C != 32 && e1.C != 64) || e1.M % 16 || e1.H != cv.pH ||
           e1.W != cv.pW || e3.kind != S_CONV || e3.epool || e3.pool)
         continue;
