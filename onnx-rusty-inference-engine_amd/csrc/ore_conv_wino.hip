@@ -548,6 +548,12 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   // the zero blocks (never written by the DMAs)
   if (threadIdx.x < 2 * WM_KC * WM_ZL)
     wm_lds[(threadIdx.x >> 6) * SS + ((threadIdx.x >> 3) & 7) * g.CS + (threadIdx.x & 7)] = 0.0f;
+  // the workgroup's 32 biases (0 past M) after the two stages, read by the epilogue: loaded here, so the
+  // prologue's wait for the first chunk covers their latency (a global load in the epilogue exposed it)
+  if (threadIdx.x >= 128 && threadIdx.x < 128 + WM_CH) {
+    const int m = m0 + (int)threadIdx.x - 128;
+    wm_lds[2 * SS + (int)threadIdx.x - 128] = p.bias && m < p.M ? p.bias[m] : 0.0f;
+  }
 
   // ---- this lane's tile (lj of the wave's 16) and the run layout of the group
   const int lk = lane >> 4, lj = lane & 15;
@@ -699,14 +705,15 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   }
   if (kc < nchunks) chunk(kc, std::false_type{}, st1{});
   // lane (lk, lj) of fragment f holds rows 4 lk + e = channel m0 + 16 f + 4 lk + e of tile lj
-  float bv[2][4];
+  wg_floatx4 bv[2];
 #pragma unroll
-  for (int f = 0; f < 2; ++f)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int m = m0 + 16 * f + 4 * lk + e;
-      bv[f][e] = p.bias && m < p.M ? p.bias[m] : 0.0f;
-    }
+  for (int f = 0; f < 2; ++f) bv[f] = *reinterpret_cast<const wg_floatx4*>(wm_lds + 2 * SS + 16 * f + 4 * lk);
+  // stores: every lane of the wave has its tile's second column (even W, or no tile at the right edge) ->
+  // 8-B row stores whose offsets past the output (invalid tiles, rows, channels) the buffer range check
+  // drops, no branches; else the per-lane wg_store_px
+  const bool fast = __builtin_amdgcn_ballot_w64(w.tok && !w.c1ok) == 0;
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, 0x7FFFFFF0, 0x00020000);
+  typedef int wg_i2 __attribute__((ext_vector_type(2)));
   // the output transform and bias of channels (e, e + 1) on packed f32 (acc[xi][f] holds e = 0 .. 3 in
   // consecutive registers); the same adds in the same order as wg_store_t
 #pragma unroll
@@ -714,7 +721,6 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
 #pragma unroll
     for (int ep = 0; ep < 4; ep += 2) {
       const int mp = m0 + 16 * f + 4 * lk + ep;
-      if (mp >= p.M) continue;
       wg_f2 mx[16], y[4];
 #pragma unroll
       for (int xi = 0; xi < 16; ++xi) mx[xi] = ep == 0 ? acc[xi][f].xy : acc[xi][f].zw;
@@ -722,14 +728,23 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
       const wg_f2 b2 = {bv[f][ep], bv[f][ep + 1]};
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        if (mp + h >= p.M) continue;
         float o[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           o[q] = (y[q] + b2)[h];
           if constexpr (RELU) o[q] = fmaxf(o[q], 0.0f);
         }
-        wg_store_px(p, w, p.y, mp + h, o);
+        const bool mok = mp + h < p.M;
+        if (fast) {
+          const int yo = (w.ybase + (mp + h) * p.y_ps) * 4;
+          const int oob = 0x7FFFFFF0;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(wg_i2, (wg_f2){o[0], o[1]}), yr,
+                                                w.tok && mok ? yo : oob, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(wg_i2, (wg_f2){o[2], o[3]}), yr,
+                                                w.tok && mok && w.r1ok ? yo + p.W * 4 : oob, 0, 0);
+        } else if (mok) {
+          wg_store_px(p, w, p.y, mp + h, o);
+        }
       }
     }
 }
@@ -749,7 +764,7 @@ static bool wm_geom(const ConvParams& p, WmGeom* g, size_t* lds, int* ndma) {
     tmax = std::max(tmax, wm_group_floats(gi * WM_TILES, T, g->TPI, g->TW, p.H, p.W));
   *ndma = (tmax + 255) / 256;
   g->CS = (WM_ZL + tmax + 5 + 31) / 64 * 64 + 32;  // + 1: odd channels' shift, + 4: the last window's overrun
-  *lds = (size_t)2 * WM_KC * (g->CS + 512) * 4;
+  *lds = (size_t)2 * WM_KC * (g->CS + 512) * 4 + WM_CH * 4;  // two stages + the biases
   return *ndma <= 8 && *lds <= 160 * 1024;
 }
 
