@@ -532,104 +532,83 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   extern __shared__ __attribute__((aligned(16))) float wm_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lk = lane >> 4, lj = lane & 15;
-  // work items (tile group, 32-channel block), the channel blocks of a tile group consecutive.  Persistent
-  // workgroups (round 5): the workgroups of XCD x (bid = x + 8 slot) walk the XCD's contiguous item range
-  // [r0, r1) with a stride of their count, so the ones running together take consecutive items (one tile
-  // group's channel blocks share its staged rows in that XCD's L2); the next item's first chunk is staged
-  // under the current item's last chunk, so only a workgroup's first item waits for its DMA.  One item per
-  // workgroup when the grid covers every item (odd chunk counts)
-  const int nitems = g.ntg * p.mtiles;
-  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7;
-  const int nwx = (nwg - xcd + 7) >> 3;  // workgroups on this XCD
-  const int nx = min(nwg, 8);             // XCDs with workgroups
-  const int r1 = (int)((long long)nitems * (xcd + 1) / nx);
-  int item = (int)((long long)nitems * xcd / nx) + (bid >> 3);
-  if (item >= r1) return;  // the whole workgroup, before any barrier
+  // block -> (tile group, 32-channel block), the channel blocks of a tile group consecutive (one XCD:
+  // they share the staged rows in L2)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
+  const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
+  const int mt = wgid % p.mtiles, tgi = wgid / p.mtiles;
+  const int m0 = mt * WM_CH;
   const int T = p.N * g.TPI;
+  const int t0 = tgi * WM_TILES, t1 = min(T, t0 + WM_TILES) - 1;
+  const int img0 = t0 / g.TPI, ty0 = (t0 - img0 * g.TPI) / g.TW;
+  const int img1 = t1 / g.TPI, ty1 = (t1 - img1 * g.TPI) / g.TW;
   const int SS = WM_KC * (g.CS + 512);  // floats per stage: [channel][CS] windows, then [channel][4 quads][32 m][4] U
-  const int nchunks = p.C / WM_KC;
 
   // the zero blocks (never written by the DMAs)
   if (threadIdx.x < 2 * WM_KC * WM_ZL)
     wm_lds[(threadIdx.x >> 6) * SS + ((threadIdx.x >> 3) & 7) * g.CS + (threadIdx.x & 7)] = 0.0f;
+  // the workgroup's 32 biases (0 past M) after the two stages, read by the epilogue: loaded here, so the
+  // prologue's wait for the first chunk covers their latency (a global load in the epilogue exposed it)
+  if (threadIdx.x >= 128 && threadIdx.x < 128 + WM_CH) {
+    const int m = m0 + (int)threadIdx.x - 128;
+    wm_lds[2 * SS + (int)threadIdx.x - 128] = p.bias && m < p.M ? p.bias[m] : 0.0f;
+  }
 
-  // ---- an item's DMA geometry: the run set of its tile group (one run per image the group touches,
-  // rows clamped to the image), DMA piece gi of a channel = floats [4 (64 gi + lane), +4) of it; and
-  // this lane's tile (lj of the wave's 16) inside the runs
-  int voff[NDMA], uoff = 0;
-  auto dma_geom = [&](int it) __attribute__((always_inline)) {
-    const int mt = it % p.mtiles, tgi = it / p.mtiles;
-    const int t0 = tgi * WM_TILES, t1 = min(T, t0 + WM_TILES) - 1;
-    const int img0 = t0 / g.TPI, ty0 = (t0 - img0 * g.TPI) / g.TW;
-    const int img1 = t1 / g.TPI, ty1 = (t1 - img1 * g.TPI) / g.TW;
-#pragma unroll
-    for (int gi = 0; gi < NDMA; ++gi) voff[gi] = -1;
-    int lb = 0;
-    for (int i = img0; i <= img1; ++i) {
-      int rs, re;
-      wm_rows(i, img0, ty0, img1, ty1, p.H, &rs, &re);
-      const int len = (re - rs + 1) * p.W;
-#pragma unroll
-      for (int gi = 0; gi < NDMA; ++gi) {
-        const int k4 = 4 * (64 * gi + lane);
-        if (k4 >= lb && k4 <= lb + len) voff[gi] = (int)((i * p.x_nstride + (long long)rs * p.W + (k4 - lb)) * 4);
-      }
-      lb += (len + 4) & ~3;  // runs of len + 1 floats (odd channels land one float later), rounded to 4
-    }
-    const int uq = 2 * (wave & 1) + (lane >> 5);
-    uoff = (uq * p.Mp + mt * WM_CH + (lane & 31)) * 16;
-  };
-  // ---- an item's window geometry (after its DMA geometry)
-  int m0 = 0;
-  int aw[4];
-  bool c0ok = false, c2ok = false, c3ok = false;
+  // ---- this lane's tile (lj of the wave's 16) and the run layout of the group
+  const int lk = lane >> 4, lj = lane & 15;
+  int t = t0 + 16 * wave + lj;
   WgTile w;
-  auto win_geom = [&](int it) __attribute__((always_inline)) {
-    m0 = (it % p.mtiles) * WM_CH;
-    const int t0 = (it / p.mtiles) * WM_TILES, t1 = min(T, t0 + WM_TILES) - 1;
-    const int img0 = t0 / g.TPI, ty0 = (t0 - img0 * g.TPI) / g.TW;
-    const int img1 = t1 / g.TPI, ty1 = (t1 - img1 * g.TPI) / g.TW;
-    int t = t0 + 16 * wave + lj;
-    w.tok = t < T;
-    if (!w.tok) t = T - 1;
-    const int img = t / g.TPI, rem = t - img * g.TPI, ty = rem / g.TW, tx = rem - ty * g.TW;
-    // this lane's image run inside the staged run set (dma_geom's layout)
-    int my_lb = 0, my_rs = 0;
-    for (int i = img0; i <= img; ++i) {
-      int rs, re;
-      wm_rows(i, img0, ty0, img1, ty1, p.H, &rs, &re);
-      my_rs = rs;
-      if (i < img) my_lb += ((re - rs + 1) * p.W + 4) & ~3;
-    }
-    // window rows (floats from the channel's area; rows outside the image -> the zero block)
+  w.tok = t < T;
+  if (!w.tok) t = T - 1;
+  const int img = t / g.TPI, rem = t - img * g.TPI, ty = rem / g.TW, tx = rem - ty * g.TW;
+  // DMA piece gi of a channel: floats [4 (64 gi + lane), +4) of the run set
+  int voff[NDMA];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gr = 2 * ty - 1 + r;
-      // odd channels are staged one float later (their DMA source starts one float early), so the two
-      // channels of a ds_read_b32 lane group (lk = 0, 1: CS = 0 mod 32 apart) use opposite bank parities
-      const int rel = ((unsigned)gr < (unsigned)p.H ? WM_ZL + my_lb + (gr - my_rs) * p.W + 2 * tx - 1 : 0) + (lk & 1);
-      aw[r] = (lk * g.CS + rel) * 4;  // bytes, channel lk of a k-step
+  for (int gi = 0; gi < NDMA; ++gi) voff[gi] = -1;
+  int my_lb = 0, my_rs = 0;
+  int lb = 0;
+  for (int i = img0; i <= img1; ++i) {
+    int rs, re;
+    wm_rows(i, img0, ty0, img1, ty1, p.H, &rs, &re);
+    const int len = (re - rs + 1) * p.W;
+#pragma unroll
+    for (int gi = 0; gi < NDMA; ++gi) {
+      const int k4 = 4 * (64 * gi + lane);
+      if (k4 >= lb && k4 <= lb + len) voff[gi] = (int)((i * p.x_nstride + (long long)rs * p.W + (k4 - lb)) * 4);
     }
-    c0ok = tx > 0;
-    c2ok = 2 * tx + 1 < p.W;
-    c3ok = 2 * tx + 2 < p.W;
-    w.ybase = img * (int)p.y_nstride + (2 * ty) * p.W + 2 * tx;
-    w.c1ok = 2 * tx + 1 < p.W;
-    w.r1ok = 2 * ty + 1 < p.H;
-  };
+    if (i == img) {
+      my_lb = lb;
+      my_rs = rs;
+    }
+    lb += (len + 4) & ~3;  // runs of len + 1 floats (odd channels land one float later), rounded to 4
+  }
+  // window rows (floats from the channel's area; rows outside the image -> the zero block)
+  int aw[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int gr = 2 * ty - 1 + r;
+    // odd channels are staged one float later (their DMA source starts one float early), so the two
+    // channels of a ds_read_b32 lane group (lk = 0, 1: CS = 0 mod 32 apart) use opposite bank parities
+    const int rel = ((unsigned)gr < (unsigned)p.H ? WM_ZL + my_lb + (gr - my_rs) * p.W + 2 * tx - 1 : 0) + (lk & 1);
+    aw[r] = (lk * g.CS + rel) * 4;  // bytes, channel lk of a k-step
+  }
+  const bool c0ok = tx > 0, c2ok = 2 * tx + 1 < p.W, c3ok = 2 * tx + 2 < p.W;
+  w.ybase = img * (int)p.y_nstride + (2 * ty) * p.W + 2 * tx;
+  w.c1ok = 2 * tx + 1 < p.W;
+  w.r1ok = 2 * ty + 1 < p.H;
   const int au = (WM_KC * g.CS + lk * 512 + lj * 4) * 4;  // bytes: U[c = lk][quad 0][m = lj] of a k-step
 
-  // ---- DMA sources: wave w stages channels w and w + 4 of a chunk, and U pieces d = w + 4 v; an item's
-  // chunk 0 also brings its 32 biases (0 past M: the range check) to bias slot `bslot` after the stages
+  // ---- DMA sources: wave w stages channels w and w + 4 of a chunk, and U pieces d = w + 4 v
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ur =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0, p.C * p.Mp * 16 * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(p.bias ? p.bias : p.wp), (short)0, p.bias ? p.M * 4 : 0, 0x00020000);
+  const int uq = 2 * (wave & 1) + (lane >> 5);
+  const int uoff = (uq * p.Mp + m0 + (lane & 31)) * 16;
   const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) float*)wm_lds;
-  auto stage = [&](int kc, int st, int bslot, int bm0) __attribute__((always_inline)) {
+  const int nchunks = p.C / WM_KC;
+  auto stage = [&](int kc, int st) __attribute__((always_inline)) {
     const unsigned sb = lds0 + (unsigned)(st * SS) * 4;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -644,9 +623,8 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
       const int d = wave + 4 * v, cc = d >> 1;
       wm_dma16(ur, sb + (WM_KC * g.CS + (cc * 4 + 2 * (d & 1)) * 128) * 4, uoff, (kc * WM_KC + cc) * 4 * p.Mp * 16);
     }
-    if (bslot >= 0 && wave == 0 && lane < WM_CH / 4)  // lanes 0-7: 16 B each
-      wm_dma16(br, lds0 + (unsigned)(2 * SS + bslot * WM_CH) * 4, lane * 16, bm0 * 4);
   };
+
   // accumulators: no zeroing -- chunk 0's first k-step takes C = 0 (an inline operand of the MFMA; 128
   // v_mov per wave otherwise, and f32 MFMAs and VALU share the SIMD's issue, nothing overlaps them)
   wg_floatx4 acc[16][2];
@@ -673,16 +651,10 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
     wg_input_transform_pk(d, v);
   };
   // one chunk (two k-steps of 4 channels); FIRST: chunk 0, its first k-step starts the accumulators
-  int nitem = 0, bslot = 0;  // the next item (valid if < r1) and the bias slot of the next item's chunk 0
   auto chunk = [&](int kc, auto first, auto stc) __attribute__((always_inline)) {
     constexpr bool FIRST = decltype(first)::value;
     constexpr int st = decltype(stc)::value;  // kc & 1, a constant: the stage's LDS bases are loop-invariant
-    if (kc + 1 < nchunks) {
-      stage(kc + 1, st ^ 1, -1, 0);
-    } else if (nitem < r1) {  // the last chunk (st = 1: even chunk counts): the next item's chunk 0
-      dma_geom(nitem);
-      stage(0, st ^ 1, bslot ^ 1, (nitem % p.mtiles) * WM_CH);
-    }
+    if (kc + 1 < nchunks) stage(kc + 1, st ^ 1);
     const int sto0 = st * SS * 4, sto1 = sto0 + 4 * g.CS * 4;  // k-step 1: channels 4 .. 7 of the chunk
     wg_floatx4 ua[2][4];
     wg_f2 d0[4][2], d1[4][2], v[8];  // v[2 i + h][e]: position 4 i + 2 h + e
@@ -720,73 +692,63 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
     __syncthreads();  // ... every wave's, and every wave is done reading stage kc & 1
   };
 
-  dma_geom(item);
-  stage(0, 0, 0, (item % p.mtiles) * WM_CH);
-  win_geom(item);
+  stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   using st0 = std::integral_constant<int, 0>;
   using st1 = std::integral_constant<int, 1>;
-  typedef int wg_i2 __attribute__((ext_vector_type(2)));
+  chunk(0, std::true_type{}, st0{});
+  int kc = 1;
+  for (; kc + 1 < nchunks; kc += 2) {  // chunk pairs: odd, even
+    chunk(kc, std::false_type{}, st1{});
+    chunk(kc + 1, std::false_type{}, st0{});
+  }
+  if (kc < nchunks) chunk(kc, std::false_type{}, st1{});
+  // lane (lk, lj) of fragment f holds rows 4 lk + e = channel m0 + 16 f + 4 lk + e of tile lj
+  wg_floatx4 bv[2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) bv[f] = *reinterpret_cast<const wg_floatx4*>(wm_lds + 2 * SS + 16 * f + 4 * lk);
+  // stores without branches: 8-B row stores whose offsets past the output (invalid tiles, rows, channels,
+  // tiles without a second column) the buffer range check drops; when some lane's tile lacks its second
+  // column (the right edge of an odd-width plane; fast = false for the wave) also 4-B first-column stores
+  const bool fast = __builtin_amdgcn_ballot_w64(w.tok && !w.c1ok) == 0;
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, 0x7FFFFFF0, 0x00020000);
-  for (;;) {
-    nitem = item + nwx;
-    chunk(0, std::true_type{}, st0{});
-    int kc = 1;
-    for (; kc + 1 < nchunks; kc += 2) {  // chunk pairs: odd, even
-      chunk(kc, std::false_type{}, st1{});
-      chunk(kc + 1, std::false_type{}, st0{});
-    }
-    if (kc < nchunks) chunk(kc, std::false_type{}, st1{});
-    // ---- epilogue: lane (lk, lj) of fragment f holds rows 4 lk + e = channel m0 + 16 f + 4 lk + e of tile lj
-    wg_floatx4 bv[2];
+  typedef int wg_i2 __attribute__((ext_vector_type(2)));
+  // the output transform and bias of channels (e, e + 1) on packed f32 (acc[xi][f] holds e = 0 .. 3 in
+  // consecutive registers); the same adds in the same order as wg_store_t
 #pragma unroll
-    for (int f = 0; f < 2; ++f)
-      bv[f] = *reinterpret_cast<const wg_floatx4*>(wm_lds + 2 * SS + bslot * WM_CH + 16 * f + 4 * lk);
-    // stores without branches: 8-B row stores whose offsets past the output (invalid tiles, rows, channels,
-    // tiles without a second column) the buffer range check drops; when some lane's tile lacks its second
-    // column (the right edge of an odd-width plane; fast = false for the wave) also 4-B first-column stores
-    const bool fast = __builtin_amdgcn_ballot_w64(w.tok && !w.c1ok) == 0;
-    // the output transform and bias of channels (e, e + 1) on packed f32 (acc[xi][f] holds e = 0 .. 3 in
-    // consecutive registers); the same adds in the same order as wg_store_t
+  for (int f = 0; f < 2; ++f)
 #pragma unroll
-    for (int f = 0; f < 2; ++f)
+    for (int ep = 0; ep < 4; ep += 2) {
+      const int mp = m0 + 16 * f + 4 * lk + ep;
+      wg_f2 mx[16], y[4];
 #pragma unroll
-      for (int ep = 0; ep < 4; ep += 2) {
-        const int mp = m0 + 16 * f + 4 * lk + ep;
-        wg_f2 mx[16], y[4];
+      for (int xi = 0; xi < 16; ++xi) mx[xi] = ep == 0 ? acc[xi][f].xy : acc[xi][f].zw;
+      wg_output_transform_pk(mx, y);
+      const wg_f2 b2 = {bv[f][ep], bv[f][ep + 1]};
 #pragma unroll
-        for (int xi = 0; xi < 16; ++xi) mx[xi] = ep == 0 ? acc[xi][f].xy : acc[xi][f].zw;
-        wg_output_transform_pk(mx, y);
-        const wg_f2 b2 = {bv[f][ep], bv[f][ep + 1]};
+      for (int h = 0; h < 2; ++h) {
+        float o[4];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          float o[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            o[q] = (y[q] + b2)[h];
-            if constexpr (RELU) o[q] = fmaxf(o[q], 0.0f);
-          }
-          const bool mok = mp + h < p.M;
-          const int yo = (w.ybase + (mp + h) * p.y_ps) * 4;
-          const int oob = 0x7FFFFFF0;
-          const bool ok0 = w.tok && mok, ok1 = ok0 && w.r1ok;
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(wg_i2, (wg_f2){o[0], o[1]}), yr,
-                                                ok0 && w.c1ok ? yo : oob, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(wg_i2, (wg_f2){o[2], o[3]}), yr,
-                                                ok1 && w.c1ok ? yo + p.W * 4 : oob, 0, 0);
-          if (!fast) {  // tiles at the right edge of an odd-width plane: their first column only
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, o[0]), yr, ok0 && !w.c1ok ? yo : oob, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, o[2]), yr,
-                                                  ok1 && !w.c1ok ? yo + p.W * 4 : oob, 0, 0);
-          }
+        for (int q = 0; q < 4; ++q) {
+          o[q] = (y[q] + b2)[h];
+          if constexpr (RELU) o[q] = fmaxf(o[q], 0.0f);
+        }
+        const bool mok = mp + h < p.M;
+        const int yo = (w.ybase + (mp + h) * p.y_ps) * 4;
+        const int oob = 0x7FFFFFF0;
+        const bool ok0 = w.tok && mok, ok1 = ok0 && w.r1ok;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(wg_i2, (wg_f2){o[0], o[1]}), yr,
+                                              ok0 && w.c1ok ? yo : oob, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(wg_i2, (wg_f2){o[2], o[3]}), yr,
+                                              ok1 && w.c1ok ? yo + p.W * 4 : oob, 0, 0);
+        if (!fast) {  // tiles at the right edge of an odd-width plane: their first column only
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, o[0]), yr, ok0 && !w.c1ok ? yo : oob, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, o[2]), yr, ok1 && !w.c1ok ? yo + p.W * 4 : oob,
+                                                0, 0);
         }
       }
-    if (nitem >= r1) break;
-    item = nitem;
-    bslot ^= 1;
-    win_geom(item);  // its DMA geometry came with its first chunk's staging
-  }
+    }
 }
 
 // the LDS kernel's geometry; false when the layer does not fit it
@@ -804,7 +766,7 @@ static bool wm_geom(const ConvParams& p, WmGeom* g, size_t* lds, int* ndma) {
     tmax = std::max(tmax, wm_group_floats(gi * WM_TILES, T, g->TPI, g->TW, p.H, p.W));
   *ndma = (tmax + 255) / 256;
   g->CS = (WM_ZL + tmax + 5 + 31) / 64 * 64 + 32;  // + 1: odd channels' shift, + 4: the last window's overrun
-  *lds = (size_t)2 * WM_KC * (g->CS + 512) * 4 + 2 * WM_CH * 4;  // two stages + two bias slots
+  *lds = (size_t)2 * WM_KC * (g->CS + 512) * 4 + WM_CH * 4;  // two stages + the biases
   return *ndma <= 8 && *lds <= 160 * 1024;
 }
 
@@ -816,28 +778,7 @@ static void launch_wm_r(const ConvParams& p0, const WmGeom& g, size_t lds, hipSt
     static std::atomic<unsigned long long> raised{0};
     ore_raise_lds_once(raised, reinterpret_cast<const void*>(&conv_winol_kernel<NDMA, RELU>), 160 * 1024);
   }
-  // persistent grid (even chunk counts: the next item's chunk 0 lands in stage 0): the workgroups that fit
-  // at once (two per CU), counted once per device; odd chunk counts: one workgroup per item
-  const long long nitems = (long long)g.ntg * p.mtiles;
-  long long grid = nitems;
-  if ((p.C / WM_KC) % 2 == 0) {
-    static std::atomic<int> resident[64];
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    int cap = resident[dev & 63].load(std::memory_order_relaxed);
-    if (cap <= 0) {
-      int ncu = 256, per_cu = 0;
-      int v = 0;
-      if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_winol_kernel<NDMA, RELU>, 256, lds) != hipSuccess ||
-          per_cu < 1)
-        per_cu = 2;
-      cap = per_cu * ncu;
-      resident[dev & 63].store(cap, std::memory_order_relaxed);
-    }
-    grid = std::min<long long>(nitems, cap);
-  }
-  hipLaunchKernelGGL((conv_winol_kernel<NDMA, RELU>), dim3((unsigned)grid), dim3(256), lds, s, p, g);
+  hipLaunchKernelGGL((conv_winol_kernel<NDMA, RELU>), dim3((unsigned)(g.ntg * p.mtiles)), dim3(256), lds, s, p, g);
 }
 
 template <int NDMA>
