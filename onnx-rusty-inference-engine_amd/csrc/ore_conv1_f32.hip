@@ -221,7 +221,20 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
     c3f4 sacc = {0.0f, 0.0f, 0.0f, 0.0f};
     const int sk = 16 * wave + (lane & 15), slk = lane >> 4;
 
-    // per 32-channel fragment: conv tile (bias, Relu, 0 outside the conv plane), 3x3 max, NCHW stores
+    // SQ: the squeeze's 8 k-steps of fragment i: B = pooled (pixel sk, channel 4 t + lk) from pt, A = W[lj][32 i + 4 t + lk]
+    const int lj = lane & 15;
+    auto squeeze = [&](int i) __attribute__((always_inline)) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const float bq = pt[sk * C3_TS + 4 * t + slk];
+        const float aq = lj < sq.M ? aqv[i][t] : 0.0f;
+        sacc = __builtin_amdgcn_mfma_f32_16x16x4f32(aq, bq, sacc, 0, 0, 0);
+      }
+    };
+    // per 32-channel fragment: conv tile (bias, Relu, 0 outside the conv plane), 3x3 max, NCHW stores.  SQ:
+    // fragment i's squeeze k-steps run after fragment i + 1's conv-tile writes, before the barrier both
+    // need (ct's pool readers of fragment i and pt's squeeze readers are done at the barriers around
+    // them): two barriers per fragment instead of three (the squeeze's k order is unchanged)
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
 #pragma unroll
@@ -248,6 +261,9 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
           *reinterpret_cast<c3f4*>(ct + tpx[f] + ch) = o;
         }
       }
+      if constexpr (SQ) {
+        if (i > 0) squeeze(i - 1);
+      }
       __syncthreads();
       if (i == 0) store_window();  // every wave is past its K loop: the window is free
       // (pooled output, 4 channels) per task, 432 tasks (a one-round 8-channel variant with all 18
@@ -270,14 +286,7 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
           *reinterpret_cast<c3f4*>(pt + k * C3_TS + 4 * cg) = mx;
         }
         __syncthreads();
-        // 8 k-steps of 4 channels: B = pooled (pixel sk, channel 4 t + lk), A = W[lj][32 i + 4 t + lk]
-        const int lj = lane & 15;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const float bq = pt[sk * C3_TS + 4 * t + slk];
-          const float aq = lj < sq.M ? aqv[i][t] : 0.0f;
-          sacc = __builtin_amdgcn_mfma_f32_16x16x4f32(aq, bq, sacc, 0, 0, 0);
-        }
+        if (i + 1 == MF) squeeze(i);
       }
       for (int t = tid; !SQ && t < C3_PR * C3_PC * 8; t += 256) {
         const int cg = t / (C3_PR * C3_PC), pp = t - cg * (C3_PR * C3_PC);
@@ -301,7 +310,7 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
           }
         }
       }
-      if (i + 1 < MF) __syncthreads();  // the conv tile is rewritten by the next fragment
+      if (!SQ && i + 1 < MF) __syncthreads();  // the conv tile is rewritten by the next fragment
     }
     if constexpr (SQ) {  // squeeze output: bias + Relu, NCHW (rows 4 lk + e of pixel sk)
       const int aa = sk / C3_PC, bb = sk - aa * C3_PC, ph = ph0 + aa, pw = pw0 + bb;
