@@ -495,7 +495,6 @@ constexpr int WM_KC = 8;      // input channels per K chunk (2 k-steps of 4)
 constexpr int WM_TILES = 64;  // 2x2 tiles per workgroup (16 per wave)
 constexpr int WM_CH = 32;     // output channels per workgroup
 constexpr int WM_ZL = 8;      // zero floats at the start of a staged channel (rows outside the image)
-constexpr int WM_OOB = 0x7FFFFFF0;  // a DMA lane offset past any input (x_bytes < 2^31 - 16): the lane reads 0
 
 __device__ __forceinline__ void wm_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, int voffset, int soffset) {
   ore_lds_dma16(rsrc, lds_addr, voffset, soffset);
@@ -504,9 +503,7 @@ __device__ __forceinline__ void wm_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned l
 // geometry of the LDS kernel (host-computed)
 struct WmGeom {
   int TW, TPI;  // tiles per row / per image
-  int RS;       // LDS floats per staged input row: column -1, the W columns, column W (+1 for odd W) -- zeros
-                // at both ends, so windows need no column masks
-  int CS;       // LDS floats per staged channel: zero block + the longest row set + slack (= 32 mod 64)
+  int CS;       // LDS floats per staged channel: zero block + the longest run set + slack (= 32 mod 64)
   int ntg;      // tile groups of WM_TILES
 };
 
@@ -516,8 +513,8 @@ __host__ __device__ __forceinline__ void wm_rows(int img, int img0, int ty0, int
   *re = img == img1 ? min(H - 1, 2 * ty1 + 2) : H - 1;
 }
 
-// input rows staged per channel for the tile group starting at t0 (each image's rows)
-static int wm_group_rows(long long t0, long long T, int TPI, int TW, int H) {
+// floats staged per channel for the tile group starting at t0 (each image's run + 1, rounded up to 4)
+static int wm_group_floats(long long t0, long long T, int TPI, int TW, int H, int W) {
   const long long t1 = std::min(T, t0 + WM_TILES) - 1;
   const int img0 = (int)(t0 / TPI), ty0 = (int)(t0 % TPI) / TW;
   const int img1 = (int)(t1 / TPI), ty1 = (int)(t1 % TPI) / TW;
@@ -525,12 +522,12 @@ static int wm_group_rows(long long t0, long long T, int TPI, int TW, int H) {
   for (int i = img0; i <= img1; ++i) {
     int rs, re;
     wm_rows(i, img0, ty0, img1, ty1, H, &rs, &re);
-    total += re - rs + 1;
+    total += ((re - rs + 1) * W + 4) & ~3;  // one spare float: odd channels' shifted last element
   }
   return total;
 }
 
-template <bool RELU>
+template <int NDMA, bool RELU>  // NDMA: 256-float DMA pieces per staged channel (ceil(longest run set / 256))
 __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom g) {
   extern __shared__ __attribute__((aligned(16))) float wm_lds[];
   const int lane = threadIdx.x & 63;
@@ -558,63 +555,68 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
     wm_lds[2 * SS + (int)threadIdx.x - 128] = p.bias && m < p.M ? p.bias[m] : 0.0f;
   }
 
-  // ---- this lane's tile (lj of the wave's 16) and its image's first row inside the group's row set
+  // ---- this lane's tile (lj of the wave's 16) and the run layout of the group
   const int lk = lane >> 4, lj = lane & 15;
   int t = t0 + 16 * wave + lj;
   WgTile w;
   w.tok = t < T;
   if (!w.tok) t = T - 1;
   const int img = t / g.TPI, rem = t - img * g.TPI, ty = rem / g.TW, tx = rem - ty * g.TW;
-  int my_rb = 0, my_rs = 0;  // row-set index of this image's first staged row, and that row
-  for (int i = img0; i <= img; ++i) {
+  // DMA piece gi of a channel: floats [4 (64 gi + lane), +4) of the run set
+  int voff[NDMA];
+#pragma unroll
+  for (int gi = 0; gi < NDMA; ++gi) voff[gi] = -1;
+  int my_lb = 0, my_rs = 0;
+  int lb = 0;
+  for (int i = img0; i <= img1; ++i) {
     int rs, re;
     wm_rows(i, img0, ty0, img1, ty1, p.H, &rs, &re);
-    my_rs = rs;
-    if (i < img) my_rb += re - rs + 1;
+    const int len = (re - rs + 1) * p.W;
+#pragma unroll
+    for (int gi = 0; gi < NDMA; ++gi) {
+      const int k4 = 4 * (64 * gi + lane);
+      if (k4 >= lb && k4 <= lb + len) voff[gi] = (int)((i * p.x_nstride + (long long)rs * p.W + (k4 - lb)) * 4);
+    }
+    if (i == img) {
+      my_lb = lb;
+      my_rs = rs;
+    }
+    lb += (len + 4) & ~3;  // runs of len + 1 floats (odd channels land one float later), rounded to 4
   }
-  // window rows (floats from the channel's area; rows outside the image -> the zero block); staged column
-  // j + 1 holds input column j, so the window's first column 2 tx - 1 sits at 2 tx
+  // window rows (floats from the channel's area; rows outside the image -> the zero block)
   int aw[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int gr = 2 * ty - 1 + r;
-    // odd channels are staged one float later, so the two channels of a ds_read_b32 lane group (lk = 0,
-    // 1: CS = 0 mod 32 apart) use opposite bank parities
-    const int rel = ((unsigned)gr < (unsigned)p.H ? WM_ZL + (my_rb + gr - my_rs) * g.RS + 2 * tx : 0) + (lk & 1);
+    // odd channels are staged one float later (their DMA source starts one float early), so the two
+    // channels of a ds_read_b32 lane group (lk = 0, 1: CS = 0 mod 32 apart) use opposite bank parities
+    const int rel = ((unsigned)gr < (unsigned)p.H ? WM_ZL + my_lb + (gr - my_rs) * p.W + 2 * tx - 1 : 0) + (lk & 1);
     aw[r] = (lk * g.CS + rel) * 4;  // bytes, channel lk of a k-step
   }
+  const bool c0ok = tx > 0, c2ok = 2 * tx + 1 < p.W, c3ok = 2 * tx + 2 < p.W;
   w.ybase = img * (int)p.y_nstride + (2 * ty) * p.W + 2 * tx;
   w.c1ok = 2 * tx + 1 < p.W;
   w.r1ok = 2 * ty + 1 < p.H;
   const int au = (WM_KC * g.CS + lk * 512 + lj * 4) * 4;  // bytes: U[c = lk][quad 0][m = lj] of a k-step
 
-  // ---- DMA sources: wave w stages channels w and w + 4 of a chunk -- one 4-B DMA per input row, lane l
-  // of it column l - 1 (lanes 0 and W + 1 .. RS - 1 read 0: the row's zero ends; lanes >= RS idle), the
-  // row's start in the scalar offset -- and U pieces d = w + 4 v
+  // ---- DMA sources: wave w stages channels w and w + 4 of a chunk, and U pieces d = w + 4 v
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ur =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0, p.C * p.Mp * 16 * 4, 0x00020000);
-  const int xvo = lane >= 1 && lane <= p.W ? (lane - 1) * 4 : WM_OOB;
   const int uq = 2 * (wave & 1) + (lane >> 5);
   const int uoff = (uq * p.Mp + m0 + (lane & 31)) * 16;
   const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) float*)wm_lds;
   const int nchunks = p.C / WM_KC;
   auto stage = [&](int kc, int st) __attribute__((always_inline)) {
     const unsigned sb = lds0 + (unsigned)(st * SS) * 4;
-    if (lane < g.RS) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int cc = wave + 4 * h;
-        unsigned dst = sb + (unsigned)(cc * g.CS + WM_ZL + (cc & 1)) * 4;
-        const int cso = (kc * WM_KC + cc) * p.x_ps;
-        for (int i = img0; i <= img1; ++i) {
-          int rs, re;
-          wm_rows(i, img0, ty0, img1, ty1, p.H, &rs, &re);
-          for (int y = rs; y <= re; ++y, dst += g.RS * 4)
-            ore_lds_dma4(xr, dst, xvo, (int)((i * p.x_nstride + y * p.W + cso) * 4));
-        }
-      }
+    for (int h = 0; h < 2; ++h) {
+      const int cc = wave + 4 * h;
+      const int so = (kc * WM_KC + cc) * p.x_ps * 4 - 4 * (cc & 1);  // odd channels: one float early (>= 0)
+#pragma unroll
+      for (int gi = 0; gi < NDMA; ++gi)
+        if (voff[gi] >= 0) wm_dma16(xr, sb + (cc * g.CS + WM_ZL + 256 * gi) * 4, voff[gi], so);
     }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
@@ -640,7 +642,13 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
     return *reinterpret_cast<const wg_floatx4*>(lds_b + au + sto + q * 512 + f * 256);  // m = 16 f + lj
   };
   auto xform = [&](wg_f2 (&d)[4][2], wg_f2 (&v)[8]) __attribute__((always_inline)) {
-    wg_input_transform_pk(d, v);  // columns outside the image read the staged rows' zero ends
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      d[r][0][0] = c0ok ? d[r][0][0] : 0.0f;
+      d[r][1][0] = c2ok ? d[r][1][0] : 0.0f;
+      d[r][1][1] = c3ok ? d[r][1][1] : 0.0f;
+    }
+    wg_input_transform_pk(d, v);
   };
   // one chunk (two k-steps of 4 channels); FIRST: chunk 0, its first k-step starts the accumulators
   auto chunk = [&](int kc, auto first, auto stc) __attribute__((always_inline)) {
@@ -744,42 +752,58 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
 }
 
 // the LDS kernel's geometry; false when the layer does not fit it
-static bool wm_geom(const ConvParams& p, WmGeom* g, size_t* lds) {
+static bool wm_geom(const ConvParams& p, WmGeom* g, size_t* lds, int* ndma) {
   if (p.C % WM_KC != 0 || p.C <= 0 || p.H <= 0 || p.W <= 0) return false;
   g->TW = (p.W + 1) / 2;
   const int TH = (p.H + 1) / 2;
   g->TPI = g->TW * TH;
-  g->RS = (p.W + 2 + 1) & ~1;  // even: an odd W's last window reads column W + 1
   const long long T = (long long)p.N * g->TPI;
   g->ntg = (int)((T + WM_TILES - 1) / WM_TILES);
   // group starts repeat modulo TPI (period TPI / gcd(64, TPI)): every case is among the first TPI
-  int rmax = 0;
+  int tmax = 0;
   const long long ng = std::min<long long>(g->ntg, g->TPI);
-  for (long long gi = 0; gi < ng; ++gi) rmax = std::max(rmax, wm_group_rows(gi * WM_TILES, T, g->TPI, g->TW, p.H));
-  g->CS = (WM_ZL + rmax * g->RS + 1 + 31) / 64 * 64 + 32;  // + 1: odd channels' shift
+  for (long long gi = 0; gi < ng; ++gi)
+    tmax = std::max(tmax, wm_group_floats(gi * WM_TILES, T, g->TPI, g->TW, p.H, p.W));
+  *ndma = (tmax + 255) / 256;
+  g->CS = (WM_ZL + tmax + 5 + 31) / 64 * 64 + 32;  // + 1: odd channels' shift, + 4: the last window's overrun
   *lds = (size_t)2 * WM_KC * (g->CS + 512) * 4 + WM_CH * 4;  // two stages + the biases
-  return g->RS <= 64 && *lds <= 160 * 1024;
+  return *ndma <= 8 && *lds <= 160 * 1024;
 }
 
-template <bool RELU>
+template <int NDMA, bool RELU>
 static void launch_wm_r(const ConvParams& p0, const WmGeom& g, size_t lds, hipStream_t s) {
   ConvParams p = p0;
   p.mtiles = (p.M + WM_CH - 1) / WM_CH;
   if (lds > 64 * 1024) {  // above the default dynamic-LDS limit: raise it once per device
     static std::atomic<unsigned long long> raised{0};
-    ore_raise_lds_once(raised, reinterpret_cast<const void*>(&conv_winol_kernel<RELU>), 160 * 1024);
+    ore_raise_lds_once(raised, reinterpret_cast<const void*>(&conv_winol_kernel<NDMA, RELU>), 160 * 1024);
   }
-  hipLaunchKernelGGL((conv_winol_kernel<RELU>), dim3((unsigned)(g.ntg * p.mtiles)), dim3(256), lds, s, p, g);
+  hipLaunchKernelGGL((conv_winol_kernel<NDMA, RELU>), dim3((unsigned)(g.ntg * p.mtiles)), dim3(256), lds, s, p, g);
+}
+
+template <int NDMA>
+static void launch_wm(const ConvParams& p, const WmGeom& g, size_t lds, hipStream_t s) {
+  if (p.relu)
+    launch_wm_r<NDMA, true>(p, g, lds, s);
+  else
+    launch_wm_r<NDMA, false>(p, g, lds, s);
 }
 
 static void launch_winol(const ConvParams& p, hipStream_t s) {
   WmGeom g;
   size_t lds = 0;
-  if (!wm_geom(p, &g, &lds)) return;  // the caller checked conv_wino_eligible
-  if (p.relu)
-    launch_wm_r<true>(p, g, lds, s);
-  else
-    launch_wm_r<false>(p, g, lds, s);
+  int ndma = 0;
+  if (!wm_geom(p, &g, &lds, &ndma)) return;  // the caller checked conv_wino_eligible
+  switch (ndma) {
+    case 1: launch_wm<1>(p, g, lds, s); break;
+    case 2: launch_wm<2>(p, g, lds, s); break;
+    case 3: launch_wm<3>(p, g, lds, s); break;
+    case 4: launch_wm<4>(p, g, lds, s); break;
+    case 5: launch_wm<5>(p, g, lds, s); break;
+    case 6: launch_wm<6>(p, g, lds, s); break;
+    case 7: launch_wm<7>(p, g, lds, s); break;
+    default: launch_wm<8>(p, g, lds, s); break;
+  }
 }
 
 // Winograd tiles (ConvPlan cfg = WINO_TILE_BASE + t): shape (32: 32x32x2, 16: 16x16x4), channels and
@@ -797,7 +821,8 @@ bool conv_wino_eligible(const ConvParams& p, int tile) {
   if (tile == 4) {
     WmGeom g;
     size_t lds;
-    return conv_wino_geometry(p.C, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.H, p.W, p.Ho, p.Wo) && wm_geom(p, &g, &lds) &&
+    int ndma;
+    return conv_wino_geometry(p.C, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.H, p.W, p.Ho, p.Wo) && wm_geom(p, &g, &lds, &ndma) &&
            p.x_bytes > 0 && p.x_bytes < (1LL << 31) - (1LL << 21) && (reinterpret_cast<uintptr_t>(p.x) & 3) == 0 &&
            p.Mp % 64 == 0 && (long long)p.C * p.Mp * 64 < (1LL << 31) &&
            (long long)p.N * ((p.H + 1) / 2) * ((p.W + 1) / 2) < (1LL << 30) &&

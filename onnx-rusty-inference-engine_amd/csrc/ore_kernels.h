@@ -84,22 +84,6 @@ __device__ __forceinline__ void ore_lds_dma16(__amdgpu_buffer_rsrc_t rsrc, unsig
       : "memory");
 }
 
-// 4-B LDS-DMA (buffer_load_dword ... lds): lane i's 4 bytes from rsrc + voffset + soffset land at LDS byte
-// lds_addr + 4 i; otherwise as ore_lds_dma16 (an out-of-range lane writes 0)
-__device__ __forceinline__ void ore_lds_dma4(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, int voffset, int soffset) {
-  int m0save;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dword %2, %3, %4 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(m0save)
-      : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voffset), "s"(rsrc),
-        "s"(__builtin_amdgcn_readfirstlane(soffset))
-      : "memory");
-}
-
 struct ConvParams {
   const float* x;      // input  [N][C][H][W], image stride x_nstride
   const float* wp;     // packed weights Wp[Kp][Mp] (launch_pack_weights)
