@@ -91,8 +91,9 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
   const int ne1 = KS1 > 0 ? p.E1 / PS_CH : 0;  // recomputed chunks
   const int bpx = PS_ROWS * p.W;
   float sb[FA1][KA1];
-  int e1_off[FA1];  // in_s offset of the lane's pixel of fragment i (channel 0), -1: past the band
-  bool e1_rin[FA1];
+  // in_s offset of the lane's pixel of fragment i (channel 0); -1: past the band or on a row outside the
+  // image (never written: the staged rows start zeroed, and the recomputed chunks come first)
+  int e1_off[FA1];
   if constexpr (KS1 > 0) {
     const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(p.s + (long long)img * p.s_nstride), (short)0, 4 * KS1 * p.s_ps * 4, 0x00020000);
@@ -105,8 +106,7 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
       for (int t = 0; t < KS1; ++t)
         sb[i][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                  sr, in ? ((4 * t + lk) * p.s_ps + g) * 4 : (int)0x80000000, 0, 0));
-      e1_off[i] = px < bpx ? r * PS_RS + PS_LC + (px - r * p.W) : -1;
-      e1_rin[i] = (unsigned)(ih0 + r) < (unsigned)p.H;
+      e1_off[i] = px < bpx && (unsigned)(ih0 + r) < (unsigned)p.H ? r * PS_RS + PS_LC + (px - r * p.W) : -1;
     }
     for (int i = tid; i < p.E1; i += 256) b1_s[i] = p.b1[i];
   }
@@ -114,22 +114,25 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
   // this thread's 16-B groups q = tid + 256 u: (channel, row, group j) -> byte offset in the image
   // minus the chunk's channel offset (rows outside the image: past the records, 0), LDS float offset
   // and the mask of the group's elements inside the row (a group may run into the next row)
-  const int nq = (p.W + 3) / 4, nld = PS_CH * PS_ROWS * nq;
+  // (computed where the loaded chunks begin: with e1 recomputed they are not live during its chunks)
   int qo[PS_NQ], qs[PS_NQ];
   unsigned qm[PS_NQ];
+  auto group_geom = [&]() __attribute__((always_inline)) {
+    const int nq = (p.W + 3) / 4, nld = PS_CH * PS_ROWS * nq;
 #pragma unroll
-  for (int u = 0; u < PS_NQ; ++u) {
-    const int q = tid + 256 * u;
-    const int c = q / (PS_ROWS * nq), rc = q - c * (PS_ROWS * nq), r = rc / nq, j = rc - r * nq;
-    const int ih = ih0 + r;
-    const bool rin = (unsigned)ih < (unsigned)p.H;
-    qo[u] = q < nld ? (rin ? (c * p.x_ps + ih * p.W + 4 * j) * 4 : (int)0x80000000) : -1;
-    qs[u] = (c * PS_ROWS + r) * PS_RS + PS_LC + 4 * j;
-    unsigned mk = 0;
+    for (int u = 0; u < PS_NQ; ++u) {
+      const int q = tid + 256 * u;
+      const int c = q / (PS_ROWS * nq), rc = q - c * (PS_ROWS * nq), r = rc / nq, j = rc - r * nq;
+      const int ih = ih0 + r;
+      const bool rin = (unsigned)ih < (unsigned)p.H;
+      qo[u] = q < nld ? (rin ? (c * p.x_ps + ih * p.W + 4 * j) * 4 : (int)0x80000000) : -1;
+      qs[u] = (c * PS_ROWS + r) * PS_RS + PS_LC + 4 * j;
+      unsigned mk = 0;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) mk |= (4 * j + e < p.W ? 1u : 0u) << e;
-    qm[u] = mk;
-  }
+      for (int e = 0; e < 4; ++e) mk |= (4 * j + e < p.W ? 1u : 0u) << e;
+      qm[u] = mk;
+    }
+  };
   ps4 xv[PS_NQ];
   auto load_chunk = [&](int c0) __attribute__((always_inline)) {
 #pragma unroll
@@ -153,8 +156,9 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
       dst[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                              wr, ((ci * PS_CH + 4 * t + lk) * p.Mp + m0 + lj) * 4, 0, 0));
   };
-  // e1's A values of a recomputed chunk (k = 4 t + lk, row 16 ci + lj of the K-major packing), one chunk ahead
-  float a1cur[KA1], a1nxt[KA1];
+  // e1's A values of a recomputed chunk (k = 4 t + lk, row 16 ci + lj of the K-major packing), reloaded with
+  // the next chunk's as soon as this chunk's e1 MFMAs have issued
+  float a1cur[KA1];
   const __amdgpu_buffer_rsrc_t w1r = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(KS1 > 0 ? p.w1 : p.wp), (short)0, 4 * KS1 * p.w1_Mp * 4, 0x00020000);
   auto load_a1 = [&](float (&dst)[KA1], int ci) __attribute__((always_inline)) {
@@ -164,14 +168,17 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
                                              w1r, ((4 * t + lk) * p.w1_Mp + PS_CH * ci + lj) * 4, 0, 0));
   };
   load_a(acur, 0);
-  if (ne1 > 0)
+  if (ne1 > 0) {
     load_a1(a1cur, 0);
-  else
+  } else {
+    group_geom();
     load_chunk(0);
-  // one chunk; RC: a recomputed e1 chunk (the two kinds run as two loops, so e1's B registers and the
-  // loaded chunks' staging registers are never live together)
-  auto chunk = [&](int ci, auto rc) __attribute__((always_inline)) {
-    constexpr bool RC = decltype(rc)::value;
+  }
+  // one chunk; RC: a recomputed e1 chunk, TR: the last of them (it starts the loaded chunks' loads).  The
+  // kinds run as separate loops and the last recomputed chunk is peeled, so e1's B registers and the
+  // loaded chunks' staging registers are never live together (two more waves per SIMD)
+  auto chunk = [&](int ci, auto rc, auto tr) __attribute__((always_inline)) {
+    constexpr bool RC = decltype(rc)::value, TR = decltype(tr)::value;
     __syncthreads();  // the previous chunk's staged rows are pooled
     if constexpr (RC) {
       // e1 channels 16 ci + 4 lk + e at the wave's band pixels: the 1x1 conv, bias, Relu -> staged rows
@@ -182,6 +189,7 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
       for (int t = 0; t < KA1; ++t)
 #pragma unroll
         for (int i = 0; i < FA1; ++i) a[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1cur[t], sb[i][t], a[i], 0, 0, 0);
+      if constexpr (!TR) load_a1(a1cur, ci + 1);
       float bb[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) bb[e] = b1_s[PS_CH * ci + 4 * lk + e];
@@ -192,7 +200,7 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
         for (int e = 0; e < 4; ++e) {
           float v = a[i][e] + bb[e];
           v = fmaxf(v, 0.0f);
-          in_s[(4 * lk + e) * PS_ROWS * PS_RS + e1_off[i]] = e1_rin[i] ? v : 0.0f;
+          in_s[(4 * lk + e) * PS_ROWS * PS_RS + e1_off[i]] = v;
         }
       }
     } else {
@@ -207,10 +215,10 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
     }
     __syncthreads();
     if (ci + 1 < nch) {  // in flight during this chunk
-      if (ci + 1 >= ne1)
+      if constexpr (!RC || TR) {
+        if constexpr (TR) group_geom();
         load_chunk((ci + 1) * PS_CH);
-      else
-        load_a1(a1nxt, ci + 1);
+      }
       load_a(anxt, ci + 1);
     }
     // pooled maxima: channels x PS_PR rows x PS_RW columns (columns >= Wp: column 0's value, unused)
@@ -235,15 +243,13 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
     }
 #pragma unroll
     for (int t = 0; t < KS; ++t) acur[t] = anxt[t];
-    if (RC && ci + 1 < ne1) {
-#pragma unroll
-      for (int t = 0; t < KA1; ++t) a1cur[t] = a1nxt[t];
-    }
   };
   int ci = 0;
-  if constexpr (KS1 > 0)
-    for (; ci < ne1; ++ci) chunk(ci, std::true_type{});
-  for (; ci < nch; ++ci) chunk(ci, std::false_type{});
+  if constexpr (KS1 > 0) {
+    for (; ci + 1 < ne1; ++ci) chunk(ci, std::true_type{}, std::false_type{});
+    chunk(ci++, std::true_type{}, std::true_type{});
+  }
+  for (; ci < nch; ++ci) chunk(ci, std::false_type{}, std::false_type{});
   // bias + Relu, NCHW stores: channel m0 + 4 lk + e, pooled pixel (pr0 + n / NF, 16 (n % NF) + lj)
   if (m0 >= p.M) return;
 #pragma unroll
