@@ -13,9 +13,10 @@ import sys
 
 CLASSES = [("conv (f32 MFMA)", ("conv_gemm_kernel", "conv_stream_kernel", "conv_stream1x1_persist_kernel", "fire_kernel", "conv_pool_stream_kernel",
                                 "conv_wino32_kernel", "conv_wino16_kernel", "conv_winol_kernel", "fire_wino_kernel",
-                                "conv_win_pool_f32_kernel", "fire_pool_kernel", "pool_conv1x1_f32_kernel")),
+                                "conv_win_pool_f32_kernel", "fire_pool_kernel", "pool_conv1x1_f32_kernel",
+                                "conv1x1_gap_f32_kernel")),
            ("conv (f16 MFMA)", ("conv_f16_kernel", "conv_f16_dma_kernel", "conv_f16_epool", "fire_f16_kernel",
-                                "fire_pool_f16_kernel", "conv_pair_pool_f16_kernel")),
+                                "fire_pool_f16_kernel", "conv_pair_pool_f16_kernel", "conv1x1_gap_f16_kernel")),
            ("conv (window)", "conv_win_kernel"), ("maxpool", "maxpool"), ("gap", ("gap_kernel", "gap_nhwc_kernel")),
            ("softmax", "softmax_kernel"), ("pack/ktab (load time)", "pack_"), ("ktab", "ktab_kernel")]
 
@@ -53,8 +54,16 @@ def main():
     if bench:
         b = bench
         r = b.get("roofline", {})
-        print(f"\nbench.py (HIP events, same run): conv per_launch_avg_us = {r.get('per_launch_avg_us')}, "
-              f"achieved {r.get('achieved')} {r.get('unit')} = {r.get('frac')} of {r.get('peak')}")
+        cc = r.get("conv_class", r)
+        print(f"\nbench.py (HIP events, same run): conv class per_launch_avg_us = {cc.get('per_launch_avg_us')}, "
+              f"achieved {cc.get('achieved')} {cc.get('unit', 'TFLOP/s')} = {cc.get('frac')} of {cc.get('peak')}")
+        if "launch_us" in r:  # round 5: the dominant launch, which the rocprof row of its kernel must agree with
+            print(f"bench.py dominant launch: {r.get('kernel')}: {r.get('launch_us')} us, achieved {r.get('achieved')} "
+                  f"{r.get('unit')} = {r.get('frac')} of {r.get('peak')}")
+            dom = [x for x in rows if "conv_win_pool_f32_kernel" in x["Name"] or "conv_pair_pool_f16_kernel" in x["Name"]]
+            for x in dom:
+                print(f"rocprofv3 row of that kernel: {int(x['Calls'])} calls, average {float(x['AverageNs']) / 1e3:.2f} us "
+                      f"({x['Name'][:90]})")
     print("\nper-kernel rows:")
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
         print(f"  {int(r['Calls']):6d} {float(r['AverageNs']) / 1e3:9.2f} us  {r['Name'][:110]}")
