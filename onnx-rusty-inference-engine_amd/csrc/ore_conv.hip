@@ -466,8 +466,11 @@ static void launch_conv_epool_cfg(const ConvParams& p0, hipStream_t s) {
 
 void launch_conv_epool(const ConvParams& p, hipStream_t s) {
   int v = p.ep_variant;
-  if (p.sq1) {  // the fused squeeze exists in the window kernel only
-    if (p.wc1 && conv_win_pool_f32_eligible(p, p.sq1)) {
+  if (p.sq1) {  // the fused squeeze: the band walker (variant 8) or the window kernel
+    if (v == EPOOL_BAND_VARIANT && p.wc1 && conv_band_pool_f32_eligible(p, p.sq1)) {
+      launch_conv_band_pool_f32(p, p.wc1, *p.sq1, s);
+      last_conv_tile = EPOOL_BAND_TILE;
+    } else if (p.wc1 && conv_win_pool_f32_eligible(p, p.sq1)) {
       launch_conv_win_pool_f32(p, p.wc1, p.sq1, s);
       last_conv_tile = EPOOL_WIN_TILE;
     } else {

@@ -376,7 +376,293 @@ static bool c3_launch_r(const ConvParams& p, const float* wc, const C1SqueezeF32
   return in ? c3_launch<MF, C, SQ, false, true>(p, wc, sq, s) : c3_launch<MF, C, SQ, false, false>(p, wc, sq, s);
 }
 
+// ---- variant 8: the band walker (conv1 + pool1 + the fused squeeze, no conv output computed twice) ----
+//
+// The window kernel above recomputes the 13 x 19 patch's halo: 256 MFMA columns per 54 pooled outputs,
+// 16 % above the 220 conv outputs they need.  Here a workgroup (8 waves, one per CU: 153 KB of LDS)
+// owns a band of pooled rows of one image and walks its conv rows row-major in steps of 256 column
+// PAIRS (each conv row padded to an even number of columns, 55 pairs for conv1's 109): lane lr of wave
+// w computes the pair's two columns as its two 32-pixel MFMA fragments, so
+//   * the step's input rows [2 r_lo, 2 r_lo + 17) x 224 x 3 sit in LDS (float4 loads one step ahead,
+//     stored after the step's MFMAs) and the K loop is the window kernel's (per-lane base registers,
+//     compile-time k offsets, A from L2);
+//   * pooling: after bias + Relu (one v_med3_i32 on the bits: negatives and out-of-plane columns -> +0),
+//     the lane's pooled column j takes max(col 2j, 2j + 1, 2j + 2) -- the third from lane lr + 1 by DPP
+//     wave_shl:1 -- into the pooled cells (row (cr + pt) / 2, and the one above for even rows) by
+//     ds_max_u32 (Relu outputs are >= +0: their bits order like the values, and a max is exact in any
+//     order); lane 0 hands its first column to the previous pair by ds_max (the previous lane sits in
+//     another wave).  Invalid targets go to a per-lane dummy cell (ring slot 4);
+//   * pooled rows live in a 4-slot LDS ring [96][5][56] (at most 4 are open while a step touches <= 6
+//     conv rows); after each step the completed rows are squeezed (16x16x4 f32 MFMA, channel-ascending,
+//     the window kernel's chain), stored NCHW and their cells cleared by the lane that read them.
+// Conv outputs are the same k-ordered chains and pooled values the max of the same nine values as the
+// window kernel: bit-identical to it (tests/test_model_gpu.py::test_conv1_band_bit_identical).
+constexpr int CB_RW = 224;                 // LDS window row stride (floats): inputs up to 224 wide
+constexpr int CB_WR = 17;                  // window rows: <= 6 conv rows per step (2 * 5 + 7)
+constexpr int CB_PLANE = CB_WR * CB_RW;    // one channel of the window
+constexpr int CB_C = 3, CB_NV = CB_C * CB_WR * (CB_RW / 4);  // float4s of the window (2856)
+constexpr int CB_NU = (CB_NV + 511) / 512;                   // per thread (6)
+constexpr int CB_RPW = 56;                 // ring row (pooled columns)
+constexpr int CB_CS = 5 * CB_RPW;          // ring channel stride: 4 row slots + the dummy slot (= 8 mod 16:
+                                           // the lane halves' channels 4 apart fall on other banks)
+constexpr int CB_LDS = (3 * CB_PLANE + 96 * CB_CS + 96 + 16) * 4;
+constexpr int CB_OOB = 0x40000000;
+
+struct CBGeo {
+  static constexpr int KH = 7, KW = 7, K = CB_C * 49, KS = (K + 1) / 2, KQ = (K + 7) / 8;
+  static constexpr int koff(int k) { return (k / 49) * CB_PLANE + ((k / 7) % 7) * CB_RW + k % 7; }
+  static constexpr int kind(int k) {
+    return k + 1 >= K ? 3 : (k % KW) < KW - 1 ? 0 : ((k / KW) % KH) < KH - 1 ? 1 : 2;
+  }
+};
+
+__device__ __forceinline__ void cb_max(char* base, int off, unsigned v) {
+  __hip_atomic_fetch_max(reinterpret_cast<unsigned*>(base + off), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__global__ __launch_bounds__(512, 1) void conv_band_pool_f32_kernel(ConvParams p, const float* __restrict__ wc,
+                                                                    C1SqueezeF32 sq, int nb) {
+  using G = CBGeo;
+  constexpr int MF = 3;
+  extern __shared__ __attribute__((aligned(16))) float cbs[];
+  float* win = cbs;                        // [3][17][224]
+  float* ring = cbs + 3 * CB_PLANE;        // [96][5][56]
+  float* sbias = ring + 96 * CB_CS;        // [96]
+  float* qbias = sbias + 96;               // [16]
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int q = tid; q < 96; q += 512) sbias[q] = (p.bias && q < p.M) ? p.bias[q] : 0.0f;
+  for (int q = tid; q < 16; q += 512) qbias[q] = q < sq.M ? sq.bias[q] : 0.0f;
+  for (int q = tid; q < 96 * CB_CS; q += 512) ring[q] = 0.0f;
+  float aqv[MF][8];  // the squeeze's A values of this lane (W[lj][32 i + 4 t + lk])
+  {
+    const int lj = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) aqv[i][t] = lj < sq.M ? sq.w[lj * p.M + 32 * i + 4 * t + lk] : 0.0f;
+  }
+  // this thread's window float4s e = tid + 512 u: (channel c, row r, float4 j4); global byte offset from
+  // the step's first input row (past the row's width: CB_OOB, which reads 0), LDS float index
+  int wg[CB_NU], wl[CB_NU];
+#pragma unroll
+  for (int u = 0; u < CB_NU; ++u) {
+    const int e = tid + 512 * u, c = e / (CB_WR * 56), rem = e - c * (CB_WR * 56), r = rem / 56, j4 = rem - r * 56;
+    const bool ok = e < CB_NV && 4 * j4 < p.W;
+    wg[u] = ok ? (c * p.x_ps + r * p.W + 4 * j4) * 4 : CB_OOB;
+    wl[u] = e < CB_NV ? c * CB_PLANE + r * CB_RW + 4 * j4 : -1;
+  }
+  c3f4 xv[CB_NU];
+  const char* winb = reinterpret_cast<const char*>(win);
+  char* ringb = reinterpret_cast<char*>(ring);
+  const int Mp32 = MF * 32;
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wc), (short)0, G::KQ * Mp32 * 32, 0x00020000);
+  const int aoff = (lr * 2 + h) * 16;
+  const int HP = (p.Wo + p.ep_pl + 1) >> 1;  // column pairs per conv row
+  const int units = p.N * nb;
+  const int hb = h * 4 * CB_CS * 4;          // the lane half's first channel (rows 4 h + 0..3 of each 8)
+  const int dummy = hb + (4 * CB_RPW + lr) * 4;
+
+  for (int unit = blockIdx.x; unit < units; unit += gridDim.x) {
+    const int img = unit / nb, band = unit - img * nb;
+    const int pb0 = band * p.ep_Ho / nb, pb1 = (band + 1) * p.ep_Ho / nb;
+    const int cr0 = max(0, 2 * pb0 - p.ep_pt), cr1 = min(p.Ho, 2 * pb1 - p.ep_pt + 1);
+    const int npairs = (cr1 - cr0) * HP, nsteps = (npairs + 255) >> 8;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(p.x + (long long)img * p.x_nstride), (short)0, CB_C * p.x_ps * 4, 0x00020000);
+    auto load_window = [&](int s) __attribute__((always_inline)) {
+      const int so = 2 * (cr0 + (s << 8) / HP) * p.W * 4;
+#pragma unroll
+      for (int u = 0; u < CB_NU; ++u)
+        xv[u] = __builtin_bit_cast(c3f4, __builtin_amdgcn_raw_buffer_load_b128(rs, wg[u], so, 0));
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto store_window = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < CB_NU; ++u)
+        if (wl[u] >= 0) *reinterpret_cast<c3f4*>(win + wl[u]) = xv[u];
+    };
+    load_window(0);
+    store_window();
+    int sq_lo = pb0;
+    for (int s = 0; s < nsteps; ++s) {
+      const int r_lo = cr0 + (s << 8) / HP;
+      __syncthreads();  // step s's window is in LDS; the previous squeeze's readers and clears are done
+      if (s + 1 < nsteps) load_window(s + 1);
+
+      // the lane's pair: conv row cr, columns 2 j - pl + f
+      const int P = (s << 8) + 32 * wave + lr;
+      const bool pv = P < npairs;
+      const int prow = P / HP, j = P - prow * HP, cr = cr0 + prow;
+      int bk0[2], bk1[2], bk2[2], bk3[2], top[2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        const int col = 2 * j - p.ep_pl + f;
+        const bool ok = pv && col >= 0 && col < p.Wo;
+        const int base = ok ? 2 * (cr - r_lo) * CB_RW + 2 * col : 0;
+        constexpr int d0 = 1, d1 = CB_RW - (G::KW - 1), d2 = CB_PLANE - (G::KH - 1) * CB_RW - (G::KW - 1);
+        bk0[f] = (base + (h ? d0 : 0)) * 4;
+        bk1[f] = (base + (h ? d1 : 0)) * 4;
+        bk2[f] = (base + (h ? d2 : 0)) * 4;
+        bk3[f] = base * 4;
+        top[f] = ok ? 0x7fffffff : 0;
+      }
+
+      c3f16 acc[MF][2];
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][f][e] = 0.0f;
+      c3f4 a[2][MF];
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+          a[g][i] = __builtin_bit_cast(c3f4, __builtin_amdgcn_raw_buffer_load_b128(wr, aoff, ((g * Mp32 + 32 * i) * 2) * 16, 0));
+      auto bread = [&](int f, int jj) __attribute__((always_inline)) {
+        const int k0 = 2 * jj, kd = G::kind(k0), ko = G::koff(k0) * 4;
+        const int bb = kd == 0 ? bk0[f] : kd == 1 ? bk1[f] : kd == 2 ? bk2[f] : bk3[f];
+        return *reinterpret_cast<const float*>(winb + bb + ko);
+      };
+      float bn[2] = {bread(0, 0), bread(1, 0)};
+#pragma unroll
+      for (int jj = 0; jj < G::KS; ++jj) {
+        const int q = jj >> 2, ii = jj & 3;
+        const float b[2] = {bn[0], bn[1]};
+        if (jj + 1 < G::KS) {
+          bn[0] = bread(0, jj + 1);
+          bn[1] = bread(1, jj + 1);
+        }
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+          for (int f = 0; f < 2; ++f)
+            acc[i][f] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q & 1][i][ii], b[f], acc[i][f], 0, 0, 0);
+        if (ii == 3 && q + 2 < G::KQ) {
+#pragma unroll
+          for (int i = 0; i < MF; ++i)
+            a[q & 1][i] = __builtin_bit_cast(
+                c3f4, __builtin_amdgcn_raw_buffer_load_b128(wr, aoff, (((q + 2) * Mp32 + 32 * i) * 2) * 16, 0));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+
+      // pooled cells of the pair (row pa = (cr + pt) / 2 and, for even cr + pt, pa - 1; column j), and
+      // of lane 0's first column (column j - 1)
+      const int ap = cr + p.ep_pt, pa = ap >> 1;
+      const bool rA = pv && pa >= pb0 && pa < pb1, rB = pv && !(ap & 1) && pa - 1 >= pb0 && pa - 1 < pb1;
+      const int cA = ((pa & 3) * CB_RPW) * 4 + hb, cB = (((pa - 1) & 3) * CB_RPW) * 4 + hb;
+      const bool jok = j < p.ep_Wo, bok = lr == 0 && j > 0 && j - 1 < p.ep_Wo;
+      const int oA = rA && jok ? cA + j * 4 : dummy, oB = rB && jok ? cB + j * 4 : dummy;
+      const int qA = rA && bok ? cA + (j - 1) * 4 : dummy, qB = rB && bok ? cB + (j - 1) * 4 : dummy;
+      const bool nbok = lr < 31 && j + 1 < HP;  // the next column pair: this wave's lane lr + 1, same row
+      unsigned first[MF][16];
+#pragma unroll
+      for (int i = 0; i < MF; ++i) {
+        char* rb = ringb + 32 * i * CB_CS * 4;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const c3f4 sb = *reinterpret_cast<const c3f4*>(sbias + 32 * i + 8 * g + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float f0 = acc[i][0][4 * g + e] + sb[e], f1 = acc[i][1][4 * g + e] + sb[e];
+            // Relu and the out-of-plane zero on the bits: median(b, 0, top) (negative floats are
+            // negative ints -> +0; top = 0 for a column outside the conv plane)
+            const int b0 = max(0, min(__builtin_bit_cast(int, f0), top[0]));
+            const int b1 = max(0, min(__builtin_bit_cast(int, f1), top[1]));
+            int nbv = __builtin_amdgcn_update_dpp(0, b0, 0x130, 0xf, 0xf, true);  // wave_shl:1: lane l + 1's b0
+            nbv = nbok ? nbv : 0;
+            const unsigned m = (unsigned)max(max(b0, b1), nbv);
+            first[i][4 * g + e] = (unsigned)b0;
+            const int off = (8 * g + e) * CB_CS * 4;
+            cb_max(rb, oA + off, m);
+            cb_max(rb, oB + off, m);
+          }
+        }
+      }
+      if (lr == 0) {
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          char* rb = ringb + 32 * i * CB_CS * 4;
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int off = (8 * g + e) * CB_CS * 4;
+              cb_max(rb, qA + off, first[i][4 * g + e]);
+              cb_max(rb, qB + off, first[i][4 * g + e]);
+            }
+        }
+      }
+      __syncthreads();  // every pooled contribution of step s is in the ring; the window is free
+
+      // the pooled rows completed by step s: squeeze (16 pooled columns per task), store, clear
+      const int rdone = s + 1 == nsteps ? p.Ho : cr0 + ((s + 1) << 8) / HP;
+      int sq_hi = sq_lo;
+      while (sq_hi < pb1 && min(2 * sq_hi - p.ep_pt + 2, p.Ho - 1) < rdone) ++sq_hi;
+      const int ng = (p.ep_Wo + 15) >> 4, ntask = (sq_hi - sq_lo) * ng;
+      const int lj = lane & 15, slk = lane >> 4;
+      for (int t = wave; t < ntask; t += 8) {
+        const int pr = sq_lo + t / ng, pc = 16 * (t - (t / ng) * ng) + lj;
+        const bool pok = pc < p.ep_Wo;
+        float* cell = ring + slk * CB_CS + (pok ? (pr & 3) * CB_RPW + pc : 4 * CB_RPW + 32 + lj);
+        c3f4 sacc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+          for (int tt = 0; tt < 8; ++tt) {
+            const float bq = cell[(32 * i + 4 * tt) * CB_CS];
+            sacc = __builtin_amdgcn_mfma_f32_16x16x4f32(aqv[i][tt], bq, sacc, 0, 0, 0);
+          }
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+          for (int tt = 0; tt < 8; ++tt) cell[(32 * i + 4 * tt) * CB_CS] = 0.0f;
+        if (pok) {
+          float* yq = sq.y + (long long)img * sq.y_nstride + pr * p.ep_Wo + pc;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int m = 4 * slk + e;
+            if (m < sq.M) yq[(long long)m * sq.y_ps] = fmaxf(sacc[e] + qbias[m], 0.0f);
+          }
+        }
+      }
+      sq_lo = sq_hi;
+      if (s + 1 < nsteps) store_window();
+    }
+    __syncthreads();  // the unit's last squeeze is done before the next unit's window and ring writes
+  }
+}
+
 }  // namespace
+
+bool conv_band_pool_f32_eligible(const ConvParams& p, const C1SqueezeF32* sq) {
+  const int HP = (p.Wo + p.ep_pl + 1) / 2;
+  return sq && sq->M >= 1 && sq->M <= 16 && sq->w && sq->bias && sq->y && sq->y_ps >= p.ep_Ho * p.ep_Wo &&
+         p.relu && p.C == 3 && p.M > 64 && p.M <= 96 && p.kh == 7 && p.kw == 7 && p.sh == 2 && p.sw == 2 &&
+         p.pt == 0 && p.pl == 0 && p.W <= CB_RW && p.W % 4 == 0 && p.x_ps % 4 == 0 && p.x_nstride % 4 == 0 &&
+         p.x_ps >= p.H * p.W && HP >= 52 && p.ep_Wo <= CB_RPW && p.ep_Ho >= 1 && p.ep_pl <= 1 && p.ep_pt <= 1 &&
+         (long long)3 * p.x_ps * 4 < (1LL << 30);
+}
+
+void launch_conv_band_pool_f32(const ConvParams& p, const float* wc, const C1SqueezeF32& sq, hipStream_t s) {
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
+  }
+  static std::atomic<unsigned long long> raised{0};
+  ore_raise_lds_once(raised, reinterpret_cast<const void*>(&conv_band_pool_f32_kernel), CB_LDS);
+  // bands of pooled rows per image: enough workgroups for one per CU (>= 4 pooled rows per band)
+  int nb = 1;
+  if ((long long)p.N < ncu) nb = std::max(1, std::min<int>((ncu + p.N - 1) / p.N, p.ep_Ho / 4));
+  const long long units = (long long)p.N * nb;
+  const long long grid = std::max<long long>(1, std::min<long long>(units, ncu));
+  hipLaunchKernelGGL(conv_band_pool_f32_kernel, dim3((unsigned)grid), dim3(512), CB_LDS, s, p, wc, sq, nb);
+}
 
 size_t c1_f32_pack_bytes(int M, int K) { return size_t((K + 7) / 8) * size_t((M + 31) / 32 * 32) * 32; }
 

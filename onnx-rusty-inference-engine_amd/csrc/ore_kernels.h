@@ -344,7 +344,7 @@ constexpr int EPOOL_TILE_BASE = 21;
 // its input window in LDS, weights packed by launch_pack_c1_f32 (ConvPlan::wc1); reported as tile
 // EPOOL_WIN_TILE (after the Winograd / fused-f16 tile ids: ore.Model.TILE_NAMES "epool window f32")
 constexpr int EPOOL_WIN_VARIANT = 7, EPOOL_WIN_TILE = 44;
-inline int epool_tile_id(int variant) { return variant == EPOOL_WIN_VARIANT ? EPOOL_WIN_TILE : EPOOL_TILE_BASE + variant; }
+
 // the pooled f32 fire module (fire_pool_kernel): ore.Model.TILE_NAMES "fire pool f32"
 constexpr int FIRE_POOL_TILE = 45;
 // sq: the pooled map's only consumer, a 1x1 conv + Relu with <= 16 channels (ONNX weights [M][K]),
@@ -359,6 +359,15 @@ struct C1SqueezeF32 {
 };
 bool conv_win_pool_f32_eligible(const ConvParams& p, const C1SqueezeF32* sq = nullptr);
 void launch_conv_win_pool_f32(const ConvParams& p, const float* wc, const C1SqueezeF32* sq, hipStream_t s);
+// variant 8 (ore_conv1_f32.hip): the fused first conv + pool + squeeze walking bands of conv rows (no
+// recomputed halo; 7x7 / stride 2, C = 3, 64 < M <= 96, inputs <= 224 wide); tile EPOOL_BAND_TILE
+// ("epool band f32"), an autotune candidate beside the window kernel for the fused squeeze
+constexpr int EPOOL_BAND_VARIANT = 8, EPOOL_BAND_TILE = 51;
+bool conv_band_pool_f32_eligible(const ConvParams& p, const C1SqueezeF32* sq);
+void launch_conv_band_pool_f32(const ConvParams& p, const float* wc, const C1SqueezeF32& sq, hipStream_t s);
+inline int epool_tile_id(int variant) {
+  return variant == EPOOL_WIN_VARIANT ? EPOOL_WIN_TILE : variant == EPOOL_BAND_VARIANT ? EPOOL_BAND_TILE : EPOOL_TILE_BASE + variant;
+}
 size_t c1_f32_pack_bytes(int M, int K);
 void launch_pack_c1_f32(const float* w, int M, int K, float* out, hipStream_t s);
 bool conv_pool_stream_eligible(const ConvParams& p, int variant);

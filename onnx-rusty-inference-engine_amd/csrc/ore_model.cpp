@@ -1012,7 +1012,7 @@ struct Planner {
         cv.sq_w = m->fire_packs[key];
       } else {
         cv.sq_w = val(q.in1).cptr;  // ONNX [M][C][1][1] = [M][K]
-        cv.plan.epv = EPOOL_WIN_VARIANT;
+        if (cv.plan.epv != EPOOL_BAND_VARIANT) cv.plan.epv = EPOOL_WIN_VARIANT;  // the window kernel unless tuned
       }
       cv.c1sq = true;
       cv.sq_b = val(q.in2).cptr;
@@ -1647,7 +1647,7 @@ std::vector<int> step_tile_family(const Step& s) {
   std::vector<int> c;
   if (s.kind != S_CONV && s.kind != S_MATMUL) return c;
   if (s.kind == S_CONV && s.epool && !s.plan.f16) {  // f32 pooled conv: patch / row-walk variants, the window kernel
-    if (s.c1sq) return {EPOOL_WIN_TILE};            // the fused squeeze exists in the window kernel only
+    if (s.c1sq) return {EPOOL_WIN_TILE, EPOOL_BAND_TILE};  // the fused squeeze: window kernel, band walker
     for (int v = 1; v <= 5; ++v) c.push_back(EPOOL_TILE_BASE + v);
     if (s.wc1) c.push_back(EPOOL_WIN_TILE);
     return c;
@@ -1676,7 +1676,10 @@ void set_tile(ore_model* m, int k, int t) {
   Step& s = m->steps[m->exec_steps[k]];
   Step& b = m->base_steps[m->exec_steps[k]];
   if (s.kind == S_CONV && s.epool) {
-    const int v = t == EPOOL_WIN_TILE ? EPOOL_WIN_VARIANT : t == C1_POOL_F16_TILE ? 0 : t - EPOOL_TILE_BASE;
+    const int v = t == EPOOL_WIN_TILE    ? EPOOL_WIN_VARIANT
+                  : t == EPOOL_BAND_TILE ? EPOOL_BAND_VARIANT
+                  : t == C1_POOL_F16_TILE ? 0
+                                          : t - EPOOL_TILE_BASE;
     s.plan.epv = b.plan.epv = v;
     return;
   }

@@ -358,7 +358,7 @@ ore_status run_conv_epool(ore_ctx* ctx, const ConvPlan& pln, const float* x, int
     q.x_bytes = ((nc - 1) * x_nstride + C * x_ps) * 4;
     launch_conv_epool(q, ctx->stream);
     ORE_HIP_CHECK(ctx, hipGetLastError());
-    if (sq1 && last_conv_tile != EPOOL_WIN_TILE)
+    if (sq1 && last_conv_tile != EPOOL_WIN_TILE && last_conv_tile != EPOOL_BAND_TILE)
       return set_error(ctx, ORE_ERR_INVALID, "internal: the fused first conv + squeeze declined its launch");
   }
   return ORE_OK;

@@ -190,6 +190,34 @@ def test_benched_plan_parity_calibrated(gpu_ctx, winograd):
     m.close()
 
 
+def test_benched_plan_conv1_band_vs_window(gpu_ctx):
+    """bench.py's plan at B = 256 (one band per image: the headline launch of the band walker) with conv1 +
+    pool1 + fire2/squeeze1x1 forced onto each of its two kernels: the 256 probability rows are equal bit
+    for bit, and the calibrated images stay within the strict 1e-5 of the oracle fixture."""
+    import torch
+    import ore
+    from ore import squeezenet
+    from golden.make_golden import squeezenet_inputs_calib16
+    ref = np.load(os.path.join(GOLD, "squeezenet_calib16_oracle.npz"))["output"]
+    B = 256
+    m = ore.Model(gpu_ctx, squeezenet.build_calibrated(224), max_batch=B)
+    x = _batch(B, 1000)
+    pos = sorted({int(round(i * (B - 1) / 15)) for i in range(16)})
+    x[pos] = torch.from_numpy(squeezenet_inputs_calib16()).cuda()
+    out = torch.empty((B, m.output_elems), device="cuda")
+    m.autotune(x, out)
+    ys = []
+    for name in ("epool window f32", "epool band f32"):
+        m.set_tile(0, ore.Model.TILE_NAMES.index(name))
+        m.run_into(x, out)
+        torch.cuda.synchronize()
+        assert ore.Model.TILE_NAMES[m.tiles()[0]] == name
+        ys.append(out.cpu().numpy())
+    np.testing.assert_array_equal(ys[1], ys[0])
+    assert float(np.abs(ys[1][pos] - ref).max()) <= 1e-5
+    m.close()
+
+
 def test_bench_world1_rccl():
     """bench.py's collective path at world size 1 on this GPU (--dist): torch.distributed.run with one
     process, init_process_group("nccl", device_id=...) -- a one-rank RCCL communicator -- and the

@@ -746,6 +746,58 @@ def test_conv_pool_squeeze_fused_bit_identical(gpu_ctx, case):
     np.testing.assert_allclose(vals[0][0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("case", [(224, 224, 16, [0, 0, 0, 0], 2), (61, 224, 13, [0, 0, 1, 1], 3),
+                                  (23, 216, 16, [1, 1, 1, 1], 2), (40, 212, 9, [0, 0, 0, 0], 5),
+                                  (15, 224, 16, [1, 1, 0, 0], 1)])
+def test_conv1_band_bit_identical(gpu_ctx, case):
+    """The band walker (pooled-conv variant 8, "epool band f32": conv rows walked in steps of 256 column
+    pairs, pooling by DPP + LDS max, completed pooled rows squeezed) equals the window kernel (variant 7)
+    bit for bit on the squeeze output, over heights that give 1-13 bands per image, pool pads on every
+    side and widths down to the eligibility edge (52 column pairs per conv row); and the oracle within
+    the conv tolerance."""
+    import ore
+    import oracle
+    H, W, Q, pads, B = case
+    mb = _conv_pool_squeeze_model(H, W, 96, Q, pads)
+    x = (np.random.default_rng(H * 7 + W).standard_normal((B, 3, H, W)) * 20).astype(np.float32)
+    band = ore.Model.TILE_NAMES.index("epool band f32")
+    vals = []
+    for tile in (None, band):
+        m = _model(gpu_ctx, mb, max_batch=B)
+        m.set_fusion(ore.FUSE_ALL | ore.FUSE_EAGER | ore.KEEP_VALUES)
+        if tile is not None:
+            m.set_tile(0, tile)
+        y = _np(m.run(_t(x)))
+        vals.append((y, m.read_value("qr")))
+        names = [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0]
+        assert names == ["epool band f32" if tile is not None else "epool window f32"], names
+        m.close()
+    np.testing.assert_array_equal(vals[1][1], vals[0][1])
+    np.testing.assert_array_equal(vals[1][0], vals[0][0])
+    ref = oracle.Model(mb).run(x, Q)
+    np.testing.assert_allclose(vals[1][0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_squeezenet_conv1_band(gpu_ctx):
+    """SqueezeNet-1.0 @224 f32 with conv1 + pool1 + fire2/squeeze1x1 on the band walker: probabilities
+    equal the window kernel's plan bit for bit (batch 3: 13 bands per image, and batch 256's one band
+    per image via a 260-image chunk-free run is covered by the benched-plan parity tests)."""
+    import ore
+    from ore import squeezenet
+    mb = squeezenet.build(224)
+    x = _t(squeezenet.synthetic_input(3, 224, seed=37))
+    band = ore.Model.TILE_NAMES.index("epool band f32")
+    outs = []
+    for tile in (None, band):
+        m = _model(gpu_ctx, mb, max_batch=3)
+        if tile is not None:
+            m.set_tile(0, tile)
+        outs.append(_np(m.run(x)))
+        assert ore.Model.TILE_NAMES[m.tiles()[0]] == ("epool band f32" if tile is not None else "epool window f32")
+        m.close()
+    np.testing.assert_array_equal(outs[1], outs[0])
+
+
 def test_squeezenet_conv1_squeeze_fused(gpu_ctx):
     """SqueezeNet-1.0 @224 f32: conv1 + pool1 + fire2/squeeze1x1 in one launch; probabilities equal the
     plan without that fusion bit for bit."""
