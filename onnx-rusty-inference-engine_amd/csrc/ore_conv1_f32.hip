@@ -416,6 +416,12 @@ struct CBGeo {
   }
 };
 
+// median(b, 0, top) on ints: one v_med3_i32 (the compiler keeps a min and a max for a variable bound)
+__device__ __forceinline__ int cb_med3(int b, int top) {
+  int r;
+  asm volatile("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(b), "v"(top));
+  return r;
+}
 __device__ __forceinline__ void cb_max(char* base, int off, unsigned v) {
   __hip_atomic_fetch_max(reinterpret_cast<unsigned*>(base + off), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -485,10 +491,54 @@ __global__ __launch_bounds__(512, 1) void conv_band_pool_f32_kernel(ConvParams p
     };
     load_window(0);
     store_window();
+    // A: 16-B groups of four k-steps (group u = i KQ + q of the step's 3 KQ: fragment i, k-steps 4 q ..),
+    // two groups ahead, across fragments and steps
+    constexpr int NG = MF * G::KQ;
+    c3f4 a[2];
+    auto load_a = [&](int u) __attribute__((always_inline)) {
+      const int i = u / G::KQ, q = u - i * G::KQ;
+      a[u & 1] = __builtin_bit_cast(c3f4, __builtin_amdgcn_raw_buffer_load_b128(wr, aoff, ((q * Mp32 + 32 * i) * 2) * 16, 0));
+    };
+    load_a(0);
+    load_a(1);
+    // the pooled rows [q_lo, q_hi) completed by a step: squeezed after it, between its two barriers
     int sq_lo = pb0;
+    const int ng = (p.ep_Wo + 15) >> 4, lj = lane & 15, slk = lane >> 4;
+    auto squeeze_rows = [&](int q_lo, int q_hi) __attribute__((always_inline)) {
+      const int ntask = (q_hi - q_lo) * ng;
+      for (int t = wave; t < ntask; t += 8) {
+        const int pr = q_lo + t / ng, pc = 16 * (t - (t / ng) * ng) + lj;
+        const bool pok = pc < p.ep_Wo;
+        float* cell = ring + slk * CB_CS + (pok ? (pr & 3) * CB_RPW + pc : 4 * CB_RPW + 32 + lj);
+        // all 24 B values in flight at once (one LDS round trip, not one per MFMA), then the chain
+        float bq[MF][8];
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+          for (int tt = 0; tt < 8; ++tt) bq[i][tt] = cell[(32 * i + 4 * tt) * CB_CS];
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+          for (int tt = 0; tt < 8; ++tt) cell[(32 * i + 4 * tt) * CB_CS] = 0.0f;
+        __builtin_amdgcn_sched_barrier(0);
+        c3f4 sacc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+          for (int tt = 0; tt < 8; ++tt) sacc = __builtin_amdgcn_mfma_f32_16x16x4f32(aqv[i][tt], bq[i][tt], sacc, 0, 0, 0);
+        if (pok) {
+          float* yq = sq.y + (long long)img * sq.y_nstride + pr * p.ep_Wo + pc;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int m = 4 * slk + e;
+            if (m < sq.M) yq[(long long)m * sq.y_ps] = fmaxf(sacc[e] + qbias[m], 0.0f);
+          }
+        }
+      }
+    };
     for (int s = 0; s < nsteps; ++s) {
       const int r_lo = cr0 + (s << 8) / HP;
-      __syncthreads();  // step s's window is in LDS; the previous squeeze's readers and clears are done
+      __syncthreads();  // window s is in LDS; the previous squeeze's reads and clears are done
       if (s + 1 < nsteps) load_window(s + 1);
 
       // the lane's pair: conv row cr, columns 2 j - pl + f
@@ -508,48 +558,6 @@ __global__ __launch_bounds__(512, 1) void conv_band_pool_f32_kernel(ConvParams p
         bk3[f] = base * 4;
         top[f] = ok ? 0x7fffffff : 0;
       }
-
-      c3f16 acc[MF][2];
-#pragma unroll
-      for (int i = 0; i < MF; ++i)
-#pragma unroll
-        for (int f = 0; f < 2; ++f)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[i][f][e] = 0.0f;
-      c3f4 a[2][MF];
-#pragma unroll
-      for (int g = 0; g < 2; ++g)
-#pragma unroll
-        for (int i = 0; i < MF; ++i)
-          a[g][i] = __builtin_bit_cast(c3f4, __builtin_amdgcn_raw_buffer_load_b128(wr, aoff, ((g * Mp32 + 32 * i) * 2) * 16, 0));
-      auto bread = [&](int f, int jj) __attribute__((always_inline)) {
-        const int k0 = 2 * jj, kd = G::kind(k0), ko = G::koff(k0) * 4;
-        const int bb = kd == 0 ? bk0[f] : kd == 1 ? bk1[f] : kd == 2 ? bk2[f] : bk3[f];
-        return *reinterpret_cast<const float*>(winb + bb + ko);
-      };
-      float bn[2] = {bread(0, 0), bread(1, 0)};
-#pragma unroll
-      for (int jj = 0; jj < G::KS; ++jj) {
-        const int q = jj >> 2, ii = jj & 3;
-        const float b[2] = {bn[0], bn[1]};
-        if (jj + 1 < G::KS) {
-          bn[0] = bread(0, jj + 1);
-          bn[1] = bread(1, jj + 1);
-        }
-#pragma unroll
-        for (int i = 0; i < MF; ++i)
-#pragma unroll
-          for (int f = 0; f < 2; ++f)
-            acc[i][f] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q & 1][i][ii], b[f], acc[i][f], 0, 0, 0);
-        if (ii == 3 && q + 2 < G::KQ) {
-#pragma unroll
-          for (int i = 0; i < MF; ++i)
-            a[q & 1][i] = __builtin_bit_cast(
-                c3f4, __builtin_amdgcn_raw_buffer_load_b128(wr, aoff, (((q + 2) * Mp32 + 32 * i) * 2) * 16, 0));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-
       // pooled cells of the pair (row pa = (cr + pt) / 2 and, for even cr + pt, pa - 1; column j), and
       // of lane 0's first column (column j - 1)
       const int ap = cr + p.ep_pt, pa = ap >> 1;
@@ -559,77 +567,85 @@ __global__ __launch_bounds__(512, 1) void conv_band_pool_f32_kernel(ConvParams p
       const int oA = rA && jok ? cA + j * 4 : dummy, oB = rB && jok ? cB + j * 4 : dummy;
       const int qA = rA && bok ? cA + (j - 1) * 4 : dummy, qB = rB && bok ? cB + (j - 1) * 4 : dummy;
       const bool nbok = lr < 31 && j + 1 < HP;  // the next column pair: this wave's lane lr + 1, same row
-      unsigned first[MF][16];
+      // wave-uniform skips of LDS max operations that would all go to dummy cells: a wave on one odd row
+      // has no second pooled row, and lane 0's first column rarely has nowhere to go
+      const bool anyB = __builtin_amdgcn_ballot_w64(rB && jok) != 0;
+      const bool anyQ = __builtin_amdgcn_ballot_w64(bok && (rA || rB)) != 0;
+      auto bread = [&](int f, int jj) __attribute__((always_inline)) {
+        const int k0 = 2 * jj, kd = G::kind(k0), ko = G::koff(k0) * 4;
+        const int bb = kd == 0 ? bk0[f] : kd == 1 ? bk1[f] : kd == 2 ? bk2[f] : bk3[f];
+        return *reinterpret_cast<const float*>(winb + bb + ko);
+      };
+      // per 32-channel fragment i: its K loop (both pixels), then its pooled contributions, whose LDS
+      // max operations drain under the next fragment's MFMAs
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
+        c3f16 acc[2];
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[f][e] = 0.0f;
+        float bn[2] = {bread(0, 0), bread(1, 0)};
+#pragma unroll
+        for (int jj = 0; jj < G::KS; ++jj) {
+          const int q = jj >> 2, ii = jj & 3, u = i * G::KQ + q;
+          const float b[2] = {bn[0], bn[1]};
+          if (jj + 1 < G::KS) {
+            bn[0] = bread(0, jj + 1);
+            bn[1] = bread(1, jj + 1);
+          }
+#pragma unroll
+          for (int f = 0; f < 2; ++f)
+            acc[f] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u & 1][ii], b[f], acc[f], 0, 0, 0);
+          if (ii == 3 || jj + 1 == G::KS) {  // group u is done: its slot takes group u + 2
+            if (u + 2 < NG) {
+              load_a(u + 2);
+            } else if (u + 1 == NG) {  // NG is odd: the next step's groups 0 and 1 after the last one
+              load_a(0);
+              load_a(1);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
         char* rb = ringb + 32 * i * CB_CS * 4;
+        unsigned first[16];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const c3f4 sb = *reinterpret_cast<const c3f4*>(sbias + 32 * i + 8 * g + 4 * h);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float f0 = acc[i][0][4 * g + e] + sb[e], f1 = acc[i][1][4 * g + e] + sb[e];
+            const float f0 = acc[0][4 * g + e] + sb[e], f1 = acc[1][4 * g + e] + sb[e];
             // Relu and the out-of-plane zero on the bits: median(b, 0, top) (negative floats are
             // negative ints -> +0; top = 0 for a column outside the conv plane)
-            const int b0 = max(0, min(__builtin_bit_cast(int, f0), top[0]));
-            const int b1 = max(0, min(__builtin_bit_cast(int, f1), top[1]));
+            const int b0 = cb_med3(__builtin_bit_cast(int, f0), top[0]);
+            const int b1 = cb_med3(__builtin_bit_cast(int, f1), top[1]);
             int nbv = __builtin_amdgcn_update_dpp(0, b0, 0x130, 0xf, 0xf, true);  // wave_shl:1: lane l + 1's b0
             nbv = nbok ? nbv : 0;
             const unsigned m = (unsigned)max(max(b0, b1), nbv);
-            first[i][4 * g + e] = (unsigned)b0;
+            first[4 * g + e] = (unsigned)b0;
             const int off = (8 * g + e) * CB_CS * 4;
             cb_max(rb, oA + off, m);
-            cb_max(rb, oB + off, m);
+            if (anyB) cb_max(rb, oB + off, m);
           }
         }
-      }
-      if (lr == 0) {
-#pragma unroll
-        for (int i = 0; i < MF; ++i) {
-          char* rb = ringb + 32 * i * CB_CS * 4;
+        if (anyQ && lr == 0) {
 #pragma unroll
           for (int g = 0; g < 4; ++g)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const int off = (8 * g + e) * CB_CS * 4;
-              cb_max(rb, qA + off, first[i][4 * g + e]);
-              cb_max(rb, qB + off, first[i][4 * g + e]);
+              cb_max(rb, qA + off, first[4 * g + e]);
+              cb_max(rb, qB + off, first[4 * g + e]);
             }
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __syncthreads();  // every pooled contribution of step s is in the ring; the window is free
-
-      // the pooled rows completed by step s: squeeze (16 pooled columns per task), store, clear
+      // the pooled rows completed by step s
       const int rdone = s + 1 == nsteps ? p.Ho : cr0 + ((s + 1) << 8) / HP;
       int sq_hi = sq_lo;
       while (sq_hi < pb1 && min(2 * sq_hi - p.ep_pt + 2, p.Ho - 1) < rdone) ++sq_hi;
-      const int ng = (p.ep_Wo + 15) >> 4, ntask = (sq_hi - sq_lo) * ng;
-      const int lj = lane & 15, slk = lane >> 4;
-      for (int t = wave; t < ntask; t += 8) {
-        const int pr = sq_lo + t / ng, pc = 16 * (t - (t / ng) * ng) + lj;
-        const bool pok = pc < p.ep_Wo;
-        float* cell = ring + slk * CB_CS + (pok ? (pr & 3) * CB_RPW + pc : 4 * CB_RPW + 32 + lj);
-        c3f4 sacc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int i = 0; i < MF; ++i)
-#pragma unroll
-          for (int tt = 0; tt < 8; ++tt) {
-            const float bq = cell[(32 * i + 4 * tt) * CB_CS];
-            sacc = __builtin_amdgcn_mfma_f32_16x16x4f32(aqv[i][tt], bq, sacc, 0, 0, 0);
-          }
-#pragma unroll
-        for (int i = 0; i < MF; ++i)
-#pragma unroll
-          for (int tt = 0; tt < 8; ++tt) cell[(32 * i + 4 * tt) * CB_CS] = 0.0f;
-        if (pok) {
-          float* yq = sq.y + (long long)img * sq.y_nstride + pr * p.ep_Wo + pc;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int m = 4 * slk + e;
-            if (m < sq.M) yq[(long long)m * sq.y_ps] = fmaxf(sacc[e] + qbias[m], 0.0f);
-          }
-        }
-      }
+      __syncthreads();  // every pooled contribution of step s is in the ring; every K loop is done
+      squeeze_rows(sq_lo, sq_hi);
       sq_lo = sq_hi;
       if (s + 1 < nsteps) store_window();
     }

@@ -17,8 +17,11 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256)
     a = ap.parse_args()
+    import ctypes
+    import numpy as np
     import torch
     import ore
+    lib = ctypes.CDLL(ore._lib.LIB_PATH)
     from test_model_gpu import _conv_pool_squeeze_model
     mb = _conv_pool_squeeze_model(224, 224, 96, 16, [0, 0, 0, 0])
     ctx = ore.Context(0)
@@ -40,6 +43,14 @@ def main():
         ev[1].record()
         torch.cuda.synchronize()
         ys[name] = out.clone()
+        if name == "epool band f32" and hasattr(lib, "ore_debug_stamps_band"):  # a stamps build
+            st = np.zeros((1024, 8), dtype=np.uint64)
+            assert lib.ore_debug_stamps_band(st.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(st.nbytes)) == 0
+            st = st[: min(a.batch, 256)].astype(np.float64)
+            tot = st.sum(1).mean()
+            names = ["barrier T + top", "K loops", "epilogues", "-", "barrier E", "squeeze", "window store", "tail"]
+            print("wave-0 phase shares (s_memtime):", ", ".join(f"{n} {100 * st[:, k].mean() / tot:.1f}%"
+                                                               for k, n in enumerate(names)), f"total {tot:.0f}")
         print(f"{name}: {1000 * ev[0].elapsed_time(ev[1]) / a.reps:.1f} us/run "
               f"(ran {ore.Model.TILE_NAMES[m.tiles()[0]]})", flush=True)
         m.close()
