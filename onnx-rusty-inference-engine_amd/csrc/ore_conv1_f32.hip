@@ -416,12 +416,9 @@ struct CBGeo {
   }
 };
 
-// median(b, 0, top) on ints: one v_med3_i32 (the compiler keeps a min and a max for a variable bound)
-__device__ __forceinline__ int cb_med3(int b, int top) {
-  int r;
-  asm volatile("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(b), "v"(top));
-  return r;
-}
+// median(b, 0, top) on ints (a min and a max: no inline asm here, whose VALU writes the hazard recognizer
+// does not see ahead of the DPP reads that follow)
+__device__ __forceinline__ int cb_med3(int b, int top) { return max(0, min(b, top)); }
 __device__ __forceinline__ void cb_max(char* base, int off, unsigned v) {
   __hip_atomic_fetch_max(reinterpret_cast<unsigned*>(base + off), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
