@@ -452,7 +452,7 @@ def main():
             kname = ("Conv class: conv_pair_pool_f16_kernel (conv1 + pool1 straight from the f32 input), "
                      "fire_f16_kernel / fire_pool_f16_kernel (fire module [+ MaxPool] + next squeeze) and "
                      "conv_f16_kernel (implicit GEMM), all MFMA 32x32x16 f16 with f32 accumulate" if f16 else
-                     "Conv class: conv_win_pool_f32_kernel (conv1 + pool1 + fire2 squeeze), fire_kernel (fire "
+                     "Conv class: conv_band_pool_f32_kernel / conv_win_pool_f32_kernel (conv1 + pool1 + fire2 squeeze, autotuned), fire_kernel (fire "
                      "module + next squeeze), conv_winol_kernel (Winograd F(2x2,3x3) expand3x3, LDS-staged, MFMA "
                      "16x16x4 f32), conv_stream_kernel / conv_stream1x1_persist_kernel (LDS-free implicit GEMM, "
                      "MFMA 16x16x4 f32), pool_conv1x1_f32_kernel (pool3 / pool5 + the next squeeze) and "

@@ -13,7 +13,7 @@ import sys
 
 CLASSES = [("conv (f32 MFMA)", ("conv_gemm_kernel", "conv_stream_kernel", "conv_stream1x1_persist_kernel", "fire_kernel", "conv_pool_stream_kernel",
                                 "conv_wino32_kernel", "conv_wino16_kernel", "conv_winol_kernel", "fire_wino_kernel",
-                                "conv_win_pool_f32_kernel", "fire_pool_kernel", "pool_conv1x1_f32_kernel",
+                                "conv_win_pool_f32_kernel", "conv_band_pool_f32_kernel", "fire_pool_kernel", "pool_conv1x1_f32_kernel",
                                 "conv1x1_gap_f32_kernel")),
            ("conv (f16 MFMA)", ("conv_f16_kernel", "conv_f16_dma_kernel", "conv_f16_epool", "fire_f16_kernel",
                                 "fire_pool_f16_kernel", "conv_pair_pool_f16_kernel", "conv1x1_gap_f16_kernel")),
@@ -60,7 +60,10 @@ def main():
         if "launch_us" in r:  # round 5: the dominant launch, which the rocprof row of its kernel must agree with
             print(f"bench.py dominant launch: {r.get('kernel')}: {r.get('launch_us')} us, achieved {r.get('achieved')} "
                   f"{r.get('unit')} = {r.get('frac')} of {r.get('peak')}")
-            dom = [x for x in rows if "conv_win_pool_f32_kernel" in x["Name"] or "conv_pair_pool_f16_kernel" in x["Name"]]
+            kern = {"epool band f32": "conv_band_pool_f32_kernel", "epool window f32": "conv_win_pool_f32_kernel",
+                    "first conv pool f16": "conv_pair_pool_f16_kernel"}
+            names = [k for t, k in kern.items() if f"tile '{t}'" in str(r.get("kernel"))] or list(kern.values())
+            dom = [x for x in rows if any(k in x["Name"] for k in names)]
             for x in dom:
                 print(f"rocprofv3 row of that kernel: {int(x['Calls'])} calls, average {float(x['AverageNs']) / 1e3:.2f} us "
                       f"({x['Name'][:90]})")
