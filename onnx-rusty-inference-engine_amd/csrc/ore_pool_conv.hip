@@ -267,12 +267,17 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
     }
     __syncthreads();
     // squeeze k-steps of this chunk: k = PS_CH ci + 4 t + lk
-    if (m0 < p.M) {
+    if (m0 < p.M) {  // every B value read before the MFMAs: one LDS round trip, not one per k-step
+      float bq[KS][PS_PR * NF];
 #pragma unroll
       for (int t = 0; t < KS; ++t)
 #pragma unroll
-        for (int n = 0; n < PS_PR * NF; ++n)
-          acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(acur[t], pt[4 * t + lk][16 * n + lj], acc[n], 0, 0, 0);
+        for (int n = 0; n < PS_PR * NF; ++n) bq[t][n] = pt[4 * t + lk][16 * n + lj];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < KS; ++t)
+#pragma unroll
+        for (int n = 0; n < PS_PR * NF; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(acur[t], bq[t][n], acc[n], 0, 0, 0);
     }
 #pragma unroll
     for (int t = 0; t < KS; ++t) acur[t] = anxt[t];
