@@ -778,6 +778,24 @@ def test_conv1_band_bit_identical(gpu_ctx, case):
     np.testing.assert_allclose(vals[1][0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-5)
 
 
+def test_conv1_band_units_per_workgroup(gpu_ctx):
+    """Batch 300 at 224 x 224: more (image, band) units than workgroups (one per CU), so workgroups walk
+    a second unit after their first (the ring and window reused across units); equal to the window
+    kernel bit for bit."""
+    import ore
+    B = 300
+    mb = _conv_pool_squeeze_model(224, 224, 96, 16, [0, 0, 0, 0])
+    x = (np.random.default_rng(300).standard_normal((B, 3, 224, 224)) * 20).astype(np.float32)
+    outs = []
+    for name in ("epool window f32", "epool band f32"):
+        m = _model(gpu_ctx, mb, max_batch=B)
+        m.set_tile(0, ore.Model.TILE_NAMES.index(name))
+        outs.append(_np(m.run(_t(x))))
+        assert ore.Model.TILE_NAMES[m.tiles()[0]] == name
+        m.close()
+    np.testing.assert_array_equal(outs[1], outs[0])
+
+
 def test_squeezenet_conv1_band(gpu_ctx):
     """SqueezeNet-1.0 @224 f32 with conv1 + pool1 + fire2/squeeze1x1 on the band walker: probabilities
     equal the window kernel's plan bit for bit (batch 3: 13 bands per image, and batch 256's one band
