@@ -81,7 +81,10 @@ __global__ __launch_bounds__(256, 2) void conv_win_pool_f32_kernel(ConvParams p,
 #pragma unroll
     for (int i = 0; i < MF; ++i)
 #pragma unroll
-      for (int t = 0; t < 8; ++t) aqv[i][t] = sq.w[(lj < sq.M ? lj : 0) * p.M + 32 * i + 4 * t + lk];
+      for (int t = 0; t < 8; ++t) {  // channels past M (M < 96): a zero weight, not the next row's
+        const int k = 32 * i + 4 * t + lk;
+        aqv[i][t] = k < p.M ? sq.w[(lj < sq.M ? lj : 0) * p.M + k] : 0.0f;
+      }
   }
   // the lane's two patch pixels: window base (bytes) per step kind (plain scalars, not an array: an
   // array indexed by the unrolled step's kind stayed in scratch), conv-tile offset
@@ -443,7 +446,10 @@ __global__ __launch_bounds__(512, 1) void conv_band_pool_f32_kernel(ConvParams p
 #pragma unroll
     for (int i = 0; i < MF; ++i)
 #pragma unroll
-      for (int t = 0; t < 8; ++t) aqv[i][t] = lj < sq.M ? sq.w[lj * p.M + 32 * i + 4 * t + lk] : 0.0f;
+      for (int t = 0; t < 8; ++t) {  // channels past M (M < 96): a zero weight, not the next row's
+        const int k = 32 * i + 4 * t + lk;
+        aqv[i][t] = lj < sq.M && k < p.M ? sq.w[lj * p.M + k] : 0.0f;
+      }
   }
   // this thread's window float4s e = tid + 512 u: (channel c, row r, float4 j4); global byte offset from
   // the step's first input row (past the row's width: CB_OOB, which reads 0), LDS float index
