@@ -422,6 +422,9 @@ struct CBGeo {
 // median(b, 0, top) on ints (a min and a max: no inline asm here, whose VALU writes the hazard recognizer
 // does not see ahead of the DPP reads that follow)
 __device__ __forceinline__ int cb_med3(int b, int top) { return max(0, min(b, top)); }
+__device__ __forceinline__ void cb_maxp(unsigned* a, unsigned v) {
+  __hip_atomic_fetch_max(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ void cb_max(char* base, int off, unsigned v) {
   __hip_atomic_fetch_max(reinterpret_cast<unsigned*>(base + off), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -610,36 +613,44 @@ __global__ __launch_bounds__(512, 1) void conv_band_pool_f32_kernel(ConvParams p
           }
           __builtin_amdgcn_sched_barrier(0);
         }
-        char* rb = ringb + 32 * i * CB_CS * 4;
-        unsigned first[16];
+        // the fragment's cell pointers (channel 32 i + 4 h of each target): the 16 channel rows are
+        // compile-time offsets of one pointer each
+        unsigned* pA = reinterpret_cast<unsigned*>(ringb + 32 * i * CB_CS * 4 + oA);
+        unsigned* pB = reinterpret_cast<unsigned*>(ringb + 32 * i * CB_CS * 4 + oB);
+        unsigned first[16], mv[16];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const c3f4 sb = *reinterpret_cast<const c3f4*>(sbias + 32 * i + 8 * g + 4 * h);
+          // the bias on packed f32 (two channels per v_pk_add_f32)
+          const c3f4 o0 = c3f4{acc[0][4 * g], acc[0][4 * g + 1], acc[0][4 * g + 2], acc[0][4 * g + 3]} + sb;
+          const c3f4 o1 = c3f4{acc[1][4 * g], acc[1][4 * g + 1], acc[1][4 * g + 2], acc[1][4 * g + 3]} + sb;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float f0 = acc[0][4 * g + e] + sb[e], f1 = acc[1][4 * g + e] + sb[e];
+            const float f0 = o0[e], f1 = o1[e];
             // Relu and the out-of-plane zero on the bits: median(b, 0, top) (negative floats are
             // negative ints -> +0; top = 0 for a column outside the conv plane)
             const int b0 = cb_med3(__builtin_bit_cast(int, f0), top[0]);
             const int b1 = cb_med3(__builtin_bit_cast(int, f1), top[1]);
             int nbv = __builtin_amdgcn_update_dpp(0, b0, 0x130, 0xf, 0xf, true);  // wave_shl:1: lane l + 1's b0
             nbv = nbok ? nbv : 0;
-            const unsigned m = (unsigned)max(max(b0, b1), nbv);
+            mv[4 * g + e] = (unsigned)max(max(b0, b1), nbv);
             first[4 * g + e] = (unsigned)b0;
-            const int off = (8 * g + e) * CB_CS * 4;
-            cb_max(rb, oA + off, m);
-            if (anyB) cb_max(rb, oB + off, m);
           }
         }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cb_maxp(pA + ((r >> 2) * 8 + (r & 3)) * CB_CS, mv[r]);
+        if (anyB) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) cb_maxp(pB + ((r >> 2) * 8 + (r & 3)) * CB_CS, mv[r]);
+        }
         if (anyQ && lr == 0) {
+          unsigned* qpA = reinterpret_cast<unsigned*>(ringb + 32 * i * CB_CS * 4 + qA);
+          unsigned* qpB = reinterpret_cast<unsigned*>(ringb + 32 * i * CB_CS * 4 + qB);
 #pragma unroll
-          for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int off = (8 * g + e) * CB_CS * 4;
-              cb_max(rb, qA + off, first[4 * g + e]);
-              cb_max(rb, qB + off, first[4 * g + e]);
-            }
+          for (int r = 0; r < 16; ++r) {
+            cb_maxp(qpA + ((r >> 2) * 8 + (r & 3)) * CB_CS, first[r]);
+            cb_maxp(qpB + ((r >> 2) * 8 + (r & 3)) * CB_CS, first[r]);
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
