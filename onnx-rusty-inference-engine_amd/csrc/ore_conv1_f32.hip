@@ -492,8 +492,8 @@ __global__ __launch_bounds__(512, 1) void conv_band_pool_f32_kernel(ConvParams p
     };
     auto store_window = [&]() __attribute__((always_inline)) {
 #pragma unroll
-      for (int u = 0; u < CB_NU; ++u)
-        if (wl[u] >= 0) *reinterpret_cast<c3f4*>(win + wl[u]) = xv[u];
+      for (int u = 0; u < CB_NU - 1; ++u) *reinterpret_cast<c3f4*>(win + wl[u]) = xv[u];  // 512 u + tid < CB_NV
+      if (wl[CB_NU - 1] >= 0) *reinterpret_cast<c3f4*>(win + wl[CB_NU - 1]) = xv[CB_NU - 1];
     };
     load_window(0);
     store_window();
