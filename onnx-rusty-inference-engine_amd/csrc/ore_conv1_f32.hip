@@ -583,7 +583,10 @@ __global__ __launch_bounds__(512, 1) void conv_band_pool_f32_kernel(ConvParams p
         return *reinterpret_cast<const float*>(winb + bb + ko);
       };
       // per 32-channel fragment i: its K loop (both pixels), then its pooled contributions, whose LDS
-      // max operations drain under the next fragment's MFMAs
+      // max operations drain under the next fragment's MFMAs.  A wave whose pairs all lie past the band
+      // (the band's last, partial step) skips both: its SIMD partner runs alone (its A ring already holds
+      // the next step's first groups)
+      if ((s << 8) + 32 * wave < npairs) {
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
         c3f16 acc[2];
@@ -653,6 +656,7 @@ __global__ __launch_bounds__(512, 1) void conv_band_pool_f32_kernel(ConvParams p
           }
         }
         __builtin_amdgcn_sched_barrier(0);
+      }
       }
       // the pooled rows completed by step s
       const int rdone = s + 1 == nsteps ? p.Ho : cr0 + ((s + 1) << 8) / HP;
