@@ -1012,7 +1012,11 @@ struct Planner {
         cv.sq_w = m->fire_packs[key];
       } else {
         cv.sq_w = val(q.in1).cptr;  // ONNX [M][C][1][1] = [M][K]
-        if (cv.plan.epv != EPOOL_BAND_VARIANT) cv.plan.epv = EPOOL_WIN_VARIANT;  // the window kernel unless tuned
+        // untuned: the band walker for batches that give every CU an image (one workgroup per band of an
+        // image; it bands smaller batches but the window kernel's patches fill the chip better there),
+        // else the window kernel; an autotuned / set choice (epv 7 or 8) is kept
+        if (cv.plan.epv != EPOOL_BAND_VARIANT && cv.plan.epv != EPOOL_WIN_VARIANT)
+          cv.plan.epv = m->max_batch >= 128 ? EPOOL_BAND_VARIANT : EPOOL_WIN_VARIANT;
       }
       cv.c1sq = true;
       cv.sq_b = val(q.in2).cptr;
