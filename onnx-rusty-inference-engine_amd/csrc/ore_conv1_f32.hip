@@ -425,9 +425,6 @@ __device__ __forceinline__ int cb_med3(int b, int top) { return max(0, min(b, to
 __device__ __forceinline__ void cb_maxp(unsigned* a, unsigned v) {
   __hip_atomic_fetch_max(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void cb_max(char* base, int off, unsigned v) {
-  __hip_atomic_fetch_max(reinterpret_cast<unsigned*>(base + off), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 __global__ __launch_bounds__(512, 1) void conv_band_pool_f32_kernel(ConvParams p, const float* __restrict__ wc,
                                                                     C1SqueezeF32 sq, int nb) {

@@ -212,6 +212,7 @@ struct PoolConvParams {
 };
 bool pool_conv1x1_f32_eligible(const PoolConvParams& p);
 void launch_pool_conv1x1_f32(const PoolConvParams& p, hipStream_t s);
+int pool_conv1x1_f32_rows(int Wp);  // pooled rows per workgroup (band height) for Wp pooled columns
 
 // f16 models: the fused fire module (ore_fire_f16.hip) on NHWC f16 values (pixel strides in
 // elements, image strides in elements); weights packed by launch_fire_pack_f16

@@ -1099,7 +1099,8 @@ struct Planner {
       cv.pe1_E = e1.M;
       cv.pe1_Mp = e1.plan.Mp;
       // work: e1 per band row it stages (2 PR + 1 input rows per PR pooled rows, neighbouring bands share one)
-      const double rows = double((cv.pwin.Ho + 1) / 2 * 5);
+      const int pr = pool_conv1x1_f32_rows(int(cv.pwin.Wo));
+      const double rows = double((cv.pwin.Ho + pr - 1) / pr * (2 * pr + 1));
       cv.mfma_flops_per_img = (cv.mfma_flops_per_img < 0 ? cv.flops_per_img : cv.mfma_flops_per_img) +
                               e1.flops_per_img * rows / double(e1.H);
       cv.flops_per_img += e1.flops_per_img;

@@ -3,7 +3,7 @@
 // the walker used to run maxpool_kernel (382 MB in, 95 MB out at B = 256) and then the squeeze
 // (95 MB in again)).  The pooled map never reaches HBM.
 //
-// One workgroup = PS_PR (2) pooled rows of one image (Wp <= 16 NF columns each: NF 16-pixel
+// One workgroup = PS_PR (3) pooled rows of one image (Wp <= 16 NF columns each: NF 16-pixel
 // fragments per row; NF = 1 for pool5's 13 columns, 2 for pool3's 27) x all M <= 64 output channels
 // (four waves x 16 channels, v_mfma_f32_16x16x4_f32).  Per chunk of PS_CH (16) input channels:
 //   * the 2 PS_PR + 1 input rows the pooled rows read (whole rows) go global -> registers
@@ -42,18 +42,23 @@ namespace {
 
 typedef float ps4 __attribute__((ext_vector_type(4)));
 
-#define ORE_PS_PR 2   // pooled rows per workgroup
 #define ORE_PS_CH 16  // input channels per chunk
-constexpr int PS_PR = ORE_PS_PR, PS_CH = ORE_PS_CH;
+constexpr int PS_CH = ORE_PS_CH;
 // input loads non-temporal (cache policy nt): read once, and a streamed read measured 10 % faster
 // with it (profiles/r03k_hbm_probe.txt); pool5 + squeeze 110.3 -> 105.7 us, pool3 205 -> 204 us
 constexpr int PS_AUX = 2;
-constexpr int PS_ROWS = 2 * PS_PR + 1;  // input rows of PS_PR pooled rows (3x3, stride 2)
+// pooled rows per workgroup (PS_PR): 3 for both widths.  Against 2 (B = 256, tools/r05zi.sh,
+// profiles/r05zi_ab_pool_rows.txt): pool3 + e1 + squeeze 274-276 -> 256-257 us (9 bands of 7 input rows
+// instead of 14 of 5: e1 recomputed and input fetched 1.17x instead of 1.30x / 1.25x, still two waves per
+// SIMD), pool5 + squeeze 107-109 -> 102 us; 4 rows for pool5 measured 110 us (four waves per SIMD)
+__host__ __device__ constexpr int ps_pr(int /*nf: fragments per pooled row*/) { return 3; }
 
 // NF: 16-pixel fragments per pooled row (Wp <= 16 NF); KS1: e1's k-steps (0: no e1); FRW: e1 pixel fragments
 // per wave (>= ceil(ceil((2 PS_PR + 1) W / 16) / 4))
 template <int NF, int KS1, int FRW>
 __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p) {
+  constexpr int PS_PR = ps_pr(NF);
+  constexpr int PS_ROWS = 2 * PS_PR + 1;  // input rows of PS_PR pooled rows (3x3, stride 2)
   // staged rows: input column iw at LDS column iw + PS_LC; columns left of the image and right of
   // the loaded 16-B groups are zero once (never written), loaded columns >= W are zeroed per element
   constexpr int PS_LC = 4;
@@ -309,7 +314,8 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
 }  // namespace
 
 // e1 pixel fragments per wave of the recomputed-e1 variant (the band's (2 PS_PR + 1) W pixels over 4 waves)
-static int ps_frw(const PoolConvParams& p) { return ((PS_ROWS * p.W + 15) / 16 + 3) / 4; }
+static int ps_nf(const PoolConvParams& p) { return p.Wp <= 16 ? 1 : 2; }
+static int ps_frw(const PoolConvParams& p) { return (((2 * ps_pr(ps_nf(p)) + 1) * p.W + 15) / 16 + 3) / 4; }
 
 bool pool_conv1x1_f32_eligible(const PoolConvParams& p) {
   const bool e1ok = p.E1 == 0 ||
@@ -349,9 +355,12 @@ static void ps_dispatch(const PoolConvParams& p, long long grid, hipStream_t s) 
     ps_dispatch_frw<NF, 16>(p, grid, s);
 }
 
+int pool_conv1x1_f32_rows(int Wp) { return ps_pr(Wp <= 16 ? 1 : 2); }
+
 void launch_pool_conv1x1_f32(const PoolConvParams& p, hipStream_t s) {
-  const long long grid = (long long)p.N * ((p.Hp + PS_PR - 1) / PS_PR);
-  if (p.Wp <= 16)
+  const int pr = ps_pr(ps_nf(p));
+  const long long grid = (long long)p.N * ((p.Hp + pr - 1) / pr);
+  if (ps_nf(p) == 1)
     ps_dispatch<1>(p, grid, s);
   else
     ps_dispatch<2>(p, grid, s);
