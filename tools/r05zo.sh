@@ -1,0 +1,10 @@
+# Winograd LDS kernel: first stage by plain loads + ds_write instead of LDS-DMA; parity, stamps, per-layer A/B
+set -u
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+ORE_LIB=$PWD/onnx-rusty-inference-engine_amd/lib/exp/libore_plain1.so timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
+  tests/test_wino_gpu.py tests/test_config4_gpu.py -k "wino or benched_plan_parity" > gpurun_out/r05zo_tests.log 2>&1 || { tail -30 gpurun_out/r05zo_tests.log; exit 1; }
+tail -1 gpurun_out/r05zo_tests.log
+ORE_LIB=$PWD/onnx-rusty-inference-engine_amd/lib/exp/libore_plain1s.so timeout -k 10 300 python3 -u tools/stamps.py --tag plain1_stamps > gpurun_out/r05zo_stamps.txt 2>&1 || { tail -20 gpurun_out/r05zo_stamps.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/r05zo_stamps.txt
+bash tools/ab_layers.sh r05zo f32 cur plain1 cur plain1

@@ -63,6 +63,10 @@ def wino(lib, ctx, name, tile=40, batch=256):
           f"{int(np.median(pro))}, K loop {int(np.median(kl))} (MFMA content {nks * 32 * 32} per wave), epilogue "
           f"{int(np.median(epi))}, total {int(np.median(st[:, 3] - st[:, 0]))}; p90 total "
           f"{int(np.percentile(st[:, 3] - st[:, 0], 90))}; resident WGs per CU at a WG's start {conc:.2f}")
+    if (st[:, 6] > 0).all():  # tools/patches/wino_stamps_drain.patch: slot 6 after the stores' vmcnt(0)
+        dr = st[:, 6] - st[:, 3]
+        print(f"{name}: epilogue = transform + store issue {int(np.median(epi))} + store drain {int(np.median(dr))} "
+              f"(p10 {int(np.percentile(dr, 10))}, p90 {int(np.percentile(dr, 90))}) cycles, median")
 
 
 def conv1(lib, ctx, batch=256):
@@ -127,7 +131,8 @@ def main():
     import ore
     lib = ctypes.CDLL(ore._lib.LIB_PATH)
     ctx = ore.Context(0)
-    conv1(lib, ctx, a.batch)
+    if hasattr(lib, "ore_debug_stamps_conv1"):  # built with the conv1 stamps too
+        conv1(lib, ctx, a.batch)
     for name in ("f4.e3", "f6.e3", "f8.e3", "f9.e3"):
         wino(lib, ctx, name, batch=a.batch)
 
