@@ -545,14 +545,15 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   const int img1 = t1 / g.TPI, ty1 = (t1 - img1 * g.TPI) / g.TW;
   const int SS = WM_KC * (g.CS + 512);  // floats per stage: [channel][CS] windows, then [channel][4 quads][32 m][4] U
 
-  // the zero blocks (never written by the DMAs)
-  if (threadIdx.x < 2 * WM_KC * WM_ZL)
-    wm_lds[(threadIdx.x >> 6) * SS + ((threadIdx.x >> 3) & 7) * g.CS + (threadIdx.x & 7)] = 0.0f;
-  // the workgroup's 32 biases (0 past M) after the two stages, read by the epilogue: loaded here, so the
-  // prologue's wait for the first chunk covers their latency (a global load in the epilogue exposed it)
-  if (threadIdx.x >= 128 && threadIdx.x < 128 + WM_CH) {
+  // the workgroup's 32 biases (0 past M), read by the epilogue: loaded to a register here and written to
+  // LDS after the first stage's DMAs have issued, so the prologue's wait for the first chunk covers their
+  // latency (a global load in the epilogue exposed it; written to LDS here, before the DMAs, the LDS store
+  // waited for the load and the DMAs behind it: 4.7k of fire4's 7.6k-cycle prologue, stamps r05zp)
+  const bool bias_lane = threadIdx.x >= 128 && threadIdx.x < 128 + WM_CH;
+  float bias_v = 0.0f;
+  if (bias_lane) {
     const int m = m0 + (int)threadIdx.x - 128;
-    wm_lds[2 * SS + (int)threadIdx.x - 128] = p.bias && m < p.M ? p.bias[m] : 0.0f;
+    bias_v = p.bias && m < p.M ? p.bias[m] : 0.0f;
   }
 
   // ---- this lane's tile (lj of the wave's 16) and the run layout of the group
@@ -693,6 +694,10 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   };
 
   stage(0, 0);
+  // the zero blocks (never written by the DMAs) and the biases after the two stages
+  if (threadIdx.x < 2 * WM_KC * WM_ZL)
+    wm_lds[(threadIdx.x >> 6) * SS + ((threadIdx.x >> 3) & 7) * g.CS + (threadIdx.x & 7)] = 0.0f;
+  if (bias_lane) wm_lds[2 * SS + (int)threadIdx.x - 128] = bias_v;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   using st0 = std::integral_constant<int, 0>;

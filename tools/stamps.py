@@ -63,6 +63,10 @@ def wino(lib, ctx, name, tile=40, batch=256):
           f"{int(np.median(pro))}, K loop {int(np.median(kl))} (MFMA content {nks * 32 * 32} per wave), epilogue "
           f"{int(np.median(epi))}, total {int(np.median(st[:, 3] - st[:, 0]))}; p90 total "
           f"{int(np.percentile(st[:, 3] - st[:, 0], 90))}; resident WGs per CU at a WG's start {conc:.2f}")
+    if (st[:, 7] > 0).all():  # tools/patches/wino_stamps_prologue.patch: slot 7 just before the first stage's DMAs
+        ix = st[:, 7] - st[:, 0]
+        print(f"{name}: prologue = index arithmetic + LDS zero / bias {int(np.median(ix))} + first stage DMA to landed "
+              f"{int(np.median(st[:, 1] - st[:, 7]))} cycles, median")
     if (st[:, 6] > 0).all():  # tools/patches/wino_stamps_drain.patch: slot 6 after the stores' vmcnt(0)
         dr = st[:, 6] - st[:, 3]
         print(f"{name}: epilogue = transform + store issue {int(np.median(epi))} + store drain {int(np.median(dr))} "
