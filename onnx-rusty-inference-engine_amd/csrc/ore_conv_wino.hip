@@ -503,9 +503,18 @@ __device__ __forceinline__ void wm_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned l
 // geometry of the LDS kernel (host-computed)
 struct WmGeom {
   int TW, TPI;  // tiles per row / per image
+  float rTW, rTPI, rMT;  // 1 / TW, 1 / TPI, 1 / mtiles (wm_div)
   int CS;       // LDS floats per staged channel: zero block + the longest run set + slack (= 32 mod 64)
   int ntg;      // tile groups of WM_TILES
 };
+
+// n / d for 0 <= n < 2^22 (wm_geom checks the tile count) from a float reciprocal rd = 1 / d: the float
+// quotient is within 0.05 of n / d, so the truncation is the quotient or one below, fixed by the remainder
+__device__ __forceinline__ int wm_div(int n, int d, float rd) {
+  int q = (int)((float)n * rd);
+  q += n - q * d >= d ? 1 : 0;
+  return q;
+}
 
 // rows of image `img` staged for the tile group [t0, t1]: [rs, re], clamped to the image
 __host__ __device__ __forceinline__ void wm_rows(int img, int img0, int ty0, int img1, int ty1, int H, int* rs, int* re) {
@@ -537,12 +546,15 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
   const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
-  const int mt = wgid % p.mtiles, tgi = wgid / p.mtiles;
+  // (integer divisions by reciprocals: the wave-uniform ones back to scalars by readfirstlane)
+  const int tgi = __builtin_amdgcn_readfirstlane(wm_div(wgid, p.mtiles, g.rMT)), mt = wgid - tgi * p.mtiles;
   const int m0 = mt * WM_CH;
   const int T = p.N * g.TPI;
   const int t0 = tgi * WM_TILES, t1 = min(T, t0 + WM_TILES) - 1;
-  const int img0 = t0 / g.TPI, ty0 = (t0 - img0 * g.TPI) / g.TW;
-  const int img1 = t1 / g.TPI, ty1 = (t1 - img1 * g.TPI) / g.TW;
+  const int img0 = __builtin_amdgcn_readfirstlane(wm_div(t0, g.TPI, g.rTPI));
+  const int ty0 = __builtin_amdgcn_readfirstlane(wm_div(t0 - img0 * g.TPI, g.TW, g.rTW));
+  const int img1 = __builtin_amdgcn_readfirstlane(wm_div(t1, g.TPI, g.rTPI));
+  const int ty1 = __builtin_amdgcn_readfirstlane(wm_div(t1 - img1 * g.TPI, g.TW, g.rTW));
   const int SS = WM_KC * (g.CS + 512);  // floats per stage: [channel][CS] windows, then [channel][4 quads][32 m][4] U
 
   // the workgroup's 32 biases (0 past M), read by the epilogue: loaded to a register here and written to
@@ -562,7 +574,7 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   WgTile w;
   w.tok = t < T;
   if (!w.tok) t = T - 1;
-  const int img = t / g.TPI, rem = t - img * g.TPI, ty = rem / g.TW, tx = rem - ty * g.TW;
+  const int img = wm_div(t, g.TPI, g.rTPI), rem = t - img * g.TPI, ty = wm_div(rem, g.TW, g.rTW), tx = rem - ty * g.TW;
   // DMA piece gi of a channel: floats [4 (64 gi + lane), +4) of the run set
   int voff[NDMA];
 #pragma unroll
@@ -762,7 +774,11 @@ static bool wm_geom(const ConvParams& p, WmGeom* g, size_t* lds, int* ndma) {
   g->TW = (p.W + 1) / 2;
   const int TH = (p.H + 1) / 2;
   g->TPI = g->TW * TH;
+  g->rTW = 1.0f / (float)g->TW;
+  g->rTPI = 1.0f / (float)g->TPI;
+  g->rMT = 0.0f;  // set at launch (mtiles)
   const long long T = (long long)p.N * g->TPI;
+  if (T >= (1LL << 22)) return false;  // wm_div's range (4M tiles: 5,700 images at 54 x 54)
   g->ntg = (int)((T + WM_TILES - 1) / WM_TILES);
   // group starts repeat modulo TPI (period TPI / gcd(64, TPI)): every case is among the first TPI
   int tmax = 0;
@@ -776,9 +792,11 @@ static bool wm_geom(const ConvParams& p, WmGeom* g, size_t* lds, int* ndma) {
 }
 
 template <int NDMA, bool RELU>
-static void launch_wm_r(const ConvParams& p0, const WmGeom& g, size_t lds, hipStream_t s) {
+static void launch_wm_r(const ConvParams& p0, const WmGeom& g0, size_t lds, hipStream_t s) {
   ConvParams p = p0;
   p.mtiles = (p.M + WM_CH - 1) / WM_CH;
+  WmGeom g = g0;
+  g.rMT = 1.0f / (float)p.mtiles;
   if (lds > 64 * 1024) {  // above the default dynamic-LDS limit: raise it once per device
     static std::atomic<unsigned long long> raised{0};
     ore_raise_lds_once(raised, reinterpret_cast<const void*>(&conv_winol_kernel<NDMA, RELU>), 160 * 1024);
