@@ -525,6 +525,10 @@ def main():
                                     f"{' (gathered over ' + ('gloo' if gloo else 'RCCL') + ')' if use_dist else ''}: "
                                     f"{'the strict-parity fixture (zoo image + 15 U(-50,50) draws; zoo-calibrated model, softmax max 0.074 on the zoo image)' if args.hw == 224 else 'seeded U(-50,50) images'}"
                                     f" vs the oracle (C restatement of the reference, f32) run live on this host")
+        result["max_abs_comparability"] = ("zoo-calibrated model (conv10 x ZOO_LOGIT_GAIN) since round 5; rounds 1-4 "
+                                           "sampled the uncalibrated He-normal model, whose peakier logits put the "
+                                           "same f32 roundings at up to ~1e-5 (DESIGN.md 5.1): not comparable across "
+                                           "that change")
         # the reporting legs run at N = 1 only (the CPU baseline on rank 0 at N = 1), so no
         # rank waits on the others' collectives meanwhile
         if world == 1:

@@ -582,8 +582,11 @@ __global__ __launch_bounds__(512, 1) void conv_band_pool_f32_kernel(ConvParams p
       // per 32-channel fragment i: its K loop (both pixels), then its pooled contributions, whose LDS
       // max operations drain under the next fragment's MFMAs.  A wave whose pairs all lie past the band
       // (the band's last, partial step) skips both: its SIMD partner runs alone (its A ring already holds
-      // the next step's first groups)
-      if ((s << 8) + 32 * wave < npairs) {
+      // the next step's first groups).  The condition is wave-uniform by construction (readfirstlane): the
+      // DPP neighbour exchange below must run with every lane of the wave enabled -- a DPP read from a lane
+      // that EXEC disables returns 0 (bound_ctrl) -- and tests/test_isa_guard.py checks the compiled kernel
+      // for an EXEC-masked exchange
+      if (__builtin_amdgcn_readfirstlane((s << 8) + 32 * wave - npairs) < 0) {
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
         c3f16 acc[2];
@@ -670,13 +673,19 @@ __global__ __launch_bounds__(512, 1) void conv_band_pool_f32_kernel(ConvParams p
 
 }  // namespace
 
+bool conv_band_pool_f32_geometry(int C, int M, int kh, int kw, int sh, int sw, int pt, int pl, int W, int Wo, int ep_Ho,
+                                 int ep_Wo, int ep_pt, int ep_pl, int sq_M, bool relu) {
+  const int HP = (Wo + ep_pl + 1) / 2;
+  return sq_M >= 1 && sq_M <= 16 && relu && C == 3 && M > 64 && M <= 96 && kh == 7 && kw == 7 && sh == 2 && sw == 2 &&
+         pt == 0 && pl == 0 && W <= CB_RW && W % 4 == 0 && HP >= 52 && ep_Wo <= CB_RPW && ep_Ho >= 1 && ep_pl <= 1 &&
+         ep_pt <= 1;
+}
+
 bool conv_band_pool_f32_eligible(const ConvParams& p, const C1SqueezeF32* sq) {
-  const int HP = (p.Wo + p.ep_pl + 1) / 2;
-  return sq && sq->M >= 1 && sq->M <= 16 && sq->w && sq->bias && sq->y && sq->y_ps >= p.ep_Ho * p.ep_Wo &&
-         p.relu && p.C == 3 && p.M > 64 && p.M <= 96 && p.kh == 7 && p.kw == 7 && p.sh == 2 && p.sw == 2 &&
-         p.pt == 0 && p.pl == 0 && p.W <= CB_RW && p.W % 4 == 0 && p.x_ps % 4 == 0 && p.x_nstride % 4 == 0 &&
-         p.x_ps >= p.H * p.W && HP >= 52 && p.ep_Wo <= CB_RPW && p.ep_Ho >= 1 && p.ep_pl <= 1 && p.ep_pt <= 1 &&
-         (long long)3 * p.x_ps * 4 < (1LL << 30);
+  return sq && sq->w && sq->bias && sq->y && sq->y_ps >= p.ep_Ho * p.ep_Wo &&
+         conv_band_pool_f32_geometry(p.C, p.M, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.W, p.Wo, p.ep_Ho, p.ep_Wo, p.ep_pt,
+                                     p.ep_pl, sq->M, p.relu != 0) &&
+         p.x_ps % 4 == 0 && p.x_nstride % 4 == 0 && p.x_ps >= p.H * p.W && (long long)3 * p.x_ps * 4 < (1LL << 30);
 }
 
 void launch_conv_band_pool_f32(const ConvParams& p, const float* wc, const C1SqueezeF32& sq, hipStream_t s) {

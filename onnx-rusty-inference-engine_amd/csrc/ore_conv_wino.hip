@@ -492,7 +492,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
 // Each position is the same c-ordered fma chain and the transforms the same add order as tiles 0-3:
 // bit-identical to them.
 constexpr int WM_KC = 8;      // input channels per K chunk (2 k-steps of 4)
-constexpr int WM_TILES = 64;  // 2x2 tiles per workgroup (16 per wave)
+constexpr int WM_TILES = 64;  // 2x2 tiles per 4-wave workgroup (16 per wave; 128 with 8 waves, tile 5)
 constexpr int WM_CH = 32;     // output channels per workgroup
 constexpr int WM_ZL = 8;      // zero floats at the start of a staged channel (rows outside the image)
 
@@ -502,14 +502,17 @@ __device__ __forceinline__ void wm_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned l
 
 // geometry of the LDS kernel (host-computed)
 struct WmGeom {
-  int TW, TPI;  // tiles per row / per image
-  float rTW, rTPI, rMT;  // 1 / TW, 1 / TPI, 1 / mtiles (wm_div)
-  int CS;       // LDS floats per staged channel: zero block + the longest run set + slack (= 32 mod 64)
-  int ntg;      // tile groups of WM_TILES
+  int TW, TPI;            // tiles per row / per image
+  float rTW, rTPI, rNMG;  // 1 / TW, 1 / TPI, 1 / nmg (wm_div)
+  int CS;                 // LDS floats per staged channel: zero block + the longest run set + slack (= 32 mod 64)
+  int ntg;                // tile groups of 16 NW tiles
+  int mbs;                // 32-channel m-blocks per workgroup (its m-group)
+  int nmg;                // m-groups per tile group = ceil(mtiles / mbs)
 };
 
-// n / d for 0 <= n < 2^22 (wm_geom checks the tile count) from a float reciprocal rd = 1 / d: the float
-// quotient is within 0.05 of n / d, so the truncation is the quotient or one below, fixed by the remainder
+// n / d for 0 <= n < 2^22 (wm_geom checks the workgroup and tile counts) from a float reciprocal rd = 1 / d:
+// the float quotient is within (n / d) 2^-23 < 1 / (2 d) of n / d, so the truncation is the quotient or one
+// below, fixed by the remainder
 __device__ __forceinline__ int wm_div(int n, int d, float rd) {
   int q = (int)((float)n * rd);
   q += n - q * d >= d ? 1 : 0;
@@ -523,8 +526,8 @@ __host__ __device__ __forceinline__ void wm_rows(int img, int img0, int ty0, int
 }
 
 // floats staged per channel for the tile group starting at t0 (each image's run + 1, rounded up to 4)
-static int wm_group_floats(long long t0, long long T, int TPI, int TW, int H, int W) {
-  const long long t1 = std::min(T, t0 + WM_TILES) - 1;
+static int wm_group_floats(long long t0, long long T, int TPI, int TW, int H, int W, int tiles) {
+  const long long t1 = std::min(T, t0 + tiles) - 1;
   const int img0 = (int)(t0 / TPI), ty0 = (int)(t0 % TPI) / TW;
   const int img1 = (int)(t1 / TPI), ty1 = (int)(t1 % TPI) / TW;
   int total = 0;
@@ -536,35 +539,44 @@ static int wm_group_floats(long long t0, long long T, int TPI, int TW, int H, in
   return total;
 }
 
-template <int NDMA, bool RELU>  // NDMA: 256-float DMA pieces per staged channel (ceil(longest run set / 256))
-__global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom g) {
+// Round 6: a workgroup owns a tile group x an m-group of mbs 32-channel blocks and walks the blocks in turn
+// (each of the 4-8 channel blocks of a tile group re-ran the whole prologue -- the index
+// arithmetic, the run layout, the first stage's latency -- for only C / 8 chunks of MFMAs).  The chunk
+// pipeline runs on across the blocks: the last chunk of block b stages chunk 0 of block b + 1 (the same
+// windows, the next block's U), so only the workgroup's first stage is exposed, and block b's epilogue
+// (output transform, stores) runs while that stage lands.  The per-block arithmetic is unchanged (each
+// position one c-ordered chain, the same transforms): bit-identical to one block per workgroup.
+// NW: waves per workgroup, 4 (two workgroups per CU) or 8 (one per CU: the two waves of a SIMD share one staged
+// copy of the chunk's U and of the window rows of 128 tiles, half the DMA pieces per wave; tile 5)
+template <int NDMA, bool RELU, int NW>  // NDMA: 256-float DMA pieces per staged channel (ceil(longest run set / 256))
+__global__ __launch_bounds__(64 * NW, 8 / NW) void conv_winol_kernel(ConvParams p, WmGeom g) {
+  constexpr int TILES = 16 * NW;
   extern __shared__ __attribute__((aligned(16))) float wm_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // block -> (tile group, 32-channel block), the channel blocks of a tile group consecutive (one XCD:
-  // they share the staged rows in L2)
+  // block -> (tile group, m-group), the m-groups of a tile group consecutive (one XCD: they share the staged
+  // rows in L2)
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, rr8 = nwg & 7;
   const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (bid >> 3);
   // (integer divisions by reciprocals: the wave-uniform ones back to scalars by readfirstlane)
-  const int tgi = __builtin_amdgcn_readfirstlane(wm_div(wgid, p.mtiles, g.rMT)), mt = wgid - tgi * p.mtiles;
-  const int m0 = mt * WM_CH;
+  const int tgi = __builtin_amdgcn_readfirstlane(wm_div(wgid, g.nmg, g.rNMG)), mg = wgid - tgi * g.nmg;
+  const int mb0 = mg * g.mbs, mb1 = min(p.mtiles, mb0 + g.mbs);
+  const int mw0 = mb0 * WM_CH, nch = (mb1 - mb0) * WM_CH;  // the workgroup's channels [mw0, mw0 + nch)
   const int T = p.N * g.TPI;
-  const int t0 = tgi * WM_TILES, t1 = min(T, t0 + WM_TILES) - 1;
+  const int t0 = tgi * TILES, t1 = min(T, t0 + TILES) - 1;
   const int img0 = __builtin_amdgcn_readfirstlane(wm_div(t0, g.TPI, g.rTPI));
   const int ty0 = __builtin_amdgcn_readfirstlane(wm_div(t0 - img0 * g.TPI, g.TW, g.rTW));
   const int img1 = __builtin_amdgcn_readfirstlane(wm_div(t1, g.TPI, g.rTPI));
   const int ty1 = __builtin_amdgcn_readfirstlane(wm_div(t1 - img1 * g.TPI, g.TW, g.rTW));
   const int SS = WM_KC * (g.CS + 512);  // floats per stage: [channel][CS] windows, then [channel][4 quads][32 m][4] U
 
-  // the workgroup's 32 biases (0 past M), read by the epilogue: loaded to a register here and written to
-  // LDS after the first stage's DMAs have issued, so the prologue's wait for the first chunk covers their
-  // latency (a global load in the epilogue exposed it; written to LDS here, before the DMAs, the LDS store
-  // waited for the load and the DMAs behind it: 4.7k of fire4's 7.6k-cycle prologue, stamps r05zp)
-  const bool bias_lane = threadIdx.x >= 128 && threadIdx.x < 128 + WM_CH;
+  // the workgroup's biases (0 past M), read by the epilogues: loaded to a register here and written to LDS
+  // after the first stage's DMAs have issued, so the prologue's wait for the first chunk covers their latency
+  const bool bias_lane = (int)threadIdx.x < nch;
   float bias_v = 0.0f;
   if (bias_lane) {
-    const int m = m0 + (int)threadIdx.x - 128;
+    const int m = mw0 + (int)threadIdx.x;
     bias_v = p.bias && m < p.M ? p.bias[m] : 0.0f;
   }
 
@@ -612,33 +624,35 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
   w.r1ok = 2 * ty + 1 < p.H;
   const int au = (WM_KC * g.CS + lk * 512 + lj * 4) * 4;  // bytes: U[c = lk][quad 0][m = lj] of a k-step
 
-  // ---- DMA sources: wave w stages channels w and w + 4 of a chunk, and U pieces d = w + 4 v
+  // ---- DMA sources: wave w stages channels w (and w + 4 with 4 waves) of a chunk, and U pieces d = w + NW v
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ur =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.wp), (short)0, p.C * p.Mp * 16 * 4, 0x00020000);
   const int uq = 2 * (wave & 1) + (lane >> 5);
-  const int uoff = (uq * p.Mp + m0 + (lane & 31)) * 16;
+  const int uoff = (uq * p.Mp + (lane & 31)) * 16;  // the block's first channel goes in the scalar offset
   const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) float*)wm_lds;
-  const int nchunks = p.C / WM_KC;
-  auto stage = [&](int kc, int st) __attribute__((always_inline)) {
+  const int nchunks = p.C / WM_KC;  // even (C % 16 == 0): chunk 0 of every block uses stage 0
+  // chunk kc's windows and U of channels [m0, m0 + 32) -> stage st
+  auto stage = [&](int kc, int m0, int st) __attribute__((always_inline)) {
     const unsigned sb = lds0 + (unsigned)(st * SS) * 4;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int cc = wave + 4 * h;
+    for (int h = 0; h < 8 / NW; ++h) {
+      const int cc = wave + NW * h;
       const int so = (kc * WM_KC + cc) * p.x_ps * 4 - 4 * (cc & 1);  // odd channels: one float early (>= 0)
 #pragma unroll
       for (int gi = 0; gi < NDMA; ++gi)
         if (voff[gi] >= 0) wm_dma16(xr, sb + (cc * g.CS + WM_ZL + 256 * gi) * 4, voff[gi], so);
     }
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int d = wave + 4 * v, cc = d >> 1;
-      wm_dma16(ur, sb + (WM_KC * g.CS + (cc * 4 + 2 * (d & 1)) * 128) * 4, uoff, (kc * WM_KC + cc) * 4 * p.Mp * 16);
+    for (int v = 0; v < 16 / NW; ++v) {
+      const int d = wave + NW * v, cc = d >> 1;
+      wm_dma16(ur, sb + (WM_KC * g.CS + (cc * 4 + 2 * (d & 1)) * 128) * 4, uoff,
+               ((kc * WM_KC + cc) * 4 * p.Mp + m0) * 16);
     }
   };
 
-  // accumulators: no zeroing -- chunk 0's first k-step takes C = 0 (an inline operand of the MFMA; 128
+  // accumulators: no zeroing -- each block's first k-step takes C = 0 (an inline operand of the MFMA; 128
   // v_mov per wave otherwise, and f32 MFMAs and VALU share the SIMD's issue, nothing overlaps them)
   wg_floatx4 acc[16][2];
   const wg_floatx4 zero4 = {0.f, 0.f, 0.f, 0.f};
@@ -663,11 +677,21 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
     }
     wg_input_transform_pk(d, v);
   };
-  // one chunk (two k-steps of 4 channels); FIRST: chunk 0, its first k-step starts the accumulators
-  auto chunk = [&](int kc, auto first, auto stc) __attribute__((always_inline)) {
+  // one chunk (two k-steps of 4 channels) of the block at m0; FIRST: chunk 0, its first k-step starts the
+  // accumulators.  It first stages the next job: chunk kc + 1 of this block, or chunk 0 of the next block
+  // (more), or nothing
+  // PRE: chunk 0 of a block after the first, whose next job (chunk 1) was staged before the previous block's
+  // epilogue (see the block loop)
+  auto chunk = [&](int kc, int m0, bool more, auto first, auto stc, auto prec) __attribute__((always_inline)) {
     constexpr bool FIRST = decltype(first)::value;
     constexpr int st = decltype(stc)::value;  // kc & 1, a constant: the stage's LDS bases are loop-invariant
-    if (kc + 1 < nchunks) stage(kc + 1, st ^ 1);
+    constexpr bool PRE = decltype(prec)::value;
+    if constexpr (!PRE) {
+      if (kc + 1 < nchunks)
+        stage(kc + 1, m0, st ^ 1);
+      else if (more)
+        stage(0, m0 + WM_CH, st ^ 1);
+    }
     const int sto0 = st * SS * 4, sto1 = sto0 + 4 * g.CS * 4;  // k-step 1: channels 4 .. 7 of the chunk
     wg_floatx4 ua[2][4];
     wg_f2 d0[4][2], d1[4][2], v[8];  // v[2 i + h][e]: position 4 i + 2 h + e
@@ -701,131 +725,177 @@ __global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom
         for (int f = 0; f < 2; ++f)
           acc[4 * q + j][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[f][q][j], v[2 * q + (j >> 1)][j & 1], acc[4 * q + j][f], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk kc + 1 have landed
-    __syncthreads();  // ... every wave's, and every wave is done reading stage kc & 1
+    // this wave's DMAs of the next job have landed (vmcnt counts DMAs and stores in issue order: after an
+    // epilogue, whose >= 16 stores followed them, the stores need not have completed)
+    if constexpr (PRE)
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // ... every wave's, and every wave is done reading stage st
   };
 
-  stage(0, 0);
+  stage(0, mw0, 0);
   // the zero blocks (never written by the DMAs) and the biases after the two stages
   if (threadIdx.x < 2 * WM_KC * WM_ZL)
     wm_lds[(threadIdx.x >> 6) * SS + ((threadIdx.x >> 3) & 7) * g.CS + (threadIdx.x & 7)] = 0.0f;
-  if (bias_lane) wm_lds[2 * SS + (int)threadIdx.x - 128] = bias_v;
+  if (bias_lane) wm_lds[2 * SS + (int)threadIdx.x] = bias_v;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  using st0 = std::integral_constant<int, 0>;
-  using st1 = std::integral_constant<int, 1>;
-  chunk(0, std::true_type{}, st0{});
-  int kc = 1;
-  for (; kc + 1 < nchunks; kc += 2) {  // chunk pairs: odd, even
-    chunk(kc, std::false_type{}, st1{});
-    chunk(kc + 1, std::false_type{}, st0{});
-  }
-  if (kc < nchunks) chunk(kc, std::false_type{}, st1{});
-  // lane (lk, lj) of fragment f holds rows 4 lk + e = channel m0 + 16 f + 4 lk + e of tile lj
-  wg_floatx4 bv[2];
-#pragma unroll
-  for (int f = 0; f < 2; ++f) bv[f] = *reinterpret_cast<const wg_floatx4*>(wm_lds + 2 * SS + 16 * f + 4 * lk);
-  // stores without branches: 8-B row stores whose offsets past the output (invalid tiles, rows, channels,
-  // tiles without a second column) the buffer range check drops; when some lane's tile lacks its second
-  // column (the right edge of an odd-width plane; fast = false for the wave) also 4-B first-column stores
+  // stores without branches: 8-B row stores at per-lane byte offsets fixed for the kernel (the tile, channel
+  // 4 lk), with the block's channel as the scalar offset; a missing tile, row or second column (the right
+  // edge of an odd-width plane) has its offset past the output (the buffer range check drops the store), and
+  // a wave with such right-edge tiles (fast = false) also issues their 4-B first-column stores.  Channels
+  // past M (a partial last block) take the per-lane check
+  const int oob = 0x7FFFFFF0;
+  const int ylane = (w.ybase + 4 * lk * p.y_ps) * 4;
+  const int so0 = w.tok && w.c1ok ? ylane : oob, so1 = w.tok && w.c1ok && w.r1ok ? ylane + p.W * 4 : oob;
+  const int se0 = w.tok && !w.c1ok ? ylane : oob, se1 = w.tok && !w.c1ok && w.r1ok ? ylane + p.W * 4 : oob;
   const bool fast = __builtin_amdgcn_ballot_w64(w.tok && !w.c1ok) == 0;
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, 0x7FFFFFF0, 0x00020000);
   typedef int wg_i2 __attribute__((ext_vector_type(2)));
+  // (an epilogue issues 16 8-B stores per wave, 32 stores with the right-edge ones: the vmcnt(16) of the
+  // next chunk relies on >= 16)
   // the output transform and bias of channels (e, e + 1) on packed f32 (acc[xi][f] holds e = 0 .. 3 in
-  // consecutive registers); the same adds in the same order as wg_store_t
+  // consecutive registers), the same adds in the same order as wg_store_t, then the stores; MOK: channel
+  // checks (a partial last block)
+  auto epilogue = [&](int m0, auto mokc) __attribute__((always_inline)) {
+    constexpr bool MOK = decltype(mokc)::value;
+    // lane (lk, lj) of fragment f holds rows 4 lk + e = channel m0 + 16 f + 4 lk + e of tile lj
+    wg_floatx4 bv[2];
 #pragma unroll
-  for (int f = 0; f < 2; ++f)
+    for (int f = 0; f < 2; ++f)
+      bv[f] = *reinterpret_cast<const wg_floatx4*>(wm_lds + 2 * SS + (m0 - mw0) + 16 * f + 4 * lk);
 #pragma unroll
-    for (int ep = 0; ep < 4; ep += 2) {
-      const int mp = m0 + 16 * f + 4 * lk + ep;
-      wg_f2 mx[16], y[4];
+    for (int f = 0; f < 2; ++f)
 #pragma unroll
-      for (int xi = 0; xi < 16; ++xi) mx[xi] = ep == 0 ? acc[xi][f].xy : acc[xi][f].zw;
-      wg_output_transform_pk(mx, y);
-      const wg_f2 b2 = {bv[f][ep], bv[f][ep + 1]};
+      for (int ep = 0; ep < 4; ep += 2) {
+        wg_f2 mx[16], y[4];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        float o[4];
+        for (int xi = 0; xi < 16; ++xi) mx[xi] = ep == 0 ? acc[xi][f].xy : acc[xi][f].zw;
+        wg_output_transform_pk(mx, y);
+        const wg_f2 b2 = {bv[f][ep], bv[f][ep + 1]};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          o[q] = (y[q] + b2)[h];
-          if constexpr (RELU) o[q] = fmaxf(o[q], 0.0f);
-        }
-        const bool mok = mp + h < p.M;
-        const int yo = (w.ybase + (mp + h) * p.y_ps) * 4;
-        const int oob = 0x7FFFFFF0;
-        const bool ok0 = w.tok && mok, ok1 = ok0 && w.r1ok;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(wg_i2, (wg_f2){o[0], o[1]}), yr,
-                                              ok0 && w.c1ok ? yo : oob, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(wg_i2, (wg_f2){o[2], o[3]}), yr,
-                                              ok1 && w.c1ok ? yo + p.W * 4 : oob, 0, 0);
-        if (!fast) {  // tiles at the right edge of an odd-width plane: their first column only
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, o[0]), yr, ok0 && !w.c1ok ? yo : oob, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, o[2]), yr, ok1 && !w.c1ok ? yo + p.W * 4 : oob,
-                                                0, 0);
+        for (int h = 0; h < 2; ++h) {
+          float o[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            o[q] = (y[q] + b2)[h];
+            if constexpr (RELU) o[q] = fmaxf(o[q], 0.0f);
+          }
+          const int c = m0 + 16 * f + ep + h;  // the channel of lane group lk = 0
+          const int soff = c * p.y_ps * 4;
+          int a0 = so0, a1 = so1, e0 = se0, e1 = se1;
+          if constexpr (MOK) {
+            const bool mok = c + 4 * lk < p.M;
+            a0 = mok ? a0 : oob; a1 = mok ? a1 : oob; e0 = mok ? e0 : oob; e1 = mok ? e1 : oob;
+          }
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(wg_i2, (wg_f2){o[0], o[1]}), yr, a0, soff, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(wg_i2, (wg_f2){o[2], o[3]}), yr, a1, soff, 0);
+          if (!fast) {  // tiles at the right edge of an odd-width plane: their first column only
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, o[0]), yr, e0, soff, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, o[2]), yr, e1, soff, 0);
+          }
         }
       }
+  };
+  using st0 = std::integral_constant<int, 0>;
+  using st1 = std::integral_constant<int, 1>;
+  // the blocks in turn.  At a block boundary the next block's chunk 1 is staged (stage 1 is free once the
+  // last chunk's barrier has passed) BEFORE the epilogue's stores: vmcnt counts loads, stores and LDS-DMA
+  // in issue order, so chunk 0's wait for those DMAs then does not wait for the stores
+  using pre0 = std::false_type;
+  using pre1 = std::true_type;
+  for (int mb = mb0; mb < mb1; ++mb) {
+    const int m0 = mb * WM_CH;
+    const bool more = mb + 1 < mb1;
+    if (mb == mb0)
+      chunk(0, m0, more, std::true_type{}, st0{}, pre0{});
+    else
+      chunk(0, m0, more, std::true_type{}, st0{}, pre1{});
+    int kc = 1;
+    for (; kc + 1 < nchunks; kc += 2) {  // chunk pairs: odd, even
+      chunk(kc, m0, more, std::false_type{}, st1{}, pre0{});
+      chunk(kc + 1, m0, more, std::false_type{}, st0{}, pre0{});
     }
+    chunk(kc, m0, more, std::false_type{}, st1{}, pre0{});  // the last, odd chunk (nchunks is even)
+    if (more) stage(1, m0 + WM_CH, 1);  // the next block's chunk 1
+    if (m0 + WM_CH <= p.M)
+      epilogue(m0, std::false_type{});
+    else
+      epilogue(m0, std::true_type{});
+  }
 }
 
+// workgroups the m-grouping keeps at least (4 per resident slot of a 256-CU part at two per CU): the blocks of
+// a tile group are shared out only as far as the launch stays this wide
+constexpr long long WM_MIN_WG = 2048;
+constexpr int WM_MAX_MBS = 8;
+
 // the LDS kernel's geometry; false when the layer does not fit it
-static bool wm_geom(const ConvParams& p, WmGeom* g, size_t* lds, int* ndma) {
-  if (p.C % WM_KC != 0 || p.C <= 0 || p.H <= 0 || p.W <= 0) return false;
+static bool wm_geom(const ConvParams& p, int nw, WmGeom* g, size_t* lds, int* ndma) {
+  const int tiles = 16 * nw;
+  if (p.C % 16 != 0 || p.C <= 0 || p.H <= 0 || p.W <= 0 || p.M <= 0) return false;
   g->TW = (p.W + 1) / 2;
   const int TH = (p.H + 1) / 2;
   g->TPI = g->TW * TH;
   g->rTW = 1.0f / (float)g->TW;
   g->rTPI = 1.0f / (float)g->TPI;
-  g->rMT = 0.0f;  // set at launch (mtiles)
   const long long T = (long long)p.N * g->TPI;
   if (T >= (1LL << 22)) return false;  // wm_div's range (4M tiles: 5,700 images at 54 x 54)
-  g->ntg = (int)((T + WM_TILES - 1) / WM_TILES);
-  // group starts repeat modulo TPI (period TPI / gcd(64, TPI)): every case is among the first TPI
+  g->ntg = (int)((T + tiles - 1) / tiles);
+  // m-blocks per workgroup: the largest divisor of the block count that keeps >= WM_MIN_WG workgroups
+  const int mtiles = (p.M + WM_CH - 1) / WM_CH;
+  g->mbs = 1;
+  for (int b = 2; b <= std::min(mtiles, WM_MAX_MBS); ++b)
+    if (mtiles % b == 0 && (long long)g->ntg * (mtiles / b) * nw >= WM_MIN_WG * 4) g->mbs = b;
+  g->nmg = (mtiles + g->mbs - 1) / g->mbs;
+  g->rNMG = 1.0f / (float)g->nmg;
+  if ((long long)g->ntg * g->nmg >= (1LL << 22)) return false;  // wm_div's range for the workgroup id
+  // group starts repeat modulo TPI (period TPI / gcd(tiles, TPI)): every case is among the first TPI
   int tmax = 0;
   const long long ng = std::min<long long>(g->ntg, g->TPI);
   for (long long gi = 0; gi < ng; ++gi)
-    tmax = std::max(tmax, wm_group_floats(gi * WM_TILES, T, g->TPI, g->TW, p.H, p.W));
+    tmax = std::max(tmax, wm_group_floats(gi * tiles, T, g->TPI, g->TW, p.H, p.W, tiles));
   *ndma = (tmax + 255) / 256;
   g->CS = (WM_ZL + tmax + 5 + 31) / 64 * 64 + 32;  // + 1: odd channels' shift, + 4: the last window's overrun
-  *lds = (size_t)2 * WM_KC * (g->CS + 512) * 4 + WM_CH * 4;  // two stages + the biases
+  *lds = (size_t)2 * WM_KC * (g->CS + 512) * 4 + (size_t)g->mbs * WM_CH * 4;  // two stages + the biases
   return *ndma <= 8 && *lds <= 160 * 1024;
 }
 
-template <int NDMA, bool RELU>
-static void launch_wm_r(const ConvParams& p0, const WmGeom& g0, size_t lds, hipStream_t s) {
+template <int NDMA, bool RELU, int NW>
+static void launch_wm_r(const ConvParams& p0, const WmGeom& g, size_t lds, hipStream_t s) {
   ConvParams p = p0;
   p.mtiles = (p.M + WM_CH - 1) / WM_CH;
-  WmGeom g = g0;
-  g.rMT = 1.0f / (float)p.mtiles;
   if (lds > 64 * 1024) {  // above the default dynamic-LDS limit: raise it once per device
     static std::atomic<unsigned long long> raised{0};
-    ore_raise_lds_once(raised, reinterpret_cast<const void*>(&conv_winol_kernel<NDMA, RELU>), 160 * 1024);
+    ore_raise_lds_once(raised, reinterpret_cast<const void*>(&conv_winol_kernel<NDMA, RELU, NW>), 160 * 1024);
   }
-  hipLaunchKernelGGL((conv_winol_kernel<NDMA, RELU>), dim3((unsigned)(g.ntg * p.mtiles)), dim3(256), lds, s, p, g);
+  hipLaunchKernelGGL((conv_winol_kernel<NDMA, RELU, NW>), dim3((unsigned)(g.ntg * g.nmg)), dim3(64 * NW), lds, s, p, g);
 }
 
-template <int NDMA>
+template <int NDMA, int NW>
 static void launch_wm(const ConvParams& p, const WmGeom& g, size_t lds, hipStream_t s) {
   if (p.relu)
-    launch_wm_r<NDMA, true>(p, g, lds, s);
+    launch_wm_r<NDMA, true, NW>(p, g, lds, s);
   else
-    launch_wm_r<NDMA, false>(p, g, lds, s);
+    launch_wm_r<NDMA, false, NW>(p, g, lds, s);
 }
 
+template <int NW>
 static void launch_winol(const ConvParams& p, hipStream_t s) {
   WmGeom g;
   size_t lds = 0;
   int ndma = 0;
-  if (!wm_geom(p, &g, &lds, &ndma)) return;  // the caller checked conv_wino_eligible
+  if (!wm_geom(p, NW, &g, &lds, &ndma)) return;  // the caller checked conv_wino_eligible
   switch (ndma) {
-    case 1: launch_wm<1>(p, g, lds, s); break;
-    case 2: launch_wm<2>(p, g, lds, s); break;
-    case 3: launch_wm<3>(p, g, lds, s); break;
-    case 4: launch_wm<4>(p, g, lds, s); break;
-    case 5: launch_wm<5>(p, g, lds, s); break;
-    case 6: launch_wm<6>(p, g, lds, s); break;
-    case 7: launch_wm<7>(p, g, lds, s); break;
-    default: launch_wm<8>(p, g, lds, s); break;
+    case 1: launch_wm<1, NW>(p, g, lds, s); break;
+    case 2: launch_wm<2, NW>(p, g, lds, s); break;
+    case 3: launch_wm<3, NW>(p, g, lds, s); break;
+    case 4: launch_wm<4, NW>(p, g, lds, s); break;
+    case 5: launch_wm<5, NW>(p, g, lds, s); break;
+    case 6: launch_wm<6, NW>(p, g, lds, s); break;
+    case 7: launch_wm<7, NW>(p, g, lds, s); break;
+    default: launch_wm<8, NW>(p, g, lds, s); break;
   }
 }
 
@@ -833,7 +903,8 @@ static void launch_winol(const ConvParams& p, hipStream_t s) {
 // 2x2 tiles per wave, A / B ring depths of the unrolled K loop
 struct WinoTile { int shape, ch, tiles, da, db; };
 static const WinoTile WINO_TILES[WINO_TILES_N] = {{32, 32, 32, 2, 8}, {32, 32, 32, 2, 4}, {16, 32, 16, 2, 8},
-                                                  {16, 16, 32, 2, 4}, {0, WM_CH, WM_TILES, 0, 0}};  // 4: conv_winol_kernel
+                                                  {16, 16, 32, 2, 4}, {0, WM_CH, WM_TILES, 0, 0},  // 4: conv_winol_kernel
+                                                  {0, WM_CH, 2 * WM_TILES, 0, 0}};  // 5: conv_winol_kernel, 8 waves
 
 bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo) {
   return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && Ho == H && Wo == W && C % 16 == 0 && C > 0;
@@ -841,11 +912,12 @@ bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, i
 
 bool conv_wino_eligible(const ConvParams& p, int tile) {
   if (tile < 0 || tile >= WINO_TILES_N) return false;
-  if (tile == 4) {
+  if (tile == 4 || tile == 5) {
     WmGeom g;
     size_t lds;
     int ndma;
-    return conv_wino_geometry(p.C, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.H, p.W, p.Ho, p.Wo) && wm_geom(p, &g, &lds, &ndma) &&
+    return conv_wino_geometry(p.C, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.H, p.W, p.Ho, p.Wo) &&
+           wm_geom(p, tile == 5 ? 8 : 4, &g, &lds, &ndma) &&
            p.x_bytes > 0 && p.x_bytes < (1LL << 31) - (1LL << 21) && (reinterpret_cast<uintptr_t>(p.x) & 3) == 0 &&
            p.Mp % 64 == 0 && (long long)p.C * p.Mp * 64 < (1LL << 31) &&
            (long long)p.N * ((p.H + 1) / 2) * ((p.W + 1) / 2) < (1LL << 30) &&
@@ -868,8 +940,11 @@ static void wg_grid(ConvParams& p, int ch, int tiles, dim3* grid) {
 }
 
 void launch_conv_wino(const ConvParams& p0, int tile, hipStream_t s) {
-  if (tile == 4) {
-    launch_winol(p0, s);
+  if (tile == 4 || tile == 5) {
+    if (tile == 5)
+      launch_winol<8>(p0, s);
+    else
+      launch_winol<4>(p0, s);
     return;
   }
   ConvParams p = p0;

@@ -180,6 +180,8 @@ struct ore_model {
 
 namespace {
 
+bool band_step(const Step& s);  // the band walker's geometry (below, beside step_tile_family)
+
 // IEEE binary16 -> binary32 (exact)
 float half_bits_to_float(uint16_t h) {
   const uint32_t sign = uint32_t(h & 0x8000) << 16;
@@ -1015,12 +1017,12 @@ struct Planner {
         // untuned: the band walker for batches that give every CU an image (one workgroup per band of an
         // image; it bands smaller batches but the window kernel's patches fill the chip better there),
         // else the window kernel; an autotuned / set choice (epv 7 or 8) is kept
-        if (cv.plan.epv != EPOOL_BAND_VARIANT && cv.plan.epv != EPOOL_WIN_VARIANT)
-          cv.plan.epv = m->max_batch >= 128 ? EPOOL_BAND_VARIANT : EPOOL_WIN_VARIANT;
       }
       cv.c1sq = true;
       cv.sq_b = val(q.in2).cptr;
       cv.sq_M = q.M;
+      if (!f16 && cv.plan.epv != EPOOL_BAND_VARIANT && cv.plan.epv != EPOOL_WIN_VARIANT)
+        cv.plan.epv = m->max_batch >= 128 && band_step(cv) ? EPOOL_BAND_VARIANT : EPOOL_WIN_VARIANT;
       val(cv.out).elided = true;
       cv.out = q.out;
       cv.flops_per_img += q.flops_per_img;
@@ -1081,8 +1083,9 @@ struct Planner {
       if (!plain_1x1(e1) || e1.in2 < 0 || !e1.wp || (e1.C != 32 && e1.C != 64) || e1.M % 16 || e1.H != cv.pH ||
           e1.W != cv.pW || e3.kind != S_CONV || e3.epool || e3.pool)
         continue;
-      if (!private_value(cc.in0) || !private_value(cc.in1) || val(e1.in0).es != 4 || val(e1.in0).nhwc ||
-          val(cc.in0).alias_of >= 0 || val(cc.in1).alias_of >= 0)
+      // the Concat's only reader is this launch: e1's slice of it is never written
+      if (!private_value(cc.in0) || !private_value(cc.in1) || !private_value(cc.out) || val(e1.in0).es != 4 ||
+          val(e1.in0).nhwc || val(cc.in0).alias_of >= 0 || val(cc.in1).alias_of >= 0)
         continue;
       PoolConvParams q{};  // the kernel's limits with e1 inside
       q.C = int(cv.C); q.H = int(cv.pH); q.W = int(cv.pW); q.Hp = int(cv.pwin.Ho); q.Wp = int(cv.pwin.Wo);
@@ -1648,11 +1651,22 @@ namespace {
 
 // the tile ids a step may run (its kernel family): autotune candidates and ore_model_set_step_tile's
 // accepted values; empty for steps with one fixed kernel
+// the band walker's geometry for a fused f32 first conv + pool + squeeze step (its layout checks are the
+// launch's: a layout it declines runs the window kernel)
+bool band_step(const Step& s) {
+  return conv_band_pool_f32_geometry(int(s.C), int(s.M), int(s.kh), int(s.kw), int(s.sh), int(s.sw), int(s.win.pt),
+                                     int(s.win.pl), int(s.W), int(s.win.Wo), int(s.ep_win.Ho), int(s.ep_win.Wo),
+                                     int(s.ep_win.pt), int(s.ep_win.pl), int(s.sq_M), s.relu);
+}
+
 std::vector<int> step_tile_family(const Step& s) {
   std::vector<int> c;
   if (s.kind != S_CONV && s.kind != S_MATMUL) return c;
   if (s.kind == S_CONV && s.epool && !s.plan.f16) {  // f32 pooled conv: patch / row-walk variants, the window kernel
-    if (s.c1sq) return {EPOOL_WIN_TILE, EPOOL_BAND_TILE};  // the fused squeeze: window kernel, band walker
+    if (s.c1sq) {  // the fused squeeze: window kernel, band walker (where its geometry allows it)
+      if (band_step(s)) return {EPOOL_WIN_TILE, EPOOL_BAND_TILE};
+      return {EPOOL_WIN_TILE};
+    }
     for (int v = 1; v <= 5; ++v) c.push_back(EPOOL_TILE_BASE + v);
     if (s.wc1) c.push_back(EPOOL_WIN_TILE);
     return c;

@@ -1,0 +1,81 @@
+"""CPU: guards on the machine code of the built libore.so (gfx950), read with the ROCm binutils from the
+library's offload bundle; no kernel runs.
+
+The band walker (conv_band_pool_f32_kernel, ore_conv1_f32.hip) takes the pooled neighbour column of a
+lane from lane l + 1 by a DPP wave_shl:1 read with bound_ctrl (an out-of-range source reads 0).  A DPP
+read returns 0 from a source lane that EXEC disables, so the exchange is only right while every lane of
+the wave executes it.  Round 5 saw a restructured epilogue give wrong pooled maxima (VERDICT r05 item 2,
+DESIGN.md 3.4b); this test pins the properties the product relies on, so that an edit which moves the
+exchange under divergent control flow fails here, on the CPU, before it can reach the GPU tests."""
+import os
+import re
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+import ore
+from ore import _lib
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+BUNDLER = os.path.join(LLVM, "clang-offload-bundler")
+OBJDUMP = os.path.join(LLVM, "llvm-objdump")
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _tools():
+    return os.path.exists(BUNDLER) and os.path.exists(OBJDUMP) and shutil.which("objcopy")
+
+
+def _kernel_isa(symbol_part):
+    """Disassembly lines of the first kernel whose symbol contains symbol_part."""
+    with tempfile.TemporaryDirectory() as d:
+        fat = os.path.join(d, "fat.bin")
+        subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", _lib.LIB_PATH, fat], check=True)
+        data = open(fat, "rb").read()
+        starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)] + [len(data)]
+        for i in range(len(starts) - 1):
+            part = os.path.join(d, f"b{i}.bin")
+            open(part, "wb").write(data[starts[i]:starts[i + 1]])
+            elf = os.path.join(d, f"b{i}.elf")
+            r = subprocess.run([BUNDLER, "--unbundle", "--type=o", f"--input={part}",
+                                "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={elf}"],
+                               capture_output=True)
+            if r.returncode != 0 or not os.path.exists(elf):
+                continue
+            dis = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", elf], capture_output=True, text=True).stdout
+            lines, on = [], False
+            for ln in dis.splitlines():
+                m = re.match(r"^[0-9a-f]+ <(.*)>:", ln)
+                if m:
+                    if on:
+                        return lines
+                    on = symbol_part in m.group(1)
+                    continue
+                if on and ln.startswith("\t"):
+                    ins = ln.strip().split("//")[0].strip()
+                    if ins:
+                        lines.append(ins)
+            if on:
+                return lines
+    return None
+
+
+@pytest.mark.skipif(not _tools(), reason="ROCm binutils / objcopy not present")
+def test_band_walker_dpp_exchange_runs_with_full_exec():
+    ore.load()
+    isa = _kernel_isa("conv_band_pool_f32_kernel")
+    assert isa, "conv_band_pool_f32_kernel not found in libore.so"
+    dpp = [k for k, i in enumerate(isa) if "wave_shl:1" in i]
+    # 16 channel rows per 32-channel fragment, 3 fragments per step (the compiler may duplicate the step)
+    assert dpp and len(dpp) % 16 == 0, len(dpp)
+    for k in dpp:
+        ins = isa[k]
+        # all rows and banks written, an out-of-range source (lane 63) reads 0
+        assert "row_mask:0xf" in ins and "bank_mask:0xf" in ins and "bound_ctrl:1" in ins, ins
+        # the last instruction before it that writes EXEC restores it (the end of a divergent region); an
+        # s_and_saveexec / s_and / s_andn2 of exec here would mean the exchange runs EXEC-masked
+        last = next((isa[j] for j in range(k - 1, -1, -1) if re.match(r"s_\w+ exec, ", isa[j])
+                     or "saveexec" in isa[j]), None)
+        assert last is None or re.match(r"s_(or|mov)_b64 exec, ", last), (ins, last)

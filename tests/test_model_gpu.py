@@ -1034,6 +1034,53 @@ def test_pool_expand_fused_bit_identical(gpu_ctx, case):
         np.testing.assert_allclose(outs[0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-5)
 
 
+def test_pool_expand_shared_concat_not_fused(gpu_ctx):
+    """ORE_FUSE_POOL_EXPAND leaves e1's Concat slice unwritten, so it must not fire when the Concat has
+    another reader: here GlobalAveragePool(cat) joins the graph output.  The plan keeps
+    expand1x1 as its own launch (same step count with and without the bit), and the whole output,
+    including the GAP of the Concat, matches the oracle."""
+    import ore
+    import oracle
+    from ore import onnx_wire as wr
+    C, H, W, S1, E1, E3, S2, pads = (16, 54, 54, 32, 128, 128, 32, [0, 0, 1, 1])
+    rng = np.random.default_rng(77)
+    shapes = {"wq": (S1, C, 1, 1), "w1": (E1, S1, 1, 1), "w3": (E3, S1, 3, 3), "wn": (S2, E1 + E3, 1, 1)}
+    inits, vinfo = [], [wr.encode_value_info("x", (1, C, H, W))]
+    for n, shp in shapes.items():
+        fan = shp[1] * shp[2] * shp[3]
+        w = (rng.standard_normal(shp) * np.sqrt(2.0 / fan)).astype(np.float32)
+        b = rng.uniform(-0.1, 0.1, shp[0]).astype(np.float32)
+        inits += [wr.encode_tensor(n, w), wr.encode_tensor("b" + n, b)]
+        vinfo += [wr.encode_value_info(n, w.shape), wr.encode_value_info("b" + n, b.shape)]
+    conv = lambda i, w, o, p: wr.encode_node("Conv", [i, w, "b" + w], [o], attrs=[
+        wr.encode_attr_ints("pads", p), wr.encode_attr_ints("strides", [1, 1])])
+    nodes = [conv("x", "wq", "q", [0] * 4), wr.encode_node("Relu", ["q"], ["qr"]),
+             conv("qr", "w1", "e1", [0] * 4), wr.encode_node("Relu", ["e1"], ["e1r"]),
+             conv("qr", "w3", "e3", [1] * 4), wr.encode_node("Relu", ["e3"], ["e3r"]),
+             wr.encode_node("Concat", ["e1r", "e3r"], ["cat"], attrs=[wr.encode_attr_int("axis", 1)]),
+             wr.encode_node("MaxPool", ["cat"], ["p"], attrs=[
+                 wr.encode_attr_ints("kernel_shape", [3, 3]), wr.encode_attr_ints("strides", [2, 2]),
+                 wr.encode_attr_string("auto_pad", "NOTSET"), wr.encode_attr_ints("pads", pads)]),
+             conv("p", "wn", "n", [0] * 4), wr.encode_node("Relu", ["n"], ["nr"]),
+             wr.encode_node("GlobalAveragePool", ["nr"], ["y1"]),
+             wr.encode_node("GlobalAveragePool", ["cat"], ["g2"]),
+             wr.encode_node("Concat", ["y1", "g2"], ["y"], attrs=[wr.encode_attr_int("axis", 1)])]
+    mb = wr.encode_model("firepool_shared", nodes, inits, vinfo, [wr.encode_value_info("y", (1, S2 + E1 + E3, 1, 1))])
+    x = np.random.default_rng(5).standard_normal((3, C, H, W)).astype(np.float32)
+    ref = oracle.Model(mb).run(x, S2 + E1 + E3)
+    outs, nsteps = [], []
+    for on in (True, False):
+        m = ore.Model(gpu_ctx, mb, max_batch=3)
+        m.set_fusion(ore.FUSE_ALL if on else ore.FUSE_ALL & ~ore.FUSE_POOL_EXPAND)
+        outs.append(_np(m.run(_t(x))))
+        nsteps.append(len(m.tiles()))
+        assert not any("expand1x1+" in st["name"] for st in m.steps()), [st["name"] for st in m.steps()]
+        m.close()
+    assert nsteps[0] == nsteps[1], nsteps
+    np.testing.assert_array_equal(outs[0], outs[1])
+    np.testing.assert_allclose(outs[0].reshape(ref.shape), ref, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("B", [3, 256])
 def test_squeezenet_pool_expand_fused(gpu_ctx, B):
     """SqueezeNet-1.0 @224 f32 (Winograd plan): fire4/expand1x1 inside pool3 + fire5/squeeze1x1
