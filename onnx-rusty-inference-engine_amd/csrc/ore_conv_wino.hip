@@ -492,7 +492,7 @@ __global__ __launch_bounds__(256, 1) void conv_wino16_kernel(ConvParams p) {
 // Each position is the same c-ordered fma chain and the transforms the same add order as tiles 0-3:
 // bit-identical to them.
 constexpr int WM_KC = 8;      // input channels per K chunk (2 k-steps of 4)
-constexpr int WM_TILES = 64;  // 2x2 tiles per 4-wave workgroup (16 per wave; 128 with 8 waves, tile 5)
+constexpr int WM_TILES = 64;  // 2x2 tiles per workgroup (16 per wave)
 constexpr int WM_CH = 32;     // output channels per workgroup
 constexpr int WM_ZL = 8;      // zero floats at the start of a staged channel (rows outside the image)
 
@@ -505,7 +505,7 @@ struct WmGeom {
   int TW, TPI;            // tiles per row / per image
   float rTW, rTPI, rNMG;  // 1 / TW, 1 / TPI, 1 / nmg (wm_div)
   int CS;                 // LDS floats per staged channel: zero block + the longest run set + slack (= 32 mod 64)
-  int ntg;                // tile groups of 16 NW tiles
+  int ntg;                // tile groups of WM_TILES
   int mbs;                // 32-channel m-blocks per workgroup (its m-group)
   int nmg;                // m-groups per tile group = ceil(mtiles / mbs)
 };
@@ -546,11 +546,12 @@ static int wm_group_floats(long long t0, long long T, int TPI, int TW, int H, in
 // windows, the next block's U), so only the workgroup's first stage is exposed, and block b's epilogue
 // (output transform, stores) runs while that stage lands.  The per-block arithmetic is unchanged (each
 // position one c-ordered chain, the same transforms): bit-identical to one block per workgroup.
-// NW: waves per workgroup, 4 (two workgroups per CU) or 8 (one per CU: the two waves of a SIMD share one staged
-// copy of the chunk's U and of the window rows of 128 tiles, half the DMA pieces per wave; tile 5)
-template <int NDMA, bool RELU, int NW>  // NDMA: 256-float DMA pieces per staged channel (ceil(longest run set / 256))
-__global__ __launch_bounds__(64 * NW, 8 / NW) void conv_winol_kernel(ConvParams p, WmGeom g) {
-  constexpr int TILES = 16 * NW;
+// (Measured and rejected, round 6: 8-wave workgroups of 128 tiles, one per CU, whose two waves per SIMD share one
+// staged copy of each chunk -- half the DMA pieces per wave, but both partners of a SIMD then meet at every
+// barrier: fire8 297 -> 342 us, profiles/r06_wino_ablations.txt.)
+template <int NDMA, bool RELU>  // NDMA: 256-float DMA pieces per staged channel (ceil(longest run set / 256))
+__global__ __launch_bounds__(256, 2) void conv_winol_kernel(ConvParams p, WmGeom g) {
+  constexpr int NW = 4, TILES = WM_TILES;
   extern __shared__ __attribute__((aligned(16))) float wm_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -624,7 +625,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_winol_kernel(ConvParams 
   w.r1ok = 2 * ty + 1 < p.H;
   const int au = (WM_KC * g.CS + lk * 512 + lj * 4) * 4;  // bytes: U[c = lk][quad 0][m = lj] of a k-step
 
-  // ---- DMA sources: wave w stages channels w (and w + 4 with 4 waves) of a chunk, and U pieces d = w + NW v
+  // ---- DMA sources: wave w stages channels w and w + 4 of a chunk, and U pieces d = w + 4 v
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), (short)0, (int)p.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ur =
@@ -832,8 +833,8 @@ constexpr long long WM_MIN_WG = 2048;
 constexpr int WM_MAX_MBS = 8;
 
 // the LDS kernel's geometry; false when the layer does not fit it
-static bool wm_geom(const ConvParams& p, int nw, WmGeom* g, size_t* lds, int* ndma) {
-  const int tiles = 16 * nw;
+static bool wm_geom(const ConvParams& p, WmGeom* g, size_t* lds, int* ndma) {
+  const int tiles = WM_TILES;
   if (p.C % 16 != 0 || p.C <= 0 || p.H <= 0 || p.W <= 0 || p.M <= 0) return false;
   g->TW = (p.W + 1) / 2;
   const int TH = (p.H + 1) / 2;
@@ -847,7 +848,7 @@ static bool wm_geom(const ConvParams& p, int nw, WmGeom* g, size_t* lds, int* nd
   const int mtiles = (p.M + WM_CH - 1) / WM_CH;
   g->mbs = 1;
   for (int b = 2; b <= std::min(mtiles, WM_MAX_MBS); ++b)
-    if (mtiles % b == 0 && (long long)g->ntg * (mtiles / b) * nw >= WM_MIN_WG * 4) g->mbs = b;
+    if (mtiles % b == 0 && (long long)g->ntg * (mtiles / b) >= WM_MIN_WG) g->mbs = b;
   g->nmg = (mtiles + g->mbs - 1) / g->mbs;
   g->rNMG = 1.0f / (float)g->nmg;
   if ((long long)g->ntg * g->nmg >= (1LL << 22)) return false;  // wm_div's range for the workgroup id
@@ -862,40 +863,39 @@ static bool wm_geom(const ConvParams& p, int nw, WmGeom* g, size_t* lds, int* nd
   return *ndma <= 8 && *lds <= 160 * 1024;
 }
 
-template <int NDMA, bool RELU, int NW>
+template <int NDMA, bool RELU>
 static void launch_wm_r(const ConvParams& p0, const WmGeom& g, size_t lds, hipStream_t s) {
   ConvParams p = p0;
   p.mtiles = (p.M + WM_CH - 1) / WM_CH;
   if (lds > 64 * 1024) {  // above the default dynamic-LDS limit: raise it once per device
     static std::atomic<unsigned long long> raised{0};
-    ore_raise_lds_once(raised, reinterpret_cast<const void*>(&conv_winol_kernel<NDMA, RELU, NW>), 160 * 1024);
+    ore_raise_lds_once(raised, reinterpret_cast<const void*>(&conv_winol_kernel<NDMA, RELU>), 160 * 1024);
   }
-  hipLaunchKernelGGL((conv_winol_kernel<NDMA, RELU, NW>), dim3((unsigned)(g.ntg * g.nmg)), dim3(64 * NW), lds, s, p, g);
+  hipLaunchKernelGGL((conv_winol_kernel<NDMA, RELU>), dim3((unsigned)(g.ntg * g.nmg)), dim3(256), lds, s, p, g);
 }
 
-template <int NDMA, int NW>
+template <int NDMA>
 static void launch_wm(const ConvParams& p, const WmGeom& g, size_t lds, hipStream_t s) {
   if (p.relu)
-    launch_wm_r<NDMA, true, NW>(p, g, lds, s);
+    launch_wm_r<NDMA, true>(p, g, lds, s);
   else
-    launch_wm_r<NDMA, false, NW>(p, g, lds, s);
+    launch_wm_r<NDMA, false>(p, g, lds, s);
 }
 
-template <int NW>
 static void launch_winol(const ConvParams& p, hipStream_t s) {
   WmGeom g;
   size_t lds = 0;
   int ndma = 0;
-  if (!wm_geom(p, NW, &g, &lds, &ndma)) return;  // the caller checked conv_wino_eligible
+  if (!wm_geom(p, &g, &lds, &ndma)) return;  // the caller checked conv_wino_eligible
   switch (ndma) {
-    case 1: launch_wm<1, NW>(p, g, lds, s); break;
-    case 2: launch_wm<2, NW>(p, g, lds, s); break;
-    case 3: launch_wm<3, NW>(p, g, lds, s); break;
-    case 4: launch_wm<4, NW>(p, g, lds, s); break;
-    case 5: launch_wm<5, NW>(p, g, lds, s); break;
-    case 6: launch_wm<6, NW>(p, g, lds, s); break;
-    case 7: launch_wm<7, NW>(p, g, lds, s); break;
-    default: launch_wm<8, NW>(p, g, lds, s); break;
+    case 1: launch_wm<1>(p, g, lds, s); break;
+    case 2: launch_wm<2>(p, g, lds, s); break;
+    case 3: launch_wm<3>(p, g, lds, s); break;
+    case 4: launch_wm<4>(p, g, lds, s); break;
+    case 5: launch_wm<5>(p, g, lds, s); break;
+    case 6: launch_wm<6>(p, g, lds, s); break;
+    case 7: launch_wm<7>(p, g, lds, s); break;
+    default: launch_wm<8>(p, g, lds, s); break;
   }
 }
 
@@ -903,8 +903,7 @@ static void launch_winol(const ConvParams& p, hipStream_t s) {
 // 2x2 tiles per wave, A / B ring depths of the unrolled K loop
 struct WinoTile { int shape, ch, tiles, da, db; };
 static const WinoTile WINO_TILES[WINO_TILES_N] = {{32, 32, 32, 2, 8}, {32, 32, 32, 2, 4}, {16, 32, 16, 2, 8},
-                                                  {16, 16, 32, 2, 4}, {0, WM_CH, WM_TILES, 0, 0},  // 4: conv_winol_kernel
-                                                  {0, WM_CH, 2 * WM_TILES, 0, 0}};  // 5: conv_winol_kernel, 8 waves
+                                                  {16, 16, 32, 2, 4}, {0, WM_CH, WM_TILES, 0, 0}};  // 4: conv_winol_kernel
 
 bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo) {
   return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && Ho == H && Wo == W && C % 16 == 0 && C > 0;
@@ -912,12 +911,11 @@ bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, i
 
 bool conv_wino_eligible(const ConvParams& p, int tile) {
   if (tile < 0 || tile >= WINO_TILES_N) return false;
-  if (tile == 4 || tile == 5) {
+  if (tile == 4) {
     WmGeom g;
     size_t lds;
     int ndma;
-    return conv_wino_geometry(p.C, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.H, p.W, p.Ho, p.Wo) &&
-           wm_geom(p, tile == 5 ? 8 : 4, &g, &lds, &ndma) &&
+    return conv_wino_geometry(p.C, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.H, p.W, p.Ho, p.Wo) && wm_geom(p, &g, &lds, &ndma) &&
            p.x_bytes > 0 && p.x_bytes < (1LL << 31) - (1LL << 21) && (reinterpret_cast<uintptr_t>(p.x) & 3) == 0 &&
            p.Mp % 64 == 0 && (long long)p.C * p.Mp * 64 < (1LL << 31) &&
            (long long)p.N * ((p.H + 1) / 2) * ((p.W + 1) / 2) < (1LL << 30) &&
@@ -940,11 +938,8 @@ static void wg_grid(ConvParams& p, int ch, int tiles, dim3* grid) {
 }
 
 void launch_conv_wino(const ConvParams& p0, int tile, hipStream_t s) {
-  if (tile == 4 || tile == 5) {
-    if (tile == 5)
-      launch_winol<8>(p0, s);
-    else
-      launch_winol<4>(p0, s);
+  if (tile == 4) {
+    launch_winol(p0, s);
     return;
   }
   ConvParams p = p0;

@@ -400,16 +400,14 @@ constexpr int CONV_TILES_F16 = 4;
 // 3x3 / stride-1 / pad-1 f32 conv by Winograd F(2x2, 3x3) on the f32 MFMA (ore_conv_wino.hip).  Tiles
 // WINO_TILE_BASE + 0..3 = 32 ch x 32 tiles (32x32x2 MFMA, ring 4 / 2), 32 x 16, 16 x 32 (16x16x4);
 // 4 = the LDS-staged kernel (64 tiles x 32 channels per 4-wave block, windows and U from LDS; C % 16 == 0),
-// 5 = the same with 8-wave blocks of 128 tiles (one block per CU, one staged copy per chunk for both waves of a SIMD);
 // results do not depend on the tile (not bit-identical to the direct kernels).  Weights packed by
 // launch_pack_wino: U = s_xi (G g G^T)[xi] as [C][4][Mp][4] f32 (channel, position quad, m, position)
 // (Mp = wino_packed_mp(M)), with the sign s_xi = -1 for positions xi % 4 == 3 (+1 otherwise): every kernel's
 // V carries the same sign (wg_input_transform / _pk), so each product U_xi V_xi is the unsigned one.
 // tile ids 28-35 are retired (ABI 1's opt-in bf16x3 kernels, ORE_LOAD_X3)
 constexpr int WINO_TILE_BASE = 36;
-constexpr int WINO_TILES_N = 6;
-// fused-kernel ids after the Winograd tiles (ore.Model.TILE_NAMES): 41 (the round-2 Winograd fire module, retired)
-// is the 8-wave Winograd LDS kernel since round 6
+constexpr int WINO_TILES_N = 5;
+// fused-kernel ids after the Winograd tiles (ore.Model.TILE_NAMES): 41 is retired (the Winograd fire module)
 constexpr int FIRE_F16_TILE = 42, C1_POOL_F16_TILE = 43;
 constexpr int CONV_GAP_F16_TILE = 49;  // conv1x1_gap_f16_kernel: ore.Model.TILE_NAMES "conv1x1 gap f16"
 constexpr int CONV_GAP_F32_TILE = 50;  // conv1x1_gap_f32_kernel: ore.Model.TILE_NAMES "conv1x1 gap f32"

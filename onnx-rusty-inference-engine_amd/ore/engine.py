@@ -320,7 +320,7 @@ class Model:
                   "epool walk64 b3", None,  # 27: the 2-band walker
                   None, None, None, None, None, None, None, None,  # 28-35: ABI 1's bf16x3 kernels
                   "wino 32x32 d4", "wino 32x32 d2", "wino16 32x16", "wino16 16x32",
-                  "wino lds", "wino lds 8w",  # 41: the 8-wave LDS kernel (round 6; was the retired Winograd fire module)
+                  "wino lds", None,  # 41: the Winograd fire module (retired)
                   "fire f16", "first conv pool f16", "epool window f32", "fire pool f32",
                   "stream1x1 persist 32x128", "stream1x1 persist 64x64", "stream1x1 persist 16x256",
                   "conv1x1 gap f16", "conv1x1 gap f32", "epool band f32"]
