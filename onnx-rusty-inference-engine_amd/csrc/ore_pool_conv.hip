@@ -53,9 +53,16 @@ constexpr int PS_AUX = 2;
 // SIMD), pool5 + squeeze 107-109 -> 102 us; 4 rows for pool5 measured 110 us (four waves per SIMD)
 __host__ __device__ constexpr int ps_pr(int /*nf: fragments per pooled row*/) { return 3; }
 
+// n / d for 0 <= n < 2^11, 1 <= d < 2^9 by a multiply and a shift: mg = ceil(2^20 / d) (computed once, uniform);
+// n mg / 2^20 is within n 2^-20 < 2^-9 above n / d, below the next integer: exact (round 6: the staging
+// geometry's runtime divisions were ~40 VALU each, with quarter-rate multiplies)
+__device__ __forceinline__ int ps_div(int n, unsigned mg) { return (int)(__umul24((unsigned)n, mg) >> 20); }
+__device__ __forceinline__ unsigned ps_magic(int d) { return (unsigned)(((1u << 20) + d - 1) / d); }
+
 // NF: 16-pixel fragments per pooled row (Wp <= 16 NF); KS1: e1's k-steps (0: no e1); FRW: e1 pixel fragments
-// per wave (>= ceil(ceil((2 PS_PR + 1) W / 16) / 4))
-template <int NF, int KS1, int FRW>
+// per wave (>= ceil(ceil((2 PS_PR + 1) W / 16) / 4)); SPLIT: waves per 16-channel block of the squeeze (2: M <= 32
+// on two blocks, each wave takes half the pooled-pixel fragments, so all four waves issue squeeze MFMAs)
+template <int NF, int KS1, int FRW, int SPLIT>
 __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p) {
   constexpr int PS_PR = ps_pr(NF);
   constexpr int PS_ROWS = 2 * PS_PR + 1;  // input rows of PS_PR pooled rows (3x3, stride 2)
@@ -103,14 +110,16 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
     const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(p.s + (long long)img * p.s_nstride), (short)0, 4 * KS1 * p.s_ps * 4, 0x00020000);
     const int hw = p.H * p.W;
+    const unsigned mgw = ps_magic(p.W);
 #pragma unroll
     for (int i = 0; i < FRW; ++i) {
-      const int px = 16 * (wave + 4 * i) + lj, r = px / p.W, g = ih0 * p.W + px;
+      const int px = 16 * (wave + 4 * i) + lj, r = ps_div(px, mgw), g = ih0 * p.W + px;
       const bool in = px < bpx && g >= 0 && g < hw;
+      // the lane's channel lk at pixel g; k-step t's channels 4 t + lk: + 16 t s_ps bytes, the scalar offset
+      const int vo = in ? (lk * p.s_ps + g) * 4 : (int)0x80000000;
 #pragma unroll
       for (int t = 0; t < KS1; ++t)
-        sb[i][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                 sr, in ? ((4 * t + lk) * p.s_ps + g) * 4 : (int)0x80000000, 0, 0));
+        sb[i][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(sr, vo, 16 * t * p.s_ps, 0));
       e1_off[i] = px < bpx && (unsigned)(ih0 + r) < (unsigned)p.H ? r * PS_RS + PS_LC + (px - r * p.W) : -1;
     }
     for (int i = tid; i < p.E1; i += 256) b1_s[i] = p.b1[i];
@@ -124,12 +133,14 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
   unsigned qm[PS_NQ];
   auto group_geom = [&]() __attribute__((always_inline)) {
     const int nq = (p.W + 3) / 4, nld = PS_CH * PS_ROWS * nq;
+    const unsigned mrow = ps_magic(PS_ROWS * nq), mq = ps_magic(nq);
 #pragma unroll
     for (int u = 0; u < PS_NQ; ++u) {
       const int q = tid + 256 * u;
-      const int c = q / (PS_ROWS * nq), rc = q - c * (PS_ROWS * nq), r = rc / nq, j = rc - r * nq;
+      const int c = ps_div(q, mrow), rc = q - c * (PS_ROWS * nq), r = ps_div(rc, mq), j = rc - r * nq;
       const int ih = ih0 + r;
       const bool rin = (unsigned)ih < (unsigned)p.H;
+      // -1: no group (not loaded, not stored); a row outside the image: past the records (reads 0)
       qo[u] = q < nld ? (rin ? (c * p.x_ps + ih * p.W + 4 * j) * 4 : (int)0x80000000) : -1;
       qs[u] = (c * PS_ROWS + r) * PS_RS + PS_LC + 4 * j;
       unsigned mk = 0;
@@ -140,18 +151,22 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
   };
   ps4 xv[PS_NQ];
   auto load_chunk = [&](int c0) __attribute__((always_inline)) {
+    // the chunk's first channel as the scalar offset (qo < 0 lies past the records either way)
 #pragma unroll
     for (int u = 0; u < PS_NQ; ++u)
-      xv[u] = __builtin_bit_cast(ps4, __builtin_amdgcn_raw_buffer_load_b128(
-                                          xr, qo[u] < 0 ? (int)0x80000000 : qo[u] + c0 * p.x_ps * 4, 0, PS_AUX));
+      xv[u] = __builtin_bit_cast(ps4, __builtin_amdgcn_raw_buffer_load_b128(xr, qo[u], c0 * p.x_ps * 4, PS_AUX));
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  ps4 acc[PS_PR * NF];  // rows 4 lk + e of channels 16 wave .., pixel 16 fr + lj of pooled row n
+  // the wave's squeeze share: channels m0 .. m0 + 15 at pooled-pixel fragments n0 .. n0 + NFW - 1 (fragment n:
+  // pooled row n / NF, columns 16 (n % NF) ..)
+  constexpr int NFW = PS_PR * NF / SPLIT;
+  static_assert(PS_PR * NF % SPLIT == 0, "fragments split evenly");
+  ps4 acc[NFW];  // rows 4 lk + e of channels m0 .., pixel 16 (n % NF) + lj of pooled row n / NF, n = n0 + i
 #pragma unroll
-  for (int n = 0; n < PS_PR * NF; ++n) acc[n] = ps4{0.f, 0.f, 0.f, 0.f};
+  for (int n = 0; n < NFW; ++n) acc[n] = ps4{0.f, 0.f, 0.f, 0.f};
   const int nch = p.C / PS_CH;
-  const int m0 = 16 * wave;
+  const int m0 = 16 * (wave / SPLIT), n0 = NFW * (wave % SPLIT);
   // the squeeze's A values of a chunk (k = PS_CH ci + 4 t + lk, row m0 + lj), one chunk ahead
   constexpr int KS = PS_CH / 4;  // k-steps per chunk
   float acur[KS], anxt[KS];
@@ -273,16 +288,16 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
     __syncthreads();
     // squeeze k-steps of this chunk: k = PS_CH ci + 4 t + lk
     if (m0 < p.M) {  // every B value read before the MFMAs: one LDS round trip, not one per k-step
-      float bq[KS][PS_PR * NF];
+      float bq[KS][NFW];
 #pragma unroll
       for (int t = 0; t < KS; ++t)
 #pragma unroll
-        for (int n = 0; n < PS_PR * NF; ++n) bq[t][n] = pt[4 * t + lk][16 * n + lj];
+        for (int n = 0; n < NFW; ++n) bq[t][n] = pt[4 * t + lk][16 * (n0 + n) + lj];
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int t = 0; t < KS; ++t)
 #pragma unroll
-        for (int n = 0; n < PS_PR * NF; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(acur[t], bq[t][n], acc[n], 0, 0, 0);
+        for (int n = 0; n < NFW; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(acur[t], bq[t][n], acc[n], 0, 0, 0);
     }
 #pragma unroll
     for (int t = 0; t < KS; ++t) acur[t] = anxt[t];
@@ -296,7 +311,8 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
   // bias + Relu, NCHW stores: channel m0 + 4 lk + e, pooled pixel (pr0 + n / NF, 16 (n % NF) + lj)
   if (m0 >= p.M) return;
 #pragma unroll
-  for (int n = 0; n < PS_PR * NF; ++n) {
+  for (int i = 0; i < NFW; ++i) {
+    const int n = n0 + i;
     const int prow = pr0 + n / NF, pcol = 16 * (n % NF) + lj;
     if (prow >= p.Hp || pcol >= p.Wp) continue;
     float* yp = p.y + (long long)img * p.y_nstride + prow * p.Wp + pcol;
@@ -304,7 +320,7 @@ __global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p)
     for (int e = 0; e < 4; ++e) {
       const int m = m0 + 4 * lk + e;
       if (m >= p.M) continue;
-      float v = acc[n][e] + (p.bias ? p.bias[m] : 0.0f);
+      float v = acc[i][e] + (p.bias ? p.bias[m] : 0.0f);
       if (p.relu) v = fmaxf(v, 0.0f);
       yp[(long long)m * p.y_ps] = v;
     }
@@ -331,7 +347,14 @@ bool pool_conv1x1_f32_eligible(const PoolConvParams& p) {
 
 template <int NF, int KS1, int FRW>
 static void ps_launch(const PoolConvParams& p, long long grid, hipStream_t s) {
-  hipLaunchKernelGGL((pool_conv1x1_f32_kernel<NF, KS1, FRW>), dim3((unsigned)grid), dim3(256), 0, s, p);
+  // two waves per 16-channel block when the squeeze has <= 32 channels and the fragments split evenly
+  if constexpr (ps_pr(NF) * NF % 2 == 0) {
+    if (p.M <= 32) {
+      hipLaunchKernelGGL((pool_conv1x1_f32_kernel<NF, KS1, FRW, 2>), dim3((unsigned)grid), dim3(256), 0, s, p);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((pool_conv1x1_f32_kernel<NF, KS1, FRW, 1>), dim3((unsigned)grid), dim3(256), 0, s, p);
 }
 
 template <int NF, int KS1>
