@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "ore_kernels.h"
 
@@ -358,6 +359,232 @@ static bool c1_dispatch(const ConvParams& p, const C1Squeeze& sq, unsigned grid,
   return false;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Round 6: the f16 first conv + pool + squeeze as a band walker (the f32 kernel of the same
+// name is ore_conv1_f32.hip's conv_band_pool_f32_kernel).  The patch kernel above computes 256 conv pixels per
+// 13 x 19 patch for 220 used (the halo is recomputed by the neighbouring patch) and spends most of each tile in
+// its pooled-epilogue chain (three barriers per 32-channel fragment).  Here one workgroup of 8 waves per CU owns
+// an image and walks its conv rows in steps of four (SqueezeNet conv1: 28 steps of 4 x 109 conv columns):
+//   * wave w computes conv row 4 s + w / 2 of the step, column pairs 31 (w & 1) + lr (two 32-pixel fragments of
+//     v_mfma_f32_32x32x16_f16, the pair's two columns), all 96 channels; every conv output is computed once
+//     (the pair shared by the two waves of a row aside: 1 of 63);
+//   * A (the packed weights, the patch kernel's permuted rows) sits in LDS for the workgroup's life; B reads
+//     the step's 13 input rows, staged in LDS as f16 NHWC4 (rounded as the patch kernel's window: the same
+//     operands, k order and MFMA chain, so every conv output has the same bits);
+//   * after bias, Relu and the f16 rounding (ore_f16_epilogue8, as the patch kernel), the pair's pooled column
+//     takes max(col 2j, 2j + 1, 2j + 2) on the f16 bits (values >= +0 order like their bits) -- the third by
+//     DPP wave_shl:1 from lane lr + 1, with every lane of the wave enabled (tests/test_isa_guard.py) -- into a
+//     ring of horizontally pooled conv rows [6 slots][56 columns][96 channels] (one writer per cell: no atomics);
+//   * a step completes pooled rows 2 s - 1 and 2 s (conv rows 4 s - 2 .. 4 s + 2): waves 0-3 take their 3-row
+//     maxima (the nine values of the patch kernel's max, exact) as the squeeze's B operands and run its six
+//     MFMAs per fragment in the patch kernel's order; bias, Relu, one rounding, 16-B NHWC stores.
+// Two barriers per step.  Bit-identical to the patch kernel (tests/test_f16_gpu.py::test_f16_conv1_band_*).
+constexpr int FB_RW = 264;                                  // window row stride (pixels; reads reach col 257)
+constexpr int FB_WR = 13;                                   // window rows: 4 conv rows per step (2 * 3 + 7)
+constexpr int FB_SLOTS = 6;                                 // ring of conv rows 4 s - 2 .. 4 s + 3
+constexpr int FB_HC = 56;                                   // ring columns (pooled columns <= 55)
+constexpr int FB_CHS = 104;                                 // ring channel stride (halves): 96 + 8
+constexpr int FB_KS = 14;                                   // k-steps: 7 rows x 8 taps x 4 channels / 16
+constexpr int FB_W_HALVES = FB_KS * 96 * 16;                // 43008 B
+constexpr int FB_WIN_HALVES = FB_WR * FB_RW * 4;            // 27456 B
+constexpr int FB_RING_HALVES = FB_SLOTS * FB_HC * FB_CHS;   // 69888 B
+constexpr int FB_NU = (FB_WR * 56 + 511) / 512;             // window units (row, 4 columns) per thread (2)
+constexpr int FB_LDS = (FB_W_HALVES + FB_WIN_HALVES + FB_RING_HALVES) * 2 + (96 + 32) * 4;
+
+__global__ __launch_bounds__(512, 1) void conv_band_pool_f16_kernel(ConvParams p, C1Squeeze sq) {
+  constexpr int MF = 3;
+  extern __shared__ __attribute__((aligned(16))) _Float16 fbs[];
+  _Float16* Ws = fbs;                                                    // [KS][96][16]
+  _Float16* win = Ws + FB_W_HALVES;                                      // [13][264][4]
+  _Float16* ring = win + FB_WIN_HALVES;                                  // [6][56][104]
+  float* sbias = reinterpret_cast<float*>(ring + FB_RING_HALVES);        // [96]
+  float* qbias = sbias + 96;                                             // [32]
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Kp = (p.K + 31) & ~31;
+  const _Float16* __restrict__ wh = reinterpret_cast<const _Float16*>(p.wp);  // [Mp][Kp]
+  // weights once, as the patch kernel stages them: LDS row R of each 32-row block <- packed row (R & ~31) +
+  // 16 (i >> 1) + 8 hh + 4 (i & 1) + j for R % 32 = 8 i + 4 hh + j (rows past M zero)
+  for (int q = tid; q < FB_KS * MF * 64; q += 512) {
+    const int t = q / (MF * 64), rem = q - t * (MF * 64), R = rem >> 1, hh8 = rem & 1;
+    const int r = R & 31, i = r >> 3, hq = (r >> 2) & 1, j = r & 3;
+    const int m = (R & ~31) + 16 * (i >> 1) + 8 * hq + 4 * (i & 1) + j;
+    c1h8 v = {};
+    if (m < p.M) v = *reinterpret_cast<const c1h8*>(wh + m * Kp + 16 * t + 8 * hh8);
+    *reinterpret_cast<c1h8*>(Ws + (t * MF * 32 + R) * 16 + 8 * hh8) = v;
+  }
+  for (int q = tid; q < 96; q += 512) sbias[q] = (p.bias && q < p.M) ? p.bias[q] : 0.0f;
+  for (int q = tid; q < 32; q += 512) qbias[q] = q < sq.M ? sq.bias[q] : 0.0f;
+  // the window's columns past the image (read by the last pairs' taps) stay zero: the staging writes < W
+  for (int q = tid; q < FB_WIN_HALVES / 8; q += 512) reinterpret_cast<c1h8*>(win)[q] = c1h8{};
+  // the squeeze's A fragments (waves 0-3), loaded once
+  const _Float16* __restrict__ wq = static_cast<const _Float16*>(sq.w);
+  c1h8 aqr[MF][2];
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) aqr[i][t] = *reinterpret_cast<const c1h8*>(wq + ((2 * i + t) * 32 + lr) * 16 + 8 * h);
+
+  // this wave's conv row in a step and column pair (wave 2 r: pairs 0 .., wave 2 r + 1: pairs 31 ..)
+  const int rr = wave >> 1, j = ((wave & 1) ? 31 : 0) + lr;
+  // B: the lane's two pixels (conv columns 2 j + f) at window row 2 rr, k-step 0 (lane half h: taps 2 h, 2 h + 1)
+  int bo[2];
+  bool colok[2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    bo[f] = ((2 * rr) * FB_RW + 2 * (2 * j + f) + 2 * h) * 4;
+    colok[f] = 2 * j + f < p.Wo;
+  }
+  // the pooled column of the pair (wave 2 r's lane 31 is wave 2 r + 1's lane 0)
+  const bool pok = lr < 31 && j < p.ep_Wo;
+  const int aofs = lr * 16 + 8 * h;
+  // window units of this thread: (row, 4 columns) u = tid + 512 k of FB_WR x 56
+  int wgo[FB_NU], wlo[FB_NU], wrw[FB_NU];
+#pragma unroll
+  for (int k = 0; k < FB_NU; ++k) {
+    const int u = tid + 512 * k, rw = u / 56, cg = u - rw * 56;
+    const bool ok = u < FB_WR * 56 && 4 * cg < p.W;
+    wgo[k] = ok ? (rw * p.W + 4 * cg) * 4 : (int)0x80000000;  // + the step's first row in the scalar offset
+    wlo[k] = ok ? (rw * FB_RW + 4 * cg) * 4 : -1;
+    wrw[k] = rw;
+  }
+  typedef float fbf4 __attribute__((ext_vector_type(4)));
+  fbf4 xv[FB_NU][3];
+  const int nsteps = (p.ep_Ho - 1 + 1) / 2 + 1;  // pooled row p completes at step ceil(p / 2)
+  typedef unsigned short fbu8 __attribute__((ext_vector_type(8)));
+  typedef unsigned fbu4 __attribute__((ext_vector_type(4)));
+
+  for (int img = blockIdx.x; img < p.N; img += gridDim.x) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(p.x + (long long)img * p.x_nstride), (short)0, p.C * p.x_ps * 4, 0x00020000);
+    // the step's input rows [8 s, 8 s + 13) (rows past the image, channels >= C: past the records, 0)
+    auto load_window = [&](int st) __attribute__((always_inline)) {
+      const int so = 2 * (4 * st) * p.W * 4;
+#pragma unroll
+      for (int k = 0; k < FB_NU; ++k) {
+        const int o = 8 * st + wrw[k] < p.H ? wgo[k] : (int)0x80000000;  // rows past the image: 0
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          xv[k][c] = __builtin_bit_cast(fbf4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  rs, c < p.C ? o : (int)0x80000000, so + c * p.x_ps * 4, 0));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto store_window = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < FB_NU; ++k) {
+        if (wlo[k] < 0) continue;
+        c1h8 v0, v1;  // pixels 0, 1 and 2, 3 of the unit, channels 0 .. 3 (channel 3: 0)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            v0[4 * e + c] = (_Float16)xv[k][c][e];
+            v1[4 * e + c] = (_Float16)xv[k][c][2 + e];
+          }
+          v0[4 * e + 3] = (_Float16)0.0f;
+          v1[4 * e + 3] = (_Float16)0.0f;
+        }
+        *reinterpret_cast<c1h8*>(win + wlo[k]) = v0;
+        *reinterpret_cast<c1h8*>(win + wlo[k] + 8) = v1;
+      }
+    };
+    load_window(0);
+    __syncthreads();  // (the previous image's last squeeze and the staging above are done)
+    store_window();
+    for (int st = 0; st < nsteps; ++st) {
+      __syncthreads();  // window st is in LDS; the previous squeeze has read its ring rows
+      if (st + 1 < nsteps) load_window(st + 1);
+      const int cr = 4 * st + rr;  // this wave's conv row
+      if (__builtin_amdgcn_readfirstlane(cr - p.Ho) < 0) {  // wave-uniform (the DPP below needs every lane)
+        c1f16 acc[MF][2];
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+          for (int f = 0; f < 2; ++f)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][f][e] = 0.0f;
+#pragma unroll
+        for (int ks = 0; ks < FB_KS; ++ks) {
+          // k-step ks: tap pair 2 ks + h = taps 4 ks + 2 h, + 1 (row (4 ks) / 8, column (4 ks) % 8 + 2 h)
+          const int ko = ((4 * ks) / 8 * FB_RW + (4 * ks) % 8) * 4;
+          c1h8 b[2];
+#pragma unroll
+          for (int f = 0; f < 2; ++f) b[f] = *reinterpret_cast<const c1h8*>(win + bo[f] + ko);
+#pragma unroll
+          for (int i = 0; i < MF; ++i) {
+            const c1h8 a = *reinterpret_cast<const c1h8*>(Ws + (ks * MF + i) * 512 + aofs);
+#pragma unroll
+            for (int f = 0; f < 2; ++f) acc[i][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[f], acc[i][f], 0, 0, 0);
+          }
+        }
+        // bias, Relu, f16 (the patch kernel's epilogue), 0 outside the conv plane; the pair's pooled column
+        const int slot = cr % FB_SLOTS;
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            float bv[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bv[e] = sbias[32 * i + 16 * g + 8 * h + e];
+            fbu4 v[2];
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+              float av[8];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) av[e] = acc[i][f][8 * g + e];
+              const c1h8 o = ore_f16_epilogue8(av, bv, p.relu != 0);
+              v[f] = colok[f] ? __builtin_bit_cast(fbu4, o) : fbu4{0u, 0u, 0u, 0u};
+            }
+            fbu4 nb;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)  // wave_shl:1: lane lr + 1's first column (lane 31's is the other half's)
+              nb[q] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v[0][q], 0x130, 0xf, 0xf, true);
+            fbu8 m = __builtin_elementwise_max(__builtin_bit_cast(fbu8, v[0]), __builtin_bit_cast(fbu8, v[1]));
+            m = __builtin_elementwise_max(m, __builtin_bit_cast(fbu8, nb));
+            if (pok) *reinterpret_cast<fbu8*>(ring + (slot * FB_HC + j) * FB_CHS + 32 * i + 16 * g + 8 * h) = m;
+          }
+      }
+      __syncthreads();  // the step's ring rows are written; every K loop is done (the window is free)
+      // the squeeze of pooled rows 2 st - 1 and 2 st: waves 0-3, 32 pooled pixels each
+      if (wave < 4) {
+        const int px = 32 * wave + lr, second = px >= p.ep_Wo ? 1 : 0;
+        const int prow = 2 * st - 1 + second, pcol = px - second * p.ep_Wo;
+        const bool qok = px < 2 * p.ep_Wo && prow >= 0 && prow < p.ep_Ho;
+        const int pr = qok ? prow : 0, pc = qok ? pcol : 0;
+        const _Float16* r0 = ring + (((2 * pr) % FB_SLOTS) * FB_HC + pc) * FB_CHS + 8 * h;
+        const _Float16* r1 = ring + (((2 * pr + 1) % FB_SLOTS) * FB_HC + pc) * FB_CHS + 8 * h;
+        const _Float16* r2 = ring + (((2 * pr + 2) % FB_SLOTS) * FB_HC + pc) * FB_CHS + 8 * h;
+        c1f16 sacc;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sacc[e] = 0.0f;
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const int co = 32 * i + 16 * t;
+            fbu8 m = __builtin_elementwise_max(*reinterpret_cast<const fbu8*>(r0 + co), *reinterpret_cast<const fbu8*>(r1 + co));
+            m = __builtin_elementwise_max(m, *reinterpret_cast<const fbu8*>(r2 + co));
+            sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(aqr[i][t], __builtin_bit_cast(c1h8, m), sacc, 0, 0, 0);
+          }
+        if (qok) {
+          _Float16* yq = static_cast<_Float16*>(sq.y) + (long long)img * sq.y_nstride + (prow * p.ep_Wo + pcol) * sq.y_cs;
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            const int ch = 16 * g + 8 * h;
+            if (ch >= sq.M) continue;
+            float av[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) av[e] = sacc[8 * g + e];
+            *reinterpret_cast<c1h8*>(yq + ch) = ore_f16_epilogue8(av, qbias + ch, true);
+          }
+        }
+      }
+      if (st + 1 < nsteps) store_window();
+    }
+  }
+}
+
 }  // namespace
 
 bool conv_pair_pool_f16_eligible(const ConvParams& p, const C1Squeeze* sq) {
@@ -375,6 +602,32 @@ bool conv_pair_pool_f16_eligible(const ConvParams& p, const C1Squeeze* sq) {
   }
   const C1Geom g = c1_geom(MF, p.kh, kwp, p.sh, p.sw, sq != nullptr);
   return g.lds_bytes <= 80 * 1024 && (long long)p.H * p.W < (1LL << 30) && p.ep_tr > 0 && p.ep_tc > 0;
+}
+
+bool conv_band_pool_f16_geometry(int C, int M, int kh, int kw, int sh, int sw, int pt, int pl, int W, int Wo, int ep_Ho,
+                                 int ep_Wo, int ep_pt, int ep_pl, int sq_M) {
+  return C >= 1 && C <= 3 && M == 96 && kh == 7 && kw == 7 && sh == 2 && sw == 2 && pt == 0 && pl == 0 && W <= 224 &&
+         W % 4 == 0 && (Wo + 1) / 2 <= 63 && ep_Wo >= 1 && ep_Wo <= FB_HC - 1 && ep_Ho >= 1 &&
+         ep_pt == 0 && ep_pl == 0 && 2 * (ep_Wo - 1) + 2 < Wo + 1 && sq_M >= 8 && sq_M <= 32 && sq_M % 8 == 0;
+}
+
+bool conv_band_pool_f16_eligible(const ConvParams& p, const C1Squeeze* sq) {
+  if (!sq || !p.relu || !conv_pair_pool_f16_eligible(p, sq)) return false;  // the patch kernel's layout rules
+  return conv_band_pool_f16_geometry(p.C, p.M, p.kh, p.kw, p.sh, p.sw, p.pt, p.pl, p.W, p.Wo, p.ep_Ho, p.ep_Wo, p.ep_pt,
+                                     p.ep_pl, sq->M) &&
+         p.K == 7 * 8 * 4 && (long long)p.C * p.x_ps * 4 < (1LL << 31) && 2 * (p.ep_Ho - 1) + 2 < p.Ho;
+}
+
+void launch_conv_band_pool_f16(const ConvParams& p, const C1Squeeze& sq, hipStream_t s) {
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
+  }
+  static std::atomic<unsigned long long> raised{0};
+  ore_raise_lds_once(raised, reinterpret_cast<const void*>(&conv_band_pool_f16_kernel), FB_LDS);
+  const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(p.N, ncu));  // one image per workgroup
+  hipLaunchKernelGGL(conv_band_pool_f16_kernel, dim3(grid), dim3(512), FB_LDS, s, p, sq);
 }
 
 void launch_conv_pair_pool_f16(const ConvParams& p, const C1Squeeze* sq, hipStream_t s) {

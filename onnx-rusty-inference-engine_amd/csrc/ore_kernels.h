@@ -257,6 +257,12 @@ struct C1Squeeze {
 };
 bool conv_pair_pool_f16_eligible(const ConvParams& p, const C1Squeeze* sq = nullptr);
 void launch_conv_pair_pool_f16(const ConvParams& p, const C1Squeeze* sq, hipStream_t s);
+// round 6: the same fused first conv + pool + squeeze walked in steps of four conv rows, one workgroup per image
+// (conv_band_pool_f16_kernel, tile C1_BAND_F16_TILE); bit-identical to the patch kernel
+bool conv_band_pool_f16_geometry(int C, int M, int kh, int kw, int sh, int sw, int pt, int pl, int W, int Wo, int ep_Ho,
+                                 int ep_Wo, int ep_pt, int ep_pl, int sq_M);
+bool conv_band_pool_f16_eligible(const ConvParams& p, const C1Squeeze* sq);
+void launch_conv_band_pool_f16(const ConvParams& p, const C1Squeeze& sq, hipStream_t s);
 // W [M][C][kk] f32 (kk = 1 or 9) -> [C kk / 16][roundup(M, 32)][16] f16 with permuted rows
 size_t fire_pack_f16_bytes(int M, int C, int kk);
 void launch_fire_pack_f16(const float* w, int M, int C, int kk, void* out, hipStream_t s);
@@ -409,6 +415,8 @@ constexpr int WINO_TILE_BASE = 36;
 constexpr int WINO_TILES_N = 5;
 // fused-kernel ids after the Winograd tiles (ore.Model.TILE_NAMES): 41 is retired (the Winograd fire module)
 constexpr int FIRE_F16_TILE = 42, C1_POOL_F16_TILE = 43;
+// plan.epv of the f16 first conv + pool + squeeze: the band walker, the patch kernel (chosen explicitly)
+constexpr int C1_BAND_F16_TILE = 52, C1_BAND_F16_VARIANT = 9, C1_PATCH_F16_VARIANT = 10;
 constexpr int CONV_GAP_F16_TILE = 49;  // conv1x1_gap_f16_kernel: ore.Model.TILE_NAMES "conv1x1 gap f16"
 constexpr int CONV_GAP_F32_TILE = 50;  // conv1x1_gap_f32_kernel: ore.Model.TILE_NAMES "conv1x1 gap f32"
 bool conv_wino_geometry(int C, int kh, int kw, int sh, int sw, int pt, int pl, int H, int W, int Ho, int Wo);

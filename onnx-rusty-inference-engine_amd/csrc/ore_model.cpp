@@ -180,7 +180,8 @@ struct ore_model {
 
 namespace {
 
-bool band_step(const Step& s);  // the band walker's geometry (below, beside step_tile_family)
+bool band_step(const Step& s);      // the band walkers' geometry (below, beside step_tile_family)
+bool band_f16_step(const Step& s);
 
 // IEEE binary16 -> binary32 (exact)
 float half_bits_to_float(uint16_t h) {
@@ -1023,6 +1024,10 @@ struct Planner {
       cv.sq_M = q.M;
       if (!f16 && cv.plan.epv != EPOOL_BAND_VARIANT && cv.plan.epv != EPOOL_WIN_VARIANT)
         cv.plan.epv = m->max_batch >= 128 && band_step(cv) ? EPOOL_BAND_VARIANT : EPOOL_WIN_VARIANT;
+      // f16: the band walker (one workgroup per image) for batches that give every CU an image, else the
+      // patch kernel; an autotuned / set choice is kept
+      if (f16 && cv.plan.epv != C1_BAND_F16_VARIANT && cv.plan.epv != C1_PATCH_F16_VARIANT)
+        cv.plan.epv = m->max_batch >= 128 && band_f16_step(cv) ? C1_BAND_F16_VARIANT : C1_PATCH_F16_VARIANT;
       val(cv.out).elided = true;
       cv.out = q.out;
       cv.flops_per_img += q.flops_per_img;
@@ -1502,7 +1507,7 @@ ore_status launch_step(ore_model* m, const Step& s, int64_t n) {
         const ore_status st = run_conv_pair_pool_f16(ctx, s.plan, x.p, n, s.C, s.H, s.W, x.nstride, x.ps, s.wp, s.M, s.kh,
                                                      s.kw, bias, s.win, s.sh, s.sw, s.relu, s.c1sq ? nullptr : y.p,
                                                      y.nstride, s.c1sq ? s.M : y.ps, ep, &ran, s.c1sq ? &sq : nullptr);
-        if (ran) s.ran_tile = last_conv_tile = C1_POOL_F16_TILE;
+        if (ran) s.ran_tile = last_conv_tile;  // C1_POOL_F16_TILE or C1_BAND_F16_TILE
         if (st != ORE_OK || ran) return st;
         s.ran_tile = -1;
         if (s.c1sq) return err(m, ORE_ERR_INVALID, "internal: the fused first conv + squeeze declined its launch");
@@ -1653,6 +1658,14 @@ namespace {
 // accepted values; empty for steps with one fixed kernel
 // the band walker's geometry for a fused f32 first conv + pool + squeeze step (its layout checks are the
 // launch's: a layout it declines runs the window kernel)
+bool band_f16_step(const Step& s) {
+  return s.plan.f16 && conv_band_pool_f16_geometry(int(s.C), int(s.M), int(s.kh), int(s.kw), int(s.sh), int(s.sw),
+                                                   int(s.win.pt), int(s.win.pl), int(s.W), int(s.win.Wo),
+                                                   int(s.ep_win.Ho), int(s.ep_win.Wo), int(s.ep_win.pt), int(s.ep_win.pl),
+                                                   int(s.sq_M)) &&
+         s.relu;
+}
+
 bool band_step(const Step& s) {
   return conv_band_pool_f32_geometry(int(s.C), int(s.M), int(s.kh), int(s.kw), int(s.sh), int(s.sw), int(s.win.pt),
                                      int(s.win.pl), int(s.W), int(s.win.Wo), int(s.ep_win.Ho), int(s.ep_win.Wo),
@@ -1672,7 +1685,10 @@ std::vector<int> step_tile_family(const Step& s) {
     return c;
   }
   if (s.kind == S_CONV && s.epool && s.plan.f16 && s.plan.xmode == F16_X_NHWC_PAIR) {  // f16 first conv + pool
-    if (s.c1sq) return {C1_POOL_F16_TILE};
+    if (s.c1sq) {  // the fused squeeze: the patch kernel, the band walker (where its geometry allows it)
+      if (band_f16_step(s)) return {C1_POOL_F16_TILE, C1_BAND_F16_TILE};
+      return {C1_POOL_F16_TILE};
+    }
     return {EPOOL_TILE_BASE + 1, C1_POOL_F16_TILE};  // two launches (conversion + patch kernel) / one launch
   }
   if (s.epool || s.pool || s.gap) return c;  // other f16 pooled epilogues / the pooled 1x1 / conv + GAP: one kernel
@@ -1697,7 +1713,8 @@ void set_tile(ore_model* m, int k, int t) {
   if (s.kind == S_CONV && s.epool) {
     const int v = t == EPOOL_WIN_TILE    ? EPOOL_WIN_VARIANT
                   : t == EPOOL_BAND_TILE ? EPOOL_BAND_VARIANT
-                  : t == C1_POOL_F16_TILE ? 0
+                  : t == C1_POOL_F16_TILE ? (s.c1sq ? C1_PATCH_F16_VARIANT : 0)
+                  : t == C1_BAND_F16_TILE ? C1_BAND_F16_VARIANT
                                           : t - EPOOL_TILE_BASE;
     s.plan.epv = b.plan.epv = v;
     return;

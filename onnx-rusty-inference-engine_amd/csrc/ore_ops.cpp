@@ -422,7 +422,13 @@ ore_status run_conv_pair_pool_f16(ore_ctx* ctx, const ConvPlan& pln, const float
   p.ep_pt = int(ep.win.pt); p.ep_pl = int(ep.win.pl); p.ep_Ho = int(ep.win.Ho); p.ep_Wo = int(ep.win.Wo);
   p.ep_tr = tr; p.ep_tc = tc;
   if (!conv_pair_pool_f16_eligible(p, sq)) return ORE_OK;
-  launch_conv_pair_pool_f16(p, sq, ctx->stream);
+  if (pln.epv == C1_BAND_F16_VARIANT && sq && conv_band_pool_f16_eligible(p, sq)) {  // the band walker (round 6)
+    launch_conv_band_pool_f16(p, *sq, ctx->stream);
+    last_conv_tile = C1_BAND_F16_TILE;
+  } else {
+    launch_conv_pair_pool_f16(p, sq, ctx->stream);
+    last_conv_tile = C1_POOL_F16_TILE;
+  }
   ORE_HIP_CHECK(ctx, hipGetLastError());
   *ran = true;
   return ORE_OK;

@@ -323,7 +323,7 @@ class Model:
                   "wino lds", None,  # 41: the Winograd fire module (retired)
                   "fire f16", "first conv pool f16", "epool window f32", "fire pool f32",
                   "stream1x1 persist 32x128", "stream1x1 persist 64x64", "stream1x1 persist 16x256",
-                  "conv1x1 gap f16", "conv1x1 gap f32", "epool band f32"]
+                  "conv1x1 gap f16", "conv1x1 gap f32", "epool band f32", "epool band f16"]
 
     def tiles(self):
         """Block tile per exec step (-1 for non-conv steps); names in TILE_NAMES."""

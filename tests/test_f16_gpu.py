@@ -596,3 +596,56 @@ def test_f16_first_conv_pool_squeeze_fused(gpu_ctx, case):
     np.testing.assert_array_equal(vals[0][1], vals[1][1])
     np.testing.assert_array_equal(vals[0][0], vals[1][0])
     assert np.abs(vals[0][1]).max() > 0
+
+
+@pytest.mark.parametrize("case", [
+    # N, H, W, squeeze channels
+    (3, 224, 224, 16),   # SqueezeNet conv1 + pool1 + fire2/squeeze1x1 (28 steps, the last with one conv row)
+    (2, 113, 100, 32),   # odd conv rows / columns, 32 squeeze channels (two store groups)
+    (300, 64, 72, 24),   # more images than workgroups (a workgroup walks several), 24 channels (a partial group)
+])
+def test_f16_conv1_band_bit_identical(gpu_ctx, case):
+    """Round 6: the f16 band walker (conv_band_pool_f16_kernel, tile "epool band f16") equals the patch kernel
+    ("first conv pool f16") bit for bit on the fused first conv + Relu + MaxPool + squeeze + Relu: the same
+    operands, k order and MFMA chains, the max of the same nine f16 values, the same squeeze chain."""
+    import ore
+    N, H, W, Q = case
+    rng = np.random.default_rng(N + H + W + Q)
+    x = (rng.standard_normal((N, 3, H, W)) * 20).astype(np.float32)
+    w1 = (rng.standard_normal((96, 3, 7, 7)) * np.sqrt(2.0 / 147)).astype(np.float32)
+    b1 = rng.uniform(-0.1, 0.1, 96).astype(np.float32)
+    w2 = (rng.standard_normal((Q, 96, 1, 1)) * np.sqrt(2.0 / 96)).astype(np.float32)
+    b2 = rng.uniform(-0.1, 0.1, Q).astype(np.float32)
+    mb = _chain_model((1, 3, H, W), [(w1, b1, [0] * 4, [2, 2], True), (w2, b2, [0] * 4, [1, 1], True)], pool=[0] * 4)
+    vals = []
+    for name in ("first conv pool f16", "epool band f16"):
+        m = ore.Model(gpu_ctx, mb, max_batch=N, precision="f16")
+        m.set_fusion(ore.FUSE_ALL | ore.FUSE_EAGER | ore.KEEP_VALUES)
+        m.set_tile(0, ore.Model.TILE_NAMES.index(name))
+        y = _np(m.run(_t(x)))
+        vals.append((y, m.read_value("r1")))
+        assert [ore.Model.TILE_NAMES[t] for t in m.tiles() if t >= 0] == [name]
+        m.close()
+    np.testing.assert_array_equal(vals[1][1], vals[0][1])
+    np.testing.assert_array_equal(vals[1][0], vals[0][0])
+    assert np.abs(vals[0][1]).max() > 0
+
+
+def test_f16_squeezenet_conv1_band(gpu_ctx):
+    """SqueezeNet-1.0 @224 f16 at max_batch 256 (config 5's plan): the untuned plan takes the band walker for
+    conv1 + pool1 + fire2/squeeze1x1, and the probabilities equal the patch kernel's bit for bit."""
+    import ore
+    import torch
+    from ore import squeezenet
+    mb = squeezenet.build(224)
+    x = _t(squeezenet.synthetic_input(4, 224, seed=29))
+    x = torch.cat([x] * 64).contiguous()
+    outs = []
+    for name in ("epool band f16", "first conv pool f16"):
+        m = ore.Model(gpu_ctx, mb, max_batch=256, precision="f16")
+        if name == "first conv pool f16":
+            m.set_tile(0, ore.Model.TILE_NAMES.index(name))
+        outs.append(_np(m.run(x)))
+        assert ore.Model.TILE_NAMES[m.tiles()[0]] == name, ore.Model.TILE_NAMES[m.tiles()[0]]
+        m.close()
+    np.testing.assert_array_equal(outs[0], outs[1])

@@ -63,13 +63,17 @@ def _kernel_isa(symbol_part):
 
 
 @pytest.mark.skipif(not _tools(), reason="ROCm binutils / objcopy not present")
-def test_band_walker_dpp_exchange_runs_with_full_exec():
+@pytest.mark.parametrize("kernel,group", [
+    ("conv_band_pool_f32_kernel", 16),  # 16 channel rows per 32-channel fragment, 3 fragments per step
+    ("conv_band_pool_f16_kernel", 4),   # round 6: 4 dwords (8 f16 channels) per (fragment, group), 6 per row
+])
+def test_band_walker_dpp_exchange_runs_with_full_exec(kernel, group):
     ore.load()
-    isa = _kernel_isa("conv_band_pool_f32_kernel")
-    assert isa, "conv_band_pool_f32_kernel not found in libore.so"
+    isa = _kernel_isa(kernel)
+    assert isa, f"{kernel} not found in libore.so"
     dpp = [k for k, i in enumerate(isa) if "wave_shl:1" in i]
-    # 16 channel rows per 32-channel fragment, 3 fragments per step (the compiler may duplicate the step)
-    assert dpp and len(dpp) % 16 == 0, len(dpp)
+    # (the compiler may duplicate the step)
+    assert dpp and len(dpp) % group == 0, len(dpp)
     for k in dpp:
         ins = isa[k]
         # all rows and banks written, an out-of-range source (lane 63) reads 0
