@@ -371,10 +371,11 @@ static bool c1_dispatch(const ConvParams& p, const C1Squeeze& sq, unsigned grid,
 //   * A (the packed weights, the patch kernel's permuted rows) sits in LDS for the workgroup's life; B reads
 //     the step's 13 input rows, staged in LDS as f16 NHWC4 (rounded as the patch kernel's window: the same
 //     operands, k order and MFMA chain, so every conv output has the same bits);
-//   * after bias, Relu and the f16 rounding (ore_f16_epilogue8, as the patch kernel), the pair's pooled column
-//     takes max(col 2j, 2j + 1, 2j + 2) on the f16 bits (values >= +0 order like their bits) -- the third by
-//     DPP wave_shl:1 from lane lr + 1, with every lane of the wave enabled (tests/test_isa_guard.py) -- into a
-//     ring of horizontally pooled conv rows [6 slots][56 columns][96 channels] (one writer per cell: no atomics);
+//   * after the bias (the patch kernel's f32 add), the pair's pooled column takes max(col 2j, 2j + 1, 2j + 2) --
+//     the two own columns in f32 before the f16 rounding (rounding is monotonic: the same bits as the max of the
+//     patch kernel's rounded values), the third, rounded, by DPP wave_shl:1 from lane lr + 1 with every lane of
+//     the wave enabled (tests/test_isa_guard.py) -- into a ring of horizontally pooled conv rows
+//     [6 slots][56 columns][96 channels] (one writer per cell: no atomics);
 //   * a step completes pooled rows 2 s - 1 and 2 s (conv rows 4 s - 2 .. 4 s + 2): waves 0-3 take their 3-row
 //     maxima (the nine values of the patch kernel's max, exact) as the squeeze's B operands and run its six
 //     MFMAs per fragment in the patch kernel's order; bias, Relu, one rounding, 16-B NHWC stores.
@@ -429,12 +430,8 @@ __global__ __launch_bounds__(512, 1) void conv_band_pool_f16_kernel(ConvParams p
   const int rr = wave >> 1, j = ((wave & 1) ? 31 : 0) + lr;
   // B: the lane's two pixels (conv columns 2 j + f) at window row 2 rr, k-step 0 (lane half h: taps 2 h, 2 h + 1)
   int bo[2];
-  bool colok[2];
 #pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    bo[f] = ((2 * rr) * FB_RW + 2 * (2 * j + f) + 2 * h) * 4;
-    colok[f] = 2 * j + f < p.Wo;
-  }
+  for (int f = 0; f < 2; ++f) bo[f] = ((2 * rr) * FB_RW + 2 * (2 * j + f) + 2 * h) * 4;
   // the pooled column of the pair (wave 2 r's lane 31 is wave 2 r + 1's lane 0)
   const bool pok = lr < 31 && j < p.ep_Wo;
   const int aofs = lr * 16 + 8 * h;
@@ -452,7 +449,6 @@ __global__ __launch_bounds__(512, 1) void conv_band_pool_f16_kernel(ConvParams p
   fbf4 xv[FB_NU][3];
   const int nsteps = (p.ep_Ho - 1 + 1) / 2 + 1;  // pooled row p completes at step ceil(p / 2)
   typedef unsigned short fbu8 __attribute__((ext_vector_type(8)));
-  typedef unsigned fbu4 __attribute__((ext_vector_type(4)));
 
   for (int img = blockIdx.x; img < p.N; img += gridDim.x) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -518,31 +514,42 @@ __global__ __launch_bounds__(512, 1) void conv_band_pool_f16_kernel(ConvParams p
             for (int f = 0; f < 2; ++f) acc[i][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[f], acc[i][f], 0, 0, 0);
           }
         }
-        // bias, Relu, f16 (the patch kernel's epilogue), 0 outside the conv plane; the pair's pooled column
+        // the pair's pooled column: the bias (the patch kernel's f32 add); the two own columns' max in f32, then one
+        // f16 rounding (rounding is monotonic: the rounded max is the max of the rounded values the patch kernel
+        // pools) and the Relu on the bits; the third column (2 j + 2) as lane lr + 1's rounded first column by DPP
+        // wave_shl:1, with every lane of the wave enabled (tests/test_isa_guard.py).  The DPP reads a 32-bit
+        // v_cvt_pk_f16_f32 result: ROCm 7.2's compiler mis-lowers a DPP of either half of a packed f32 pair (it
+        // shifts the low half and reuses it for the high one), the cause of round 5's
+        // wrong-output band-walker variant.  A valid pooled column's three conv columns lie inside the plane
+        // (2 ep_Wo <= Wo - 1), so no out-of-plane zero is needed
         const int slot = cr % FB_SLOTS;
+        typedef float fbf2 __attribute__((ext_vector_type(2)));
+        typedef _Float16 fbh2 __attribute__((ext_vector_type(2)));
+        typedef short fbs2 __attribute__((ext_vector_type(2)));
+        typedef unsigned short fbus2 __attribute__((ext_vector_type(2)));
 #pragma unroll
         for (int i = 0; i < MF; ++i)
 #pragma unroll
           for (int g = 0; g < 2; ++g) {
-            float bv[8];
+            unsigned o[4];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) bv[e] = sbias[32 * i + 16 * g + 8 * h + e];
-            fbu4 v[2];
-#pragma unroll
-            for (int f = 0; f < 2; ++f) {
-              float av[8];
-#pragma unroll
-              for (int e = 0; e < 8; ++e) av[e] = acc[i][f][8 * g + e];
-              const c1h8 o = ore_f16_epilogue8(av, bv, p.relu != 0);
-              v[f] = colok[f] ? __builtin_bit_cast(fbu4, o) : fbu4{0u, 0u, 0u, 0u};
+            for (int e = 0; e < 8; e += 2) {
+              const fbf2 b2 = {sbias[32 * i + 16 * g + 8 * h + e], sbias[32 * i + 16 * g + 8 * h + e + 1]};
+              const fbf2 v0 = fbf2{acc[i][0][8 * g + e], acc[i][0][8 * g + e + 1]} + b2;
+              const fbf2 v1 = fbf2{acc[i][1][8 * g + e], acc[i][1][8 * g + e + 1]} + b2;
+              const fbf2 m01 = {fmaxf(v0[0], v1[0]), fmaxf(v0[1], v1[1])};
+              const fbs2 r0 = __builtin_elementwise_max(__builtin_bit_cast(fbs2, __builtin_convertvector(v0, fbh2)), fbs2{0, 0});
+              const fbs2 rm = __builtin_elementwise_max(__builtin_bit_cast(fbs2, __builtin_convertvector(m01, fbh2)), fbs2{0, 0});
+              const int nb = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, r0), 0x130, 0xf, 0xf, true);
+              // Relu outputs are >= +0: their f16 bits order like the values (unsigned max)
+              o[e >> 1] = __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(fbus2, rm),
+                                                                                 __builtin_bit_cast(fbus2, nb)));
             }
-            fbu4 nb;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)  // wave_shl:1: lane lr + 1's first column (lane 31's is the other half's)
-              nb[q] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v[0][q], 0x130, 0xf, 0xf, true);
-            fbu8 m = __builtin_elementwise_max(__builtin_bit_cast(fbu8, v[0]), __builtin_bit_cast(fbu8, v[1]));
-            m = __builtin_elementwise_max(m, __builtin_bit_cast(fbu8, nb));
-            if (pok) *reinterpret_cast<fbu8*>(ring + (slot * FB_HC + j) * FB_CHS + 32 * i + 16 * g + 8 * h) = m;
+            if (pok) {
+              typedef unsigned fbu4v __attribute__((ext_vector_type(4)));
+              *reinterpret_cast<fbu4v*>(ring + (slot * FB_HC + j) * FB_CHS + 32 * i + 16 * g + 8 * h) =
+                  fbu4v{o[0], o[1], o[2], o[3]};
+            }
           }
       }
       __syncthreads();  // the step's ring rows are written; every K loop is done (the window is free)
@@ -608,7 +615,7 @@ bool conv_band_pool_f16_geometry(int C, int M, int kh, int kw, int sh, int sw, i
                                  int ep_Wo, int ep_pt, int ep_pl, int sq_M) {
   return C >= 1 && C <= 3 && M == 96 && kh == 7 && kw == 7 && sh == 2 && sw == 2 && pt == 0 && pl == 0 && W <= 224 &&
          W % 4 == 0 && (Wo + 1) / 2 <= 63 && ep_Wo >= 1 && ep_Wo <= FB_HC - 1 && ep_Ho >= 1 &&
-         ep_pt == 0 && ep_pl == 0 && 2 * (ep_Wo - 1) + 2 < Wo + 1 && sq_M >= 8 && sq_M <= 32 && sq_M % 8 == 0;
+         ep_pt == 0 && ep_pl == 0 && 2 * (ep_Wo - 1) + 2 <= Wo - 1 && sq_M >= 8 && sq_M <= 32 && sq_M % 8 == 0;
 }
 
 bool conv_band_pool_f16_eligible(const ConvParams& p, const C1Squeeze* sq) {

@@ -65,7 +65,7 @@ def _kernel_isa(symbol_part):
 @pytest.mark.skipif(not _tools(), reason="ROCm binutils / objcopy not present")
 @pytest.mark.parametrize("kernel,group", [
     ("conv_band_pool_f32_kernel", 16),  # 16 channel rows per 32-channel fragment, 3 fragments per step
-    ("conv_band_pool_f16_kernel", 4),   # round 6: 4 dwords (8 f16 channels) per (fragment, group), 6 per row
+    ("conv_band_pool_f16_kernel", 4),   # round 6: 4 f16 channel pairs per (fragment, group), 6 per row
 ])
 def test_band_walker_dpp_exchange_runs_with_full_exec(kernel, group):
     ore.load()
@@ -83,3 +83,43 @@ def test_band_walker_dpp_exchange_runs_with_full_exec(kernel, group):
         last = next((isa[j] for j in range(k - 1, -1, -1) if re.match(r"s_\w+ exec, ", isa[j])
                      or "saveexec" in isa[j]), None)
         assert last is None or re.match(r"s_(or|mov)_b64 exec, ", last), (ins, last)
+        # the DPP's source VGPR was last written by a single-register (32-bit) definition: ROCm 7.2's compiler
+        # lowers a DPP of either half of a packed f32 pair (a v_pk_* result, v[n:n+1]) as a DPP of the LOW half
+        # and uses it for both (tests/test_isa_guard.py::test_compiler_dpp_packed_pair_hazard)
+        src = int(re.match(r"v_\w+_dpp v\d+, v(\d+)", ins).group(1))
+        for jj in range(k - 1, -1, -1):
+            d = isa[jj].split()
+            if len(d) < 2 or not d[0].startswith("v_") or d[0].startswith("v_cmp"):
+                continue
+            dst = d[1].rstrip(",")
+            m1 = re.fullmatch(r"v(\d+)", dst)
+            m2 = re.fullmatch(r"v\[(\d+):(\d+)\]", dst)
+            if m1 and int(m1.group(1)) == src:
+                break
+            if m2 and int(m2.group(1)) <= src <= int(m2.group(2)):
+                raise AssertionError(f"DPP source v{src} last written by a multi-register definition: {isa[jj]} -> {ins}")
+
+
+@pytest.mark.skipif(not _tools(), reason="ROCm binutils / objcopy not present")
+def test_compiler_dpp_packed_pair_hazard(tmp_path):
+    """Pins the compiler behaviour the guard above avoids (ROCm 7.2, gfx950): a DPP of each half of a packed f32
+    sum compiles to ONE v_mov_b32_dpp of the low half, used for both halves -- wrong values for the high half.
+    If a future compiler fixes it this test fails, and the note in DESIGN.md 3.4b can go."""
+    src = tmp_path / "r.hip"
+    src.write_text("""#include <hip/hip_runtime.h>
+typedef float f2 __attribute__((ext_vector_type(2)));
+extern "C" __global__ void k(const f2* a, const f2* b, float* out) {
+  const f2 v = a[threadIdx.x] + b[threadIdx.x];
+  for (int q = 0; q < 2; ++q)
+    out[2 * threadIdx.x + q] = fmaxf(v[q], __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+        0, __builtin_bit_cast(int, v[q]), 0x130, 0xf, 0xf, true)));
+}
+""")
+    out = tmp_path / "r.s"
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "--cuda-device-only", "-S", "-o", str(out),
+                        str(src)], capture_output=True, text=True)
+    if r.returncode != 0 or not out.exists():
+        pytest.skip("hipcc not usable here")
+    asm = out.read_text()
+    assert "v_pk_add_f32" in asm
+    assert asm.count("_dpp") == 1, asm.count("_dpp")  # two values shifted, one DPP: the miscompile
