@@ -449,7 +449,8 @@ def main():
             conv = classes.get("Conv", {"ms": 1e-9, "flops": 0.0, "mfma_flops": 0.0, "bytes": 0.0, "launches": 1})
             effective = conv["flops"] / (conv["ms"] * 1e-3) / 1e12
             issued = conv["mfma_flops"] / (conv["ms"] * 1e-3) / 1e12
-            kname = ("Conv class: conv_pair_pool_f16_kernel (conv1 + pool1 straight from the f32 input), "
+            kname = ("Conv class: conv_band_pool_f16_kernel / conv_pair_pool_f16_kernel (conv1 + pool1 + fire2 "
+                     "squeeze straight from the f32 input, band walker or patch kernel per the autotuned tile), "
                      "fire_f16_kernel / fire_pool_f16_kernel (fire module [+ MaxPool] + next squeeze) and "
                      "conv_f16_kernel (implicit GEMM), all MFMA 32x32x16 f16 with f32 accumulate" if f16 else
                      "Conv class: conv_band_pool_f32_kernel / conv_win_pool_f32_kernel (conv1 + pool1 + fire2 squeeze, autotuned), fire_kernel (fire "
