@@ -289,7 +289,8 @@ ore_status ore_model_read_value(ore_model* m, const char* name, float* host_dst,
 ore_status ore_model_autotune(ore_model* m, const float* d_input, int64_t n, float* d_output, int32_t reps);
 /* Block tile chosen for exec step i (-1 for non-conv steps); steps with one fixed kernel report its
  * id (e.g. 49 / 50: conv + GlobalAveragePool, f16 / f32).  The f32 first conv + pool + squeeze step
- * has two: 44 (13 x 19 patches) and 51 (the band walker, round 5); the autotune keeps the faster. */
+ * has two: 44 (13 x 19 patches) and 51 (the band walker, round 5); the f16 one 43 (patches) and 52 (the
+ * f16 band walker, round 6).  The autotune keeps the faster. */
 int32_t ore_model_step_tile(ore_model* m, int32_t i);
 /* Set exec step i's tile (one of the ids ore_model_autotune chooses among for that step; e.g. to
  * restore a saved autotune result).  ORE_ERR_INVALID for an id outside the step's kernel family.
