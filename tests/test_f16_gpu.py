@@ -209,7 +209,8 @@ def test_f16_fused_equals_unfused(gpu_ctx):
     np.testing.assert_array_equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("shape", [(3, 128, 7, 7, 200, True), (2, 64, 16, 16, 96, False), (1, 192, 1, 1, 33, True)])
+@pytest.mark.parametrize("shape", [(3, 128, 7, 7, 200, True), (2, 64, 16, 16, 96, False), (1, 192, 1, 1, 33, True),
+                                   (2, 128, 13, 13, 1000, True), (1, 64, 11, 11, 130, False), (2, 64, 3, 3, 40, True)])
 def test_f16_conv_gap_fused_equals_unfused(gpu_ctx, shape):
     """ORE_FUSE_CONV_GAP (conv1x1_gap_f16_kernel: 1x1 conv + Relu + GlobalAveragePool in one launch) is
     bit-identical to conv_f16 + gap_nhwc_kernel: partial 128-channel blocks, 1-8 pixel fragments, no Relu."""
