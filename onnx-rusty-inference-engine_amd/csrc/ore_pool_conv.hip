@@ -62,8 +62,12 @@ __device__ __forceinline__ unsigned ps_magic(int d) { return (unsigned)(((1u << 
 // NF: 16-pixel fragments per pooled row (Wp <= 16 NF); KS1: e1's k-steps (0: no e1); FRW: e1 pixel fragments
 // per wave (>= ceil(ceil((2 PS_PR + 1) W / 16) / 4)); SPLIT: waves per 16-channel block of the squeeze (2: M <= 32
 // on two blocks, each wave takes half the pooled-pixel fragments, so all four waves issue squeeze MFMAs)
+// Launch bounds: with e1 inside at C1 = 32 and the squeeze split (KS1 = 8, SPLIT = 2: fire4 -> pool3 -> fire5),
+// three waves per SIMD (168 VGPRs, 100 B of scratch spills at FRW = 6) instead of two (189 VGPRs + 48 AGPRs):
+// pool3 + e1 + squeeze 230 -> 210 us (round 6, profiles/r06_pool_lb3.txt); a third resident workgroup covers the
+// other two's barrier and LDS chains.  The other instances keep the compiler's choice
 template <int NF, int KS1, int FRW, int SPLIT>
-__global__ __launch_bounds__(256) void pool_conv1x1_f32_kernel(PoolConvParams p) {
+__global__ __launch_bounds__(256, (KS1 == 8 && SPLIT == 2 ? 3 : 1)) void pool_conv1x1_f32_kernel(PoolConvParams p) {
   constexpr int PS_PR = ps_pr(NF);
   constexpr int PS_ROWS = 2 * PS_PR + 1;  // input rows of PS_PR pooled rows (3x3, stride 2)
   // staged rows: input column iw at LDS column iw + PS_LC; columns left of the image and right of
