@@ -493,6 +493,9 @@ def main():
                 "kernel_timing": f"HIP events between consecutive launches on the model stream, a separate ONE-STREAM pass of "
                                  f"the {args.steps} timed steps (events kept out of the value's timed loop; the value's loop runs "
                                  f"{args.streams} stream(s), so per-launch times describe the one-stream schedule)",
+                # what the side stream hides: the one-stream pass's summed launch times minus the timed step
+                "one_stream_kernel_ms": round(float(sum(per_step_ms)), 4),
+                "side_stream_hides_ms": round(float(sum(per_step_ms)) - 1000.0 * elapsed / args.steps, 4),
                 "conv_class": {
                     "kernel": kname, "launches": conv["launches"],
                     "achieved": round(issued, 2), "unit": "TFLOP/s", "peak": peak, "frac": round(issued / peak, 4),
