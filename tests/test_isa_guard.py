@@ -123,3 +123,55 @@ extern "C" __global__ void k(const f2* a, const f2* b, float* out) {
     asm = out.read_text()
     assert "v_pk_add_f32" in asm
     assert asm.count("_dpp") == 1, asm.count("_dpp")  # two values shifted, one DPP: the miscompile
+
+
+def _kernel_meta():
+    """{kernel name: {vgpr_count, agpr_count, private_segment_fixed_size, group_segment_fixed_size}} from the gfx950
+    code object's AMDGPU metadata note (llvm-readelf --notes)."""
+    readelf = os.path.join(LLVM, "llvm-readelf")
+    meta = {}
+    with tempfile.TemporaryDirectory() as d:
+        fat = os.path.join(d, "fat.bin")
+        subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", _lib.LIB_PATH, fat], check=True)
+        data = open(fat, "rb").read()
+        starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)] + [len(data)]
+        for i in range(len(starts) - 1):
+            part = os.path.join(d, f"b{i}.bin")
+            open(part, "wb").write(data[starts[i]:starts[i + 1]])
+            elf = os.path.join(d, f"b{i}.elf")
+            r = subprocess.run([BUNDLER, "--unbundle", "--type=o", f"--input={part}",
+                                "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={elf}"], capture_output=True)
+            if r.returncode != 0 or not os.path.exists(elf):
+                continue
+            notes = subprocess.run([readelf, "--notes", elf], capture_output=True, text=True).stdout
+            for entry in re.split(r"\n\s+- \.agpr_count:", notes)[1:]:
+                name = re.search(r"\.name:\s+(\S+)", entry)
+                if not name:
+                    continue
+                row = {"agpr_count": int(entry.split("\n", 1)[0].strip() or 0)}
+                for key in ("vgpr_count", "private_segment_fixed_size", "group_segment_fixed_size"):
+                    m = re.search(r"\." + key + r":\s+(\d+)", entry)
+                    row[key] = int(m.group(1)) if m else 0
+                meta[name.group(1)] = row
+    return meta
+
+
+@pytest.mark.skipif(not _tools() or not os.path.exists(os.path.join(LLVM, "llvm-readelf")),
+                    reason="ROCm binutils / objcopy not present")
+def test_pooled_squeeze_occupancy():
+    """Round 6: the fire4 -> pool3 -> fire5 instance of the pooled squeeze with e1 inside (KS1 = 8, SPLIT = 2) runs
+    three waves per SIMD (230 -> 210 us against two).  A unified register file of 512 per lane gives
+    three waves at <= 168 registers (the metadata's vgpr_count, AGPRs included); an edit or a compiler that needs more drops it back to two.
+    The plain pool5 instance keeps its six waves; the Winograd LDS kernel its two (two workgroups per CU)."""
+    ore.load()
+    meta = _kernel_meta()
+    assert meta, "no kernel metadata in libore.so"
+
+    def regs(part):
+        rows = [v for k, v in meta.items() if part in k]
+        assert rows, part
+        return max(r["vgpr_count"] for r in rows)  # the unified count: arch VGPRs + AGPRs (granule 8)
+
+    assert regs("pool_conv1x1_f32_kernelILi2ELi8ELi6ELi2E") <= 168
+    assert regs("pool_conv1x1_f32_kernelILi1ELi0ELi0ELi1E") <= 512 // 6 // 8 * 8
+    assert regs("conv_winol_kernel") <= 256
