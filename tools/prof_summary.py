@@ -37,6 +37,7 @@ def main():
         print(f"{label:24s} {calls:9d} {tot / 1e6:10.3f} {tot / calls / 1e3:9.2f}")
     trace = os.path.join(os.path.dirname(sys.argv[1]), "run_kernel_trace.csv")
     bench = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1]) if len(sys.argv) > 2 else None
+    last = []
     if os.path.exists(trace) and bench:
         disp = [r for r in csv.DictReader(open(trace)) if "ore::" in r["Kernel_Name"] or "_ZN3ore" in r["Kernel_Name"]]
         disp.sort(key=lambda r: int(r["Dispatch_Id"]))
@@ -61,12 +62,19 @@ def main():
             print(f"bench.py dominant launch: {r.get('kernel')}: {r.get('launch_us')} us, achieved {r.get('achieved')} "
                   f"{r.get('unit')} = {r.get('frac')} of {r.get('peak')}")
             kern = {"epool band f32": "conv_band_pool_f32_kernel", "epool window f32": "conv_win_pool_f32_kernel",
-                    "first conv pool f16": "conv_pair_pool_f16_kernel"}
+                    "first conv pool f16": "conv_pair_pool_f16_kernel", "epool band f16": "conv_band_pool_f16_kernel"}
             names = [k for t, k in kern.items() if f"tile '{t}'" in str(r.get("kernel"))] or list(kern.values())
             dom = [x for x in rows if any(k in x["Name"] for k in names)]
             for x in dom:
                 print(f"rocprofv3 row of that kernel: {int(x['Calls'])} calls, average {float(x['AverageNs']) / 1e3:.2f} us "
                       f"({x['Name'][:90]})")
+            # round 6: the same kernel over the timed steps only (the stats row also averages the autotune's
+            # candidate runs and the warm-up)
+            tl = [q for q in last if any(k in q["Kernel_Name"] for k in names)]
+            if tl:
+                tot = sum(int(q["End_Timestamp"]) - int(q["Start_Timestamp"]) for q in tl)
+                print(f"rocprofv3, that kernel over the timed steps only: {len(tl)} launches, average "
+                      f"{tot / len(tl) / 1e3:.2f} us")
     print("\nper-kernel rows:")
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
         print(f"  {int(r['Calls']):6d} {float(r['AverageNs']) / 1e3:9.2f} us  {r['Name'][:110]}")
