@@ -80,7 +80,10 @@ __global__ __launch_bounds__(256, (KS1 == 8 && SPLIT == 2 ? 3 : 1)) void pool_co
   constexpr int PS_RW = 16 * NF;                             // pooled pixels held per row
   constexpr int PS_PX = PS_RW * PS_PR;                       // pooled pixels of a workgroup
   __shared__ __attribute__((aligned(16))) float in_s[PS_IN];  // [ch][row][col]
-  __shared__ float pt[PS_CH][PS_PX + 1];   // pooled block [ch][pixel n * PS_RW + col] (+1 pad)
+  // pooled block [ch][pixel n * PS_RW + col]; row stride = 16 mod 32 floats at NF = 2 (the squeeze's B reads of
+  // lane groups lk, lk + 1 on disjoint banks; 16-B aligned rows for the pooling's 16-B stores), PS_PX + 1 at NF = 1
+  constexpr int PT_S = NF >= 2 ? PS_PX + 16 : PS_PX + 1;
+  __shared__ __attribute__((aligned(16))) float pt[PS_CH][PT_S];
   const int tid = threadIdx.x, lane = tid & 63, lk = lane >> 4, lj = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bands = (p.Hp + PS_PR - 1) / PS_PR;
@@ -267,6 +270,7 @@ __global__ __launch_bounds__(256, (KS1 == 8 && SPLIT == 2 ? 3 : 1)) void pool_co
           }
           v[r][8] = base[r * PS_RS + 8];
         }
+        ps4 m4;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           float m = -FLT_MAX;
@@ -274,8 +278,9 @@ __global__ __launch_bounds__(256, (KS1 == 8 && SPLIT == 2 ? 3 : 1)) void pool_co
           for (int r = 0; r < 3; ++r)
 #pragma unroll
             for (int s = 0; s < 3; ++s) m = fmaxf(m, v[r][2 * j + s]);
-          pt[c][n * PS_RW + 4 * c4 + j] = m;
+          m4[j] = m;
         }
+        *reinterpret_cast<ps4*>(&pt[c][n * PS_RW + 4 * c4]) = m4;  // one 16-B store (4 B at 16-B lane stride: 4-way)
       }
     } else {
       for (int t = tid; t < PS_CH * PS_PX; t += 256) {
