@@ -60,6 +60,7 @@ def parse():
     ap.add_argument("--no-b1", action="store_true", help="skip the batch-1 latency probe")
     ap.add_argument("--graph", action="store_true", help="time one HIP-graph replay per step instead of plain launches")
     ap.add_argument("--no-autotune", action="store_true", help="keep the heuristic per-layer conv tiles")
+    ap.add_argument("--tune-reps", type=int, default=3, help="timed launches per autotune candidate")
     ap.add_argument("--dump-steps", default="", help="write the plan's kernel steps (op, name, flops, bytes) as JSON")
     ap.add_argument("--streams", type=int, default=2,
                     help="ore_model_set_streams: 2 (default) runs independent neighbouring steps -- the split fire "
@@ -357,7 +358,7 @@ def main():
     if args.streams != 1:
         model.set_streams(args.streams)
     if not args.no_autotune:  # per-layer conv tile search, outside the timed region
-        model.autotune(x, out)
+        model.autotune(x, out, reps=args.tune_reps)
     if args.dump_steps and rank == 0:  # kernel-step names for tools/pmc_report.py
         with open(args.dump_steps, "w") as f:
             json.dump(model.steps(), f)
